@@ -1,0 +1,302 @@
+"""Configuration loading — parity with ``triton-core/config`` as beholder uses it.
+
+Reference behaviour (``/root/reference/index.js``):
+
+* ``index.js:24`` — ``await Config('events')`` loads the config *named* ``events``.
+* ``index.js:25`` — ``config.keys.trello.key`` / ``.token`` are dereferenced
+  unconditionally at startup (a missing ``keys.trello`` object is a startup error).
+* ``index.js:60`` — ``config.instance.flow_ids`` maps lower-case status → Trello list id.
+* ``index.js:97-115`` — telegram / emby keys are read lazily inside the status handler.
+* ``index.js:70`` — ``process.env.NO_TRELLO``: any *non-empty* value is truthy (JS
+  string semantics, so ``"0"`` is true and ``""`` is false).
+
+The file format is YAML (a JSON file is valid YAML too). Search order for a
+config named ``<name>``:
+
+1. an explicit ``path`` argument (``--config`` on the CLI);
+2. ``$BEHOLDER_CONFIG`` (a file path);
+3. ``$CONFIG_PATH/<name>.yaml`` / ``.yml`` / ``.json``;
+4. ``./config/<name>.yaml`` and ``/stack/config/<name>.yaml`` (the reference
+   image installs the service under ``/stack``, ``Dockerfile:3-6``).
+
+Environment overrides are applied on top: ``BEHOLDER_CFG__a__b__c=value`` sets
+``a.b.c`` (the value is parsed as a YAML scalar, so ``true``/``42`` are typed).
+
+Our own service knobs (transport, store, metrics port, prefetch, ...) live
+under a ``service:`` section and have defaults (``SERVICE_DEFAULTS``); the
+reference hard-codes them (prefetch 100 at ``index.js:43``).
+"""
+from __future__ import annotations
+
+import copy
+import os
+from typing import Any, Iterable, Mapping, MutableMapping, Optional
+
+import yaml
+
+ENV_PREFIX = "BEHOLDER_CFG__"
+
+#: Defaults for knobs the reference hard-codes or inherits from triton-core.
+SERVICE_DEFAULTS: dict = {
+    "service": {
+        # index.js:43 — new AMQP(dyn('rabbitmq'), 100, 2, prom): prefetch 100.
+        "prefetch": 100,
+        # index.js:43 — third AMQP arg; we use it as the reconnect/redelivery retry budget.
+        "retries": 2,
+        "transport": {"kind": "amqp", "url": None},
+        "store": {"backend": "memory", "dsn": None},
+        # index.js:28 — Prom.expose(); port/host are [inferred] (triton-core not vendored).
+        "metrics": {"enabled": True, "host": "0.0.0.0", "port": 3000, "default_metrics": True},
+        # index.js:11-13 — pino logger named after the file basename.
+        "log": {"level": "info", "name": "index.js"},
+        "http": {"timeout_s": 30.0},
+        # SURVEY §5 race detection: opt-in per-mediaId serialisation (default off = parity, Q9).
+        "ordering": "none",
+        # Q1: what to do with a status message whose handler threw.
+        #   leave_unacked (parity) | nack_requeue | nack_drop
+        "on_status_error": "leave_unacked",
+        "endpoints": {
+            "trello": "https://api.trello.com",
+            "telegram": "https://api.telegram.org",
+        },
+        "shutdown_grace_s": 10.0,
+    }
+}
+
+
+class ConfigError(Exception):
+    """Raised for a missing / malformed config (startup fails fast — documented fix of Q10)."""
+
+
+class Node:
+    """Read-only attribute + item view over a nested mapping.
+
+    ``Node`` mimics JS object access: a missing attribute yields ``None`` (JS
+    ``undefined``) instead of raising, so code can reproduce the reference's
+    ``config.instance.telegram && config.instance.telegram.enabled`` guards. Use
+    :meth:`require` where the reference dereferences unconditionally.
+    """
+
+    __slots__ = ("_d", "_path")
+
+    def __init__(self, data: Mapping, path: str = ""):
+        object.__setattr__(self, "_d", data)
+        object.__setattr__(self, "_path", path)
+
+    def __getattr__(self, key: str) -> Any:
+        if key.startswith("__"):
+            raise AttributeError(key)
+        return self[key]
+
+    def __getitem__(self, key: str) -> Any:
+        v = self._d.get(key) if isinstance(self._d, Mapping) else None
+        if isinstance(v, Mapping):
+            return Node(v, f"{self._path}.{key}" if self._path else key)
+        return v
+
+    def __setattr__(self, key, value):  # pragma: no cover - guard
+        raise AttributeError("config is read-only")
+
+    def __contains__(self, key: str) -> bool:
+        return key in self._d
+
+    def __iter__(self):
+        return iter(self._d)
+
+    def __len__(self) -> int:
+        return len(self._d)
+
+    def __bool__(self) -> bool:
+        # A present (even empty) JS object is truthy.
+        return True
+
+    def __eq__(self, other) -> bool:
+        if isinstance(other, Node):
+            return self._d == other._d
+        return self._d == other
+
+    def __repr__(self) -> str:
+        return f"Node({self._path or '<root>'}: {dict(self._d)!r})"
+
+    def keys(self):
+        return self._d.keys()
+
+    def items(self):
+        return self._d.items()
+
+    def get(self, key: str, default: Any = None) -> Any:
+        v = self[key]
+        return default if v is None else v
+
+    def to_dict(self) -> dict:
+        return copy.deepcopy(dict(self._d))
+
+    def require(self, dotted: str) -> Any:
+        """Dereference ``a.b.c`` the way JS does *without* optional chaining.
+
+        Reaching *through* a missing object raises (JS ``TypeError: Cannot read
+        property 'x' of undefined``); a missing leaf returns ``None``.
+        """
+        cur: Any = self._d
+        parts = dotted.split(".")
+        for i, p in enumerate(parts):
+            if not isinstance(cur, Mapping):
+                where = ".".join(parts[:i]) or "<root>"
+                raise ConfigError(f"Cannot read property '{p}' of undefined ({where})")
+            cur = cur.get(p)
+        return Node(cur, dotted) if isinstance(cur, Mapping) else cur
+
+
+def deep_merge(base: MutableMapping, over: Mapping) -> MutableMapping:
+    """Recursively merge ``over`` into ``base`` (in place) and return ``base``."""
+    for k, v in over.items():
+        if isinstance(v, Mapping) and isinstance(base.get(k), MutableMapping):
+            deep_merge(base[k], v)
+        else:
+            base[k] = copy.deepcopy(v)
+    return base
+
+
+def _set_path(d: MutableMapping, parts: Iterable[str], value: Any) -> None:
+    parts = list(parts)
+    cur = d
+    for p in parts[:-1]:
+        nxt = cur.get(p)
+        if not isinstance(nxt, MutableMapping):
+            nxt = {}
+            cur[p] = nxt
+        cur = nxt
+    cur[parts[-1]] = value
+
+
+def env_overrides(env: Mapping[str, str]) -> dict:
+    """Collect ``BEHOLDER_CFG__a__b=v`` overrides into a nested dict."""
+    out: dict = {}
+    for k, v in env.items():
+        if not k.startswith(ENV_PREFIX):
+            continue
+        parts = [p for p in k[len(ENV_PREFIX):].split("__") if p]
+        if not parts:
+            continue
+        try:
+            val = yaml.safe_load(v) if v != "" else ""
+        except yaml.YAMLError:
+            val = v
+        _set_path(out, parts, val)
+    return out
+
+
+def find_config_file(name: str, env: Mapping[str, str], cwd: Optional[str] = None) -> Optional[str]:
+    cands = []
+    if env.get("BEHOLDER_CONFIG"):
+        cands.append(env["BEHOLDER_CONFIG"])
+    roots = []
+    if env.get("CONFIG_PATH"):
+        roots.append(env["CONFIG_PATH"])
+    roots.append(os.path.join(cwd or os.getcwd(), "config"))
+    roots.append("/stack/config")
+    for r in roots:
+        for ext in (".yaml", ".yml", ".json"):
+            cands.append(os.path.join(r, name + ext))
+    for c in cands:
+        if c and os.path.isfile(c):
+            return c
+    return None
+
+
+def js_truthy_env(env: Mapping[str, str], key: str) -> bool:
+    """``if (process.env.KEY)`` — any non-empty string is truthy (index.js:70)."""
+    return bool(env.get(key, ""))
+
+
+class Config:
+    """Loaded configuration: the reference's keys plus our ``service`` section."""
+
+    def __init__(self, data: Mapping, source: Optional[str] = None, env: Optional[Mapping[str, str]] = None):
+        merged = deep_merge(copy.deepcopy(SERVICE_DEFAULTS), data or {})
+        self._data = merged
+        self.root = Node(merged)
+        self.source = source
+        self._env = dict(os.environ if env is None else env)
+        self.validate()
+
+    # -- construction -------------------------------------------------------
+    @classmethod
+    def load(cls, name: str = "events", path: Optional[str] = None,
+             env: Optional[Mapping[str, str]] = None, cwd: Optional[str] = None) -> "Config":
+        """``Config('events')`` (index.js:24)."""
+        env = dict(os.environ if env is None else env)
+        fpath = path or find_config_file(name, env, cwd)
+        data: dict = {}
+        if fpath:
+            try:
+                with open(fpath, "r", encoding="utf-8") as f:
+                    loaded = yaml.safe_load(f)
+            except OSError as e:
+                raise ConfigError(f"cannot read config {fpath}: {e}") from e
+            except yaml.YAMLError as e:
+                raise ConfigError(f"invalid YAML in {fpath}: {e}") from e
+            if loaded is None:
+                loaded = {}
+            if not isinstance(loaded, Mapping):
+                raise ConfigError(f"config {fpath} must be a mapping, got {type(loaded).__name__}")
+            data = dict(loaded)
+        elif path:
+            raise ConfigError(f"config file not found: {path}")
+        deep_merge(data, env_overrides(env))
+        if not fpath and not data:
+            raise ConfigError(
+                f"no config named '{name}' found (set --config, BEHOLDER_CONFIG or CONFIG_PATH)")
+        return cls(data, source=fpath, env=env)
+
+    @classmethod
+    def from_dict(cls, data: Mapping, env: Optional[Mapping[str, str]] = None) -> "Config":
+        return cls(copy.deepcopy(dict(data)), env=env if env is not None else {})
+
+    # -- validation ---------------------------------------------------------
+    def validate(self) -> None:
+        # index.js:25 dereferences config.keys.trello.{key,token} unconditionally.
+        self.root.require("keys.trello.key")
+        self.root.require("keys.trello.token")
+        # index.js:60 — `config.instance.flow_ids` is read at startup (needs `instance`).
+        self.root.require("instance.flow_ids")
+        svc = self._data["service"]
+        if int(svc["prefetch"]) < 1:
+            raise ConfigError("service.prefetch must be >= 1")
+        if svc["ordering"] not in ("none", "per_media"):
+            raise ConfigError("service.ordering must be 'none' or 'per_media'")
+        if svc["on_status_error"] not in ("leave_unacked", "nack_requeue", "nack_drop"):
+            raise ConfigError("service.on_status_error must be leave_unacked|nack_requeue|nack_drop")
+        fl = self._data.get("instance", {}).get("flow_ids") if isinstance(self._data.get("instance"), Mapping) else None
+        if fl is not None and not isinstance(fl, Mapping):
+            raise ConfigError("instance.flow_ids must be a mapping of status -> list id")
+
+    # -- accessors ------------------------------------------------------------
+    def __getattr__(self, key: str) -> Any:
+        if key.startswith("_"):
+            raise AttributeError(key)
+        return self.root[key]
+
+    @property
+    def data(self) -> dict:
+        return self._data
+
+    @property
+    def service(self) -> Node:
+        return self.root["service"]
+
+    @property
+    def env(self) -> Mapping[str, str]:
+        return self._env
+
+    @property
+    def no_trello(self) -> bool:
+        return js_truthy_env(self._env, "NO_TRELLO")
+
+    @property
+    def flow_ids(self) -> Optional[dict]:
+        inst = self._data.get("instance")
+        if not isinstance(inst, Mapping):
+            return None
+        fl = inst.get("flow_ids")
+        return dict(fl) if isinstance(fl, Mapping) else fl

@@ -1,0 +1,214 @@
+"""Telemetry handlers — the business logic of the reference (index.js:50-155).
+
+:class:`TelemetryHandlers` reproduces, branch for branch:
+
+* ``comment(cardId, text)`` — index.js:50-58 (C8);
+* the status handler for ``v1.telemetry.status`` — index.js:62-125 (C10);
+* the progress handler for ``v1.telemetry.progress`` — index.js:127-155 (C11).
+
+Quirks kept on purpose, each covered by tests/test_handlers.py:
+
+Q1  status handler has no try/catch: decode / DB / enum / Trello-move errors
+    escape and the delivery is left un-acked (the service applies
+    ``service.on_status_error``; default ``leave_unacked`` = reference).
+Q2  ``NO_TRELLO`` acks right after the DB update and skips Trello, Telegram
+    and Emby — for the status handler only.
+Q3  Telegram / Emby fire when the *re-read* DB status is ``DEPLOYED``.
+Q4  Telegram and Emby share one try: a Telegram failure skips Emby; errors
+    are logged at warn and the message is still acked.
+Q5  a missing flow-list mapping logs a warn (with the available keys).
+Q6  an unknown status enum: status handler throws (un-acked); progress
+    handler warns + acks without touching the counter.
+Q7  the progress handler always acks.
+Q8  card moves use ``pos: 2``; comment text is
+    ``"{STATUS}: Progress **{p}%**"`` + ``" (_{host}_)"`` if host is truthy.
+Q9  no per-media ordering (opt-in serialisation lives in
+    :mod:`beholder_amd.parallel.ordering`).
+
+Log messages are the reference's text, rendered with JS ``String()`` rules.
+"""
+from __future__ import annotations
+
+from typing import Any, Callable, Mapping, Optional
+
+from .models import proto
+from .sinks.trello import COMMENT_FALLBACK
+from .sinks.telegram import deployed_text
+from .utils.log import js_str
+
+TRELLO_CREATOR = 1  # index.js:79 compares `media.creator === 1`
+
+
+def js_truthy(v: Any) -> bool:
+    """JavaScript truthiness (``""``, ``0``, ``NaN``, ``None``/undefined, ``False`` are falsy)."""
+    if v is None or v is False:
+        return False
+    if isinstance(v, (int, float)) and not isinstance(v, bool):
+        return v == v and v != 0
+    if isinstance(v, str):
+        return v != ""
+    return True  # objects / arrays (even empty) are truthy
+
+
+def err_message(err: BaseException) -> str:
+    """``err.message || err``."""
+    msg = getattr(err, "message", None)
+    if isinstance(msg, str) and msg:
+        return msg
+    s = str(err)
+    return s if s else type(err).__name__
+
+
+class JsTypeError(TypeError):
+    """What V8 raises where the reference dereferences ``undefined``."""
+
+
+def _get(obj: Any, key: str) -> Any:
+    """``obj[key]`` with JS semantics on config nodes / dicts (``undefined`` → None)."""
+    if obj is None:
+        raise JsTypeError(f"Cannot read property '{key}' of undefined")
+    if isinstance(obj, Mapping):
+        return obj.get(key)
+    try:
+        return obj[key]
+    except (KeyError, TypeError, IndexError):
+        return getattr(obj, key, None)
+
+
+class TelemetryHandlers:
+    """Status / progress handlers bound to their dependencies.
+
+    ``decode_status`` / ``decode_progress`` default to the native codec built
+    from the ``.proto`` schema (upb fallback for non-flat schemas).
+    """
+
+    def __init__(self, *, config, store, trello, telegram, emby, progress_counter, comments_counter,
+                 logger, no_trello: Optional[bool] = None,
+                 decode_status: Optional[Callable] = None, decode_progress: Optional[Callable] = None):
+        self.config = config
+        self.store = store
+        self.trello = trello
+        self.telegram = telegram
+        self.emby = emby
+        self.progress_counter = progress_counter
+        self.comments_counter = comments_counter
+        self.log = logger
+        self.no_trello = config.no_trello if no_trello is None else bool(no_trello)
+
+        self.status_proto = proto.load("api.TelemetryStatus")      # index.js:47
+        self.progress_proto = proto.load("api.TelemetryProgress")  # index.js:46
+        self.media_proto = proto.load("api.Media")                 # index.js:48
+        self.decode_status = decode_status or _decoder(self.status_proto)
+        self.decode_progress = decode_progress or _decoder(self.progress_proto)
+
+        # enumToString tables (index.js:74,134): number -> name, first name wins
+        self._status_names_s = self.status_proto.enum("TelemetryStatusEntry")[0]
+        self._status_names_p = self.progress_proto.enum("TelemetryStatusEntry")[0]
+        # stringToEnum (index.js:94,142)
+        self.deployed = proto.string_to_enum(self.status_proto, "TelemetryStatusEntry", "DEPLOYED")
+        self.trello_creator = proto.string_to_enum(self.media_proto, "CreatorType", "TRELLO")
+        self.lists = config.flow_ids  # index.js:60
+
+    # ------------------------------------------------------------------ C8 ---
+    async def comment(self, card_id: Any, text: Optional[str]) -> None:
+        """index.js:50-58."""
+        self.log.info("creating comment on", card_id, "with text:", text)
+        await self.trello.make_request("post", f"/1/cards/{js_str(card_id)}/actions/comments",
+                                       {"text": text or COMMENT_FALLBACK})
+        self.comments_counter.inc()
+
+    # ----------------------------------------------------------------- C10 ---
+    async def on_status(self, rmsg) -> Any:
+        """``v1.telemetry.status`` (index.js:62-125). Exceptions escape on purpose (Q1)."""
+        log = self.log
+        msg = self.decode_status(rmsg.message.content)  # index.js:63
+        media_id = msg.mediaId
+        status = msg.status
+
+        log.info(f"processing status update for media {js_str(media_id)}, status: {js_str(status)}")
+
+        await self.store.update_status(media_id, status)  # index.js:68
+
+        if self.no_trello:  # index.js:70-72 (Q2)
+            return rmsg.ack()
+
+        status_text = self._status_names_s.get(status)  # index.js:74 (None = undefined)
+
+        media = await self.store.get_by_id(media_id)  # index.js:76
+
+        # TRELLO Movement (index.js:78-90)
+        if media.creator == TRELLO_CREATOR:
+            if status_text is None:  # `statusText.toLowerCase()` on undefined (Q6)
+                raise JsTypeError("Cannot read property 'toLowerCase' of undefined")
+            lists = self.lists
+            list_pointer = _get(lists, status_text.lower())
+            if js_truthy(list_pointer):
+                log.info(f"moving media card {js_str(media_id)} (card id {js_str(media.creatorId)})")
+                await self.trello.make_request("put", f"/1/cards/{js_str(media.creatorId)}",
+                                               {"idList": list_pointer, "pos": 2})
+            else:  # Q5
+                log.warn("unable to find list for status", status, f"({js_str(status_text)})",
+                         f"avail ([{','.join(str(k) for k in lists.keys())}])")
+
+        try:  # index.js:92-122 (Q3, Q4)
+            if media.status == self.deployed:
+                cfg = self.config
+                inst = cfg.instance
+                tg = _get(inst, "telegram")
+                if js_truthy(tg) and js_truthy(_get(tg, "enabled")):
+                    log.info(f"informing telegram that media '{js_str(media_id)}' is available")
+                    chat_id = _get(tg, "channel")
+                    token = _get(_get(cfg.keys, "telegram"), "token")
+                    await self.telegram.send_message(chat_id, deployed_text(media.name, media.metadataId),
+                                                     "markdown", token=token)
+                keys_emby = _get(cfg.keys, "emby")
+                inst_emby = _get(inst, "emby")
+                if (js_truthy(keys_emby) and js_truthy(_get(keys_emby, "token")) and js_truthy(inst_emby)
+                        and js_truthy(_get(inst_emby, "enabled"))):
+                    host = _get(inst_emby, "host")
+                    log.info(f"telling emby to refresh at {js_str(host)}")
+                    await self.emby.refresh_library(host=host, api_key=_get(keys_emby, "token"))
+        except Exception as err:  # noqa: BLE001 — reference catches everything here
+            log.warn("failed to run deployed hooks:", err_message(err))
+
+        return rmsg.ack()  # index.js:124
+
+    # ----------------------------------------------------------------- C11 ---
+    async def on_progress(self, rmsg) -> Any:
+        """``v1.telemetry.progress`` (index.js:127-155). Always acks (Q7)."""
+        log = self.log
+        try:
+            msg = self.decode_progress(rmsg.message.content)  # index.js:129
+            media_id = msg.mediaId
+            status = msg.status
+            progress = msg.progress
+            host = msg.host
+
+            log.info("processing progress update on media", media_id, "status", status, "percent", progress)
+            status_text = self._status_names_p.get(status)  # index.js:134
+            if status_text is None:  # Q6
+                raise JsTypeError("Cannot read property 'toLowerCase' of undefined")
+
+            self.progress_counter.child_for(status_text.lower()).inc()  # index.js:136-138
+
+            media = await self.store.get_by_id(media_id)  # index.js:140
+
+            if media.creator == self.trello_creator:  # index.js:142
+                comment_text = f"{status_text}: Progress **{js_str(progress)}%**"  # Q8
+                if js_truthy(host):
+                    comment_text += f" (_{js_str(host)}_)"
+                await self.comment(media.creatorId, comment_text)
+        except Exception as err:  # noqa: BLE001 — index.js:149-151
+            log.warn("failed to update media progress", err_message(err))
+            return rmsg.ack()
+
+        return rmsg.ack()  # index.js:154
+
+
+def _decoder(ptype) -> Callable:
+    """Native decode if the schema is flat, else upb (same field names either way)."""
+    from .ops import codec_for
+    codec = codec_for(ptype)
+    if codec is not None:
+        return codec.decode
+    return lambda data: proto.decode(ptype, data)

@@ -1,0 +1,510 @@
+// MessageCodec: schema-driven native protobuf codec for flat messages.
+//
+// Hot path of both reference handlers: `proto.decode(type, content)`
+// (index.js:63, :129). The field table comes from the runtime descriptor
+// built from beholder_amd/models/proto/*.proto (see ops/__init__.py), so the
+// codec follows the .proto file instead of hard-coding field numbers.
+// Decoded messages are PyStructSequence instances: attribute access by proto
+// field name (msg.mediaId, msg.status, ...) like protobufjs / upb messages.
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "py_common.hpp"
+#include "wire.hpp"
+
+namespace beholder {
+
+namespace {
+
+constexpr int MAX_FIELDS = 64;
+constexpr uint32_t MAX_FIELD_NUMBER = 65535;
+
+struct FieldSpec {
+  uint32_t number;
+  int kind;
+};
+
+struct CodecObject {
+  PyObject_HEAD PyTypeObject* result_type;
+  std::vector<int16_t>* by_number;  // field number -> slot (-1 = unknown)
+  std::vector<FieldSpec>* fields;   // by slot
+  PyObject* defaults;               // tuple, per slot
+  PyObject* names;                  // tuple of str, per slot
+  PyObject* type_name;              // str
+};
+
+union SlotVal {
+  uint64_t u;
+  double d;
+  struct {
+    const uint8_t* p;
+    size_t n;
+  } s;
+};
+
+PyObject* default_for(int kind) {
+  switch (kind) {
+    case wire::K_STRING:
+      return PyUnicode_FromStringAndSize("", 0);
+    case wire::K_BYTES:
+      return PyBytes_FromStringAndSize("", 0);
+    case wire::K_BOOL:
+      Py_RETURN_FALSE;
+    case wire::K_FLOAT:
+    case wire::K_DOUBLE:
+      return PyFloat_FromDouble(0.0);
+    default:
+      return PyLong_FromLong(0);
+  }
+}
+
+void codec_dealloc(CodecObject* self) {
+  Py_XDECREF(self->result_type);
+  Py_XDECREF(self->defaults);
+  Py_XDECREF(self->names);
+  Py_XDECREF(self->type_name);
+  delete self->by_number;
+  delete self->fields;
+  Py_TYPE(self)->tp_free(reinterpret_cast<PyObject*>(self));
+}
+
+PyObject* codec_new(PyTypeObject* type, PyObject*, PyObject*) {
+  CodecObject* self = reinterpret_cast<CodecObject*>(type->tp_alloc(type, 0));
+  if (!self) return nullptr;
+  self->result_type = nullptr;
+  self->by_number = nullptr;
+  self->fields = nullptr;
+  self->defaults = nullptr;
+  self->names = nullptr;
+  self->type_name = nullptr;
+  return reinterpret_cast<PyObject*>(self);
+}
+
+// MessageCodec(type_name: str, fields: sequence of (number, name, kind))
+int codec_init(CodecObject* self, PyObject* args, PyObject* kwds) {
+  static const char* kwlist[] = {"type_name", "fields", nullptr};
+  const char* tname;
+  PyObject* fields;
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "sO", const_cast<char**>(kwlist), &tname, &fields))
+    return -1;
+  PyObject* seq = PySequence_Fast(fields, "fields must be a sequence");
+  if (!seq) return -1;
+  Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  if (n < 1 || n > MAX_FIELDS) {
+    Py_DECREF(seq);
+    PyErr_Format(PyExc_ValueError, "MessageCodec supports 1..%d fields", MAX_FIELDS);
+    return -1;
+  }
+  auto* specs = new std::vector<FieldSpec>();
+  PyObject* names = PyTuple_New(n);
+  PyObject* defaults = PyTuple_New(n);
+  uint32_t max_no = 0;
+  // PyStructSequence field names must outlive the type: they are copied into
+  // heap memory that is intentionally never freed (codecs are created once per
+  // message type per process).
+  auto* members = static_cast<PyStructSequence_Field*>(PyMem_RawCalloc(size_t(n) + 1, sizeof(PyStructSequence_Field)));
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* item = PySequence_Fast_GET_ITEM(seq, i);
+    unsigned long number;
+    const char* fname;
+    int kind;
+    if (!PyArg_ParseTuple(item, "ksi", &number, &fname, &kind)) goto fail;
+    if (number == 0 || number > MAX_FIELD_NUMBER) {
+      PyErr_Format(PyExc_ValueError, "field number %lu out of range", number);
+      goto fail;
+    }
+    if (kind < wire::K_STRING || kind > wire::K_SFIXED64) {
+      PyErr_Format(PyExc_ValueError, "unknown field kind %d", kind);
+      goto fail;
+    }
+    for (auto& s : *specs) {
+      if (s.number == number) {
+        PyErr_Format(PyExc_ValueError, "duplicate field number %lu", number);
+        goto fail;
+      }
+    }
+    specs->push_back(FieldSpec{uint32_t(number), kind});
+    if (number > max_no) max_no = uint32_t(number);
+    size_t L = strlen(fname);
+    char* copy = static_cast<char*>(PyMem_RawMalloc(L + 1));
+    memcpy(copy, fname, L + 1);
+    members[i].name = copy;
+    members[i].doc = nullptr;
+    PyTuple_SET_ITEM(names, i, PyUnicode_FromString(fname));
+    PyTuple_SET_ITEM(defaults, i, default_for(kind));
+  }
+  {
+    size_t tl = strlen(tname);
+    char* tcopy = static_cast<char*>(PyMem_RawMalloc(tl + 1));
+    memcpy(tcopy, tname, tl + 1);
+    auto* desc = static_cast<PyStructSequence_Desc*>(PyMem_RawCalloc(1, sizeof(PyStructSequence_Desc)));
+    desc->name = tcopy;
+    desc->doc = "decoded protobuf message (native codec)";
+    desc->fields = members;
+    desc->n_in_sequence = int(n);
+    PyTypeObject* rt = PyStructSequence_NewType(desc);
+    if (!rt) goto fail;
+    self->result_type = rt;
+  }
+  self->by_number = new std::vector<int16_t>(size_t(max_no) + 1, int16_t(-1));
+  for (size_t i = 0; i < specs->size(); ++i) (*self->by_number)[(*specs)[i].number] = int16_t(i);
+  self->fields = specs;
+  self->names = names;
+  self->defaults = defaults;
+  self->type_name = PyUnicode_FromString(tname);
+  Py_DECREF(seq);
+  return 0;
+fail:
+  delete specs;
+  Py_DECREF(names);
+  Py_DECREF(defaults);
+  Py_DECREF(seq);
+  return -1;
+}
+
+inline PyObject* raise_decode(const char* why, PyObject* tname) {
+  PyErr_Format(g_state.decode_error ? g_state.decode_error : PyExc_ValueError,
+               "invalid wire format for %U: %s", tname, why);
+  return nullptr;
+}
+
+// Core decode: fills `vals`/`seen`. Returns nullptr on success, else error text.
+const char* decode_into(CodecObject* self, const uint8_t* data, size_t len, SlotVal* vals, bool* seen) {
+  wire::Reader r(data, len);
+  const auto& bynum = *self->by_number;
+  const auto& specs = *self->fields;
+  while (!r.eof()) {
+    uint64_t tag;
+    if (!r.varint(&tag)) return r.err;
+    if (tag > 0xffffffffull) return "tag overflow";
+    uint32_t field = uint32_t(tag >> 3);
+    uint32_t wt = uint32_t(tag & 7);
+    if (field == 0) return "invalid field number 0";
+    int slot = field < bynum.size() ? bynum[field] : -1;
+    if (slot < 0 || wire::expected_wire_type(specs[slot].kind) != wt) {
+      if (!r.skip(wt, field)) return r.err;
+      continue;
+    }
+    SlotVal& v = vals[slot];
+    switch (wt) {
+      case wire::WT_VARINT:
+        if (!r.varint(&v.u)) return r.err;
+        break;
+      case wire::WT_LEN:
+        if (!r.bytes(&v.s.p, &v.s.n)) return r.err;
+        break;
+      case wire::WT_I32: {
+        uint32_t x;
+        if (!r.fixed32(&x)) return r.err;
+        v.u = x;
+        break;
+      }
+      case wire::WT_I64:
+        if (!r.fixed64(&v.u)) return r.err;
+        break;
+    }
+    seen[slot] = true;
+  }
+  return nullptr;
+}
+
+PyObject* value_for(int kind, const SlotVal& v) {
+  switch (kind) {
+    case wire::K_STRING:
+      return PyUnicode_DecodeUTF8(reinterpret_cast<const char*>(v.s.p), Py_ssize_t(v.s.n), "strict");
+    case wire::K_BYTES:
+      return PyBytes_FromStringAndSize(reinterpret_cast<const char*>(v.s.p), Py_ssize_t(v.s.n));
+    case wire::K_INT32:
+    case wire::K_ENUM:
+      return PyLong_FromLong(long(int32_t(uint32_t(v.u))));
+    case wire::K_INT64:
+      return PyLong_FromLongLong(int64_t(v.u));
+    case wire::K_UINT32:
+      return PyLong_FromUnsignedLong(uint32_t(v.u));
+    case wire::K_UINT64:
+      return PyLong_FromUnsignedLongLong(v.u);
+    case wire::K_SINT32:
+      return PyLong_FromLong(wire::unzigzag32(uint32_t(v.u)));
+    case wire::K_SINT64:
+      return PyLong_FromLongLong(wire::unzigzag64(v.u));
+    case wire::K_BOOL:
+      return PyBool_FromLong(v.u != 0);
+    case wire::K_FLOAT: {
+      uint32_t b = uint32_t(v.u);
+      float f;
+      memcpy(&f, &b, 4);
+      return PyFloat_FromDouble(double(f));
+    }
+    case wire::K_DOUBLE: {
+      double d;
+      memcpy(&d, &v.u, 8);
+      return PyFloat_FromDouble(d);
+    }
+    case wire::K_FIXED32:
+      return PyLong_FromUnsignedLong(uint32_t(v.u));
+    case wire::K_FIXED64:
+      return PyLong_FromUnsignedLongLong(v.u);
+    case wire::K_SFIXED32:
+      return PyLong_FromLong(int32_t(uint32_t(v.u)));
+    case wire::K_SFIXED64:
+      return PyLong_FromLongLong(int64_t(v.u));
+  }
+  Py_RETURN_NONE;
+}
+
+}  // namespace
+
+// Decodes `data` with codec `self_obj`; used by MessageCodec.decode.
+PyObject* codec_decode_raw(PyObject* self_obj, const uint8_t* data, size_t len) {
+  CodecObject* self = reinterpret_cast<CodecObject*>(self_obj);
+  const size_t n = self->fields->size();
+  SlotVal vals[MAX_FIELDS];
+  bool seen[MAX_FIELDS] = {false};
+  const char* err = decode_into(self, data, len, vals, seen);
+  if (err) return raise_decode(err, self->type_name);
+  PyObject* out = PyStructSequence_New(self->result_type);
+  if (!out) return nullptr;
+  for (size_t i = 0; i < n; ++i) {
+    PyObject* v;
+    if (seen[i]) {
+      v = value_for((*self->fields)[i].kind, vals[i]);
+      if (!v) {
+        Py_DECREF(out);
+        if (PyErr_ExceptionMatches(PyExc_UnicodeDecodeError)) {
+          PyErr_Clear();
+          return raise_decode("string field contains invalid UTF-8", self->type_name);
+        }
+        return nullptr;
+      }
+    } else {
+      v = PyTuple_GET_ITEM(self->defaults, Py_ssize_t(i));
+      Py_INCREF(v);
+    }
+    PyStructSequence_SET_ITEM(out, Py_ssize_t(i), v);
+  }
+  return out;
+}
+
+namespace {
+
+PyObject* codec_decode(CodecObject* self, PyObject* arg) {
+  if (PyBytes_CheckExact(arg)) {
+    return codec_decode_raw(reinterpret_cast<PyObject*>(self),
+                            reinterpret_cast<const uint8_t*>(PyBytes_AS_STRING(arg)),
+                            size_t(PyBytes_GET_SIZE(arg)));
+  }
+  Py_buffer view;
+  if (PyObject_GetBuffer(arg, &view, PyBUF_SIMPLE) < 0) {
+    PyErr_Clear();
+    PyErr_Format(g_state.decode_error ? g_state.decode_error : PyExc_ValueError,
+                 "illegal buffer: expected bytes-like, got %s", Py_TYPE(arg)->tp_name);
+    return nullptr;
+  }
+  PyObject* out = codec_decode_raw(reinterpret_cast<PyObject*>(self),
+                                   static_cast<const uint8_t*>(view.buf), size_t(view.len));
+  PyBuffer_Release(&view);
+  return out;
+}
+
+// Encode a value for `kind`; appends to `buf`. Returns false with Python error set.
+bool encode_field(std::string& buf, uint32_t number, int kind, PyObject* v) {
+  using namespace wire;
+  uint8_t tmp[16];
+  auto put_tag = [&](uint32_t wt) {
+    uint8_t* e = put_varint(tmp, (uint64_t(number) << 3) | wt);
+    buf.append(reinterpret_cast<char*>(tmp), size_t(e - tmp));
+  };
+  auto put_v = [&](uint64_t x) {
+    uint8_t* e = put_varint(tmp, x);
+    buf.append(reinterpret_cast<char*>(tmp), size_t(e - tmp));
+  };
+  switch (kind) {
+    case K_STRING: {
+      Py_ssize_t L;
+      const char* s = PyUnicode_AsUTF8AndSize(v, &L);
+      if (!s) return false;
+      if (L == 0) return true;
+      put_tag(WT_LEN);
+      put_v(uint64_t(L));
+      buf.append(s, size_t(L));
+      return true;
+    }
+    case K_BYTES: {
+      char* s;
+      Py_ssize_t L;
+      if (PyBytes_AsStringAndSize(v, &s, &L) < 0) return false;
+      if (L == 0) return true;
+      put_tag(WT_LEN);
+      put_v(uint64_t(L));
+      buf.append(s, size_t(L));
+      return true;
+    }
+    case K_FLOAT:
+    case K_DOUBLE: {
+      double d = PyFloat_AsDouble(v);
+      if (d == -1.0 && PyErr_Occurred()) return false;
+      if (d == 0.0 && !std::signbit(d)) return true;
+      if (kind == K_FLOAT) {
+        float f = float(d);
+        put_tag(WT_I32);
+        buf.append(reinterpret_cast<char*>(&f), 4);
+      } else {
+        put_tag(WT_I64);
+        buf.append(reinterpret_cast<char*>(&d), 8);
+      }
+      return true;
+    }
+    case K_BOOL: {
+      int t = PyObject_IsTrue(v);
+      if (t < 0) return false;
+      if (!t) return true;
+      put_tag(WT_VARINT);
+      put_v(1);
+      return true;
+    }
+    default:
+      break;
+  }
+  // integer kinds
+  int overflow = 0;
+  long long sv = PyLong_AsLongLongAndOverflow(v, &overflow);
+  uint64_t uv;
+  if (sv == -1 && PyErr_Occurred()) return false;
+  if (overflow > 0) {
+    uv = PyLong_AsUnsignedLongLong(v);
+    if (PyErr_Occurred()) return false;
+    sv = int64_t(uv);
+  } else if (overflow < 0) {
+    PyErr_SetString(PyExc_OverflowError, "integer out of range");
+    return false;
+  } else {
+    uv = uint64_t(sv);
+  }
+  if (uv == 0) return true;
+  switch (kind) {
+    case K_INT32:
+    case K_ENUM:
+      put_tag(WT_VARINT);
+      put_v(uint64_t(int64_t(int32_t(sv))));  // negative int32 -> 10-byte varint
+      return true;
+    case K_UINT32:
+      put_tag(WT_VARINT);
+      put_v(uint32_t(uv));
+      return true;
+    case K_INT64:
+    case K_UINT64:
+      put_tag(WT_VARINT);
+      put_v(uv);
+      return true;
+    case K_SINT32:
+      put_tag(WT_VARINT);
+      put_v(zigzag32(int32_t(sv)));
+      return true;
+    case K_SINT64:
+      put_tag(WT_VARINT);
+      put_v(zigzag64(sv));
+      return true;
+    case K_FIXED32:
+    case K_SFIXED32: {
+      uint32_t x = uint32_t(uv);
+      put_tag(WT_I32);
+      buf.append(reinterpret_cast<char*>(&x), 4);
+      return true;
+    }
+    case K_FIXED64:
+    case K_SFIXED64:
+      put_tag(WT_I64);
+      buf.append(reinterpret_cast<char*>(&uv), 8);
+      return true;
+  }
+  PyErr_SetString(PyExc_ValueError, "bad kind");
+  return false;
+}
+
+// encode(obj) where obj is a sequence in slot order or a mapping by field name.
+PyObject* codec_encode(CodecObject* self, PyObject* obj) {
+  const size_t n = self->fields->size();
+  std::string buf;
+  buf.reserve(64);
+  bool is_map = PyDict_Check(obj);
+  PyObject* seq = nullptr;
+  if (!is_map) {
+    seq = PySequence_Fast(obj, "encode() takes a mapping or a sequence in field order");
+    if (!seq) return nullptr;
+    if (size_t(PySequence_Fast_GET_SIZE(seq)) != n) {
+      Py_DECREF(seq);
+      PyErr_Format(PyExc_ValueError, "expected %zu values", n);
+      return nullptr;
+    }
+  }
+  for (size_t i = 0; i < n; ++i) {
+    PyObject* v;
+    if (is_map) {
+      v = PyDict_GetItemWithError(obj, PyTuple_GET_ITEM(self->names, Py_ssize_t(i)));
+      if (!v) {
+        if (PyErr_Occurred()) return nullptr;
+        continue;
+      }
+    } else {
+      v = PySequence_Fast_GET_ITEM(seq, Py_ssize_t(i));
+    }
+    if (v == Py_None) continue;
+    const FieldSpec& f = (*self->fields)[i];
+    if (!encode_field(buf, f.number, f.kind, v)) {
+      Py_XDECREF(seq);
+      return nullptr;
+    }
+  }
+  Py_XDECREF(seq);
+  return PyBytes_FromStringAndSize(buf.data(), Py_ssize_t(buf.size()));
+}
+
+PyObject* codec_get_result_type(CodecObject* self, void*) {
+  Py_INCREF(self->result_type);
+  return reinterpret_cast<PyObject*>(self->result_type);
+}
+PyObject* codec_get_names(CodecObject* self, void*) {
+  Py_INCREF(self->names);
+  return self->names;
+}
+PyObject* codec_get_type_name(CodecObject* self, void*) {
+  Py_INCREF(self->type_name);
+  return self->type_name;
+}
+
+PyMethodDef codec_methods[] = {
+    {"decode", reinterpret_cast<PyCFunction>(codec_decode), METH_O,
+     "decode(data) -> message; raises DecodeError on malformed input"},
+    {"encode", reinterpret_cast<PyCFunction>(codec_encode), METH_O,
+     "encode(mapping_or_sequence) -> bytes (proto3: default values omitted)"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyGetSetDef codec_getset[] = {
+    {"result_type", reinterpret_cast<getter>(codec_get_result_type), nullptr, "decoded message type", nullptr},
+    {"field_names", reinterpret_cast<getter>(codec_get_names), nullptr, "field names in slot order", nullptr},
+    {"type_name", reinterpret_cast<getter>(codec_get_type_name), nullptr, "message type name", nullptr},
+    {nullptr, nullptr, nullptr, nullptr, nullptr}};
+
+}  // namespace
+
+PyTypeObject CodecType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+int init_codec_types(PyObject* m) {
+  CodecType.tp_name = "beholder_amd.ops._native.MessageCodec";
+  CodecType.tp_basicsize = sizeof(CodecObject);
+  CodecType.tp_flags = Py_TPFLAGS_DEFAULT;
+  CodecType.tp_doc = "MessageCodec(type_name, fields): native protobuf codec for flat messages";
+  CodecType.tp_new = codec_new;
+  CodecType.tp_init = reinterpret_cast<initproc>(codec_init);
+  CodecType.tp_dealloc = reinterpret_cast<destructor>(codec_dealloc);
+  CodecType.tp_methods = codec_methods;
+  CodecType.tp_getset = codec_getset;
+  if (PyType_Ready(&CodecType) < 0) return -1;
+  Py_INCREF(&CodecType);
+  if (PyModule_AddObject(m, "MessageCodec", reinterpret_cast<PyObject*>(&CodecType)) < 0) return -1;
+  return 0;
+}
+
+}  // namespace beholder

@@ -1,0 +1,73 @@
+// Shared declarations for the `_native` CPython extension.
+#pragma once
+
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+
+#include <cstdint>
+
+#include "histogram.hpp"
+
+namespace beholder {
+
+// Module-level state (single-phase init; one interpreter).
+struct ModuleState {
+  PyObject* decode_error;  // exception raised by MessageCodec.decode
+  PyObject* topics;        // tuple: topic id -> topic name (str) or None
+};
+extern ModuleState g_state;
+
+// ---- Histogram ------------------------------------------------------------
+struct HistogramObject {
+  PyObject_HEAD LogHistogram* h;
+};
+extern PyTypeObject HistogramType;
+
+// ---- Counter --------------------------------------------------------------
+struct CounterObject {
+  PyObject_HEAD double value;
+};
+extern PyTypeObject CounterType;
+
+// ---- Settler: ack accounting shared by all deliveries of one source --------
+struct SettlerObject {
+  PyObject_HEAD HistogramObject* handle_hist;  // start() -> settle, ns
+  HistogramObject* ingest_hist;                // recv -> settle, ns
+  uint64_t created, acked, nacked, rejected, abandoned;
+  PyObject* on_settle;   // optional callable(delivery, kind:str, requeue:bool)
+  PyObject* on_abandon;  // optional callable(tag, topic_id, content)
+};
+extern PyTypeObject SettlerType;
+
+// ---- Delivery: one inbound message (rmsg of index.js:62,127) ---------------
+enum DeliveryState : uint8_t { D_PENDING = 0, D_ACKED = 1, D_NACKED = 2, D_REJECTED = 3 };
+
+struct DeliveryObject {
+  PyObject_HEAD PyObject* content;  // bytes
+  SettlerObject* settler;           // may be NULL
+  PyObject* extra;                  // transport-specific payload, may be NULL
+  uint64_t tag;
+  int64_t recv_ns;
+  int64_t start_ns;
+  uint8_t topic;
+  uint8_t state;
+  uint8_t redelivered;
+};
+extern PyTypeObject DeliveryType;
+
+// Creates a pending delivery; steals nothing (increfs content/settler).
+PyObject* delivery_new(PyObject* content, uint8_t topic, uint64_t tag, int64_t recv_ns,
+                       SettlerObject* settler, bool redelivered);
+
+// ---- Ingest ring + reader thread --------------------------------------------
+extern PyTypeObject IngestType;
+
+// ---- MessageCodec -----------------------------------------------------------
+extern PyTypeObject CodecType;
+
+int init_codec_types(PyObject* m);
+int init_metric_types(PyObject* m);
+int init_ingest_types(PyObject* m);
+int init_text_functions(PyObject* m);
+
+}  // namespace beholder

@@ -1,0 +1,253 @@
+// Native metric primitives: Counter (prom-client Counter semantics, used for
+// `beholder_progress_updates_total` / `beholder_trello_comments`,
+// index.js:29-40) and Histogram (log-linear latency histogram, ns).
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "py_common.hpp"
+
+namespace beholder {
+
+// ============================== Histogram ===================================
+namespace {
+
+PyObject* hist_new(PyTypeObject* type, PyObject*, PyObject*) {
+  HistogramObject* self = reinterpret_cast<HistogramObject*>(type->tp_alloc(type, 0));
+  if (!self) return nullptr;
+  self->h = new (std::nothrow) LogHistogram();
+  if (!self->h) {
+    Py_DECREF(self);
+    return PyErr_NoMemory();
+  }
+  return reinterpret_cast<PyObject*>(self);
+}
+
+void hist_dealloc(HistogramObject* self) {
+  delete self->h;
+  Py_TYPE(self)->tp_free(reinterpret_cast<PyObject*>(self));
+}
+
+bool as_u64(PyObject* v, uint64_t* out) {
+  if (PyFloat_Check(v)) {
+    double d = PyFloat_AS_DOUBLE(v);
+    *out = d <= 0 ? 0 : uint64_t(d);
+    return true;
+  }
+  long long x = PyLong_AsLongLong(v);
+  if (x == -1 && PyErr_Occurred()) return false;
+  *out = x < 0 ? 0 : uint64_t(x);
+  return true;
+}
+
+PyObject* hist_record(HistogramObject* self, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs < 1 || nargs > 2) {
+    PyErr_SetString(PyExc_TypeError, "record(value, count=1)");
+    return nullptr;
+  }
+  uint64_t v, n = 1;
+  if (!as_u64(args[0], &v)) return nullptr;
+  if (nargs == 2 && !as_u64(args[1], &n)) return nullptr;
+  self->h->record(v, n);
+  Py_RETURN_NONE;
+}
+
+PyObject* hist_record_many(HistogramObject* self, PyObject* seq_in) {
+  PyObject* seq = PySequence_Fast(seq_in, "record_many expects a sequence");
+  if (!seq) return nullptr;
+  Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    uint64_t v;
+    if (!as_u64(PySequence_Fast_GET_ITEM(seq, i), &v)) {
+      Py_DECREF(seq);
+      return nullptr;
+    }
+    self->h->record(v);
+  }
+  Py_DECREF(seq);
+  Py_RETURN_NONE;
+}
+
+PyObject* hist_percentile(HistogramObject* self, PyObject* arg) {
+  double p = PyFloat_AsDouble(arg);
+  if (p == -1.0 && PyErr_Occurred()) return nullptr;
+  return PyFloat_FromDouble(self->h->percentile(p));
+}
+
+PyObject* hist_count_le(HistogramObject* self, PyObject* arg) {
+  uint64_t v;
+  if (!as_u64(arg, &v)) return nullptr;
+  return PyLong_FromUnsignedLongLong(self->h->count_le(v));
+}
+
+PyObject* hist_reset(HistogramObject* self, PyObject*) {
+  self->h->reset();
+  Py_RETURN_NONE;
+}
+
+PyObject* hist_merge(HistogramObject* self, PyObject* other) {
+  if (!PyObject_TypeCheck(other, &HistogramType)) {
+    PyErr_SetString(PyExc_TypeError, "merge() expects a Histogram");
+    return nullptr;
+  }
+  self->h->merge(*reinterpret_cast<HistogramObject*>(other)->h);
+  Py_RETURN_NONE;
+}
+
+// Serialization for cross-rank aggregation: header (total, sum, min, max) +
+// sparse (index, count) pairs.
+PyObject* hist_to_bytes(HistogramObject* self, PyObject*) {
+  const auto& c = self->h->counts();
+  std::string out;
+  uint64_t hdr[4] = {self->h->total(), 0, self->h->min(), self->h->max()};
+  double s = self->h->sum();
+  memcpy(&hdr[1], &s, 8);
+  out.append(reinterpret_cast<const char*>(hdr), sizeof hdr);
+  for (size_t i = 0; i < c.size(); ++i) {
+    if (!c[i]) continue;
+    uint64_t pair[2] = {uint64_t(i), c[i]};
+    out.append(reinterpret_cast<const char*>(pair), sizeof pair);
+  }
+  return PyBytes_FromStringAndSize(out.data(), Py_ssize_t(out.size()));
+}
+
+PyObject* hist_merge_bytes(HistogramObject* self, PyObject* arg) {
+  char* p;
+  Py_ssize_t n;
+  if (PyBytes_AsStringAndSize(arg, &p, &n) < 0) return nullptr;
+  if (n < 32 || (n - 32) % 16 != 0) {
+    PyErr_SetString(PyExc_ValueError, "corrupt histogram bytes");
+    return nullptr;
+  }
+  uint64_t hdr[4];
+  memcpy(hdr, p, 32);
+  LogHistogram tmp;
+  auto& c = tmp.mutable_counts();
+  for (Py_ssize_t off = 32; off < n; off += 16) {
+    uint64_t pair[2];
+    memcpy(pair, p + off, 16);
+    if (pair[0] >= c.size()) {
+      PyErr_SetString(PyExc_ValueError, "corrupt histogram bytes (bucket index)");
+      return nullptr;
+    }
+    c[pair[0]] += pair[1];
+  }
+  double s;
+  memcpy(&s, &hdr[1], 8);
+  tmp.set_stats(hdr[0], s, hdr[0] ? hdr[2] : UINT64_MAX, hdr[3]);
+  self->h->merge(tmp);
+  Py_RETURN_NONE;
+}
+
+PyObject* hist_summary(HistogramObject* self, PyObject*) {
+  LogHistogram* h = self->h;
+  return Py_BuildValue("{s:K,s:d,s:K,s:K,s:d,s:d,s:d,s:d,s:d}", "count", (unsigned long long)h->total(), "sum",
+                       h->sum(), "min", (unsigned long long)h->min(), "max", (unsigned long long)h->max(), "mean",
+                       h->total() ? h->sum() / double(h->total()) : 0.0, "p50", h->percentile(50), "p90",
+                       h->percentile(90), "p99", h->percentile(99), "p999", h->percentile(99.9));
+}
+
+PyObject* hist_get_count(HistogramObject* self, void*) { return PyLong_FromUnsignedLongLong(self->h->total()); }
+PyObject* hist_get_sum(HistogramObject* self, void*) { return PyFloat_FromDouble(self->h->sum()); }
+PyObject* hist_get_min(HistogramObject* self, void*) { return PyLong_FromUnsignedLongLong(self->h->min()); }
+PyObject* hist_get_max(HistogramObject* self, void*) { return PyLong_FromUnsignedLongLong(self->h->max()); }
+
+PyMethodDef hist_methods[] = {
+    {"record", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(hist_record)), METH_FASTCALL,
+     "record(value, count=1)"},
+    {"record_many", reinterpret_cast<PyCFunction>(hist_record_many), METH_O, "record each value of a sequence"},
+    {"percentile", reinterpret_cast<PyCFunction>(hist_percentile), METH_O, "percentile(p in [0,100])"},
+    {"count_le", reinterpret_cast<PyCFunction>(hist_count_le), METH_O, "number of samples <= value"},
+    {"reset", reinterpret_cast<PyCFunction>(hist_reset), METH_NOARGS, "clear all samples"},
+    {"merge", reinterpret_cast<PyCFunction>(hist_merge), METH_O, "add another Histogram's samples"},
+    {"to_bytes", reinterpret_cast<PyCFunction>(hist_to_bytes), METH_NOARGS, "serialize (sparse)"},
+    {"merge_bytes", reinterpret_cast<PyCFunction>(hist_merge_bytes), METH_O, "merge a to_bytes() payload"},
+    {"summary", reinterpret_cast<PyCFunction>(hist_summary), METH_NOARGS, "dict of count/sum/min/max/percentiles"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyGetSetDef hist_getset[] = {
+    {"count", reinterpret_cast<getter>(hist_get_count), nullptr, "number of samples", nullptr},
+    {"sum", reinterpret_cast<getter>(hist_get_sum), nullptr, "sum of samples", nullptr},
+    {"min", reinterpret_cast<getter>(hist_get_min), nullptr, "smallest sample", nullptr},
+    {"max", reinterpret_cast<getter>(hist_get_max), nullptr, "largest sample", nullptr},
+    {nullptr, nullptr, nullptr, nullptr, nullptr}};
+
+// ================================ Counter ===================================
+PyObject* counter_new(PyTypeObject* type, PyObject*, PyObject*) {
+  CounterObject* self = reinterpret_cast<CounterObject*>(type->tp_alloc(type, 0));
+  if (self) self->value = 0.0;
+  return reinterpret_cast<PyObject*>(self);
+}
+
+void counter_dealloc(CounterObject* self) { Py_TYPE(self)->tp_free(reinterpret_cast<PyObject*>(self)); }
+
+PyObject* counter_inc(CounterObject* self, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs == 0) {
+    self->value += 1.0;
+    Py_RETURN_NONE;
+  }
+  if (nargs > 1) {
+    PyErr_SetString(PyExc_TypeError, "inc(amount=1)");
+    return nullptr;
+  }
+  double d = PyFloat_AsDouble(args[0]);
+  if (d == -1.0 && PyErr_Occurred()) return nullptr;
+  if (!(d >= 0.0) || std::isinf(d)) {
+    // prom-client: "It is not possible to decrease a counter"
+    PyErr_SetString(PyExc_ValueError, "counters can only be incremented by a non-negative finite amount");
+    return nullptr;
+  }
+  self->value += d;
+  Py_RETURN_NONE;
+}
+
+PyObject* counter_reset(CounterObject* self, PyObject*) {
+  self->value = 0.0;
+  Py_RETURN_NONE;
+}
+
+PyObject* counter_get(CounterObject* self, void*) { return PyFloat_FromDouble(self->value); }
+
+PyMethodDef counter_methods[] = {
+    {"inc", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(counter_inc)), METH_FASTCALL,
+     "inc(amount=1)"},
+    {"reset", reinterpret_cast<PyCFunction>(counter_reset), METH_NOARGS, "reset to 0"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyGetSetDef counter_getset[] = {{"value", reinterpret_cast<getter>(counter_get), nullptr, "current value", nullptr},
+                                {nullptr, nullptr, nullptr, nullptr, nullptr}};
+
+}  // namespace
+
+PyTypeObject HistogramType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+PyTypeObject CounterType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+int init_metric_types(PyObject* m) {
+  HistogramType.tp_name = "beholder_amd.ops._native.Histogram";
+  HistogramType.tp_basicsize = sizeof(HistogramObject);
+  HistogramType.tp_flags = Py_TPFLAGS_DEFAULT;
+  HistogramType.tp_doc = "Log-linear histogram of non-negative integers (ns), <0.8% relative error";
+  HistogramType.tp_new = hist_new;
+  HistogramType.tp_dealloc = reinterpret_cast<destructor>(hist_dealloc);
+  HistogramType.tp_methods = hist_methods;
+  HistogramType.tp_getset = hist_getset;
+  if (PyType_Ready(&HistogramType) < 0) return -1;
+
+  CounterType.tp_name = "beholder_amd.ops._native.Counter";
+  CounterType.tp_basicsize = sizeof(CounterObject);
+  CounterType.tp_flags = Py_TPFLAGS_DEFAULT;
+  CounterType.tp_doc = "Monotonic float64 counter (prom-client Counter semantics)";
+  CounterType.tp_new = counter_new;
+  CounterType.tp_dealloc = reinterpret_cast<destructor>(counter_dealloc);
+  CounterType.tp_methods = counter_methods;
+  CounterType.tp_getset = counter_getset;
+  if (PyType_Ready(&CounterType) < 0) return -1;
+
+  Py_INCREF(&HistogramType);
+  if (PyModule_AddObject(m, "Histogram", reinterpret_cast<PyObject*>(&HistogramType)) < 0) return -1;
+  Py_INCREF(&CounterType);
+  if (PyModule_AddObject(m, "Counter", reinterpret_cast<PyObject*>(&CounterType)) < 0) return -1;
+  return 0;
+}
+
+}  // namespace beholder

@@ -1,0 +1,374 @@
+"""Service bootstrap and dispatch loop — ``init()`` of the reference (index.js:23-160).
+
+Startup order mirrors index.js:23-158:
+
+1. config (``Config('events')``)                        index.js:24
+2. Trello client                                         index.js:25
+3. Prometheus registry + HTTP exposure                   index.js:27-28
+4. the two counters                                      index.js:29-40
+5. media store                                           index.js:42
+6. transport connect (prefetch 100)                      index.js:43-44
+7. proto types                                           index.js:46-48
+8. ``listen`` on status + progress                       index.js:62,127
+9. log ``initialized``                                   index.js:157
+
+Differences, all documented fixes:
+
+* **Q10** — ``init()`` in the reference is fire-and-forget; a startup failure
+  is an unhandled rejection that leaves a half-started process. Here startup
+  errors propagate and the CLI exits non-zero.
+* graceful shutdown (SIGTERM/SIGINT): stop consuming, drain in-flight
+  handlers for ``service.shutdown_grace_s``, close transport/store/sinks.
+
+Dispatch: deliveries arrive in batches; each handler coroutine runs eagerly
+(:mod:`beholder_amd.utils.eager`). Handlers that suspend (real I/O) become
+tasks; at most ``service.prefetch`` (default 100, index.js:43) are in flight,
+matching the broker's prefetch window.
+"""
+from __future__ import annotations
+
+import asyncio
+import time
+from typing import Any, Callable, Dict, List, Optional
+
+from . import topics as T
+from .config import Config
+from .handlers import TelemetryHandlers, err_message
+from .metrics import MetricsServer, NativeHistogramView, Registry, default_metrics
+from .metrics.registry import Gauge
+from .parallel.ordering import KeyedSerializer
+from .sinks import AiohttpClient, EmbyClient, HttpClient, TelegramClient, TrelloClient
+from .store import MediaStore, open_store
+from .transport.base import Source
+from .utils.eager import DONE, ERROR, run_eager
+from .utils.log import Logger
+
+Handler = Callable[[Any], Any]
+
+
+def build_source(config: Config, logger: Optional[Logger] = None) -> Source:
+    """Construct the ingest transport from ``service.transport``."""
+    tcfg = config.data["service"]["transport"]
+    kind = (tcfg.get("kind") or "amqp").lower()
+    prefetch = int(config.data["service"]["prefetch"])
+    if kind == "stdin":
+        from .transport.ingest import FdSource
+        return FdSource(policy=tcfg.get("policy", "block"),
+                        capacity_bytes=int(tcfg.get("capacity_bytes", 64 << 20)),
+                        capacity_events=int(tcfg.get("capacity_events", 0)),
+                        dead_letter=tcfg.get("dead_letter"))
+    if kind == "file":
+        from .transport.ingest import FdSource
+        if not tcfg.get("path"):
+            raise ValueError("service.transport.path is required for kind=file")
+        return FdSource(path=tcfg["path"], policy=tcfg.get("policy", "block"),
+                        capacity_bytes=int(tcfg.get("capacity_bytes", 64 << 20)),
+                        capacity_events=int(tcfg.get("capacity_events", 0)),
+                        dead_letter=tcfg.get("dead_letter"))
+    if kind == "amqp":
+        from .dynamics import dyn
+        from .transport.amqp import AmqpSource
+        url = tcfg.get("url") or dyn("rabbitmq", env=config.env, config=config)
+        return AmqpSource(url, prefetch=prefetch, retries=int(config.data["service"]["retries"]),
+                          logger=logger)
+    raise ValueError(f"unknown transport kind {kind!r} (amqp|stdin|file)")
+
+
+class Service:
+    """The beholder service. Inject ``source``/``store``/``http`` for tests and benches."""
+
+    def __init__(self, config: Config, *, source: Optional[Source] = None, store: Optional[MediaStore] = None,
+                 http: Optional[HttpClient] = None, registry: Optional[Registry] = None,
+                 logger: Optional[Logger] = None, serve_metrics: Optional[bool] = None):
+        self.config = config
+        svc = config.data["service"]
+        self.log = logger or Logger(name=svc["log"]["name"], level=svc["log"]["level"])
+        self._source = source
+        self._store = store
+        self._http = http
+        self.registry = registry
+        self._serve_metrics = svc["metrics"]["enabled"] if serve_metrics is None else serve_metrics
+        self.metrics_server: Optional[MetricsServer] = None
+        self.prefetch = int(svc["prefetch"])
+        self.on_status_error = svc["on_status_error"]
+        self.ordering = svc["ordering"]
+        self.grace_s = float(svc["shutdown_grace_s"])
+        self._routes: List[Optional[Handler]] = [None] * len(T.TOPIC_NAMES_BY_ID)
+        self._inflight: set = set()
+        self._slot_free: Optional[asyncio.Event] = None
+        self._stop = False
+        self._running = False
+        self._initialized = False
+        self.handlers: Optional[TelemetryHandlers] = None
+        self.serializer: Optional[KeyedSerializer] = None
+        self.started_at = 0.0
+        self.received = [0] * len(T.TOPIC_NAMES_BY_ID)
+
+    # ------------------------------------------------------------ properties --
+    @property
+    def source(self) -> Source:
+        assert self._source is not None, "service not initialised"
+        return self._source
+
+    @property
+    def store(self) -> MediaStore:
+        assert self._store is not None, "service not initialised"
+        return self._store
+
+    # ------------------------------------------------------------------ init --
+    async def init(self) -> "Service":
+        cfg = self.config
+        svc = cfg.data["service"]
+        keys = cfg.root.require("keys.trello")
+        # 2. Trello client (index.js:25)
+        if self._http is None:
+            self._http = AiohttpClient(timeout_s=float(svc["http"]["timeout_s"]))
+        endpoints = svc["endpoints"]
+        self.trello = TrelloClient(keys.get("key"), keys.get("token"), self._http, base_url=endpoints["trello"])
+        self.telegram = TelegramClient(None, self._http, base_url=endpoints["telegram"])
+        self.emby = EmbyClient(None, None, self._http)
+
+        # 3-4. registry + counters (index.js:27-40)
+        if self.registry is None:
+            self.registry = Registry("beholder")
+        reg = self.registry
+        self.progress_updates_total = reg.counter(
+            "beholder_progress_updates_total", "Total number of messages processed in this processes lifetime",
+            ["status"])
+        # name without `_total` and the "crreated" typo are the reference's (index.js:35-38)
+        self.trello_comments_total = reg.counter(
+            "beholder_trello_comments", "Total trello comments crreated in this processes lifetime")
+        self._register_service_metrics(reg)
+        if svc["metrics"].get("default_metrics", True):
+            reg.add_collector(default_metrics)
+        if self._serve_metrics:
+            m = svc["metrics"]
+            self.metrics_server = await MetricsServer(reg, m["host"], int(m["port"]), health=self.healthy,
+                                                      stats=self.stats, logger=self.log).start()
+
+        # 5. store (index.js:42)
+        if self._store is None:
+            st = svc["store"]
+            self._store = open_store(st.get("backend", "memory"), st.get("dsn"))
+        await self._store.connect()
+
+        # 6. transport (index.js:43-44)
+        if self._source is None:
+            self._source = build_source(cfg, self.log)
+
+        # 7. proto types + handlers (index.js:46-60)
+        self.handlers = TelemetryHandlers(
+            config=cfg, store=self._store, trello=self.trello, telegram=self.telegram, emby=self.emby,
+            progress_counter=self.progress_updates_total, comments_counter=self.trello_comments_total,
+            logger=self.log)
+
+        # 8. listeners (index.js:62,127)
+        self.listen(T.STATUS, self.handlers.on_status)
+        self.listen(T.PROGRESS, self.handlers.on_progress)
+        await self._source.start([t for t in T.TOPIC_IDS if self._routes[T.TOPIC_IDS[t]] is not None])
+        if self.ordering == "per_media":
+            self.serializer = KeyedSerializer(self._dispatch_now, self._media_key)
+
+        # 9.
+        self._initialized = True
+        self.started_at = time.time()
+        self.log.info("initialized")
+        return self
+
+    def _media_key(self, d) -> Any:
+        h = self.handlers
+        if d.topic_id == T.STATUS_ID:
+            return h.decode_status(d.content).mediaId
+        if d.topic_id == T.PROGRESS_ID:
+            return h.decode_progress(d.content).mediaId
+        return None
+
+    def listen(self, topic: str, handler: Handler) -> None:
+        """``amqp.listen(topic, fn)`` — register the handler for a topic."""
+        self._routes[T.topic_id(topic)] = handler
+
+    # --------------------------------------------------------------- metrics --
+    def _register_service_metrics(self, reg: Registry) -> None:
+        """Our additions for the §6 measurement plan (ingest rate, latency, drops)."""
+
+        def settler():
+            return self._source.settler if self._source is not None else None
+
+        def ack_collect(g: Gauge):
+            s = settler()
+            if s is not None:
+                st = s.stats()
+                for k in ("acked", "nacked", "rejected", "abandoned", "pending"):
+                    g.set({"state": k}, st[k])
+
+        reg.register(Gauge("beholder_deliveries", "Deliveries by settlement state since start "
+                           "(abandoned = never acked, reference quirk Q1)", ["state"], collect=ack_collect))
+
+        def recv_collect(g: Gauge):
+            for tid, n in enumerate(self.received):
+                if T.TOPIC_NAMES_BY_ID[tid]:
+                    g.set({"topic": T.TOPIC_NAMES_BY_ID[tid]}, n)
+
+        reg.register(Gauge("beholder_messages_received", "Messages received per topic since start", ["topic"],
+                           collect=recv_collect))
+        self.handler_errors = reg.counter("beholder_handler_errors_total",
+                                          "Handler invocations that raised (status handler: quirk Q1)", ["topic"])
+
+        def drop_collect(g: Gauge):
+            st = self._source.stats() if self._source is not None else {}
+            for tid, n in (st.get("dropped_by_topic") or {}).items():
+                g.set({"topic": T.topic_name(int(tid)) or str(tid)}, n)
+
+        reg.register(Gauge("beholder_ingest_dropped", "Messages dropped by ingest backpressure", ["topic"],
+                           collect=drop_collect))
+        reg.register(Gauge("beholder_inflight", "Handlers currently suspended on I/O",
+                           collect=lambda g: g.set(len(self._inflight))))
+
+        reg.register(NativeHistogramView("beholder_handle_latency_seconds",
+                                         "Handler start to ack latency",
+                                         lambda: settler().handle_latency if settler() is not None else None))
+        reg.register(NativeHistogramView("beholder_ingest_latency_seconds",
+                                         "Receive to ack latency (includes queueing)",
+                                         lambda: settler().ingest_latency if settler() is not None else None))
+
+    # ------------------------------------------------------------------ run ---
+    def healthy(self) -> bool:
+        return self._initialized and not self._stop and (self._source is None or self._source.ready())
+
+    def request_stop(self) -> None:
+        self._stop = True
+        if self._source is not None:
+            asyncio.ensure_future(self._source.close())
+
+    async def run(self) -> Dict[str, Any]:
+        """Consume until the source ends or :meth:`request_stop`; then drain and return stats."""
+        if not self._initialized:
+            await self.init()
+        self._running = True
+        self._slot_free = asyncio.Event()
+        log = self.log
+        routes = self._routes
+        nroutes = len(routes)
+        received = self.received
+        dispatch = self.serializer.submit if self.serializer is not None else self._dispatch_now
+        try:
+            async for batch in self.source.batches():
+                for d in batch:
+                    tid = d.topic_id
+                    if tid >= nroutes or routes[tid] is None:
+                        self._unroutable(d)
+                        continue
+                    received[tid] += 1
+                    dispatch(d)
+                if len(self._inflight) >= self.prefetch:
+                    await self._wait_slots()
+                log.flush()
+                if self._stop:
+                    break
+        finally:
+            self._running = False
+            await self._drain()
+            log.flush()
+        return self.stats()
+
+    def _dispatch_now(self, d, on_finish: Optional[Callable[[], None]] = None) -> None:
+        handler = self._routes[d.topic_id]
+        d.start()
+        kind, val = run_eager(handler(d))
+        if kind == DONE:
+            if on_finish is not None:
+                on_finish()
+            return
+        if kind == ERROR:
+            self._on_handler_error(d, val)
+            if on_finish is not None:
+                on_finish()
+            return
+        task = val
+        self._inflight.add(task)
+
+        def _done(t, d=d):
+            self._inflight.discard(t)
+            if not t.cancelled():
+                exc = t.exception()
+                if exc is not None:
+                    self._on_handler_error(d, exc)
+            if on_finish is not None:
+                on_finish()
+            if self._slot_free is not None and len(self._inflight) < self.prefetch:
+                self._slot_free.set()
+
+        task.add_done_callback(_done)
+
+    async def _wait_slots(self) -> None:
+        while len(self._inflight) >= self.prefetch:
+            self._slot_free.clear()
+            await self._slot_free.wait()
+
+    def _on_handler_error(self, d, exc: BaseException) -> None:
+        topic = d.topic or str(d.topic_id)
+        self.handler_errors.labels(topic).inc()
+        # Node would print an UnhandledPromiseRejectionWarning here (index.js:62 has no catch).
+        self.log.error(f"unhandled error in {topic} handler: {err_message(exc)}")
+        if d.settled:
+            return
+        policy = self.on_status_error
+        try:
+            if policy == "nack_requeue":
+                d.nack(True)
+            elif policy == "nack_drop":
+                d.nack(False)
+            # leave_unacked: reference behaviour (Q1) — the delivery stays pending
+        except Exception as e:  # noqa: BLE001
+            self.log.warn("failed to settle errored delivery:", err_message(e))
+
+    def _unroutable(self, d) -> None:
+        self.log.warn(f"dropping message for unknown topic id {d.topic_id}")
+        if not d.settled:
+            d.reject(False)
+
+    async def _drain(self) -> None:
+        if self.serializer is not None:
+            await self.serializer.drain(self.grace_s)
+        if self._inflight:
+            done, pending = await asyncio.wait(list(self._inflight), timeout=self.grace_s)
+            for t in pending:
+                t.cancel()
+
+    async def close(self) -> None:
+        """Release transport, store, HTTP client and the metrics server."""
+        if self._source is not None:
+            await self._source.close()
+        if self._store is not None:
+            await self._store.close()
+        if self._http is not None:
+            await self._http.close()
+        if self.metrics_server is not None:
+            await self.metrics_server.stop()
+        self.log.flush()
+
+    # ---------------------------------------------------------------- stats ---
+    def stats(self) -> Dict[str, Any]:
+        out: Dict[str, Any] = {"received": {T.TOPIC_NAMES_BY_ID[i]: n for i, n in enumerate(self.received) if i},
+                               "inflight": len(self._inflight)}
+        if self._source is not None:
+            out["source"] = self._source.stats()
+            s = self._source.settler
+            if s is not None:
+                out["handle_latency_ns"] = s.handle_latency.summary()
+                out["ingest_latency_ns"] = s.ingest_latency.summary()
+        if self.registry is not None and hasattr(self, "handler_errors"):
+            out["handler_errors"] = {k[0]: v for k, v in self.handler_errors.values().items()}
+            out["trello_comments"] = self.trello_comments_total.get()
+            out["progress_updates"] = {k[0]: v for k, v in self.progress_updates_total.values().items()}
+        return out
+
+
+async def run_service(config: Config, **kw) -> Dict[str, Any]:
+    """Build, initialise, run to completion and close a service."""
+    svc = Service(config, **kw)
+    try:
+        await svc.init()
+        return await svc.run()
+    finally:
+        await svc.close()

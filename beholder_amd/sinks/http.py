@@ -1,0 +1,221 @@
+"""Outbound HTTP clients for the sinks.
+
+Two reference semantics matter (SURVEY.md §2.4 "Outbound HTTP"):
+
+* ``request-promise-native`` (Telegram, Emby — index.js:99,112) **rejects on
+  non-2xx** (``simple: true``): ``StatusCodeError: 500 - "body"``;
+* the ``trello`` npm client (index.js:53,83) resolves with the body on *any*
+  HTTP status and only rejects on transport errors.
+
+``HttpClient.request`` returns an :class:`HttpResponse`; callers decide
+whether a status is an error (:meth:`HttpResponse.raise_for_status`).
+
+Query strings are encoded like ``encodeURIComponent`` (Node's ``querystring``)
+so URLs are byte-identical to the reference's.
+"""
+from __future__ import annotations
+
+import abc
+import asyncio
+import collections
+import json as _json
+import time
+from typing import Any, Callable, Deque, Dict, List, Mapping, Optional, Tuple
+from urllib.parse import quote
+
+from ..ops import encode_query as _native_encode_query
+
+_SAFE = "-_.!~*'()"
+
+
+def js_qs_value(v: Any) -> str:
+    """``querystring.stringify`` value rendering (bool→'true', None→'', numbers JS-style)."""
+    from ..utils.log import js_number
+    if v is None:
+        return ""
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, (int, float)):
+        return js_number(v)
+    return str(v)
+
+
+def py_encode_query(params: Optional[Mapping[str, Any]]) -> str:
+    """Pure-Python reference for :func:`encode_query` (tests pin the native one to it)."""
+    if not params:
+        return ""
+    return "&".join(f"{quote(str(k), safe=_SAFE)}={quote(js_qs_value(v), safe=_SAFE)}" for k, v in params.items())
+
+
+def encode_query(params: Optional[Mapping[str, Any]]) -> str:
+    if not params:
+        return ""
+    if type(params) is not dict:
+        params = dict(params)
+    return _native_encode_query(params)
+
+
+def with_query(url: str, params: Optional[Mapping[str, Any]]) -> str:
+    q = encode_query(params)
+    if not q:
+        return url
+    return url + ("&" if "?" in url else "?") + q
+
+
+class HttpError(Exception):
+    """Transport failure or (for strict callers) a non-2xx status."""
+
+    def __init__(self, message: str, status: Optional[int] = None, body: bytes = b""):
+        super().__init__(message)
+        self.status = status
+        self.body = body
+
+    @property
+    def message(self) -> str:
+        return str(self)
+
+
+class HttpResponse:
+    __slots__ = ("status", "body", "headers", "url")
+
+    def __init__(self, status: int, body: bytes = b"", headers: Optional[Mapping[str, str]] = None, url: str = ""):
+        self.status = status
+        self.body = body
+        self.headers = dict(headers or {})
+        self.url = url
+
+    @property
+    def ok(self) -> bool:
+        return 200 <= self.status < 300
+
+    def text(self) -> str:
+        return self.body.decode("utf-8", "replace")
+
+    def json(self) -> Any:
+        return _json.loads(self.body or b"null")
+
+    def raise_for_status(self) -> "HttpResponse":
+        if not self.ok:
+            # request-promise StatusCodeError: `${statusCode} - ${JSON.stringify(body)}`
+            raise HttpError(f"{self.status} - {_json.dumps(self.text())}", self.status, self.body)
+        return self
+
+
+class HttpClient(abc.ABC):
+    @abc.abstractmethod
+    async def request(self, method: str, url: str, *, params: Optional[Mapping[str, Any]] = None,
+                      timeout: Optional[float] = None) -> HttpResponse:
+        ...
+
+    async def close(self) -> None:
+        pass
+
+
+class AiohttpClient(HttpClient):
+    """Production client on aiohttp (connection pooling, per-request timeout)."""
+
+    def __init__(self, timeout_s: float = 30.0, user_agent: str = "beholder/1.0"):
+        self.timeout_s = timeout_s
+        self.user_agent = user_agent
+        self._session = None
+
+    async def _sess(self):
+        if self._session is None or self._session.closed:
+            import aiohttp
+            self._session = aiohttp.ClientSession(headers={"User-Agent": self.user_agent})
+        return self._session
+
+    async def request(self, method, url, *, params=None, timeout=None) -> HttpResponse:
+        import aiohttp
+        full = with_query(url, params)
+        sess = await self._sess()
+        try:
+            to = aiohttp.ClientTimeout(total=timeout or self.timeout_s)
+            # encoded=True: keep our encodeURIComponent-style query untouched
+            from yarl import URL
+            async with sess.request(method.upper(), URL(full, encoded=True), timeout=to) as r:
+                body = await r.read()
+                return HttpResponse(r.status, body, dict(r.headers), full)
+        except asyncio.TimeoutError as e:
+            raise HttpError(f"ETIMEDOUT: {method.upper()} {url}") from e
+        except aiohttp.ClientError as e:
+            raise HttpError(f"{type(e).__name__}: {e}") from e
+
+    async def close(self) -> None:
+        if self._session is not None and not self._session.closed:
+            await self._session.close()
+
+
+Rule = Tuple[str, str, Callable[[str, str], Any]]
+
+
+class RecordingHttpClient(HttpClient):
+    """In-process fake: records every request and answers from rules.
+
+    ``add_rule(method, url_prefix, fn)`` — ``fn(method, url)`` returns an
+    ``HttpResponse``, an ``int`` status, or raises (fault injection). Without a
+    matching rule the answer is ``200 {}``. ``keep`` bounds the call log (the
+    total count is always exact), so benches can use it as a null sink.
+    ``delay_s`` simulates network latency (forces a real suspension).
+    """
+
+    def __init__(self, keep: Optional[int] = None, delay_s: float = 0.0):
+        self.calls: Deque[Tuple[str, str]] = collections.deque(maxlen=keep)
+        self.count = 0
+        self.rules: List[Rule] = []
+        self.delay_s = delay_s
+
+    def add_rule(self, method: str, url_prefix: str, fn) -> None:
+        self.rules.append((method.upper(), url_prefix, fn))
+
+    def fail(self, method: str, url_prefix: str, status: Optional[int] = None, message: str = "ECONNREFUSED"):
+        if status is None:
+            def boom(m, u):
+                raise HttpError(message)
+            self.add_rule(method, url_prefix, boom)
+        else:
+            self.add_rule(method, url_prefix, lambda m, u: HttpResponse(status, b'"error"', url=u))
+
+    async def request(self, method, url, *, params=None, timeout=None) -> HttpResponse:
+        m = method.upper()
+        full = with_query(url, params)
+        self.count += 1
+        self.calls.append((m, full))
+        if self.delay_s:
+            await asyncio.sleep(self.delay_s)
+        for rm, pref, fn in self.rules:
+            if (rm == "*" or rm == m) and full.startswith(pref):
+                r = fn(m, full)
+                if isinstance(r, int):
+                    return HttpResponse(r, b"{}", url=full)
+                return r
+        return HttpResponse(200, b"{}", url=full)
+
+    def urls(self, method: Optional[str] = None) -> List[str]:
+        return [u for m, u in self.calls if method is None or m == method.upper()]
+
+
+class TimedHttpClient(HttpClient):
+    """Wraps a client and feeds per-sink request metrics (count by code, latency)."""
+
+    def __init__(self, inner: HttpClient, on_result: Callable[[str, Optional[int], float], None]):
+        self.inner = inner
+        self.on_result = on_result
+
+    async def request(self, method, url, *, params=None, timeout=None) -> HttpResponse:
+        t0 = time.perf_counter()
+        try:
+            r = await self.inner.request(method, url, params=params, timeout=timeout)
+        except Exception:
+            self.on_result(url, None, time.perf_counter() - t0)
+            raise
+        self.on_result(url, r.status, time.perf_counter() - t0)
+        return r
+
+    async def close(self) -> None:
+        await self.inner.close()
+
+
+def parse_query(url: str) -> Dict[str, str]:
+    from urllib.parse import parse_qsl, urlsplit
+    return dict(parse_qsl(urlsplit(url).query, keep_blank_values=True))

@@ -1,0 +1,60 @@
+"""Trello sink — the subset of the ``trello`` npm client (0.9.1) beholder uses.
+
+Reference: ``new Trello(key, token)`` (index.js:25) and
+``trello.makeRequest(method, path, body)`` for
+
+* comments: ``POST /1/cards/{cardId}/actions/comments {text}`` (index.js:53-55);
+* card moves: ``PUT /1/cards/{creatorId} {idList, pos: 2}`` (index.js:83-86).
+
+The npm client sends ``key``/``token`` and every body field as query-string
+parameters against ``https://api.trello.com`` and resolves with the response
+body on any HTTP status (only transport errors reject). Both behaviours are
+kept; ``strict=True`` opts into raising on non-2xx.
+"""
+from __future__ import annotations
+
+from typing import Any, Mapping, Optional
+
+from .http import HttpClient, HttpError, HttpResponse
+
+COMMENT_FALLBACK = "Failed to retrieve comment text."  # index.js:54
+
+_METHODS = ("get", "post", "put", "delete")
+
+
+class TrelloClient:
+    def __init__(self, key: Optional[str], token: Optional[str], http: HttpClient,
+                 base_url: str = "https://api.trello.com", strict: bool = False, timeout: Optional[float] = None):
+        self.key = key
+        self.token = token
+        self.http = http
+        self.base_url = base_url.rstrip("/")
+        self.strict = strict
+        self.timeout = timeout
+
+    def create_query(self) -> dict:
+        return {"key": self.key, "token": self.token}
+
+    async def make_request(self, method: str, path: str, options: Optional[Mapping[str, Any]] = None) -> HttpResponse:
+        """``trello.makeRequest(requestMethod, path, options)``."""
+        m = method.lower()
+        if m not in _METHODS:
+            raise HttpError("Unsupported requestMethod. Pass one of these methods: POST, GET, PUT, DELETE.")
+        if not path.startswith("/"):
+            raise HttpError("Path must start with /")
+        query = self.create_query()
+        for k, v in (options or {}).items():
+            query[k] = v
+        r = await self.http.request(m.upper(), self.base_url + path, params=query, timeout=self.timeout)
+        if self.strict:
+            r.raise_for_status()
+        return r
+
+    makeRequest = make_request  # noqa: N815 (reference name)
+
+    async def add_comment(self, card_id: str, text: Optional[str]) -> HttpResponse:
+        return await self.make_request("post", f"/1/cards/{card_id}/actions/comments",
+                                       {"text": text or COMMENT_FALLBACK})
+
+    async def move_card(self, card_id: str, list_id: str, pos: Any = 2) -> HttpResponse:
+        return await self.make_request("put", f"/1/cards/{card_id}", {"idList": list_id, "pos": pos})

@@ -1,0 +1,110 @@
+"""Media storage interface — parity with ``triton-core/db`` as beholder uses it.
+
+The reference uses exactly two methods of ``new Storage()`` (index.js:42):
+
+* ``updateStatus(mediaId, status)`` — index.js:68 (status handler, before the
+  ``NO_TRELLO`` short-circuit);
+* ``getByID(mediaId)`` → ``{creator, creatorId, status, name, metadataId}`` —
+  index.js:76 and :140.
+
+Semantics we pin down (triton-core is not vendored, so these are documented
+choices): ``update_status`` of an unknown id is a no-op (an SQL ``UPDATE``
+matching zero rows); ``get_by_id`` of an unknown id raises
+:class:`MediaNotFound` — in the reference ``media.creator`` on a missing row
+throws a ``TypeError`` either way, so the handler-level outcome is identical
+(status: un-acked, Q1; progress: warn + ack, Q7).
+"""
+from __future__ import annotations
+
+import abc
+from typing import Iterable, NamedTuple, Optional
+
+
+class MediaNotFound(LookupError):
+    def __init__(self, media_id: str):
+        super().__init__(f"media {media_id!r} not found")
+        self.media_id = media_id
+
+
+class StoreError(RuntimeError):
+    pass
+
+
+class Media(NamedTuple):
+    """One media row (fields of ``api.Media``, see models/proto/api.proto).
+
+    Rows are immutable values: a read returns the stored tuple itself (no
+    per-read copy), an update stores a new tuple (``_replace``).
+    """
+
+    id: str
+    name: str = ""
+    creator: int = 0          # CreatorType; TRELLO == 1 (index.js:79)
+    creatorId: str = ""       # Trello card id (index.js:82-83,147)
+    type: int = 0
+    source: int = 0
+    sourceURI: str = ""
+    metadata: int = 0
+    metadataId: str = ""      # Kitsu id (index.js:103)
+    status: int = 0           # TelemetryStatusEntry (index.js:94)
+
+    def as_dict(self) -> dict:
+        return self._asdict()
+
+
+FIELDS = Media._fields
+
+
+class MediaStore(abc.ABC):
+    """Async media-store interface. Implementations: memory, sqlite, postgres."""
+
+    name = "abstract"
+
+    async def connect(self) -> None:
+        """Open connections (called once by the service at startup)."""
+
+    async def close(self) -> None:
+        """Release resources."""
+
+    @abc.abstractmethod
+    async def update_status(self, media_id: str, status: int) -> None:
+        """``db.updateStatus`` (index.js:68)."""
+
+    @abc.abstractmethod
+    async def get_by_id(self, media_id: str) -> Media:
+        """``db.getByID`` (index.js:76,140); raises :class:`MediaNotFound`."""
+
+    # -- administration (used by tools/tests; not on the reference hot path) --
+    @abc.abstractmethod
+    async def upsert(self, media: Media) -> None:
+        ...
+
+    async def upsert_many(self, medias: Iterable[Media]) -> None:
+        for m in medias:
+            await self.upsert(m)
+
+    @abc.abstractmethod
+    async def count(self) -> int:
+        ...
+
+    # camelCase aliases (triton-core API names)
+    async def updateStatus(self, media_id: str, status: int) -> None:  # noqa: N802
+        await self.update_status(media_id, status)
+
+    async def getByID(self, media_id: str) -> Media:  # noqa: N802
+        return await self.get_by_id(media_id)
+
+
+def open_store(backend: str, dsn: Optional[str] = None, **kw) -> MediaStore:
+    """Factory used by the service from ``service.store`` config."""
+    backend = (backend or "memory").lower()
+    if backend == "memory":
+        from .memory import MemoryStore
+        return MemoryStore(**kw)
+    if backend == "sqlite":
+        from .sqlite import SqliteStore
+        return SqliteStore(dsn or ":memory:", **kw)
+    if backend in ("postgres", "postgresql", "pg"):
+        from .postgres import PostgresStore
+        return PostgresStore(dsn, **kw)
+    raise ValueError(f"unknown store backend {backend!r} (memory|sqlite|postgres)")

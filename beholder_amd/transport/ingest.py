@@ -1,0 +1,166 @@
+"""File-descriptor source: framed stdin / file / pipe / FIFO via the native reader.
+
+The native :class:`~beholder_amd.ops.Ingest` owns a reader thread that reads
+the fd in large chunks, splits frames and copies them into a bounded byte ring
+without holding the GIL; this source pops whole batches of
+:class:`~beholder_amd.ops.Delivery` objects for the event loop.
+
+Waiting for data never blocks the loop: a non-blocking ``pop`` is tried
+first (the common case under load), and only an empty ring parks in a
+worker thread with a short timeout.
+
+Backpressure (BASELINE config 4): ``policy='block'`` makes the reader stall
+when the ring is full (the kernel pipe then fills and the producer blocks);
+``policy='drop_newest'`` drops and counts per topic
+(``stats()['dropped_by_topic']``).
+
+Ack semantics: there is no broker behind a file, so an ack just settles the
+delivery (latency + counters). A delivery that is never acked (quirk Q1) is
+reported through ``on_abandon`` — optionally appended to a dead-letter file
+in the same frame format so it can be replayed.
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+import sys
+import threading
+from typing import List, Optional, Sequence
+
+from ..ops import Ingest, Settler, frame
+from .base import Source
+
+
+class FdSource(Source):
+    kind = "fd"
+
+    def __init__(self, fd: Optional[int] = None, path: Optional[str] = None, *,
+                 capacity_bytes: int = 64 << 20, capacity_events: int = 0, policy: str = "block",
+                 batch: int = 512, chunk_bytes: int = 1 << 20, dead_letter: Optional[str] = None,
+                 idle_timeout: float = 0.05):
+        if fd is None and path is None:
+            fd = sys.stdin.fileno()
+        self._fd = fd
+        self._path = path
+        self._own_fd = path is not None
+        self.batch = batch
+        self.chunk_bytes = chunk_bytes
+        self.idle_timeout = idle_timeout
+        self._dl_path = dead_letter
+        self._dl_file = None
+        self._dl_lock = threading.Lock()
+        self.abandoned_frames = 0
+        self._settler = Settler(on_abandon=self._on_abandon)
+        self._ingest = Ingest(capacity_bytes=capacity_bytes, capacity_events=capacity_events,
+                              policy=policy, settler=self._settler)
+        self._started = False
+        self._closed = False
+
+    # -- Source API -------------------------------------------------------------
+    async def start(self, topics: Sequence[str] = ()) -> None:
+        if self._started:
+            return
+        fd = self._fd
+        if self._path is not None:
+            fd = os.open(self._path, os.O_RDONLY)
+            self._fd = fd
+        self._ingest.start_reader(fd, chunk_bytes=self.chunk_bytes, own_fd=self._own_fd)
+        self._started = True
+
+    async def batches(self):
+        ing = self._ingest
+        loop = asyncio.get_running_loop()
+        n = self.batch
+        while True:
+            got = ing.pop(n, 0.0)
+            if got is None:
+                return
+            if not got:
+                got = await loop.run_in_executor(None, ing.pop, n, self.idle_timeout)
+                if got is None:
+                    return
+                if not got:
+                    continue
+            yield got
+
+    async def close(self) -> None:
+        if self._closed:
+            return
+        self._closed = True
+        self._ingest.close()
+        if self._dl_file is not None:
+            self._dl_file.close()
+            self._dl_file = None
+
+    @property
+    def settler(self) -> Settler:
+        return self._settler
+
+    @property
+    def ingest(self) -> Ingest:
+        return self._ingest
+
+    def stats(self) -> dict:
+        s = self._ingest.stats()
+        s.update(self._settler.stats())
+        s["abandoned_frames_written"] = self.abandoned_frames
+        return s
+
+    def ready(self) -> bool:
+        return self._started and not self._closed
+
+    # -- dead letters -------------------------------------------------------------
+    def _on_abandon(self, tag: int, topic_id: int, content: bytes) -> None:
+        if self._dl_path is None:
+            return
+        with self._dl_lock:
+            if self._dl_file is None:
+                self._dl_file = open(self._dl_path, "ab")
+            self._dl_file.write(frame(topic_id, content))
+            self.abandoned_frames += 1
+
+
+class BytesSource(FdSource):
+    """Feeds an in-memory framed buffer through the same ring (tests / tools)."""
+
+    kind = "bytes"
+
+    def __init__(self, data: bytes, **kw):
+        r, w = os.pipe()
+        super().__init__(fd=r, **kw)
+        self._own_fd = True
+        self._data = data
+        self._wfd = w
+        self._writer: Optional[threading.Thread] = None
+
+    async def start(self, topics: Sequence[str] = ()) -> None:
+        await super().start(topics)
+
+        def pump():
+            try:
+                mv = memoryview(self._data)
+                while mv:
+                    n = os.write(self._wfd, mv[:1 << 20])
+                    mv = mv[n:]
+            except OSError:
+                pass
+            finally:
+                os.close(self._wfd)
+
+        self._writer = threading.Thread(target=pump, name="bytes-source", daemon=True)
+        self._writer.start()
+
+    async def close(self) -> None:
+        await super().close()
+        if self._writer is not None:
+            self._writer.join(timeout=5)
+
+
+def read_all(source: FdSource) -> List:
+    """Synchronously drain a source (tests)."""
+    out = []
+    while True:
+        got = source.ingest.pop(1 << 16, 1.0)
+        if got is None:
+            return out
+        out.extend(got)

@@ -1,0 +1,335 @@
+"""pino-compatible JSON-lines logger (reference: ``index.js:11-13``).
+
+The reference logs with ``pino({name: path.basename(__filename)})``, i.e. one
+JSON object per line::
+
+    {"level":30,"time":1571234567890,"pid":7,"hostname":"box","name":"index.js","msg":"initialized","v":1}
+
+Levels are pino's numeric levels (trace 10 … fatal 60). ``logger.info(obj,
+'msg')`` merges ``obj``'s keys into the line, as pino does.
+
+Message formatting follows pino's ``quick-format-unescaped`` for ``%s %d %i
+%f %j %o %O %%``. **Documented fix of quirk Q11** (SURVEY.md §2.6): pino v5
+silently *drops* positional arguments that have no format specifier, so the
+reference's ``logger.info('creating comment on', cardId, 'with text:', text)``
+(index.js:51) logs only ``"creating comment on"``. We append such extra
+arguments space-separated (like ``util.format``) so the information survives.
+
+Values are rendered with JavaScript's ``String()`` rules (:func:`js_str`), so
+message text matches the reference's template literals (``45`` not ``45.0``,
+``undefined`` for a missing value).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import socket
+import sys
+import threading
+import time
+from typing import Any, Dict, Optional, TextIO
+
+LEVELS: Dict[str, float] = {
+    "trace": 10, "debug": 20, "info": 30, "warn": 40, "error": 50, "fatal": 60,
+    "silent": math.inf,
+}
+
+
+def js_number(x: float) -> str:
+    """``String(x)`` for a JS number (ECMAScript Number::toString)."""
+    if isinstance(x, bool):
+        return "true" if x else "false"
+    if isinstance(x, int):
+        return str(x)
+    if x != x:
+        return "NaN"
+    if x == math.inf:
+        return "Infinity"
+    if x == -math.inf:
+        return "-Infinity"
+    if x == 0:
+        return "0"
+    sign = "-" if x < 0 else ""
+    r = repr(abs(x))  # shortest round-trip digits
+    if "e" in r:
+        mant, exp = r.split("e")
+        exp_i = int(exp)
+    else:
+        mant, exp_i = r, 0
+    if "." in mant:
+        ip, fp = mant.split(".")
+    else:
+        ip, fp = mant, ""
+    digits = (ip + fp).lstrip("0")
+    # decimal point position n relative to the first significant digit
+    lead_zeros = len(ip + fp) - len((ip + fp).lstrip("0"))
+    n = len(ip) - lead_zeros + exp_i
+    digits = digits.rstrip("0") or "0"
+    k = len(digits)
+    if k <= n <= 21:
+        s = digits + "0" * (n - k)
+    elif 0 < n <= 21:
+        s = digits[:n] + "." + digits[n:]
+    elif -6 < n <= 0:
+        s = "0." + "0" * (-n) + digits
+    else:
+        e = n - 1
+        es = ("+" if e >= 0 else "-") + str(abs(e))
+        s = digits[0] + ("." + digits[1:] if k > 1 else "") + "e" + es
+    return sign + s
+
+
+def js_str(v: Any) -> str:
+    """``String(v)`` with JS semantics for the types the service logs."""
+    if v is None:
+        return "undefined"
+    if isinstance(v, str):
+        return v
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, (int, float)):
+        return js_number(v)
+    if isinstance(v, (list, tuple)):
+        return ",".join("" if x is None else js_str(x) for x in v)
+    if isinstance(v, dict):
+        return "[object Object]"
+    if isinstance(v, BaseException):
+        return f"{type(v).__name__}: {v}"
+    return str(v)
+
+
+def _json_safe(v: Any) -> Any:
+    try:
+        json.dumps(v)
+        return v
+    except (TypeError, ValueError):
+        return js_str(v)
+
+
+def quick_format(args: tuple) -> str:
+    """Format positional args like pino v5 (see module doc for the Q11 fix)."""
+    if not args:
+        return ""
+    f = args[0]
+    rest = args[1:]
+    if not isinstance(f, str):
+        return " ".join(js_str(a) for a in args)
+    if not rest:
+        return f
+    out = []
+    ai = 0
+    i = 0
+    last = 0
+    n = len(f)
+    while i < n - 1:
+        if f[i] == "%":
+            c = f[i + 1]
+            if c == "%":
+                out.append(f[last:i] + "%")
+                i += 2
+                last = i
+                continue
+            if c in "sdifjoO" and ai < len(rest):
+                a = rest[ai]
+                ai += 1
+                if c == "s":
+                    rep = js_str(a)
+                elif c in "di":
+                    try:
+                        num = float(a) if not isinstance(a, (int, float)) else a
+                        rep = js_number(math.floor(num) if c == "i" and num == num and abs(num) != math.inf else num)
+                    except (TypeError, ValueError):
+                        rep = "NaN"
+                elif c == "f":
+                    try:
+                        rep = js_number(float(a))
+                    except (TypeError, ValueError):
+                        rep = "NaN"
+                else:
+                    try:
+                        rep = json.dumps(a, separators=(",", ":"), ensure_ascii=False)
+                    except (TypeError, ValueError):
+                        rep = '"[Circular]"'
+                out.append(f[last:i] + rep)
+                i += 2
+                last = i
+                continue
+        i += 1
+    out.append(f[last:])
+    s = "".join(out)
+    if ai < len(rest):
+        s += " " + " ".join(js_str(a) for a in rest[ai:])
+    return s
+
+
+class Logger:
+    """Minimal pino: ``trace/debug/info/warn/error/fatal(*args)``, ``child(**bindings)``."""
+
+    def __init__(self, name: str = "index.js", level: str = "info", stream: Optional[TextIO] = None,
+                 bindings: Optional[dict] = None, _shared: Optional[dict] = None):
+        if level not in LEVELS:
+            raise ValueError(f"unknown log level {level!r}")
+        self.name = name
+        self._shared = _shared if _shared is not None else {
+            "stream": stream if stream is not None else sys.stdout,
+            "lock": threading.Lock(),
+            "pid": os.getpid(),
+            "hostname": socket.gethostname(),
+            "counts": {k: 0 for k in LEVELS if k != "silent"},
+        }
+        self._bindings = dict(bindings or {})
+        self._prefix = self._make_prefix()
+        try:  # native pino line formatter (same semantics, ~10x faster)
+            from ..ops import format_line as _fl
+            self._format_line = _fl
+        except ImportError:  # pragma: no cover - native runtime missing
+            self._format_line = None
+        self.set_level(level)
+
+    def _make_prefix(self) -> str:
+        sh = self._shared
+        head = f'"pid":{sh["pid"]},"hostname":{json.dumps(sh["hostname"])},"name":{json.dumps(self.name)}'
+        for k, v in self._bindings.items():
+            head += f",{json.dumps(str(k))}:{json.dumps(_json_safe(v), ensure_ascii=False)}"
+        return head
+
+    # -- configuration -------------------------------------------------------
+    def set_level(self, level: str) -> None:
+        if level not in LEVELS:
+            raise ValueError(f"unknown log level {level!r}")
+        self.level = level
+        self._min = LEVELS[level]
+        self.is_trace = self._min <= 10
+        self.is_debug = self._min <= 20
+        self.is_info = self._min <= 30
+
+    @property
+    def stream(self) -> TextIO:
+        return self._shared["stream"]
+
+    @stream.setter
+    def stream(self, s: TextIO) -> None:
+        self._shared["stream"] = s
+
+    @property
+    def counts(self) -> Dict[str, int]:
+        """Lines emitted per level (all children share one counter table)."""
+        return self._shared["counts"]
+
+    def child(self, **bindings) -> "Logger":
+        b = dict(self._bindings)
+        b.update(bindings)
+        lg = Logger(self.name, self.level, bindings=b, _shared=self._shared)
+        return lg
+
+    # -- emit ------------------------------------------------------------------
+    def _emit(self, lvl: int, lname: str, args: tuple) -> None:
+        extra = None
+        if args and isinstance(args[0], dict):
+            extra = args[0]
+            args = args[1:]
+        elif args and isinstance(args[0], BaseException):
+            e = args[0]
+            extra = {"type": type(e).__name__, "stack": f"{type(e).__name__}: {e}"}
+            args = args[1:] if len(args) > 1 else (str(e),)
+        extra_s = None
+        if extra:
+            extra_s = "".join(f",{json.dumps(str(k))}:{json.dumps(_json_safe(v), ensure_ascii=False)}"
+                              for k, v in extra.items())
+        fl = self._format_line
+        if fl is not None:
+            line = fl(lvl, int(time.time() * 1000), self._prefix, extra_s, args)
+        else:
+            line = self._py_line(lvl, extra_s, args)
+        sh = self._shared
+        sh["counts"][lname] += 1
+        with sh["lock"]:
+            sh["stream"].write(line)
+            if lvl >= 50:
+                try:
+                    sh["stream"].flush()
+                except (OSError, ValueError):
+                    pass
+
+    def _py_line(self, lvl: int, extra_s, args: tuple) -> str:
+        """Pure-Python line formatter (reference implementation for the native one)."""
+        parts = [f'{{"level":{lvl},"time":{int(time.time() * 1000)},', self._prefix]
+        if extra_s:
+            parts.append(extra_s)
+        if args:
+            parts.append(',"msg":')
+            parts.append(json.dumps(quick_format(args), ensure_ascii=False))
+        parts.append(',"v":1}\n')
+        return "".join(parts)
+
+    def trace(self, *args) -> None:
+        if self._min <= 10:
+            self._emit(10, "trace", args)
+
+    def debug(self, *args) -> None:
+        if self._min <= 20:
+            self._emit(20, "debug", args)
+
+    def info(self, *args) -> None:
+        if self._min <= 30:
+            self._emit(30, "info", args)
+
+    def warn(self, *args) -> None:
+        if self._min <= 40:
+            self._emit(40, "warn", args)
+
+    warning = warn
+
+    def error(self, *args) -> None:
+        if self._min <= 50:
+            self._emit(50, "error", args)
+
+    def fatal(self, *args) -> None:
+        if self._min <= 60:
+            self._emit(60, "fatal", args)
+
+    def flush(self) -> None:
+        sh = self._shared
+        with sh["lock"]:
+            try:
+                sh["stream"].flush()
+            except (OSError, ValueError):
+                pass
+
+
+class NullStream:
+    """A write-only sink that discards (used by benches that still format every line)."""
+
+    def __init__(self):
+        self.bytes = 0
+        self.lines = 0
+
+    def write(self, s: str) -> int:
+        self.bytes += len(s)
+        self.lines += 1
+        return len(s)
+
+    def flush(self) -> None:
+        pass
+
+
+class MemoryStream:
+    """Collects lines in memory (tests)."""
+
+    def __init__(self):
+        self.lines = []
+
+    def write(self, s: str) -> int:
+        self.lines.extend(x for x in s.splitlines() if x)
+        return len(s)
+
+    def flush(self) -> None:
+        pass
+
+    def records(self):
+        return [json.loads(x) for x in self.lines]
+
+
+def get_logger(name: str = "index.js", level: str = "info", stream: Optional[TextIO] = None) -> Logger:
+    return Logger(name=name, level=level, stream=stream)
