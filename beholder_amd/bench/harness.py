@@ -1,0 +1,257 @@
+"""The five BASELINE.json measurement configs.
+
+====  ============  ==========================================================
+ #    name          what is measured
+====  ============  ==========================================================
+ 1    plumbing      100 synthetic events on **stdin** of ``python -m beholder_amd run``
+                    (real CLI process): all acked, counters exposed
+ 2    firehose_1k   1k events/s paced producer for N s: sustained ingest rate,
+                    receive→ack latency
+ 3    rate_10k      10k events/s: p50 / p99 ingest (receive→ack) latency
+ 4    backpressure  100k events/s offered into a small ring with the
+                    ``drop_newest`` policy (drop accounting) and with ``block``
+                    (producer stall time)
+ 5    soak          1M events unpaced: throughput, RSS growth, GC pause
+                    distribution
+====  ============  ==========================================================
+
+Every in-process config runs the real service path (native reader thread on
+an OS pipe → ring → handlers → store → metrics → sinks → acks) with sinks
+stubbed in-process and info logs written to /dev/null.
+
+Usage: ``python -m beholder_amd bench [all|<name>...] [--out FILE]``
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import gc
+import json
+import os
+import resource
+import subprocess
+import sys
+import tempfile
+import threading
+import time
+from typing import Dict, List, Optional
+
+from .generator import Workload, bench_config
+
+CONFIGS = ("plumbing", "firehose_1k", "rate_10k", "backpressure", "soak")
+
+
+def _rss_mb() -> float:
+    try:
+        with open("/proc/self/statm") as f:
+            return int(f.read().split()[1]) * os.sysconf("SC_PAGE_SIZE") / 2**20
+    except OSError:
+        return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024
+
+
+class GcPauses:
+    """Collects GC pause durations through ``gc.callbacks``."""
+
+    def __init__(self):
+        self.pauses_ns: List[int] = []
+        self._t0 = 0
+
+    def _cb(self, phase, info):
+        if phase == "start":
+            self._t0 = time.perf_counter_ns()
+        elif self._t0:
+            self.pauses_ns.append(time.perf_counter_ns() - self._t0)
+            self._t0 = 0
+
+    def __enter__(self):
+        gc.callbacks.append(self._cb)
+        return self
+
+    def __exit__(self, *exc):
+        gc.callbacks.remove(self._cb)
+
+    def summary(self) -> Dict[str, float]:
+        p = sorted(self.pauses_ns)
+        if not p:
+            return {"count": 0}
+
+        def pct(q):
+            return p[min(len(p) - 1, int(q / 100 * len(p)))] / 1e3
+
+        return {"count": len(p), "p50_us": pct(50), "p99_us": pct(99), "max_us": p[-1] / 1e3,
+                "total_ms": sum(p) / 1e6}
+
+
+class _Producer(threading.Thread):
+    """Writes pre-framed events into a pipe at ``rate`` events/s (0 = unpaced)."""
+
+    def __init__(self, wfd: int, events, rate: float):
+        super().__init__(daemon=True, name="producer")
+        from ..ops import frame
+        self.wfd = wfd
+        self.rate = rate
+        self.chunks = [frame(t, p) for t, p in events]
+        self.offered = len(self.chunks)
+        self.elapsed = 0.0
+
+    def run(self):
+        try:
+            t0 = time.perf_counter()
+            if self.rate <= 0:
+                data = b"".join(self.chunks)
+                mv = memoryview(data)
+                while mv:
+                    n = os.write(self.wfd, mv[:1 << 20])
+                    mv = mv[n:]
+            else:
+                sent = 0
+                n = len(self.chunks)
+                while sent < n:
+                    due = min(n, int((time.perf_counter() - t0) * self.rate) + 1)
+                    if due > sent:
+                        os.write(self.wfd, b"".join(self.chunks[sent:due]))
+                        sent = due
+                    else:
+                        time.sleep(0.0002)
+            self.elapsed = time.perf_counter() - t0
+        except OSError:
+            pass
+        finally:
+            os.close(self.wfd)
+
+
+async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_events: int = 0,
+                      n_media: int = 10000, media=None, log_level: str = "info") -> dict:
+    from ..config import Config
+    from ..service import Service
+    from ..sinks import RecordingHttpClient
+    from ..store import MemoryStore
+    from ..transport.ingest import FdSource
+    from ..utils.log import Logger
+
+    rfd, wfd = os.pipe()
+    cfgd = bench_config()
+    cfgd["service"]["log"]["level"] = log_level
+    sink = open(os.devnull, "w", buffering=1 << 16)
+    src = FdSource(fd=rfd, policy=policy, capacity_events=capacity_events)
+    svc = Service(Config.from_dict(cfgd), source=src, store=MemoryStore(media), http=RecordingHttpClient(keep=8),
+                  logger=Logger(stream=sink, level=log_level), serve_metrics=False)
+    await svc.init()
+    prod = _Producer(wfd, events, rate)
+    t0 = time.perf_counter()
+    prod.start()
+    stats = await svc.run()
+    elapsed = time.perf_counter() - t0
+    prod.join()
+    await svc.close()
+    sink.close()
+    s = stats["source"]
+    return {
+        "offered": prod.offered, "accepted": s["pushed"], "dropped": s["dropped_total"],
+        "acked": s["acked"], "abandoned": s["abandoned"], "errors": sum(stats.get("handler_errors", {}).values()),
+        "elapsed_s": elapsed, "producer_s": prod.elapsed,
+        "ingest_rate_eps": s["acked"] / elapsed if elapsed else 0.0,
+        "offered_rate_eps": prod.offered / prod.elapsed if prod.elapsed else 0.0,
+        "ingest_latency_us": {k: v / 1e3 for k, v in stats["ingest_latency_ns"].items() if k.startswith("p")},
+        "handle_latency_us": {k: v / 1e3 for k, v in stats["handle_latency_ns"].items() if k.startswith("p")},
+        "producer_blocked_ms": s["blocked_ns"] / 1e6, "ring_high_water": s["high_water_events"],
+    }
+
+
+def run_config(name: str, *, duration_s: Optional[float] = None, events: Optional[int] = None,
+               seed: int = 0) -> dict:
+    w = Workload(n_media=10000, seed=seed)
+    if name == "plumbing":
+        return _plumbing(w)
+    if name == "firehose_1k":
+        d = duration_s or 5.0
+        res = asyncio.run(_run_inproc(w.events(int(1000 * d)), 1000, media=w.media))
+    elif name == "rate_10k":
+        d = duration_s or 5.0
+        res = asyncio.run(_run_inproc(w.events(int(10000 * d)), 10000, media=w.media))
+    elif name == "backpressure":
+        d = duration_s or 3.0
+        evs = w.events(int(100000 * d))
+        res = {"drop_newest": asyncio.run(_run_inproc(evs, 100000, policy="drop_newest", capacity_events=4096,
+                                                      media=w.media)),
+               "block": asyncio.run(_run_inproc(evs, 100000, policy="block", capacity_events=4096,
+                                                media=w.media)),
+               # overload: the same events offered unpaced (pipe speed) into the small ring
+               "overload_drop_newest": asyncio.run(_run_inproc(evs, 0, policy="drop_newest",
+                                                               capacity_events=4096, media=w.media))}
+        dn = res["drop_newest"]
+        res.update({"offered": dn["offered"], "accepted": dn["accepted"], "dropped": dn["dropped"]})
+    elif name == "soak":
+        n = events or 1_000_000
+        gc.collect()
+        rss0 = _rss_mb()
+        evs = w.events(n)
+        with GcPauses() as g:
+            res = asyncio.run(_run_inproc(evs, 0, media=w.media))
+        del evs
+        gc.collect()
+        res["rss_start_mb"] = rss0
+        res["rss_end_mb"] = _rss_mb()
+        res["rss_growth_mb"] = res["rss_end_mb"] - rss0
+        res["rss_peak_mb"] = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024
+        res["gc_pauses"] = g.summary()
+    else:
+        raise ValueError(f"unknown config {name!r} (one of {', '.join(CONFIGS)})")
+    res["config"] = name
+    return res
+
+
+def _plumbing(w: Workload) -> dict:
+    """Config 1: 100 events on the stdin of the real CLI process."""
+    import yaml
+
+    from .fakes import FakeHttpServer
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    with tempfile.TemporaryDirectory() as td, FakeHttpServer() as fake:
+        cfgd = bench_config()
+        cfgd["service"]["endpoints"] = {"trello": fake.url, "telegram": fake.url}
+        cfgd["instance"]["emby"]["host"] = fake.url
+        cfgd["service"]["http"] = {"timeout_s": 5.0}
+        cfgd["service"]["transport"] = {"kind": "stdin"}
+        cp = os.path.join(td, "events.yaml")
+        with open(cp, "w") as f:
+            yaml.safe_dump(cfgd, f)
+        mp = os.path.join(td, "media.json")
+        with open(mp, "w") as f:
+            json.dump([m._asdict() for m in w.media], f)
+        data = w.framed(100)
+        env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+        t0 = time.perf_counter()
+        p = subprocess.run([sys.executable, "-m", "beholder_amd", "run", "--config", cp, "--media-fixture", mp,
+                            "--stats"], input=data, capture_output=True, timeout=300, env=env, cwd=root)
+        elapsed = time.perf_counter() - t0
+    if p.returncode != 0:
+        raise RuntimeError(f"plumbing run failed ({p.returncode}): {p.stderr.decode()[-2000:]}")
+    stats = json.loads(p.stderr.decode().strip().splitlines()[-1])
+    lines = [json.loads(x) for x in p.stdout.decode().splitlines() if x.startswith("{")]
+    s = stats["source"]
+    return {"config": "plumbing", "offered": 100, "acked": s["acked"], "abandoned": s["abandoned"],
+            "errors": sum(stats.get("handler_errors", {}).values()), "process_wall_s": elapsed,
+            "http_requests": len(fake.requests),
+            "log_lines": len(lines), "warn_lines": sum(1 for x in lines if x["level"] == 40),
+            "received": stats["received"]}
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    ap = argparse.ArgumentParser(prog="beholder bench", description="BASELINE.json measurement configs")
+    ap.add_argument("configs", nargs="*", default=["all"])
+    ap.add_argument("--duration", type=float, default=None)
+    ap.add_argument("--events", type=int, default=None)
+    ap.add_argument("--out", default=None, help="write results JSON here")
+    a = ap.parse_args(argv)
+    names = CONFIGS if (not a.configs or a.configs == ["all"]) else a.configs
+    results = {}
+    for n in names:
+        t0 = time.perf_counter()
+        results[n] = run_config(n, duration_s=a.duration, events=a.events if n == "soak" else None)
+        results[n]["wall_s"] = time.perf_counter() - t0
+        print(json.dumps(results[n], default=str), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(results, f, indent=2, default=str)
+    return 0

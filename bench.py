@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Headline benchmark: metric-events/sec ingested + p50 handle latency (BASELINE.json ``metric``).
+
+One *step* = ``--events-per-step`` synthetic telemetry events (90% progress /
+10% status, protobuf-encoded, framed) pushed through the **whole** service
+path of each rank:
+
+    producer thread -> OS pipe -> native reader thread (framing, ring)
+      -> event loop: Delivery batches -> eager handler dispatch
+      -> native protobuf decode -> handler logic (index.js:62-155)
+      -> media store (in-memory, 10k rows) -> Prometheus counters
+      -> Trello/Telegram/Emby request construction (URL + query encoding)
+         into an in-process HTTP recorder (no network)
+      -> pino JSON log line per reference log call (info level, written to /dev/null)
+      -> ack (latency recorded natively)
+
+A step ends when every event of the step has been settled. ``W`` warm-up
+steps run untimed, then exactly ``K`` steps are timed between barriers.
+
+Multi-GPU contract: launched with ``torch.distributed.run`` each rank is an
+independent consumer process (competing consumers over its own stream:
+per-rank work is fixed, so scaling is *weak*); ranks synchronise with gloo
+barriers, the elapsed time is the MAX over ranks and ``value`` is the
+whole-job events/s. The service has no device work (the reference has none),
+so nothing is launched on the GPU.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import gc
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+BASELINE_METRIC = "metric_events_ingested_per_sec"
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1, help="number of ranks (one process per GPU slot)")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--events-per-step", type=int, default=65536)
+    ap.add_argument("--media", type=int, default=10000)
+    ap.add_argument("--log-level", default="info")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--ordering", default="none", choices=["none", "per_media"])
+    return ap.parse_args(argv)
+
+
+class _Dist:
+    """gloo process group when launched under torch.distributed.run, no-op otherwise."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if self.dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def gather(self, obj):
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+
+
+async def run_rank(a, dist: _Dist) -> dict:
+    from beholder_amd.bench.generator import Workload, bench_config
+    from beholder_amd.config import Config
+    from beholder_amd.service import Service
+    from beholder_amd.sinks import RecordingHttpClient
+    from beholder_amd.store import MemoryStore
+    from beholder_amd.transport.ingest import FdSource
+    from beholder_amd.utils.log import Logger
+
+    E = a.events_per_step
+    total_steps = a.warmup + a.steps
+    w = Workload(n_media=a.media, seed=a.seed + 7919 * dist.rank)
+    step_bytes = [w.framed(E) for _ in range(total_steps)]
+
+    rfd, wfd = os.pipe()
+    cfg_d = bench_config()
+    cfg_d["service"]["log"]["level"] = a.log_level
+    cfg_d["service"]["ordering"] = a.ordering
+    cfg = Config.from_dict(cfg_d)
+    log_sink = open(os.devnull, "w", buffering=1 << 16)
+    http = RecordingHttpClient(keep=16)
+    svc = Service(cfg, source=FdSource(fd=rfd, batch=512), store=MemoryStore(w.media), http=http,
+                  logger=Logger(stream=log_sink, level=a.log_level), serve_metrics=False)
+    await svc.init()
+    gc.collect()
+    gc.freeze()  # long-lived startup objects out of the young generations (service does the same)
+
+    run_task = asyncio.ensure_future(svc.run())
+    settler = svc.source.settler
+
+    def write_step(i: int) -> threading.Thread:
+        def pump(data=step_bytes[i]):
+            mv = memoryview(data)
+            while mv:
+                n = os.write(wfd, mv[:1 << 20])
+                mv = mv[n:]
+        t = threading.Thread(target=pump, daemon=True)
+        t.start()
+        return t
+
+    def settled() -> int:
+        st = settler.stats()
+        return st["acked"] + st["nacked"] + st["rejected"] + st["abandoned"]
+
+    async def wait_settled(target: int):
+        while settled() < target or svc._inflight:
+            await asyncio.sleep(0.0002)
+
+    t0 = t1 = 0.0
+    for i in range(total_steps):
+        if i == a.warmup:
+            settler.reset_latency()
+            dist.barrier()
+            t0 = time.perf_counter()
+        th = write_step(i)
+        await wait_settled((i + 1) * E)
+        th.join()
+    t1 = time.perf_counter()
+    os.close(wfd)
+    await run_task
+    await svc.close()
+    log_sink.close()
+    elapsed = t1 - t0
+    st = svc.stats()
+    return {
+        "elapsed": elapsed,
+        "events": E * a.steps,
+        "handle_hist": settler.handle_latency.to_bytes(),
+        "ingest_hist": settler.ingest_latency.to_bytes(),
+        "http_calls": http.count,
+        "errors": sum(st.get("handler_errors", {}).values()),
+        "abandoned": st["source"]["abandoned"],
+    }
+
+
+def main(argv=None) -> int:
+    a = parse(argv)
+    dist = _Dist()
+    n = dist.world if dist.world > 1 else a.gpus
+    if dist.world == 1 and a.gpus > 1:
+        print(f"bench.py: --gpus {a.gpus} requires torch.distributed.run; running 1 rank", file=sys.stderr)
+        n = 1
+    res = asyncio.run(run_rank(a, dist))
+    dist.barrier()
+    elapsed = dist.max(res["elapsed"])
+    parts = dist.gather({k: res[k] for k in ("handle_hist", "ingest_hist", "http_calls", "errors", "abandoned")})
+    if dist.rank == 0:
+        from beholder_amd.ops import Histogram
+        hh, ih = Histogram(), Histogram()
+        for p in parts:
+            hh.merge_bytes(p["handle_hist"])
+            ih.merge_bytes(p["ingest_hist"])
+        total_events = res["events"] * n
+        value = total_events / elapsed
+        out = {
+            "metric": BASELINE_METRIC,
+            "value": round(value, 1),
+            "unit": "events/s",
+            "n_gpus": n,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1000, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "protobuf-events (no tensor compute)",
+            "data": "synthetic telemetry (90% progress / 10% status), 10k-media in-memory store, "
+                    "Trello/Telegram/Emby stubbed in-process, info logs to /dev/null",
+            "config": {
+                "model": "beholder telemetry consumer (status+progress handlers, index.js:62-155)",
+                "global_batch": a.events_per_step * n,
+                "seq_len": None,
+                "parallelism": f"dp{n} (competing consumers, one process per rank)",
+            },
+            "p50_handle_latency_us": round(hh.percentile(50) / 1e3, 3),
+            "p99_handle_latency_us": round(hh.percentile(99) / 1e3, 3),
+            "p50_ingest_latency_us": round(ih.percentile(50) / 1e3, 3),
+            "events_per_rank_per_sec": round(value / n, 1),
+            "http_requests": sum(p["http_calls"] for p in parts),
+            "handler_errors": sum(p["errors"] for p in parts),
+        }
+        print(json.dumps(out), flush=True)
+    dist.close()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,56 @@
+"""Box-tier tests (``-m gpu``): run on the MI355X box at round end.
+
+Beholder has no device kernels (the reference service has none), so these do
+not touch the accelerator. They exercise the *native* runtime on the target
+machine image at full scale: the in-tree extension must be the one loaded,
+the BASELINE.json configs must meet their targets, and the multi-rank bench
+launcher must work.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.gpu
+
+
+def test_native_runtime_is_in_tree_and_loaded():
+    from beholder_amd import ops
+    path = os.path.realpath(ops.native.__file__)
+    assert path.startswith(os.path.realpath(os.path.join(ROOT, "beholder_amd", "ops"))), path
+    assert ops.native.ABI_VERSION == 1
+    # every hot-path entry point is native
+    for name in ("MessageCodec", "Ingest", "Delivery", "Settler", "Histogram", "format_line", "encode_query"):
+        assert hasattr(ops.native, name), name
+
+
+def test_bench_single_rank_full_path():
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "1"],
+                         capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = [x for x in out.stdout.splitlines() if x.startswith("{")][-1]
+    r = json.loads(line)
+    assert r["metric"] == "metric_events_ingested_per_sec" and r["n_gpus"] == 1
+    assert r["handler_errors"] == 0
+    assert r["value"] > 20000, r
+
+
+def test_baseline_configs_plumbing_and_backpressure():
+    """BASELINE configs 1 (100 events on stdin) and 4 (100k ev/s, backpressure + drop accounting)."""
+    from beholder_amd.bench import harness
+    res = harness.run_config("plumbing")
+    assert res["acked"] == 100 and res["errors"] == 0
+    res = harness.run_config("backpressure", duration_s=2.0)
+    assert res["offered"] == res["accepted"] + res["dropped"], res
+
+
+def test_soak_1m_events_rss_and_gc():
+    """BASELINE config 5: 1M events, report RSS and GC pauses; RSS must stay bounded."""
+    from beholder_amd.bench import harness
+    res = harness.run_config("soak", events=1_000_000)
+    assert res["acked"] == 1_000_000
+    assert res["rss_growth_mb"] < 512, res
