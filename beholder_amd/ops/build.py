@@ -57,7 +57,8 @@ def compile_flags(debug: bool = False, sanitize: str = "") -> list:
 def build(force: bool = False, debug: bool = False, sanitize: str = "", cxx: str = "", verbose: bool = False) -> str:
     cxx = cxx or os.environ.get("CXX") or "g++"
     flags = compile_flags(debug, sanitize)
-    digest = source_hash(flags + [cxx])
+    # hash path-independent flags so a snapshot copied elsewhere (GPU box) reuses the .so
+    digest = source_hash([f for f in flags if not f.startswith("-I")] + [cxx, sysconfig.get_config_var("SOABI") or ""])
     if not force and os.path.exists(TARGET) and os.path.exists(STAMP):
         with open(STAMP) as f:
             if f.read().strip() == digest:

@@ -1,0 +1,163 @@
+"""Native protobuf codec vs the upb (google.protobuf) oracle.
+
+The reference decodes with protobufjs via triton-core (index.js:63,129); our
+hot path uses the native MessageCodec. It must agree with upb on every valid
+input (same field values) and reject the same malformed inputs.
+"""
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from beholder_amd.models import proto
+from beholder_amd.models.proto import DecodeError
+from beholder_amd.models.protoparse import parse_proto
+from beholder_amd.ops import MessageCodec, codec_for, field_table
+
+STATUS = proto.load("api.TelemetryStatus")
+PROGRESS = proto.load("api.TelemetryProgress")
+MEDIA = proto.load("api.Media")
+
+
+def as_tuple(ptype, msg):
+    return tuple(getattr(msg, f.name) for f in ptype.descriptor.fields)
+
+
+def test_schema_field_numbers_pinned():
+    """The documented wire contract (models/proto/api.proto)."""
+    assert field_table(STATUS.descriptor) == [(1, "mediaId", 1), (2, "status", 10)]
+    assert field_table(PROGRESS.descriptor) == [(1, "mediaId", 1), (2, "status", 10), (3, "progress", 3),
+                                                (4, "host", 1)]
+    assert [f.name for f in MEDIA.descriptor.fields][:4] == ["id", "name", "creator", "creatorId"]
+
+
+def test_enum_semantics():
+    """index.js:74,94,134,142: enumToString / stringToEnum; CreatorType.TRELLO == 1."""
+    assert proto.enum_to_string(STATUS, "TelemetryStatusEntry", 4) == "DEPLOYED"
+    assert proto.enumToString(PROGRESS, "TelemetryStatusEntry", 0) == "QUEUED"
+    assert proto.enum_to_string(STATUS, "TelemetryStatusEntry", 99) is None  # undefined (Q6)
+    assert proto.string_to_enum(STATUS, "TelemetryStatusEntry", "DEPLOYED") == 4
+    assert proto.stringToEnum(MEDIA, "CreatorType", "TRELLO") == 1
+    assert proto.string_to_enum(MEDIA, "CreatorType", "NOPE") is None
+
+
+def test_proto3_defaults():
+    for codec_dec in (codec_for(PROGRESS).decode, lambda b: proto.decode(PROGRESS, b)):
+        m = codec_dec(b"")
+        assert (m.mediaId, m.status, m.progress, m.host) == ("", 0, 0, "")
+
+
+def test_roundtrip_matches_upb():
+    c = codec_for(PROGRESS)
+    for vals in [("m", 4, 45, "h"), ("", 0, 0, ""), ("é✓", 5, -7, "w" * 300), ("x" * 70000, 2, 2**31 - 1, "")]:
+        native_bytes = c.encode(vals)
+        upb_bytes = proto.encode(PROGRESS, dict(zip(("mediaId", "status", "progress", "host"), vals)))
+        assert native_bytes == upb_bytes
+        assert tuple(c.decode(upb_bytes)) == vals
+
+
+def test_unknown_fields_and_wire_type_mismatch_skipped():
+    c = codec_for(STATUS)
+    # field 9 varint (unknown), field 2 as LEN (wrong wire type -> unknown), then real status
+    data = b"\x48\x05" + b"\x12\x01x" + b"\x0a\x02ab" + b"\x10\x03"
+    assert tuple(c.decode(data)) == ("ab", 3)
+    assert as_tuple(STATUS, proto.decode(STATUS, data)) == ("ab", 3)
+
+
+def test_last_value_wins():
+    c = codec_for(STATUS)
+    data = b"\x0a\x01a\x10\x01\x0a\x01b\x10\x02"
+    assert tuple(c.decode(data)) == ("b", 2) == as_tuple(STATUS, proto.decode(STATUS, data))
+
+
+def test_group_skipping():
+    c = codec_for(STATUS)
+    # unknown group field 5 containing a varint field 1, then mediaId
+    data = b"\x2b\x08\x01\x2c" + b"\x0a\x01z"
+    assert tuple(c.decode(data)) == ("z", 0)
+    assert as_tuple(STATUS, proto.decode(STATUS, data)) == ("z", 0)
+
+
+@pytest.mark.parametrize("bad", [
+    b"\x0a\x05ab",            # truncated string
+    b"\x0a",                  # truncated length
+    b"\x10",                  # truncated varint
+    b"\x10\xff\xff\xff\xff\xff\xff\xff\xff\xff\xff\x01",  # > 10-byte varint
+    b"\x00\x01",              # field number 0
+    b"\x0e\x01",              # wire type 6
+    b"\x0c",                  # stray end-group
+    b"\x0a\x02\xff\xfe",      # invalid UTF-8 in a proto3 string
+    b"\x2b\x08\x01",          # unterminated group
+])
+def test_malformed_rejected_by_both(bad):
+    with pytest.raises(DecodeError):
+        codec_for(STATUS).decode(bad)
+    with pytest.raises(DecodeError):
+        proto.decode(STATUS, bad)
+
+
+def test_negative_int32_is_10_byte_varint():
+    c = codec_for(PROGRESS)
+    b = c.encode({"progress": -1})
+    assert b == b"\x18" + b"\xff" * 9 + b"\x01"
+    assert c.decode(b).progress == -1 == proto.decode(PROGRESS, b).progress
+
+
+def test_int32_truncation_of_large_varint():
+    """A 64-bit varint on an int32 field keeps the low 32 bits (upb semantics)."""
+    data = b"\x18\x80\x80\x80\x80\x10"  # 2**32 -> low 32 bits = 0
+    assert codec_for(PROGRESS).decode(data).progress == proto.decode(PROGRESS, data).progress == 0
+
+
+def test_all_scalar_kinds_against_upb():
+    src = """
+    syntax = "proto3";
+    package t;
+    enum E { A = 0; B = 1; }
+    message All {
+      string s = 1; bytes b = 2; int32 i32 = 3; int64 i64 = 4; uint32 u32 = 5; uint64 u64 = 6;
+      sint32 s32 = 7; sint64 s64 = 8; bool bo = 9; E e = 10; float f = 11; double d = 12;
+      fixed32 f32 = 13; fixed64 f64 = 14; sfixed32 sf32 = 15; sfixed64 sf64 = 16;
+    }
+    """
+    from google.protobuf import descriptor_pool, message_factory
+    pool = descriptor_pool.DescriptorPool()
+    pool.Add(parse_proto(src, "t.proto"))
+    desc = pool.FindMessageTypeByName("t.All")
+    cls = message_factory.GetMessageClass(desc)
+    codec = MessageCodec("t.All", field_table(desc))
+    vals = dict(s="héllo", b=b"\x00\xff", i32=-5, i64=-(2**40), u32=2**32 - 1, u64=2**64 - 1, s32=-77,
+                s64=-(2**50), bo=True, e=1, f=1.5, d=-2.25, f32=7, f64=2**63, sf32=-8, sf64=-(2**62))
+    upb = cls(**vals).SerializeToString()
+    dec = codec.decode(upb)
+    for k, v in vals.items():
+        assert getattr(dec, k) == v, k
+    assert codec.encode(vals) == upb
+
+
+# ------------------------------------------------------------- fuzzing ----
+int32s = st.integers(min_value=-(2**31), max_value=2**31 - 1)
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.text(max_size=64), int32s, int32s, st.text(max_size=16))
+def test_fuzz_roundtrip(mid, status, prog, host):
+    c = codec_for(PROGRESS)
+    b = proto.encode(PROGRESS, {"mediaId": mid, "status": status, "progress": prog, "host": host})
+    assert tuple(c.decode(b)) == (mid, status, prog, host)
+    assert c.encode((mid, status, prog, host)) == b
+
+
+@settings(max_examples=1500, deadline=None)
+@given(st.binary(max_size=48))
+def test_fuzz_arbitrary_bytes_agree_with_upb(data):
+    """On random bytes the native codec accepts exactly what upb accepts, with equal values."""
+    c = codec_for(PROGRESS)
+    try:
+        want = as_tuple(PROGRESS, proto.decode(PROGRESS, data))
+    except DecodeError:
+        want = None
+    try:
+        got = tuple(c.decode(data))
+    except DecodeError:
+        got = None
+    assert got == want

@@ -1,0 +1,76 @@
+"""Native JS-semantics text helpers vs their Python reference implementations."""
+import json
+import math
+import random
+import struct
+
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from beholder_amd import ops
+from beholder_amd.sinks.http import encode_query, py_encode_query
+from beholder_amd.utils import log
+
+
+def test_js_number_known_values():
+    cases = {45.0: "45", 45.5: "45.5", 1e21: "1e+21", 1e-7: "1e-7", 1e-6: "0.000001", 100.0: "100",
+             -2.5: "-2.5", 0.1 + 0.2: "0.30000000000000004", 1e20: "100000000000000000000",
+             123456789.125: "123456789.125", 5e-324: "5e-324", math.inf: "Infinity", -math.inf: "-Infinity",
+             float("nan"): "NaN", 0.0: "0", -0.0: "0"}
+    for x, want in cases.items():
+        assert log.js_number(x) == want, x
+        assert ops.js_number(x) == want, x
+
+
+def test_js_number_random_doubles_agree():
+    rng = random.Random(7)
+    for _ in range(20000):
+        x = struct.unpack("d", struct.pack("Q", rng.getrandbits(64)))[0]
+        if x != x:
+            continue
+        assert ops.js_number(x) == log.js_number(x), x
+
+
+def test_js_str():
+    for v, want in [(None, "undefined"), (True, "true"), (3, "3"), (2.0, "2"), ("s", "s"), ([1, None, 2], "1,,2"),
+                    ({"a": 1}, "[object Object]")]:
+        assert log.js_str(v) == want
+        assert ops.js_str(v) == want
+
+
+ARGS = st.lists(st.one_of(st.text(max_size=12), st.integers(-10**6, 10**6), st.floats(allow_nan=False),
+                          st.none(), st.booleans()), max_size=5)
+FMT = st.text(alphabet="ab %sdifjoO", max_size=16)
+
+
+@settings(max_examples=500, deadline=None)
+@given(FMT, ARGS)
+def test_quick_format_native_matches_python(fmt, args):
+    assert ops.quick_format(fmt, *args) == log.quick_format((fmt, *args))
+
+
+def test_quick_format_q11_fix_appends_extra_args():
+    """pino v5 would drop these (index.js:51); we append them."""
+    assert ops.quick_format("creating comment on", "C1", "with text:", "X") == "creating comment on C1 with text: X"
+    assert ops.quick_format("a %s %% %d", "x", 4.0, "tail") == "a x % 4 tail"
+
+
+def test_format_line_is_valid_pino_json():
+    line = ops.format_line(40, 1700000000000, '"pid":1,"hostname":"h","name":"index.js"', None,
+                           ('he said "hi"\n\x01 é', 3))
+    rec = json.loads(line)
+    assert list(rec) == ["level", "time", "pid", "hostname", "name", "msg", "v"]
+    assert rec["msg"] == 'he said "hi"\n\x01 é 3' and rec["level"] == 40 and rec["v"] == 1
+    assert line.endswith("}\n")
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.dictionaries(st.text(max_size=6), st.one_of(st.text(max_size=20), st.integers(), st.booleans(),
+                                                       st.none(), st.floats(allow_nan=False)), max_size=5))
+def test_encode_query_native_matches_python(d):
+    assert encode_query(d) == py_encode_query(d)
+
+
+def test_encode_query_matches_encodeURIComponent():
+    assert encode_query({"text": "A: **45%** (_h_) é/?&="}) == \
+        "text=A%3A%20**45%25**%20(_h_)%20%C3%A9%2F%3F%26%3D"
