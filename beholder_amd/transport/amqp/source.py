@@ -1,0 +1,275 @@
+"""AMQP consumer source and publisher — ``triton-core/amqp`` parity.
+
+Reference usage (index.js:43-44,62,127)::
+
+    const amqp = new AMQP(dyn('rabbitmq'), 100, 2, prom)
+    await amqp.connect()
+    amqp.listen('v1.telemetry.status', async rmsg => { ... rmsg.ack() })
+
+:class:`AmqpSource` does the same: one channel with ``basic.qos(prefetch)``
+(100), a durable queue per topic (named after the topic, so publishers use
+the default exchange with ``routing_key = topic``), manual acks.
+
+Reliability (amqp-connection-manager parity):
+
+* startup: ``retries + 1`` connection attempts with exponential backoff, then
+  the error propagates (fail fast — the Q10 fix);
+* after startup: on connection / channel loss, reconnect forever with
+  exponential backoff (0.25 s … 30 s), re-declare, re-qos, re-consume;
+* deliveries from a dead channel are *stale*: settling them is a no-op
+  (the broker already requeued them, ``redelivered`` set on the next delivery).
+"""
+from __future__ import annotations
+
+import asyncio
+import time
+from typing import Dict, List, Optional, Sequence
+
+from ...ops import Delivery, Settler
+from ...topics import TOPIC_IDS, topic_id
+from ..base import Source
+from .connection import Channel, Connection
+from .wire import AmqpError
+
+
+class AmqpSource(Source):
+    kind = "amqp"
+
+    def __init__(self, url: str, prefetch: int = 100, retries: int = 2, *, logger=None,
+                 durable: bool = True, heartbeat: Optional[int] = None, backoff_initial: float = 0.25,
+                 backoff_max: float = 30.0, connect_timeout: float = 10.0):
+        self.url = url
+        self._prefetch = int(prefetch)
+        self.retries = int(retries)
+        self.log = logger
+        self.durable = durable
+        self.heartbeat = heartbeat
+        self.backoff_initial = backoff_initial
+        self.backoff_max = backoff_max
+        self.connect_timeout = connect_timeout
+        self._settler = Settler(on_settle=self._on_settle)
+        self._topics: List[str] = []
+        self._tag_topic: Dict[str, int] = {}
+        self._conn: Optional[Connection] = None
+        self._ch: Optional[Channel] = None
+        self._pending: List = []
+        self._event: Optional[asyncio.Event] = None
+        self._closing = False
+        self._reconnect_task: Optional[asyncio.Task] = None
+        self.reconnects = 0
+        self.delivered = 0
+        self.stale_settles = 0
+        self.last_error: Optional[str] = None
+        self.connected_since = 0.0
+
+    # ------------------------------------------------------------ Source ---
+    @property
+    def prefetch(self) -> int:
+        return self._prefetch
+
+    @property
+    def settler(self) -> Settler:
+        return self._settler
+
+    async def start(self, topics: Sequence[str]) -> None:
+        for t in topics:
+            topic_id(t)
+        self._topics = list(topics)
+        self._event = asyncio.Event()
+        delay = self.backoff_initial
+        for attempt in range(self.retries + 1):
+            try:
+                await self._connect()
+                return
+            except (OSError, AmqpError, asyncio.TimeoutError) as e:
+                self.last_error = f"{type(e).__name__}: {e}"
+                if attempt == self.retries:
+                    raise
+                self._warn(f"amqp connect failed ({self.last_error}), retrying in {delay:.2f}s")
+                await asyncio.sleep(delay)
+                delay = min(delay * 2, self.backoff_max)
+
+    async def _connect(self) -> None:
+        conn = Connection(self.url, heartbeat=self.heartbeat, connect_timeout=self.connect_timeout,
+                          logger=self.log, on_lost=self._on_lost)
+        await conn.open()
+        try:
+            ch = await conn.channel()
+            await ch.basic_qos(self._prefetch)
+            tags = {}
+            for t in self._topics:
+                await ch.queue_declare(t, durable=self.durable)
+                tag = await ch.basic_consume(t, self._on_message)
+                tags[tag] = TOPIC_IDS[t]
+        except BaseException:
+            await conn.close()
+            raise
+        ch.on_close = self._on_channel_close
+        self._conn, self._ch, self._tag_topic = conn, ch, tags
+        self.connected_since = time.time()
+
+    def _on_message(self, ch: Channel, method, props, body: bytes) -> None:
+        tid = self._tag_topic.get(method.consumer_tag, 0)
+        d = Delivery(body, tid, method.delivery_tag, self._settler, None, method.redelivered, ch)
+        self.delivered += 1
+        self._pending.append(d)
+        if len(self._pending) == 1:
+            self._event.set()
+
+    def _on_settle(self, d, kind: str, requeue: bool) -> None:
+        ch: Channel = d.extra
+        if ch is None or not ch.is_open or ch is not self._ch:
+            self.stale_settles += 1  # channel gone: broker already requeued it
+            return
+        if kind == "ack":
+            ch.basic_ack(d.tag)
+        elif kind == "nack":
+            ch.basic_nack(d.tag, requeue=requeue)
+        else:
+            ch.basic_reject(d.tag, requeue=requeue)
+
+    async def batches(self):
+        while True:
+            if self._pending:
+                batch, self._pending = self._pending, []
+                yield batch
+                continue
+            if self._closing:
+                return
+            self._event.clear()
+            await self._event.wait()
+
+    async def close(self) -> None:
+        if self._closing:
+            return
+        self._closing = True
+        if self._reconnect_task is not None:
+            self._reconnect_task.cancel()
+        ch, conn = self._ch, self._conn
+        self._ch = None
+        if ch is not None and ch.is_open:
+            for tag in list(self._tag_topic):
+                try:
+                    await asyncio.wait_for(ch.basic_cancel(tag), 5)
+                except (AmqpError, asyncio.TimeoutError, ConnectionError):
+                    break
+            await ch.close()
+        if conn is not None:
+            await conn.close()
+        if self._event is not None:
+            self._event.set()
+
+    def ready(self) -> bool:
+        return self._ch is not None and self._ch.is_open and not self._closing
+
+    def stats(self) -> dict:
+        s = self._settler.stats()
+        c = self._conn
+        s.update({"connected": self.ready(), "reconnects": self.reconnects, "delivered": self.delivered,
+                  "stale_settles": self.stale_settles, "last_error": self.last_error,
+                  "bytes_in": c.bytes_in if c else 0, "bytes_out": c.bytes_out if c else 0,
+                  "buffered": len(self._pending)})
+        return s
+
+    # --------------------------------------------------------- recovery ---
+    def _on_channel_close(self, ch: Channel, err) -> None:
+        if err is not None and not self._closing:
+            self.last_error = str(err)
+            self._schedule_reconnect()
+
+    def _on_lost(self, err) -> None:
+        if self._closing:
+            return
+        self.last_error = str(err) if err else "connection lost"
+        self._schedule_reconnect()
+
+    def _schedule_reconnect(self) -> None:
+        if self._closing or (self._reconnect_task is not None and not self._reconnect_task.done()):
+            return
+        self._ch = None
+        self._reconnect_task = asyncio.get_running_loop().create_task(self._reconnect_loop())
+
+    async def _reconnect_loop(self) -> None:
+        old = self._conn
+        if old is not None:
+            try:
+                await old.close()
+            except Exception:  # noqa: BLE001
+                pass
+        delay = self.backoff_initial
+        while not self._closing:
+            self._warn(f"amqp connection lost ({self.last_error}); reconnecting in {delay:.2f}s")
+            await asyncio.sleep(delay)
+            try:
+                await self._connect()
+                self.reconnects += 1
+                self._info(f"amqp reconnected (attempt {self.reconnects})")
+                return
+            except (OSError, AmqpError, asyncio.TimeoutError) as e:
+                self.last_error = f"{type(e).__name__}: {e}"
+                delay = min(delay * 2, self.backoff_max)
+
+    def _warn(self, msg: str) -> None:
+        if self.log is not None:
+            self.log.warn(msg)
+
+    def _info(self, msg: str) -> None:
+        if self.log is not None:
+            self.log.info(msg)
+
+
+class AmqpPublisher:
+    """``amqp.publish(topic, buffer)`` — what the other triton services call (default exchange)."""
+
+    def __init__(self, url: str, confirm: bool = True, durable: bool = True, persistent: bool = True):
+        self.url = url
+        self.confirm = confirm
+        self.durable = durable
+        self.persistent = persistent
+        self._conn: Optional[Connection] = None
+        self._ch: Optional[Channel] = None
+        self._declared: set = set()
+
+    async def connect(self) -> "AmqpPublisher":
+        self._conn = await Connection(self.url).open()
+        self._ch = await self._conn.channel()
+        if self.confirm:
+            await self._ch.confirm_select()
+        return self
+
+    async def publish(self, topic: str, body: bytes, wait: bool = False):
+        if topic not in self._declared:
+            await self._ch.queue_declare(topic, durable=self.durable)
+            self._declared.add(topic)
+        props = {"delivery_mode": 2} if self.persistent else None
+        return await self._ch.basic_publish(body, routing_key=topic, properties=props, wait_confirm=wait)
+
+    async def flush(self) -> None:
+        if self._ch is not None:
+            await self._ch.wait_confirms()
+
+    async def close(self) -> None:
+        if self._ch is not None:
+            await self.flush()
+            await self._ch.close()
+        if self._conn is not None:
+            await self._conn.close()
+
+
+async def publish_frames(url: str, data: bytes) -> int:
+    """Publish every frame of a framed stream to its topic queue (CLI ``publish``)."""
+    from ...topics import topic_name
+    from ..framing import iter_frames
+    pub = await AmqpPublisher(url).connect()
+    n = 0
+    try:
+        for tid, payload in iter_frames(data):
+            name = topic_name(tid)
+            if name is None:
+                raise ValueError(f"frame with unknown topic id {tid}")
+            await pub.publish(name, payload)
+            n += 1
+        await pub.flush()
+    finally:
+        await pub.close()
+    return n
