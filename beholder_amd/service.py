@@ -251,6 +251,9 @@ class Service:
         nroutes = len(routes)
         received = self.received
         dispatch = self.serializer.submit if self.serializer is not None else self._dispatch_now
+        inflight = self._inflight
+        prefetch = self.prefetch
+        sleep = asyncio.sleep
         try:
             async for batch in self.source.batches():
                 for d in batch:
@@ -260,11 +263,12 @@ class Service:
                         continue
                     received[tid] += 1
                     dispatch(d)
-                if len(self._inflight) >= self.prefetch:
-                    await self._wait_slots()
+                    if inflight and len(inflight) >= prefetch:
+                        await self._wait_slots()  # at most `prefetch` handlers suspended (index.js:43)
                 log.flush()
                 if self._stop:
                     break
+                await sleep(0)  # keep timers / the metrics endpoint responsive under sustained load
         finally:
             self._running = False
             await self._drain()

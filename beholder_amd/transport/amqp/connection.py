@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import asyncio
 import itertools
+import os
 import time
 from typing import Any, Callable, Dict, Optional
 
@@ -117,11 +118,21 @@ class Channel:
 
     async def basic_consume(self, queue: str, on_message: Callable, consumer_tag: str = "",
                             no_ack: bool = False, exclusive: bool = False, arguments=None) -> str:
-        """``on_message(channel, deliver_method, properties, body)`` runs in the reader task."""
-        m = await self._rpc("basic.consume", ("basic.consume_ok",), queue=queue, consumer_tag=consumer_tag,
+        """``on_message(channel, deliver_method, properties, body)`` runs in the reader task.
+
+        The consumer tag is chosen client-side and the callback registered
+        *before* ``basic.consume`` is sent: the broker may deliver in the same
+        TCP segment as ``consume_ok``.
+        """
+        tag = consumer_tag or f"beholder.ctag-{self.conn._ctag_prefix}-{next(self.conn._ctags)}"
+        self._consumers[tag] = on_message
+        try:
+            await self._rpc("basic.consume", ("basic.consume_ok",), queue=queue, consumer_tag=tag,
                             no_local=False, no_ack=no_ack, exclusive=exclusive, arguments=arguments or {})
-        self._consumers[m.consumer_tag] = on_message
-        return m.consumer_tag
+        except BaseException:
+            self._consumers.pop(tag, None)
+            raise
+        return tag
 
     async def basic_cancel(self, consumer_tag: str) -> None:
         if self.is_open:
@@ -282,6 +293,8 @@ class Connection:
         self._parser = wire.FrameParser(0)
         self._channels: Dict[int, Channel] = {}
         self._ids = itertools.count(1)
+        self._ctags = itertools.count(1)
+        self._ctag_prefix = f"{os.getpid()}-{id(self):x}"
         self._rx_task: Optional[asyncio.Task] = None
         self._hb_task: Optional[asyncio.Task] = None
         self._wbuf = bytearray()

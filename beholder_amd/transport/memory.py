@@ -83,8 +83,8 @@ class MemoryBroker:
                        "unacked": sum(len(c._unacked_by_q.get(name, ())) for c in q.consumers)}
                 for name, q in self._queues.items()}
 
-    def consumer(self, prefetch: int = 100) -> "MemoryConsumer":
-        return MemoryConsumer(self, prefetch)
+    def consumer(self, prefetch: int = 100, batch: int = 512) -> "MemoryConsumer":
+        return MemoryConsumer(self, prefetch, batch)
 
     def _kick(self, q: _Queue) -> None:
         for c in q.consumers:

@@ -1,0 +1,39 @@
+"""bench.py driver contract: one JSON line, required keys, multi-rank launch via torch.distributed.run."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config"}
+
+
+def _last_json(stdout: str) -> dict:
+    lines = [x for x in stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+def test_bench_single_rank_contract():
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--events-per-step", "4096"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = _last_json(r.stdout)
+    assert REQUIRED <= set(out) and out["n_gpus"] == 1 and out["steps"] == 2 and out["warmup"] == 1
+    assert {"model", "global_batch", "seq_len", "parallelism"} <= set(out["config"])
+    assert out["value"] > 0 and out["handler_errors"] == 0
+    assert out["value"] == pytest.approx(4096 * 2 / (out["ms_per_step"] * 2 / 1000), rel=0.01)
+
+
+def test_bench_two_ranks_gloo():
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29561", "bench.py", "--gpus", "2",
+                        "--steps", "2", "--warmup", "1", "--events-per-step", "4096"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _last_json(r.stdout)
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 8192
+    assert out["config"]["parallelism"].startswith("dp2")

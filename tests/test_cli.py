@@ -1,0 +1,55 @@
+"""CLI: `gen | run --source stdin` (the BASELINE plumbing config) and tools."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ENV = dict(os.environ, PYTHONPATH=ROOT)
+
+
+def cli(*args, **kw):
+    return subprocess.run([sys.executable, "-m", "beholder_amd", *args], capture_output=True, env=ENV, cwd=ROOT,
+                          timeout=120, **kw)
+
+
+def test_gen_decode_roundtrip(tmp_path):
+    out = tmp_path / "ev.bin"
+    r = cli("gen", "--events", "25", "--media", "5", "--out", str(out), "--media-out", str(tmp_path / "m.json"))
+    assert r.returncode == 0
+    d = cli("decode", str(out))
+    recs = [json.loads(x) for x in d.stdout.decode().splitlines()]
+    assert len(recs) == 25 and all("json" in x for x in recs)
+    assert len(json.load(open(tmp_path / "m.json"))) == 5
+
+
+def test_run_stdin_plumbing(tmp_path):
+    cfg = tmp_path / "events.yaml"
+    cfg.write_text("keys: {trello: {key: k, token: t}}\ninstance: {flow_ids: {queued: L}}\n"
+                   "service: {metrics: {enabled: false}, endpoints: {trello: 'http://127.0.0.1:9',"
+                   " telegram: 'http://127.0.0.1:9'}, http: {timeout_s: 0.2}}\n")
+    ev = cli("gen", "--events", "30", "--media", "4", "--media-out", str(tmp_path / "m.json"),
+             "--progress-fraction", "1.0")
+    r = cli("run", "--config", str(cfg), "--source", "stdin", "--media-fixture", str(tmp_path / "m.json"),
+            "--stats", input=ev.stdout)
+    assert r.returncode == 0, r.stderr
+    stats = json.loads(r.stderr.decode().strip().splitlines()[-1])
+    assert stats["source"]["acked"] == 30  # progress handler always acks (Q7), even with Trello down
+    lines = [json.loads(x) for x in r.stdout.decode().splitlines()]
+    assert lines[0]["msg"] == "initialized" and lines[0]["name"] == "index.js"
+
+
+def test_run_config_error_exit_code(tmp_path):
+    cfg = tmp_path / "bad.yaml"
+    cfg.write_text("instance: {flow_ids: {}}\n")
+    r = cli("run", "--config", str(cfg), "--source", "stdin", input=b"")
+    assert r.returncode == 2 and b"config error" in r.stderr
+
+
+def test_run_amqp_unreachable_fails_fast(tmp_path):
+    """Q10 fix: a startup failure exits non-zero instead of an unhandled rejection."""
+    cfg = tmp_path / "events.yaml"
+    cfg.write_text("keys: {trello: {key: k, token: t}}\ninstance: {flow_ids: {}}\n"
+                   "service: {metrics: {enabled: false}, retries: 0}\n")
+    r = cli("run", "--config", str(cfg), "--source", "amqp", "--url", "amqp://guest:guest@127.0.0.1:1/")
+    assert r.returncode == 1 and b"fatal" in r.stderr

@@ -1,0 +1,81 @@
+"""Config loading (index.js:24-25,60,70,97-115)."""
+import os
+
+import pytest
+
+from beholder_amd.config import Config, ConfigError, env_overrides, js_truthy_env
+from beholder_amd.dynamics import dyn
+
+MIN = "keys:\n  trello: {key: k, token: t}\ninstance:\n  flow_ids: {queued: L1}\n"
+
+
+def test_load_by_name_from_config_path(tmp_path):
+    (tmp_path / "events.yaml").write_text(MIN)
+    c = Config.load("events", env={"CONFIG_PATH": str(tmp_path)})
+    assert c.keys.trello.key == "k" and c.flow_ids == {"queued": "L1"}
+    assert c.source.endswith("events.yaml")
+    assert c.service.prefetch == 100  # index.js:43 default
+
+
+def test_explicit_path_and_json(tmp_path):
+    p = tmp_path / "x.json"
+    p.write_text('{"keys": {"trello": {"key": "a", "token": "b"}}, "instance": {"flow_ids": {}}}')
+    assert Config.load(path=str(p), env={}).keys.trello.token == "b"
+
+
+def test_env_overrides_typed(tmp_path):
+    (tmp_path / "events.yaml").write_text(MIN)
+    env = {"CONFIG_PATH": str(tmp_path), "BEHOLDER_CFG__instance__telegram__enabled": "true",
+           "BEHOLDER_CFG__service__prefetch": "7", "BEHOLDER_CFG__keys__trello__token": "override"}
+    c = Config.load(env=env)
+    assert c.instance.telegram.enabled is True and c.service.prefetch == 7 and c.keys.trello.token == "override"
+    assert env_overrides({"BEHOLDER_CFG__a__b": "x"}) == {"a": {"b": "x"}}
+
+
+def test_missing_config_and_bad_yaml(tmp_path):
+    with pytest.raises(ConfigError):
+        Config.load(env={"CONFIG_PATH": str(tmp_path)}, cwd=str(tmp_path))
+    (tmp_path / "events.yaml").write_text("keys: [unclosed")
+    with pytest.raises(ConfigError):
+        Config.load(env={"CONFIG_PATH": str(tmp_path)})
+    with pytest.raises(ConfigError):
+        Config.load(path=str(tmp_path / "nope.yaml"), env={})
+
+
+def test_required_keys_like_reference():
+    with pytest.raises(ConfigError, match="trello"):
+        Config.from_dict({"instance": {"flow_ids": {}}})
+    # keys.trello present with missing leaf values is fine (JS reads undefined)
+    Config.from_dict({"keys": {"trello": {}}, "instance": {"flow_ids": {}}})
+
+
+def test_js_style_missing_values():
+    c = Config.from_dict({"keys": {"trello": {"key": "k"}}, "instance": {"flow_ids": {}}})
+    assert c.instance.telegram is None and c.keys.emby is None
+    assert bool(c.instance) is True
+
+
+def test_validation_of_service_knobs():
+    base = {"keys": {"trello": {}}, "instance": {"flow_ids": {}}}
+    for bad in ({"prefetch": 0}, {"ordering": "weird"}, {"on_status_error": "explode"}):
+        with pytest.raises(ConfigError):
+            Config.from_dict({**base, "service": bad})
+
+
+def test_no_trello_flag():
+    base = {"keys": {"trello": {}}, "instance": {"flow_ids": {}}}
+    assert Config.from_dict(base, env={"NO_TRELLO": "1"}).no_trello
+    assert not js_truthy_env({"NO_TRELLO": ""}, "NO_TRELLO")
+
+
+def test_dynamics():
+    assert dyn("rabbitmq", env={"RABBITMQ_ENDPOINT": "amqp://x"}) == "amqp://x"
+    assert dyn("rabbitmq", env={}).startswith("amqp://")
+    with pytest.raises(KeyError):
+        dyn("unknown-service", env={})
+
+
+def test_repo_example_config_loads():
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    c = Config.load(path=os.path.join(root, "config", "events.example.yaml"), env={})
+    assert "deployed" in c.flow_ids

@@ -1,0 +1,84 @@
+"""Prometheus exposition parity with prom-client 11 (index.js:27-40,57,136-138)."""
+import pytest
+
+from beholder_amd.metrics import Registry, parse_exposition
+from beholder_amd.metrics.registry import Histogram
+
+
+def reference_registry():
+    r = Registry("beholder")
+    p = r.counter("beholder_progress_updates_total", "Total number of messages processed in this processes lifetime",
+                  ["status"])
+    t = r.counter("beholder_trello_comments", "Total trello comments crreated in this processes lifetime")
+    return r, p, t
+
+
+def test_exact_initial_exposition():
+    r, _, _ = reference_registry()
+    assert r.render() == (
+        "# HELP beholder_progress_updates_total Total number of messages processed in this processes lifetime\n"
+        "# TYPE beholder_progress_updates_total counter\n"
+        "\n"
+        "# HELP beholder_trello_comments Total trello comments crreated in this processes lifetime\n"
+        "# TYPE beholder_trello_comments counter\n"
+        "beholder_trello_comments 0\n")
+
+
+def test_counter_api_variants():
+    r, p, t = reference_registry()
+    p.inc({"status": "deployed"})
+    p.inc({"status": "deployed"}, 2)
+    p.labels(status="queued").inc()
+    p.child_for("queued").inc(0.5)
+    t.inc()
+    t.inc(3)
+    m = parse_exposition(r.render())
+    assert m['beholder_progress_updates_total{status="deployed"}'] == 3
+    assert m['beholder_progress_updates_total{status="queued"}'] == 1.5
+    assert m["beholder_trello_comments"] == 4
+
+
+def test_counter_rejects_decrease_and_bad_labels():
+    r, p, t = reference_registry()
+    with pytest.raises(ValueError):
+        t.inc(-1)
+    with pytest.raises(ValueError):
+        p.inc({"nope": "x"})
+    with pytest.raises(ValueError):
+        t.inc({"status": "x"})
+    with pytest.raises(ValueError):
+        r.counter("beholder_trello_comments", "dup")
+
+
+def test_label_escaping():
+    r = Registry()
+    c = r.counter("x_total", "help with \\ and\nnewline", ["l"])
+    c.inc({"l": 'a"b\\c\nd'})
+    out = r.render()
+    assert '# HELP x_total help with \\\\ and\\nnewline' in out
+    assert 'x_total{l="a\\"b\\\\c\\nd"} 1' in out
+
+
+def test_histogram_and_gauge():
+    r = Registry()
+    h = r.histogram("lat_seconds", "latency", buckets=[0.1, 1])
+    for v in (0.05, 0.5, 5):
+        h.observe(v)
+    g = r.gauge("depth", "queue depth", ["q"])
+    g.set({"q": "a"}, 3)
+    g.inc({"q": "a"})
+    m = parse_exposition(r.render())
+    assert m['lat_seconds_bucket{le="0.1"}'] == 1 and m['lat_seconds_bucket{le="1"}'] == 2
+    assert m['lat_seconds_bucket{le="+Inf"}'] == 3 and m["lat_seconds_count"] == 3
+    assert m["lat_seconds_sum"] == pytest.approx(5.55)
+    assert m['depth{q="a"}'] == 4
+    with pytest.raises(ValueError):
+        Histogram("h", "x", ["le"])
+
+
+def test_invalid_names():
+    r = Registry()
+    with pytest.raises(ValueError):
+        r.counter("bad-name", "x")
+    with pytest.raises(ValueError):
+        r.counter("ok", "x", ["__reserved"])
