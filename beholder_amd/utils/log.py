@@ -137,7 +137,7 @@ def quick_format(args: tuple) -> str:
                     rep = js_str(a)
                 elif c in "di":
                     try:
-                        num = float(a) if not isinstance(a, (int, float)) else a
+                        num = float(a) if not isinstance(a, (int, float)) or isinstance(a, bool) else a
                         rep = js_number(math.floor(num) if c == "i" and num == num and abs(num) != math.inf else num)
                     except (TypeError, ValueError):
                         rep = "NaN"
