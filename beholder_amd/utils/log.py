@@ -138,7 +138,9 @@ def quick_format(args: tuple) -> str:
                 elif c in "di":
                     try:
                         num = float(a) if not isinstance(a, (int, float)) or isinstance(a, bool) else a
-                        rep = js_number(math.floor(num) if c == "i" and num == num and abs(num) != math.inf else num)
+                        if c == "i" and num == num and abs(num) != math.inf:
+                            num = float(math.floor(num)) if isinstance(num, float) else num
+                        rep = js_number(num)
                     except (TypeError, ValueError):
                         rep = "NaN"
                 elif c == "f":
