@@ -33,6 +33,16 @@ def _load_fixture(path: str):
 
 
 def cmd_run(a: argparse.Namespace) -> int:
+    if a.workers and a.workers > 1:
+        if a.source in ("stdin", "file"):
+            print("beholder: --workers needs a shared broker transport (amqp)", file=sys.stderr)
+            return 2
+        from .parallel.workers import Supervisor, strip_workers_arg
+        argv = strip_workers_arg(sys.argv[1:] if a.argv is None else a.argv)
+        if a.metrics_port is not None:
+            argv = strip_opt(argv, "--metrics-port")
+        return Supervisor(argv, a.workers, metrics_port=a.metrics_port,
+                          log=lambda m: print(f"beholder supervisor: {m}", file=sys.stderr)).run()
     env = dict(os.environ)
     try:
         cfg = Config.load("events", path=a.config, env=env)
@@ -187,6 +197,15 @@ def cmd_bench(a: argparse.Namespace) -> int:
     return harness.main(a.rest)
 
 
+def cmd_broker(a: argparse.Namespace) -> int:
+    from .transport.amqp.broker import serve_forever
+    try:
+        asyncio.run(serve_forever(a.host, a.port))
+    except KeyboardInterrupt:
+        pass
+    return 0
+
+
 def cmd_publish(a: argparse.Namespace) -> int:
     from .transport.amqp import publish_frames
     data = open(a.input, "rb").read() if a.input else sys.stdin.buffer.read()
@@ -213,6 +232,8 @@ def build_parser() -> argparse.ArgumentParser:
     r.add_argument("--ordering", choices=["none", "per_media"])
     r.add_argument("--media-fixture", help="JSON list of media rows to preload (memory store)")
     r.add_argument("--stats", action="store_true", help="print final stats JSON to stderr")
+    r.add_argument("--workers", type=int, default=0,
+                   help="N competing-consumer processes on the same queues (amqp); metrics port + worker id")
     r.set_defaults(fn=cmd_run)
 
     g = sub.add_parser("gen", help="generate synthetic framed telemetry")
@@ -241,6 +262,11 @@ def build_parser() -> argparse.ArgumentParser:
     b.add_argument("rest", nargs=argparse.REMAINDER)
     b.set_defaults(fn=cmd_bench)
 
+    k = sub.add_parser("broker", help="run the built-in AMQP test broker (local development)")
+    k.add_argument("--host", default="127.0.0.1")
+    k.add_argument("--port", type=int, default=5672)
+    k.set_defaults(fn=cmd_broker)
+
     p = sub.add_parser("publish", help="publish a framed stream to AMQP")
     p.add_argument("--url", required=True)
     p.add_argument("input", nargs="?")
@@ -248,6 +274,22 @@ def build_parser() -> argparse.ArgumentParser:
     return ap
 
 
+def strip_opt(argv: List[str], name: str) -> List[str]:
+    out, skip = [], False
+    for x in argv:
+        if skip:
+            skip = False
+            continue
+        if x == name:
+            skip = True
+            continue
+        if x.startswith(name + "="):
+            continue
+        out.append(x)
+    return out
+
+
 def main(argv: Optional[List[str]] = None) -> int:
     a = build_parser().parse_args(argv)
+    a.argv = argv
     return a.fn(a)

@@ -18,16 +18,71 @@
 // rec_bytes == 0 is a wrap marker: the consumer jumps to offset 0.
 #pragma once
 
-#include <atomic>
-#include <chrono>
-#include <condition_variable>
+#include <pthread.h>
+#include <time.h>
+
 #include <cstdint>
 #include <cstring>
-#include <mutex>
-#include <time.h>
 #include <vector>
 
 namespace beholder {
+
+// Thin pthread wrappers. The condition variable waits on CLOCK_MONOTONIC via
+// pthread_cond_timedwait: std::condition_variable::wait_for in libstdc++ 11
+// uses pthread_cond_clockwait, which ThreadSanitizer (GCC 11) does not
+// intercept, producing false race reports in tests/native/.
+class Mutex {
+ public:
+  Mutex() { pthread_mutex_init(&m_, nullptr); }
+  ~Mutex() { pthread_mutex_destroy(&m_); }
+  Mutex(const Mutex&) = delete;
+  Mutex& operator=(const Mutex&) = delete;
+  void lock() { pthread_mutex_lock(&m_); }
+  void unlock() { pthread_mutex_unlock(&m_); }
+  pthread_mutex_t* native() { return &m_; }
+
+ private:
+  pthread_mutex_t m_;
+};
+
+class Lock {
+ public:
+  explicit Lock(Mutex& m) : m_(m) { m_.lock(); }
+  ~Lock() { m_.unlock(); }
+  Lock(const Lock&) = delete;
+  Lock& operator=(const Lock&) = delete;
+  Mutex& mutex() { return m_; }
+
+ private:
+  Mutex& m_;
+};
+
+class CondVar {
+ public:
+  CondVar() {
+    pthread_condattr_t a;
+    pthread_condattr_init(&a);
+    pthread_condattr_setclock(&a, CLOCK_MONOTONIC);
+    pthread_cond_init(&c_, &a);
+    pthread_condattr_destroy(&a);
+  }
+  ~CondVar() { pthread_cond_destroy(&c_); }
+  CondVar(const CondVar&) = delete;
+  CondVar& operator=(const CondVar&) = delete;
+  void wait(Lock& l) { pthread_cond_wait(&c_, l.mutex().native()); }
+  // Waits until the absolute CLOCK_MONOTONIC deadline; returns false on timeout.
+  bool wait_until(Lock& l, int64_t deadline_ns) {
+    struct timespec ts;
+    ts.tv_sec = time_t(deadline_ns / 1000000000LL);
+    ts.tv_nsec = long(deadline_ns % 1000000000LL);
+    return pthread_cond_timedwait(&c_, l.mutex().native(), &ts) == 0;
+  }
+  void notify_one() { pthread_cond_signal(&c_); }
+  void notify_all() { pthread_cond_broadcast(&c_); }
+
+ private:
+  pthread_cond_t c_;
+};
 
 inline int64_t mono_ns() {
   struct timespec ts;
@@ -81,7 +136,7 @@ class ByteRing {
   // -1 if the ring was closed while waiting.
   int push(uint8_t topic, uint8_t flags, const uint8_t* payload, uint32_t len, int64_t recv_ns) {
     size_t need = record_size(len);
-    std::unique_lock<std::mutex> lk(mu_);
+    Lock lk(mu_);
     if (need > cap_ / 2) {
       count_drop_locked(topic);
       return 0;
@@ -141,14 +196,17 @@ class ByteRing {
   // timeout passes. Returns the number of bytes readable [rpos, wpos).
   // timeout_ns < 0 waits forever.
   size_t wait_readable(int64_t timeout_ns) {
-    std::unique_lock<std::mutex> lk(mu_);
+    Lock lk(mu_);
     if (wpos_ == rpos_ && !closed_ && !eof_ && timeout_ns != 0) {
       consumer_waiting_ = true;
-      auto pred = [&] { return wpos_ != rpos_ || closed_ || eof_; };
+      auto ready = [&] { return wpos_ != rpos_ || closed_ || eof_; };
       if (timeout_ns < 0) {
-        cv_data_.wait(lk, pred);
+        while (!ready()) cv_data_.wait(lk);
       } else {
-        cv_data_.wait_for(lk, std::chrono::nanoseconds(timeout_ns), pred);
+        const int64_t deadline = mono_ns() + timeout_ns;
+        while (!ready()) {
+          if (!cv_data_.wait_until(lk, deadline) && mono_ns() >= deadline) break;
+        }
       }
       consumer_waiting_ = false;
     }
@@ -158,11 +216,11 @@ class ByteRing {
   // Snapshot of the readable region (call after wait_readable). The consumer
   // walks records with next_record() and then releases with consume().
   uint64_t read_begin() {
-    std::lock_guard<std::mutex> g(mu_);
+    Lock g(mu_);
     return rpos_;
   }
   uint64_t read_end() {
-    std::lock_guard<std::mutex> g(mu_);
+    Lock g(mu_);
     return wpos_;
   }
 
@@ -194,7 +252,7 @@ class ByteRing {
   }
 
   void consume(uint64_t new_rpos, uint64_t nrecords) {
-    std::lock_guard<std::mutex> g(mu_);
+    Lock g(mu_);
     rpos_ = new_rpos;
     rcount_ += nrecords;
     stats_.popped += nrecords;
@@ -203,38 +261,38 @@ class ByteRing {
 
   // ---- lifecycle ----------------------------------------------------------
   void set_eof() {
-    std::lock_guard<std::mutex> g(mu_);
+    Lock g(mu_);
     eof_ = true;
     cv_data_.notify_all();
   }
   void close() {
-    std::lock_guard<std::mutex> g(mu_);
+    Lock g(mu_);
     closed_ = true;
     cv_data_.notify_all();
     cv_space_.notify_all();
   }
   bool eof() {
-    std::lock_guard<std::mutex> g(mu_);
+    Lock g(mu_);
     return eof_;
   }
   bool closed() {
-    std::lock_guard<std::mutex> g(mu_);
+    Lock g(mu_);
     return closed_;
   }
   bool drained() {
-    std::lock_guard<std::mutex> g(mu_);
+    Lock g(mu_);
     return (eof_ || closed_) && wpos_ == rpos_;
   }
   size_t depth_events() {
-    std::lock_guard<std::mutex> g(mu_);
+    Lock g(mu_);
     return size_t(wcount_ - rcount_);
   }
   RingStats stats() {
-    std::lock_guard<std::mutex> g(mu_);
+    Lock g(mu_);
     return stats_;
   }
   void count_external_drop(uint8_t topic) {
-    std::lock_guard<std::mutex> g(mu_);
+    Lock g(mu_);
     count_drop_locked(topic);
   }
 
@@ -249,8 +307,8 @@ class ByteRing {
   const int policy_;
   std::vector<uint8_t> buf_;
 
-  std::mutex mu_;
-  std::condition_variable cv_data_, cv_space_;
+  Mutex mu_;
+  CondVar cv_data_, cv_space_;
   uint64_t wpos_ = 0, rpos_ = 0;      // logical byte positions (monotonic)
   uint64_t wcount_ = 0, rcount_ = 0;  // records pushed / consumed
   uint64_t seq_ = 0;

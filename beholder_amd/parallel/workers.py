@@ -1,0 +1,127 @@
+"""Multi-process competing consumers: ``beholder run --workers N``.
+
+The reference scales horizontally only by running more replicas that consume
+the same RabbitMQ queues (SURVEY.md §2.3 "horizontal scaling"). One Python
+process is bound by one core, so on a many-core host the idiomatic scale-out
+is N worker processes on the same queues (the broker round-robins between
+them, each with its own prefetch window). This module is the supervisor:
+
+* spawns N children running the same ``run`` command with
+  ``BEHOLDER_WORKER_ID=i`` and the metrics port offset by ``i``;
+* restarts a crashed worker with exponential backoff (a crash loop is capped
+  at ``max_restarts`` per worker);
+* forwards SIGTERM/SIGINT and waits for graceful shutdown, then SIGKILLs
+  stragglers after ``grace_s``.
+
+Only broker transports can be shared (AMQP); a stdin/file stream has a single
+reader.
+"""
+from __future__ import annotations
+
+import os
+import signal
+import subprocess
+import sys
+import time
+from typing import Dict, List, Optional
+
+
+class Supervisor:
+    def __init__(self, argv: List[str], workers: int, *, metrics_port: Optional[int] = None,
+                 max_restarts: int = 10, grace_s: float = 15.0, env: Optional[Dict[str, str]] = None,
+                 log=print):
+        if workers < 1:
+            raise ValueError("workers must be >= 1")
+        self.argv = list(argv)
+        self.n = workers
+        self.metrics_port = metrics_port
+        self.max_restarts = max_restarts
+        self.grace_s = grace_s
+        self.env = dict(os.environ if env is None else env)
+        self.log = log
+        self.procs: Dict[int, subprocess.Popen] = {}
+        self.restarts = [0] * workers
+        self.next_start = [0.0] * workers
+        self._stop = False
+
+    def _cmd(self, i: int) -> List[str]:
+        cmd = [sys.executable, "-m", "beholder_amd", *self.argv]
+        if self.metrics_port is not None and self.metrics_port >= 0:
+            cmd += ["--metrics-port", str(self.metrics_port + i)]
+        return cmd
+
+    def _spawn(self, i: int) -> None:
+        env = dict(self.env, BEHOLDER_WORKER_ID=str(i), BEHOLDER_WORKERS=str(self.n))
+        self.procs[i] = subprocess.Popen(self._cmd(i), env=env)
+        self.log(f"worker {i} started pid={self.procs[i].pid}")
+
+    def stop(self, *_a) -> None:
+        self._stop = True
+
+    def run(self) -> int:
+        signal.signal(signal.SIGTERM, self.stop)
+        signal.signal(signal.SIGINT, self.stop)
+        for i in range(self.n):
+            self._spawn(i)
+        failed = False
+        done = set()  # workers that exited cleanly (finite source)
+        while not self._stop and len(done) < self.n:
+            time.sleep(0.1)
+            for i in range(self.n):
+                if i in done:
+                    continue
+                p = self.procs.get(i)
+                if p is None:
+                    if time.monotonic() >= self.next_start[i]:
+                        self._spawn(i)
+                    continue
+                rc = p.poll()
+                if rc is None:
+                    continue
+                del self.procs[i]
+                if rc == 0:
+                    self.log(f"worker {i} exited cleanly")
+                    done.add(i)
+                    continue
+                self.restarts[i] += 1
+                if self.restarts[i] > self.max_restarts:
+                    self.log(f"worker {i} crashed {self.restarts[i]} times (rc={rc}); giving up")
+                    failed = True
+                    self._stop = True
+                    break
+                delay = min(30.0, 0.5 * 2 ** (self.restarts[i] - 1))
+                self.log(f"worker {i} exited rc={rc}; restart {self.restarts[i]} in {delay:.1f}s")
+                self.next_start[i] = time.monotonic() + delay
+        return self._shutdown(failed)
+
+    def _shutdown(self, failed: bool) -> int:
+        for p in self.procs.values():
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        deadline = time.monotonic() + self.grace_s
+        rc = 1 if failed else 0
+        for i, p in list(self.procs.items()):
+            try:
+                r = p.wait(max(0.0, deadline - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                r = p.wait()
+                self.log(f"worker {i} killed after grace period")
+            if r not in (0, -signal.SIGTERM):
+                rc = rc or 1
+        return rc
+
+
+def strip_workers_arg(argv: List[str]) -> List[str]:
+    out, skip = [], False
+    for a in argv:
+        if skip:
+            skip = False
+            continue
+        if a == "--workers":
+            skip = True
+            continue
+        if a.startswith("--workers="):
+            continue
+        out.append(a)
+    return out

@@ -581,3 +581,58 @@ async def serve_forever(host: str = "127.0.0.1", port: int = 5672) -> None:
         await asyncio.Event().wait()
     finally:
         await b.stop()
+
+
+class BrokerThread:
+    """Runs an :class:`AmqpBroker` on its own event loop in a background thread."""
+
+    def __init__(self, **kw):
+        import threading
+        self._kw = kw
+        self.broker: Optional[AmqpBroker] = None
+        self._loop: Optional[asyncio.AbstractEventLoop] = None
+        self._ready = threading.Event()
+        self._thread = threading.Thread(target=self._run, daemon=True, name="amqp-broker")
+
+    def _run(self) -> None:
+        self._loop = asyncio.new_event_loop()
+        asyncio.set_event_loop(self._loop)
+        self.broker = self._loop.run_until_complete(AmqpBroker(**self._kw).start())
+        self._ready.set()
+        self._loop.run_forever()
+        self._loop.run_until_complete(self.broker.stop())
+        self._loop.close()
+
+    def start(self) -> "BrokerThread":
+        self._thread.start()
+        self._ready.wait(10)
+        return self
+
+    def call(self, fn, *args):
+        """Run ``fn(broker, *args)`` on the broker loop and return its result."""
+        import concurrent.futures
+        fut: concurrent.futures.Future = concurrent.futures.Future()
+
+        def go():
+            try:
+                fut.set_result(fn(self.broker, *args))
+            except BaseException as e:  # noqa: BLE001
+                fut.set_exception(e)
+
+        self._loop.call_soon_threadsafe(go)
+        return fut.result(10)
+
+    @property
+    def url(self) -> str:
+        return self.broker.url
+
+    def stop(self) -> None:
+        if self._loop is not None:
+            self._loop.call_soon_threadsafe(self._loop.stop)
+        self._thread.join(10)
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()
