@@ -89,8 +89,10 @@ class Node:
         return self[key]
 
     def __getitem__(self, key: str) -> Any:
-        v = self._d.get(key) if isinstance(self._d, Mapping) else None
-        if isinstance(v, Mapping):
+        d = self._d
+        v = d.get(key) if (type(d) is dict or isinstance(d, Mapping)) else None
+        if type(v) is dict or (v is not None and not isinstance(v, (str, int, float, bool, list))
+                               and isinstance(v, Mapping)):
             return Node(v, f"{self._path}.{key}" if self._path else key)
         return v
 

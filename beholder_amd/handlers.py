@@ -34,14 +34,19 @@ from typing import Any, Callable, Mapping, Optional
 from .models import proto
 from .sinks.trello import COMMENT_FALLBACK
 from .sinks.telegram import deployed_text
-from .utils.log import js_str
+from .ops import js_str
 
 TRELLO_CREATOR = 1  # index.js:79 compares `media.creator === 1`
 
 
 def js_truthy(v: Any) -> bool:
     """JavaScript truthiness (``""``, ``0``, ``NaN``, ``None``/undefined, ``False`` are falsy)."""
-    if v is None or v is False:
+    t = type(v)
+    if t is str:
+        return v != ""
+    if t is bool:
+        return v
+    if v is None:
         return False
     if isinstance(v, (int, float)) and not isinstance(v, bool):
         return v == v and v != 0
@@ -65,6 +70,8 @@ class JsTypeError(TypeError):
 
 def _get(obj: Any, key: str) -> Any:
     """``obj[key]`` with JS semantics on config nodes / dicts (``undefined`` → None)."""
+    if type(obj) is dict:
+        return obj.get(key)
     if obj is None:
         raise JsTypeError(f"Cannot read property '{key}' of undefined")
     if isinstance(obj, Mapping):
@@ -109,6 +116,41 @@ class TelemetryHandlers:
         self.trello_creator = proto.string_to_enum(self.media_proto, "CreatorType", "TRELLO")
         self.lists = config.flow_ids  # index.js:60
 
+    def _hooks_plan(self):
+        """The DEPLOYED-hook config reads of index.js:97-115, evaluated once.
+
+        The config is immutable, so the JS expressions are evaluated at first
+        use and cached. Dereferences that throw in the reference (e.g.
+        ``config.keys.telegram.token`` with no ``keys.telegram``) are kept
+        lazy: the cached plan re-raises at the same point of the handler.
+        """
+        plan = self.__dict__.get("_plan")
+        if plan is None:
+            cfg = self.config
+            inst = cfg.instance
+            tg = _get(inst, "telegram")
+            tg_on = js_truthy(tg) and js_truthy(_get(tg, "enabled"))
+            chat_id = _get(tg, "channel") if tg_on else None
+            try:
+                token_val = _get(_get(cfg.keys, "telegram"), "token")
+                token_exc = None
+            except JsTypeError as e:
+                token_val, token_exc = None, e
+
+            def tg_token(v=token_val, e=token_exc):
+                if e is not None:
+                    raise JsTypeError(str(e))
+                return v
+
+            keys_emby = _get(cfg.keys, "emby")
+            inst_emby = _get(inst, "emby")
+            emby_on = (js_truthy(keys_emby) and js_truthy(_get(keys_emby, "token")) and js_truthy(inst_emby)
+                       and js_truthy(_get(inst_emby, "enabled")))
+            plan = (tg_on, chat_id, tg_token, emby_on, _get(inst_emby, "host") if emby_on else None,
+                    _get(keys_emby, "token") if emby_on else None)
+            self._plan = plan
+        return plan
+
     # ------------------------------------------------------------------ C8 ---
     async def comment(self, card_id: Any, text: Optional[str]) -> None:
         """index.js:50-58."""
@@ -152,22 +194,14 @@ class TelemetryHandlers:
 
         try:  # index.js:92-122 (Q3, Q4)
             if media.status == self.deployed:
-                cfg = self.config
-                inst = cfg.instance
-                tg = _get(inst, "telegram")
-                if js_truthy(tg) and js_truthy(_get(tg, "enabled")):
+                tg_on, chat_id, tg_token, emby_on, emby_host, emby_key = self._hooks_plan()
+                if tg_on:
                     log.info(f"informing telegram that media '{js_str(media_id)}' is available")
-                    chat_id = _get(tg, "channel")
-                    token = _get(_get(cfg.keys, "telegram"), "token")
                     await self.telegram.send_message(chat_id, deployed_text(media.name, media.metadataId),
-                                                     "markdown", token=token)
-                keys_emby = _get(cfg.keys, "emby")
-                inst_emby = _get(inst, "emby")
-                if (js_truthy(keys_emby) and js_truthy(_get(keys_emby, "token")) and js_truthy(inst_emby)
-                        and js_truthy(_get(inst_emby, "enabled"))):
-                    host = _get(inst_emby, "host")
-                    log.info(f"telling emby to refresh at {js_str(host)}")
-                    await self.emby.refresh_library(host=host, api_key=_get(keys_emby, "token"))
+                                                     "markdown", token=tg_token())
+                if emby_on:
+                    log.info(f"telling emby to refresh at {js_str(emby_host)}")
+                    await self.emby.refresh_library(host=emby_host, api_key=emby_key)
         except Exception as err:  # noqa: BLE001 — reference catches everything here
             log.warn("failed to run deployed hooks:", err_message(err))
 

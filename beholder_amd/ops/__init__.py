@@ -41,13 +41,8 @@ def _load():
             from . import build as _build
             _build.build()
             mod = importlib.import_module("beholder_amd.ops._native")
-        import json as _json
-
         from ..models.proto import DecodeError
-        from ..utils import log as _log
         mod.configure(decode_error=DecodeError, topics=TOPIC_NAMES_BY_ID)
-        mod.configure_text(_log.js_str, lambda v: _json.dumps(v, separators=(",", ":"), ensure_ascii=False,
-                                                               default=_log.js_str))
         _native = mod
         return mod
 
@@ -118,3 +113,7 @@ __all__ = [
     "frame", "frames", "mono_ns", "codec_for", "field_table", "format_line", "quick_format", "js_str",
     "js_number", "encode_query", "quote_component",
 ]
+
+# JS-semantics fallbacks for the native text helpers (lists, dicts, %j) live in
+# utils.log, which imports this package; importing it last avoids a cycle.
+from ..utils import log as _log  # noqa: E402,F401

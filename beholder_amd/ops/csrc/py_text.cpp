@@ -8,7 +8,10 @@
 //     (Trello / Telegram / Emby URLs, index.js:53,83,99,112).
 // Semantics are pinned by tests/test_text.py against the Python reference
 // implementations in beholder_amd/utils/log.py and sinks/http.py.
+#include <time.h>
+
 #include <cmath>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -297,6 +300,37 @@ bool quick_format_append(std::string& out, PyObject* const* args, Py_ssize_t nar
   return true;
 }
 
+// Appends one pino line for `args` to `out`. Returns false with a Python error set.
+bool append_line(std::string& out, long lvl, long long t, const char* prefix, Py_ssize_t plen, PyObject* extra,
+                 PyObject* const* argv, Py_ssize_t nargs) {
+  char head[64];
+  int hl = snprintf(head, sizeof head, "{\"level\":%ld,\"time\":%lld,", lvl, t);
+  out.append(head, size_t(hl));
+  out.append(prefix, size_t(plen));
+  if (extra && extra != Py_None) {
+    Py_ssize_t el;
+    const char* ex = PyUnicode_AsUTF8AndSize(extra, &el);
+    if (!ex) return false;
+    out.append(ex, size_t(el));
+  }
+  if (nargs) {
+    std::string msg;
+    msg.reserve(128);
+    if (!quick_format_append(msg, argv, nargs)) return false;
+    out += ",\"msg\":\"";
+    json_escape_append(out, msg.data(), msg.size());
+    out += '"';
+  }
+  out += ",\"v\":1}\n";
+  return true;
+}
+
+long long wall_ms() {
+  struct timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  return (long long)ts.tv_sec * 1000 + ts.tv_nsec / 1000000;
+}
+
 // format_line(level:int, time_ms:int, prefix:str, extra:str|None, args:tuple) -> str
 PyObject* mod_format_line(PyObject*, PyObject* const* a, Py_ssize_t n) {
   if (n != 5 || !PyUnicode_Check(a[2]) || !PyTuple_Check(a[4])) {
@@ -311,28 +345,184 @@ PyObject* mod_format_line(PyObject*, PyObject* const* a, Py_ssize_t n) {
   if (!prefix) return nullptr;
   std::string out;
   out.reserve(192);
-  char head[64];
-  int hl = snprintf(head, sizeof head, "{\"level\":%ld,\"time\":%lld,", lvl, t);
-  out.append(head, size_t(hl));
-  out.append(prefix, size_t(plen));
-  if (a[3] != Py_None) {
-    Py_ssize_t el;
-    const char* ex = PyUnicode_AsUTF8AndSize(a[3], &el);
-    if (!ex) return nullptr;
-    out.append(ex, size_t(el));
-  }
-  Py_ssize_t nargs = PyTuple_GET_SIZE(a[4]);
-  if (nargs) {
-    std::string msg;
-    msg.reserve(128);
-    if (!quick_format_append(msg, &PyTuple_GET_ITEM(a[4], 0), nargs)) return nullptr;
-    out += ",\"msg\":\"";
-    json_escape_append(out, msg.data(), msg.size());
-    out += '"';
-  }
-  out += ",\"v\":1}\n";
+  if (!append_line(out, lvl, t, prefix, plen, a[3], &PyTuple_GET_ITEM(a[4], 0), PyTuple_GET_SIZE(a[4])))
+    return nullptr;
   return PyUnicode_DecodeUTF8(out.data(), Py_ssize_t(out.size()), "strict");
 }
+
+// ---- LogSink: buffered pino writer ------------------------------------------
+// LogSink(write, buffer_bytes=65536): emit() formats into a C++ buffer; the
+// buffer is handed to `write` (e.g. sys.stdout.write) as one str when it
+// passes `buffer_bytes`, on flush(), and immediately for level >= 50.
+struct LogSinkObject {
+  PyObject_HEAD PyObject* write;
+  PyObject* flush_cb;
+  std::string* buf;
+  size_t limit;
+  unsigned long long counts[7];  // trace..fatal by level/10 - 1, [6] other
+  unsigned long long bytes;
+};
+
+int sink_drain(LogSinkObject* self) {
+  if (self->buf->empty()) return 0;
+  PyObject* s = PyUnicode_DecodeUTF8(self->buf->data(), Py_ssize_t(self->buf->size()), "replace");
+  self->bytes += self->buf->size();
+  self->buf->clear();
+  if (!s) return -1;
+  PyObject* r = PyObject_CallOneArg(self->write, s);
+  Py_DECREF(s);
+  if (!r) return -1;
+  Py_DECREF(r);
+  return 0;
+}
+
+PyObject* sink_new(PyTypeObject* type, PyObject*, PyObject*) {
+  LogSinkObject* self = reinterpret_cast<LogSinkObject*>(type->tp_alloc(type, 0));
+  if (!self) return nullptr;
+  self->write = nullptr;
+  self->flush_cb = nullptr;
+  self->buf = new std::string();
+  self->limit = 65536;
+  memset(self->counts, 0, sizeof self->counts);
+  self->bytes = 0;
+  return reinterpret_cast<PyObject*>(self);
+}
+
+int sink_init(LogSinkObject* self, PyObject* args, PyObject* kwds) {
+  static const char* kwlist[] = {"write", "flush", "buffer_bytes", nullptr};
+  PyObject* w;
+  PyObject* f = Py_None;
+  Py_ssize_t lim = 65536;
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "O|On", const_cast<char**>(kwlist), &w, &f, &lim)) return -1;
+  if (!PyCallable_Check(w)) {
+    PyErr_SetString(PyExc_TypeError, "write must be callable");
+    return -1;
+  }
+  Py_INCREF(w);
+  Py_XSETREF(self->write, w);
+  if (f != Py_None) {
+    Py_INCREF(f);
+    Py_XSETREF(self->flush_cb, f);
+  }
+  self->limit = lim < 0 ? 0 : size_t(lim);
+  self->buf->reserve(self->limit + 512);
+  return 0;
+}
+
+int sink_traverse(LogSinkObject* self, visitproc visit, void* arg) {
+  Py_VISIT(self->write);
+  Py_VISIT(self->flush_cb);
+  return 0;
+}
+
+int sink_clear(LogSinkObject* self) {
+  Py_CLEAR(self->write);
+  Py_CLEAR(self->flush_cb);
+  return 0;
+}
+
+void sink_dealloc(LogSinkObject* self) {
+  PyObject_GC_UnTrack(self);
+  if (self->write && !self->buf->empty()) {
+    PyObject *et, *ev, *tb;
+    PyErr_Fetch(&et, &ev, &tb);
+    if (sink_drain(self) < 0) PyErr_Clear();
+    PyErr_Restore(et, ev, tb);
+  }
+  sink_clear(self);
+  delete self->buf;
+  Py_TYPE(self)->tp_free(reinterpret_cast<PyObject*>(self));
+}
+
+// Formats one line into the sink buffer; drains on size / error level.
+bool sink_emit_core(LogSinkObject* self, long lvl, const char* prefix, Py_ssize_t plen, PyObject* extra,
+                    PyObject* const* argv, Py_ssize_t nargs) {
+  size_t before = self->buf->size();
+  if (!append_line(*self->buf, lvl, wall_ms(), prefix, plen, extra, argv, nargs)) {
+    self->buf->resize(before);
+    return false;
+  }
+  int slot = (lvl >= 10 && lvl <= 60 && lvl % 10 == 0) ? int(lvl / 10 - 1) : 6;
+  self->counts[slot]++;
+  if (lvl >= 50 || self->buf->size() >= self->limit) {
+    if (sink_drain(self) < 0) return false;
+    if (lvl >= 50 && self->flush_cb) {
+      PyObject* r = PyObject_CallNoArgs(self->flush_cb);
+      if (!r) return false;
+      Py_DECREF(r);
+    }
+  }
+  return true;
+}
+
+// emit(level, prefix, extra, args)
+PyObject* sink_emit(LogSinkObject* self, PyObject* const* a, Py_ssize_t n) {
+  if (n != 4 || !PyUnicode_Check(a[1]) || !PyTuple_Check(a[3])) {
+    PyErr_SetString(PyExc_TypeError, "emit(level, prefix, extra, args)");
+    return nullptr;
+  }
+  long lvl = PyLong_AsLong(a[0]);
+  if (lvl == -1 && PyErr_Occurred()) return nullptr;
+  Py_ssize_t plen;
+  const char* prefix = PyUnicode_AsUTF8AndSize(a[1], &plen);
+  if (!prefix) return nullptr;
+  if (!sink_emit_core(self, lvl, prefix, plen, a[2], &PyTuple_GET_ITEM(a[3], 0), PyTuple_GET_SIZE(a[3])))
+    return nullptr;
+  Py_RETURN_NONE;
+}
+
+// retarget(write, flush=None): flush, then send future lines elsewhere
+PyObject* sink_retarget(LogSinkObject* self, PyObject* args) {
+  PyObject* w;
+  PyObject* f = Py_None;
+  if (!PyArg_ParseTuple(args, "O|O", &w, &f)) return nullptr;
+  if (!PyCallable_Check(w)) {
+    PyErr_SetString(PyExc_TypeError, "write must be callable");
+    return nullptr;
+  }
+  if (sink_drain(self) < 0) return nullptr;
+  Py_INCREF(w);
+  Py_XSETREF(self->write, w);
+  if (f == Py_None) {
+    Py_CLEAR(self->flush_cb);
+  } else {
+    Py_INCREF(f);
+    Py_XSETREF(self->flush_cb, f);
+  }
+  Py_RETURN_NONE;
+}
+
+PyObject* sink_flush(LogSinkObject* self, PyObject*) {
+  if (sink_drain(self) < 0) return nullptr;
+  if (self->flush_cb) {
+    PyObject* r = PyObject_CallNoArgs(self->flush_cb);
+    if (!r) return nullptr;
+    Py_DECREF(r);
+  }
+  Py_RETURN_NONE;
+}
+
+PyObject* sink_get_counts(LogSinkObject* self, void*) {
+  return Py_BuildValue("{s:K,s:K,s:K,s:K,s:K,s:K}", "trace", self->counts[0], "debug", self->counts[1], "info",
+                       self->counts[2], "warn", self->counts[3], "error", self->counts[4], "fatal", self->counts[5]);
+}
+PyObject* sink_get_pending(LogSinkObject* self, void*) { return PyLong_FromSize_t(self->buf->size()); }
+PyObject* sink_get_bytes(LogSinkObject* self, void*) { return PyLong_FromUnsignedLongLong(self->bytes); }
+
+PyMethodDef sink_methods[] = {
+    {"emit", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(sink_emit)), METH_FASTCALL,
+     "emit(level, prefix, extra, args): format one pino line into the buffer"},
+    {"flush", reinterpret_cast<PyCFunction>(sink_flush), METH_NOARGS, "write out buffered lines"},
+    {"retarget", reinterpret_cast<PyCFunction>(sink_retarget), METH_VARARGS, "retarget(write, flush=None)"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyGetSetDef sink_getset[] = {
+    {"counts", reinterpret_cast<getter>(sink_get_counts), nullptr, "lines emitted per level", nullptr},
+    {"pending_bytes", reinterpret_cast<getter>(sink_get_pending), nullptr, "buffered bytes", nullptr},
+    {"bytes_written", reinterpret_cast<getter>(sink_get_bytes), nullptr, "bytes handed to write()", nullptr},
+    {nullptr, nullptr, nullptr, nullptr, nullptr}};
+
+PyTypeObject LogSinkType = {PyVarObject_HEAD_INIT(nullptr, 0)};
 
 PyObject* mod_quick_format(PyObject*, PyObject* args) {
   std::string msg;
@@ -425,6 +615,131 @@ PyObject* mod_configure_text(PyObject*, PyObject* args) {
   Py_RETURN_NONE;
 }
 
+
+// ---- LogCore: native base class of utils.log.Logger -------------------------
+// logger.info(...) etc. resolve to these C methods directly. A dict or
+// exception first argument (pino merge-object / error forms) is delegated to
+// the Python subclass's `_emit(level, name, args)`.
+struct LogCoreObject {
+  PyObject_HEAD PyObject* dict;
+  LogSinkObject* sink;
+  PyObject* prefix;
+  long min_level;
+};
+
+const char* level_name(long lvl) {
+  switch (lvl) {
+    case 10:
+      return "trace";
+    case 20:
+      return "debug";
+    case 30:
+      return "info";
+    case 40:
+      return "warn";
+    case 50:
+      return "error";
+    default:
+      return "fatal";
+  }
+}
+
+PyObject* core_new(PyTypeObject* type, PyObject*, PyObject*) {
+  LogCoreObject* self = reinterpret_cast<LogCoreObject*>(type->tp_alloc(type, 0));
+  if (!self) return nullptr;
+  self->sink = nullptr;
+  self->prefix = nullptr;
+  self->min_level = 30;
+  return reinterpret_cast<PyObject*>(self);
+}
+
+int core_traverse(LogCoreObject* self, visitproc visit, void* arg) {
+  Py_VISIT(self->dict);
+  Py_VISIT(self->sink);
+  return 0;
+}
+
+int core_clear(LogCoreObject* self) {
+  Py_CLEAR(self->dict);
+  Py_CLEAR(self->sink);
+  Py_CLEAR(self->prefix);
+  return 0;
+}
+
+void core_dealloc(LogCoreObject* self) {
+  PyObject_GC_UnTrack(self);
+  core_clear(self);
+  Py_TYPE(self)->tp_free(reinterpret_cast<PyObject*>(self));
+}
+
+// _set_core(sink, prefix, min_level)
+PyObject* core_set(LogCoreObject* self, PyObject* args) {
+  PyObject *sink, *prefix;
+  double minl;
+  if (!PyArg_ParseTuple(args, "OUd", &sink, &prefix, &minl)) return nullptr;
+  if (!PyObject_TypeCheck(sink, &LogSinkType)) {
+    PyErr_SetString(PyExc_TypeError, "sink must be a LogSink");
+    return nullptr;
+  }
+  Py_INCREF(sink);
+  Py_XSETREF(self->sink, reinterpret_cast<LogSinkObject*>(sink));
+  Py_INCREF(prefix);
+  Py_XSETREF(self->prefix, prefix);
+  self->min_level = minl > 1e9 ? 1000000000L : long(minl);
+  Py_RETURN_NONE;
+}
+
+PyObject* core_log(LogCoreObject* self, long lvl, PyObject* const* args, Py_ssize_t nargs) {
+  if (lvl < self->min_level) Py_RETURN_NONE;
+  if (!self->sink || !self->prefix) {
+    PyErr_SetString(PyExc_RuntimeError, "logger core not configured");
+    return nullptr;
+  }
+  if (nargs && (PyDict_Check(args[0]) || PyExceptionInstance_Check(args[0]))) {
+    PyObject* tup = PyTuple_New(nargs);
+    if (!tup) return nullptr;
+    for (Py_ssize_t i = 0; i < nargs; ++i) {
+      Py_INCREF(args[i]);
+      PyTuple_SET_ITEM(tup, i, args[i]);
+    }
+    PyObject* r = PyObject_CallMethod(reinterpret_cast<PyObject*>(self), "_emit", "lsN", lvl, level_name(lvl), tup);
+    return r;
+  }
+  Py_ssize_t plen;
+  const char* prefix = PyUnicode_AsUTF8AndSize(self->prefix, &plen);
+  if (!prefix) return nullptr;
+  if (!sink_emit_core(self->sink, lvl, prefix, plen, nullptr, args, nargs)) return nullptr;
+  Py_RETURN_NONE;
+}
+
+#define CORE_LEVEL(name, lvl)                                                          \
+  PyObject* core_##name(LogCoreObject* self, PyObject* const* args, Py_ssize_t nargs) { \
+    return core_log(self, lvl, args, nargs);                                           \
+  }
+CORE_LEVEL(trace, 10)
+CORE_LEVEL(debug, 20)
+CORE_LEVEL(info, 30)
+CORE_LEVEL(warn, 40)
+CORE_LEVEL(error, 50)
+CORE_LEVEL(fatal, 60)
+
+#define CORE_METHOD(name, doc) \
+  {#name, reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(core_##name)), METH_FASTCALL, doc}
+
+PyMethodDef core_methods[] = {CORE_METHOD(trace, "log at level 10"),
+                              CORE_METHOD(debug, "log at level 20"),
+                              CORE_METHOD(info, "log at level 30"),
+                              CORE_METHOD(warn, "log at level 40"),
+                              {"warning", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(core_warn)),
+                               METH_FASTCALL, "alias of warn"},
+                              CORE_METHOD(error, "log at level 50"),
+                              CORE_METHOD(fatal, "log at level 60"),
+                              {"_set_core", reinterpret_cast<PyCFunction>(core_set), METH_VARARGS,
+                               "_set_core(sink, prefix, min_level)"},
+                              {nullptr, nullptr, 0, nullptr}};
+
+PyTypeObject LogCoreType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
 PyMethodDef text_methods[] = {
     {"format_line", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(mod_format_line)), METH_FASTCALL,
      "format_line(level, time_ms, prefix, extra, args) -> pino JSON line"},
@@ -438,6 +753,35 @@ PyMethodDef text_methods[] = {
 
 }  // namespace
 
-int init_text_functions(PyObject* m) { return PyModule_AddFunctions(m, text_methods); }
+int init_text_functions(PyObject* m) {
+  LogSinkType.tp_name = "beholder_amd.ops._native.LogSink";
+  LogSinkType.tp_basicsize = sizeof(LogSinkObject);
+  LogSinkType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC;
+  LogSinkType.tp_doc = "LogSink(write, flush=None, buffer_bytes=65536): buffered pino JSON-lines writer";
+  LogSinkType.tp_new = sink_new;
+  LogSinkType.tp_init = reinterpret_cast<initproc>(sink_init);
+  LogSinkType.tp_dealloc = reinterpret_cast<destructor>(sink_dealloc);
+  LogSinkType.tp_traverse = reinterpret_cast<traverseproc>(sink_traverse);
+  LogSinkType.tp_clear = reinterpret_cast<inquiry>(sink_clear);
+  LogSinkType.tp_methods = sink_methods;
+  LogSinkType.tp_getset = sink_getset;
+  if (PyType_Ready(&LogSinkType) < 0) return -1;
+  LogCoreType.tp_name = "beholder_amd.ops._native.LogCore";
+  LogCoreType.tp_basicsize = sizeof(LogCoreObject);
+  LogCoreType.tp_dictoffset = offsetof(LogCoreObject, dict);
+  LogCoreType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_BASETYPE | Py_TPFLAGS_HAVE_GC;
+  LogCoreType.tp_doc = "native base of the pino-compatible Logger (level methods in C)";
+  LogCoreType.tp_new = core_new;
+  LogCoreType.tp_dealloc = reinterpret_cast<destructor>(core_dealloc);
+  LogCoreType.tp_traverse = reinterpret_cast<traverseproc>(core_traverse);
+  LogCoreType.tp_clear = reinterpret_cast<inquiry>(core_clear);
+  LogCoreType.tp_methods = core_methods;
+  if (PyType_Ready(&LogCoreType) < 0) return -1;
+  Py_INCREF(&LogCoreType);
+  if (PyModule_AddObject(m, "LogCore", reinterpret_cast<PyObject*>(&LogCoreType)) < 0) return -1;
+  Py_INCREF(&LogSinkType);
+  if (PyModule_AddObject(m, "LogSink", reinterpret_cast<PyObject*>(&LogSinkType)) < 0) return -1;
+  return PyModule_AddFunctions(m, text_methods);
+}
 
 }  // namespace beholder

@@ -81,7 +81,7 @@ class HttpResponse:
     def __init__(self, status: int, body: bytes = b"", headers: Optional[Mapping[str, str]] = None, url: str = ""):
         self.status = status
         self.body = body
-        self.headers = dict(headers or {})
+        self.headers = dict(headers) if headers else {}
         self.url = url
 
     @property
@@ -178,11 +178,13 @@ class RecordingHttpClient(HttpClient):
 
     async def request(self, method, url, *, params=None, timeout=None) -> HttpResponse:
         m = method.upper()
-        full = with_query(url, params)
+        full = url + "?" + _native_encode_query(params) if type(params) is dict and params else with_query(url, params)
         self.count += 1
         self.calls.append((m, full))
         if self.delay_s:
             await asyncio.sleep(self.delay_s)
+        if not self.rules:
+            return HttpResponse(200, b"{}", None, full)
         for rm, pref, fn in self.rules:
             if (rm == "*" or rm == m) and full.startswith(pref):
                 r = fn(m, full)

@@ -19,7 +19,7 @@ from .http import HttpClient, HttpError, HttpResponse
 
 COMMENT_FALLBACK = "Failed to retrieve comment text."  # index.js:54
 
-_METHODS = ("get", "post", "put", "delete")
+_METHODS = {"get": "GET", "post": "POST", "put": "PUT", "delete": "DELETE"}
 
 
 class TrelloClient:
@@ -37,15 +37,15 @@ class TrelloClient:
 
     async def make_request(self, method: str, path: str, options: Optional[Mapping[str, Any]] = None) -> HttpResponse:
         """``trello.makeRequest(requestMethod, path, options)``."""
-        m = method.lower()
-        if m not in _METHODS:
+        m = _METHODS.get(method) or _METHODS.get(method.lower())
+        if m is None:
             raise HttpError("Unsupported requestMethod. Pass one of these methods: POST, GET, PUT, DELETE.")
         if not path.startswith("/"):
             raise HttpError("Path must start with /")
-        query = self.create_query()
-        for k, v in (options or {}).items():
-            query[k] = v
-        r = await self.http.request(m.upper(), self.base_url + path, params=query, timeout=self.timeout)
+        query = {"key": self.key, "token": self.token}
+        if options:
+            query.update(options)
+        r = await self.http.request(m, self.base_url + path, params=query, timeout=self.timeout)
         if self.strict:
             r.raise_for_status()
         return r

@@ -165,33 +165,48 @@ def quick_format(args: tuple) -> str:
     return s
 
 
-class Logger:
-    """Minimal pino: ``trace/debug/info/warn/error/fatal(*args)``, ``child(**bindings)``."""
+from ..ops import native as _native  # noqa: E402  (after js_str: ops configures its fallbacks from us)
+
+_native.configure_text(js_str, lambda v: json.dumps(v, separators=(",", ":"), ensure_ascii=False, default=js_str))
+
+
+class _Shared:
+    """State shared by a logger and its children: one native sink, one stream."""
+
+    __slots__ = ("stream", "pid", "hostname", "sink")
+
+    def __init__(self, stream, buffer_bytes: int):
+        self.stream = stream
+        self.pid = os.getpid()
+        self.hostname = socket.gethostname()
+        self.sink = _native.LogSink(stream.write, getattr(stream, "flush", None), buffer_bytes)
+
+
+class Logger(_native.LogCore):
+    """pino-compatible logger: ``trace/debug/info/warn/error/fatal(*args)``, ``child(**bindings)``.
+
+    The level methods are implemented in C (:class:`~beholder_amd.ops.LogCore`):
+    lines are formatted straight into a native :class:`~beholder_amd.ops.LogSink`
+    buffer that is handed to ``stream.write`` in large chunks — on
+    :meth:`flush`, when 64 KiB accumulate, and immediately for error/fatal.
+    The service flushes after every delivery batch and every 100 ms. A dict
+    (merge object) or exception first argument goes through :meth:`_emit`.
+    """
 
     def __init__(self, name: str = "index.js", level: str = "info", stream: Optional[TextIO] = None,
-                 bindings: Optional[dict] = None, _shared: Optional[dict] = None):
+                 bindings: Optional[dict] = None, _shared: Optional[_Shared] = None, buffer_bytes: int = 65536):
+        super().__init__()
         if level not in LEVELS:
             raise ValueError(f"unknown log level {level!r}")
         self.name = name
-        self._shared = _shared if _shared is not None else {
-            "stream": stream if stream is not None else sys.stdout,
-            "lock": threading.Lock(),
-            "pid": os.getpid(),
-            "hostname": socket.gethostname(),
-            "counts": {k: 0 for k in LEVELS if k != "silent"},
-        }
+        self._shared = _shared or _Shared(stream if stream is not None else sys.stdout, buffer_bytes)
         self._bindings = dict(bindings or {})
         self._prefix = self._make_prefix()
-        try:  # native pino line formatter (same semantics, ~10x faster)
-            from ..ops import format_line as _fl
-            self._format_line = _fl
-        except ImportError:  # pragma: no cover - native runtime missing
-            self._format_line = None
         self.set_level(level)
 
     def _make_prefix(self) -> str:
         sh = self._shared
-        head = f'"pid":{sh["pid"]},"hostname":{json.dumps(sh["hostname"])},"name":{json.dumps(self.name)}'
+        head = f'"pid":{sh.pid},"hostname":{json.dumps(sh.hostname)},"name":{json.dumps(self.name)}'
         for k, v in self._bindings.items():
             head += f",{json.dumps(str(k))}:{json.dumps(_json_safe(v), ensure_ascii=False)}"
         return head
@@ -205,99 +220,57 @@ class Logger:
         self.is_trace = self._min <= 10
         self.is_debug = self._min <= 20
         self.is_info = self._min <= 30
+        self._set_core(self._shared.sink, self._prefix, float(self._min))
 
     @property
     def stream(self) -> TextIO:
-        return self._shared["stream"]
+        return self._shared.stream
 
     @stream.setter
     def stream(self, s: TextIO) -> None:
-        self._shared["stream"] = s
+        self._shared.stream = s
+        self._shared.sink.retarget(s.write, getattr(s, "flush", None))
 
     @property
     def counts(self) -> Dict[str, int]:
-        """Lines emitted per level (all children share one counter table)."""
-        return self._shared["counts"]
+        """Lines emitted per level (a logger and its children share one table)."""
+        return dict(self._shared.sink.counts)
 
     def child(self, **bindings) -> "Logger":
         b = dict(self._bindings)
         b.update(bindings)
-        lg = Logger(self.name, self.level, bindings=b, _shared=self._shared)
-        return lg
+        return Logger(self.name, self.level, bindings=b, _shared=self._shared)
 
-    # -- emit ------------------------------------------------------------------
+    # -- slow path (merge object / exception first argument) -----------------
     def _emit(self, lvl: int, lname: str, args: tuple) -> None:
-        extra = None
-        if args and isinstance(args[0], dict):
-            extra = args[0]
-            args = args[1:]
-        elif args and isinstance(args[0], BaseException):
-            e = args[0]
-            extra = {"type": type(e).__name__, "stack": f"{type(e).__name__}: {e}"}
-            args = args[1:] if len(args) > 1 else (str(e),)
         extra_s = None
-        if extra:
-            extra_s = "".join(f",{json.dumps(str(k))}:{json.dumps(_json_safe(v), ensure_ascii=False)}"
-                              for k, v in extra.items())
-        fl = self._format_line
-        if fl is not None:
-            line = fl(lvl, int(time.time() * 1000), self._prefix, extra_s, args)
-        else:
-            line = self._py_line(lvl, extra_s, args)
-        sh = self._shared
-        sh["counts"][lname] += 1
-        with sh["lock"]:
-            sh["stream"].write(line)
-            if lvl >= 50:
-                try:
-                    sh["stream"].flush()
-                except (OSError, ValueError):
-                    pass
+        if args:
+            a0 = args[0]
+            if isinstance(a0, dict):
+                extra_s = "".join(f",{json.dumps(str(k))}:{json.dumps(_json_safe(v), ensure_ascii=False)}"
+                                  for k, v in a0.items()) or None
+                args = args[1:]
+            elif isinstance(a0, BaseException):
+                extra_s = (f',"type":{json.dumps(type(a0).__name__)},'
+                           f'"stack":{json.dumps(f"{type(a0).__name__}: {a0}", ensure_ascii=False)}')
+                args = args[1:] if len(args) > 1 else (str(a0),)
+        self._shared.sink.emit(lvl, self._prefix, extra_s, args)
 
-    def _py_line(self, lvl: int, extra_s, args: tuple) -> str:
-        """Pure-Python line formatter (reference implementation for the native one)."""
-        parts = [f'{{"level":{lvl},"time":{int(time.time() * 1000)},', self._prefix]
-        if extra_s:
-            parts.append(extra_s)
+    def py_line(self, lvl: int, args: tuple, time_ms: Optional[int] = None) -> str:
+        """Pure-Python line formatter — the reference the native one is tested against."""
+        parts = [f'{{"level":{lvl},"time":{int(time.time() * 1000) if time_ms is None else time_ms},',
+                 self._prefix]
         if args:
             parts.append(',"msg":')
             parts.append(json.dumps(quick_format(args), ensure_ascii=False))
         parts.append(',"v":1}\n')
         return "".join(parts)
 
-    def trace(self, *args) -> None:
-        if self._min <= 10:
-            self._emit(10, "trace", args)
-
-    def debug(self, *args) -> None:
-        if self._min <= 20:
-            self._emit(20, "debug", args)
-
-    def info(self, *args) -> None:
-        if self._min <= 30:
-            self._emit(30, "info", args)
-
-    def warn(self, *args) -> None:
-        if self._min <= 40:
-            self._emit(40, "warn", args)
-
-    warning = warn
-
-    def error(self, *args) -> None:
-        if self._min <= 50:
-            self._emit(50, "error", args)
-
-    def fatal(self, *args) -> None:
-        if self._min <= 60:
-            self._emit(60, "fatal", args)
-
     def flush(self) -> None:
-        sh = self._shared
-        with sh["lock"]:
-            try:
-                sh["stream"].flush()
-            except (OSError, ValueError):
-                pass
+        try:
+            self._shared.sink.flush()
+        except (OSError, ValueError):
+            pass
 
 
 class NullStream:
@@ -309,7 +282,7 @@ class NullStream:
 
     def write(self, s: str) -> int:
         self.bytes += len(s)
-        self.lines += 1
+        self.lines += s.count("\n")
         return len(s)
 
     def flush(self) -> None:
@@ -331,6 +304,9 @@ class MemoryStream:
 
     def records(self):
         return [json.loads(x) for x in self.lines]
+
+    def __iter__(self):
+        return iter(self.lines)
 
 
 def get_logger(name: str = "index.js", level: str = "info", stream: Optional[TextIO] = None) -> Logger:

@@ -97,6 +97,7 @@ class Rig:
         return [(m, u.split("?")[0], parse_query(u)) for m, u in self.http.calls]
 
     def msgs(self, level: Optional[int] = None):
+        self.log.flush()
         return [r.get("msg") for r in self.stream.records() if level is None or r["level"] == level]
 
 
