@@ -3,7 +3,7 @@
 
 One *step* = ``--events-per-step`` synthetic telemetry events (90% progress /
 10% status, protobuf-encoded, framed) pushed through the **whole** service
-path of each rank:
+path of each consumer process:
 
     producer thread -> OS pipe -> native reader thread (framing, ring)
       -> event loop: Delivery batches -> eager handler dispatch
@@ -11,18 +11,22 @@ path of each rank:
       -> media store (in-memory, 10k rows) -> Prometheus counters
       -> Trello/Telegram/Emby request construction (URL + query encoding)
          into an in-process HTTP recorder (no network)
-      -> pino JSON log line per reference log call (info level, written to /dev/null)
+      -> pino JSON log line per reference log call (info level, to /dev/null)
       -> ack (latency recorded natively)
 
 A step ends when every event of the step has been settled. ``W`` warm-up
-steps run untimed, then exactly ``K`` steps are timed between barriers.
+steps run untimed, then exactly ``K`` steps are timed.
 
-Multi-GPU contract: launched with ``torch.distributed.run`` each rank is an
-independent consumer process (competing consumers over its own stream:
-per-rank work is fixed, so scaling is *weak*); ranks synchronise with gloo
-barriers, the elapsed time is the MAX over ranks and ``value`` is the
-whole-job events/s. The service has no device work (the reference has none),
-so nothing is launched on the GPU.
+Scale-out is the reference's: competing consumers, one process each
+(SURVEY.md §2.3). Each rank runs ``--procs-per-rank`` consumer processes
+(default: its share of the host's CPUs, at most 8) on independent streams.
+Timing: every consumer finishes its warm-up and parks on a barrier; the
+rank's coordinator passes a gloo barrier across ranks, releases its
+consumers and starts the clock; it stops the clock when all of its
+consumers report their K steps done, then passes another gloo barrier. The
+elapsed time is the MAX over ranks and ``value`` is whole-job events/s.
+Per-consumer work is fixed as N grows: weak scaling. The service has no
+device work (the reference has none), so nothing runs on the GPU.
 
 Prints ONE JSON line on rank 0.
 """
@@ -32,6 +36,7 @@ import argparse
 import asyncio
 import gc
 import json
+import multiprocessing as mp
 import os
 import sys
 import threading
@@ -44,12 +49,41 @@ if ROOT not in sys.path:
 BASELINE_METRIC = "metric_events_ingested_per_sec"
 
 
+def available_cpus() -> int:
+    """CPUs this process may use: affinity mask, capped by a cgroup v2/v1 CPU quota."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(p)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                p = int(f.read())
+            if q > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        n = min(n, max(1, int(quota)))
+    return max(1, n)
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
-    ap.add_argument("--gpus", type=int, default=1, help="number of ranks (one process per GPU slot)")
+    ap.add_argument("--gpus", type=int, default=1, help="number of ranks (one process group member per GPU slot)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--events-per-step", type=int, default=65536)
+    ap.add_argument("--events-per-step", type=int, default=65536, help="events per step per consumer process")
+    ap.add_argument("--procs-per-rank", type=int, default=0,
+                    help="consumer processes per rank (0 = min(8, CPUs per rank - 1))")
     ap.add_argument("--media", type=int, default=10000)
     ap.add_argument("--log-level", default="info")
     ap.add_argument("--seed", type=int, default=0)
@@ -63,6 +97,7 @@ class _Dist:
     def __init__(self):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
+        self.local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(self.world)))
         self.dist = None
         if self.world > 1:
             import torch.distributed as dist
@@ -93,7 +128,8 @@ class _Dist:
             self.dist.destroy_process_group()
 
 
-async def run_rank(a, dist: _Dist) -> dict:
+async def run_consumer(a, seed: int, go) -> dict:
+    """One consumer process: build the service, warm up, ``go()``, time K steps."""
     from beholder_amd.bench.generator import Workload, bench_config
     from beholder_amd.config import Config
     from beholder_amd.service import Service
@@ -104,7 +140,7 @@ async def run_rank(a, dist: _Dist) -> dict:
 
     E = a.events_per_step
     total_steps = a.warmup + a.steps
-    w = Workload(n_media=a.media, seed=a.seed + 7919 * dist.rank)
+    w = Workload(n_media=a.media, seed=seed)
     step_bytes = [w.framed(E) for _ in range(total_steps)]
 
     rfd, wfd = os.pipe()
@@ -117,9 +153,6 @@ async def run_rank(a, dist: _Dist) -> dict:
     svc = Service(cfg, source=FdSource(fd=rfd, batch=512), store=MemoryStore(w.media), http=http,
                   logger=Logger(stream=log_sink, level=a.log_level), serve_metrics=False)
     await svc.init()
-    gc.collect()
-    gc.freeze()  # long-lived startup objects out of the young generations (service does the same)
-
     run_task = asyncio.ensure_future(svc.run())
     settler = svc.source.settler
 
@@ -141,21 +174,20 @@ async def run_rank(a, dist: _Dist) -> dict:
         while settled() < target or svc._inflight:
             await asyncio.sleep(0.0002)
 
-    t0 = t1 = 0.0
+    t0 = 0.0
     for i in range(total_steps):
         if i == a.warmup:
             settler.reset_latency()
-            dist.barrier()
+            go()
             t0 = time.perf_counter()
         th = write_step(i)
         await wait_settled((i + 1) * E)
         th.join()
-    t1 = time.perf_counter()
+    elapsed = time.perf_counter() - t0
     os.close(wfd)
     await run_task
     await svc.close()
     log_sink.close()
-    elapsed = t1 - t0
     st = svc.stats()
     return {
         "elapsed": elapsed,
@@ -168,6 +200,58 @@ async def run_rank(a, dist: _Dist) -> dict:
     }
 
 
+def _consumer_entry(a, seed, barrier, results):
+    """Spawned consumer process."""
+    try:
+        res = asyncio.run(run_consumer(a, seed, barrier.wait))
+        results.put(res)
+    except BaseException as e:  # report, never hang the coordinator
+        try:
+            barrier.abort()
+        except Exception:  # noqa: BLE001
+            pass
+        results.put({"error": f"{type(e).__name__}: {e}"})
+        raise
+
+
+def run_rank(a, dist: _Dist, procs: int) -> dict:
+    """Coordinator for one rank's consumer processes; returns the rank's merged result."""
+    base_seed = a.seed + 7919 * dist.rank
+    if procs == 1:
+        def go():
+            dist.barrier()
+        res = asyncio.run(run_consumer(a, base_seed, go))
+        res["procs"] = 1
+        return res
+    ctx = mp.get_context("spawn")
+    barrier = ctx.Barrier(procs + 1)
+    results = ctx.Queue()
+    children = [ctx.Process(target=_consumer_entry, args=(a, base_seed + 104729 * i, barrier, results),
+                            daemon=True) for i in range(procs)]
+    for c in children:
+        c.start()
+    barrier.wait()          # every consumer has warmed up
+    dist.barrier()          # ... on every rank
+    t0 = time.perf_counter()
+    # releasing the barrier is the consumers' go signal (they were parked in it)
+    got = [results.get() for _ in range(procs)]
+    t1 = time.perf_counter()
+    for c in children:
+        c.join(60)
+    errs = [g["error"] for g in got if "error" in g]
+    if errs:
+        raise RuntimeError("consumer failed: " + "; ".join(errs))
+    from beholder_amd.ops import Histogram
+    hh, ih = Histogram(), Histogram()
+    for g in got:
+        hh.merge_bytes(g["handle_hist"])
+        ih.merge_bytes(g["ingest_hist"])
+    return {"elapsed": t1 - t0, "events": sum(g["events"] for g in got), "handle_hist": hh.to_bytes(),
+            "ingest_hist": ih.to_bytes(), "http_calls": sum(g["http_calls"] for g in got),
+            "errors": sum(g["errors"] for g in got), "abandoned": sum(g["abandoned"] for g in got),
+            "procs": procs, "max_consumer_elapsed": max(g["elapsed"] for g in got)}
+
+
 def main(argv=None) -> int:
     a = parse(argv)
     dist = _Dist()
@@ -175,17 +259,21 @@ def main(argv=None) -> int:
     if dist.world == 1 and a.gpus > 1:
         print(f"bench.py: --gpus {a.gpus} requires torch.distributed.run; running 1 rank", file=sys.stderr)
         n = 1
-    res = asyncio.run(run_rank(a, dist))
+    procs = a.procs_per_rank or max(1, min(8, available_cpus() // max(1, dist.local_world) - 1))
+    gc.collect()
+    res = run_rank(a, dist, procs)
     dist.barrier()
     elapsed = dist.max(res["elapsed"])
-    parts = dist.gather({k: res[k] for k in ("handle_hist", "ingest_hist", "http_calls", "errors", "abandoned")})
+    parts = dist.gather({k: res[k] for k in ("handle_hist", "ingest_hist", "http_calls", "errors", "abandoned",
+                                             "events", "procs")})
     if dist.rank == 0:
         from beholder_amd.ops import Histogram
         hh, ih = Histogram(), Histogram()
         for p in parts:
             hh.merge_bytes(p["handle_hist"])
             ih.merge_bytes(p["ingest_hist"])
-        total_events = res["events"] * n
+        total_events = sum(p["events"] for p in parts)
+        total_procs = sum(p["procs"] for p in parts)
         value = total_events / elapsed
         out = {
             "metric": BASELINE_METRIC,
@@ -203,14 +291,15 @@ def main(argv=None) -> int:
                     "Trello/Telegram/Emby stubbed in-process, info logs to /dev/null",
             "config": {
                 "model": "beholder telemetry consumer (status+progress handlers, index.js:62-155)",
-                "global_batch": a.events_per_step * n,
+                "global_batch": a.events_per_step * total_procs,
                 "seq_len": None,
-                "parallelism": f"dp{n} (competing consumers, one process per rank)",
+                "parallelism": f"dp{n} x {procs} consumer procs/rank (competing consumers)",
             },
+            "procs_per_rank": procs,
+            "events_per_proc_per_sec": round(value / total_procs, 1),
             "p50_handle_latency_us": round(hh.percentile(50) / 1e3, 3),
             "p99_handle_latency_us": round(hh.percentile(99) / 1e3, 3),
             "p50_ingest_latency_us": round(ih.percentile(50) / 1e3, 3),
-            "events_per_rank_per_sec": round(value / n, 1),
             "http_requests": sum(p["http_calls"] for p in parts),
             "handler_errors": sum(p["errors"] for p in parts),
         }

@@ -18,8 +18,8 @@ def _last_json(stdout: str) -> dict:
 
 
 def test_bench_single_rank_contract():
-    r = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--events-per-step", "4096"],
-                       cwd=ROOT, capture_output=True, text=True, timeout=300)
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--events-per-step", "4096",
+                        "--procs-per-rank", "1"], cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     out = _last_json(r.stdout)
     assert REQUIRED <= set(out) and out["n_gpus"] == 1 and out["steps"] == 2 and out["warmup"] == 1
@@ -31,9 +31,20 @@ def test_bench_single_rank_contract():
 def test_bench_two_ranks_gloo():
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", "29561", "bench.py", "--gpus", "2",
-                        "--steps", "2", "--warmup", "1", "--events-per-step", "4096"],
+                        "--steps", "2", "--warmup", "1", "--events-per-step", "4096", "--procs-per-rank", "1"],
                        cwd=ROOT, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     out = _last_json(r.stdout)
     assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 8192
     assert out["config"]["parallelism"].startswith("dp2")
+
+
+def test_bench_multiprocess_rank():
+    """Consumer processes per rank: events add up, value = total events / coordinator time."""
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--events-per-step", "4096",
+                        "--procs-per-rank", "2"], cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _last_json(r.stdout)
+    assert out["procs_per_rank"] == 2 and out["config"]["global_batch"] == 8192
+    assert out["value"] == pytest.approx(8192 * 2 / (out["ms_per_step"] * 2 / 1000), rel=0.01)
+    assert out["handler_errors"] == 0
