@@ -60,6 +60,8 @@ SERVICE_DEFAULTS: dict = {
             "telegram": "https://api.telegram.org",
         },
         "shutdown_grace_s": 10.0,
+        # gc.freeze() after init: long-lived startup objects leave the collected generations
+        "gc_freeze": True,
     }
 }
 

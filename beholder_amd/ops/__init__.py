@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import importlib
 import os
+import subprocess
 import threading
 from typing import Dict, Optional
 
@@ -32,15 +33,19 @@ def _load():
     with _lock:
         if _native is not None:
             return _native
+        if os.environ.get("BEHOLDER_ALLOW_BUILD", "1") != "0":
+            # no-op when the in-tree .so matches the sources (hash stamp); rebuilds a stale one
+            from .. import _build
+            try:
+                _build.build()
+            except (OSError, subprocess.CalledProcessError) as e:  # no compiler: use what is there
+                if not os.path.exists(_build.TARGET):
+                    raise ImportError(f"cannot build the beholder native runtime: {e}") from e
         try:
             mod = importlib.import_module("beholder_amd.ops._native")
         except ImportError as first:
-            if os.environ.get("BEHOLDER_ALLOW_BUILD", "1") == "0":
-                raise ImportError(
-                    "beholder native runtime is not built; run `python -m beholder_amd.ops.build`") from first
-            from . import build as _build
-            _build.build()
-            mod = importlib.import_module("beholder_amd.ops._native")
+            raise ImportError(
+                "beholder native runtime is not built; run `python -m beholder_amd.ops.build`") from first
         from ..models.proto import DecodeError
         mod.configure(decode_error=DecodeError, topics=TOPIC_NAMES_BY_ID)
         _native = mod
@@ -55,6 +60,7 @@ Delivery = native.Delivery
 Settler = native.Settler
 Counter = native.Counter
 Histogram = native.Histogram
+AmqpDemux = native.AmqpDemux
 frame = native.frame
 frames = native.frames
 mono_ns = native.mono_ns
@@ -109,7 +115,7 @@ def codec_for(ptype) -> Optional[object]:
 
 
 __all__ = [
-    "native", "MessageCodec", "Ingest", "Delivery", "Settler", "Counter", "Histogram",
+    "native", "AmqpDemux", "MessageCodec", "Ingest", "Delivery", "Settler", "Counter", "Histogram",
     "frame", "frames", "mono_ns", "codec_for", "field_table", "format_line", "quick_format", "js_str",
     "js_number", "encode_query", "quote_component",
 ]

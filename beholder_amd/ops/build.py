@@ -1,89 +1,5 @@
-"""Build the native runtime in-tree (``beholder_amd/ops/_native*.so``).
-
-Beholder's runtime around the Python handlers (ingest reader thread, ring,
-codec, deliveries, histograms) is C++ — see ``csrc/``. The service has no
-device kernels (the reference has none), so this is a host
-build with the system C++ compiler; ``__graft_entry__.build()`` calls it.
-
-Usage: ``python -m beholder_amd.ops.build [--debug] [--sanitize=address,undefined]``
-"""
-from __future__ import annotations
-
-import argparse
-import glob
-import hashlib
-import os
-import subprocess
-import sys
-import sysconfig
-
-HERE = os.path.dirname(os.path.abspath(__file__))
-CSRC = os.path.join(HERE, "csrc")
-EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-TARGET = os.path.join(HERE, "_native" + EXT_SUFFIX)
-STAMP = TARGET + ".srchash"
-
-
-def sources() -> list:
-    return sorted(glob.glob(os.path.join(CSRC, "*.cpp")))
-
-
-def source_hash(flags: list) -> str:
-    h = hashlib.sha256()
-    for p in sorted(glob.glob(os.path.join(CSRC, "*"))):
-        with open(p, "rb") as f:
-            h.update(os.path.basename(p).encode())
-            h.update(f.read())
-    h.update(" ".join(flags).encode())
-    return h.hexdigest()
-
-
-def compile_flags(debug: bool = False, sanitize: str = "") -> list:
-    inc = sysconfig.get_paths()["include"]
-    flags = ["-std=c++17", "-fPIC", "-shared", "-pthread", "-fvisibility=hidden",
-             "-Wall", "-Wextra", "-Wno-missing-field-initializers", "-Wno-cast-function-type",
-             f"-I{inc}", f"-I{CSRC}"]
-    if debug:
-        flags += ["-O0", "-g"]
-    else:
-        # x86-64-v2 keeps the .so portable across the build container and the
-        # GPU box hosts (both are x86-64 with SSE4.2/POPCNT).
-        flags += ["-O3", "-march=x86-64-v2", "-mtune=generic", "-DNDEBUG"]
-    if sanitize:
-        flags += [f"-fsanitize={sanitize}", "-fno-omit-frame-pointer", "-g"]
-    return flags
-
-
-def build(force: bool = False, debug: bool = False, sanitize: str = "", cxx: str = "", verbose: bool = False) -> str:
-    cxx = cxx or os.environ.get("CXX") or "g++"
-    flags = compile_flags(debug, sanitize)
-    # hash path-independent flags so a snapshot copied elsewhere (GPU box) reuses the .so
-    digest = source_hash([f for f in flags if not f.startswith("-I")] + [cxx, sysconfig.get_config_var("SOABI") or ""])
-    if not force and os.path.exists(TARGET) and os.path.exists(STAMP):
-        with open(STAMP) as f:
-            if f.read().strip() == digest:
-                return TARGET
-    tmp = TARGET + ".tmp"
-    cmd = [cxx, *flags, *sources(), "-o", tmp]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
-    os.replace(tmp, TARGET)
-    with open(STAMP, "w") as f:
-        f.write(digest)
-    return TARGET
-
-
-def main(argv=None) -> int:
-    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
-    ap.add_argument("--force", action="store_true")
-    ap.add_argument("--debug", action="store_true")
-    ap.add_argument("--sanitize", default="")
-    ap.add_argument("--cxx", default="")
-    a = ap.parse_args(argv)
-    print(build(force=a.force, debug=a.debug, sanitize=a.sanitize, cxx=a.cxx, verbose=True))
-    return 0
-
+"""CLI: ``python -m beholder_amd.ops.build`` — build the native runtime in-tree (see :mod:`beholder_amd._build`)."""
+from .._build import TARGET, build, main  # noqa: F401
 
 if __name__ == "__main__":
     raise SystemExit(main())

@@ -69,5 +69,6 @@ int init_codec_types(PyObject* m);
 int init_metric_types(PyObject* m);
 int init_ingest_types(PyObject* m);
 int init_text_functions(PyObject* m);
+int init_amqp_types(PyObject* m);
 
 }  // namespace beholder

@@ -28,6 +28,7 @@ matching the broker's prefetch window.
 from __future__ import annotations
 
 import asyncio
+import gc
 import time
 from typing import Any, Callable, Dict, List, Optional
 
@@ -172,6 +173,11 @@ class Service:
         # 9.
         self._initialized = True
         self.started_at = time.time()
+        if svc.get("gc_freeze", True):
+            # Config, descriptors, store rows and handlers live for the whole process:
+            # move them out of the collected generations so young-gen passes stay cheap.
+            gc.collect()
+            gc.freeze()
         self.log.info("initialized")
         return self
 
@@ -246,6 +252,7 @@ class Service:
             await self.init()
         self._running = True
         self._slot_free = asyncio.Event()
+        flusher = asyncio.ensure_future(self._flush_logs_periodically())
         log = self.log
         routes = self._routes
         nroutes = len(routes)
@@ -271,9 +278,19 @@ class Service:
                 await sleep(0)  # keep timers / the metrics endpoint responsive under sustained load
         finally:
             self._running = False
+            flusher.cancel()
             await self._drain()
             log.flush()
         return self.stats()
+
+    async def _flush_logs_periodically(self, every_s: float = 0.1) -> None:
+        """Lines logged outside the batch loop (reconnects, idle periods) reach the stream within 100 ms."""
+        try:
+            while True:
+                await asyncio.sleep(every_s)
+                self.log.flush()
+        except asyncio.CancelledError:
+            pass
 
     def _dispatch_now(self, d, on_finish: Optional[Callable[[], None]] = None) -> None:
         handler = self._routes[d.topic_id]

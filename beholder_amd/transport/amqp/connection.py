@@ -117,7 +117,8 @@ class Channel:
                         global_=global_)
 
     async def basic_consume(self, queue: str, on_message: Callable, consumer_tag: str = "",
-                            no_ack: bool = False, exclusive: bool = False, arguments=None) -> str:
+                            no_ack: bool = False, exclusive: bool = False, arguments=None,
+                            native_topic: Optional[int] = None) -> str:
         """``on_message(channel, deliver_method, properties, body)`` runs in the reader task.
 
         The consumer tag is chosen client-side and the callback registered
@@ -126,11 +127,18 @@ class Channel:
         """
         tag = consumer_tag or f"beholder.ctag-{self.conn._ctag_prefix}-{next(self.conn._ctags)}"
         self._consumers[tag] = on_message
+        demux = self.conn._demux
+        if native_topic is not None and demux is not None:
+            # deliveries for this consumer are assembled natively into Delivery objects
+            # (extra = this channel, so settling routes the ack back here)
+            demux.add_consumer(self.id, tag, int(native_topic), self)
         try:
             await self._rpc("basic.consume", ("basic.consume_ok",), queue=queue, consumer_tag=tag,
                             no_local=False, no_ack=no_ack, exclusive=exclusive, arguments=arguments or {})
         except BaseException:
             self._consumers.pop(tag, None)
+            if demux is not None:
+                demux.remove_consumer(self.id, tag)
             raise
         return tag
 
@@ -138,6 +146,8 @@ class Channel:
         if self.is_open:
             await self._rpc("basic.cancel", ("basic.cancel_ok",), consumer_tag=consumer_tag)
         self._consumers.pop(consumer_tag, None)
+        if self.conn._demux is not None:
+            self.conn._demux.remove_consumer(self.id, consumer_tag)
 
     def basic_ack(self, delivery_tag: int, multiple: bool = False) -> None:
         self.conn._write(wire.encode_method(self.id, "basic.ack", delivery_tag=delivery_tag, multiple=multiple))
@@ -193,6 +203,8 @@ class Channel:
             return
         if name == "basic.cancel":  # consumer_cancel_notify (queue deleted, ...)
             self._consumers.pop(m.consumer_tag, None)
+            if self.conn._demux is not None:
+                self.conn._demux.remove_consumer(self.id, m.consumer_tag)
             if self.on_close:
                 self.on_close(self, AmqpError(f"consumer {m.consumer_tag} cancelled by broker"))
             return
@@ -260,6 +272,8 @@ class Channel:
         self.is_open = False
         self.close_reason = err
         self.conn._channels.pop(self.id, None)
+        if self.conn._demux is not None:
+            self.conn._demux.reset_channel(self.id)
         w = self._waiter
         if w is not None and not w.done():
             w.set_exception(err or AmqpError(f"channel {self.id} closed", wire.CHANNEL_ERROR))
@@ -274,7 +288,12 @@ class Channel:
 
 class Connection:
     def __init__(self, url: str, *, heartbeat: Optional[int] = None, connect_timeout: float = 10.0,
-                 logger=None, on_lost: Optional[Callable[[Optional[BaseException]], None]] = None):
+                 logger=None, on_lost: Optional[Callable[[Optional[BaseException]], None]] = None,
+                 native_settler=None, on_delivery: Optional[Callable[[Any], None]] = None):
+        """``native_settler`` + ``on_delivery`` enable the native delivery path
+        (:class:`~beholder_amd.ops.AmqpDemux`): deliveries for consumers
+        registered with ``native_topic`` arrive as native ``Delivery`` objects
+        through ``on_delivery``; all other frames take the Python path."""
         self.params = wire.parse_url(url)
         if heartbeat is not None:
             self.params["heartbeat"] = heartbeat
@@ -306,6 +325,11 @@ class Connection:
         self._lost_reported = False
         self.bytes_in = 0
         self.bytes_out = 0
+        self.on_delivery = on_delivery
+        self._demux = None
+        if native_settler is not None and on_delivery is not None:
+            from ...ops import AmqpDemux
+            self._demux = AmqpDemux(native_settler, 0)
 
     # ------------------------------------------------------------- open ----
     async def open(self) -> "Connection":
@@ -394,8 +418,21 @@ class Connection:
                     break
                 self.bytes_in += len(data)
                 self._last_rx = time.monotonic()
-                for ftype, ch, payload in self._parser.feed(data):
-                    self._dispatch(ftype, ch, payload)
+                demux = self._demux
+                if demux is not None:
+                    try:
+                        items = demux.feed(data)
+                    except ValueError as e:
+                        raise wire.FrameError(str(e), wire.FRAME_ERROR) from None
+                    on_delivery = self.on_delivery
+                    for it in items:
+                        if type(it) is tuple:
+                            self._dispatch(*it)
+                        else:
+                            on_delivery(it)
+                else:
+                    for ftype, ch, payload in self._parser.feed(data):
+                        self._dispatch(ftype, ch, payload)
         except asyncio.CancelledError:
             return
         except (ConnectionError, OSError, AmqpError) as e:
@@ -439,6 +476,8 @@ class Connection:
             self.frame_max = _negotiate(m.frame_max, p["frame_max"]) or 131072
             self.heartbeat = _negotiate(m.heartbeat, p["heartbeat"])
             self._parser.frame_max = self.frame_max
+            if self._demux is not None:
+                self._demux.set_frame_max(self.frame_max)
             self._write(wire.encode_method(0, "connection.tune_ok", channel_max=self.channel_max,
                                            frame_max=self.frame_max, heartbeat=self.heartbeat))
             self._write(wire.encode_method(0, "connection.open", virtual_host=p["vhost"], capabilities="",

@@ -37,7 +37,7 @@ class AmqpSource(Source):
 
     def __init__(self, url: str, prefetch: int = 100, retries: int = 2, *, logger=None,
                  durable: bool = True, heartbeat: Optional[int] = None, backoff_initial: float = 0.25,
-                 backoff_max: float = 30.0, connect_timeout: float = 10.0):
+                 backoff_max: float = 30.0, connect_timeout: float = 10.0, native: bool = True):
         self.url = url
         self._prefetch = int(prefetch)
         self.retries = int(retries)
@@ -47,6 +47,7 @@ class AmqpSource(Source):
         self.backoff_initial = backoff_initial
         self.backoff_max = backoff_max
         self.connect_timeout = connect_timeout
+        self.native = native  # assemble deliveries in C (ops.AmqpDemux)
         self._settler = Settler(on_settle=self._on_settle)
         self._topics: List[str] = []
         self._tag_topic: Dict[str, int] = {}
@@ -91,7 +92,9 @@ class AmqpSource(Source):
 
     async def _connect(self) -> None:
         conn = Connection(self.url, heartbeat=self.heartbeat, connect_timeout=self.connect_timeout,
-                          logger=self.log, on_lost=self._on_lost)
+                          logger=self.log, on_lost=self._on_lost,
+                          native_settler=self._settler if self.native else None,
+                          on_delivery=self._on_native_delivery if self.native else None)
         await conn.open()
         try:
             ch = await conn.channel()
@@ -99,7 +102,7 @@ class AmqpSource(Source):
             tags = {}
             for t in self._topics:
                 await ch.queue_declare(t, durable=self.durable)
-                tag = await ch.basic_consume(t, self._on_message)
+                tag = await ch.basic_consume(t, self._on_message, native_topic=TOPIC_IDS[t])
                 tags[tag] = TOPIC_IDS[t]
         except BaseException:
             await conn.close()
@@ -111,6 +114,12 @@ class AmqpSource(Source):
     def _on_message(self, ch: Channel, method, props, body: bytes) -> None:
         tid = self._tag_topic.get(method.consumer_tag, 0)
         d = Delivery(body, tid, method.delivery_tag, self._settler, None, method.redelivered, ch)
+        self.delivered += 1
+        self._pending.append(d)
+        if len(self._pending) == 1:
+            self._event.set()
+
+    def _on_native_delivery(self, d) -> None:
         self.delivered += 1
         self._pending.append(d)
         if len(self._pending) == 1:
