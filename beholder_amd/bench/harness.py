@@ -38,7 +38,7 @@ from typing import Dict, List, Optional
 
 from .generator import Workload, bench_config
 
-CONFIGS = ("plumbing", "firehose_1k", "rate_10k", "backpressure", "soak")
+CONFIGS = ("plumbing", "firehose_1k", "rate_10k", "backpressure", "soak", "amqp")
 
 
 def _rss_mb() -> float:
@@ -181,6 +181,8 @@ def run_config(name: str, *, duration_s: Optional[float] = None, events: Optiona
                                                                capacity_events=4096, media=w.media))}
         dn = res["drop_newest"]
         res.update({"offered": dn["offered"], "accepted": dn["accepted"], "dropped": dn["dropped"]})
+    elif name == "amqp":
+        res = _amqp(events or 200_000)
     elif name == "soak":
         n = events or 1_000_000
         gc.collect()
@@ -199,6 +201,60 @@ def run_config(name: str, *, duration_s: Optional[float] = None, events: Optiona
         raise ValueError(f"unknown config {name!r} (one of {', '.join(CONFIGS)})")
     res["config"] = name
     return res
+
+
+def _amqp(n: int) -> dict:
+    """AMQP ingest (the reference's transport): a replay broker process streams n pre-encoded
+    deliveries over TCP; this process runs the service (AmqpSource, prefetch 100, native
+    delivery demux) and acks every message. Measures the consumer side end to end."""
+    import subprocess
+
+    from ..config import Config
+    from ..service import Service
+    from ..sinks import RecordingHttpClient
+    from ..store import MemoryStore
+    from ..transport.amqp import AmqpSource
+    from ..utils.log import Logger
+
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    proc = subprocess.Popen([sys.executable, "-m", "beholder_amd.bench.replay_broker", "--events", str(n)],
+                            stdout=subprocess.PIPE, text=True, env=env, cwd=root)
+    try:
+        line = proc.stdout.readline().split()
+        if not line or line[0] != "READY":
+            raise RuntimeError("replay broker failed to start")
+        port = int(line[1])
+        w = Workload(n_media=10000, seed=0)
+
+        async def go():
+            sink = open(os.devnull, "w", buffering=1 << 16)
+            src = AmqpSource(f"amqp://guest:guest@127.0.0.1:{port}/", prefetch=100)
+            svc = Service(Config.from_dict(bench_config()), source=src, store=MemoryStore(w.media),
+                          http=RecordingHttpClient(keep=8), logger=Logger(stream=sink), serve_metrics=False)
+            await svc.init()
+            t0 = time.perf_counter()
+            task = asyncio.ensure_future(svc.run())
+            while src.settler.acked < n:
+                await asyncio.sleep(0.001)
+            elapsed = time.perf_counter() - t0
+            await asyncio.sleep(0.05)  # let the last acks flush
+            svc.request_stop()
+            await task
+            stats = svc.stats()
+            await svc.close()
+            sink.close()
+            return elapsed, stats
+
+        elapsed, stats = asyncio.run(go())
+        tail = proc.stdout.readline().strip()
+        proc.wait(30)
+    finally:
+        if proc.poll() is None:
+            proc.kill()
+    return {"events": n, "acked": stats["source"]["acked"], "elapsed_s": elapsed, "ingest_rate_eps": n / elapsed,
+            "handle_latency_us": {k: v / 1e3 for k, v in stats["handle_latency_ns"].items() if k.startswith("p")},
+            "broker": tail, "prefetch": 100, "native_demux": True}
 
 
 def _plumbing(w: Workload) -> dict:

@@ -22,6 +22,7 @@ Reliability (amqp-connection-manager parity):
 from __future__ import annotations
 
 import asyncio
+import collections
 import time
 from typing import Dict, List, Optional, Sequence
 
@@ -32,12 +33,81 @@ from .connection import Channel, Connection
 from .wire import AmqpError
 
 
+class _AckCoalescer:
+    """Per-channel ack batching.
+
+    Deliveries on a channel carry increasing delivery tags. Acks issued during
+    one event-loop iteration are flushed together: the longest *contiguous*
+    prefix of settled tags goes out as one ``basic.ack(multiple=true)``, acks
+    above a gap (a still-pending or nacked delivery) go out individually, so
+    nothing is ever delayed past the current iteration (a never-acked Q1
+    message cannot hold other acks back). ``multiple`` only ever covers tags
+    this consumer has already received on the channel, all of them settled.
+    """
+
+    __slots__ = ("ch", "order", "settled", "pending", "scheduled", "frames", "acks")
+
+    def __init__(self, ch: Channel):
+        self.ch = ch
+        self.order = collections.deque()   # tags in arrival order, not yet popped
+        self.settled = set()               # settled tags still inside `order`
+        self.pending: List[int] = []       # acked, not yet sent
+        self.scheduled = False
+        self.frames = 0
+        self.acks = 0
+
+    def seen(self, tag: int) -> None:
+        self.order.append(tag)
+
+    def ack(self, tag: int) -> None:
+        self.settled.add(tag)
+        self.pending.append(tag)
+        self.acks += 1
+        if not self.scheduled:
+            self.scheduled = True
+            asyncio.get_running_loop().call_soon(self.flush)
+
+    def other(self, tag: int) -> None:
+        """A nack/reject was sent immediately: the tag is settled at the broker."""
+        self.settled.add(tag)
+
+    def flush(self) -> None:
+        self.scheduled = False
+        if not self.pending:
+            return
+        ch = self.ch
+        order, settled = self.order, self.settled
+        prefix = 0
+        while order and order[0] in settled:
+            prefix = order.popleft()
+            settled.discard(prefix)
+        if not ch.is_open:
+            self.pending.clear()
+            return
+        top = 0
+        rest = []
+        for t in self.pending:
+            if t <= prefix:
+                if t > top:
+                    top = t
+            else:
+                rest.append(t)
+        self.pending.clear()
+        if top:
+            ch.basic_ack(top, multiple=True)
+            self.frames += 1
+        for t in rest:
+            ch.basic_ack(t)
+            self.frames += 1
+
+
 class AmqpSource(Source):
     kind = "amqp"
 
     def __init__(self, url: str, prefetch: int = 100, retries: int = 2, *, logger=None,
                  durable: bool = True, heartbeat: Optional[int] = None, backoff_initial: float = 0.25,
-                 backoff_max: float = 30.0, connect_timeout: float = 10.0, native: bool = True):
+                 backoff_max: float = 30.0, connect_timeout: float = 10.0, native: bool = True,
+                 coalesce_acks: bool = True):
         self.url = url
         self._prefetch = int(prefetch)
         self.retries = int(retries)
@@ -48,6 +118,8 @@ class AmqpSource(Source):
         self.backoff_max = backoff_max
         self.connect_timeout = connect_timeout
         self.native = native  # assemble deliveries in C (ops.AmqpDemux)
+        self.coalesce_acks = coalesce_acks
+        self._acks: Optional[_AckCoalescer] = None
         self._settler = Settler(on_settle=self._on_settle)
         self._topics: List[str] = []
         self._tag_topic: Dict[str, int] = {}
@@ -108,18 +180,24 @@ class AmqpSource(Source):
             await conn.close()
             raise
         ch.on_close = self._on_channel_close
+        self._acks = _AckCoalescer(ch) if self.coalesce_acks else None
         self._conn, self._ch, self._tag_topic = conn, ch, tags
         self.connected_since = time.time()
 
     def _on_message(self, ch: Channel, method, props, body: bytes) -> None:
         tid = self._tag_topic.get(method.consumer_tag, 0)
         d = Delivery(body, tid, method.delivery_tag, self._settler, None, method.redelivered, ch)
+        if self._acks is not None:
+            self._acks.seen(method.delivery_tag)
         self.delivered += 1
         self._pending.append(d)
         if len(self._pending) == 1:
             self._event.set()
 
     def _on_native_delivery(self, d) -> None:
+        acks = self._acks
+        if acks is not None:
+            acks.seen(d.tag)
         self.delivered += 1
         self._pending.append(d)
         if len(self._pending) == 1:
@@ -130,9 +208,16 @@ class AmqpSource(Source):
         if ch is None or not ch.is_open or ch is not self._ch:
             self.stale_settles += 1  # channel gone: broker already requeued it
             return
+        acks = self._acks
         if kind == "ack":
-            ch.basic_ack(d.tag)
-        elif kind == "nack":
+            if acks is not None:
+                acks.ack(d.tag)
+            else:
+                ch.basic_ack(d.tag)
+            return
+        if acks is not None:
+            acks.other(d.tag)
+        if kind == "nack":
             ch.basic_nack(d.tag, requeue=requeue)
         else:
             ch.basic_reject(d.tag, requeue=requeue)
@@ -177,7 +262,8 @@ class AmqpSource(Source):
         s.update({"connected": self.ready(), "reconnects": self.reconnects, "delivered": self.delivered,
                   "stale_settles": self.stale_settles, "last_error": self.last_error,
                   "bytes_in": c.bytes_in if c else 0, "bytes_out": c.bytes_out if c else 0,
-                  "buffered": len(self._pending)})
+                  "buffered": len(self._pending),
+                  "ack_frames": self._acks.frames if self._acks else None})
         return s
 
     # --------------------------------------------------------- recovery ---

@@ -295,3 +295,37 @@ def test_source_reconnects_after_broker_drop_and_redelivers():
         finally:
             await b.stop()
     run(go())
+
+
+class _FakeCh:
+    def __init__(self):
+        self.is_open = True
+        self.sent = []
+
+    def basic_ack(self, tag, multiple=False):
+        self.sent.append((tag, multiple))
+
+
+def test_ack_coalescer_prefix_gap_and_nack():
+    from beholder_amd.transport.amqp.source import _AckCoalescer
+
+    async def go():
+        ch = _FakeCh()
+        c = _AckCoalescer(ch)
+        for t in range(1, 11):
+            c.seen(t)
+        for t in (1, 2, 3, 5, 6):   # 4 still pending (e.g. a Q1 message that is never acked)
+            c.ack(t)
+        await asyncio.sleep(0)
+        assert ch.sent == [(3, True), (5, False), (6, False)]
+        ch.sent.clear()
+        c.other(4)                  # 4 nacked (sent immediately elsewhere)
+        for t in (7, 8):
+            c.ack(t)
+        await asyncio.sleep(0)
+        assert ch.sent == [(8, True)]  # 4..8 now contiguous; never covers unseen tags 9, 10
+        ch.sent.clear()
+        c.ack(10)
+        await asyncio.sleep(0)
+        assert ch.sent == [(10, False)]  # 9 outstanding -> no multiple
+    run(go())
