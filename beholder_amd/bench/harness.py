@@ -121,7 +121,7 @@ class _Producer(threading.Thread):
 
 
 async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_events: int = 0,
-                      n_media: int = 10000, media=None, log_level: str = "info") -> dict:
+                      n_media: int = 10000, media=None, log_level: str = "info", rss_probe=None) -> dict:
     from ..config import Config
     from ..service import Service
     from ..sinks import RecordingHttpClient
@@ -138,11 +138,16 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
                   logger=Logger(stream=sink, level=log_level), serve_metrics=False)
     await svc.init()
     prod = _Producer(wfd, events, rate)
+    if rss_probe is not None:
+        gc.collect()
+        rss_probe.append(_rss_mb())  # service initialised, workload already in memory
     t0 = time.perf_counter()
     prod.start()
     stats = await svc.run()
     elapsed = time.perf_counter() - t0
     prod.join()
+    if rss_probe is not None:
+        rss_probe.append(_rss_mb())  # after 1M events, before teardown
     await svc.close()
     sink.close()
     s = stats["source"]
@@ -185,16 +190,15 @@ def run_config(name: str, *, duration_s: Optional[float] = None, events: Optiona
         res = _amqp(events or 200_000)
     elif name == "soak":
         n = events or 1_000_000
-        gc.collect()
-        rss0 = _rss_mb()
         evs = w.events(n)
+        probe: list = []
         with GcPauses() as g:
-            res = asyncio.run(_run_inproc(evs, 0, media=w.media))
-        del evs
-        gc.collect()
-        res["rss_start_mb"] = rss0
-        res["rss_end_mb"] = _rss_mb()
-        res["rss_growth_mb"] = res["rss_end_mb"] - rss0
+            res = asyncio.run(_run_inproc(evs, 0, media=w.media, rss_probe=probe))
+        # RSS of the service itself: measured after init with the workload already generated,
+        # and again after all n events went through (so the workload's own memory is excluded)
+        res["rss_start_mb"] = probe[0]
+        res["rss_end_mb"] = probe[1]
+        res["rss_growth_mb"] = probe[1] - probe[0]
         res["rss_peak_mb"] = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024
         res["gc_pauses"] = g.summary()
     else:

@@ -53,4 +53,4 @@ def test_soak_1m_events_rss_and_gc():
     from beholder_amd.bench import harness
     res = harness.run_config("soak", events=1_000_000)
     assert res["acked"] == 1_000_000
-    assert res["rss_growth_mb"] < 512, res
+    assert res["rss_growth_mb"] < 64, res  # the service itself must not grow with traffic
