@@ -242,9 +242,11 @@ class Service:
         return self._initialized and not self._stop and (self._source is None or self._source.ready())
 
     def request_stop(self) -> None:
+        """Graceful stop: stop consuming, let in-flight handlers finish and ack, then return
+        from :meth:`run` (the caller closes the source/store afterwards)."""
         self._stop = True
         if self._source is not None:
-            asyncio.ensure_future(self._source.close())
+            asyncio.ensure_future(self._source.stop_consuming())
 
     async def run(self) -> Dict[str, Any]:
         """Consume until the source ends or :meth:`request_stop`; then drain and return stats."""

@@ -128,6 +128,7 @@ class AmqpSource(Source):
         self._pending: List = []
         self._event: Optional[asyncio.Event] = None
         self._closing = False
+        self._stopping = False
         self._reconnect_task: Optional[asyncio.Task] = None
         self.reconnects = 0
         self.delivered = 0
@@ -228,10 +229,28 @@ class AmqpSource(Source):
                 batch, self._pending = self._pending, []
                 yield batch
                 continue
-            if self._closing:
+            if self._closing or self._stopping:
                 return
             self._event.clear()
             await self._event.wait()
+
+    async def stop_consuming(self) -> None:
+        """``basic.cancel`` every consumer; the channel stays open so acks of in-flight
+        handlers still reach the broker (no redelivery of work already done)."""
+        if self._stopping or self._closing:
+            return
+        self._stopping = True
+        if self._reconnect_task is not None:
+            self._reconnect_task.cancel()
+        ch = self._ch
+        if ch is not None and ch.is_open:
+            for tag in list(self._tag_topic):
+                try:
+                    await asyncio.wait_for(ch.basic_cancel(tag), 5)
+                except (AmqpError, asyncio.TimeoutError, ConnectionError):
+                    break
+        if self._event is not None:
+            self._event.set()
 
     async def close(self) -> None:
         if self._closing:
@@ -240,13 +259,16 @@ class AmqpSource(Source):
         if self._reconnect_task is not None:
             self._reconnect_task.cancel()
         ch, conn = self._ch, self._conn
+        if self._acks is not None:
+            self._acks.flush()  # acks of the last handlers go out before the channel closes
         self._ch = None
         if ch is not None and ch.is_open:
-            for tag in list(self._tag_topic):
-                try:
-                    await asyncio.wait_for(ch.basic_cancel(tag), 5)
-                except (AmqpError, asyncio.TimeoutError, ConnectionError):
-                    break
+            if not self._stopping:
+                for tag in list(self._tag_topic):
+                    try:
+                        await asyncio.wait_for(ch.basic_cancel(tag), 5)
+                    except (AmqpError, asyncio.TimeoutError, ConnectionError):
+                        break
             await ch.close()
         if conn is not None:
             await conn.close()

@@ -40,6 +40,12 @@ class Source(abc.ABC):
     async def close(self) -> None:
         """Stop delivering; un-acked deliveries follow the transport's redelivery rules."""
 
+    async def stop_consuming(self) -> None:
+        """Graceful-shutdown step 1: deliver nothing new, but keep settlement working so
+        in-flight handlers can still ack; :meth:`batches` ends once buffered deliveries are
+        handed out. Default: same as :meth:`close`."""
+        await self.close()
+
     @property
     def settler(self):
         """The native Settler shared by this source's deliveries (ack accounting/latency)."""

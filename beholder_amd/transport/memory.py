@@ -108,6 +108,7 @@ class MemoryConsumer(Source):
         self._tags = itertools.count(1)
         self._event: Optional[asyncio.Event] = None
         self._closed = False
+        self._stopping = False
         self._settler = Settler(on_settle=self._on_settle)
         self.delivered = 0
 
@@ -156,7 +157,7 @@ class MemoryConsumer(Source):
         return out
 
     async def batches(self):
-        while not self._closed:
+        while not self._closed and not self._stopping:
             got = self._take()
             if got:
                 yield got
@@ -180,6 +181,11 @@ class MemoryConsumer(Source):
                 self.broker._requeue_front(q, body)
             else:
                 q.dead_lettered += 1
+        self._wake()
+
+    async def stop_consuming(self) -> None:
+        """Take nothing new; un-acked deliveries can still be settled until :meth:`close`."""
+        self._stopping = True
         self._wake()
 
     @property

@@ -189,10 +189,11 @@ def test_graceful_stop_drains_inflight():
         svc.request_stop()
         await task
         await svc.close()
-        return src
-    src = run(go())
+        return src, b
+    src, b = run(go())
     st = src.settler.stats()
     assert st["acked"] == 5 and st["pending"] == 0
+    assert b.depth(PROGRESS) == 0 and src.unacked == 0  # nothing requeued: the acks landed
 
 
 def test_metrics_http_endpoint():
@@ -249,3 +250,28 @@ def test_amqp_end_to_end_service():
     sp, ss, http = run(go())
     assert sp["acked"] == 20 and ss["acked"] == 1 and sp["unacked"] == 0
     assert http.count == 20 + 3  # 20 comments + move + telegram + emby
+
+
+def test_graceful_stop_over_amqp_acks_inflight_not_redelivered():
+    """SIGTERM during slow handlers: consumers are cancelled first, in-flight handlers finish and
+    their acks reach the broker, nothing is redelivered."""
+    async def go():
+        broker = await AmqpBroker().start()
+        try:
+            http = SlowHttp(0.05)
+            svc = make_service(AmqpSource(broker.url, prefetch=10), [trello_media("m1")], http=http)
+            await svc.init()
+            task = asyncio.ensure_future(svc.run())
+            for p in range(30):
+                broker.publish(PROGRESS, progress_msg("m1", "QUEUED", p))
+            await asyncio.sleep(0.02)  # some handlers are mid-request
+            svc.request_stop()
+            await task
+            await svc.close()
+            await asyncio.sleep(0.05)
+            return broker.stats(PROGRESS), http.count
+        finally:
+            await broker.stop()
+    st, calls = run(go())
+    assert st["requeued"] == 0  # nothing that was handled comes back
+    assert st["acked"] == calls and st["acked"] + st["depth"] == 30 and st["unacked"] == 0
