@@ -38,7 +38,7 @@ from .handlers import TelemetryHandlers, err_message
 from .metrics import MetricsServer, NativeHistogramView, Registry, default_metrics
 from .metrics.registry import Gauge
 from .parallel.ordering import KeyedSerializer
-from .sinks import AiohttpClient, EmbyClient, HttpClient, TelegramClient, TrelloClient
+from .sinks import AiohttpClient, EmbyClient, HttpClient, SinkObserver, TelegramClient, TrelloClient
 from .store import MediaStore, open_store
 from .transport.base import Source
 from .utils.eager import DONE, ERROR, run_eager
@@ -125,14 +125,16 @@ class Service:
         if self._http is None:
             self._http = AiohttpClient(timeout_s=float(svc["http"]["timeout_s"]))
         endpoints = svc["endpoints"]
-        self.trello = TrelloClient(keys.get("key"), keys.get("token"), self._http, base_url=endpoints["trello"])
-        self.telegram = TelegramClient(None, self._http, base_url=endpoints["telegram"])
-        self.emby = EmbyClient(None, None, self._http)
-
         # 3-4. registry + counters (index.js:27-40)
         if self.registry is None:
             self.registry = Registry("beholder")
         reg = self.registry
+        observer = SinkObserver(reg) if svc["metrics"].get("sink_metrics", True) else None
+        self.trello = TrelloClient(keys.get("key"), keys.get("token"), self._http, base_url=endpoints["trello"],
+                                   observer=observer)
+        self.telegram = TelegramClient(None, self._http, base_url=endpoints["telegram"], observer=observer)
+        self.emby = EmbyClient(None, None, self._http, observer=observer)
+
         self.progress_updates_total = reg.counter(
             "beholder_progress_updates_total", "Total number of messages processed in this processes lifetime",
             ["status"])
@@ -304,6 +306,7 @@ class Service:
             return
         if kind == ERROR:
             self._on_handler_error(d, val)
+            val = None  # the traceback reaches this frame via f_back: don't keep a cycle alive
             if on_finish is not None:
                 on_finish()
             return
@@ -333,6 +336,9 @@ class Service:
         self.handler_errors.labels(topic).inc()
         # Node would print an UnhandledPromiseRejectionWarning here (index.js:62 has no catch).
         self.log.error(f"unhandled error in {topic} handler: {err_message(exc)}")
+        # Drop the traceback: it references the handler frame (and so the delivery). Freeing it
+        # promptly lets an un-acked delivery be reported as abandoned right away (Q1 accounting).
+        exc.__traceback__ = None
         if d.settled:
             return
         policy = self.on_status_error

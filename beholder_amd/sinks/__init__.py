@@ -1,6 +1,6 @@
 """Side-effect sinks (L2 of SURVEY.md §1): Trello, Telegram, Emby over a pluggable HTTP client."""
 from .http import (AiohttpClient, HttpClient, HttpError, HttpResponse, RecordingHttpClient,  # noqa: F401
-                   TimedHttpClient, encode_query, parse_query, with_query)
+                   SinkObserver, encode_query, observed, parse_query, redact, with_query)
 from .trello import COMMENT_FALLBACK, TrelloClient  # noqa: F401
 from .telegram import TelegramClient, deployed_text  # noqa: F401
 from .emby import EmbyClient  # noqa: F401

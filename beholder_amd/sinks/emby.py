@@ -3,20 +3,23 @@ from __future__ import annotations
 
 from typing import Any, Optional
 
-from .http import HttpClient, HttpResponse
+from .http import HttpClient, HttpResponse, observed
 from ..utils.log import js_str
 
 
 class EmbyClient:
-    def __init__(self, host: Optional[str], api_key: Optional[str], http: HttpClient, timeout: Optional[float] = None):
+    def __init__(self, host: Optional[str], api_key: Optional[str], http: HttpClient, timeout: Optional[float] = None,
+                 observer=None):
         self.host = host
         self.api_key = api_key
         self.http = http
         self.timeout = timeout
+        self.observer = observer
 
     async def refresh_library(self, host: Any = ..., api_key: Any = ...) -> HttpResponse:
         h = self.host if host is ... else host
         k = self.api_key if api_key is ... else api_key
         url = f"{js_str(h)}/emby/library/refresh"
-        r = await self.http.request("GET", url, params={"api_key": k}, timeout=self.timeout)
+        r = await observed(self.observer, "emby", self.http.request("GET", url, params={"api_key": k},
+                                                                    timeout=self.timeout))
         return r.raise_for_status()

@@ -19,6 +19,7 @@ import abc
 import asyncio
 import collections
 import json as _json
+import re
 import time
 from typing import Any, Callable, Deque, Dict, List, Mapping, Optional, Tuple
 from urllib.parse import quote
@@ -60,6 +61,14 @@ def with_query(url: str, params: Optional[Mapping[str, Any]]) -> str:
     if not q:
         return url
     return url + ("&" if "?" in url else "?") + q
+
+
+_BOT_TOKEN = re.compile(r"/bot[^/?#]+")
+
+
+def redact(url: str) -> str:
+    """URL safe for logs: no query string (Trello key/token ride there), no Telegram bot token."""
+    return _BOT_TOKEN.sub("/bot***", url.split("?", 1)[0])
 
 
 class HttpError(Exception):
@@ -137,9 +146,12 @@ class AiohttpClient(HttpClient):
                 body = await r.read()
                 return HttpResponse(r.status, body, dict(r.headers), full)
         except asyncio.TimeoutError as e:
-            raise HttpError(f"ETIMEDOUT: {method.upper()} {url}") from e
+            raise HttpError(f"ETIMEDOUT: {method.upper()} {redact(url)}") from e
         except aiohttp.ClientError as e:
-            raise HttpError(f"{type(e).__name__}: {e}") from e
+            msg = str(e)
+            if full in msg or url in msg:
+                msg = msg.replace(full, redact(full)).replace(url, redact(url))
+            raise HttpError(f"{type(e).__name__}: {_BOT_TOKEN.sub('/bot***', msg)}") from e
 
     async def close(self) -> None:
         if self._session is not None and not self._session.closed:
@@ -197,25 +209,39 @@ class RecordingHttpClient(HttpClient):
         return [u for m, u in self.calls if method is None or m == method.upper()]
 
 
-class TimedHttpClient(HttpClient):
-    """Wraps a client and feeds per-sink request metrics (count by code, latency)."""
+class SinkObserver:
+    """Per-sink request accounting: ``beholder_sink_requests_total{sink,code}`` and
+    ``beholder_sink_request_seconds{sink}`` (``code`` = HTTP status or ``error``)."""
 
-    def __init__(self, inner: HttpClient, on_result: Callable[[str, Optional[int], float], None]):
-        self.inner = inner
-        self.on_result = on_result
+    def __init__(self, registry):
+        self.requests = registry.counter("beholder_sink_requests_total",
+                                         "Outbound sink requests by sink and HTTP status (error = transport failure)",
+                                         ["sink", "code"])
+        self.seconds = registry.histogram("beholder_sink_request_seconds", "Outbound sink request duration",
+                                          ["sink"], buckets=(0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1, 2.5, 5, 10))
+        self._children = {}
 
-    async def request(self, method, url, *, params=None, timeout=None) -> HttpResponse:
-        t0 = time.perf_counter()
-        try:
-            r = await self.inner.request(method, url, params=params, timeout=timeout)
-        except Exception:
-            self.on_result(url, None, time.perf_counter() - t0)
-            raise
-        self.on_result(url, r.status, time.perf_counter() - t0)
-        return r
+    def __call__(self, sink: str, status: Optional[int], seconds: float) -> None:
+        key = (sink, status)
+        c = self._children.get(key)
+        if c is None:
+            c = self._children[key] = self.requests.labels(sink, "error" if status is None else str(status))
+        c.inc()
+        self.seconds.observe({"sink": sink}, seconds)
 
-    async def close(self) -> None:
-        await self.inner.close()
+
+async def observed(observer, sink: str, coro):
+    """Await an HTTP request coroutine, reporting (sink, status|None, seconds) to ``observer``."""
+    if observer is None:
+        return await coro
+    t0 = time.perf_counter()
+    try:
+        r = await coro
+    except Exception:
+        observer(sink, None, time.perf_counter() - t0)
+        raise
+    observer(sink, r.status, time.perf_counter() - t0)
+    return r
 
 
 def parse_query(url: str) -> Dict[str, str]:

@@ -3,7 +3,7 @@ from __future__ import annotations
 
 from typing import Any, Optional
 
-from .http import HttpClient, HttpResponse
+from .http import HttpClient, HttpResponse, observed
 from ..utils.log import js_str
 
 
@@ -14,17 +14,19 @@ def deployed_text(name: Any, metadata_id: Any) -> str:
 
 class TelegramClient:
     def __init__(self, token: Optional[str], http: HttpClient, base_url: str = "https://api.telegram.org",
-                 timeout: Optional[float] = None):
+                 timeout: Optional[float] = None, observer=None):
         self.token = token
         self.http = http
         self.base_url = base_url.rstrip("/")
         self.timeout = timeout
+        self.observer = observer
 
     async def send_message(self, chat_id: Any, text: str, parse_mode: str = "markdown",
                            token: Any = ...) -> HttpResponse:
         # `bot${token}` — an undefined token renders as "botundefined" in the reference
         tok = self.token if token is ... else token
         url = f"{self.base_url}/bot{js_str(tok)}/sendMessage"
-        r = await self.http.request("GET", url, params={"chat_id": chat_id, "text": text, "parse_mode": parse_mode},
-                                    timeout=self.timeout)
+        r = await observed(self.observer, "telegram",
+                           self.http.request("GET", url, params={"chat_id": chat_id, "text": text,
+                                                                 "parse_mode": parse_mode}, timeout=self.timeout))
         return r.raise_for_status()  # request-promise: reject on non-2xx

@@ -15,7 +15,7 @@ from __future__ import annotations
 
 from typing import Any, Mapping, Optional
 
-from .http import HttpClient, HttpError, HttpResponse
+from .http import HttpClient, HttpError, HttpResponse, observed
 
 COMMENT_FALLBACK = "Failed to retrieve comment text."  # index.js:54
 
@@ -24,13 +24,15 @@ _METHODS = {"get": "GET", "post": "POST", "put": "PUT", "delete": "DELETE"}
 
 class TrelloClient:
     def __init__(self, key: Optional[str], token: Optional[str], http: HttpClient,
-                 base_url: str = "https://api.trello.com", strict: bool = False, timeout: Optional[float] = None):
+                 base_url: str = "https://api.trello.com", strict: bool = False, timeout: Optional[float] = None,
+                 observer=None):
         self.key = key
         self.token = token
         self.http = http
         self.base_url = base_url.rstrip("/")
         self.strict = strict
         self.timeout = timeout
+        self.observer = observer
 
     def create_query(self) -> dict:
         return {"key": self.key, "token": self.token}
@@ -45,7 +47,8 @@ class TrelloClient:
         query = {"key": self.key, "token": self.token}
         if options:
             query.update(options)
-        r = await self.http.request(m, self.base_url + path, params=query, timeout=self.timeout)
+        req = self.http.request(m, self.base_url + path, params=query, timeout=self.timeout)
+        r = await (observed(self.observer, "trello", req) if self.observer is not None else req)
         if self.strict:
             r.raise_for_status()
         return r

@@ -114,9 +114,13 @@ class FdSource(Source):
         if self._dl_path is None:
             return
         with self._dl_lock:
-            if self._dl_file is None:
-                self._dl_file = open(self._dl_path, "ab")
-            self._dl_file.write(frame(topic_id, content))
+            if self._closed:  # after close(): append and flush immediately
+                with open(self._dl_path, "ab") as f:
+                    f.write(frame(topic_id, content))
+            else:
+                if self._dl_file is None:
+                    self._dl_file = open(self._dl_path, "ab")
+                self._dl_file.write(frame(topic_id, content))
             self.abandoned_frames += 1
 
 

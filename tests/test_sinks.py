@@ -1,0 +1,117 @@
+"""Trello / Telegram / Emby sinks over real HTTP (aiohttp -> local fake server).
+
+Pins the outbound contract of SURVEY.md §2.4: methods, paths, query parameters,
+and the error semantics of the two reference HTTP libraries.
+"""
+import asyncio
+
+import pytest
+
+from beholder_amd.bench.fakes import FakeHttpServer
+from beholder_amd.metrics import Registry, parse_exposition
+from beholder_amd.sinks import (AiohttpClient, EmbyClient, HttpError, SinkObserver, TelegramClient, TrelloClient,
+                                deployed_text, redact)
+
+
+def run(coro):
+    return asyncio.run(asyncio.wait_for(coro, 30))
+
+
+@pytest.fixture
+def server():
+    with FakeHttpServer() as s:
+        yield s
+
+
+def test_trello_comment_and_move_over_http(server):
+    async def go():
+        http = AiohttpClient(timeout_s=5)
+        t = TrelloClient("KEY", "TOK", http, base_url=server.url)
+        await t.make_request("post", "/1/cards/C1/actions/comments", {"text": "DEPLOYED: Progress **5%** (_h_)"})
+        await t.make_request("put", "/1/cards/C1", {"idList": "L9", "pos": 2})
+        await http.close()
+    run(go())
+    assert server.requests == [
+        ("POST", "/1/cards/C1/actions/comments", {"key": "KEY", "token": "TOK",
+                                                  "text": "DEPLOYED: Progress **5%** (_h_)"}),
+        ("PUT", "/1/cards/C1", {"key": "KEY", "token": "TOK", "idList": "L9", "pos": "2"}),
+    ]
+
+
+def test_trello_resolves_on_http_error_status(server):
+    """trello npm only rejects on transport errors (index.js:83 move failures surface only then)."""
+    server.status_for["/1/cards"] = 401
+
+    async def go():
+        http = AiohttpClient(timeout_s=5)
+        r = await TrelloClient("k", "t", http, base_url=server.url).make_request("put", "/1/cards/x", {"pos": 2})
+        strict = TrelloClient("k", "t", http, base_url=server.url, strict=True)
+        with pytest.raises(HttpError):
+            await strict.make_request("put", "/1/cards/x", {})
+        await http.close()
+        return r.status
+    assert run(go()) == 401
+
+
+def test_telegram_and_emby_over_http(server):
+    async def go():
+        http = AiohttpClient(timeout_s=5)
+        await TelegramClient("123:ABC", http, base_url=server.url).send_message(
+            "-100", deployed_text("Bebop", "1"), "markdown")
+        await EmbyClient(server.url, "EK", http).refresh_library()
+        await http.close()
+    run(go())
+    assert server.requests == [
+        ("GET", "/bot123:ABC/sendMessage", {"chat_id": "-100", "parse_mode": "markdown",
+                                            "text": "*New Anime:* Bebop\nKitsu: https://kitsu.io/anime/1"}),
+        ("GET", "/emby/library/refresh", {"api_key": "EK"}),
+    ]
+
+
+def test_request_promise_semantics_reject_non_2xx(server):
+    server.status_for["/emby"] = 500
+
+    async def go():
+        http = AiohttpClient(timeout_s=5)
+        with pytest.raises(HttpError) as ei:
+            await EmbyClient(server.url, "k", http).refresh_library()
+        await http.close()
+        return ei.value
+    e = run(go())
+    assert e.status == 500 and str(e).startswith("500 - ")
+
+
+def test_transport_errors_never_leak_tokens():
+    async def go():
+        http = AiohttpClient(timeout_s=0.5)
+        with pytest.raises(HttpError) as ei:
+            await TelegramClient("SECRET:TOKEN", http, base_url="http://127.0.0.1:9").send_message("c", "t")
+        with pytest.raises(HttpError) as ej:
+            await TrelloClient("SECRETKEY", "SECRETTOK", http, base_url="http://127.0.0.1:9").make_request(
+                "post", "/1/cards/x/actions/comments", {"text": "x"})
+        await http.close()
+        return str(ei.value) + str(ej.value)
+    msg = run(go())
+    assert "SECRET" not in msg
+    assert redact("https://api.telegram.org/bot1:AB/sendMessage?chat_id=1") == "https://api.telegram.org/bot***/sendMessage"
+
+
+def test_sink_metrics(server):
+    server.status_for["/emby"] = 503
+
+    async def go():
+        reg = Registry()
+        obs = SinkObserver(reg)
+        http = AiohttpClient(timeout_s=5)
+        await TrelloClient("k", "t", http, base_url=server.url, observer=obs).make_request("put", "/1/cards/a", {})
+        with pytest.raises(HttpError):
+            await EmbyClient(server.url, "k", http, observer=obs).refresh_library()
+        with pytest.raises(HttpError):
+            await EmbyClient("http://127.0.0.1:9", "k", AiohttpClient(timeout_s=0.5), observer=obs).refresh_library()
+        await http.close()
+        return parse_exposition(reg.render())
+    m = run(go())
+    assert m['beholder_sink_requests_total{sink="trello",code="200"}'] == 1
+    assert m['beholder_sink_requests_total{sink="emby",code="503"}'] == 1
+    assert m['beholder_sink_requests_total{sink="emby",code="error"}'] == 1
+    assert m['beholder_sink_request_seconds_count{sink="trello"}'] == 1
