@@ -16,7 +16,10 @@ import runpy  # noqa: E402
 
 prof = cProfile.Profile()
 prof.enable()
-runpy.run_path(os.path.join(ROOT, "bench.py"), run_name="__main__")
+try:
+    runpy.run_path(os.path.join(ROOT, "bench.py"), run_name="__main__")
+except SystemExit:
+    pass
 prof.disable()
 s = io.StringIO()
 pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(40)
