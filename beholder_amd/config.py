@@ -62,6 +62,8 @@ SERVICE_DEFAULTS: dict = {
         "shutdown_grace_s": 10.0,
         # gc.freeze() after init: long-lived startup objects leave the collected generations
         "gc_freeze": True,
+        # per-message trace span at debug level (needs log.level: debug)
+        "trace": False,
     }
 }
 

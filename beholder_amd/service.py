@@ -94,6 +94,8 @@ class Service:
         self.on_status_error = svc["on_status_error"]
         self.ordering = svc["ordering"]
         self.grace_s = float(svc["shutdown_grace_s"])
+        # per-message trace spans (SURVEY.md §5 tracing): one debug line per handled delivery
+        self.trace = bool(svc.get("trace", False))
         self._routes: List[Optional[Handler]] = [None] * len(T.TOPIC_NAMES_BY_ID)
         self._inflight: set = set()
         self._slot_free: Optional[asyncio.Event] = None
@@ -296,7 +298,20 @@ class Service:
         except asyncio.CancelledError:
             pass
 
+    def _span(self, d, outcome: str) -> None:
+        now = time.monotonic_ns()
+        self.log.debug({"span": d.topic, "tag": d.tag, "queue_us": (d.start_ns - d.recv_ns) // 1000,
+                        "handle_us": (now - d.start_ns) // 1000, "outcome": outcome, "state": d.state},
+                       "handled")
+
     def _dispatch_now(self, d, on_finish: Optional[Callable[[], None]] = None) -> None:
+        if self.trace:
+            user_finish = on_finish
+
+            def on_finish(d=d, user_finish=user_finish):
+                self._span(d, "ok" if d.settled else "unsettled")
+                if user_finish is not None:
+                    user_finish()
         handler = self._routes[d.topic_id]
         d.start()
         kind, val = run_eager(handler(d))

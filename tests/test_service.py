@@ -275,3 +275,23 @@ def test_graceful_stop_over_amqp_acks_inflight_not_redelivered():
     st, calls = run(go())
     assert st["requeued"] == 0  # nothing that was handled comes back
     assert st["acked"] == calls and st["acked"] + st["depth"] == 30 and st["unacked"] == 0
+
+
+def test_trace_spans():
+    async def go():
+        b = MemoryBroker()
+        stream = MemoryStream()
+        c = cfg({"service": {"trace": True}})
+        svc = Service(c, source=b.consumer(), store=MemoryStore([trello_media("m1")]), http=RecordingHttpClient(),
+                      logger=Logger(stream=stream, level="debug"), serve_metrics=False)
+        await svc.init()
+        b.publish(PROGRESS, progress_msg("m1", "QUEUED", 1))
+        b.publish(STATUS, b"\x0a\x05ab")
+        b.finish()
+        await svc.run()
+        await svc.close()
+        return [r for r in stream.records() if r.get("msg") == "handled"]
+    spans = run(go())
+    assert sorted((s["span"], s["outcome"], s["state"]) for s in spans) == [
+        (PROGRESS, "ok", "acked"), (STATUS, "unsettled", "pending")]
+    assert all(s["handle_us"] >= 0 and s["queue_us"] >= 0 for s in spans)
