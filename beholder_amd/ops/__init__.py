@@ -61,6 +61,7 @@ Settler = native.Settler
 Counter = native.Counter
 Histogram = native.Histogram
 AmqpDemux = native.AmqpDemux
+dispatch_batch = native.dispatch_batch
 frame = native.frame
 frames = native.frames
 mono_ns = native.mono_ns

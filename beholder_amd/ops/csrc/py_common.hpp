@@ -70,5 +70,6 @@ int init_metric_types(PyObject* m);
 int init_ingest_types(PyObject* m);
 int init_text_functions(PyObject* m);
 int init_amqp_types(PyObject* m);
+int init_dispatch_functions(PyObject* m);
 
 }  // namespace beholder

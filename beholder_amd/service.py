@@ -27,8 +27,10 @@ matching the broker's prefetch window.
 """
 from __future__ import annotations
 
+import array
 import asyncio
 import gc
+import os
 import time
 from typing import Any, Callable, Dict, List, Optional
 
@@ -41,7 +43,8 @@ from .parallel.ordering import KeyedSerializer
 from .sinks import AiohttpClient, EmbyClient, HttpClient, SinkObserver, TelegramClient, TrelloClient
 from .store import MediaStore, open_store
 from .transport.base import Source
-from .utils.eager import DONE, ERROR, run_eager
+from .ops import dispatch_batch
+from .utils.eager import DONE, ERROR, _drive, run_eager
 from .utils.log import Logger
 
 Handler = Callable[[Any], Any]
@@ -105,7 +108,7 @@ class Service:
         self.handlers: Optional[TelemetryHandlers] = None
         self.serializer: Optional[KeyedSerializer] = None
         self.started_at = 0.0
-        self.received = [0] * len(T.TOPIC_NAMES_BY_ID)
+        self.received = array.array("Q", [0] * len(T.TOPIC_NAMES_BY_ID))
 
     # ------------------------------------------------------------ properties --
     @property
@@ -267,17 +270,31 @@ class Service:
         inflight = self._inflight
         prefetch = self.prefetch
         sleep = asyncio.sleep
+        # native fast path: the per-delivery loop runs in C (ops.dispatch_batch); per-media
+        # ordering and trace spans keep the Python loop
+        native = (self.serializer is None and not self.trace
+                  and os.environ.get("BEHOLDER_NATIVE_DISPATCH", "1") != "0")
+        native_dispatch = dispatch_batch
+        routes = tuple(routes)
+        on_error, on_suspend, on_unroutable = self._on_handler_error, self._on_suspend, self._unroutable
         try:
             async for batch in self.source.batches():
-                for d in batch:
-                    tid = d.topic_id
-                    if tid >= nroutes or routes[tid] is None:
-                        self._unroutable(d)
-                        continue
-                    received[tid] += 1
-                    dispatch(d)
-                    if inflight and len(inflight) >= prefetch:
-                        await self._wait_slots()  # at most `prefetch` handlers suspended (index.js:43)
+                if native:
+                    i, n = 0, len(batch)
+                    while i < n:
+                        i = native_dispatch(batch, i, routes, received, on_error, on_suspend, on_unroutable)
+                        if i < n or len(inflight) >= prefetch:
+                            await self._wait_slots()  # at most `prefetch` handlers suspended (index.js:43)
+                else:
+                    for d in batch:
+                        tid = d.topic_id
+                        if tid >= nroutes or routes[tid] is None:
+                            self._unroutable(d)
+                            continue
+                        received[tid] += 1
+                        dispatch(d)
+                        if inflight and len(inflight) >= prefetch:
+                            await self._wait_slots()
                 log.flush()
                 if self._stop:
                     break
@@ -340,6 +357,23 @@ class Service:
                 self._slot_free.set()
 
         task.add_done_callback(_done)
+
+    def _on_suspend(self, d, coro, first_yield) -> bool:
+        """A handler awaited real I/O: continue it in a Task; True = prefetch window full."""
+        task = asyncio.get_running_loop().create_task(_drive(coro, first_yield))
+        self._inflight.add(task)
+
+        def _done(t, d=d):
+            self._inflight.discard(t)
+            if not t.cancelled():
+                exc = t.exception()
+                if exc is not None:
+                    self._on_handler_error(d, exc)
+            if self._slot_free is not None and len(self._inflight) < self.prefetch:
+                self._slot_free.set()
+
+        task.add_done_callback(_done)
+        return len(self._inflight) >= self.prefetch
 
     async def _wait_slots(self) -> None:
         while len(self._inflight) >= self.prefetch:
