@@ -99,6 +99,9 @@ class TelemetryHandlers:
         self.emby = emby
         self.progress_counter = progress_counter
         self.comments_counter = comments_counter
+        # hot-path handle (native counter) when the registry provides one
+        self._comment_inc = comments_counter.child().inc if hasattr(comments_counter, "child") else \
+            comments_counter.inc
         self.log = logger
         self.no_trello = config.no_trello if no_trello is None else bool(no_trello)
 
@@ -157,7 +160,7 @@ class TelemetryHandlers:
         self.log.info("creating comment on", card_id, "with text:", text)
         await self.trello.make_request("post", f"/1/cards/{js_str(card_id)}/actions/comments",
                                        {"text": text or COMMENT_FALLBACK})
-        self.comments_counter.inc()
+        self._comment_inc()
 
     # ----------------------------------------------------------------- C10 ---
     async def on_status(self, rmsg) -> Any:

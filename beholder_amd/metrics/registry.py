@@ -123,6 +123,12 @@ class Counter(Metric):
                     self._children[key] = c
         return c
 
+    def child(self) -> _NativeCounter:
+        """The native counter behind an unlabelled metric (hot-path handle)."""
+        if self.label_names:
+            raise ValueError(f"{self.name} has labels; use labels()/child_for()")
+        return self._children[()]
+
     def child_for(self, value: str) -> _NativeCounter:
         """Fast path for single-label counters (``progress_updates_total{status}``)."""
         c = self._by_value.get(value)
@@ -227,6 +233,16 @@ class Histogram(Metric):
         d[1] += value
         d[2] += 1
 
+    def labels(self, *values) -> "_HistogramChild":
+        """Pre-resolved per-labelset observer (hot path: no label-dict handling per call)."""
+        key = tuple(str(v) for v in values) if values else ()
+        if len(key) != len(self.label_names):
+            raise ValueError(f"{self.name} expects {len(self.label_names)} label values")
+        d = self._data.get(key)
+        if d is None:
+            d = self._data.setdefault(key, [[0] * len(self.buckets), 0.0, 0])
+        return _HistogramChild(self.buckets, d)
+
     def samples(self) -> List[str]:
         out = []
         for k, (counts, total, n) in list(self._data.items()):
@@ -238,6 +254,23 @@ class Histogram(Metric):
             out.append(f"{self.name}_sum{_label_str(self.label_names, k)} {fmt_value(total)}")
             out.append(f"{self.name}_count{_label_str(self.label_names, k)} {n}")
         return out
+
+
+class _HistogramChild:
+    __slots__ = ("_buckets", "_d", "_nb")
+
+    def __init__(self, buckets, d):
+        self._buckets = buckets
+        self._d = d
+        self._nb = len(buckets)
+
+    def observe(self, value: float) -> None:
+        d = self._d
+        i = bisect.bisect_left(self._buckets, value)
+        if i < self._nb:
+            d[0][i] += 1
+        d[1] += value
+        d[2] += 1
 
 
 class NativeHistogramView(Metric):

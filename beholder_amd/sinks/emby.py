@@ -14,12 +14,12 @@ class EmbyClient:
         self.api_key = api_key
         self.http = http
         self.timeout = timeout
-        self.observer = observer
+        self.stats = observer.child("emby") if observer is not None else None
 
     async def refresh_library(self, host: Any = ..., api_key: Any = ...) -> HttpResponse:
         h = self.host if host is ... else host
         k = self.api_key if api_key is ... else api_key
         url = f"{js_str(h)}/emby/library/refresh"
-        r = await observed(self.observer, "emby", self.http.request("GET", url, params={"api_key": k},
+        r = await observed(self.stats, self.http.request("GET", url, params={"api_key": k},
                                                                     timeout=self.timeout))
         return r.raise_for_status()

@@ -219,28 +219,45 @@ class SinkObserver:
                                          ["sink", "code"])
         self.seconds = registry.histogram("beholder_sink_request_seconds", "Outbound sink request duration",
                                           ["sink"], buckets=(0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1, 2.5, 5, 10))
-        self._children = {}
+
+    def child(self, sink: str) -> "SinkStats":
+        return SinkStats(self, sink)
 
     def __call__(self, sink: str, status: Optional[int], seconds: float) -> None:
-        key = (sink, status)
-        c = self._children.get(key)
+        self.child(sink).record(status, seconds)
+
+
+class SinkStats:
+    """Hot-path handle for one sink: native counter per status code + histogram child."""
+
+    __slots__ = ("_obs", "_sink", "_codes", "_hist")
+
+    def __init__(self, obs: SinkObserver, sink: str):
+        self._obs = obs
+        self._sink = sink
+        self._codes = {}
+        self._hist = obs.seconds.labels(sink)
+
+    def record(self, status: Optional[int], seconds: float) -> None:
+        c = self._codes.get(status)
         if c is None:
-            c = self._children[key] = self.requests.labels(sink, "error" if status is None else str(status))
+            c = self._codes[status] = self._obs.requests.labels(self._sink, "error" if status is None
+                                                                else str(status))
         c.inc()
-        self.seconds.observe({"sink": sink}, seconds)
+        self._hist.observe(seconds)
 
 
-async def observed(observer, sink: str, coro):
-    """Await an HTTP request coroutine, reporting (sink, status|None, seconds) to ``observer``."""
-    if observer is None:
+async def observed(stats: Optional["SinkStats"], coro):
+    """Await an HTTP request coroutine, recording status and duration into ``stats``."""
+    if stats is None:
         return await coro
     t0 = time.perf_counter()
     try:
         r = await coro
     except Exception:
-        observer(sink, None, time.perf_counter() - t0)
+        stats.record(None, time.perf_counter() - t0)
         raise
-    observer(sink, r.status, time.perf_counter() - t0)
+    stats.record(r.status, time.perf_counter() - t0)
     return r
 
 

@@ -19,14 +19,14 @@ class TelegramClient:
         self.http = http
         self.base_url = base_url.rstrip("/")
         self.timeout = timeout
-        self.observer = observer
+        self.stats = observer.child("telegram") if observer is not None else None
 
     async def send_message(self, chat_id: Any, text: str, parse_mode: str = "markdown",
                            token: Any = ...) -> HttpResponse:
         # `bot${token}` — an undefined token renders as "botundefined" in the reference
         tok = self.token if token is ... else token
         url = f"{self.base_url}/bot{js_str(tok)}/sendMessage"
-        r = await observed(self.observer, "telegram",
+        r = await observed(self.stats,
                            self.http.request("GET", url, params={"chat_id": chat_id, "text": text,
                                                                  "parse_mode": parse_mode}, timeout=self.timeout))
         return r.raise_for_status()  # request-promise: reject on non-2xx

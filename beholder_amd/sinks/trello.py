@@ -13,9 +13,10 @@ kept; ``strict=True`` opts into raising on non-2xx.
 """
 from __future__ import annotations
 
+import time
 from typing import Any, Mapping, Optional
 
-from .http import HttpClient, HttpError, HttpResponse, observed
+from .http import HttpClient, HttpError, HttpResponse
 
 COMMENT_FALLBACK = "Failed to retrieve comment text."  # index.js:54
 
@@ -32,7 +33,7 @@ class TrelloClient:
         self.base_url = base_url.rstrip("/")
         self.strict = strict
         self.timeout = timeout
-        self.observer = observer
+        self.stats = observer.child("trello") if observer is not None else None
 
     def create_query(self) -> dict:
         return {"key": self.key, "token": self.token}
@@ -47,8 +48,17 @@ class TrelloClient:
         query = {"key": self.key, "token": self.token}
         if options:
             query.update(options)
-        req = self.http.request(m, self.base_url + path, params=query, timeout=self.timeout)
-        r = await (observed(self.observer, "trello", req) if self.observer is not None else req)
+        stats = self.stats
+        if stats is None:
+            r = await self.http.request(m, self.base_url + path, params=query, timeout=self.timeout)
+        else:
+            t0 = time.perf_counter()
+            try:
+                r = await self.http.request(m, self.base_url + path, params=query, timeout=self.timeout)
+            except Exception:
+                stats.record(None, time.perf_counter() - t0)
+                raise
+            stats.record(r.status, time.perf_counter() - t0)
         if self.strict:
             r.raise_for_status()
         return r

@@ -19,7 +19,7 @@ steps run untimed, then exactly ``K`` steps are timed.
 
 Scale-out is the reference's: competing consumers, one process each
 (SURVEY.md §2.3). Each rank runs ``--procs-per-rank`` consumer processes
-(default: its share of the host's CPUs, at most 8) on independent streams.
+(default: its share of the host CPUs minus one, at most 16) on independent streams.
 Timing: every consumer finishes its warm-up and parks on a barrier; the
 rank's coordinator passes a gloo barrier across ranks, releases its
 consumers and starts the clock; it stops the clock when all of its
@@ -83,7 +83,7 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--events-per-step", type=int, default=65536, help="events per step per consumer process")
     ap.add_argument("--procs-per-rank", type=int, default=0,
-                    help="consumer processes per rank (0 = min(8, CPUs per rank - 1))")
+                    help="consumer processes per rank (0 = min(16, CPUs per rank - 1))")
     ap.add_argument("--media", type=int, default=10000)
     ap.add_argument("--log-level", default="info")
     ap.add_argument("--seed", type=int, default=0)
@@ -259,7 +259,7 @@ def main(argv=None) -> int:
     if dist.world == 1 and a.gpus > 1:
         print(f"bench.py: --gpus {a.gpus} requires torch.distributed.run; running 1 rank", file=sys.stderr)
         n = 1
-    procs = a.procs_per_rank or max(1, min(8, available_cpus() // max(1, dist.local_world) - 1))
+    procs = a.procs_per_rank or max(1, min(16, available_cpus() // max(1, dist.local_world) - 1))
     gc.collect()
     res = run_rank(a, dist, procs)
     dist.barrier()
