@@ -154,6 +154,17 @@ class TelemetryHandlers:
             self._plan = plan
         return plan
 
+    @property
+    def store(self):
+        return self._store
+
+    @store.setter
+    def store(self, store) -> None:
+        self._store = store
+        # synchronous accessors when the backend has them (memory); None -> await the async API
+        self._get_nowait = getattr(store, "get_by_id_nowait", None)
+        self._update_nowait = getattr(store, "update_status_nowait", None)
+
     # ------------------------------------------------------------------ C8 ---
     async def comment(self, card_id: Any, text: Optional[str]) -> None:
         """index.js:50-58."""
@@ -172,14 +183,19 @@ class TelemetryHandlers:
 
         log.info(f"processing status update for media {js_str(media_id)}, status: {js_str(status)}")
 
-        await self.store.update_status(media_id, status)  # index.js:68
+        upd = self._update_nowait
+        if upd is not None:
+            upd(media_id, status)  # index.js:68
+        else:
+            await self.store.update_status(media_id, status)
 
         if self.no_trello:  # index.js:70-72 (Q2)
             return rmsg.ack()
 
         status_text = self._status_names_s.get(status)  # index.js:74 (None = undefined)
 
-        media = await self.store.get_by_id(media_id)  # index.js:76
+        get = self._get_nowait
+        media = get(media_id) if get is not None else await self.store.get_by_id(media_id)  # index.js:76
 
         # TRELLO Movement (index.js:78-90)
         if media.creator == TRELLO_CREATOR:
@@ -228,7 +244,8 @@ class TelemetryHandlers:
 
             self.progress_counter.child_for(status_text.lower()).inc()  # index.js:136-138
 
-            media = await self.store.get_by_id(media_id)  # index.js:140
+            get = self._get_nowait
+            media = get(media_id) if get is not None else await self.store.get_by_id(media_id)  # index.js:140
 
             if media.creator == self.trello_creator:  # index.js:142
                 comment_text = f"{status_text}: Progress **{js_str(progress)}%**"  # Q8

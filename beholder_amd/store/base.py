@@ -74,6 +74,12 @@ class MediaStore(abc.ABC):
     async def get_by_id(self, media_id: str) -> Media:
         """``db.getByID`` (index.js:76,140); raises :class:`MediaNotFound`."""
 
+    #: Optional synchronous accessors for stores that answer without I/O (memory).
+    #: Handlers call these when not None and skip one coroutine per message; the
+    #: semantics (return value / MediaNotFound) are identical to the async methods.
+    get_by_id_nowait = None
+    update_status_nowait = None
+
     # -- administration (used by tools/tests; not on the reference hot path) --
     @abc.abstractmethod
     async def upsert(self, media: Media) -> None:
