@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import random
 import uuid
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Dict, List, Sequence, Tuple
 
 from ..models import proto
 from ..ops import codec_for, frames

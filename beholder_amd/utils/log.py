@@ -26,7 +26,6 @@ import math
 import os
 import socket
 import sys
-import threading
 import time
 from typing import Any, Dict, Optional, TextIO
 

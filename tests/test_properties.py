@@ -17,7 +17,7 @@ from beholder_amd.transport.ingest import BytesSource, FdSource
 from beholder_amd.transport.memory import MemoryBroker
 from beholder_amd.utils.log import Logger, NullStream
 
-from helpers import ENUM, cfg, progress_msg, status_msg, trello_media
+from helpers import cfg, progress_msg, status_msg, trello_media
 
 MEDIA = [trello_media("m1"), trello_media("m2", card="C2")]
 
