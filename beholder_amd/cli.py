@@ -60,6 +60,8 @@ def cmd_run(a: argparse.Namespace) -> int:
         svc_cfg["transport"]["policy"] = a.policy
     if a.dead_letter:
         svc_cfg["transport"]["dead_letter"] = a.dead_letter
+    if a.format:
+        svc_cfg["transport"]["format"] = a.format
     if a.log_level:
         svc_cfg["log"]["level"] = a.log_level
     if a.metrics_port is not None:
@@ -224,6 +226,7 @@ def build_parser() -> argparse.ArgumentParser:
     r.add_argument("--path", help="input file for --source file")
     r.add_argument("--url", help="AMQP URL (default: dyn('rabbitmq'))")
     r.add_argument("--policy", choices=["block", "drop_newest"], help="ingest backpressure policy")
+    r.add_argument("--format", choices=["binary", "ndjson"], help="stdin/file framing (default binary)")
     r.add_argument("--dead-letter", help="append never-acked frames to this file")
     r.add_argument("--log-level", choices=["trace", "debug", "info", "warn", "error", "fatal", "silent"])
     r.add_argument("--metrics-port", type=int, help="metrics port (-1 disables the exposer)")

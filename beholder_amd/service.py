@@ -55,6 +55,10 @@ def build_source(config: Config, logger: Optional[Logger] = None) -> Source:
     tcfg = config.data["service"]["transport"]
     kind = (tcfg.get("kind") or "amqp").lower()
     prefetch = int(config.data["service"]["prefetch"])
+    if kind in ("stdin", "file") and tcfg.get("format", "binary") == "ndjson":
+        from .transport.ingest import NdjsonSource
+        return NdjsonSource(path=tcfg.get("path") if kind == "file" else None,
+                            policy=tcfg.get("policy", "block"), dead_letter=tcfg.get("dead_letter"))
     if kind == "stdin":
         from .transport.ingest import FdSource
         return FdSource(policy=tcfg.get("policy", "block"),

@@ -168,3 +168,57 @@ def read_all(source: FdSource) -> List:
         if got is None:
             return out
         out.extend(got)
+
+
+class NdjsonSource(FdSource):
+    """Line-oriented input: one JSON record per line (see :mod:`.framing` for the record shape).
+
+    A reader thread parses lines and pushes ``(topic_id, payload)`` into the same native ring
+    the binary reader uses, so everything downstream (batches, deliveries, acks, backpressure)
+    is identical. Malformed lines are counted and logged to stderr, not fatal.
+    """
+
+    kind = "ndjson"
+
+    def __init__(self, fd: Optional[int] = None, path: Optional[str] = None, **kw):
+        super().__init__(fd=fd, path=path, **kw)
+        self.bad_lines = 0
+        self._thread: Optional[threading.Thread] = None
+
+    async def start(self, topics: Sequence[str] = ()) -> None:
+        if self._started:
+            return
+        fd = self._fd
+        if self._path is not None:
+            fd = os.open(self._path, os.O_RDONLY)
+            self._fd = fd
+        from .framing import ndjson_line_to_frame
+
+        def run():
+            try:
+                with os.fdopen(fd, "r", encoding="utf-8", closefd=self._own_fd) as f:
+                    for line in f:
+                        line = line.strip()
+                        if not line:
+                            continue
+                        try:
+                            tid, payload = ndjson_line_to_frame(line)
+                        except (ValueError, KeyError, TypeError) as e:
+                            self.bad_lines += 1
+                            print(f"beholder: skipping malformed ndjson line: {e}", file=sys.stderr)
+                            continue
+                        try:
+                            self._ingest.push(tid, payload)
+                        except RuntimeError:  # closed
+                            return
+            finally:
+                self._ingest.set_eof()
+
+        self._thread = threading.Thread(target=run, daemon=True, name="ndjson-reader")
+        self._thread.start()
+        self._started = True
+
+    def stats(self) -> dict:
+        s = super().stats()
+        s["bad_lines"] = self.bad_lines
+        return s

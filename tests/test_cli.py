@@ -53,3 +53,21 @@ def test_run_amqp_unreachable_fails_fast(tmp_path):
                    "service: {metrics: {enabled: false}, retries: 0}\n")
     r = cli("run", "--config", str(cfg), "--source", "amqp", "--url", "amqp://guest:guest@127.0.0.1:1/")
     assert r.returncode == 1 and b"fatal" in r.stderr
+
+
+def test_run_stdin_ndjson(tmp_path):
+    cfg = tmp_path / "events.yaml"
+    cfg.write_text("keys: {trello: {key: k, token: t}}\ninstance: {flow_ids: {}}\n"
+                   "service: {metrics: {enabled: false}}\n")
+    (tmp_path / "m.json").write_text('[{"id": "m1", "creator": 0}]')
+    lines = "\n".join([
+        '{"topic": "v1.telemetry.progress", "json": {"mediaId": "m1", "status": "CONVERTING", "progress": 40}}',
+        'not json',
+        '{"topic": "v1.telemetry.status", "json": {"mediaId": "m1", "status": "DEPLOYED"}}',
+    ]) + "\n"
+    r = cli("run", "--config", str(cfg), "--source", "stdin", "--format", "ndjson", "--media-fixture",
+            str(tmp_path / "m.json"), "--stats", input=lines.encode())
+    assert r.returncode == 0, r.stderr
+    stats = json.loads(r.stderr.decode().strip().splitlines()[-1])
+    assert stats["source"]["acked"] == 2 and stats["source"]["bad_lines"] == 1
+    assert stats["progress_updates"] == {"converting": 1.0}
