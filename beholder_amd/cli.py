@@ -95,7 +95,7 @@ def cmd_run(a: argparse.Namespace) -> int:
             await svc.close()
         if a.stats:
             print(json.dumps(stats, default=str), file=sys.stderr)
-        return 0
+        return 1 if svc.source_error else 0
 
     try:
         return asyncio.run(main())

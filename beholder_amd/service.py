@@ -113,6 +113,7 @@ class Service:
         self.serializer: Optional[KeyedSerializer] = None
         self.started_at = 0.0
         self.received = array.array("Q", [0] * len(T.TOPIC_NAMES_BY_ID))
+        self.source_error: Optional[str] = None
 
     # ------------------------------------------------------------ properties --
     @property
@@ -307,6 +308,10 @@ class Service:
             self._running = False
             flusher.cancel()
             await self._drain()
+            err = (self._source.stats() or {}).get("error") if self._source is not None else None
+            if err:
+                self.source_error = err
+                log.error(f"ingest source failed: {err}")
             log.flush()
         return self.stats()
 

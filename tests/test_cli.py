@@ -71,3 +71,12 @@ def test_run_stdin_ndjson(tmp_path):
     stats = json.loads(r.stderr.decode().strip().splitlines()[-1])
     assert stats["source"]["acked"] == 2 and stats["source"]["bad_lines"] == 1
     assert stats["progress_updates"] == {"converting": 1.0}
+
+
+def test_run_corrupt_stream_exits_nonzero(tmp_path):
+    cfg = tmp_path / "events.yaml"
+    cfg.write_text("keys: {trello: {key: k, token: t}}\ninstance: {flow_ids: {}}\n"
+                   "service: {metrics: {enabled: false}}\n")
+    r = cli("run", "--config", str(cfg), "--source", "stdin", input=b"\x09\x00\x00\x00\x01abc")  # truncated frame
+    assert r.returncode == 1
+    assert b"ingest source failed" in r.stdout and b"truncated" in r.stdout
