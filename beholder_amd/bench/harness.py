@@ -38,7 +38,7 @@ from typing import Dict, List, Optional
 
 from .generator import Workload, bench_config
 
-CONFIGS = ("plumbing", "firehose_1k", "rate_10k", "backpressure", "soak", "amqp")
+CONFIGS = ("plumbing", "firehose_1k", "rate_10k", "backpressure", "soak", "amqp", "io_bound")
 
 
 def _rss_mb() -> float:
@@ -121,7 +121,8 @@ class _Producer(threading.Thread):
 
 
 async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_events: int = 0,
-                      n_media: int = 10000, media=None, log_level: str = "info", rss_probe=None) -> dict:
+                      n_media: int = 10000, media=None, log_level: str = "info", rss_probe=None,
+                      sink_delay_s: float = 0.0) -> dict:
     from ..config import Config
     from ..service import Service
     from ..sinks import RecordingHttpClient
@@ -134,8 +135,16 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
     cfgd["service"]["log"]["level"] = log_level
     sink = open(os.devnull, "w", buffering=1 << 16)
     src = FdSource(fd=rfd, policy=policy, capacity_events=capacity_events)
-    svc = Service(Config.from_dict(cfgd), source=src, store=MemoryStore(media), http=RecordingHttpClient(keep=8),
+    http = RecordingHttpClient(keep=8, delay_s=sink_delay_s)
+    svc = Service(Config.from_dict(cfgd), source=src, store=MemoryStore(media), http=http,
                   logger=Logger(stream=sink, level=log_level), serve_metrics=False)
+    max_inflight = [0]
+    if sink_delay_s:
+        async def watch():
+            while True:
+                max_inflight[0] = max(max_inflight[0], len(svc._inflight))
+                await asyncio.sleep(0.001)
+        watcher = asyncio.ensure_future(watch())
     await svc.init()
     prod = _Producer(wfd, events, rate)
     if rss_probe is not None:
@@ -148,6 +157,8 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
     prod.join()
     if rss_probe is not None:
         rss_probe.append(_rss_mb())  # after 1M events, before teardown
+    if sink_delay_s:
+        watcher.cancel()
     await svc.close()
     sink.close()
     s = stats["source"]
@@ -160,6 +171,7 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
         "ingest_latency_us": {k: v / 1e3 for k, v in stats["ingest_latency_ns"].items() if k.startswith("p")},
         "handle_latency_us": {k: v / 1e3 for k, v in stats["handle_latency_ns"].items() if k.startswith("p")},
         "producer_blocked_ms": s["blocked_ns"] / 1e6, "ring_high_water": s["high_water_events"],
+        "sink_requests": http.count, "max_inflight": max_inflight[0],
     }
 
 
@@ -186,6 +198,11 @@ def run_config(name: str, *, duration_s: Optional[float] = None, events: Optiona
                                                                capacity_events=4096, media=w.media))}
         dn = res["drop_newest"]
         res.update({"offered": dn["offered"], "accepted": dn["accepted"], "dropped": dn["dropped"]})
+    elif name == "io_bound":
+        # every sink call waits 2 ms (network): throughput is bounded by prefetch / latency
+        res = asyncio.run(_run_inproc(w.events(events or 100_000), 0, media=w.media, sink_delay_s=0.002))
+        res["sink_delay_ms"] = 2.0
+        res["prefetch"] = 100
     elif name == "amqp":
         res = _amqp(events or 200_000)
     elif name == "soak":

@@ -54,3 +54,22 @@ def test_soak_1m_events_rss_and_gc():
     res = harness.run_config("soak", events=1_000_000)
     assert res["acked"] == 1_000_000
     assert res["rss_growth_mb"] < 64, res  # the service itself must not grow with traffic
+
+
+def test_bench_two_ranks_torchrun_on_box():
+    """The driver's multi-GPU launch path (torch.distributed.run, gloo barriers, MAX over ranks)."""
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", "29571", os.path.join(ROOT, "bench.py"),
+                          "--gpus", "2", "--steps", "3", "--warmup", "1", "--procs-per-rank", "2"],
+                         capture_output=True, text=True, timeout=900, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
+    assert r["n_gpus"] == 2 and r["procs_per_rank"] == 2 and r["handler_errors"] == 0
+    assert r["config"]["global_batch"] == 4 * 65536
+
+
+def test_io_bound_concurrency_reaches_prefetch():
+    """Sinks with 2 ms latency: up to prefetch (100, index.js:43) handlers in flight."""
+    from beholder_amd.bench import harness
+    res = harness.run_config("io_bound", events=20000)
+    assert res["acked"] == 20000 and res["max_inflight"] == 100
