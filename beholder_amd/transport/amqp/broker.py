@@ -121,7 +121,8 @@ class _BConn:
 
 class AmqpBroker:
     def __init__(self, host: str = "127.0.0.1", port: int = 0, users: Optional[Dict[str, str]] = None,
-                 vhosts: Tuple[str, ...] = ("/",), frame_max: int = 131072, heartbeat: int = 60):
+                 vhosts: Tuple[str, ...] = ("/",), frame_max: int = 131072, heartbeat: int = 60,
+                 ssl_context=None):
         self.host = host
         self.port = port
         self.users = users  # None = accept any credentials
@@ -136,14 +137,16 @@ class AmqpBroker:
         self._server: Optional[asyncio.AbstractServer] = None
         self.mute_heartbeats = False
         self.connections_total = 0
+        self.ssl_context = ssl_context
 
     # -------------------------------------------------------------- admin ---
     @property
     def url(self) -> str:
-        return f"amqp://guest:guest@{self.host}:{self.port}/"
+        scheme = "amqps" if self.ssl_context is not None else "amqp"
+        return f"{scheme}://guest:guest@{self.host}:{self.port}/"
 
     async def start(self) -> "AmqpBroker":
-        self._server = await asyncio.start_server(self._serve, self.host, self.port)
+        self._server = await asyncio.start_server(self._serve, self.host, self.port, ssl=self.ssl_context)
         self.port = self._server.sockets[0].getsockname()[1]
         return self
 

@@ -336,11 +336,19 @@ class Connection:
         p = self.params
         loop = asyncio.get_running_loop()
         ssl_ctx = None
+        server_hostname = None
         if p["ssl"]:
             import ssl
-            ssl_ctx = ssl.create_default_context()
+            ssl_ctx = ssl.create_default_context(cafile=p.get("cafile"))
+            if p.get("certfile"):
+                ssl_ctx.load_cert_chain(p["certfile"], p.get("keyfile"))
+            if not p.get("verify", True):
+                ssl_ctx.check_hostname = False
+                ssl_ctx.verify_mode = ssl.CERT_NONE
+            server_hostname = p.get("server_name") or p["host"]
         self._reader, self._writer = await asyncio.wait_for(
-            asyncio.open_connection(p["host"], p["port"], ssl=ssl_ctx), self.connect_timeout)
+            asyncio.open_connection(p["host"], p["port"], ssl=ssl_ctx, server_hostname=server_hostname),
+            self.connect_timeout)
         self._handshake = loop.create_future()
         self._writer.write(wire.PROTOCOL_HEADER)
         self._last_rx = self._last_tx = time.monotonic()

@@ -490,4 +490,10 @@ def parse_url(url: str) -> Dict[str, Any]:
         "frame_max": int(q.get("frame_max", 131072)),
         "channel_max": int(q.get("channel_max", 2047)),
         "ssl": u.scheme == "amqps",
+        # TLS options (amqps): ?cafile=/path/ca.pem&certfile=..&keyfile=..&verify=false&server_name=host
+        "cafile": q.get("cafile"),
+        "certfile": q.get("certfile"),
+        "keyfile": q.get("keyfile"),
+        "verify": q.get("verify", "true").lower() not in ("false", "0", "no"),
+        "server_name": q.get("server_name"),
     }

@@ -329,3 +329,36 @@ def test_ack_coalescer_prefix_gap_and_nack():
         await asyncio.sleep(0)
         assert ch.sent == [(10, False)]  # 9 outstanding -> no multiple
     run(go())
+
+
+def test_amqps_tls_with_ca_verification(tmp_path):
+    """amqps:// with a private CA (?cafile=...) and hostname verification."""
+    import shutil
+    import ssl
+    import subprocess
+    if shutil.which("openssl") is None:
+        pytest.skip("needs openssl")
+    key, crt = tmp_path / "k.pem", tmp_path / "c.pem"
+    r = subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", str(key), "-out",
+                        str(crt), "-days", "1", "-subj", "/CN=localhost", "-addext", "subjectAltName=DNS:localhost"],
+                       capture_output=True)
+    assert r.returncode == 0, r.stderr
+
+    async def go():
+        ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+        ctx.load_cert_chain(str(crt), str(key))
+        b = await AmqpBroker(ssl_context=ctx).start()
+        try:
+            url = f"amqps://guest:guest@127.0.0.1:{b.port}/?cafile={crt}&server_name=localhost"
+            src = AmqpSource(url, prefetch=10)
+            await src.start([STATUS])
+            b.publish(STATUS, b"secure")
+            got = await src.batches().__anext__()
+            assert got[0].content == b"secure"
+            got[0].ack()
+            await src.close()
+            with pytest.raises((ssl.SSLError, OSError)):  # untrusted without the CA
+                await Connection(f"amqps://guest:guest@127.0.0.1:{b.port}/?server_name=localhost").open()
+        finally:
+            await b.stop()
+    run(go())
