@@ -80,3 +80,19 @@ def test_run_corrupt_stream_exits_nonzero(tmp_path):
     r = cli("run", "--config", str(cfg), "--source", "stdin", input=b"\x09\x00\x00\x00\x01abc")  # truncated frame
     assert r.returncode == 1
     assert b"ingest source failed" in r.stdout and b"truncated" in r.stdout
+
+
+def test_seed_sqlite_and_publish_to_broker(tmp_path):
+    from beholder_amd.topics import PROGRESS, STATUS
+    from beholder_amd.transport.amqp.broker import BrokerThread
+    ev = cli("gen", "--events", "40", "--media", "3", "--media-out", str(tmp_path / "m.json"), "--out",
+             str(tmp_path / "ev.bin"))
+    assert ev.returncode == 0
+    db = tmp_path / "media.db"
+    r = cli("seed", str(tmp_path / "m.json"), "--store", "sqlite", "--dsn", str(db))
+    assert r.returncode == 0 and r.stdout.strip() == b"3"
+    with BrokerThread() as bt:
+        r = cli("publish", "--url", bt.url, str(tmp_path / "ev.bin"))
+        assert r.returncode == 0 and r.stdout.strip() == b"40"
+        depth = bt.call(lambda b: b.depth(STATUS) + b.depth(PROGRESS))
+    assert depth == 40
