@@ -50,7 +50,13 @@ void append_frame(std::string& out, int topic, const char* p, size_t n) {
 }
 
 // frame(topic, payload) -> bytes  (u32le len | u8 topic | payload)
+PyObject* mod_frame_impl(PyObject*, PyObject* args);
 PyObject* mod_frame(PyObject*, PyObject* args) {
+  BEHOLDER_TRY { return mod_frame_impl(nullptr, args); }
+  BEHOLDER_CATCH(nullptr)
+}
+
+PyObject* mod_frame_impl(PyObject*, PyObject* args) {
   int topic;
   Py_buffer view;
   if (!PyArg_ParseTuple(args, "iy*", &topic, &view)) return nullptr;
@@ -67,7 +73,13 @@ PyObject* mod_frame(PyObject*, PyObject* args) {
 }
 
 // frames(iterable of (topic, payload)) -> bytes
+PyObject* mod_frames_impl(PyObject*, PyObject* it_in);
 PyObject* mod_frames(PyObject*, PyObject* it_in) {
+  BEHOLDER_TRY { return mod_frames_impl(nullptr, it_in); }
+  BEHOLDER_CATCH(nullptr)
+}
+
+PyObject* mod_frames_impl(PyObject*, PyObject* it_in) {
   PyObject* it = PyObject_GetIter(it_in);
   if (!it) return nullptr;
   std::string out;

@@ -38,6 +38,9 @@ struct Pending {
   PyObject* extra = nullptr;  // borrowed from ConsumerInfo (kept alive by the map)
 };
 
+// RabbitMQ's hard upper bound for a message body (max_message_size <= 512 MiB).
+constexpr uint64_t kMaxBody = 512ull << 20;
+
 struct AmqpDemuxObject {
   PyObject_HEAD SettlerObject* settler;
   std::string* carry;
@@ -256,8 +259,13 @@ bool handle_frame(AmqpDemuxObject* self, PyObject* out, uint8_t type, uint16_t c
     }
     pd.have_header = true;
     pd.size = be64(p + 4);
+    if (pd.size > kMaxBody) {
+      PyErr_Format(PyExc_ValueError, "content body size %llu exceeds the %llu byte limit",
+                   (unsigned long long)pd.size, (unsigned long long)kMaxBody);
+      return false;
+    }
     if (pd.size == 0) return emit_delivery(self, out, pd, now);
-    pd.body.reserve(size_t(pd.size));
+    pd.body.reserve(size_t(pd.size < (1u << 20) ? pd.size : (1u << 20)));
     return true;
   }
   if (type == 3) {
@@ -278,7 +286,13 @@ bool handle_frame(AmqpDemuxObject* self, PyObject* out, uint8_t type, uint16_t c
 }
 
 // feed(data) -> list of Delivery | (type, channel, payload)
+PyObject* demux_feed_impl(AmqpDemuxObject* self, PyObject* arg);
 PyObject* demux_feed(AmqpDemuxObject* self, PyObject* arg) {
+  BEHOLDER_TRY { return demux_feed_impl(self, arg); }
+  BEHOLDER_CATCH(nullptr)
+}
+
+PyObject* demux_feed_impl(AmqpDemuxObject* self, PyObject* arg) {
   Py_buffer view;
   if (PyObject_GetBuffer(arg, &view, PyBUF_SIMPLE) < 0) return nullptr;
   PyObject* out = PyList_New(0);

@@ -83,7 +83,13 @@ PyObject* codec_new(PyTypeObject* type, PyObject*, PyObject*) {
 }
 
 // MessageCodec(type_name: str, fields: sequence of (number, name, kind))
+int codec_init_impl(CodecObject* self, PyObject* args, PyObject* kwds);
 int codec_init(CodecObject* self, PyObject* args, PyObject* kwds) {
+  BEHOLDER_TRY { return codec_init_impl(self, args, kwds); }
+  BEHOLDER_CATCH(-1)
+}
+
+int codec_init_impl(CodecObject* self, PyObject* args, PyObject* kwds) {
   static const char* kwlist[] = {"type_name", "fields", nullptr};
   const char* tname;
   PyObject* fields;
@@ -424,7 +430,13 @@ bool encode_field(std::string& buf, uint32_t number, int kind, PyObject* v) {
 }
 
 // encode(obj) where obj is a sequence in slot order or a mapping by field name.
+PyObject* codec_encode_impl(CodecObject* self, PyObject* obj);
 PyObject* codec_encode(CodecObject* self, PyObject* obj) {
+  BEHOLDER_TRY { return codec_encode_impl(self, obj); }
+  BEHOLDER_CATCH(nullptr)
+}
+
+PyObject* codec_encode_impl(CodecObject* self, PyObject* obj) {
   const size_t n = self->fields->size();
   std::string buf;
   buf.reserve(64);

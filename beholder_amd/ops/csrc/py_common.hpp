@@ -8,7 +8,23 @@
 
 #include "histogram.hpp"
 
+#include <new>
+#include <stdexcept>
+
 namespace beholder {
+
+// C++ exceptions must never cross into CPython (std::terminate). Entry points
+// that allocate wrap their body: BEHOLDER_TRY { ... } BEHOLDER_CATCH(nullptr)
+#define BEHOLDER_TRY try
+#define BEHOLDER_CATCH(errval)                                 \
+  catch (const std::bad_alloc&) {                              \
+    PyErr_NoMemory();                                          \
+    return errval;                                             \
+  }                                                            \
+  catch (const std::exception& e) {                            \
+    PyErr_Format(PyExc_RuntimeError, "native error: %s", e.what()); \
+    return errval;                                             \
+  }
 
 // Module-level state (single-phase init; one interpreter).
 struct ModuleState {

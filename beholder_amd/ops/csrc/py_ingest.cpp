@@ -388,7 +388,19 @@ void set_error(IngestObject* self, const std::string& e) {
   if (self->error->empty()) *self->error = e;
 }
 
+void reader_loop(IngestObject* self, int fd, size_t chunk_bytes);
+
+// Thread entry: an exception escaping a std::thread would terminate the process.
 void reader_main(IngestObject* self, int fd, size_t chunk_bytes) {
+  try {
+    reader_loop(self, fd, chunk_bytes);
+  } catch (const std::exception& e) {
+    set_error(self, std::string("reader thread: ") + e.what());
+    self->ring->set_eof();
+  }
+}
+
+void reader_loop(IngestObject* self, int fd, size_t chunk_bytes) {
   std::vector<uint8_t> chunk(chunk_bytes);
   Framer framer(self->max_frame);
   struct pollfd pfd;
@@ -463,7 +475,13 @@ PyObject* ingest_new(PyTypeObject* type, PyObject*, PyObject*) {
   return reinterpret_cast<PyObject*>(self);
 }
 
+int ingest_init_impl(IngestObject* self, PyObject* args, PyObject* kwds);
 int ingest_init(IngestObject* self, PyObject* args, PyObject* kwds) {
+  BEHOLDER_TRY { return ingest_init_impl(self, args, kwds); }
+  BEHOLDER_CATCH(-1)
+}
+
+int ingest_init_impl(IngestObject* self, PyObject* args, PyObject* kwds) {
   static const char* kwlist[] = {"capacity_bytes", "capacity_events", "policy", "max_frame", "settler", nullptr};
   unsigned long long cap_bytes = 64ull << 20, cap_events = 0;
   const char* policy = "block";
@@ -533,7 +551,13 @@ bool check_ready(IngestObject* self) {
 }
 
 // start_reader(fd, chunk_bytes=1MiB, own_fd=False)
+PyObject* ingest_start_reader_impl(IngestObject* self, PyObject* args, PyObject* kwds);
 PyObject* ingest_start_reader(IngestObject* self, PyObject* args, PyObject* kwds) {
+  BEHOLDER_TRY { return ingest_start_reader_impl(self, args, kwds); }
+  BEHOLDER_CATCH(nullptr)
+}
+
+PyObject* ingest_start_reader_impl(IngestObject* self, PyObject* args, PyObject* kwds) {
   static const char* kwlist[] = {"fd", "chunk_bytes", "own_fd", nullptr};
   int fd;
   unsigned long chunk = 1ul << 20;
@@ -584,7 +608,13 @@ PyObject* ingest_push(IngestObject* self, PyObject* args) {
 }
 
 // feed(data): frame a byte stream fed from Python; returns frames accepted.
+PyObject* ingest_feed_impl(IngestObject* self, PyObject* arg);
 PyObject* ingest_feed(IngestObject* self, PyObject* arg) {
+  BEHOLDER_TRY { return ingest_feed_impl(self, arg); }
+  BEHOLDER_CATCH(nullptr)
+}
+
+PyObject* ingest_feed_impl(IngestObject* self, PyObject* arg) {
   if (!check_ready(self)) return nullptr;
   Py_buffer view;
   if (PyObject_GetBuffer(arg, &view, PyBUF_SIMPLE) < 0) return nullptr;
@@ -618,7 +648,13 @@ PyObject* ingest_set_eof(IngestObject* self, PyObject*) {
 }
 
 // pop(max_n=256, timeout=-1.0) -> list[Delivery] ([] on timeout) | None when drained
+PyObject* ingest_pop_impl(IngestObject* self, PyObject* args, PyObject* kwds);
 PyObject* ingest_pop(IngestObject* self, PyObject* args, PyObject* kwds) {
+  BEHOLDER_TRY { return ingest_pop_impl(self, args, kwds); }
+  BEHOLDER_CATCH(nullptr)
+}
+
+PyObject* ingest_pop_impl(IngestObject* self, PyObject* args, PyObject* kwds) {
   static const char* kwlist[] = {"max_n", "timeout", nullptr};
   Py_ssize_t max_n = 256;
   double timeout = -1.0;

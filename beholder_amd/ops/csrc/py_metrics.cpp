@@ -96,7 +96,13 @@ PyObject* hist_merge(HistogramObject* self, PyObject* other) {
 
 // Serialization for cross-rank aggregation: header (total, sum, min, max) +
 // sparse (index, count) pairs.
+PyObject* hist_to_bytes_impl(HistogramObject* self, PyObject*);
 PyObject* hist_to_bytes(HistogramObject* self, PyObject*) {
+  BEHOLDER_TRY { return hist_to_bytes_impl(self, nullptr); }
+  BEHOLDER_CATCH(nullptr)
+}
+
+PyObject* hist_to_bytes_impl(HistogramObject* self, PyObject*) {
   const auto& c = self->h->counts();
   std::string out;
   uint64_t hdr[4] = {self->h->total(), 0, self->h->min(), self->h->max()};
@@ -111,7 +117,13 @@ PyObject* hist_to_bytes(HistogramObject* self, PyObject*) {
   return PyBytes_FromStringAndSize(out.data(), Py_ssize_t(out.size()));
 }
 
+PyObject* hist_merge_bytes_impl(HistogramObject* self, PyObject* arg);
 PyObject* hist_merge_bytes(HistogramObject* self, PyObject* arg) {
+  BEHOLDER_TRY { return hist_merge_bytes_impl(self, arg); }
+  BEHOLDER_CATCH(nullptr)
+}
+
+PyObject* hist_merge_bytes_impl(HistogramObject* self, PyObject* arg) {
   char* p;
   Py_ssize_t n;
   if (PyBytes_AsStringAndSize(arg, &p, &n) < 0) return nullptr;

@@ -332,7 +332,13 @@ long long wall_ms() {
 }
 
 // format_line(level:int, time_ms:int, prefix:str, extra:str|None, args:tuple) -> str
+PyObject* mod_format_line_impl(PyObject*, PyObject* const* a, Py_ssize_t n);
 PyObject* mod_format_line(PyObject*, PyObject* const* a, Py_ssize_t n) {
+  BEHOLDER_TRY { return mod_format_line_impl(nullptr, a, n); }
+  BEHOLDER_CATCH(nullptr)
+}
+
+PyObject* mod_format_line_impl(PyObject*, PyObject* const* a, Py_ssize_t n) {
   if (n != 5 || !PyUnicode_Check(a[2]) || !PyTuple_Check(a[4])) {
     PyErr_SetString(PyExc_TypeError, "format_line(level, time_ms, prefix, extra, args)");
     return nullptr;
@@ -456,7 +462,13 @@ bool sink_emit_core(LogSinkObject* self, long lvl, const char* prefix, Py_ssize_
 }
 
 // emit(level, prefix, extra, args)
+PyObject* sink_emit_impl(LogSinkObject* self, PyObject* const* a, Py_ssize_t n);
 PyObject* sink_emit(LogSinkObject* self, PyObject* const* a, Py_ssize_t n) {
+  BEHOLDER_TRY { return sink_emit_impl(self, a, n); }
+  BEHOLDER_CATCH(nullptr)
+}
+
+PyObject* sink_emit_impl(LogSinkObject* self, PyObject* const* a, Py_ssize_t n) {
   if (n != 4 || !PyUnicode_Check(a[1]) || !PyTuple_Check(a[3])) {
     PyErr_SetString(PyExc_TypeError, "emit(level, prefix, extra, args)");
     return nullptr;
@@ -524,13 +536,25 @@ PyGetSetDef sink_getset[] = {
 
 PyTypeObject LogSinkType = {PyVarObject_HEAD_INIT(nullptr, 0)};
 
+PyObject* mod_quick_format_impl(PyObject*, PyObject* args);
 PyObject* mod_quick_format(PyObject*, PyObject* args) {
+  BEHOLDER_TRY { return mod_quick_format_impl(nullptr, args); }
+  BEHOLDER_CATCH(nullptr)
+}
+
+PyObject* mod_quick_format_impl(PyObject*, PyObject* args) {
   std::string msg;
   if (!quick_format_append(msg, &PyTuple_GET_ITEM(args, 0), PyTuple_GET_SIZE(args))) return nullptr;
   return PyUnicode_DecodeUTF8(msg.data(), Py_ssize_t(msg.size()), "strict");
 }
 
+PyObject* mod_js_str_impl(PyObject*, PyObject* v);
 PyObject* mod_js_str(PyObject*, PyObject* v) {
+  BEHOLDER_TRY { return mod_js_str_impl(nullptr, v); }
+  BEHOLDER_CATCH(nullptr)
+}
+
+PyObject* mod_js_str_impl(PyObject*, PyObject* v) {
   std::string out;
   if (!js_str_append(out, v)) return nullptr;
   return PyUnicode_DecodeUTF8(out.data(), Py_ssize_t(out.size()), "strict");
@@ -584,7 +608,13 @@ PyObject* mod_quote_component(PyObject*, PyObject* v) {
 }
 
 // encode_query(mapping) -> "k=v&k2=v2" (insertion order)
+PyObject* mod_encode_query_impl(PyObject*, PyObject* m);
 PyObject* mod_encode_query(PyObject*, PyObject* m) {
+  BEHOLDER_TRY { return mod_encode_query_impl(nullptr, m); }
+  BEHOLDER_CATCH(nullptr)
+}
+
+PyObject* mod_encode_query_impl(PyObject*, PyObject* m) {
   if (!PyDict_Check(m)) {
     PyErr_SetString(PyExc_TypeError, "encode_query expects a dict");
     return nullptr;
@@ -689,7 +719,13 @@ PyObject* core_set(LogCoreObject* self, PyObject* args) {
   Py_RETURN_NONE;
 }
 
+PyObject* core_log_impl(LogCoreObject* self, long lvl, PyObject* const* args, Py_ssize_t nargs);
 PyObject* core_log(LogCoreObject* self, long lvl, PyObject* const* args, Py_ssize_t nargs) {
+  BEHOLDER_TRY { return core_log_impl(self, lvl, args, nargs); }
+  BEHOLDER_CATCH(nullptr)
+}
+
+PyObject* core_log_impl(LogCoreObject* self, long lvl, PyObject* const* args, Py_ssize_t nargs) {
   if (lvl < self->min_level) Py_RETURN_NONE;
   if (!self->sink || !self->prefix) {
     PyErr_SetString(PyExc_RuntimeError, "logger core not configured");
