@@ -1,7 +1,7 @@
 SHELL=/bin/bash
 PY ?= python
 
-.PHONY: native test test-gpu bench bench-configs lint tsan docker clean
+.PHONY: native test test-gpu bench bench-configs lint tsan asan docker clean
 
 native:            ## build the C++ runtime in-tree
 	$(PY) -m beholder_amd.ops.build
@@ -23,6 +23,15 @@ lint:
 
 tsan:              ## ring/framer stress test under ThreadSanitizer + ASan/UBSan
 	$(MAKE) -C tests/native run
+
+asan:             ## CPython suites against an ASan+UBSan build of the extension (host code only)
+	$(PY) -m beholder_amd.ops.build --force --sanitize=address,undefined
+	BEHOLDER_ALLOW_BUILD=0 ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=halt_on_error=1 \
+	  LD_PRELOAD="$$(gcc -print-file-name=libasan.so) $$(gcc -print-file-name=libubsan.so)" \
+	  $(PY) -m pytest -q -p no:cacheprovider tests/test_native_fuzz.py tests/test_codec.py tests/test_ingest.py \
+	  tests/test_amqp_demux.py tests/test_text.py tests/test_delivery.py tests/test_histogram.py \
+	  tests/test_handlers.py tests/test_amqp.py tests/test_service.py; \
+	  rc=$$?; $(PY) -m beholder_amd.ops.build --force >/dev/null; exit $$rc
 
 docker:
 	DOCKER_BUILDKIT=1 docker build -t tritonmedia/beholder -f Dockerfile .
