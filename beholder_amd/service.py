@@ -242,6 +242,21 @@ class Service:
         reg.register(Gauge("beholder_inflight", "Handlers currently suspended on I/O",
                            collect=lambda g: g.set(len(self._inflight))))
 
+        # transport metrics (the reference hands `prom` to triton-core/amqp, index.js:43)
+        def transport_collect(g: Gauge):
+            if self._source is None:
+                return
+            st = self._source.stats()
+            g.set({"kind": self._source.kind, "field": "connected"}, 1.0 if self._source.ready() else 0.0)
+            for k in ("reconnects", "stale_settles", "bytes_in", "bytes_out", "ack_frames", "bytes_read",
+                      "frames_read", "depth", "high_water_events"):
+                v = st.get(k)
+                if isinstance(v, (int, float)):
+                    g.set({"kind": self._source.kind, "field": k}, v)
+
+        reg.register(Gauge("beholder_transport", "Ingest transport state (connected flag, reconnects, bytes, "
+                           "ring depth)", ["kind", "field"], collect=transport_collect))
+
         reg.register(NativeHistogramView("beholder_handle_latency_seconds",
                                          "Handler start to ack latency",
                                          lambda: settler().handle_latency if settler() is not None else None))

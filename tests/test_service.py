@@ -295,3 +295,19 @@ def test_trace_spans():
     assert sorted((s["span"], s["outcome"], s["state"]) for s in spans) == [
         (PROGRESS, "ok", "acked"), (STATUS, "unsettled", "pending")]
     assert all(s["handle_us"] >= 0 and s["queue_us"] >= 0 for s in spans)
+
+
+def test_transport_metrics_exposed():
+    async def go():
+        broker = await AmqpBroker().start()
+        try:
+            svc = make_service(AmqpSource(broker.url), [trello_media("m1")])
+            await svc.init()
+            text = svc.registry.render()
+            await svc.close()
+            return parse_exposition(text)
+        finally:
+            await broker.stop()
+    m = run(go())
+    assert m['beholder_transport{kind="amqp",field="connected"}'] == 1
+    assert m['beholder_transport{kind="amqp",field="reconnects"}'] == 0
