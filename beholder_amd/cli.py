@@ -3,6 +3,7 @@
 Commands
 --------
 run      start the service (``--source amqp|stdin|file``); the reference's only mode.
+config   validate and print the effective config (secrets masked).
 gen      write synthetic framed telemetry to stdout/a file (+ optional media fixture).
 decode   turn a framed stream into NDJSON (debugging).
 seed     load a media fixture into a sqlite/postgres store.
@@ -107,6 +108,35 @@ def cmd_run(a: argparse.Namespace) -> int:
     except Exception as e:  # startup failure is fatal (Q10 fix)
         print(f"beholder: fatal: {type(e).__name__}: {e}", file=sys.stderr)
         return 1
+
+
+_SECRET_KEYS = ("token", "key", "password", "secret", "dsn", "url")
+
+
+def redact_config(obj, parent: str = ""):
+    """Copy of the config with credentials masked (keys.*, tokens, passwords, DSN/URL userinfo)."""
+    import re
+    if isinstance(obj, dict):
+        return {k: redact_config(v, k) for k, v in obj.items()}
+    if isinstance(obj, list):
+        return [redact_config(v, parent) for v in obj]
+    if isinstance(obj, str) and any(s in parent.lower() for s in _SECRET_KEYS):
+        if parent.lower() in ("dsn", "url"):
+            return re.sub(r"//([^:/@]+):([^@]+)@", r"//\1:***@", obj)
+        return "***" if obj else obj
+    return obj
+
+
+def cmd_config(a: argparse.Namespace) -> int:
+    """Validate the config and print the effective (merged, env-overridden) result, secrets masked."""
+    try:
+        cfg = Config.load("events", path=a.config, env=dict(os.environ))
+    except ConfigError as e:
+        print(f"beholder: config error: {e}", file=sys.stderr)
+        return 2
+    out = {"source": cfg.source, "no_trello": cfg.no_trello, "config": redact_config(cfg.data)}
+    print(json.dumps(out, indent=2, default=str))
+    return 0
 
 
 def cmd_gen(a: argparse.Namespace) -> int:
@@ -238,6 +268,10 @@ def build_parser() -> argparse.ArgumentParser:
     r.add_argument("--workers", type=int, default=0,
                    help="N competing-consumer processes on the same queues (amqp); metrics port + worker id")
     r.set_defaults(fn=cmd_run)
+
+    c = sub.add_parser("config", help="validate and print the effective config (secrets masked)")
+    c.add_argument("--config")
+    c.set_defaults(fn=cmd_config)
 
     g = sub.add_parser("gen", help="generate synthetic framed telemetry")
     g.add_argument("--events", type=int, default=100)

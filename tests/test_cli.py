@@ -96,3 +96,17 @@ def test_seed_sqlite_and_publish_to_broker(tmp_path):
         assert r.returncode == 0 and r.stdout.strip() == b"40"
         depth = bt.call(lambda b: b.depth(STATUS) + b.depth(PROGRESS))
     assert depth == 40
+
+
+def test_config_command_masks_secrets(tmp_path):
+    cfg = tmp_path / "events.yaml"
+    cfg.write_text("keys: {trello: {key: SECRETK, token: SECRETT}, telegram: {token: 'SECRET:TG'}}\n"
+                   "instance: {flow_ids: {queued: L1}}\n"
+                   "service: {store: {backend: postgres, dsn: 'postgres://u:SECRETPW@db/media'}}\n")
+    r = cli("config", "--config", str(cfg))
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    assert b"SECRET" not in r.stdout
+    assert out["config"]["instance"]["flow_ids"] == {"queued": "L1"}
+    assert out["config"]["service"]["store"]["dsn"] == "postgres://u:***@db/media"
+    assert out["config"]["service"]["prefetch"] == 100
