@@ -302,6 +302,8 @@ def main(argv=None) -> int:
             "p50_ingest_latency_us": round(ih.percentile(50) / 1e3, 3),
             "http_requests": sum(p["http_calls"] for p in parts),
             "handler_errors": sum(p["errors"] for p in parts),
+            "notes": "CPU event-consumer workload (the reference has no device compute; see docs/DESIGN.md); "
+                     "each consumer process runs the full service path on its own synthetic stream",
         }
         print(json.dumps(out), flush=True)
     dist.close()
