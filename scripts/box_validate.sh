@@ -19,5 +19,7 @@ if [ $? -eq 0 ]; then
       -d "$GRAFT_REPO_ROOT/gpurun_out/rocprof" -o bench -- python3 "$GRAFT_REPO_ROOT/bench.py" \
       --steps 3 --warmup 1 --procs-per-rank 1 > "$GRAFT_REPO_ROOT/gpurun_out/rocprof_bench.log" 2>&1 )
   echo "rocprof rc=$?" >> gpurun_out/rocprof_bench.log
-  find gpurun_out/rocprof -type f | head -50 > gpurun_out/rocprof_files.txt 2>&1
+  (find gpurun_out/rocprof -type f 2>/dev/null || echo "no rocprof output files (no kernel dispatches)") \
+    > gpurun_out/rocprof_files.txt
 fi
+true
