@@ -38,7 +38,7 @@ from typing import Dict, List, Optional
 
 from .generator import Workload, bench_config
 
-CONFIGS = ("plumbing", "firehose_1k", "rate_10k", "backpressure", "soak", "amqp", "io_bound")
+CONFIGS = ("plumbing", "firehose_1k", "rate_10k", "backpressure", "soak", "amqp", "io_bound", "http_tcp")
 
 
 def _rss_mb() -> float:
@@ -54,6 +54,7 @@ class GcPauses:
 
     def __init__(self):
         self.pauses_ns: List[int] = []
+        self.by_gen = [0, 0, 0]
         self._t0 = 0
 
     def _cb(self, phase, info):
@@ -61,6 +62,7 @@ class GcPauses:
             self._t0 = time.perf_counter_ns()
         elif self._t0:
             self.pauses_ns.append(time.perf_counter_ns() - self._t0)
+            self.by_gen[info["generation"]] += 1
             self._t0 = 0
 
     def __enter__(self):
@@ -79,7 +81,7 @@ class GcPauses:
             return p[min(len(p) - 1, int(q / 100 * len(p)))] / 1e3
 
         return {"count": len(p), "p50_us": pct(50), "p99_us": pct(99), "max_us": p[-1] / 1e3,
-                "total_ms": sum(p) / 1e6}
+                "total_ms": sum(p) / 1e6, "by_generation": list(self.by_gen)}
 
 
 class _Producer(threading.Thread):
@@ -122,7 +124,8 @@ class _Producer(threading.Thread):
 
 async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_events: int = 0,
                       n_media: int = 10000, media=None, log_level: str = "info", rss_probe=None,
-                      sink_delay_s: float = 0.0) -> dict:
+                      sink_delay_s: float = 0.0, gc_probe: "Optional[GcPauses]" = None,
+                      http=None, sink_url: Optional[str] = None) -> dict:
     from ..config import Config
     from ..service import Service
     from ..sinks import RecordingHttpClient
@@ -133,9 +136,13 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
     rfd, wfd = os.pipe()
     cfgd = bench_config()
     cfgd["service"]["log"]["level"] = log_level
+    if sink_url:  # real HTTP: every sink points at the fake endpoint
+        cfgd["service"]["endpoints"] = {"trello": sink_url, "telegram": sink_url}
+        cfgd["instance"]["emby"]["host"] = sink_url
     sink = open(os.devnull, "w", buffering=1 << 16)
     src = FdSource(fd=rfd, policy=policy, capacity_events=capacity_events)
-    http = RecordingHttpClient(keep=8, delay_s=sink_delay_s)
+    if http is None:
+        http = RecordingHttpClient(keep=8, delay_s=sink_delay_s)
     svc = Service(Config.from_dict(cfgd), source=src, store=MemoryStore(media), http=http,
                   logger=Logger(stream=sink, level=log_level), serve_metrics=False)
     max_inflight = [0]
@@ -150,11 +157,18 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
     if rss_probe is not None:
         gc.collect()
         rss_probe.append(_rss_mb())  # service initialised, workload already in memory
+    if gc_probe is not None:
+        gc_probe.__enter__()  # steady state only: init's own collect+freeze is not a run pause
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
     prod.start()
     stats = await svc.run()
     elapsed = time.perf_counter() - t0
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    cpu_s = (ru1.ru_utime + ru1.ru_stime) - (ru0.ru_utime + ru0.ru_stime)
     prod.join()
+    if gc_probe is not None:
+        gc_probe.__exit__(None, None, None)
     if rss_probe is not None:
         rss_probe.append(_rss_mb())  # after 1M events, before teardown
     if sink_delay_s:
@@ -171,7 +185,10 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
         "ingest_latency_us": {k: v / 1e3 for k, v in stats["ingest_latency_ns"].items() if k.startswith("p")},
         "handle_latency_us": {k: v / 1e3 for k, v in stats["handle_latency_ns"].items() if k.startswith("p")},
         "producer_blocked_ms": s["blocked_ns"] / 1e6, "ring_high_water": s["high_water_events"],
-        "sink_requests": http.count, "max_inflight": max_inflight[0],
+        "sink_requests": (http.count if hasattr(http, "count") else
+                          http.counts["requests"] if hasattr(http, "counts") else None),
+        "max_inflight": max_inflight[0],
+        "cpu_us_per_event": cpu_s / s["acked"] * 1e6 if s["acked"] else None,
     }
 
 
@@ -203,14 +220,16 @@ def run_config(name: str, *, duration_s: Optional[float] = None, events: Optiona
         res = asyncio.run(_run_inproc(w.events(events or 100_000), 0, media=w.media, sink_delay_s=0.002))
         res["sink_delay_ms"] = 2.0
         res["prefetch"] = 100
+    elif name == "http_tcp":
+        res = _http_tcp(w, events or 100_000)
     elif name == "amqp":
         res = _amqp(events or 200_000)
     elif name == "soak":
         n = events or 1_000_000
         evs = w.events(n)
         probe: list = []
-        with GcPauses() as g:
-            res = asyncio.run(_run_inproc(evs, 0, media=w.media, rss_probe=probe))
+        g = GcPauses()
+        res = asyncio.run(_run_inproc(evs, 0, media=w.media, rss_probe=probe, gc_probe=g))
         # RSS of the service itself: measured after init with the workload already generated,
         # and again after all n events went through (so the workload's own memory is excluded)
         res["rss_start_mb"] = probe[0]
@@ -222,6 +241,51 @@ def run_config(name: str, *, duration_s: Optional[float] = None, events: Optiona
         raise ValueError(f"unknown config {name!r} (one of {', '.join(CONFIGS)})")
     res["config"] = name
     return res
+
+
+def _http_tcp(w: Workload, n: int, servers: int = 3) -> dict:
+    """Sinks over real TCP: n events through the service with the production HTTP client
+    (``h1``) and with ``aiohttp``, against ``servers`` fake endpoint processes sharing one
+    port. About half the events make a Trello / Telegram / Emby request. ``prefetch`` (100)
+    bounds the requests in flight, as in production."""
+    import subprocess
+
+    from ..sinks import AiohttpClient, H1Client
+
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    cmd = [sys.executable, "-m", "beholder_amd.bench.http_sink_server"]
+    procs = [subprocess.Popen(cmd + ["--port", "0"], stdout=subprocess.PIPE, text=True, env=env, cwd=root)]
+    try:
+        line = procs[0].stdout.readline().split()
+        if not line or line[0] != "READY":
+            raise RuntimeError("fake HTTP endpoint failed to start")
+        port = int(line[1])
+        for _ in range(servers - 1):
+            p = subprocess.Popen(cmd + ["--port", str(port)], stdout=subprocess.PIPE, text=True, env=env, cwd=root)
+            procs.append(p)
+            if not p.stdout.readline().startswith("READY"):
+                raise RuntimeError("fake HTTP endpoint failed to start")
+        url = f"http://127.0.0.1:{port}"
+        evs = w.events(n)
+        out = {"servers": servers, "events": n}
+        for kind, cls in (("h1", H1Client), ("aiohttp", AiohttpClient)):
+            http = cls(timeout_s=30)
+            out[kind] = asyncio.run(_run_inproc(evs, 0, media=w.media, http=http, sink_url=url))
+        return out
+    finally:
+        total = 0
+        for p in procs:
+            p.terminate()
+            try:
+                tail = p.communicate(timeout=10)[0]
+                for ln in tail.split("\n"):
+                    if ln.startswith("DONE requests="):
+                        total += int(ln.split("=", 1)[1])
+            except subprocess.TimeoutExpired:
+                p.kill()
+        if "out" in locals():
+            out["server_requests_total"] = total
 
 
 def _amqp(n: int) -> dict:

@@ -49,7 +49,8 @@ SERVICE_DEFAULTS: dict = {
         "metrics": {"enabled": True, "host": "0.0.0.0", "port": 3000, "default_metrics": True},
         # index.js:11-13 — pino logger named after the file basename.
         "log": {"level": "info", "name": "index.js"},
-        "http": {"timeout_s": 30.0},
+        # outbound sink HTTP: `h1` = native-parsed keep-alive client (sinks/h1.py), `aiohttp` = library client
+        "http": {"timeout_s": 30.0, "client": "h1", "max_per_host": 100, "keepalive_s": 4.0},
         # SURVEY §5 race detection: opt-in per-mediaId serialisation (default off = parity, Q9).
         "ordering": "none",
         # Q1: what to do with a status message whose handler threw.
@@ -273,6 +274,8 @@ class Config:
             raise ConfigError("service.ordering must be 'none' or 'per_media'")
         if svc["on_status_error"] not in ("leave_unacked", "nack_requeue", "nack_drop"):
             raise ConfigError("service.on_status_error must be leave_unacked|nack_requeue|nack_drop")
+        if svc["http"].get("client", "h1") not in ("h1", "aiohttp"):
+            raise ConfigError("service.http.client must be 'h1' or 'aiohttp'")
         fl = self._data.get("instance", {}).get("flow_ids") if isinstance(self._data.get("instance"), Mapping) else None
         if fl is not None and not isinstance(fl, Mapping):
             raise ConfigError("instance.flow_ids must be a mapping of status -> list id")

@@ -87,5 +87,6 @@ int init_ingest_types(PyObject* m);
 int init_text_functions(PyObject* m);
 int init_amqp_types(PyObject* m);
 int init_dispatch_functions(PyObject* m);
+int init_http_types(PyObject* m);
 
 }  // namespace beholder

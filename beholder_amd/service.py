@@ -40,7 +40,7 @@ from .handlers import TelemetryHandlers, err_message
 from .metrics import MetricsServer, NativeHistogramView, Registry, default_metrics
 from .metrics.registry import Gauge
 from .parallel.ordering import KeyedSerializer
-from .sinks import AiohttpClient, EmbyClient, HttpClient, SinkObserver, TelegramClient, TrelloClient
+from .sinks import AiohttpClient, EmbyClient, H1Client, HttpClient, SinkObserver, TelegramClient, TrelloClient
 from .store import MediaStore, open_store
 from .transport.base import Source
 from .ops import dispatch_batch
@@ -80,6 +80,15 @@ def build_source(config: Config, logger: Optional[Logger] = None) -> Source:
         return AmqpSource(url, prefetch=prefetch, retries=int(config.data["service"]["retries"]),
                           logger=logger)
     raise ValueError(f"unknown transport kind {kind!r} (amqp|stdin|file)")
+
+
+def make_http_client(http_cfg) -> HttpClient:
+    """``service.http``: ``client: h1`` (default, sinks/h1.py) or ``aiohttp``."""
+    timeout = float(http_cfg.get("timeout_s", 30.0))
+    if http_cfg.get("client", "h1") == "aiohttp":
+        return AiohttpClient(timeout_s=timeout)
+    return H1Client(timeout_s=timeout, max_per_host=int(http_cfg.get("max_per_host", 100)),
+                    keepalive_s=float(http_cfg.get("keepalive_s", 4.0)))
 
 
 class Service:
@@ -133,7 +142,7 @@ class Service:
         keys = cfg.root.require("keys.trello")
         # 2. Trello client (index.js:25)
         if self._http is None:
-            self._http = AiohttpClient(timeout_s=float(svc["http"]["timeout_s"]))
+            self._http = make_http_client(svc["http"])
         endpoints = svc["endpoints"]
         # 3-4. registry + counters (index.js:27-40)
         if self.registry is None:

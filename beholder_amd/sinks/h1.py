@@ -1,0 +1,419 @@
+"""Keep-alive HTTP/1.1 client for the sinks (default production client).
+
+The reference's outbound calls (index.js:53,83,99,112) go through ``request``.
+The service makes one of these per Trello-created progress event, so the
+client's per-request CPU bounds production throughput. aiohttp costs about
+140 µs of CPU per request on this host. This client is an ``asyncio.Protocol``
+per connection. Response framing is done by the native ``H1Parser``
+(``ops/csrc/py_http.cpp``), and connections are pooled per origin with
+keep-alive. A request costs one ``write`` and one ``data_received`` callback.
+
+Semantics that match ``request`` (the library behind the reference):
+
+* redirects are followed for GET/HEAD only (``followRedirect``; at most 10);
+* bodies are not decompressed (no ``Accept-Encoding`` is sent);
+* the query string is passed through unmodified (``encodeURIComponent``
+  encoding, see :func:`.http.with_query`).
+
+Additions over the reference:
+
+* keep-alive pooling: at most ``max_per_host`` connections per origin, and
+  idle connections expire after ``keepalive_s``;
+* one transparent retry on a fresh connection when a *reused* idle connection
+  dies before any response byte arrives. This applies to idempotent methods only,
+  so a POST (a Trello comment) is never sent twice;
+* a per-request deadline that covers connect, TLS, request and response;
+* HTTP proxies (``HTTP_PROXY``) are not supported.
+"""
+from __future__ import annotations
+
+import asyncio
+import base64
+import collections
+import ssl as _ssl
+import time
+from typing import Deque, Dict, Optional, Tuple
+from urllib.parse import quote, unquote, urljoin
+
+from ..ops import H1Parser
+from .http import HttpClient, HttpError, HttpResponse, redact, with_query
+
+_IDEMPOTENT = frozenset(("GET", "HEAD", "PUT", "DELETE", "OPTIONS"))
+_BODY_METHODS = frozenset(("POST", "PUT", "PATCH", "DELETE"))
+_REDIRECTS = frozenset((301, 302, 303, 307, 308))
+_TICK = 0.05  # deadline sweep period (s): timeouts fire at most this late
+_PATH_SAFE = "".join(chr(c) for c in range(0x21, 0x7F) if chr(c) not in '"<>\\^`{|}')
+
+
+class _Reset(Exception):
+    """The connection closed before the response completed (``started``: bytes of it seen)."""
+
+    def __init__(self, started: bool, detail: str = ""):
+        super().__init__(detail or "socket hang up")
+        self.started = started
+
+
+class _Conn(asyncio.Protocol):
+    __slots__ = ("origin", "parser", "transport", "waiter", "closed", "last_used", "uses", "deadline", "what")
+
+    def __init__(self, origin: "_Origin"):
+        self.origin = origin
+        self.parser = H1Parser()
+        self.transport = None
+        self.waiter: Optional[asyncio.Future] = None
+        self.closed = False
+        self.last_used = 0.0
+        self.uses = 0
+        self.deadline = 0.0
+        self.what = ("", "")
+
+    # -- protocol callbacks --------------------------------------------------
+    def connection_made(self, transport):
+        self.transport = transport
+
+    def data_received(self, data):
+        try:
+            r = self.parser.feed(data)
+        except ValueError as e:
+            self._fail(HttpError(f"HPE_INVALID_RESPONSE: {e}"))
+            self.abort()
+            return
+        if r is not None:
+            w = self.waiter
+            self.waiter = None
+            if w is None or w.done():
+                self.abort()  # unsolicited response
+            else:
+                w.set_result(r)
+
+    def eof_received(self):
+        return False  # let the transport close; connection_lost completes the response
+
+    def connection_lost(self, exc):
+        self.closed = True
+        w = self.waiter
+        self.waiter = None
+        if w is None or w.done():
+            return
+        try:
+            r = self.parser.eof()
+        except ValueError as e:
+            w.set_exception(_Reset(True, f"socket hang up ({e})"))
+            return
+        if r is not None:
+            w.set_result(r)
+        else:
+            w.set_exception(_Reset(False, f"ECONNRESET: {exc}" if exc else "socket hang up"))
+
+    # -- client side ---------------------------------------------------------
+    def _fail(self, exc: BaseException) -> None:
+        w = self.waiter
+        self.waiter = None
+        if w is not None and not w.done():
+            w.set_exception(exc)
+
+    def abort(self) -> None:
+        self.closed = True
+        if self.transport is not None:
+            self.transport.abort()
+
+    def timed_out(self) -> None:
+        m, url = self.what
+        self._fail(HttpError(f"ETIMEDOUT: {m} {redact(url)}"))
+        self.abort()
+
+
+class _Origin:
+    __slots__ = ("scheme", "host", "port", "tls", "host_header", "auth", "idle", "open", "waiters")
+
+    def __init__(self, scheme: str, host: str, port: int, host_header: str, auth: Optional[str]):
+        self.scheme = scheme
+        self.host = host
+        self.port = port
+        self.tls = scheme == "https"
+        self.host_header = host_header
+        self.auth = auth
+        self.idle: Deque[_Conn] = collections.deque()
+        self.open = 0
+        self.waiters: Deque[asyncio.Future] = collections.deque()
+
+
+def _split_url(url: str) -> Tuple[str, str]:
+    """``(scheme://authority, target)``; target keeps path + query, drops the fragment."""
+    i = url.find("://")
+    if i <= 0:
+        raise HttpError(f"Invalid URI \"{redact(url)}\"")
+    k = url.find("/", i + 3)
+    if k < 0:
+        k = len(url)
+    q = url.find("?", i + 3, k)
+    if q >= 0:
+        k = q
+    h = url.find("#", i + 3, k)
+    if h >= 0:
+        k = h
+    target = url[k:]
+    if "#" in target:
+        target = target[:target.index("#")]
+    if not target.startswith("/"):
+        target = "/" + target
+    return url[:k], target
+
+
+class H1Client(HttpClient):
+    """Pooled keep-alive HTTP/1.1 (+TLS) client. See the module docstring."""
+
+    def __init__(self, timeout_s: float = 30.0, user_agent: str = "beholder/1.0", max_per_host: int = 100,
+                 keepalive_s: float = 4.0, ssl_context: Optional[_ssl.SSLContext] = None,
+                 max_redirects: int = 10):
+        self.timeout_s = float(timeout_s)
+        self.user_agent = user_agent
+        self.max_per_host = max(1, int(max_per_host))
+        self.keepalive_s = float(keepalive_s)
+        self.max_redirects = int(max_redirects)
+        self._ssl = ssl_context
+        self._origins: Dict[str, _Origin] = {}
+        self._closed = False
+        self._busy: set = set()
+        self._sweeper = None
+        self._tail = f"User-Agent: {user_agent}\r\n\r\n".encode("latin-1")
+        self._tail_cl0 = f"User-Agent: {user_agent}\r\nContent-Length: 0\r\n\r\n".encode("latin-1")
+        self.counts = {"requests": 0, "connections": 0, "reused": 0, "retries": 0, "errors": 0, "timeouts": 0}
+
+    # -- pool ----------------------------------------------------------------
+    def _origin(self, key: str) -> _Origin:
+        o = self._origins.get(key)
+        if o is not None:
+            return o
+        scheme, _, authority = key.partition("://")
+        scheme = scheme.lower()
+        if scheme not in ("http", "https"):
+            raise HttpError(f"Invalid protocol: {scheme}:")
+        auth = None
+        if "@" in authority:
+            userinfo, authority = authority.rsplit("@", 1)
+            auth = "Basic " + base64.b64encode(unquote(userinfo).encode("utf-8")).decode("ascii")
+        if authority.startswith("["):
+            e = authority.find("]")
+            if e < 0:
+                raise HttpError(f"Invalid URI \"{redact(key)}\"")
+            host, rest = authority[1:e], authority[e + 1:]
+            port_s = rest[1:] if rest.startswith(":") else ""
+        else:
+            host, _, port_s = authority.partition(":")
+        if not host:
+            raise HttpError(f"Invalid URI \"{redact(key)}\"")
+        try:
+            port = int(port_s) if port_s else (443 if scheme == "https" else 80)
+        except ValueError:
+            raise HttpError(f"Invalid URI \"{redact(key)}\"") from None
+        o = _Origin(scheme, host, port, authority, auth)
+        self._origins[key] = o
+        return o
+
+    def _ssl_context(self) -> _ssl.SSLContext:
+        if self._ssl is None:
+            self._ssl = _ssl.create_default_context()
+        return self._ssl
+
+    async def _connect(self, o: _Origin, deadline: float) -> _Conn:
+        loop = asyncio.get_running_loop()
+        conn = _Conn(o)
+        o.open += 1
+        try:
+            remaining = deadline - loop.time()
+            if remaining <= 0:
+                raise asyncio.TimeoutError
+            kw = {"ssl": self._ssl_context(), "server_hostname": o.host} if o.tls else {}
+            await asyncio.wait_for(loop.create_connection(lambda: conn, o.host, o.port, **kw), remaining)
+        except BaseException:
+            o.open -= 1
+            self._wake(o)
+            raise
+        self.counts["connections"] += 1
+        return conn
+
+    async def _acquire(self, o: _Origin, deadline: float, fresh: bool = False) -> _Conn:
+        now = time.monotonic()
+        idle = o.idle
+        while idle and not fresh:
+            c = idle.pop()
+            if not c.closed and now - c.last_used < self.keepalive_s:
+                self.counts["reused"] += 1
+                return c
+            self._drop(c)
+        while o.open >= self.max_per_host:
+            w = asyncio.get_running_loop().create_future()
+            o.waiters.append(w)
+            loop = asyncio.get_running_loop()
+            th = loop.call_at(deadline, lambda: w.done() or w.set_exception(asyncio.TimeoutError()))
+            try:
+                c = await w
+            except asyncio.CancelledError:
+                # a connection handed over just before the cancel must go back to the pool
+                if w.done() and not w.cancelled() and w.exception() is None and w.result() is not None:
+                    self._release(w.result(), True)
+                raise
+            finally:
+                th.cancel()
+            if c is not None:
+                if not c.closed and not fresh:
+                    self.counts["reused"] += 1
+                    return c
+                self._drop(c)
+        return await self._connect(o, deadline)
+
+    def _release(self, c: _Conn, keep: bool) -> None:
+        o = c.origin
+        if not keep or c.closed or self._closed:
+            self._drop(c)
+            return
+        c.last_used = time.monotonic()
+        while o.waiters:
+            w = o.waiters.popleft()
+            if not w.done():
+                w.set_result(c)
+                return
+        o.idle.append(c)
+
+    def _drop(self, c: _Conn) -> None:
+        c.abort()
+        o = c.origin
+        o.open -= 1
+        self._wake(o)
+
+    def _wake(self, o: _Origin) -> None:
+        while o.waiters:
+            w = o.waiters.popleft()
+            if not w.done():
+                w.set_result(None)  # a slot is free: the waiter opens its own connection
+                return
+
+    # -- deadlines -------------------------------------------------------------
+    # One sweep timer per client instead of a TimerHandle per request: busy connections
+    # carry their deadline and are checked every `_TICK` seconds while any is busy.
+    def _arm(self, loop) -> None:
+        self._sweeper = loop.call_later(_TICK, self._sweep, loop)
+
+    def _sweep(self, loop) -> None:
+        self._sweeper = None
+        now = loop.time()
+        for c in [c for c in self._busy if c.deadline <= now]:
+            self._busy.discard(c)
+            self.counts["timeouts"] += 1
+            c.timed_out()
+        if self._busy and not self._closed:
+            self._arm(loop)
+
+    # -- request -------------------------------------------------------------
+    async def request(self, method, url, *, params=None, timeout=None) -> HttpResponse:
+        if self._closed:
+            raise HttpError("client closed")
+        m = method.upper()
+        full = with_query(url, params)
+        loop = asyncio.get_running_loop()
+        deadline = loop.time() + (timeout or self.timeout_s)
+        counts = self.counts
+        counts["requests"] += 1
+        cur = full
+        redirects = 0
+        fresh = False
+        while True:
+            key, target = _split_url(cur)
+            o = self._origin(key)
+            if not target.isascii() or " " in target:
+                target = quote(target, safe=_PATH_SAFE)
+            head = f"{m} {target} HTTP/1.1\r\nHost: {o.host_header}\r\n"
+            if o.auth:
+                head += f"Authorization: {o.auth}\r\n"
+            req = head.encode("latin-1") + (self._tail_cl0 if m in _BODY_METHODS else self._tail)
+            try:
+                c = await self._acquire(o, deadline, fresh)
+            except asyncio.TimeoutError:
+                counts["timeouts"] += 1
+                counts["errors"] += 1
+                raise HttpError(f"ETIMEDOUT: {m} {redact(cur)}") from None
+            except OSError as e:
+                counts["errors"] += 1
+                raise HttpError(f"{_errname(e)}: {m} {redact(cur)}") from None
+            reused = c.uses > 0
+            c.uses += 1
+            w = loop.create_future()
+            c.waiter = w
+            c.deadline = deadline
+            c.what = (m, cur)
+            c.parser.start(head=m == "HEAD")
+            c.transport.write(req)
+            busy = self._busy
+            busy.add(c)
+            if self._sweeper is None:
+                self._arm(loop)
+            try:
+                status, _reason, raw, body, keep = await w
+            except _Reset as e:
+                self._release(c, False)
+                if reused and not e.started and m in _IDEMPOTENT and not fresh:
+                    counts["retries"] += 1
+                    fresh = True
+                    continue
+                counts["errors"] += 1
+                raise HttpError(f"{e}: {m} {redact(cur)}") from None
+            except HttpError:
+                self._release(c, False)
+                counts["errors"] += 1
+                raise
+            except BaseException:
+                self._release(c, False)  # cancelled mid-request: the connection state is unknown
+                raise
+            finally:
+                busy.discard(c)
+            self._release(c, keep and c.parser.buffered == 0)
+            if status in _REDIRECTS and m in ("GET", "HEAD"):
+                loc = _header(raw, b"location")
+                if loc is not None:
+                    redirects += 1
+                    if redirects > self.max_redirects:
+                        counts["errors"] += 1
+                        raise HttpError(f"Exceeded maxRedirects. Probably stuck in a redirect loop {redact(cur)}")
+                    cur = urljoin(cur, loc)
+                    fresh = False
+                    continue
+            return HttpResponse(status, body, url=full, raw_headers=raw)
+
+    def stats(self) -> Dict[str, int]:
+        out = dict(self.counts)
+        out["open"] = sum(o.open for o in self._origins.values())
+        out["idle"] = sum(len(o.idle) for o in self._origins.values())
+        return out
+
+    async def close(self) -> None:
+        self._closed = True
+        if self._sweeper is not None:
+            self._sweeper.cancel()
+            self._sweeper = None
+        for o in self._origins.values():
+            while o.idle:
+                self._drop(o.idle.pop())
+            while o.waiters:
+                w = o.waiters.popleft()
+                if not w.done():
+                    w.set_exception(HttpError("client closed"))
+
+
+def _header(raw: bytes, name: bytes) -> Optional[str]:
+    for line in raw.split(b"\r\n"):
+        k, sep, v = line.partition(b":")
+        if sep and k.strip().lower() == name:
+            return v.strip().decode("latin-1")
+    return None
+
+
+def _errname(e: OSError) -> str:
+    """Node-style error code (ECONNREFUSED, ENOTFOUND-like gaierror names, TLS reason)."""
+    import errno
+    import socket
+    if isinstance(e, _ssl.SSLError):
+        return e.reason or type(e).__name__
+    if isinstance(e, socket.gaierror):
+        return "ENOTFOUND"
+    return errno.errorcode.get(e.errno or 0, type(e).__name__) if e.errno else type(e).__name__

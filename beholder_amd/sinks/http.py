@@ -66,9 +66,13 @@ def with_query(url: str, params: Optional[Mapping[str, Any]]) -> str:
 _BOT_TOKEN = re.compile(r"/bot[^/?#]+")
 
 
+_USERINFO = re.compile(r"^([A-Za-z][A-Za-z0-9+.-]*://)[^/?#@]*@")
+
+
 def redact(url: str) -> str:
-    """URL safe for logs: no query string (Trello key/token ride there), no Telegram bot token."""
-    return _BOT_TOKEN.sub("/bot***", url.split("?", 1)[0])
+    """URL safe for logs: no query string (Trello key/token ride there), no Telegram bot token,
+    no ``user:password@``."""
+    return _USERINFO.sub(r"\1***@", _BOT_TOKEN.sub("/bot***", url.split("?", 1)[0]))
 
 
 class HttpError(Exception):
@@ -85,13 +89,25 @@ class HttpError(Exception):
 
 
 class HttpResponse:
-    __slots__ = ("status", "body", "headers", "url")
+    """``status``, ``body`` (bytes), ``headers`` (lower-cased names; parsed on first access
+    when built from a raw header block) and the requested ``url``."""
 
-    def __init__(self, status: int, body: bytes = b"", headers: Optional[Mapping[str, str]] = None, url: str = ""):
+    __slots__ = ("status", "body", "_headers", "_raw", "url")
+
+    def __init__(self, status: int, body: bytes = b"", headers: Optional[Mapping[str, str]] = None, url: str = "",
+                 raw_headers: Optional[bytes] = None):
         self.status = status
         self.body = body
-        self.headers = dict(headers) if headers else {}
+        self._headers = {k.lower(): v for k, v in headers.items()} if headers else None
+        self._raw = raw_headers
         self.url = url
+
+    @property
+    def headers(self) -> Dict[str, str]:
+        h = self._headers
+        if h is None:
+            h = self._headers = parse_raw_headers(self._raw) if self._raw else {}
+        return h
 
     @property
     def ok(self) -> bool:
@@ -108,6 +124,19 @@ class HttpResponse:
             # request-promise StatusCodeError: `${statusCode} - ${JSON.stringify(body)}`
             raise HttpError(f"{self.status} - {_json.dumps(self.text())}", self.status, self.body)
         return self
+
+
+def parse_raw_headers(raw: bytes) -> Dict[str, str]:
+    """``name: value`` lines → dict (lower-cased names; repeated names joined with ', ' like Node)."""
+    out: Dict[str, str] = {}
+    for line in raw.split(b"\r\n"):
+        k, sep, v = line.partition(b":")
+        if not sep:
+            continue
+        name = k.strip().lower().decode("latin-1")
+        val = v.strip().decode("latin-1")
+        out[name] = f"{out[name]}, {val}" if name in out else val
+    return out
 
 
 class HttpClient(abc.ABC):

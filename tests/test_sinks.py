@@ -1,4 +1,4 @@
-"""Trello / Telegram / Emby sinks over real HTTP (aiohttp -> local fake server).
+"""Trello / Telegram / Emby sinks over real HTTP (both clients -> local fake server).
 
 Pins the outbound contract of SURVEY.md §2.4: methods, paths, query parameters,
 and the error semantics of the two reference HTTP libraries.
@@ -9,12 +9,17 @@ import pytest
 
 from beholder_amd.bench.fakes import FakeHttpServer
 from beholder_amd.metrics import Registry, parse_exposition
-from beholder_amd.sinks import (AiohttpClient, EmbyClient, HttpError, SinkObserver, TelegramClient, TrelloClient,
+from beholder_amd.sinks import (AiohttpClient, EmbyClient, H1Client, HttpError, SinkObserver, TelegramClient, TrelloClient,
                                 deployed_text, redact)
 
 
 def run(coro):
     return asyncio.run(asyncio.wait_for(coro, 30))
+
+
+@pytest.fixture(params=["h1", "aiohttp"])
+def http_cls(request):
+    return H1Client if request.param == "h1" else AiohttpClient
 
 
 @pytest.fixture
@@ -23,9 +28,9 @@ def server():
         yield s
 
 
-def test_trello_comment_and_move_over_http(server):
+def test_trello_comment_and_move_over_http(server, http_cls):
     async def go():
-        http = AiohttpClient(timeout_s=5)
+        http = http_cls(timeout_s=5)
         t = TrelloClient("KEY", "TOK", http, base_url=server.url)
         await t.make_request("post", "/1/cards/C1/actions/comments", {"text": "DEPLOYED: Progress **5%** (_h_)"})
         await t.make_request("put", "/1/cards/C1", {"idList": "L9", "pos": 2})
@@ -38,12 +43,12 @@ def test_trello_comment_and_move_over_http(server):
     ]
 
 
-def test_trello_resolves_on_http_error_status(server):
+def test_trello_resolves_on_http_error_status(server, http_cls):
     """trello npm only rejects on transport errors (index.js:83 move failures surface only then)."""
     server.status_for["/1/cards"] = 401
 
     async def go():
-        http = AiohttpClient(timeout_s=5)
+        http = http_cls(timeout_s=5)
         r = await TrelloClient("k", "t", http, base_url=server.url).make_request("put", "/1/cards/x", {"pos": 2})
         strict = TrelloClient("k", "t", http, base_url=server.url, strict=True)
         with pytest.raises(HttpError):
@@ -53,9 +58,9 @@ def test_trello_resolves_on_http_error_status(server):
     assert run(go()) == 401
 
 
-def test_telegram_and_emby_over_http(server):
+def test_telegram_and_emby_over_http(server, http_cls):
     async def go():
-        http = AiohttpClient(timeout_s=5)
+        http = http_cls(timeout_s=5)
         await TelegramClient("123:ABC", http, base_url=server.url).send_message(
             "-100", deployed_text("Bebop", "1"), "markdown")
         await EmbyClient(server.url, "EK", http).refresh_library()
@@ -68,11 +73,11 @@ def test_telegram_and_emby_over_http(server):
     ]
 
 
-def test_request_promise_semantics_reject_non_2xx(server):
+def test_request_promise_semantics_reject_non_2xx(server, http_cls):
     server.status_for["/emby"] = 500
 
     async def go():
-        http = AiohttpClient(timeout_s=5)
+        http = http_cls(timeout_s=5)
         with pytest.raises(HttpError) as ei:
             await EmbyClient(server.url, "k", http).refresh_library()
         await http.close()
@@ -81,9 +86,9 @@ def test_request_promise_semantics_reject_non_2xx(server):
     assert e.status == 500 and str(e).startswith("500 - ")
 
 
-def test_transport_errors_never_leak_tokens():
+def test_transport_errors_never_leak_tokens(http_cls):
     async def go():
-        http = AiohttpClient(timeout_s=0.5)
+        http = http_cls(timeout_s=0.5)
         with pytest.raises(HttpError) as ei:
             await TelegramClient("SECRET:TOKEN", http, base_url="http://127.0.0.1:9").send_message("c", "t")
         with pytest.raises(HttpError) as ej:
@@ -96,18 +101,20 @@ def test_transport_errors_never_leak_tokens():
     assert redact("https://api.telegram.org/bot1:AB/sendMessage?chat_id=1") == "https://api.telegram.org/bot***/sendMessage"
 
 
-def test_sink_metrics(server):
+def test_sink_metrics(server, http_cls):
     server.status_for["/emby"] = 503
 
     async def go():
         reg = Registry()
         obs = SinkObserver(reg)
-        http = AiohttpClient(timeout_s=5)
+        http = http_cls(timeout_s=5)
         await TrelloClient("k", "t", http, base_url=server.url, observer=obs).make_request("put", "/1/cards/a", {})
         with pytest.raises(HttpError):
             await EmbyClient(server.url, "k", http, observer=obs).refresh_library()
+        refused = http_cls(timeout_s=0.5)
         with pytest.raises(HttpError):
-            await EmbyClient("http://127.0.0.1:9", "k", AiohttpClient(timeout_s=0.5), observer=obs).refresh_library()
+            await EmbyClient("http://127.0.0.1:9", "k", refused, observer=obs).refresh_library()
+        await refused.close()
         await http.close()
         return parse_exposition(reg.render())
     m = run(go())
