@@ -38,7 +38,7 @@ from typing import Dict, List, Optional
 
 from .generator import Workload, bench_config
 
-CONFIGS = ("plumbing", "firehose_1k", "rate_10k", "backpressure", "soak", "amqp", "io_bound", "http_tcp")
+CONFIGS = ("plumbing", "firehose_1k", "rate_10k", "backpressure", "soak", "amqp", "io_bound", "http_tcp", "tcp_e2e")
 
 
 def _rss_mb() -> float:
@@ -222,6 +222,8 @@ def run_config(name: str, *, duration_s: Optional[float] = None, events: Optiona
         res["prefetch"] = 100
     elif name == "http_tcp":
         res = _http_tcp(w, events or 100_000)
+    elif name == "tcp_e2e":
+        res = _tcp_e2e(events or 100_000)
     elif name == "amqp":
         res = _amqp(events or 200_000)
     elif name == "soak":
@@ -243,49 +245,135 @@ def run_config(name: str, *, duration_s: Optional[float] = None, events: Optiona
     return res
 
 
+def _spawn(module: str, copies: int = 1, args=()) -> "tuple":
+    """Starts ``copies`` of a bench endpoint process sharing one port (SO_REUSEPORT).
+    Returns ``(port, procs)``; each process printed ``READY <port>``."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    procs: list = []
+    port = 0
+    try:
+        for _ in range(copies):
+            p = subprocess.Popen([sys.executable, "-m", module, "--port", str(port), *args],
+                                 stdout=subprocess.PIPE, text=True, env=env, cwd=root)
+            procs.append(p)
+            line = p.stdout.readline().split()
+            if not line or line[0] != "READY":
+                raise RuntimeError(f"{module} failed to start")
+            port = int(line[1])
+    except BaseException:
+        _reap(procs)
+        raise
+    return port, procs
+
+
+def _reap(procs) -> Dict[str, int]:
+    """SIGTERM the endpoint processes; sums their ``DONE key=value`` counters."""
+    import subprocess
+    total: Dict[str, int] = {}
+    for p in procs:
+        if p.poll() is None:
+            p.terminate()
+        try:
+            out = p.communicate(timeout=10)[0] or ""
+        except subprocess.TimeoutExpired:
+            p.kill()
+            continue
+        for ln in out.split("\n"):
+            if ln.startswith("DONE "):
+                for kv in ln.split()[1:]:
+                    k, _, v = kv.partition("=")
+                    if v.isdigit():
+                        total[k] = total.get(k, 0) + int(v)
+    return total
+
+
 def _http_tcp(w: Workload, n: int, servers: int = 3) -> dict:
     """Sinks over real TCP: n events through the service with the production HTTP client
     (``h1``) and with ``aiohttp``, against ``servers`` fake endpoint processes sharing one
     port. About half the events make a Trello / Telegram / Emby request. ``prefetch`` (100)
     bounds the requests in flight, as in production."""
-    import subprocess
-
     from ..sinks import AiohttpClient, H1Client
 
-    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
-    cmd = [sys.executable, "-m", "beholder_amd.bench.http_sink_server"]
-    procs = [subprocess.Popen(cmd + ["--port", "0"], stdout=subprocess.PIPE, text=True, env=env, cwd=root)]
+    port, procs = _spawn("beholder_amd.bench.http_sink_server", servers)
+    out: dict = {"servers": servers, "events": n}
     try:
-        line = procs[0].stdout.readline().split()
-        if not line or line[0] != "READY":
-            raise RuntimeError("fake HTTP endpoint failed to start")
-        port = int(line[1])
-        for _ in range(servers - 1):
-            p = subprocess.Popen(cmd + ["--port", str(port)], stdout=subprocess.PIPE, text=True, env=env, cwd=root)
-            procs.append(p)
-            if not p.stdout.readline().startswith("READY"):
-                raise RuntimeError("fake HTTP endpoint failed to start")
         url = f"http://127.0.0.1:{port}"
         evs = w.events(n)
-        out = {"servers": servers, "events": n}
         for kind, cls in (("h1", H1Client), ("aiohttp", AiohttpClient)):
-            http = cls(timeout_s=30)
-            out[kind] = asyncio.run(_run_inproc(evs, 0, media=w.media, http=http, sink_url=url))
-        return out
+            out[kind] = asyncio.run(_run_inproc(evs, 0, media=w.media, http=cls(timeout_s=30), sink_url=url))
     finally:
-        total = 0
-        for p in procs:
-            p.terminate()
-            try:
-                tail = p.communicate(timeout=10)[0]
-                for ln in tail.split("\n"):
-                    if ln.startswith("DONE requests="):
-                        total += int(ln.split("=", 1)[1])
-            except subprocess.TimeoutExpired:
-                p.kill()
-        if "out" in locals():
-            out["server_requests_total"] = total
+        out["server_requests_total"] = _reap(procs).get("requests", 0)
+    return out
+
+
+def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2) -> dict:
+    """Production-shaped: every dependency over real TCP. A replay AMQP broker streams n
+    events (prefetch 100, index.js:43). Each handler reads / updates the media row in a
+    fake Postgres (pipelined ``pgwire``). Every sink call goes to a fake HTTP endpoint
+    (keep-alive ``h1`` client). The fakes are separate processes; the numbers describe
+    the consumer process."""
+    from ..config import Config
+    from ..service import Service
+    from ..sinks import H1Client
+    from ..store.postgres import PostgresStore
+    from ..transport.amqp import AmqpSource
+    from ..utils.log import Logger
+
+    bport, bprocs = _spawn("beholder_amd.bench.replay_broker", 1, ("--events", str(n)))
+    procs = list(bprocs)
+    out: dict = {"events": n, "prefetch": 100}
+    try:
+        hport, hp = _spawn("beholder_amd.bench.http_sink_server", http_servers)
+        procs += hp
+        pport, pp = _spawn("beholder_amd.bench.pg_sink_server", pg_servers, ("--media", "10000", "--seed", "0"))
+        procs += pp
+        url = f"http://127.0.0.1:{hport}"
+
+        async def go():
+            cfgd = bench_config()
+            cfgd["service"]["endpoints"] = {"trello": url, "telegram": url}
+            cfgd["instance"]["emby"]["host"] = url
+            sink = open(os.devnull, "w", buffering=1 << 16)
+            src = AmqpSource(f"amqp://guest:guest@127.0.0.1:{bport}/", prefetch=100)
+            store = PostgresStore(f"postgres://beholder@127.0.0.1:{pport}/media", pool_size=4)
+            http = H1Client(timeout_s=30)
+            svc = Service(Config.from_dict(cfgd), source=src, store=store, http=http, logger=Logger(stream=sink),
+                          serve_metrics=False)
+            await svc.init()
+            ru0 = resource.getrusage(resource.RUSAGE_SELF)
+            t0 = time.perf_counter()
+            task = asyncio.ensure_future(svc.run())
+            while src.settler.acked < n and not task.done():
+                await asyncio.sleep(0.001)
+            elapsed = time.perf_counter() - t0
+            ru1 = resource.getrusage(resource.RUSAGE_SELF)
+            await asyncio.sleep(0.05)  # let the last acks flush
+            svc.request_stop()
+            await task
+            stats = svc.stats()
+            pg_conns = store._pool.connections if store._pool else 0
+            http_stats = http.stats()
+            await svc.close()
+            sink.close()
+            cpu = (ru1.ru_utime + ru1.ru_stime) - (ru0.ru_utime + ru0.ru_stime)
+            return elapsed, stats, cpu, ru1.ru_stime - ru0.ru_stime, pg_conns, http_stats
+
+        elapsed, stats, cpu, sys_s, pg_conns, http_stats = asyncio.run(go())
+        acked = stats["source"]["acked"]
+        out.update({
+            "acked": acked, "elapsed_s": elapsed, "ingest_rate_eps": acked / elapsed,
+            "cpu_us_per_event": cpu / acked * 1e6 if acked else None,
+            "sys_cpu_us_per_event": sys_s / acked * 1e6 if acked else None,
+            "handle_latency_us": {k: v / 1e3 for k, v in stats["handle_latency_ns"].items() if k.startswith("p")},
+            "errors": sum(stats.get("handler_errors", {}).values()),
+            "pg_connections": pg_conns, "http": http_stats,
+        })
+    finally:
+        counters = _reap(procs)
+        out["server_side"] = counters
+    return out
 
 
 def _amqp(n: int) -> dict:

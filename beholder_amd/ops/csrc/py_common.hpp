@@ -88,5 +88,7 @@ int init_text_functions(PyObject* m);
 int init_amqp_types(PyObject* m);
 int init_dispatch_functions(PyObject* m);
 int init_http_types(PyObject* m);
+int init_pg_types(PyObject* m);
+int init_driver_types(PyObject* m);
 
 }  // namespace beholder

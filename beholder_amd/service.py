@@ -43,8 +43,7 @@ from .parallel.ordering import KeyedSerializer
 from .sinks import AiohttpClient, EmbyClient, H1Client, HttpClient, SinkObserver, TelegramClient, TrelloClient
 from .store import MediaStore, open_store
 from .transport.base import Source
-from .ops import dispatch_batch
-from .utils.eager import DONE, ERROR, _drive, run_eager
+from .ops import Driver, dispatch_batch
 from .utils.log import Logger
 
 Handler = Callable[[Any], Any]
@@ -115,6 +114,7 @@ class Service:
         self._routes: List[Optional[Handler]] = [None] * len(T.TOPIC_NAMES_BY_ID)
         self._inflight: set = set()
         self._slot_free: Optional[asyncio.Event] = None
+        self._idle: Optional[asyncio.Event] = None  # set when the last suspended handler finishes
         self._stop = False
         self._running = False
         self._initialized = False
@@ -364,49 +364,49 @@ class Service:
                     user_finish()
         handler = self._routes[d.topic_id]
         d.start()
-        kind, val = run_eager(handler(d))
-        if kind == DONE:
+        coro = handler(d)
+        try:
+            first = coro.send(None)
+        except StopIteration:
             if on_finish is not None:
                 on_finish()
             return
-        if kind == ERROR:
-            self._on_handler_error(d, val)
-            val = None  # the traceback reaches this frame via f_back: don't keep a cycle alive
+        except BaseException as exc:  # noqa: BLE001 — handler errors are data here
+            self._on_handler_error(d, exc)
+            exc = None  # the traceback reaches this frame via f_back: don't keep a cycle alive
             if on_finish is not None:
                 on_finish()
             return
-        task = val
-        self._inflight.add(task)
+        if on_finish is None:
+            self._on_suspend(d, coro, first)
+            return
 
-        def _done(t, d=d):
-            self._inflight.discard(t)
-            if not t.cancelled():
-                exc = t.exception()
-                if exc is not None:
-                    self._on_handler_error(d, exc)
-            if on_finish is not None:
-                on_finish()
-            if self._slot_free is not None and len(self._inflight) < self.prefetch:
-                self._slot_free.set()
-
-        task.add_done_callback(_done)
+        def done(drv, exc, on_finish=on_finish):
+            self._driver_done(drv, exc)
+            on_finish()
+        drv = Driver(coro, done, d)
+        self._inflight.add(drv)
+        drv.start(first)
 
     def _on_suspend(self, d, coro, first_yield) -> bool:
-        """A handler awaited real I/O: continue it in a Task; True = prefetch window full."""
-        task = asyncio.get_running_loop().create_task(_drive(coro, first_yield))
-        self._inflight.add(task)
+        """A handler awaited real I/O: a native Driver resumes it when the awaited future
+        completes (no asyncio.Task). True = prefetch window full."""
+        drv = Driver(coro, self._driver_done, d)
+        inflight = self._inflight
+        inflight.add(drv)
+        drv.start(first_yield)
+        return len(inflight) >= self.prefetch
 
-        def _done(t, d=d):
-            self._inflight.discard(t)
-            if not t.cancelled():
-                exc = t.exception()
-                if exc is not None:
-                    self._on_handler_error(d, exc)
-            if self._slot_free is not None and len(self._inflight) < self.prefetch:
-                self._slot_free.set()
-
-        task.add_done_callback(_done)
-        return len(self._inflight) >= self.prefetch
+    def _driver_done(self, drv, exc) -> None:
+        inflight = self._inflight
+        inflight.discard(drv)
+        if exc is not None and not drv.cancelled:
+            self._on_handler_error(drv.payload, exc)
+        n = len(inflight)
+        if n < self.prefetch and self._slot_free is not None:
+            self._slot_free.set()
+        if not n and self._idle is not None:
+            self._idle.set()
 
     async def _wait_slots(self) -> None:
         while len(self._inflight) >= self.prefetch:
@@ -442,9 +442,15 @@ class Service:
         if self.serializer is not None:
             await self.serializer.drain(self.grace_s)
         if self._inflight:
-            done, pending = await asyncio.wait(list(self._inflight), timeout=self.grace_s)
-            for t in pending:
-                t.cancel()
+            self._idle = asyncio.Event()
+            try:
+                await asyncio.wait_for(self._idle.wait(), self.grace_s)
+            except asyncio.TimeoutError:
+                for drv in list(self._inflight):
+                    drv.cancel()
+                await asyncio.sleep(0)  # deliver the cancellations
+            finally:
+                self._idle = None
 
     async def close(self) -> None:
         """Release transport, store, HTTP client and the metrics server."""

@@ -9,21 +9,32 @@ implements the protocol subset a media store needs:
 * the extended query protocol (Parse / Bind / Describe / Execute / Sync)
   with server-side prepared statements cached per connection — parameters
   are always sent out-of-band, never interpolated into SQL;
-* text-format results decoded by type OID (bool, int2/4/8, float4/8,
-  numeric, text/varchar/name, json, bytea);
+* **pipelining**: queries from concurrent handlers share a connection without
+  waiting for each other. Each is its own Sync group, and all the groups queued in
+  one event-loop iteration go out in one ``write``. With ``prefetch`` 100
+  (index.js:43), up to 100 lookups are in flight on a few connections instead of
+  one round trip per connection at a time;
+* results assembled natively (``ops/csrc/py_pg.cpp`` ``PgReader``): text-format
+  values decoded by type OID (bool, int2/4/8, float4/8, numeric, text/varchar/
+  name, json, bytea). :data:`DECODERS` is the Python reference of that mapping;
 * ``ErrorResponse`` → :class:`PgError` (with SQLSTATE), connection reuse
-  after errors, and a small connection :class:`Pool`.
+  after errors, and a :class:`Pool` that spreads load over up to ``size``
+  connections.
 """
 from __future__ import annotations
 
 import asyncio
 import base64
+import collections
 import hashlib
 import hmac
 import os
 import struct
-from typing import Any, Dict, List, Optional, Sequence, Tuple
+from typing import Any, Deque, Dict, List, Optional, Sequence, Tuple
 from urllib.parse import parse_qs, unquote, urlsplit
+
+from ..ops import PgReader
+from ..ops import native as _native
 
 PROTOCOL_V3 = 196608
 
@@ -117,37 +128,126 @@ class _Scram:
 
 
 # ----------------------------------------------------------- connection -----
-class PgConnection:
+_LOST = object()
+_pg_bind = _native.pg_bind
+_PACK_LEN = struct.Struct("!I").pack
+
+
+class PgConnection(asyncio.Protocol):
+    """One Postgres connection with **pipelined** extended-protocol queries.
+
+    ``execute()`` appends Parse (first use of a statement on this connection) +
+    Bind + Describe + Execute + Sync to an output buffer. The buffer is flushed once
+    per event-loop iteration, so a batch of handlers costs one ``write``. Each
+    Sync group answers exactly one ``execute()``: the native ``PgReader``
+    assembles rows / tag / error per ReadyForQuery, and the results are matched to
+    callers in FIFO order. An error in one group does not affect the next one
+    (Postgres discards until Sync). A parse error evicts the statement from the cache.
+    """
+
     def __init__(self, dsn: str, connect_timeout: float = 10.0):
         self.params = parse_dsn(dsn)
         self.connect_timeout = connect_timeout
-        self.reader: Optional[asyncio.StreamReader] = None
-        self.writer: Optional[asyncio.StreamWriter] = None
         self.server_params: Dict[str, str] = {}
         self.backend_pid = 0
-        self._stmts: Dict[str, str] = {}
-        self._lock = asyncio.Lock()
+        self.notices: Deque[Dict[str, str]] = collections.deque(maxlen=64)
         self.closed = True
+        self._transport = None
+        self._reader = PgReader()
+        self._startup: Optional[asyncio.Queue] = None
+        self._pending: Deque[Tuple[asyncio.Future, Optional[str], bytes]] = collections.deque()
+        self._out: List[bytes] = []
+        self._flush_handle = None
+        self._stmts: Dict[str, bytes] = {}
+        self._n_stmts = 0
+        self._lost_exc: Optional[BaseException] = None
 
+    # -- protocol callbacks --------------------------------------------------
+    def connection_made(self, transport):
+        self._transport = transport
+
+    def data_received(self, data):
+        try:
+            items = self._reader.feed(data)
+        except ValueError as e:
+            self._transport.abort()
+            self._fail_all(PgProtocolError(f"protocol error: {e}"))
+            return
+        for it in items:
+            if len(it) == 4:
+                if not self._pending:
+                    self._transport.abort()
+                    self._fail_all(PgProtocolError("unexpected ReadyForQuery"))
+                    return
+                fut, new_sql, name = self._pending.popleft()
+                rows, tag, err, parse_ok = it
+                if err is not None:
+                    if new_sql is not None and not parse_ok and self._stmts.get(new_sql) == name:
+                        del self._stmts[new_sql]
+                    if not fut.done():
+                        fut.set_exception(PgError(err))
+                elif not fut.done():
+                    fut.set_result((rows, tag))
+            else:
+                self._message(it[0], it[1])
+
+    def _message(self, typ: bytes, body: bytes) -> None:
+        if self._startup is not None:
+            self._startup.put_nowait((typ, body))
+        elif typ == b"S":
+            k, _, v = body.rstrip(b"\x00").partition(b"\x00")
+            self.server_params[k.decode()] = v.decode()
+        elif typ == b"N":
+            self.notices.append(_fields(body))
+        # b"A" NotificationResponse (LISTEN is never used here): ignored
+
+    def connection_lost(self, exc):
+        self.closed = True
+        if self._flush_handle is not None:
+            self._flush_handle.cancel()
+            self._flush_handle = None
+        self._out.clear()
+        if self._startup is not None:
+            self._startup.put_nowait(_LOST)
+        self._fail_all(PgProtocolError(f"connection lost: {exc}" if exc else "connection lost"))
+
+    def _fail_all(self, exc: BaseException) -> None:
+        self.closed = True
+        while self._pending:
+            fut = self._pending.popleft()[0]
+            if not fut.done():
+                fut.set_exception(exc)
+
+    # -- startup -------------------------------------------------------------
     async def _read_msg(self) -> Tuple[bytes, bytes]:
-        hdr = await self.reader.readexactly(5)
-        typ, ln = hdr[:1], struct.unpack("!I", hdr[1:])[0]
-        body = await self.reader.readexactly(ln - 4) if ln > 4 else b""
-        return typ, body
+        item = await self._startup.get()
+        if item is _LOST:
+            raise PgProtocolError("connection lost during startup")
+        return item
 
     def _send(self, typ: bytes, body: bytes) -> None:
-        self.writer.write(typ + struct.pack("!I", len(body) + 4) + body)
+        self._transport.write(typ + _PACK_LEN(len(body) + 4) + body)
 
     async def connect(self) -> "PgConnection":
         p = self.params
-        self.reader, self.writer = await asyncio.wait_for(asyncio.open_connection(p["host"], p["port"]),
-                                                          self.connect_timeout)
-        kv = b"".join(k.encode() + b"\x00" + str(v).encode() + b"\x00" for k, v in
-                      (("user", p["user"]), ("database", p["database"]),
-                       ("application_name", p["application_name"]), ("client_encoding", "UTF8")))
-        body = struct.pack("!I", PROTOCOL_V3) + kv + b"\x00"
-        self.writer.write(struct.pack("!I", len(body) + 4) + body)
-        await asyncio.wait_for(self._auth(), self.connect_timeout)
+        loop = asyncio.get_running_loop()
+        self._reader = PgReader()
+        self._startup = asyncio.Queue()
+        self._stmts.clear()
+        await asyncio.wait_for(loop.create_connection(lambda: self, p["host"], p["port"]), self.connect_timeout)
+        try:
+            kv = b"".join(k.encode() + b"\x00" + str(v).encode() + b"\x00" for k, v in
+                          (("user", p["user"]), ("database", p["database"]),
+                           ("application_name", p["application_name"]), ("client_encoding", "UTF8")))
+            body = struct.pack("!I", PROTOCOL_V3) + kv + b"\x00"
+            self._transport.write(_PACK_LEN(len(body) + 4) + body)
+            await asyncio.wait_for(self._auth(), self.connect_timeout)
+        except BaseException:
+            self._transport.abort()
+            self._startup = None
+            raise
+        self._startup = None
+        self._reader.query_mode = True
         self.closed = False
         return self
 
@@ -197,65 +297,56 @@ class PgConnection:
             else:
                 raise PgProtocolError(f"unexpected message {typ!r} during startup")
 
-    async def execute(self, sql: str, params: Sequence[Any] = ()) -> Tuple[List[Tuple], str]:
-        """Run one statement with ``$n`` parameters. Returns ``(rows, command_tag)``."""
-        async with self._lock:
-            if self.closed:
-                raise PgProtocolError("connection is closed")
-            name = self._stmts.get(sql)
-            parts = []
-            if name is None:
-                name = f"b{len(self._stmts) + 1}"
-                parts.append(_msg(b"P", name.encode() + b"\x00" + sql.encode() + b"\x00" + struct.pack("!H", 0)))
-            enc = [encode_param(v) for v in params]
-            bind = name.encode()
-            bind = b"\x00" + bind + b"\x00" + struct.pack("!H", 0) + struct.pack("!H", len(enc))
-            for e in enc:
-                bind += struct.pack("!i", -1) if e is None else struct.pack("!i", len(e)) + e
-            bind += struct.pack("!H", 0)
-            parts.append(_msg(b"B", bind))
-            parts.append(_msg(b"D", b"P\x00"))
-            parts.append(_msg(b"E", b"\x00" + struct.pack("!I", 0)))
-            parts.append(_msg(b"S", b""))
-            self.writer.write(b"".join(parts))
-            rows: List[Tuple] = []
-            cols: List[int] = []
-            tag = ""
-            err: Optional[PgError] = None
-            parsed_ok = False
-            try:
-                while True:
-                    typ, body = await self._read_msg()
-                    if typ == b"1":
-                        parsed_ok = True
-                    elif typ == b"T":
-                        cols = _row_description(body)
-                    elif typ == b"D":
-                        rows.append(_data_row(body, cols))
-                    elif typ == b"C":
-                        tag = body.rstrip(b"\x00").decode()
-                    elif typ == b"E":
-                        err = PgError(_fields(body))
-                    elif typ == b"Z":
-                        break
-                    # 2 BindComplete, n NoData, s PortalSuspended, I EmptyQuery, N Notice, S ParamStatus: ignore
-            except (asyncio.IncompleteReadError, ConnectionError) as e:
-                self.closed = True
-                raise PgProtocolError(f"connection lost: {e}") from e
-            if parsed_ok or sql in self._stmts:
-                self._stmts[sql] = name
-            if err is not None:
-                raise err
-            return rows, tag
+    # -- queries -------------------------------------------------------------
+    @property
+    def pending(self) -> int:
+        """Queries sent (or buffered) and not yet answered."""
+        return len(self._pending)
+
+    def execute(self, sql: str, params: Sequence[Any] = ()) -> "asyncio.Future[Tuple[List[Tuple], str]]":
+        """Queue one statement with ``$n`` parameters; the returned future resolves to
+        ``(rows, command_tag)`` or raises :class:`PgError`."""
+        if self.closed:
+            raise PgProtocolError("connection is closed")
+        out = self._out
+        name = self._stmts.get(sql)
+        new_sql = None
+        if name is None:
+            self._n_stmts += 1
+            name = b"b%d" % self._n_stmts
+            self._stmts[sql] = name
+            new_sql = sql
+            pbody = name + b"\x00" + sql.encode() + b"\x00\x00\x00"
+            out.append(b"P" + _PACK_LEN(len(pbody) + 4) + pbody)
+        out.append(_pg_bind(name, params))  # Bind + Describe + Execute + Sync (ops/csrc/py_pg.cpp)
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        self._pending.append((fut, new_sql, name))
+        if self._flush_handle is None:
+            self._flush_handle = loop.call_soon(self._flush)
+        return fut
+
+    def _flush(self) -> None:
+        self._flush_handle = None
+        if self._out and not self.closed:
+            data = b"".join(self._out)
+            self._out.clear()
+            self._transport.write(data)
 
     async def close(self) -> None:
-        if self.writer is not None and not self.closed:
+        if self._transport is None or self.closed:
+            self.closed = True
+            return
+        pending = [f for f, _, _ in self._pending]
+        if pending:
+            await asyncio.gather(*pending, return_exceptions=True)
+        if not self.closed:
+            self._flush()
             try:
                 self._send(b"X", b"")
-                await self.writer.drain()
             except (ConnectionError, OSError):
                 pass
-            self.writer.close()
+            self._transport.close()
         self.closed = True
 
 
@@ -271,67 +362,58 @@ def _fields(body: bytes) -> Dict[str, str]:
     return out
 
 
-def _row_description(body: bytes) -> List[int]:
-    n = struct.unpack_from("!H", body)[0]
-    i = 2
-    oids = []
-    for _ in range(n):
-        j = body.index(b"\x00", i)
-        i = j + 1
-        _table, _col, oid, _size, _mod, _fmt = struct.unpack_from("!IhIhih", body, i)
-        oids.append(oid)
-        i += 18
-    return oids
-
-
-def _data_row(body: bytes, oids: List[int]) -> Tuple:
-    n = struct.unpack_from("!H", body)[0]
-    i = 2
-    out = []
-    for k in range(n):
-        ln = struct.unpack_from("!i", body, i)[0]
-        i += 4
-        if ln < 0:
-            out.append(None)
-            continue
-        s = body[i:i + ln].decode("utf-8")
-        i += ln
-        dec = DECODERS.get(oids[k] if k < len(oids) else 25, str)
-        out.append(dec(s))
-    return tuple(out)
-
-
 class Pool:
-    """Fixed-size pool of :class:`PgConnection` (lazy connect, replaces broken connections)."""
+    """Up to ``size`` pipelined :class:`PgConnection` s.
 
-    def __init__(self, dsn: str, size: int = 4):
+    A query goes to the open connection with the fewest queries in flight. A new
+    connection is opened (up to ``size``) only when every open one already has
+    ``spread_at`` or more in flight, so light load stays on one connection and one
+    ``write`` per loop iteration. Broken connections are dropped and replaced on demand.
+    """
+
+    def __init__(self, dsn: str, size: int = 4, spread_at: int = 8):
         self.dsn = dsn
-        self.size = size
-        self._free: "asyncio.Queue[PgConnection]" = asyncio.Queue()
-        self._all: List[PgConnection] = []
+        self.size = max(1, int(size))
+        self.spread_at = spread_at
+        self._conns: List[PgConnection] = []
+        self._lock = asyncio.Lock()
 
     async def open(self) -> "Pool":
-        first = await PgConnection(self.dsn).connect()  # fail fast on bad DSN/credentials
-        self._all.append(first)
-        self._free.put_nowait(first)
-        for _ in range(self.size - 1):
-            c = PgConnection(self.dsn)
-            self._all.append(c)
-            self._free.put_nowait(c)
+        self._conns.append(await PgConnection(self.dsn).connect())  # fail fast on bad DSN/credentials
         return self
 
-    async def execute(self, sql: str, params: Sequence[Any] = ()) -> Tuple[List[Tuple], str]:
-        c = await self._free.get()
-        try:
-            if c.closed:
-                await c.connect()
-            return await c.execute(sql, params)
-        except PgProtocolError:
-            c.closed = True
-            raise
-        finally:
-            self._free.put_nowait(c)
+    def execute(self, sql: str, params: Sequence[Any] = ()):
+        """Awaitable ``(rows, command_tag)`` (a future on the fast path)."""
+        best = None
+        bp = 0
+        for c in self._conns:
+            if not c.closed:
+                n = len(c._pending)
+                if best is None or n < bp:
+                    best, bp = c, n
+        if best is not None and (bp < self.spread_at or len(self._conns) >= self.size):
+            return best.execute(sql, params)
+        return self._execute_slow(sql, params)
+
+    async def _execute_slow(self, sql: str, params: Sequence[Any]):
+        async with self._lock:
+            self._conns = [c for c in self._conns if not c.closed]
+            live = self._conns
+            if len(live) < self.size and (not live or min(len(c._pending) for c in live) >= self.spread_at):
+                try:
+                    c = await PgConnection(self.dsn).connect()
+                    live.append(c)
+                except (OSError, asyncio.TimeoutError, PgError, PgProtocolError):
+                    if not live:
+                        raise
+            c = min(live, key=lambda c: len(c._pending))
+        return await c.execute(sql, params)
+
+    @property
+    def connections(self) -> int:
+        return sum(1 for c in self._conns if not c.closed)
 
     async def close(self) -> None:
-        for c in self._all:
+        for c in self._conns:
             await c.close()
+        self._conns = []

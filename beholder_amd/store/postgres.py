@@ -38,6 +38,8 @@ class PostgresStore(MediaStore):
         self.pool_size = pool_size
         self.create_schema = create_schema
         self._pool: Optional[Pool] = None
+        self._select = f"SELECT {_COLS} FROM {table} WHERE id = $1"
+        self._update = f"UPDATE {table} SET status = $1 WHERE id = $2"
 
     async def connect(self) -> None:
         if self._pool is None:
@@ -61,13 +63,19 @@ class PostgresStore(MediaStore):
         return await self._pool.execute(sql, params)
 
     async def update_status(self, media_id: str, status: int) -> None:
-        await self._exec(f"UPDATE {self.table} SET status = $1 WHERE id = $2", (int(status), media_id))
+        await self._exec(self._update, (int(status), media_id))
 
     async def get_by_id(self, media_id: str) -> Media:
-        rows, _ = await self._exec(f"SELECT {_COLS} FROM {self.table} WHERE id = $1", (media_id,))
+        pool = self._pool
+        if pool is None:
+            await self.connect()
+            pool = self._pool
+        rows, _ = await pool.execute(self._select, (media_id,))
         if not rows:
             raise MediaNotFound(media_id)
         r = rows[0]
+        if None not in r and type(r[2]) is type(r[4]) is type(r[5]) is type(r[7]) is type(r[9]) is int:
+            return Media._make(r)  # int columns arrived as int4/int8: no per-field conversion
         return Media(*(("" if v is None else v) if i in (0, 1, 3, 6, 8) else (0 if v is None else int(v))
                        for i, v in enumerate(r)))
 

@@ -16,7 +16,7 @@ import asyncio
 import itertools
 import os
 import time
-from typing import Any, Callable, Dict, Optional
+from typing import Any, Callable, Dict, List, Optional
 
 from . import wire
 from .wire import AmqpError, Method
@@ -150,7 +150,17 @@ class Channel:
             self.conn._demux.remove_consumer(self.id, consumer_tag)
 
     def basic_ack(self, delivery_tag: int, multiple: bool = False) -> None:
-        self.conn._write(wire.encode_method(self.id, "basic.ack", delivery_tag=delivery_tag, multiple=multiple))
+        self.conn._write(wire.encode_ack(self.id, delivery_tag, multiple))
+
+    def basic_ack_many(self, top: int, tags: List[int]) -> None:
+        """``basic.ack(top, multiple=true)`` (if ``top``) then one ack per tag in ``tags``, one write."""
+        cid = self.id
+        enc = wire.encode_ack
+        frames = [enc(cid, t) for t in tags]
+        if top:
+            frames.insert(0, enc(cid, top, True))
+        if frames:
+            self.conn._write(b"".join(frames))
 
     def basic_nack(self, delivery_tag: int, multiple: bool = False, requeue: bool = True) -> None:
         self.conn._write(wire.encode_method(self.id, "basic.nack", delivery_tag=delivery_tag, multiple=multiple,

@@ -93,12 +93,8 @@ class _AckCoalescer:
             else:
                 rest.append(t)
         self.pending.clear()
-        if top:
-            ch.basic_ack(top, multiple=True)
-            self.frames += 1
-        for t in rest:
-            ch.basic_ack(t)
-            self.frames += 1
+        ch.basic_ack_many(top, rest)
+        self.frames += len(rest) + (1 if top else 0)
 
 
 class AmqpSource(Source):

@@ -249,6 +249,14 @@ def encode_method(channel: int, name: str, **args) -> bytes:
     return struct.pack(">BHI", FRAME_METHOD, channel, len(payload)) + payload + b"\xce"
 
 
+_ACK_FRAME = struct.Struct(">BHIHHQBB")  # method frame: basic.ack(delivery_tag, multiple)
+
+
+def encode_ack(channel: int, delivery_tag: int, multiple: bool = False) -> bytes:
+    """``basic.ack`` method frame (hot path: one per settled delivery or batch)."""
+    return _ACK_FRAME.pack(FRAME_METHOD, channel, 13, 60, 80, delivery_tag, 1 if multiple else 0, 0xCE)
+
+
 def encode_heartbeat() -> bytes:
     return b"\x08\x00\x00\x00\x00\x00\x00\xce"
 

@@ -302,6 +302,12 @@ class _FakeCh:
         self.is_open = True
         self.sent = []
 
+    def basic_ack_many(self, top, tags):
+        if top:
+            self.basic_ack(top, True)
+        for t in tags:
+            self.basic_ack(t)
+
     def basic_ack(self, tag, multiple=False):
         self.sent.append((tag, multiple))
 

@@ -1,0 +1,165 @@
+"""Native Task-free coroutine driver (`ops/csrc/py_driver.cpp`) used for handlers that
+suspend on I/O (index.js:62,127 handlers awaiting the DB / HTTP)."""
+import asyncio
+import gc
+import weakref
+
+import pytest
+
+from beholder_amd.ops import Driver
+
+
+def run(coro):
+    return asyncio.run(asyncio.wait_for(coro, 30))
+
+
+def drive(coro_fn, *args, payload=None):
+    """Starts coro like dispatch_batch does and returns (driver, outcome-future)."""
+    loop = asyncio.get_running_loop()
+    out = loop.create_future()
+    coro = coro_fn(*args)
+    first = coro.send(None)
+    d = Driver(coro, lambda drv, exc: out.set_result((drv, exc)), payload)
+    d.start(first)
+    return d, out
+
+
+def test_results_exceptions_and_payload():
+    async def h(x):
+        await asyncio.sleep(0)  # bare yield: rescheduled through call_soon
+        await asyncio.sleep(0.001)
+        f = asyncio.get_running_loop().create_future()
+        asyncio.get_running_loop().call_soon(f.set_result, x * 2)
+        v = await f
+        if x == 3:
+            raise ValueError(f"boom {v}")
+        return v
+
+    async def go():
+        outs = [drive(h, x, payload=f"p{x}")[1] for x in range(5)]
+        res = await asyncio.gather(*outs)
+        return [(type(e).__name__ if e else None, str(e) if e else None) for _, e in res], res[0][0]
+    res, drv = run(go())
+    assert res[3] == ("ValueError", "boom 6") and [r for i, r in enumerate(res) if i != 3] == [(None, None)] * 4
+    assert drv.done() and drv.steps >= 3 and drv.payload is None  # payload released on completion
+
+
+def test_awaited_exception_is_thrown_into_the_coroutine():
+    async def h():
+        f = asyncio.get_running_loop().create_future()
+        asyncio.get_running_loop().call_soon(f.set_exception, KeyError("k"))
+        try:
+            await f
+        except KeyError as e:
+            return f"caught {e}"
+
+    async def go():
+        d, out = drive(h)
+        return await out
+    drv, exc = run(go())
+    assert exc is None
+
+
+def test_cancel_while_waiting_and_before_rearm():
+    async def hang():
+        await asyncio.sleep(10)
+
+    async def swallow():
+        try:
+            await asyncio.sleep(10)
+        except asyncio.CancelledError:
+            return "cleaned up"
+
+    async def yields_then_waits():
+        await asyncio.sleep(0)
+        await asyncio.sleep(10)
+
+    async def go():
+        d1, o1 = drive(hang)
+        d2, o2 = drive(swallow)
+        d3, o3 = drive(yields_then_waits)
+        assert d3.cancel()  # pending on a bare-yield reschedule: cancelled at the next await
+        await asyncio.sleep(0.01)
+        assert d1.cancel() and d2.cancel()
+        (a, ea), (b, eb), (c, ec) = await asyncio.gather(o1, o2, o3)
+        return ea, a.cancelled, eb, ec, d1.cancel()
+    ea, cancelled, eb, ec, again = run(go())
+    assert isinstance(ea, asyncio.CancelledError) and cancelled
+    assert eb is None  # the coroutine handled the cancellation and returned
+    assert isinstance(ec, asyncio.CancelledError)
+    assert again is False  # cancelling a finished driver is a no-op
+
+
+def test_non_future_yield_raises_runtime_error_inside_the_coroutine():
+    import types
+
+    @types.coroutine
+    def bad():
+        yield 42
+
+    async def h():
+        try:
+            await bad()
+        except RuntimeError as e:
+            return str(e)
+
+    async def go():
+        loop = asyncio.get_running_loop()
+        out = loop.create_future()
+        coro = h()
+        first = coro.send(None)  # 42 reaches the dispatcher
+        Driver(coro, lambda drv, exc: out.set_result(exc)).start(first)
+        return await out
+    assert run(go()) is None
+
+
+def test_keyboard_interrupt_reaches_the_loop_after_on_done():
+    seen = []
+
+    async def h():
+        await asyncio.sleep(0)
+        raise KeyboardInterrupt
+
+    async def go():
+        coro = h()
+        Driver(coro, lambda drv, exc: seen.append(type(exc).__name__)).start(coro.send(None))
+        await asyncio.sleep(0.05)
+    with pytest.raises(KeyboardInterrupt):
+        asyncio.run(go())
+    assert seen == ["KeyboardInterrupt"]
+
+
+def test_start_twice_and_bad_args():
+    async def go():
+        async def h():
+            await asyncio.sleep(0.001)
+        coro = h()
+        d = Driver(coro, lambda drv, exc: None)
+        d.start(coro.send(None))
+        with pytest.raises(RuntimeError):
+            d.start(None)
+        with pytest.raises(TypeError):
+            Driver(coro, "not callable")
+        await asyncio.sleep(0.01)
+    run(go())
+
+
+def test_no_reference_leaks():
+    class Payload:
+        pass
+
+    async def h(p):
+        await asyncio.sleep(0.001)
+
+    async def go():
+        p = Payload()
+        ref = weakref.ref(p)
+        d, out = drive(h, p, payload=p)
+        del p
+        await out
+        dref = weakref.ref(d) if hasattr(d, "__weakref__") else None
+        del d, out
+        return ref, dref
+    ref, _ = run(go())
+    gc.collect()
+    assert ref() is None

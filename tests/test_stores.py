@@ -118,3 +118,184 @@ def test_postgres_store_in_service():
             await pg.stop()
     row, http = run(go())
     assert row.status == 4 and http.count == 3  # move + telegram + emby
+
+
+# ------------------------------------------------- pipelining (store/pgwire.py) --
+
+def test_pipelined_queries_share_one_connection():
+    """Concurrent lookups (as many as prefetch allows, index.js:43) go out back to back on
+    one connection and are answered in order."""
+    async def go():
+        pg = await FakePg(auth="trust").start()
+        try:
+            st = PostgresStore(pg.dsn, create_schema=True, pool_size=1)
+            await st.connect()
+            for i in range(50):
+                await st.upsert(Media(id=f"m{i}", name=f"Show {i}", creator=i % 2, status=i % 5))
+            c = st._pool._conns[0]
+            futs = [asyncio.ensure_future(st.get_by_id(f"m{i}")) for i in range(50)]
+            await asyncio.sleep(0)
+            peak = c.pending
+            got = await asyncio.gather(*futs)
+            assert [m.name for m in got] == [f"Show {i}" for i in range(50)]
+            assert [m.status for m in got] == [i % 5 for i in range(50)]
+            await st.close()
+            return peak
+        finally:
+            await pg.stop()
+    assert run(go()) == 50
+
+
+def test_pipeline_error_isolated_to_its_query():
+    async def go():
+        pg = await FakePg(auth="trust").start()
+        try:
+            c = await PgConnection(pg.dsn).connect()
+            res = await asyncio.gather(c.execute("SELECT 1 + $1", (1,)), c.execute("this is a syntax error"),
+                                       c.execute("SELECT 2 + $1", (2,)), return_exceptions=True)
+            assert res[0] == ([(2,)], "SELECT 1") and res[2] == ([(4,)], "SELECT 1")
+            assert isinstance(res[1], PgError) and res[1].sqlstate == "42601"
+            assert "this is a syntax error" not in c._stmts  # failed Parse evicted from the cache
+            assert await c.execute("SELECT 1 + $1", (9,)) == ([(10,)], "SELECT 1")  # cached statement reused
+            await c.close()
+            return pg.statements_parsed
+        finally:
+            await pg.stop()
+    assert run(go()) == 2  # the two good statements; the bad one failed to parse
+
+
+async def _dropping_server(after_bytes: int):
+    """Accepts one connection, completes trust auth, reads `after_bytes` of queries, drops it."""
+    import struct
+
+    async def serve(r, w):
+        n = struct.unpack("!I", await r.readexactly(4))[0]
+        await r.readexactly(n - 4)
+        w.write(b"R" + struct.pack("!II", 8, 0) + b"Z" + struct.pack("!I", 5) + b"I")
+        await r.readexactly(after_bytes)
+        w.transport.abort()
+    srv = await asyncio.start_server(serve, "127.0.0.1", 0)
+    return srv, srv.sockets[0].getsockname()[1]
+
+
+def test_connection_loss_fails_every_pending_query():
+    async def go():
+        srv, port = await _dropping_server(10)
+        try:
+            c = await PgConnection(f"postgres://u@127.0.0.1:{port}/db").connect()
+            futs = [c.execute("SELECT $1", (i,)) for i in range(5)]
+            res = await asyncio.gather(*futs, return_exceptions=True)
+            assert all(isinstance(e, PgProtocolError) for e in res)
+            assert c.closed
+            with pytest.raises(PgProtocolError):
+                c.execute("SELECT 1")
+        finally:
+            srv.close()
+    run(go())
+
+
+def test_pool_spreads_load_and_replaces_broken_connections():
+    from beholder_amd.store.pgwire import Pool
+
+    async def go():
+        pg = await FakePg(auth="trust").start()
+        try:
+            pool = await Pool(pg.dsn, size=3, spread_at=2).open()
+            assert pool.connections == 1
+            res = await asyncio.gather(*[pool.execute("SELECT $1 + 0", (i,)) for i in range(30)])
+            assert [r[0][0][0] for r in res] == list(range(30))
+            spread = pool.connections
+            pool._conns[0]._transport.abort()  # a broken connection is dropped and replaced
+            await asyncio.sleep(0.01)
+            res = await asyncio.gather(*[pool.execute("SELECT $1 + 0", (i,)) for i in range(10)])
+            assert [r[0][0][0] for r in res] == list(range(10))
+            await pool.close()
+            return spread
+        finally:
+            await pg.stop()
+    assert run(go()) == 3
+
+
+def test_pg_reader_decoding_matches_python_reference():
+    from beholder_amd.ops import native
+    from beholder_amd.store.pgwire import DECODERS
+    cases = [(16, b"t"), (16, b"f"), (20, b"-9223372036854775808"), (21, b"7"), (23, b"42"), (26, b"4294967295"),
+             (700, b"1.5"), (701, b"-2.25e-10"), (701, b"Infinity"), (1700, b"12345678901234567890"),
+             (1700, b"3.14"), (25, "héllo".encode()), (1043, b""), (114, b'{"a": 1}'), (17, b"\\x00ff10")]
+    for oid, raw in cases:
+        assert native.pg_decode_text(oid, raw) == DECODERS[oid](raw.decode()), (oid, raw)
+    assert native.pg_decode_text(99999, b"unknown type") == "unknown type"
+
+
+def test_pg_reader_split_feeding_and_malformed_input():
+    import struct
+
+    from beholder_amd.ops import PgReader
+
+    def m(t, b):
+        return t + struct.pack("!I", len(b) + 4) + b
+    rd = struct.pack("!H", 1) + b"x\x00" + struct.pack("!IhIhih", 0, 0, 23, 4, -1, 0)
+    stream = (m(b"1", b"") + m(b"2", b"") + m(b"T", rd) + m(b"D", struct.pack("!Hi", 1, 2) + b"42") +
+              m(b"C", b"SELECT 1\x00") + m(b"Z", b"I")) * 3
+    for step in (1, 5, 13, len(stream)):
+        r = PgReader()
+        r.query_mode = True
+        out = []
+        for i in range(0, len(stream), step):
+            out += r.feed(stream[i:i + step])
+        assert out == [([(42,)], "SELECT 1", None, True)] * 3 and r.buffered == 0
+    r = PgReader()
+    r.query_mode = True
+    with pytest.raises(ValueError):
+        r.feed(b"D" + struct.pack("!I", 2))  # length < 4
+    with pytest.raises(ValueError):
+        r.feed(m(b"D", struct.pack("!Hi", 1, 50) + b"short"))
+
+
+def test_pg_reader_fuzz_never_crashes():
+    from hypothesis import given, settings, strategies as st
+
+    from beholder_amd.ops import PgReader
+
+    @settings(max_examples=400, deadline=None)
+    @given(st.lists(st.tuples(st.sampled_from(b"12TDCZENSnIA"), st.binary(max_size=40)), max_size=8),
+           st.booleans())
+    def check(msgs, query_mode):
+        import struct
+        r = PgReader(max_message=1 << 16)
+        r.query_mode = query_mode
+        data = b"".join(bytes([t]) + struct.pack("!I", len(b) + 4) + b for t, b in msgs)
+        try:
+            r.feed(data)
+        except ValueError:
+            pass
+    check()
+
+
+def test_pg_bind_matches_python_encoding():
+    """The native Bind encoder (ops/csrc/py_pg.cpp) against encode_param, the Python reference."""
+    import struct
+
+    from hypothesis import given, settings, strategies as st
+
+    from beholder_amd.ops import native
+    from beholder_amd.store.pgwire import encode_param
+
+    def ref(name, params):
+        parts = [b"\x00", name, b"\x00\x00\x00", struct.pack("!H", len(params))]
+        for v in params:
+            e = encode_param(v)
+            parts.append(struct.pack("!i", -1) if e is None else struct.pack("!i", len(e)) + e)
+        parts.append(b"\x00\x00")
+        b = b"".join(parts)
+        return (b"B" + struct.pack("!I", len(b) + 4) + b + b"D" + struct.pack("!I", 6) + b"P\x00" +
+                b"E" + struct.pack("!I", 9) + b"\x00" + struct.pack("!I", 0) + b"S" + struct.pack("!I", 4))
+
+    value = st.one_of(st.none(), st.booleans(), st.integers(), st.floats(allow_nan=False), st.text(),
+                      st.binary(max_size=20))
+
+    @settings(max_examples=300, deadline=None)
+    @given(st.binary(min_size=1, max_size=8).filter(lambda b: b"\x00" not in b), st.lists(value, max_size=12))
+    def check(name, params):
+        assert native.pg_bind(name, tuple(params)) == ref(name, params)
+    check()
