@@ -14,7 +14,7 @@ timeout -k 10 300 python bench.py --procs-per-rank 1 > gpurun_out/bench_1proc.js
 timeout -k 10 600 python -m beholder_amd bench all --out gpurun_out/baseline_configs.json > gpurun_out/baseline.log 2>&1 &&
 timeout -k 10 300 python scripts/profile_consumer.py > gpurun_out/cprofile_consumer.txt 2>&1
 # rocprofv3 kernel trace of the flagship bench: documents that the path dispatches no GPU kernels
-if [ $? -eq 0 ]; then
+if [ $? -eq 0 ] && [ "${SKIP_ROCPROF:-0}" != "1" ]; then
   ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats \
       -d "$GRAFT_REPO_ROOT/gpurun_out/rocprof" -o bench -- python3 "$GRAFT_REPO_ROOT/bench.py" \
       --steps 3 --warmup 1 --procs-per-rank 1 > "$GRAFT_REPO_ROOT/gpurun_out/rocprof_bench.log" 2>&1 )

@@ -24,7 +24,8 @@ def test_native_runtime_is_in_tree_and_loaded():
     assert path.startswith(os.path.realpath(os.path.join(ROOT, "beholder_amd", "ops"))), path
     assert ops.native.ABI_VERSION == 1
     # every hot-path entry point is native
-    for name in ("MessageCodec", "Ingest", "Delivery", "Settler", "Histogram", "format_line", "encode_query"):
+    for name in ("MessageCodec", "Ingest", "Delivery", "Settler", "Histogram", "format_line", "encode_query",
+                 "AmqpDemux", "H1Parser", "PgReader", "Driver", "dispatch_batch", "pg_bind"):
         assert hasattr(ops.native, name), name
 
 
@@ -73,3 +74,13 @@ def test_io_bound_concurrency_reaches_prefetch():
     from beholder_amd.bench import harness
     res = harness.run_config("io_bound", events=20000)
     assert res["acked"] == 20000 and res["max_inflight"] == 100
+
+
+def test_tcp_e2e_every_dependency_over_tcp():
+    """Production shape: AMQP broker -> service -> Postgres (pipelined) + HTTP sinks (keep-alive),
+    all over real sockets; every event acked, every DB read / sink call answered."""
+    from beholder_amd.bench import harness
+    res = harness.run_config("tcp_e2e", events=50_000)
+    assert res["acked"] == 50_000 and res["errors"] == 0, res
+    assert res["server_side"]["queries"] >= 50_000  # one media read per event (index.js:76,140)
+    assert res["server_side"]["requests"] == res["http"]["requests"] and res["http"]["errors"] == 0
