@@ -139,7 +139,8 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
     if sink_url:  # real HTTP: every sink points at the fake endpoint
         cfgd["service"]["endpoints"] = {"trello": sink_url, "telegram": sink_url}
         cfgd["instance"]["emby"]["host"] = sink_url
-    sink = open(os.devnull, "w", buffering=1 << 16)
+    from ..utils.log import ErrorSampleStream
+    sink = ErrorSampleStream()
     src = FdSource(fd=rfd, policy=policy, capacity_events=capacity_events)
     if http is None:
         http = RecordingHttpClient(keep=8, delay_s=sink_delay_s)
@@ -174,7 +175,6 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
     if sink_delay_s:
         watcher.cancel()
     await svc.close()
-    sink.close()
     s = stats["source"]
     return {
         "offered": prod.offered, "accepted": s["pushed"], "dropped": s["dropped_total"],
@@ -189,6 +189,7 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
                           http.counts["requests"] if hasattr(http, "counts") else None),
         "max_inflight": max_inflight[0],
         "cpu_us_per_event": cpu_s / s["acked"] * 1e6 if s["acked"] else None,
+        "error_samples": sink.samples,
     }
 
 

@@ -288,6 +288,27 @@ class NullStream:
         pass
 
 
+class ErrorSampleStream:
+    """Discards lines but keeps the first ``keep`` error-level (50+) lines (benches: why did a
+    run report handler errors?)."""
+
+    def __init__(self, keep: int = 5):
+        self.keep = keep
+        self.samples: list = []
+        self.bytes = 0
+
+    def write(self, s: str) -> int:
+        self.bytes += len(s)
+        if len(self.samples) < self.keep and ('"level":50' in s or '"level":60' in s):
+            for line in s.splitlines():
+                if ('"level":50' in line or '"level":60' in line) and len(self.samples) < self.keep:
+                    self.samples.append(line[:400])
+        return len(s)
+
+    def flush(self) -> None:
+        pass
+
+
 class MemoryStream:
     """Collects lines in memory (tests)."""
 
