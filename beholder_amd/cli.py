@@ -70,6 +70,8 @@ def cmd_run(a: argparse.Namespace) -> int:
         svc_cfg["metrics"]["enabled"] = a.metrics_port >= 0
     if a.store:
         svc_cfg["store"]["backend"] = a.store
+    elif a.media_fixture:
+        svc_cfg["store"]["backend"] = "memory"  # a fixture preloads the in-memory store
     if a.dsn:
         svc_cfg["store"]["dsn"] = a.dsn
     if a.ordering:
@@ -263,7 +265,7 @@ def build_parser() -> argparse.ArgumentParser:
     r.add_argument("--store", choices=["memory", "sqlite", "postgres"])
     r.add_argument("--dsn")
     r.add_argument("--ordering", choices=["none", "per_media"])
-    r.add_argument("--media-fixture", help="JSON list of media rows to preload (memory store)")
+    r.add_argument("--media-fixture", help="JSON list of media rows to preload (implies --store memory)")
     r.add_argument("--stats", action="store_true", help="print final stats JSON to stderr")
     r.add_argument("--workers", type=int, default=0,
                    help="N competing-consumer processes on the same queues (amqp); metrics port + worker id")

@@ -44,7 +44,8 @@ SERVICE_DEFAULTS: dict = {
         # index.js:43 — third AMQP arg; we use it as the reconnect/redelivery retry budget.
         "retries": 2,
         "transport": {"kind": "amqp", "url": None},
-        "store": {"backend": "memory", "dsn": None},
+        # index.js:42 `new Storage()` is always Postgres (triton-core/db); dsn default: dyn('postgres')
+        "store": {"backend": "postgres", "dsn": None, "pool_size": 4, "create_schema": False},
         # index.js:28 — Prom.expose(); port/host are [inferred] (triton-core not vendored).
         "metrics": {"enabled": True, "host": "0.0.0.0", "port": 3000, "default_metrics": True},
         # index.js:11-13 — pino logger named after the file basename.

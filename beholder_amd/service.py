@@ -171,7 +171,10 @@ class Service:
         # 5. store (index.js:42)
         if self._store is None:
             st = svc["store"]
-            self._store = open_store(st.get("backend", "memory"), st.get("dsn"))
+            backend = st.get("backend", "postgres")
+            kw = ({"pool_size": int(st.get("pool_size", 4)), "create_schema": bool(st.get("create_schema", False))}
+                  if backend in ("postgres", "postgresql", "pg") else {})
+            self._store = open_store(backend, st.get("dsn"), **kw)
         await self._store.connect()
 
         # 6. transport (index.js:43-44)

@@ -26,7 +26,7 @@ def test_gen_decode_roundtrip(tmp_path):
 def test_run_stdin_plumbing(tmp_path):
     cfg = tmp_path / "events.yaml"
     cfg.write_text("keys: {trello: {key: k, token: t}}\ninstance: {flow_ids: {queued: L}}\n"
-                   "service: {metrics: {enabled: false}, endpoints: {trello: 'http://127.0.0.1:9',"
+                   "service: {store: {backend: memory}, metrics: {enabled: false}, endpoints: {trello: 'http://127.0.0.1:9',"
                    " telegram: 'http://127.0.0.1:9'}, http: {timeout_s: 0.2}}\n")
     ev = cli("gen", "--events", "30", "--media", "4", "--media-out", str(tmp_path / "m.json"),
              "--progress-fraction", "1.0")
@@ -50,7 +50,7 @@ def test_run_amqp_unreachable_fails_fast(tmp_path):
     """Q10 fix: a startup failure exits non-zero instead of an unhandled rejection."""
     cfg = tmp_path / "events.yaml"
     cfg.write_text("keys: {trello: {key: k, token: t}}\ninstance: {flow_ids: {}}\n"
-                   "service: {metrics: {enabled: false}, retries: 0}\n")
+                   "service: {store: {backend: memory}, metrics: {enabled: false}, retries: 0}\n")
     r = cli("run", "--config", str(cfg), "--source", "amqp", "--url", "amqp://guest:guest@127.0.0.1:1/")
     assert r.returncode == 1 and b"fatal" in r.stderr
 
@@ -58,7 +58,7 @@ def test_run_amqp_unreachable_fails_fast(tmp_path):
 def test_run_stdin_ndjson(tmp_path):
     cfg = tmp_path / "events.yaml"
     cfg.write_text("keys: {trello: {key: k, token: t}}\ninstance: {flow_ids: {}}\n"
-                   "service: {metrics: {enabled: false}}\n")
+                   "service: {store: {backend: memory}, metrics: {enabled: false}}\n")
     (tmp_path / "m.json").write_text('[{"id": "m1", "creator": 0}]')
     lines = "\n".join([
         '{"topic": "v1.telemetry.progress", "json": {"mediaId": "m1", "status": "CONVERTING", "progress": 40}}',
@@ -76,7 +76,7 @@ def test_run_stdin_ndjson(tmp_path):
 def test_run_corrupt_stream_exits_nonzero(tmp_path):
     cfg = tmp_path / "events.yaml"
     cfg.write_text("keys: {trello: {key: k, token: t}}\ninstance: {flow_ids: {}}\n"
-                   "service: {metrics: {enabled: false}}\n")
+                   "service: {store: {backend: memory}, metrics: {enabled: false}}\n")
     r = cli("run", "--config", str(cfg), "--source", "stdin", input=b"\x09\x00\x00\x00\x01abc")  # truncated frame
     assert r.returncode == 1
     assert b"ingest source failed" in r.stdout and b"truncated" in r.stdout

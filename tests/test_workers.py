@@ -22,7 +22,7 @@ def test_strip_workers_arg():
 def test_two_workers_share_the_queue(tmp_path):
     cfg = tmp_path / "events.yaml"
     cfg.write_text("keys: {trello: {key: k, token: t}}\ninstance: {flow_ids: {}}\n"
-                   "service: {metrics: {enabled: false}, log: {level: warn}}\n")
+                   "service: {store: {backend: memory}, metrics: {enabled: false}, log: {level: warn}}\n")
     with BrokerThread() as bt:
         env = dict(os.environ, PYTHONPATH=ROOT)
         p = subprocess.Popen([sys.executable, "-m", "beholder_amd", "run", "--config", str(cfg), "--source", "amqp",
