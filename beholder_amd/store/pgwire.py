@@ -5,7 +5,8 @@ The reference's ``triton-core/db`` talks to Postgres through ``pg`` 7.12
 implements the protocol subset a media store needs:
 
 * startup + authentication: trust, cleartext, MD5 and SCRAM-SHA-256
-  (the Postgres ≥ 14 default);
+  (the Postgres ≥ 14 default); TLS via ``sslmode`` (disable — node-pg's
+  default — prefer, require, verify-ca, verify-full; ``sslrootcert``);
 * the extended query protocol (Parse / Bind / Describe / Execute / Sync)
   with server-side prepared statements cached per connection — parameters
   are always sent out-of-band, never interpolated into SQL;
@@ -63,7 +64,24 @@ def parse_dsn(dsn: str) -> Dict[str, Any]:
         "password": unquote(u.password) if u.password else os.environ.get("PGPASSWORD"),
         "database": unquote(u.path[1:]) if u.path and u.path != "/" else "postgres",
         "application_name": q.get("application_name", "beholder"),
+        # node-pg's default is a plaintext connection; libpq names for the TLS modes
+        "sslmode": q.get("sslmode", os.environ.get("PGSSLMODE", "disable")),
+        "sslrootcert": q.get("sslrootcert"),
     }
+
+
+SSL_MODES = ("disable", "prefer", "require", "verify-ca", "verify-full")
+
+
+def _ssl_context(mode: str, rootcert: Optional[str]):
+    import ssl
+    ctx = ssl.create_default_context(cafile=rootcert) if rootcert else ssl.create_default_context()
+    if mode in ("prefer", "require"):  # libpq: encrypt, no certificate checks
+        ctx.check_hostname = False
+        ctx.verify_mode = ssl.CERT_NONE
+    elif mode == "verify-ca":
+        ctx.check_hostname = False
+    return ctx
 
 
 # ------------------------------------------------------------ type decoding --
@@ -160,13 +178,21 @@ class PgConnection(asyncio.Protocol):
         self._flush_handle = None
         self._stmts: Dict[str, bytes] = {}
         self._n_stmts = 0
-        self._lost_exc: Optional[BaseException] = None
+        self._ssl_answer: Optional[asyncio.Future] = None
+        self.tls = False
 
     # -- protocol callbacks --------------------------------------------------
     def connection_made(self, transport):
         self._transport = transport
 
     def data_received(self, data):
+        w = self._ssl_answer
+        if w is not None:
+            # exactly one byte may precede the TLS handshake; anything more was injected
+            # by a man in the middle (CVE-2021-23222)
+            if not w.done():
+                w.set_result(data if len(data) == 1 else b"?")
+            return
         try:
             items = self._reader.feed(data)
         except ValueError as e:
@@ -209,6 +235,8 @@ class PgConnection(asyncio.Protocol):
         self._out.clear()
         if self._startup is not None:
             self._startup.put_nowait(_LOST)
+        if self._ssl_answer is not None and not self._ssl_answer.done():
+            self._ssl_answer.set_result(b"")
         self._fail_all(PgProtocolError(f"connection lost: {exc}" if exc else "connection lost"))
 
     def _fail_all(self, exc: BaseException) -> None:
@@ -234,8 +262,13 @@ class PgConnection(asyncio.Protocol):
         self._reader = PgReader()
         self._startup = asyncio.Queue()
         self._stmts.clear()
+        mode = p["sslmode"]
+        if mode not in SSL_MODES:
+            raise PgProtocolError(f"invalid sslmode {mode!r} (one of {', '.join(SSL_MODES)})")
         await asyncio.wait_for(loop.create_connection(lambda: self, p["host"], p["port"]), self.connect_timeout)
         try:
+            if mode != "disable":
+                await asyncio.wait_for(self._negotiate_tls(mode, p), self.connect_timeout)
             kv = b"".join(k.encode() + b"\x00" + str(v).encode() + b"\x00" for k, v in
                           (("user", p["user"]), ("database", p["database"]),
                            ("application_name", p["application_name"]), ("client_encoding", "UTF8")))
@@ -250,6 +283,23 @@ class PgConnection(asyncio.Protocol):
         self._reader.query_mode = True
         self.closed = False
         return self
+
+    async def _negotiate_tls(self, mode: str, p: Dict[str, Any]) -> None:
+        """SSLRequest; on 'S' upgrade the transport in place (``loop.start_tls``)."""
+        self._ssl_answer = asyncio.get_running_loop().create_future()
+        self._transport.write(_PACK_LEN(8) + struct.pack("!I", 80877103))
+        ans = await self._ssl_answer
+        self._ssl_answer = None
+        if ans == b"S":
+            ctx = _ssl_context(mode, p.get("sslrootcert"))
+            self._transport = await asyncio.get_running_loop().start_tls(
+                self._transport, self, ctx, server_hostname=p["host"])
+            self.tls = True
+        elif ans == b"N":
+            if mode != "prefer":
+                raise PgProtocolError(f"server does not support SSL, but sslmode={mode}")
+        else:
+            raise PgProtocolError(f"unexpected answer to SSLRequest: {ans!r}")
 
     async def _auth(self) -> None:
         p = self.params

@@ -20,8 +20,10 @@ def _msg(t: bytes, body: bytes) -> bytes:
 
 
 class FakePg:
-    def __init__(self, auth="scram", user="beholder", password="s3cret"):
+    def __init__(self, auth="scram", user="beholder", password="s3cret", ssl_context=None):
         self.auth = auth
+        self.ssl_context = ssl_context  # answer SSLRequest with 'S' and upgrade
+        self.tls_sessions = 0
         self.user = user
         self.password = password
         self.db = sqlite3.connect(":memory:", check_same_thread=False, isolation_level=None)
@@ -53,7 +55,20 @@ class FakePg:
             n = struct.unpack("!I", await r.readexactly(4))[0]
             body = await r.readexactly(n - 4)
             if struct.unpack("!I", body[:4])[0] == 80877103:  # SSLRequest
-                w.write(b"N")
+                if self.ssl_context is None:
+                    w.write(b"N")
+                else:
+                    w.write(b"S")
+                    await w.drain()
+                    # asyncio 3.10 streams have no server-side start_tls: upgrade the transport and
+                    # point the stream objects at the TLS one
+                    proto = w.transport.get_protocol()
+                    tls = await asyncio.get_running_loop().start_tls(w.transport, proto, self.ssl_context,
+                                                                     server_side=True)
+                    w._transport = tls
+                    proto._transport = tls
+                    r._transport = tls
+                    self.tls_sessions += 1
                 n = struct.unpack("!I", await r.readexactly(4))[0]
                 body = await r.readexactly(n - 4)
             kv = body[4:].split(b"\x00")

@@ -299,3 +299,42 @@ def test_pg_bind_matches_python_encoding():
     def check(name, params):
         assert native.pg_bind(name, tuple(params)) == ref(name, params)
     check()
+
+
+def test_postgres_tls_sslmodes(tmp_path):
+    import shutil
+    import ssl
+    import subprocess
+    if shutil.which("openssl") is None:
+        pytest.skip("needs openssl")
+    key, crt = tmp_path / "k.pem", tmp_path / "c.pem"
+    r = subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", str(key), "-out",
+                        str(crt), "-days", "1", "-subj", "/CN=localhost", "-addext", "subjectAltName=DNS:localhost"],
+                       capture_output=True)
+    assert r.returncode == 0, r.stderr
+    sctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+    sctx.load_cert_chain(str(crt), str(key))
+
+    async def go():
+        tls = await FakePg(auth="scram", ssl_context=sctx).start()
+        plain = await FakePg(auth="trust").start()
+        try:
+            base = tls.dsn.replace("127.0.0.1", "localhost")
+            for mode in ("require", "prefer", f"verify-full&sslrootcert={crt}"):
+                c = await PgConnection(f"{base}?sslmode={mode}").connect()
+                assert c.tls and await c.execute("SELECT 1 + $1", (1,)) == ([(2,)], "SELECT 1")
+                await c.close()
+            with pytest.raises(ssl.SSLError):  # verify-full against an unknown CA
+                await PgConnection(f"{base}?sslmode=verify-full").connect()
+            c = await PgConnection(plain.dsn + "?sslmode=prefer").connect()  # server says 'N': plaintext
+            assert not c.tls
+            await c.close()
+            with pytest.raises(PgProtocolError, match="does not support SSL"):
+                await PgConnection(plain.dsn + "?sslmode=require").connect()
+            with pytest.raises(PgProtocolError, match="invalid sslmode"):
+                await PgConnection(plain.dsn + "?sslmode=bogus").connect()
+            return tls.tls_sessions
+        finally:
+            await tls.stop()
+            await plain.stop()
+    assert run(go()) == 3  # the failed verification never completes a handshake
