@@ -31,6 +31,25 @@ from ..ops import Ingest, Settler, frame
 from .base import Source
 
 
+def _grow_pipe(fd: int, size: int) -> None:
+    """If ``fd`` is a pipe, ask for a ``size``-byte kernel buffer (Linux F_SETPIPE_SZ, capped by
+    /proc/sys/fs/pipe-max-size). The default is 64 KiB. A bigger buffer means fewer reads by the
+    reader thread, and fewer writer wake-ups, when events arrive faster than they are consumed."""
+    import fcntl
+    import stat
+    try:
+        if not stat.S_ISFIFO(os.fstat(fd).st_mode):
+            return
+        try:
+            with open("/proc/sys/fs/pipe-max-size") as f:
+                size = min(size, int(f.read()))
+        except (OSError, ValueError):
+            pass
+        fcntl.fcntl(fd, getattr(fcntl, "F_SETPIPE_SZ", 1031), size)
+    except OSError:
+        pass  # not permitted / not Linux: keep the default buffer
+
+
 class FdSource(Source):
     kind = "fd"
 
@@ -64,6 +83,7 @@ class FdSource(Source):
         if self._path is not None:
             fd = os.open(self._path, os.O_RDONLY)
             self._fd = fd
+        _grow_pipe(fd, self.chunk_bytes)
         self._ingest.start_reader(fd, chunk_bytes=self.chunk_bytes, own_fd=self._own_fd)
         self._started = True
 
