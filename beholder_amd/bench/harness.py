@@ -407,20 +407,22 @@ def _amqp(n: int) -> dict:
             svc = Service(Config.from_dict(bench_config()), source=src, store=MemoryStore(w.media),
                           http=RecordingHttpClient(keep=8), logger=Logger(stream=sink), serve_metrics=False)
             await svc.init()
+            ru0 = resource.getrusage(resource.RUSAGE_SELF)
             t0 = time.perf_counter()
             task = asyncio.ensure_future(svc.run())
             while src.settler.acked < n:
                 await asyncio.sleep(0.001)
             elapsed = time.perf_counter() - t0
+            ru1 = resource.getrusage(resource.RUSAGE_SELF)
             await asyncio.sleep(0.05)  # let the last acks flush
             svc.request_stop()
             await task
             stats = svc.stats()
             await svc.close()
             sink.close()
-            return elapsed, stats
+            return elapsed, stats, (ru1.ru_utime + ru1.ru_stime) - (ru0.ru_utime + ru0.ru_stime)
 
-        elapsed, stats = asyncio.run(go())
+        elapsed, stats, cpu = asyncio.run(go())
         tail = proc.stdout.readline().strip()
         proc.wait(30)
     finally:
@@ -428,7 +430,8 @@ def _amqp(n: int) -> dict:
             proc.kill()
     return {"events": n, "acked": stats["source"]["acked"], "elapsed_s": elapsed, "ingest_rate_eps": n / elapsed,
             "handle_latency_us": {k: v / 1e3 for k, v in stats["handle_latency_ns"].items() if k.startswith("p")},
-            "broker": tail, "prefetch": 100, "native_demux": True}
+            "broker": tail, "prefetch": 100, "native_demux": True, "cpu_us_per_event": cpu / n * 1e6,
+            "ack_frames": stats["source"].get("ack_frames")}
 
 
 def _plumbing(w: Workload) -> dict:

@@ -357,6 +357,15 @@ PyObject* demux_stats(AmqpDemuxObject* self, PyObject*) {
                        Py_ssize_t(self->consumers->size()), "buffered", Py_ssize_t(self->carry->size()));
 }
 
+PyObject* demux_get_passthrough(AmqpDemuxObject* self, void*) {
+  return PyLong_FromUnsignedLongLong(self->passthrough);
+}
+
+PyGetSetDef demux_getset[] = {
+    {"passthrough", reinterpret_cast<getter>(demux_get_passthrough), nullptr,
+     "frames handed to Python so far (unchanged across a feed() = the result holds only deliveries)", nullptr},
+    {nullptr, nullptr, nullptr, nullptr, nullptr}};
+
 PyMethodDef demux_methods[] = {
     {"feed", reinterpret_cast<PyCFunction>(demux_feed), METH_O,
      "feed(bytes) -> list of Delivery | (frame_type, channel, payload)"},
@@ -384,6 +393,7 @@ int init_amqp_types(PyObject* m) {
   AmqpDemuxType.tp_traverse = reinterpret_cast<traverseproc>(demux_traverse);
   AmqpDemuxType.tp_clear = reinterpret_cast<inquiry>(demux_clear);
   AmqpDemuxType.tp_methods = demux_methods;
+  AmqpDemuxType.tp_getset = demux_getset;
   if (PyType_Ready(&AmqpDemuxType) < 0) return -1;
   Py_INCREF(&AmqpDemuxType);
   return PyModule_AddObject(m, "AmqpDemux", reinterpret_cast<PyObject*>(&AmqpDemuxType));

@@ -388,8 +388,11 @@ class PgConnection(asyncio.Protocol):
             self.closed = True
             return
         pending = [f for f, _, _ in self._pending]
-        if pending:
-            await asyncio.gather(*pending, return_exceptions=True)
+        if pending:  # let in-flight queries finish, but never hang shutdown on a dead server
+            try:
+                await asyncio.wait_for(asyncio.gather(*pending, return_exceptions=True), self.connect_timeout)
+            except asyncio.TimeoutError:
+                self._transport.abort()
         if not self.closed:
             self._flush()
             try:

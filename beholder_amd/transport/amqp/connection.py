@@ -299,11 +299,11 @@ class Channel:
 class Connection:
     def __init__(self, url: str, *, heartbeat: Optional[int] = None, connect_timeout: float = 10.0,
                  logger=None, on_lost: Optional[Callable[[Optional[BaseException]], None]] = None,
-                 native_settler=None, on_delivery: Optional[Callable[[Any], None]] = None):
-        """``native_settler`` + ``on_delivery`` enable the native delivery path
+                 native_settler=None, on_deliveries: Optional[Callable[[List[Any]], None]] = None):
+        """``native_settler`` + ``on_deliveries`` enable the native delivery path
         (:class:`~beholder_amd.ops.AmqpDemux`): deliveries for consumers
         registered with ``native_topic`` arrive as native ``Delivery`` objects
-        through ``on_delivery``; all other frames take the Python path."""
+        through ``on_deliveries`` (a list per socket read); all other frames take the Python path."""
         self.params = wire.parse_url(url)
         if heartbeat is not None:
             self.params["heartbeat"] = heartbeat
@@ -335,9 +335,9 @@ class Connection:
         self._lost_reported = False
         self.bytes_in = 0
         self.bytes_out = 0
-        self.on_delivery = on_delivery
+        self.on_deliveries = on_deliveries
         self._demux = None
-        if native_settler is not None and on_delivery is not None:
+        if native_settler is not None and on_deliveries is not None:
             from ...ops import AmqpDemux
             self._demux = AmqpDemux(native_settler, 0)
 
@@ -438,16 +438,21 @@ class Connection:
                 self._last_rx = time.monotonic()
                 demux = self._demux
                 if demux is not None:
+                    before = demux.passthrough
                     try:
                         items = demux.feed(data)
                     except ValueError as e:
                         raise wire.FrameError(str(e), wire.FRAME_ERROR) from None
-                    on_delivery = self.on_delivery
-                    for it in items:
-                        if type(it) is tuple:
-                            self._dispatch(*it)
-                        else:
-                            on_delivery(it)
+                    if demux.passthrough == before:
+                        if items:
+                            self.on_deliveries(items)  # only deliveries: hand over the whole list
+                    else:
+                        on_deliveries = self.on_deliveries
+                        for it in items:  # control frames interleaved: keep stream order
+                            if type(it) is tuple:
+                                self._dispatch(*it)
+                            else:
+                                on_deliveries([it])
                 else:
                     for ftype, ch, payload in self._parser.feed(data):
                         self._dispatch(ftype, ch, payload)

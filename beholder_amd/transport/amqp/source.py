@@ -36,28 +36,26 @@ from .wire import AmqpError
 class _AckCoalescer:
     """Per-channel ack batching.
 
-    Deliveries on a channel carry increasing delivery tags. Acks issued during
-    one event-loop iteration are flushed together: the longest *contiguous*
-    prefix of settled tags goes out as one ``basic.ack(multiple=true)``, acks
-    above a gap (a still-pending or nacked delivery) go out individually, so
-    nothing is ever delayed past the current iteration (a never-acked Q1
-    message cannot hold other acks back). ``multiple`` only ever covers tags
-    this consumer has already received on the channel, all of them settled.
+    AMQP delivery tags are a per-channel counter: 1, 2, 3, ... with no gaps for a
+    channel whose consumers are all ours. Acks issued during one event-loop
+    iteration are flushed together. The longest *contiguous* run of settled tags
+    starting at the lowest unsettled one goes out as one
+    ``basic.ack(multiple=true)``. Acks above a gap (a still-pending, abandoned or
+    never-handled delivery) go out individually. Nothing is delayed past the
+    current iteration, so a never-acked Q1 message cannot hold other acks back, and
+    ``multiple`` never covers a tag this process did not settle.
     """
 
-    __slots__ = ("ch", "order", "settled", "pending", "scheduled", "frames", "acks")
+    __slots__ = ("ch", "low", "settled", "pending", "scheduled", "frames", "acks")
 
     def __init__(self, ch: Channel):
         self.ch = ch
-        self.order = collections.deque()   # tags in arrival order, not yet popped
-        self.settled = set()               # settled tags still inside `order`
+        self.low = 1                       # lowest tag not yet covered by a sent/implied ack
+        self.settled = set()               # settled tags >= low
         self.pending: List[int] = []       # acked, not yet sent
         self.scheduled = False
         self.frames = 0
         self.acks = 0
-
-    def seen(self, tag: int) -> None:
-        self.order.append(tag)
 
     def ack(self, tag: int) -> None:
         self.settled.add(tag)
@@ -76,11 +74,13 @@ class _AckCoalescer:
         if not self.pending:
             return
         ch = self.ch
-        order, settled = self.order, self.settled
-        prefix = 0
-        while order and order[0] in settled:
-            prefix = order.popleft()
-            settled.discard(prefix)
+        settled = self.settled
+        low = self.low
+        while low in settled:
+            settled.discard(low)
+            low += 1
+        prefix = low - 1
+        self.low = low
         if not ch.is_open:
             self.pending.clear()
             return
@@ -163,7 +163,7 @@ class AmqpSource(Source):
         conn = Connection(self.url, heartbeat=self.heartbeat, connect_timeout=self.connect_timeout,
                           logger=self.log, on_lost=self._on_lost,
                           native_settler=self._settler if self.native else None,
-                          on_delivery=self._on_native_delivery if self.native else None)
+                          on_deliveries=self._on_native_deliveries if self.native else None)
         await conn.open()
         try:
             ch = await conn.channel()
@@ -184,20 +184,15 @@ class AmqpSource(Source):
     def _on_message(self, ch: Channel, method, props, body: bytes) -> None:
         tid = self._tag_topic.get(method.consumer_tag, 0)
         d = Delivery(body, tid, method.delivery_tag, self._settler, None, method.redelivered, ch)
-        if self._acks is not None:
-            self._acks.seen(method.delivery_tag)
-        self.delivered += 1
-        self._pending.append(d)
-        if len(self._pending) == 1:
-            self._event.set()
+        self._on_native_deliveries([d])
 
-    def _on_native_delivery(self, d) -> None:
-        acks = self._acks
-        if acks is not None:
-            acks.seen(d.tag)
-        self.delivered += 1
-        self._pending.append(d)
-        if len(self._pending) == 1:
+    def _on_native_deliveries(self, ds) -> None:
+        self.delivered += len(ds)
+        pending = self._pending
+        if pending:
+            pending.extend(ds)
+        else:
+            self._pending = ds
             self._event.set()
 
     def _on_settle(self, d, kind: str, requeue: bool) -> None:

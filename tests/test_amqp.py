@@ -317,9 +317,7 @@ def test_ack_coalescer_prefix_gap_and_nack():
 
     async def go():
         ch = _FakeCh()
-        c = _AckCoalescer(ch)
-        for t in range(1, 11):
-            c.seen(t)
+        c = _AckCoalescer(ch)       # tags 1..10 delivered on a fresh channel
         for t in (1, 2, 3, 5, 6):   # 4 still pending (e.g. a Q1 message that is never acked)
             c.ack(t)
         await asyncio.sleep(0)
@@ -335,6 +333,22 @@ def test_ack_coalescer_prefix_gap_and_nack():
         await asyncio.sleep(0)
         assert ch.sent == [(10, False)]  # 9 outstanding -> no multiple
     run(go())
+
+
+def test_ack_coalescer_never_covers_an_unhandled_delivery():
+    """A delivery the process received but never handled (e.g. for a consumer it just
+    cancelled, connection.py `_deliver`) must stay un-acked even when later tags are
+    all acked: `multiple` stops at the gap."""
+    from beholder_amd.transport.amqp.source import _AckCoalescer
+
+    async def go():
+        ch = _FakeCh()
+        c = _AckCoalescer(ch)
+        for t in (1, 2, 4, 5):  # tag 3 never reaches a handler
+            c.ack(t)
+        await asyncio.sleep(0)
+        return ch.sent
+    assert run(go()) == [(2, True), (4, False), (5, False)]
 
 
 def test_amqps_tls_with_ca_verification(tmp_path):
