@@ -64,6 +64,7 @@ AmqpDemux = native.AmqpDemux
 H1Parser = native.H1Parser
 PgReader = native.PgReader
 Driver = native.Driver
+AckBatcher = native.AckBatcher
 dispatch_batch = native.dispatch_batch
 frame = native.frame
 frames = native.frames
@@ -119,7 +120,7 @@ def codec_for(ptype) -> Optional[object]:
 
 
 __all__ = [
-    "native", "AmqpDemux", "Driver", "H1Parser", "PgReader", "MessageCodec", "Ingest", "Delivery", "Settler", "Counter", "Histogram",
+    "native", "AckBatcher", "AmqpDemux", "Driver", "H1Parser", "PgReader", "MessageCodec", "Ingest", "Delivery", "Settler", "Counter", "Histogram",
     "frame", "frames", "mono_ns", "codec_for", "field_table", "format_line", "quick_format", "js_str",
     "js_number", "encode_query", "quote_component",
 ]

@@ -122,7 +122,8 @@ PyMODINIT_FUNC PyInit__native(void) {
   if (init_metric_types(m) < 0 || init_codec_types(m) < 0 || init_ingest_types(m) < 0 ||
       init_text_functions(m) < 0 || init_amqp_types(m) < 0 ||
       init_dispatch_functions(m) < 0 || init_http_types(m) < 0 ||
-      init_pg_types(m) < 0 || init_driver_types(m) < 0) {
+      init_pg_types(m) < 0 || init_driver_types(m) < 0 ||
+      init_ack_types(m) < 0) {
     Py_DECREF(m);
     return nullptr;
   }

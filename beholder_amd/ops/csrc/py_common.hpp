@@ -52,7 +52,13 @@ struct SettlerObject {
   uint64_t created, acked, nacked, rejected, abandoned;
   PyObject* on_settle;   // optional callable(delivery, kind:str, requeue:bool)
   PyObject* on_abandon;  // optional callable(tag, topic_id, content)
+  PyObject* batcher;     // optional AckBatcher: acks of its channel's deliveries stay in C
 };
+
+// AckBatcher hooks (py_acks.cpp): 1 = handled, 0 = other channel, -1 = error
+int ack_batcher_ack(PyObject* batcher, PyObject* channel, uint64_t tag);
+void ack_batcher_abandon(PyObject* batcher, PyObject* channel, uint64_t tag);
+bool is_ack_batcher(PyObject* o);
 extern PyTypeObject SettlerType;
 
 // ---- Delivery: one inbound message (rmsg of index.js:62,127) ---------------
@@ -90,5 +96,6 @@ int init_dispatch_functions(PyObject* m);
 int init_http_types(PyObject* m);
 int init_pg_types(PyObject* m);
 int init_driver_types(PyObject* m);
+int init_ack_types(PyObject* m);
 
 }  // namespace beholder

@@ -39,6 +39,7 @@ PyObject* settler_new(PyTypeObject* type, PyObject*, PyObject*) {
   }
   self->created = self->acked = self->nacked = self->rejected = self->abandoned = 0;
   self->on_settle = nullptr;
+  self->batcher = nullptr;
   self->on_abandon = nullptr;
   return reinterpret_cast<PyObject*>(self);
 }
@@ -64,12 +65,34 @@ int settler_init(SettlerObject* self, PyObject* args, PyObject* kwds) {
 int settler_traverse(SettlerObject* self, visitproc visit, void* arg) {
   Py_VISIT(self->on_settle);
   Py_VISIT(self->on_abandon);
+  Py_VISIT(self->batcher);
   return 0;
 }
 
 int settler_clear(SettlerObject* self) {
   Py_CLEAR(self->on_settle);
   Py_CLEAR(self->on_abandon);
+  Py_CLEAR(self->batcher);
+  return 0;
+}
+
+PyObject* settler_get_batcher(SettlerObject* self, void*) {
+  PyObject* b = self->batcher ? self->batcher : Py_None;
+  Py_INCREF(b);
+  return b;
+}
+
+int settler_set_batcher(SettlerObject* self, PyObject* v, void*) {
+  if (v == nullptr || v == Py_None) {
+    Py_CLEAR(self->batcher);
+    return 0;
+  }
+  if (!is_ack_batcher(v)) {
+    PyErr_SetString(PyExc_TypeError, "ack_batcher must be an AckBatcher or None");
+    return -1;
+  }
+  Py_INCREF(v);
+  Py_XSETREF(self->batcher, v);
   return 0;
 }
 
@@ -131,6 +154,9 @@ PyGetSetDef settler_getset[] = {
     {"rejected", reinterpret_cast<getter>(settler_get_rejected), nullptr, nullptr, nullptr},
     {"abandoned", reinterpret_cast<getter>(settler_get_abandoned), nullptr, nullptr, nullptr},
     {"pending", reinterpret_cast<getter>(settler_get_pending), nullptr, nullptr, nullptr},
+    {"ack_batcher", reinterpret_cast<getter>(settler_get_batcher), reinterpret_cast<setter>(settler_set_batcher),
+     "AckBatcher receiving acks of its channel's deliveries natively (None: every settle calls on_settle)",
+     nullptr},
     {nullptr, nullptr, nullptr, nullptr, nullptr}};
 
 }  // namespace
@@ -217,6 +243,7 @@ void delivery_dealloc(DeliveryObject* self) {
   SettlerObject* s = self->settler;
   if (s && self->state == D_PENDING) {
     s->abandoned++;
+    if (s->batcher && self->extra) ack_batcher_abandon(s->batcher, self->extra, self->tag);
     if (s->on_abandon) {
       PyObject *et, *ev, *tb;
       PyErr_Fetch(&et, &ev, &tb);
@@ -255,6 +282,11 @@ PyObject* settle(DeliveryObject* self, uint8_t to, const char* kind, bool requeu
       s->nacked++;
     else
       s->rejected++;
+    if (to == D_ACKED && s->batcher && self->extra) {
+      int h = ack_batcher_ack(s->batcher, self->extra, self->tag);
+      if (h < 0) return nullptr;
+      if (h == 1) Py_RETURN_NONE;  // queued natively; the source flushes once per loop iteration
+    }
     if (s->on_settle) {
       PyObject* r = PyObject_CallFunction(s->on_settle, "OsO", reinterpret_cast<PyObject*>(self), kind,
                                           requeue ? Py_True : Py_False);

@@ -152,16 +152,6 @@ class Channel:
     def basic_ack(self, delivery_tag: int, multiple: bool = False) -> None:
         self.conn._write(wire.encode_ack(self.id, delivery_tag, multiple))
 
-    def basic_ack_many(self, top: int, tags: List[int]) -> None:
-        """``basic.ack(top, multiple=true)`` (if ``top``) then one ack per tag in ``tags``, one write."""
-        cid = self.id
-        enc = wire.encode_ack
-        frames = [enc(cid, t) for t in tags]
-        if top:
-            frames.insert(0, enc(cid, top, True))
-        if frames:
-            self.conn._write(b"".join(frames))
-
     def basic_nack(self, delivery_tag: int, multiple: bool = False, requeue: bool = True) -> None:
         self.conn._write(wire.encode_method(self.id, "basic.nack", delivery_tag=delivery_tag, multiple=multiple,
                                             requeue=requeue))

@@ -26,75 +26,11 @@ import collections
 import time
 from typing import Dict, List, Optional, Sequence
 
-from ...ops import Delivery, Settler
+from ...ops import AckBatcher, Delivery, Settler
 from ...topics import TOPIC_IDS, topic_id
 from ..base import Source
 from .connection import Channel, Connection
 from .wire import AmqpError
-
-
-class _AckCoalescer:
-    """Per-channel ack batching.
-
-    AMQP delivery tags are a per-channel counter: 1, 2, 3, ... with no gaps for a
-    channel whose consumers are all ours. Acks issued during one event-loop
-    iteration are flushed together. The longest *contiguous* run of settled tags
-    starting at the lowest unsettled one goes out as one
-    ``basic.ack(multiple=true)``. Acks above a gap (a still-pending, abandoned or
-    never-handled delivery) go out individually. Nothing is delayed past the
-    current iteration, so a never-acked Q1 message cannot hold other acks back, and
-    ``multiple`` never covers a tag this process did not settle.
-    """
-
-    __slots__ = ("ch", "low", "settled", "pending", "scheduled", "frames", "acks")
-
-    def __init__(self, ch: Channel):
-        self.ch = ch
-        self.low = 1                       # lowest tag not yet covered by a sent/implied ack
-        self.settled = set()               # settled tags >= low
-        self.pending: List[int] = []       # acked, not yet sent
-        self.scheduled = False
-        self.frames = 0
-        self.acks = 0
-
-    def ack(self, tag: int) -> None:
-        self.settled.add(tag)
-        self.pending.append(tag)
-        self.acks += 1
-        if not self.scheduled:
-            self.scheduled = True
-            asyncio.get_running_loop().call_soon(self.flush)
-
-    def other(self, tag: int) -> None:
-        """A nack/reject was sent immediately: the tag is settled at the broker."""
-        self.settled.add(tag)
-
-    def flush(self) -> None:
-        self.scheduled = False
-        if not self.pending:
-            return
-        ch = self.ch
-        settled = self.settled
-        low = self.low
-        while low in settled:
-            settled.discard(low)
-            low += 1
-        prefix = low - 1
-        self.low = low
-        if not ch.is_open:
-            self.pending.clear()
-            return
-        top = 0
-        rest = []
-        for t in self.pending:
-            if t <= prefix:
-                if t > top:
-                    top = t
-            else:
-                rest.append(t)
-        self.pending.clear()
-        ch.basic_ack_many(top, rest)
-        self.frames += len(rest) + (1 if top else 0)
 
 
 class AmqpSource(Source):
@@ -115,8 +51,12 @@ class AmqpSource(Source):
         self.connect_timeout = connect_timeout
         self.native = native  # assemble deliveries in C (ops.AmqpDemux)
         self.coalesce_acks = coalesce_acks
-        self._acks: Optional[_AckCoalescer] = None
         self._settler = Settler(on_settle=self._on_settle)
+        # acks of the current channel's deliveries are coalesced natively (ops/csrc/py_acks.cpp):
+        # one basic.ack(multiple) for the settled prefix + singles above a gap, one write per
+        # loop iteration; nack/reject and stale settles still go through _on_settle
+        self._batcher: Optional[AckBatcher] = AckBatcher(self._schedule_ack_flush) if coalesce_acks else None
+        self._settler.ack_batcher = self._batcher
         self._topics: List[str] = []
         self._tag_topic: Dict[str, int] = {}
         self._conn: Optional[Connection] = None
@@ -177,7 +117,8 @@ class AmqpSource(Source):
             await conn.close()
             raise
         ch.on_close = self._on_channel_close
-        self._acks = _AckCoalescer(ch) if self.coalesce_acks else None
+        if self._batcher is not None:
+            self._batcher.bind(ch, ch.id)  # fresh channel: delivery tags restart at 1
         self._conn, self._ch, self._tag_topic = conn, ch, tags
         self.connected_since = time.time()
 
@@ -195,20 +136,27 @@ class AmqpSource(Source):
             self._pending = ds
             self._event.set()
 
+    def _schedule_ack_flush(self) -> None:
+        asyncio.get_running_loop().call_soon(self._flush_acks)
+
+    def _flush_acks(self) -> None:
+        b = self._batcher
+        data = b.flush()
+        ch = self._ch
+        if data and ch is not None and ch.is_open and b.channel is ch:
+            ch.conn._write(data)
+
     def _on_settle(self, d, kind: str, requeue: bool) -> None:
+        """Settles the native batcher did not take: nack/reject, stale channels, no batching."""
         ch: Channel = d.extra
         if ch is None or not ch.is_open or ch is not self._ch:
             self.stale_settles += 1  # channel gone: broker already requeued it
             return
-        acks = self._acks
         if kind == "ack":
-            if acks is not None:
-                acks.ack(d.tag)
-            else:
-                ch.basic_ack(d.tag)
+            ch.basic_ack(d.tag)
             return
-        if acks is not None:
-            acks.other(d.tag)
+        if self._batcher is not None:
+            self._batcher.settled_elsewhere(d.tag)
         if kind == "nack":
             ch.basic_nack(d.tag, requeue=requeue)
         else:
@@ -250,8 +198,9 @@ class AmqpSource(Source):
         if self._reconnect_task is not None:
             self._reconnect_task.cancel()
         ch, conn = self._ch, self._conn
-        if self._acks is not None:
-            self._acks.flush()  # acks of the last handlers go out before the channel closes
+        if self._batcher is not None:
+            self._flush_acks()  # acks of the last handlers go out before the channel closes
+            self._batcher.unbind()
         self._ch = None
         if ch is not None and ch.is_open:
             if not self._stopping:
@@ -276,7 +225,9 @@ class AmqpSource(Source):
                   "stale_settles": self.stale_settles, "last_error": self.last_error,
                   "bytes_in": c.bytes_in if c else 0, "bytes_out": c.bytes_out if c else 0,
                   "buffered": len(self._pending),
-                  "ack_frames": self._acks.frames if self._acks else None})
+                  "ack_frames": self._batcher.frames if self._batcher is not None else None,
+                  "ack_multiples": self._batcher.multiples if self._batcher is not None else None,
+                  "ack_stuck_tag": self._batcher.stuck if self._batcher is not None else None})
         return s
 
     # --------------------------------------------------------- recovery ---
@@ -295,6 +246,8 @@ class AmqpSource(Source):
         if self._closing or (self._reconnect_task is not None and not self._reconnect_task.done()):
             return
         self._ch = None
+        if self._batcher is not None:
+            self._batcher.unbind()  # acks of the dead channel's deliveries are stale from now on
         self._reconnect_task = asyncio.get_running_loop().create_task(self._reconnect_loop())
 
     async def _reconnect_loop(self) -> None:

@@ -297,58 +297,96 @@ def test_source_reconnects_after_broker_drop_and_redelivers():
     run(go())
 
 
-class _FakeCh:
-    def __init__(self):
-        self.is_open = True
-        self.sent = []
-
-    def basic_ack_many(self, top, tags):
-        if top:
-            self.basic_ack(top, True)
-        for t in tags:
-            self.basic_ack(t)
-
-    def basic_ack(self, tag, multiple=False):
-        self.sent.append((tag, multiple))
+def _acks(frames: bytes):
+    """basic.ack frames -> [(tag, multiple), ...]"""
+    import struct
+    out = []
+    for i in range(0, len(frames), 21):
+        ftype, ch, size, cls, meth, tag, bits, end = struct.unpack(">BHIHHQBB", frames[i:i + 21])
+        assert (ftype, size, cls, meth, end) == (1, 13, 60, 80, 0xCE)
+        out.append((tag, bool(bits)))
+    return out
 
 
-def test_ack_coalescer_prefix_gap_and_nack():
-    from beholder_amd.transport.amqp.source import _AckCoalescer
-
-    async def go():
-        ch = _FakeCh()
-        c = _AckCoalescer(ch)       # tags 1..10 delivered on a fresh channel
-        for t in (1, 2, 3, 5, 6):   # 4 still pending (e.g. a Q1 message that is never acked)
-            c.ack(t)
-        await asyncio.sleep(0)
-        assert ch.sent == [(3, True), (5, False), (6, False)]
-        ch.sent.clear()
-        c.other(4)                  # 4 nacked (sent immediately elsewhere)
-        for t in (7, 8):
-            c.ack(t)
-        await asyncio.sleep(0)
-        assert ch.sent == [(8, True)]  # 4..8 now contiguous; never covers unseen tags 9, 10
-        ch.sent.clear()
-        c.ack(10)
-        await asyncio.sleep(0)
-        assert ch.sent == [(10, False)]  # 9 outstanding -> no multiple
-    run(go())
+class _Token:
+    pass
 
 
-def test_ack_coalescer_never_covers_an_unhandled_delivery():
-    """A delivery the process received but never handled (e.g. for a consumer it just
-    cancelled, connection.py `_deliver`) must stay un-acked even when later tags are
-    all acked: `multiple` stops at the gap."""
-    from beholder_amd.transport.amqp.source import _AckCoalescer
+def _batcher():
+    from beholder_amd.ops import AckBatcher
+    scheduled = []
+    b = AckBatcher(lambda: scheduled.append(1))
+    ch = _Token()
+    b.bind(ch, 1)
+    return b, ch, scheduled
 
-    async def go():
-        ch = _FakeCh()
-        c = _AckCoalescer(ch)
-        for t in (1, 2, 4, 5):  # tag 3 never reaches a handler
-            c.ack(t)
-        await asyncio.sleep(0)
-        return ch.sent
-    assert run(go()) == [(2, True), (4, False), (5, False)]
+
+def test_ack_batcher_prefix_gap_and_nack():
+    b, ch, scheduled = _batcher()  # tags 1..10 delivered on a fresh channel
+    for t in (1, 2, 3, 5, 6):      # 4 still pending
+        b.ack(t)
+    assert len(scheduled) == 1     # one flush per burst
+    assert _acks(b.flush()) == [(3, True), (5, False), (6, False)]
+    b.settled_elsewhere(4)         # 4 nacked (sent immediately elsewhere)
+    for t in (7, 8):
+        b.ack(t)
+    assert _acks(b.flush()) == [(8, True)]  # 4..8 contiguous now; never covers 9, 10
+    b.ack(10)
+    assert _acks(b.flush()) == [(10, False)]  # 9 outstanding -> no multiple
+    assert b.flush() == b"" and len(scheduled) == 3
+
+
+def test_ack_batcher_never_covers_an_unhandled_delivery():
+    """A delivery received but never handled (connection.py `_deliver` for a cancelled
+    consumer) stays un-acked even when later tags are acked: `multiple` stops at the gap."""
+    b, ch, _ = _batcher()
+    for t in (1, 2, 4, 5):
+        b.ack(t)
+    assert _acks(b.flush()) == [(2, True), (4, False), (5, False)]
+
+
+def test_ack_batcher_abandoned_tag_stops_multiple_and_bounds_memory():
+    """Q1: a status message left un-acked (its Delivery is freed pending) can never be covered
+    by basic.ack(multiple); everything after it is acked singly and nothing is tracked."""
+    b, ch, _ = _batcher()
+    b.ack(1)
+    b.abandon(2)
+    for t in range(3, 1003):
+        b.ack(t)
+    frames = _acks(b.flush())
+    assert frames[0] == (1, True) and all(not m for _, m in frames[1:]) and len(frames) == 1001
+    assert b.stuck == 2 and b.tracked == 0
+
+
+def test_ack_batcher_bounds_tracking_without_an_abandon_report():
+    from beholder_amd.ops import AckBatcher
+    b = AckBatcher(lambda: None, max_settled=100)
+    b.bind(_Token(), 1)
+    for t in range(2, 500):  # tag 1 never settles and is never reported
+        b.ack(t)
+    assert b.tracked <= 100 and b.stuck == 1
+    assert all(not m for _, m in _acks(b.flush()))
+
+
+def test_ack_batcher_native_settle_path():
+    """Delivery.ack() of a bound channel's delivery is queued in C (no on_settle call); other
+    channels and nacks take the Python callback; a freed pending delivery marks its tag stuck."""
+    import gc
+
+    from beholder_amd.ops import Delivery, Settler
+    b, ch, _ = _batcher()
+    calls = []
+    s = Settler(on_settle=lambda d, kind, rq: calls.append((d.tag, kind)))
+    s.ack_batcher = b
+    Delivery(b"x", 1, 1, s, None, False, ch).ack()
+    Delivery(b"x", 1, 2, s, None, False, ch).nack(True)
+    Delivery(b"x", 1, 3, s, None, False, _Token()).ack()  # a stale channel's delivery
+    d4 = Delivery(b"x", 1, 4, s, None, False, ch)
+    del d4
+    gc.collect()
+    assert calls == [(2, "nack"), (3, "ack")] and b.acks == 1 and b.stuck == 4
+    assert _acks(b.flush()) == [(1, True)]
+    assert s.acked == 2 and s.nacked == 1 and s.abandoned == 1
 
 
 def test_amqps_tls_with_ca_verification(tmp_path):
