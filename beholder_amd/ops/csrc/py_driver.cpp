@@ -21,6 +21,10 @@
 //   * cancellation cancels the awaited future;
 //   * KeyboardInterrupt / SystemExit propagate to the loop after on_done.
 // Context variables are not switched. Handlers run in the dispatch loop's context.
+// asyncio.current_task() is not set while a Driver steps a coroutine (and during the
+// eager first step it is the dispatch loop's task). Library code that needs its own
+// task must run in one. sinks/http.py AiohttpClient does this, because aiohttp's
+// timeouts cancel current_task().
 #include "py_common.hpp"
 
 namespace beholder {

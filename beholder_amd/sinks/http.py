@@ -164,6 +164,12 @@ class AiohttpClient(HttpClient):
         return self._session
 
     async def request(self, method, url, *, params=None, timeout=None) -> HttpResponse:
+        # aiohttp's timeout machinery needs asyncio.current_task() to be the request's own task
+        # (it cancels that task on timeout). Handlers run eagerly inside the dispatch loop and are
+        # resumed by a native Driver, not a Task, so the request gets a Task of its own.
+        return await asyncio.ensure_future(self._request(method, url, params, timeout))
+
+    async def _request(self, method, url, params, timeout) -> HttpResponse:
         import aiohttp
         full = with_query(url, params)
         sess = await self._sess()

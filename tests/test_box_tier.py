@@ -84,3 +84,12 @@ def test_tcp_e2e_every_dependency_over_tcp():
     assert res["acked"] == 50_000 and res["errors"] == 0, res
     assert res["server_side"]["queries"] >= 50_000  # one media read per event (index.js:76,140)
     assert res["server_side"]["requests"] == res["http"]["requests"] and res["http"]["errors"] == 0
+
+
+def test_http_tcp_both_clients_error_free():
+    """Sinks over real TCP with the default keep-alive client and with aiohttp: every event
+    acked, no handler errors (aiohttp under the native Driver needs its own task)."""
+    from beholder_amd.bench import harness
+    res = harness.run_config("http_tcp", events=20_000)
+    for kind in ("h1", "aiohttp"):
+        assert res[kind]["acked"] == 20_000 and res[kind]["errors"] == 0, (kind, res[kind]["error_samples"])

@@ -122,3 +122,24 @@ def test_sink_metrics(server, http_cls):
     assert m['beholder_sink_requests_total{sink="emby",code="503"}'] == 1
     assert m['beholder_sink_requests_total{sink="emby",code="error"}'] == 1
     assert m['beholder_sink_request_seconds_count{sink="trello"}'] == 1
+
+
+def test_aiohttp_client_works_under_the_native_driver(server):
+    """aiohttp's timeout context needs a current task; handlers suspended on I/O are resumed by
+    ops.Driver (no Task), so the client runs each request in its own task."""
+    from beholder_amd.ops import Driver
+
+    async def handler(http):
+        await asyncio.sleep(0.001)  # first suspension: from here on the Driver steps us
+        r = await http.request("GET", server.url + "/emby/library/refresh", params={"api_key": "k"})
+        return r.status
+
+    async def go():
+        http = AiohttpClient(timeout_s=5)
+        out = asyncio.get_running_loop().create_future()
+        coro = handler(http)
+        Driver(coro, lambda drv, exc: out.set_result(exc)).start(coro.send(None))
+        exc = await out
+        await http.close()
+        return exc
+    assert run(go()) is None
