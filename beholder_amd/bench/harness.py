@@ -481,7 +481,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     results = {}
     for n in names:
         t0 = time.perf_counter()
-        results[n] = run_config(n, duration_s=a.duration, events=a.events if n == "soak" else None)
+        results[n] = run_config(n, duration_s=a.duration, events=a.events)
         results[n]["wall_s"] = time.perf_counter() - t0
         print(json.dumps(results[n], default=str), flush=True)
     if a.out:
