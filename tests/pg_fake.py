@@ -31,6 +31,15 @@ class FakePg:
         self._server = None
         self.statements_parsed = 0
         self.queries = []
+        self._writers = set()
+        self.connections = 0
+
+    def drop_connections(self) -> int:
+        """Abort every open client connection (a Postgres restart / failover)."""
+        n = len(self._writers)
+        for w in list(self._writers):
+            w.transport.abort()
+        return n
 
     @property
     def dsn(self):
@@ -51,6 +60,8 @@ class FakePg:
         return hdr[:1], (await r.readexactly(n - 4) if n > 4 else b"")
 
     async def _serve(self, r, w):
+        self._writers.add(w)
+        self.connections += 1
         try:
             n = struct.unpack("!I", await r.readexactly(4))[0]
             body = await r.readexactly(n - 4)
@@ -86,6 +97,7 @@ class FakePg:
         except (asyncio.IncompleteReadError, ConnectionError):
             pass
         finally:
+            self._writers.discard(w)
             w.close()
 
     async def _authenticate(self, r, w) -> bool:

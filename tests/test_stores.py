@@ -338,3 +338,49 @@ def test_postgres_tls_sslmodes(tmp_path):
             await tls.stop()
             await plain.stop()
     assert run(go()) == 3  # the failed verification never completes a handshake
+
+
+def test_service_survives_a_postgres_restart():
+    """Connections dropped mid-stream (failover / restart): lookups in flight fail like any
+    DB error (progress handlers warn and ack, Q7), the pool reconnects, and later events
+    are handled normally again."""
+    from beholder_amd.service import Service
+    from beholder_amd.sinks import RecordingHttpClient
+    from beholder_amd.topics import PROGRESS
+    from beholder_amd.transport.memory import MemoryBroker
+    from beholder_amd.utils.log import Logger, MemoryStream
+
+    from helpers import cfg, progress_msg
+
+    async def go():
+        pg = await FakePg(auth="trust").start()
+        try:
+            st = PostgresStore(pg.dsn, create_schema=True, pool_size=2)
+            await st.connect()
+            await st.upsert(M1)  # a Trello-created media: every progress event comments
+            b = MemoryBroker()
+            http = RecordingHttpClient()
+            log = MemoryStream()
+            svc = Service(cfg(), source=b.consumer(), store=st, http=http, logger=Logger(stream=log),
+                          serve_metrics=False)
+            await svc.init()
+            run = asyncio.ensure_future(svc.run())
+            for i in range(20):
+                b.publish(PROGRESS, progress_msg("m1", "CONVERTING", i))
+            while http.count < 20:
+                await asyncio.sleep(0.005)
+            dropped = pg.drop_connections()
+            for i in range(20, 60):
+                b.publish(PROGRESS, progress_msg("m1", "CONVERTING", i))
+                await asyncio.sleep(0.002)
+            b.finish()
+            stats = await run
+            await svc.close()
+            return dropped, http.count, stats, log.records(), pg.connections
+        finally:
+            await pg.stop()
+    dropped, comments, stats, records, conns = run(go())
+    assert dropped >= 1 and conns > dropped  # reconnected after the drop
+    assert stats["source"]["acked"] == 60  # Q7: progress always acks, even on DB errors
+    failed = [r for r in records if r["msg"].startswith("failed to update media progress")]
+    assert comments + len(failed) == 60 and comments >= 50, (comments, len(failed))
