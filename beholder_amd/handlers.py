@@ -114,6 +114,9 @@ class TelemetryHandlers:
         # enumToString tables (index.js:74,134): number -> name, first name wins
         self._status_names_s = self.status_proto.enum("TelemetryStatusEntry")[0]
         self._status_names_p = self.progress_proto.enum("TelemetryStatusEntry")[0]
+        # status -> (statusText, progress_updates_total{status=statusText.toLowerCase()}.inc),
+        # filled on first use so the labelled child appears exactly when the reference creates it
+        self._progress_plan: dict = {}
         # stringToEnum (index.js:94,142)
         self.deployed = proto.string_to_enum(self.status_proto, "TelemetryStatusEntry", "DEPLOYED")
         self.trello_creator = proto.string_to_enum(self.media_proto, "CreatorType", "TRELLO")
@@ -238,11 +241,15 @@ class TelemetryHandlers:
             host = msg.host
 
             log.info("processing progress update on media", media_id, "status", status, "percent", progress)
-            status_text = self._status_names_p.get(status)  # index.js:134
-            if status_text is None:  # Q6
-                raise JsTypeError("Cannot read property 'toLowerCase' of undefined")
-
-            self.progress_counter.child_for(status_text.lower()).inc()  # index.js:136-138
+            plan = self._progress_plan.get(status)
+            if plan is None:
+                status_text = self._status_names_p.get(status)  # index.js:134
+                if status_text is None:  # Q6
+                    raise JsTypeError("Cannot read property 'toLowerCase' of undefined")
+                plan = self._progress_plan[status] = (status_text,
+                                                      self.progress_counter.child_for(status_text.lower()).inc)
+            status_text, count = plan
+            count()  # index.js:136-138
 
             get = self._get_nowait
             media = get(media_id) if get is not None else await self.store.get_by_id(media_id)  # index.js:140

@@ -15,14 +15,16 @@ path (``progress_updates_total.inc({status})``) is one dict lookup + one C call.
 """
 from __future__ import annotations
 
-import bisect
 import math
 import re
 import threading
-from typing import Callable, Dict, Iterable, List, Optional, Sequence, Tuple
+from typing import Any, Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 
 from ..ops import Counter as _NativeCounter
+from ..ops import native as _native
 from ..utils.log import js_number
+
+_Buckets = _native.Buckets
 
 _NAME_RE = re.compile(r"^[a-zA-Z_:][a-zA-Z0-9_:]*$")
 _LABEL_RE = re.compile(r"^[a-zA-Z_][a-zA-Z0-9_]*$")
@@ -216,9 +218,10 @@ class Histogram(Metric):
         if not b:
             raise ValueError("at least one bucket required")
         self.buckets = tuple(b)
-        self._data: Dict[Tuple[str, ...], list] = {}
-        if not self.label_names:
-            self._data[()] = [[0] * len(self.buckets), 0.0, 0]
+        # one native Buckets cell (ops/csrc/py_metrics.cpp) per label set
+        self._data: Dict[Tuple[str, ...], Any] = {}
+        if not label_names:
+            self._data[()] = _Buckets(self.buckets)
 
     def observe(self, labels=None, value: Optional[float] = None) -> None:
         if value is None:
@@ -226,26 +229,24 @@ class Histogram(Metric):
         k = self._key(labels)
         d = self._data.get(k)
         if d is None:
-            d = self._data.setdefault(k, [[0] * len(self.buckets), 0.0, 0])
-        i = bisect.bisect_left(self.buckets, value)
-        if i < len(self.buckets):
-            d[0][i] += 1
-        d[1] += value
-        d[2] += 1
+            d = self._data.setdefault(k, _Buckets(self.buckets))
+        d.observe(value)
 
-    def labels(self, *values) -> "_HistogramChild":
-        """Pre-resolved per-labelset observer (hot path: no label-dict handling per call)."""
+    def labels(self, *values):
+        """Pre-resolved per-labelset cell with ``observe(value)`` (hot path: native, no label
+        handling per call)."""
         key = tuple(str(v) for v in values) if values else ()
         if len(key) != len(self.label_names):
             raise ValueError(f"{self.name} expects {len(self.label_names)} label values")
         d = self._data.get(key)
         if d is None:
-            d = self._data.setdefault(key, [[0] * len(self.buckets), 0.0, 0])
-        return _HistogramChild(self.buckets, d)
+            d = self._data.setdefault(key, _Buckets(self.buckets))
+        return d
 
     def samples(self) -> List[str]:
         out = []
-        for k, (counts, total, n) in list(self._data.items()):
+        for k, cell in list(self._data.items()):
+            counts, total, n = cell.snapshot()
             cum = 0
             for b, c in zip(self.buckets, counts):
                 cum += c
@@ -254,23 +255,6 @@ class Histogram(Metric):
             out.append(f"{self.name}_sum{_label_str(self.label_names, k)} {fmt_value(total)}")
             out.append(f"{self.name}_count{_label_str(self.label_names, k)} {n}")
         return out
-
-
-class _HistogramChild:
-    __slots__ = ("_buckets", "_d", "_nb")
-
-    def __init__(self, buckets, d):
-        self._buckets = buckets
-        self._d = d
-        self._nb = len(buckets)
-
-    def observe(self, value: float) -> None:
-        d = self._d
-        i = bisect.bisect_left(self._buckets, value)
-        if i < self._nb:
-            d[0][i] += 1
-        d[1] += value
-        d[2] += 1
 
 
 class NativeHistogramView(Metric):

@@ -234,7 +234,125 @@ PyGetSetDef counter_getset[] = {{"value", reinterpret_cast<getter>(counter_get),
 PyTypeObject HistogramType = {PyVarObject_HEAD_INIT(nullptr, 0)};
 PyTypeObject CounterType = {PyVarObject_HEAD_INIT(nullptr, 0)};
 
+// ---- Buckets: prom-client fixed-bucket histogram cell (one label set) ----------
+// observe(v) counts v in the first bucket whose upper bound is >= v (`le`), plus sum/count.
+struct BucketsObject {
+  PyObject_HEAD double* bounds;
+  uint64_t* counts;  // per bucket, non-cumulative
+  Py_ssize_t n;
+  double sum;
+  uint64_t count;
+};
+
+PyTypeObject BucketsType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+PyObject* buckets_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
+  static const char* kwlist[] = {"bounds", nullptr};
+  PyObject* seq;
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "O", const_cast<char**>(kwlist), &seq)) return nullptr;
+  PyObject* fast = PySequence_Fast(seq, "bounds must be a sequence of numbers");
+  if (!fast) return nullptr;
+  Py_ssize_t n = PySequence_Fast_GET_SIZE(fast);
+  if (n < 1 || n > 4096) {
+    Py_DECREF(fast);
+    PyErr_SetString(PyExc_ValueError, "1..4096 bucket bounds required");
+    return nullptr;
+  }
+  BucketsObject* self = reinterpret_cast<BucketsObject*>(type->tp_alloc(type, 0));
+  if (!self) {
+    Py_DECREF(fast);
+    return nullptr;
+  }
+  self->bounds = static_cast<double*>(PyMem_Calloc(size_t(n), sizeof(double)));
+  self->counts = static_cast<uint64_t*>(PyMem_Calloc(size_t(n), sizeof(uint64_t)));
+  self->n = n;
+  self->sum = 0.0;
+  self->count = 0;
+  if (!self->bounds || !self->counts) {
+    Py_DECREF(fast);
+    Py_DECREF(self);
+    return PyErr_NoMemory();
+  }
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    double b = PyFloat_AsDouble(PySequence_Fast_GET_ITEM(fast, i));
+    if (b == -1.0 && PyErr_Occurred()) {
+      Py_DECREF(fast);
+      Py_DECREF(self);
+      return nullptr;
+    }
+    if (i && !(b > self->bounds[i - 1])) {
+      Py_DECREF(fast);
+      Py_DECREF(self);
+      PyErr_SetString(PyExc_ValueError, "bucket bounds must be strictly increasing");
+      return nullptr;
+    }
+    self->bounds[i] = b;
+  }
+  Py_DECREF(fast);
+  return reinterpret_cast<PyObject*>(self);
+}
+
+void buckets_dealloc(BucketsObject* self) {
+  PyMem_Free(self->bounds);
+  PyMem_Free(self->counts);
+  Py_TYPE(self)->tp_free(reinterpret_cast<PyObject*>(self));
+}
+
+PyObject* buckets_observe(BucketsObject* self, PyObject* arg) {
+  double v = PyFloat_AsDouble(arg);
+  if (v == -1.0 && PyErr_Occurred()) return nullptr;
+  // lower_bound: first bound >= v (bisect_left); NaN lands past the last bucket (+Inf only)
+  Py_ssize_t lo = 0, hi = self->n;
+  while (lo < hi) {
+    Py_ssize_t mid = (lo + hi) >> 1;
+    if (self->bounds[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  if (lo < self->n && !(v != v)) self->counts[lo]++;
+  self->sum += v;
+  self->count++;
+  Py_RETURN_NONE;
+}
+
+PyObject* buckets_snapshot(BucketsObject* self, PyObject*) {
+  PyObject* counts = PyList_New(self->n);
+  if (!counts) return nullptr;
+  for (Py_ssize_t i = 0; i < self->n; ++i) {
+    PyObject* c = PyLong_FromUnsignedLongLong(self->counts[i]);
+    if (!c) {
+      Py_DECREF(counts);
+      return nullptr;
+    }
+    PyList_SET_ITEM(counts, i, c);
+  }
+  return Py_BuildValue("(NdK)", counts, self->sum, (unsigned long long)self->count);
+}
+
+PyObject* buckets_reset(BucketsObject* self, PyObject*) {
+  for (Py_ssize_t i = 0; i < self->n; ++i) self->counts[i] = 0;
+  self->sum = 0.0;
+  self->count = 0;
+  Py_RETURN_NONE;
+}
+
+PyMethodDef buckets_methods[] = {
+    {"observe", reinterpret_cast<PyCFunction>(buckets_observe), METH_O, "observe(value)"},
+    {"snapshot", reinterpret_cast<PyCFunction>(buckets_snapshot), METH_NOARGS,
+     "snapshot() -> ([per-bucket counts], sum, count)"},
+    {"reset", reinterpret_cast<PyCFunction>(buckets_reset), METH_NOARGS, "zero everything"},
+    {nullptr, nullptr, 0, nullptr}};
+
 int init_metric_types(PyObject* m) {
+  BucketsType.tp_name = "beholder_amd.ops._native.Buckets";
+  BucketsType.tp_basicsize = sizeof(BucketsObject);
+  BucketsType.tp_flags = Py_TPFLAGS_DEFAULT;
+  BucketsType.tp_doc = "Buckets(bounds): prom fixed-bucket histogram cell (le semantics)";
+  BucketsType.tp_new = buckets_new;
+  BucketsType.tp_dealloc = reinterpret_cast<destructor>(buckets_dealloc);
+  BucketsType.tp_methods = buckets_methods;
+  if (PyType_Ready(&BucketsType) < 0) return -1;
+  Py_INCREF(&BucketsType);
+  if (PyModule_AddObject(m, "Buckets", reinterpret_cast<PyObject*>(&BucketsType)) < 0) return -1;
+
   HistogramType.tp_name = "beholder_amd.ops._native.Histogram";
   HistogramType.tp_basicsize = sizeof(HistogramObject);
   HistogramType.tp_flags = Py_TPFLAGS_DEFAULT;

@@ -45,9 +45,8 @@ class TrelloClient:
             raise HttpError("Unsupported requestMethod. Pass one of these methods: POST, GET, PUT, DELETE.")
         if not path.startswith("/"):
             raise HttpError("Path must start with /")
-        query = {"key": self.key, "token": self.token}
-        if options:
-            query.update(options)
+        query = {"key": self.key, "token": self.token, **options} if options else \
+            {"key": self.key, "token": self.token}
         stats = self.stats
         if stats is None:
             r = await self.http.request(m, self.base_url + path, params=query, timeout=self.timeout)

@@ -82,3 +82,33 @@ def test_invalid_names():
         r.counter("bad-name", "x")
     with pytest.raises(ValueError):
         r.counter("ok", "x", ["__reserved"])
+
+
+def test_native_buckets_match_bisect_reference():
+    """Histogram cells are native (ops.Buckets); pinned to the prom-client `le` rule."""
+    import bisect
+    import math
+
+    from hypothesis import given, settings, strategies as st
+
+    from beholder_amd.ops import native
+
+    @settings(max_examples=200, deadline=None)
+    @given(st.lists(st.floats(-1e3, 1e3, allow_nan=False), min_size=1, max_size=12, unique=True),
+           st.lists(st.floats(allow_nan=False, allow_infinity=True, width=64), max_size=50))
+    def check(bounds, values):
+        bounds = sorted(bounds)
+        cell = native.Buckets(bounds)
+        ref = [0] * len(bounds)
+        for v in values:
+            cell.observe(v)
+            i = bisect.bisect_left(bounds, v)
+            if i < len(bounds):
+                ref[i] += 1
+        counts, total, n = cell.snapshot()
+        assert counts == ref and n == len(values)
+        s = math.fsum(values) if values else 0.0
+        assert (math.isnan(total) and math.isnan(s)) or total == sum(values) or math.isclose(total, s)
+    check()
+    with pytest.raises(ValueError):
+        native.Buckets([1, 1])
