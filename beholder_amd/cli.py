@@ -42,7 +42,14 @@ def cmd_run(a: argparse.Namespace) -> int:
         argv = strip_workers_arg(sys.argv[1:] if a.argv is None else a.argv)
         if a.metrics_port is not None:
             argv = strip_opt(argv, "--metrics-port")
-        return Supervisor(argv, a.workers, metrics_port=a.metrics_port,
+        try:
+            mcfg = Config.load("events", path=a.config, env=dict(os.environ)).data["service"]["metrics"]
+        except ConfigError as e:
+            print(f"beholder: config error: {e}", file=sys.stderr)
+            return 2
+        port = a.metrics_port if a.metrics_port is not None else (
+            int(mcfg.get("port", 3000)) if mcfg.get("enabled", True) else -1)
+        return Supervisor(argv, a.workers, metrics_port=port, metrics_host=str(mcfg.get("host", "0.0.0.0")),
                           log=lambda m: print(f"beholder supervisor: {m}", file=sys.stderr)).run()
     env = dict(os.environ)
     try:

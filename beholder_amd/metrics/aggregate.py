@@ -1,0 +1,172 @@
+"""Cluster-wide ``/metrics`` for ``beholder run --workers N``.
+
+The reference exposes one registry per process (``Prom.expose()``, index.js:28).
+With N competing-consumer workers on one host, a scraper should still see one
+target, so the supervisor serves the merged exposition on the configured port.
+Workers listen on internal ports. This is prom-client's ``AggregatorRegistry``
+idea, rebuilt for processes that share no memory: the supervisor fetches each
+worker's text exposition and merges the samples.
+
+Merge rules, per metric family:
+
+* counters and histograms (buckets, ``_sum``, ``_count``) are summed;
+* gauges are summed (in-flight handlers, ring depth, resident memory), except:
+  * ``*_start_time_seconds``: min;
+  * ``*_info`` and ``process_max_fds``: first value seen;
+* a sample present in only some workers is summed over the workers that have it.
+
+The output keeps family order, HELP and TYPE lines from the first worker that
+reports them.
+"""
+from __future__ import annotations
+
+import json
+import math
+import threading
+import urllib.request
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+from .registry import fmt_value
+
+_SUFFIXES = ("_bucket", "_sum", "_count")
+
+
+def _strategy(family: str, mtype: str) -> str:
+    if mtype == "gauge":
+        if family.endswith("_start_time_seconds"):
+            return "min"
+        if family.endswith("_info") or family == "process_max_fds":
+            return "first"
+    return "sum"
+
+
+def _parse_value(s: str) -> float:
+    return {"+Inf": math.inf, "-Inf": -math.inf, "NaN": math.nan}.get(s) or float(s)
+
+
+def aggregate(texts: Sequence[str]) -> str:
+    """Merges Prometheus text expositions (see module docstring for the rules)."""
+    order: List[str] = []
+    meta: Dict[str, Dict[str, str]] = {}
+    samples: Dict[str, Dict[str, float]] = {}  # family -> {sample key: value}
+    sample_order: Dict[str, List[str]] = {}
+    for text in texts:
+        family = None
+        for line in text.splitlines():
+            if not line:
+                continue
+            if line.startswith("#"):
+                parts = line.split(" ", 3)
+                if len(parts) >= 3 and parts[1] in ("HELP", "TYPE"):
+                    family = parts[2]
+                    if family not in meta:
+                        meta[family] = {}
+                        order.append(family)
+                        samples[family] = {}
+                        sample_order[family] = []
+                    meta[family].setdefault(parts[1], parts[3] if len(parts) > 3 else "")
+                continue
+            key, _, val = line.rpartition(" ")
+            if not key:
+                continue
+            name = key.split("{", 1)[0]
+            fam = family if family is not None and (name == family or (
+                name.startswith(family) and name[len(family):] in _SUFFIXES)) else name
+            if fam not in meta:
+                meta[fam] = {}
+                order.append(fam)
+                samples[fam] = {}
+                sample_order[fam] = []
+            try:
+                v = _parse_value(val)
+            except ValueError:
+                continue
+            bucket = samples[fam]
+            if key not in bucket:
+                bucket[key] = v
+                sample_order[fam].append(key)
+                continue
+            how = _strategy(fam, meta[fam].get("TYPE", "untyped"))
+            if how == "sum":
+                bucket[key] += v
+            elif how == "min":
+                bucket[key] = min(bucket[key], v)
+            # "first": keep
+    out: List[str] = []
+    for fam in order:
+        m = meta[fam]
+        if "HELP" in m:
+            out.append(f"# HELP {fam} {m['HELP']}")
+        if "TYPE" in m:
+            out.append(f"# TYPE {fam} {m['TYPE']}")
+        for key in sample_order[fam]:
+            out.append(f"{key} {fmt_value(samples[fam][key])}")
+    return "\n".join(out) + "\n"
+
+
+def fetch(url: str, timeout: float = 2.0) -> Optional[str]:
+    try:
+        with urllib.request.urlopen(url, timeout=timeout) as r:  # noqa: S310 (loopback worker endpoints)
+            return r.read().decode("utf-8", "replace")
+    except (OSError, ValueError):
+        return None
+
+
+class ClusterMetricsServer:
+    """Supervisor-side HTTP endpoint: ``/metrics`` (merged), ``/healthz`` (all workers up),
+    ``/stats`` (per-worker JSON)."""
+
+    def __init__(self, host: str, port: int, worker_ports: Callable[[], List[Tuple[int, int]]],
+                 alive: Callable[[], bool]):
+        self.host = host
+        self.port = port
+        self._worker_ports = worker_ports  # [(worker id, port)]
+        self._alive = alive
+        self._httpd: Optional[ThreadingHTTPServer] = None
+        self._thread: Optional[threading.Thread] = None
+
+    def _gather(self, path: str) -> List[Tuple[int, Optional[str]]]:
+        return [(i, fetch(f"http://127.0.0.1:{p}{path}")) for i, p in self._worker_ports()]
+
+    def start(self) -> "ClusterMetricsServer":
+        outer = self
+
+        class Handler(BaseHTTPRequestHandler):
+            def log_message(self, *a):  # quiet
+                pass
+
+            def _send(self, code: int, body: bytes, ctype: str) -> None:
+                self.send_response(code)
+                self.send_header("Content-Type", ctype)
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+            def do_GET(self):  # noqa: N802
+                path = self.path.split("?", 1)[0]
+                if path == "/metrics":
+                    texts = [t for _, t in outer._gather("/metrics") if t]
+                    self._send(200, aggregate(texts).encode(), "text/plain; version=0.0.4; charset=utf-8")
+                elif path == "/healthz":
+                    ok = outer._alive() and all(t is not None and t.strip() == "ok"
+                                                for _, t in outer._gather("/healthz"))
+                    self._send(200 if ok else 503, b"ok\n" if ok else b"unavailable\n", "text/plain")
+                elif path == "/stats":
+                    body = {str(i): (json.loads(t) if t else None) for i, t in outer._gather("/stats")}
+                    self._send(200, json.dumps({"workers": body}).encode(), "application/json")
+                else:
+                    self._send(404, b"not found\n", "text/plain")
+
+        self._httpd = ThreadingHTTPServer((self.host, self.port), Handler)
+        self._httpd.daemon_threads = True
+        self.port = self._httpd.server_address[1]
+        self._thread = threading.Thread(target=self._httpd.serve_forever, daemon=True, name="cluster-metrics")
+        self._thread.start()
+        return self
+
+    def stop(self) -> None:
+        if self._httpd is not None:
+            self._httpd.shutdown()
+            self._httpd.server_close()
+            self._httpd = None

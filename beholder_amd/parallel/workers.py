@@ -7,7 +7,10 @@ is N worker processes on the same queues (the broker round-robins between
 them, each with its own prefetch window). This module is the supervisor:
 
 * spawns N children running the same ``run`` command with
-  ``BEHOLDER_WORKER_ID=i`` and the metrics port offset by ``i``;
+  ``BEHOLDER_WORKER_ID=i``;
+* metrics: the supervisor serves the *merged* exposition of all workers on
+  the configured port (:mod:`beholder_amd.metrics.aggregate`). Worker ``i``
+  listens on ``127.0.0.1:port+1+i``, so one scrape target covers the host;
 * restarts a crashed worker with exponential backoff (a crash loop is capped
   at ``max_restarts`` per worker);
 * forwards SIGTERM/SIGINT and waits for graceful shutdown, then SIGKILLs
@@ -28,13 +31,15 @@ from typing import Dict, List, Optional
 
 class Supervisor:
     def __init__(self, argv: List[str], workers: int, *, metrics_port: Optional[int] = None,
-                 max_restarts: int = 10, grace_s: float = 15.0, env: Optional[Dict[str, str]] = None,
-                 log=print):
+                 metrics_host: str = "0.0.0.0", max_restarts: int = 10, grace_s: float = 15.0,
+                 env: Optional[Dict[str, str]] = None, log=print):
         if workers < 1:
             raise ValueError("workers must be >= 1")
         self.argv = list(argv)
         self.n = workers
-        self.metrics_port = metrics_port
+        self.metrics_port = metrics_port  # None / < 0: workers run without metrics endpoints
+        self.metrics_host = metrics_host
+        self.cluster_metrics = None
         self.max_restarts = max_restarts
         self.grace_s = grace_s
         self.env = dict(os.environ if env is None else env)
@@ -44,14 +49,22 @@ class Supervisor:
         self.next_start = [0.0] * workers
         self._stop = False
 
+    @property
+    def _metrics_on(self) -> bool:
+        return self.metrics_port is not None and self.metrics_port >= 0
+
+    def worker_port(self, i: int) -> int:
+        return self.metrics_port + 1 + i
+
     def _cmd(self, i: int) -> List[str]:
         cmd = [sys.executable, "-m", "beholder_amd", *self.argv]
-        if self.metrics_port is not None and self.metrics_port >= 0:
-            cmd += ["--metrics-port", str(self.metrics_port + i)]
+        cmd += ["--metrics-port", str(self.worker_port(i)) if self._metrics_on else "-1"]
         return cmd
 
     def _spawn(self, i: int) -> None:
         env = dict(self.env, BEHOLDER_WORKER_ID=str(i), BEHOLDER_WORKERS=str(self.n))
+        if self._metrics_on:
+            env["BEHOLDER_CFG__service__metrics__host"] = "127.0.0.1"  # internal; merged on the main port
         self.procs[i] = subprocess.Popen(self._cmd(i), env=env)
         self.log(f"worker {i} started pid={self.procs[i].pid}")
 
@@ -61,6 +74,13 @@ class Supervisor:
     def run(self) -> int:
         signal.signal(signal.SIGTERM, self.stop)
         signal.signal(signal.SIGINT, self.stop)
+        if self._metrics_on:
+            from ..metrics.aggregate import ClusterMetricsServer
+            self.cluster_metrics = ClusterMetricsServer(
+                self.metrics_host, self.metrics_port,
+                worker_ports=lambda: [(i, self.worker_port(i)) for i in sorted(self.procs)],
+                alive=lambda: not self._stop and len(self.procs) == self.n).start()
+            self.log(f"merged metrics on {self.metrics_host}:{self.cluster_metrics.port}")
         for i in range(self.n):
             self._spawn(i)
         failed = False
@@ -95,6 +115,8 @@ class Supervisor:
         return self._shutdown(failed)
 
     def _shutdown(self, failed: bool) -> int:
+        if self.cluster_metrics is not None:
+            self.cluster_metrics.stop()
         for p in self.procs.values():
             if p.poll() is None:
                 p.send_signal(signal.SIGTERM)
