@@ -20,10 +20,11 @@ Differences, all documented fixes:
 * graceful shutdown (SIGTERM/SIGINT): stop consuming, drain in-flight
   handlers for ``service.shutdown_grace_s``, close transport/store/sinks.
 
-Dispatch: deliveries arrive in batches; each handler coroutine runs eagerly
-(:mod:`beholder_amd.utils.eager`). Handlers that suspend (real I/O) become
-tasks; at most ``service.prefetch`` (default 100, index.js:43) are in flight,
-matching the broker's prefetch window.
+Dispatch: deliveries arrive in batches. Each handler coroutine is driven eagerly by
+the native ``dispatch_batch`` (``PyIter_Send``; no Task for a handler that never
+blocks). A handler that suspends on real I/O is resumed by a native ``Driver``
+when the awaited future completes. At most ``service.prefetch`` (default 100,
+index.js:43) are in flight, matching the broker's prefetch window.
 """
 from __future__ import annotations
 
