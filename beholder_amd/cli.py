@@ -275,7 +275,7 @@ def build_parser() -> argparse.ArgumentParser:
     r.add_argument("--media-fixture", help="JSON list of media rows to preload (implies --store memory)")
     r.add_argument("--stats", action="store_true", help="print final stats JSON to stderr")
     r.add_argument("--workers", type=int, default=0,
-                   help="N competing-consumer processes on the same queues (amqp); metrics port + worker id")
+                   help="N competing-consumer processes on the same queues (amqp); one merged /metrics")
     r.set_defaults(fn=cmd_run)
 
     c = sub.add_parser("config", help="validate and print the effective config (secrets masked)")

@@ -77,8 +77,9 @@ def build_source(config: Config, logger: Optional[Logger] = None) -> Source:
         from .dynamics import dyn
         from .transport.amqp import AmqpSource
         url = tcfg.get("url") or dyn("rabbitmq", env=config.env, config=config)
+        hb = tcfg.get("heartbeat")
         return AmqpSource(url, prefetch=prefetch, retries=int(config.data["service"]["retries"]),
-                          logger=logger)
+                          logger=logger, heartbeat=None if hb is None else int(hb))
     raise ValueError(f"unknown transport kind {kind!r} (amqp|stdin|file)")
 
 
