@@ -19,7 +19,8 @@ bench-configs: native  ## the five BASELINE.json configs
 	$(PY) -m beholder_amd bench all --out profiles/baseline_configs.json
 
 lint:
-	@$(PY) -m pyflakes beholder_amd tests bench.py 2>/dev/null || $(PY) -m compileall -q beholder_amd tests bench.py
+	$(PY) -m compileall -q beholder_amd tests bench.py
+	$(PY) scripts/lint.py beholder_amd tests bench.py __graft_entry__.py scripts
 
 tsan:              ## ring/framer stress test under ThreadSanitizer + ASan/UBSan
 	$(MAKE) -C tests/native run

@@ -22,7 +22,6 @@ Reliability (amqp-connection-manager parity):
 from __future__ import annotations
 
 import asyncio
-import collections
 import time
 from typing import Dict, List, Optional, Sequence
 

@@ -79,3 +79,14 @@ def test_repo_example_config_loads():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     c = Config.load(path=os.path.join(root, "config", "events.example.yaml"), env={})
     assert "deployed" in c.flow_ids
+
+
+def test_repo_has_no_unused_imports():
+    """`make lint` (scripts/lint.py): pyflakes is not installed in the image."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "lint.py"), "beholder_amd", "tests",
+                        "bench.py", "__graft_entry__.py", "scripts"], capture_output=True, text=True, cwd=root)
+    assert r.returncode == 0, r.stdout
