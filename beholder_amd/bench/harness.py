@@ -147,6 +147,13 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
     svc = Service(Config.from_dict(cfgd), source=src, store=MemoryStore(media), http=http,
                   logger=Logger(stream=sink, level=log_level), serve_metrics=False)
     max_inflight = [0]
+    rss_curve: List[float] = []
+    sampler = None
+    if rss_probe is not None:
+        async def sample_rss():
+            while True:
+                await asyncio.sleep(0.5)
+                rss_curve.append(round(_rss_mb(), 1))
     if sink_delay_s:
         async def watch():
             while True:
@@ -160,6 +167,8 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
         rss_probe.append(_rss_mb())  # service initialised, workload already in memory
     if gc_probe is not None:
         gc_probe.__enter__()  # steady state only: init's own collect+freeze is not a run pause
+    if rss_probe is not None:
+        sampler = asyncio.ensure_future(sample_rss())
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
     prod.start()
@@ -170,6 +179,8 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
     prod.join()
     if gc_probe is not None:
         gc_probe.__exit__(None, None, None)
+    if sampler is not None:
+        sampler.cancel()
     if rss_probe is not None:
         rss_probe.append(_rss_mb())  # after 1M events, before teardown
     if sink_delay_s:
@@ -190,6 +201,7 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
         "max_inflight": max_inflight[0],
         "cpu_us_per_event": cpu_s / s["acked"] * 1e6 if s["acked"] else None,
         "error_samples": sink.samples,
+        **({"rss_curve_mb": rss_curve} if rss_probe is not None else {}),
     }
 
 
