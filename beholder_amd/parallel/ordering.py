@@ -12,18 +12,20 @@ from __future__ import annotations
 
 import asyncio
 import collections
+import functools
 from typing import Any, Callable, Deque, Dict, Optional
 
 
 class KeyedSerializer:
-    """Serialise ``dispatch(item, on_finish)`` calls per ``key_fn(item)``.
+    """Serialise ``dispatch(item, on_finish) -> bool`` calls per ``key_fn(item)``.
 
-    ``dispatch`` must call ``on_finish()`` exactly once when the item's work is
-    done — synchronously (eager completion) or later from a task callback.
-    Items whose key is ``None`` are dispatched immediately (unordered).
+    ``dispatch`` returns True when the item's work finished synchronously (eager
+    completion; ``on_finish`` is then not called), or False and calls
+    ``on_finish()`` exactly once later. Items whose key is ``None`` are
+    dispatched immediately (unordered).
     """
 
-    def __init__(self, dispatch: Callable[[Any, Optional[Callable[[], None]]], None],
+    def __init__(self, dispatch: Callable[[Any, Optional[Callable[[], None]]], bool],
                  key_fn: Optional[Callable[[Any], Any]] = None):
         self._dispatch = dispatch
         self._key_fn = key_fn or (lambda item: None)
@@ -59,19 +61,12 @@ class KeyedSerializer:
 
     def _run_chain(self, key: Any, item: Any) -> None:
         # Trampoline: eager completions loop here instead of recursing.
+        fin = None
         while True:
-            state = {"in_call": True, "done_sync": False}
-
-            def on_finish(state=state, key=key):
-                if state["in_call"]:
-                    state["done_sync"] = True
-                else:
-                    self._advance(key)
-
-            self._dispatch(item, on_finish)
-            state["in_call"] = False
-            if not state["done_sync"]:
-                return
+            if fin is None:
+                fin = functools.partial(self._advance, key)
+            if not self._dispatch(item, fin):
+                return  # suspended: fin() resumes the chain
             q = self._chains.get(key)
             if not q:
                 self._chains.pop(key, None)

@@ -359,39 +359,38 @@ class Service:
                         "handle_us": (now - d.start_ns) // 1000, "outcome": outcome, "state": d.state},
                        "handled")
 
-    def _dispatch_now(self, d, on_finish: Optional[Callable[[], None]] = None) -> None:
-        if self.trace:
-            user_finish = on_finish
-
-            def on_finish(d=d, user_finish=user_finish):
-                self._span(d, "ok" if d.settled else "unsettled")
-                if user_finish is not None:
-                    user_finish()
+    def _dispatch_now(self, d, on_finish: Optional[Callable[[], None]] = None) -> bool:
+        """Python dispatch path (per-media ordering, trace spans). Returns True when the handler
+        finished synchronously; otherwise a Driver finishes it and calls ``on_finish()`` then."""
         handler = self._routes[d.topic_id]
         d.start()
         coro = handler(d)
         try:
             first = coro.send(None)
         except StopIteration:
-            if on_finish is not None:
-                on_finish()
-            return
+            if self.trace:
+                self._span(d, "ok" if d.settled else "unsettled")
+            return True
         except BaseException as exc:  # noqa: BLE001 — handler errors are data here
             self._on_handler_error(d, exc)
             exc = None  # the traceback reaches this frame via f_back: don't keep a cycle alive
+            if self.trace:
+                self._span(d, "ok" if d.settled else "unsettled")
+            return True
+        if on_finish is None and not self.trace:
+            self._on_suspend(d, coro, first)
+            return False
+
+        def done(drv, exc, on_finish=on_finish, d=d):
+            self._driver_done(drv, exc)
+            if self.trace:
+                self._span(d, "ok" if d.settled else "unsettled")
             if on_finish is not None:
                 on_finish()
-            return
-        if on_finish is None:
-            self._on_suspend(d, coro, first)
-            return
-
-        def done(drv, exc, on_finish=on_finish):
-            self._driver_done(drv, exc)
-            on_finish()
         drv = Driver(coro, done, d)
         self._inflight.add(drv)
         drv.start(first)
+        return False
 
     def _on_suspend(self, d, coro, first_yield) -> bool:
         """A handler awaited real I/O: a native Driver resumes it when the awaited future
