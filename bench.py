@@ -26,7 +26,10 @@ consumers and starts the clock; it stops the clock when all of its
 consumers report their K steps done, then passes another gloo barrier. The
 elapsed time is the MAX over ranks and ``value`` is whole-job events/s.
 Per-consumer work is fixed as N grows: weak scaling. The service has no
-device work (the reference has none), so nothing runs on the GPU.
+device work (the reference has none), so nothing runs on the GPU. The
+timed region is bracketed by barriers, but not by torch.cuda.synchronize():
+no kernel is ever queued, and initialising HIP in a rank process that then
+spawns consumer processes would only add start-up cost.
 
 Prints ONE JSON line on rank 0.
 """
