@@ -482,6 +482,12 @@ class Service:
             out["handler_errors"] = {k[0]: v for k, v in self.handler_errors.values().items()}
             out["trello_comments"] = self.trello_comments_total.get()
             out["progress_updates"] = {k[0]: v for k, v in self.progress_updates_total.values().items()}
+        http_stats = getattr(self._http, "stats", None)
+        if callable(http_stats):  # keep-alive pool accounting (sinks/h1.py)
+            out["http"] = http_stats()
+        store_pool = getattr(self._store, "_pool", None)
+        if store_pool is not None and hasattr(store_pool, "connections"):
+            out["store"] = {"connections": store_pool.connections}
         return out
 
 
