@@ -271,6 +271,20 @@ class Service:
         reg.register(Gauge("beholder_transport", "Ingest transport state (connected flag, reconnects, bytes, "
                            "ring depth)", ["kind", "field"], collect=transport_collect))
 
+        # outbound dependency pools: HTTP keep-alive connections (sinks/h1.py), Postgres connections
+        def pools_collect(g: Gauge):
+            http_stats = getattr(self._http, "stats", None)
+            if callable(http_stats):
+                for k, v in http_stats().items():
+                    g.set({"pool": "http", "field": k}, v)
+            pool = getattr(self._store, "_pool", None)
+            if pool is not None and hasattr(pool, "connections"):
+                g.set({"pool": "postgres", "field": "open"}, pool.connections)
+
+        reg.register(Gauge("beholder_pool", "Outbound connection pools (HTTP sinks, Postgres): open/idle "
+                           "connections and request/connect/error counts", ["pool", "field"],
+                           collect=pools_collect))
+
         reg.register(NativeHistogramView("beholder_handle_latency_seconds",
                                          "Handler start to ack latency",
                                          lambda: settler().handle_latency if settler() is not None else None))
