@@ -64,10 +64,25 @@ def build(force: bool = False, debug: bool = False, sanitize: str = "", cxx: str
             if f.read().strip() == digest:
                 return TARGET
     tmp = TARGET + ".tmp"
-    cmd = [cxx, *flags, *sources(), "-o", tmp]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
+    # compile translation units in parallel (one compiler process each), then link
+    import concurrent.futures
+    import tempfile
+    cflags = [f for f in flags if f != "-shared"]
+    jobs = max(1, min(len(sources()), int(os.environ.get("MAX_JOBS", "0") or 0) or (os.cpu_count() or 1), 16))
+    with tempfile.TemporaryDirectory(prefix="beholder-build-") as td:
+        def compile_one(src: str) -> str:
+            obj = os.path.join(td, os.path.basename(src) + ".o")
+            cmd = [cxx, *cflags, "-c", src, "-o", obj]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            subprocess.run(cmd, check=True)
+            return obj
+        with concurrent.futures.ThreadPoolExecutor(jobs) as ex:
+            objs = list(ex.map(compile_one, sources()))
+        link = [cxx, *[f for f in flags if not f.startswith("-I") and not f.startswith("-W")], *objs, "-o", tmp]
+        if verbose:
+            print(" ".join(link), file=sys.stderr)
+        subprocess.run(link, check=True)
     os.replace(tmp, TARGET)
     with open(STAMP, "w") as f:
         f.write(digest)
