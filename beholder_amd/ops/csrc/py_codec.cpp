@@ -183,8 +183,7 @@ const char* decode_into(CodecObject* self, const uint8_t* data, size_t len, Slot
   const auto& specs = *self->fields;
   while (!r.eof()) {
     uint64_t tag;
-    if (!r.varint(&tag)) return r.err;
-    if (tag > 0xffffffffull) return "tag overflow";
+    if (!r.tag(&tag)) return r.err;
     uint32_t field = uint32_t(tag >> 3);
     uint32_t wt = uint32_t(tag & 7);
     if (field == 0) return "invalid field number 0";

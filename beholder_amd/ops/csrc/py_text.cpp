@@ -573,16 +573,20 @@ PyObject* mod_js_number(PyObject*, PyObject* v) {
 }
 
 // ---- URL encoding -----------------------------------------------------------
-bool unreserved(unsigned char c) {
-  return (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9') || c == '-' || c == '_' ||
-         c == '.' || c == '!' || c == '~' || c == '*' || c == '\'' || c == '(' || c == ')';
+// encodeURIComponent leaves A-Z a-z 0-9 - _ . ! ~ * ' ( ) unescaped; RFC 3986 strict (the
+// `qs` 6.x encoder behind request's `qs` option) escapes ! * ' ( ) too.
+bool unreserved(unsigned char c, bool rfc3986) {
+  if ((c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9') || c == '-' || c == '_' ||
+      c == '.' || c == '~')
+    return true;
+  return !rfc3986 && (c == '!' || c == '*' || c == '\'' || c == '(' || c == ')');
 }
 
-void quote_append(std::string& out, const char* s, size_t n) {
+void quote_append(std::string& out, const char* s, size_t n, bool rfc3986 = false) {
   static const char* hex = "0123456789ABCDEF";
   for (size_t i = 0; i < n; ++i) {
     unsigned char c = static_cast<unsigned char>(s[i]);
-    if (unreserved(c)) {
+    if (unreserved(c, rfc3986)) {
       out += char(c);
     } else {
       out += '%';
@@ -593,11 +597,11 @@ void quote_append(std::string& out, const char* s, size_t n) {
 }
 
 // querystring value rendering: None -> "", bool -> true/false, numbers JS-style
-bool qs_value_append(std::string& out, PyObject* v) {
+bool qs_value_append(std::string& out, PyObject* v, bool rfc3986 = false) {
   std::string tmp;
   if (v == Py_None) return true;
   if (!js_str_append(tmp, v)) return false;
-  quote_append(out, tmp.data(), tmp.size());
+  quote_append(out, tmp.data(), tmp.size(), rfc3986);
   return true;
 }
 
@@ -607,14 +611,35 @@ PyObject* mod_quote_component(PyObject*, PyObject* v) {
   return PyUnicode_FromStringAndSize(out.data(), Py_ssize_t(out.size()));
 }
 
-// encode_query(mapping) -> "k=v&k2=v2" (insertion order)
-PyObject* mod_encode_query_impl(PyObject*, PyObject* m);
-PyObject* mod_encode_query(PyObject*, PyObject* m) {
-  BEHOLDER_TRY { return mod_encode_query_impl(nullptr, m); }
+// encode_query(mapping, rfc3986=False) -> "k=v&k2=v2" (insertion order). The `qs` library the
+// reference's HTTP clients use (1.2 under restler/trello, 6.5 under request) drops keys whose
+// value is undefined (None here); values are String(v), JS-style.
+PyObject* mod_encode_query_impl(PyObject* m, bool rfc3986);
+PyObject* mod_encode_query(PyObject*, PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames) {
+  bool rfc3986 = false;
+  Py_ssize_t nkw = kwnames ? PyTuple_GET_SIZE(kwnames) : 0;
+  if (nargs < 1 || nargs + nkw > 2 || nargs > 2) {
+    PyErr_SetString(PyExc_TypeError, "encode_query(mapping, rfc3986=False)");
+    return nullptr;
+  }
+  PyObject* flag = nargs == 2 ? args[1] : nullptr;
+  for (Py_ssize_t i = 0; i < nkw; ++i) {
+    if (PyUnicode_CompareWithASCIIString(PyTuple_GET_ITEM(kwnames, i), "rfc3986") != 0) {
+      PyErr_SetString(PyExc_TypeError, "encode_query: unexpected keyword");
+      return nullptr;
+    }
+    flag = args[nargs + i];
+  }
+  if (flag) {
+    int t = PyObject_IsTrue(flag);
+    if (t < 0) return nullptr;
+    rfc3986 = t != 0;
+  }
+  BEHOLDER_TRY { return mod_encode_query_impl(args[0], rfc3986); }
   BEHOLDER_CATCH(nullptr)
 }
 
-PyObject* mod_encode_query_impl(PyObject*, PyObject* m) {
+PyObject* mod_encode_query_impl(PyObject* m, bool rfc3986) {
   if (!PyDict_Check(m)) {
     PyErr_SetString(PyExc_TypeError, "encode_query expects a dict");
     return nullptr;
@@ -624,13 +649,14 @@ PyObject* mod_encode_query_impl(PyObject*, PyObject* m) {
   PyObject *k, *v;
   bool first = true;
   while (PyDict_Next(m, &pos, &k, &v)) {
+    if (v == Py_None) continue;  // undefined: qs omits the key
     if (!first) out += '&';
     first = false;
     std::string ks;
     if (!js_str_append(ks, k)) return nullptr;
-    quote_append(out, ks.data(), ks.size());
+    quote_append(out, ks.data(), ks.size(), rfc3986);
     out += '=';
-    if (!qs_value_append(out, v)) return nullptr;
+    if (!qs_value_append(out, v, rfc3986)) return nullptr;
   }
   return PyUnicode_FromStringAndSize(out.data(), Py_ssize_t(out.size()));
 }
@@ -783,7 +809,9 @@ PyMethodDef text_methods[] = {
     {"js_str", mod_js_str, METH_O, "JavaScript String(v)"},
     {"js_number", mod_js_number, METH_O, "JavaScript Number::toString"},
     {"quote_component", mod_quote_component, METH_O, "encodeURIComponent(String(v))"},
-    {"encode_query", mod_encode_query, METH_O, "querystring.stringify(dict)"},
+    {"encode_query", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(mod_encode_query)),
+     METH_FASTCALL | METH_KEYWORDS,
+     "encode_query(dict, rfc3986=False): qs.stringify (undefined/None keys omitted; rfc3986 also escapes !'()*)"},
     {"configure_text", mod_configure_text, METH_VARARGS, "configure_text(js_str_fallback, json_fallback)"},
     {nullptr, nullptr, 0, nullptr}};
 

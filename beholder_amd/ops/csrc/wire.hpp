@@ -7,8 +7,11 @@
 //   * a known field whose wire type does not match its declared type is
 //     treated as an unknown field and skipped;
 //   * unknown fields (incl. groups) are skipped;
-//   * truncated input, over-long varints, field number 0, stray END_GROUP and
-//     wire types 6/7 are errors.
+//   * truncated input, varints longer than 10 bytes, tags longer than 5 bytes
+//     or wider than 32 bits, field number 0, stray END_GROUP and wire types 6/7
+//     are errors;
+//   * a 10-byte value varint keeps bit 63 and drops the overflow bits of its
+//     last byte (upb does the same).
 #pragma once
 
 #include <cstddef>
@@ -88,11 +91,8 @@ struct Reader {
         return false;
       }
       uint8_t b = *p++;
-      if (shift == 63 && b > 1) {
-        // 10th byte may only carry the top bit; upb rejects larger values.
-        err = "varint overflow";
-        return false;
-      }
+      // 10th byte: bit 0 is bit 63 of the value; higher bits overflow and are dropped,
+      // exactly as upb does (a continuation bit there is still an error, below)
       v |= uint64_t(b & 0x7f) << shift;
       if (b < 0x80) {
         *out = v;
@@ -100,6 +100,34 @@ struct Reader {
       }
     }
     err = "varint too long";
+    return false;
+  }
+
+  // Reads a field tag: a varint of at most 5 bytes whose value fits 32 bits (upb's rule;
+  // a longer encoding of a small tag is still an error).
+  inline bool tag(uint64_t* out) {
+    if (p < end && *p < 0x80) {
+      *out = *p++;
+      return true;
+    }
+    uint64_t v = 0;
+    for (int i = 0; i < 5; ++i) {
+      if (p >= end) {
+        err = "truncated varint";
+        return false;
+      }
+      uint8_t b = *p++;
+      v |= uint64_t(b & 0x7f) << (7 * i);
+      if (b < 0x80) {
+        if (v > 0xffffffffull) {
+          err = "tag overflow";
+          return false;
+        }
+        *out = v;
+        return true;
+      }
+    }
+    err = "tag too long";
     return false;
   }
 
@@ -163,12 +191,10 @@ struct Reader {
             err = "unterminated group";
             return false;
           }
-          if (!varint(&tag)) return false;
+          if (!this->tag(&tag)) return false;
+          // field number 0 is tolerated inside a skipped group (upb only rejects it at
+          // message level)
           uint32_t f = uint32_t(tag >> 3), w = uint32_t(tag & 7);
-          if (f == 0) {
-            err = "invalid field number 0";
-            return false;
-          }
           if (w == WT_EGROUP) {
             if (f != field) {
               err = "mismatched end group";

@@ -3,7 +3,7 @@ from __future__ import annotations
 
 from typing import Any, Optional
 
-from .http import HttpClient, HttpResponse, observed
+from .http import HttpClient, HttpResponse, observed, with_query
 from ..utils.log import js_str
 
 
@@ -20,6 +20,6 @@ class EmbyClient:
         h = self.host if host is ... else host
         k = self.api_key if api_key is ... else api_key
         url = f"{js_str(h)}/emby/library/refresh"
-        r = await observed(self.stats, self.http.request("GET", url, params={"api_key": k},
-                                                                    timeout=self.timeout))
+        full = with_query(url, {"api_key": k}, rfc3986=True)  # request `qs` -> qs 6.5 encoding
+        r = await observed(self.stats, self.http.request("GET", full, timeout=self.timeout))
         return r.raise_for_status()

@@ -10,8 +10,14 @@ Two reference semantics matter (SURVEY.md §2.4 "Outbound HTTP"):
 ``HttpClient.request`` returns an :class:`HttpResponse`; callers decide
 whether a status is an error (:meth:`HttpResponse.raise_for_status`).
 
-Query strings are encoded like ``encodeURIComponent`` (Node's ``querystring``)
-so URLs are byte-identical to the reference's.
+Query strings are encoded the way each reference client does it, so the URLs are byte-identical:
+
+* Trello goes through ``restler`` and ``qs`` 1.2 (``yarn.lock:1665-1673``), which applies
+  ``encodeURIComponent`` to every key and value;
+* Telegram and Emby go through ``request``'s ``qs`` option, i.e. ``qs`` 6.5
+  (``yarn.lock:1545-1548``), which uses RFC 3986 strict encoding: ``!'()*`` are escaped too.
+  The sinks ask for it with ``rfc3986=True``;
+* in both, a key whose value is ``undefined`` (``None`` here) is left out entirely.
 """
 from __future__ import annotations
 
@@ -26,7 +32,8 @@ from urllib.parse import quote
 
 from ..ops import encode_query as _native_encode_query
 
-_SAFE = "-_.!~*'()"
+_SAFE = "-_.!~*'()"    # encodeURIComponent
+_SAFE_RFC3986 = "-_.~"  # qs 6.x / RFC 3986 unreserved
 
 
 def js_qs_value(v: Any) -> str:
@@ -41,23 +48,25 @@ def js_qs_value(v: Any) -> str:
     return str(v)
 
 
-def py_encode_query(params: Optional[Mapping[str, Any]]) -> str:
+def py_encode_query(params: Optional[Mapping[str, Any]], rfc3986: bool = False) -> str:
     """Pure-Python reference for :func:`encode_query` (tests pin the native one to it)."""
     if not params:
         return ""
-    return "&".join(f"{quote(str(k), safe=_SAFE)}={quote(js_qs_value(v), safe=_SAFE)}" for k, v in params.items())
+    safe = _SAFE_RFC3986 if rfc3986 else _SAFE
+    return "&".join(f"{quote(str(k), safe=safe)}={quote(js_qs_value(v), safe=safe)}"
+                    for k, v in params.items() if v is not None)
 
 
-def encode_query(params: Optional[Mapping[str, Any]]) -> str:
+def encode_query(params: Optional[Mapping[str, Any]], rfc3986: bool = False) -> str:
     if not params:
         return ""
     if type(params) is not dict:
         params = dict(params)
-    return _native_encode_query(params)
+    return _native_encode_query(params, rfc3986)
 
 
-def with_query(url: str, params: Optional[Mapping[str, Any]]) -> str:
-    q = encode_query(params)
+def with_query(url: str, params: Optional[Mapping[str, Any]], rfc3986: bool = False) -> str:
+    q = encode_query(params, rfc3986)
     if not q:
         return url
     return url + ("&" if "?" in url else "?") + q

@@ -3,7 +3,7 @@ from __future__ import annotations
 
 from typing import Any, Optional
 
-from .http import HttpClient, HttpResponse, observed
+from .http import HttpClient, HttpResponse, observed, with_query
 from ..utils.log import js_str
 
 
@@ -26,7 +26,7 @@ class TelegramClient:
         # `bot${token}` — an undefined token renders as "botundefined" in the reference
         tok = self.token if token is ... else token
         url = f"{self.base_url}/bot{js_str(tok)}/sendMessage"
-        r = await observed(self.stats,
-                           self.http.request("GET", url, params={"chat_id": chat_id, "text": text,
-                                                                 "parse_mode": parse_mode}, timeout=self.timeout))
+        # request-promise `qs` option -> qs 6.5 (RFC 3986 strict) query encoding
+        full = with_query(url, {"chat_id": chat_id, "text": text, "parse_mode": parse_mode}, rfc3986=True)
+        r = await observed(self.stats, self.http.request("GET", full, timeout=self.timeout))
         return r.raise_for_status()  # request-promise: reject on non-2xx

@@ -161,3 +161,32 @@ def test_fuzz_arbitrary_bytes_agree_with_upb(data):
     except DecodeError:
         got = None
     assert got == want
+
+
+@pytest.mark.parametrize("data", [
+    b"\x60" + b"\x80" * 9 + b"\x02",          # unknown varint, overflow bits in the 10th byte
+    b"\x60" + b"\x80" * 9 + b"\x7f",
+    b"\x18" + b"\x80" * 9 + b"\x02",          # known int32 field, same
+    b"\x18" + b"\xff" * 9 + b"\x01",
+    b"\xe0\x80\x80\x80\x80\x00\x00",          # 6-byte encoding of a small tag
+    b"\xe0\x80\x80\x80\x00\x00",              # 5-byte encoding of a small tag
+    b"\x80\x80\x80\x80\x10\x00",              # tag wider than 32 bits
+    b"\xe0\x00\x80\x80\x80\x80\x80\x80\x80\x80\x80\x02\x08\x00\x08\x00\r\x00\x00\x00\x00",  # fuzz find
+    bytes.fromhex("3b003a983f2e3c"),          # field number 0 inside a skipped group: tolerated
+    bytes.fromhex("3b03043c"),                # nested group with field number 0
+    bytes.fromhex("3b1b0c3c"),                # mismatched nested end group
+])
+def test_varint_edge_cases_agree_with_upb(data):
+    """Fuzzing found that upb keeps only bit 63 of a 10-byte varint (no error) and caps tags
+    at 5 bytes; the native reader follows both rules."""
+    c = codec_for(PROGRESS)
+    try:
+        m = proto.decode(PROGRESS, data)
+        want = (m.mediaId, m.status, m.progress, m.host)
+    except DecodeError:
+        want = None
+    try:
+        got = tuple(c.decode(data))
+    except DecodeError:
+        got = None
+    assert got == want
