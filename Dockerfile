@@ -6,7 +6,7 @@ WORKDIR /stack
 RUN useradd --uid 999 --create-home --home-dir /home/beholder beholder && chown 999:999 /stack
 
 COPY --chown=999:999 pyproject.toml /stack/
-RUN pip install --no-cache-dir protobuf pyyaml aiohttp
+RUN pip install --no-cache-dir protobuf pyyaml
 COPY --chown=999:999 . /stack
 # native runtime (ingest ring, codec, deliveries, metrics, text) built in-tree
 RUN python -m beholder_amd.ops.build --force && chown -R 999:999 /stack
