@@ -335,7 +335,7 @@ class H1Client(HttpClient):
                 raise HttpError(f"ETIMEDOUT: {m} {redact(cur)}") from None
             except OSError as e:
                 counts["errors"] += 1
-                raise HttpError(f"{_errname(e)}: {m} {redact(cur)}") from None
+                raise HttpError(_connect_error(e, o)) from None
             reused = c.uses > 0
             c.uses += 1
             w = loop.create_future()
@@ -408,12 +408,14 @@ def _header(raw: bytes, name: bytes) -> Optional[str]:
     return None
 
 
-def _errname(e: OSError) -> str:
-    """Node-style error code (ECONNREFUSED, ENOTFOUND-like gaierror names, TLS reason)."""
+def _connect_error(e: OSError, o: "_Origin") -> str:
+    """Node-style messages (what the reference logs via err.message): ``getaddrinfo ENOTFOUND
+    host``, ``connect ECONNREFUSED host:port``; TLS failures keep OpenSSL's reason."""
     import errno
     import socket
     if isinstance(e, _ssl.SSLError):
         return e.reason or type(e).__name__
     if isinstance(e, socket.gaierror):
-        return "ENOTFOUND"
-    return errno.errorcode.get(e.errno or 0, type(e).__name__) if e.errno else type(e).__name__
+        return f"getaddrinfo ENOTFOUND {o.host}"
+    name = errno.errorcode.get(e.errno or 0) if e.errno else None
+    return f"connect {name or type(e).__name__} {o.host}:{o.port}"

@@ -398,12 +398,14 @@ def test_max_per_host_bounds_connections():
 def test_connection_refused_and_bad_urls():
     async def go():
         c = H1Client(timeout_s=2)
-        with pytest.raises(HttpError, match="ECONNREFUSED: GET http://127.0.0.1:9/x"):
+        with pytest.raises(HttpError, match="^connect ECONNREFUSED 127.0.0.1:9$"):  # Node's err.message
             await c.request("GET", "http://127.0.0.1:9/x", params={"api_key": "s3cret"})
         with pytest.raises(HttpError, match="Invalid protocol"):
             await c.request("GET", "ftp://h/x")
         with pytest.raises(HttpError, match="Invalid URI"):
             await c.request("GET", "undefined/emby/library/refresh")  # js_str(undefined host)
+        with pytest.raises(HttpError, match="^getaddrinfo ENOTFOUND no-such-host.invalid$"):
+            await c.request("GET", "http://no-such-host.invalid/x")
         await c.close()
     run(go())
 
