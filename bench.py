@@ -91,6 +91,8 @@ def parse(argv=None):
     ap.add_argument("--log-level", default="info")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--ordering", default="none", choices=["none", "per_media"])
+    ap.add_argument("--pin", action="store_true",
+                    help="pin each consumer process to its own CPU of the rank's affinity mask")
     return ap.parse_args(argv)
 
 
@@ -101,6 +103,7 @@ class _Dist:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(self.world)))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", str(self.rank)))
         self.dist = None
         if self.world > 1:
             import torch.distributed as dist
@@ -203,8 +206,13 @@ async def run_consumer(a, seed: int, go) -> dict:
     }
 
 
-def _consumer_entry(a, seed, barrier, results):
+def _consumer_entry(a, seed, barrier, results, cpu=None):
     """Spawned consumer process."""
+    if cpu is not None:
+        try:
+            os.sched_setaffinity(0, {cpu})
+        except OSError:
+            pass
     try:
         res = asyncio.run(run_consumer(a, seed, barrier.wait))
         results.put(res)
@@ -229,7 +237,12 @@ def run_rank(a, dist: _Dist, procs: int) -> dict:
     ctx = mp.get_context("spawn")
     barrier = ctx.Barrier(procs + 1)
     results = ctx.Queue()
-    children = [ctx.Process(target=_consumer_entry, args=(a, base_seed + 104729 * i, barrier, results),
+    cpus = sorted(os.sched_getaffinity(0)) if a.pin and hasattr(os, "sched_getaffinity") else []
+    first = dist.local_rank * procs
+
+    def cpu_for(i):
+        return cpus[(first + i) % len(cpus)] if cpus else None
+    children = [ctx.Process(target=_consumer_entry, args=(a, base_seed + 104729 * i, barrier, results, cpu_for(i)),
                             daemon=True) for i in range(procs)]
     for c in children:
         c.start()
