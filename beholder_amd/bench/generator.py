@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import random
 import uuid
-from typing import Dict, List, Sequence, Tuple
+from typing import List, Sequence, Tuple
 
 from ..models import proto
 from ..ops import codec_for, frames
@@ -88,10 +88,3 @@ class Workload:
 
     def framed(self, n: int) -> bytes:
         return frames(self.events(n))
-
-
-def count_topics(events: Sequence[Tuple[int, bytes]]) -> Dict[int, int]:
-    c: Dict[int, int] = {}
-    for t, _ in events:
-        c[t] = c.get(t, 0) + 1
-    return c

@@ -136,9 +136,6 @@ class Node:
         v = self[key]
         return default if v is None else v
 
-    def to_dict(self) -> dict:
-        return copy.deepcopy(dict(self._d))
-
     def require(self, dotted: str) -> Any:
         """Dereference ``a.b.c`` the way JS does *without* optional chaining.
 

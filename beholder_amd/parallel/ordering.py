@@ -34,9 +34,6 @@ class KeyedSerializer:
         self.max_chain = 0
         self.serialized = 0  # items that had to wait behind another with the same key
 
-    def set_key_fn(self, fn: Callable[[Any], Any]) -> None:
-        self._key_fn = fn
-
     @property
     def active_keys(self) -> int:
         return len(self._chains)

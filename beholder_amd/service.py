@@ -496,6 +496,12 @@ class Service:
             out["handler_errors"] = {k[0]: v for k, v in self.handler_errors.values().items()}
             out["trello_comments"] = self.trello_comments_total.get()
             out["progress_updates"] = {k[0]: v for k, v in self.progress_updates_total.values().items()}
+        if self.serializer is not None:  # per-media ordering (opt-in)
+            out["ordering"] = {"active_keys": self.serializer.active_keys,
+                               "serialized": self.serializer.serialized, "max_chain": self.serializer.max_chain}
+        if self.serializer is not None:  # per-media ordering (opt-in)
+            out["ordering"] = {"active_keys": self.serializer.active_keys,
+                               "serialized": self.serializer.serialized, "max_chain": self.serializer.max_chain}
         http_stats = getattr(self._http, "stats", None)
         if callable(http_stats):  # keep-alive pool accounting (sinks/h1.py)
             out["http"] = http_stats()

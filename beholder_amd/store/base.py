@@ -48,9 +48,6 @@ class Media(NamedTuple):
     metadataId: str = ""      # Kitsu id (index.js:103)
     status: int = 0           # TelemetryStatusEntry (index.js:94)
 
-    def as_dict(self) -> dict:
-        return self._asdict()
-
 
 FIELDS = Media._fields
 

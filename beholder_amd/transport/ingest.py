@@ -25,7 +25,7 @@ import asyncio
 import os
 import sys
 import threading
-from typing import List, Optional, Sequence
+from typing import Optional, Sequence
 
 from ..ops import Ingest, Settler, frame
 from .base import Source
@@ -179,15 +179,6 @@ class BytesSource(FdSource):
         if self._writer is not None:
             self._writer.join(timeout=5)
 
-
-def read_all(source: FdSource) -> List:
-    """Synchronously drain a source (tests)."""
-    out = []
-    while True:
-        got = source.ingest.pop(1 << 16, 1.0)
-        if got is None:
-            return out
-        out.extend(got)
 
 
 class NdjsonSource(FdSource):

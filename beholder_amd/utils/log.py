@@ -327,7 +327,3 @@ class MemoryStream:
 
     def __iter__(self):
         return iter(self.lines)
-
-
-def get_logger(name: str = "index.js", level: str = "info", stream: Optional[TextIO] = None) -> Logger:
-    return Logger(name=name, level=level, stream=stream)

@@ -74,3 +74,17 @@ def test_encode_query_native_matches_python(d):
 def test_encode_query_matches_encodeURIComponent():
     assert encode_query({"text": "A: **45%** (_h_) é/?&="}) == \
         "text=A%3A%20**45%25**%20(_h_)%20%C3%A9%2F%3F%26%3D"
+
+
+def test_native_log_line_matches_python_formatter():
+    """utils.log.Logger.py_line is the readable reference of the native pino line formatter."""
+    from beholder_amd.ops import native
+    from beholder_amd.utils.log import Logger, NullStream
+    lg = Logger(stream=NullStream())
+    cases = [("plain",), ("creating comment on", "c1", "with text:", "DEPLOYED: Progress **5%** (_h_)"),
+             ("processing progress update on media", "m", "status", 4, "percent", 99.5),
+             ("quote \" and \\ and \n", None, True, -0.0, 1e21), ("%s and %d", "x", 42)]
+    for args in cases:
+        want = lg.py_line(30, args, time_ms=1234)
+        got = native.format_line(30, 1234, lg._prefix, None, args)
+        assert got == want, args
