@@ -27,11 +27,28 @@ valid_status = st.builds(lambda m, s: status_msg(m, s), st.sampled_from(["m1", "
 payload = st.one_of(st.binary(max_size=40), valid_progress, valid_status)
 
 
-def _run(msgs):
+class _SlowStore(MemoryStore):
+    """Every store call really suspends, so handlers run through the native Driver."""
+
+    get_by_id_nowait = None
+    update_status_nowait = None
+
+    async def get_by_id(self, media_id):
+        await asyncio.sleep(0)
+        return await super().get_by_id(media_id)
+
+    async def update_status(self, media_id, status):
+        await asyncio.sleep(0)
+        return await super().update_status(media_id, status)
+
+
+def _run(msgs, suspend: bool = False):
     async def go():
         b = MemoryBroker()
         src = b.consumer(prefetch=1000)
-        svc = Service(cfg(), source=src, store=MemoryStore(MEDIA), http=RecordingHttpClient(keep=4),
+        store = _SlowStore(MEDIA) if suspend else MemoryStore(MEDIA)
+        http = RecordingHttpClient(keep=4, delay_s=0.0005 if suspend else 0.0)
+        svc = Service(cfg(), source=src, store=store, http=http,
                       logger=Logger(stream=NullStream()), serve_metrics=False)
         await svc.init()
         for topic, body in msgs:
@@ -45,9 +62,10 @@ def _run(msgs):
 
 
 @settings(max_examples=60, deadline=None, suppress_health_check=[HealthCheck.too_slow])
-@given(st.lists(st.tuples(st.sampled_from([STATUS, PROGRESS]), payload), max_size=30))
-def test_fuzzed_messages_are_all_accounted_for(msgs):
-    s, broker = _run(msgs)
+@given(st.lists(st.tuples(st.sampled_from([STATUS, PROGRESS]), payload), max_size=30), st.booleans())
+def test_fuzzed_messages_are_all_accounted_for(msgs, suspend):
+    """Both dispatch paths: eager completion and suspension (native Driver resumes handlers)."""
+    s, broker = _run(msgs, suspend)
     n_prog = sum(1 for t, _ in msgs if t == PROGRESS)
     n = len(msgs)
     # Q7: every progress message is acked; nothing is settled twice
