@@ -64,6 +64,13 @@ AmqpDemux = native.AmqpDemux
 H1Parser = native.H1Parser
 PgReader = native.PgReader
 Driver = native.Driver
+IOFuture = native.IOFuture
+if os.environ.get("BEHOLDER_IOFUTURE", "1") == "0":  # A/B switch: plain asyncio futures for I/O replies
+    import asyncio as _asyncio
+
+    class IOFuture(_asyncio.Future):  # type: ignore[no-redef]
+        resolve = _asyncio.Future.set_result
+        reject = _asyncio.Future.set_exception
 AckBatcher = native.AckBatcher
 dispatch_batch = native.dispatch_batch
 frame = native.frame
@@ -120,7 +127,7 @@ def codec_for(ptype) -> Optional[object]:
 
 
 __all__ = [
-    "native", "AckBatcher", "AmqpDemux", "Driver", "H1Parser", "PgReader", "MessageCodec", "Ingest", "Delivery", "Settler", "Counter", "Histogram",
+    "native", "AckBatcher", "AmqpDemux", "Driver", "IOFuture", "H1Parser", "PgReader", "MessageCodec", "Ingest", "Delivery", "Settler", "Counter", "Histogram",
     "frame", "frames", "mono_ns", "codec_for", "field_table", "format_line", "quick_format", "js_str",
     "js_number", "encode_query", "quote_component",
 ]

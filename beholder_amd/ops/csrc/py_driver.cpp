@@ -314,6 +314,423 @@ PyGetSetDef driver_getset[] = {
     {"steps", reinterpret_cast<getter>(driver_get_steps), nullptr, "resumptions so far", nullptr},
     {nullptr, nullptr, nullptr, nullptr, nullptr}};
 
+// ---- IOFuture ------------------------------------------------------------------
+// A minimal asyncio-compatible future for the I/O clients' replies (store/pgwire.py,
+// sinks/h1.py). It implements the subset of the asyncio.Future API that Task, gather and
+// wait_for use: _asyncio_future_blocking, get_loop, done/cancelled/result/exception,
+// add/remove_done_callback(context=), cancel, _make_cancelled_error, and __await__.
+// The point is resolve()/reject(). When a protocol callback (data_received) completes a
+// reply, a Driver waiting on it is resumed right there. asyncio would instead pay a
+// call_soon, a Handle and a trip through the event loop per reply. Every other
+// callback (a Task, gather, wait_for) is still scheduled with loop.call_soon, as
+// asyncio does. set_result/set_exception/cancel always schedule.
+struct IOFutureObject {
+  PyObject_HEAD PyObject* loop;
+  PyObject* result;
+  PyObject* exc;
+  PyObject* cancel_msg;
+  PyObject* cb0;    // first callback (common case: exactly one)
+  PyObject* ctx0;   // its context or NULL
+  PyObject* more;   // list of (fn, ctx) for further callbacks, or NULL
+  uint8_t state;    // 0 pending, 1 finished, 2 cancelled
+  uint8_t blocking;
+};
+
+PyTypeObject IOFutureType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+PyObject* g_invalid_state = nullptr;  // asyncio.InvalidStateError
+PyObject* s_call_exception_handler = nullptr;
+
+int iof_traverse(IOFutureObject* f, visitproc visit, void* arg) {
+  Py_VISIT(f->loop);
+  Py_VISIT(f->result);
+  Py_VISIT(f->exc);
+  Py_VISIT(f->cancel_msg);
+  Py_VISIT(f->cb0);
+  Py_VISIT(f->ctx0);
+  Py_VISIT(f->more);
+  return 0;
+}
+
+int iof_clear(IOFutureObject* f) {
+  Py_CLEAR(f->loop);
+  Py_CLEAR(f->result);
+  Py_CLEAR(f->exc);
+  Py_CLEAR(f->cancel_msg);
+  Py_CLEAR(f->cb0);
+  Py_CLEAR(f->ctx0);
+  Py_CLEAR(f->more);
+  return 0;
+}
+
+void iof_dealloc(IOFutureObject* f) {
+  PyObject_GC_UnTrack(f);
+  iof_clear(f);
+  Py_TYPE(f)->tp_free(reinterpret_cast<PyObject*>(f));
+}
+
+PyObject* iof_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
+  static const char* kwlist[] = {"loop", nullptr};
+  PyObject* loop = nullptr;
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "|O", const_cast<char**>(kwlist), &loop)) return nullptr;
+  IOFutureObject* f = reinterpret_cast<IOFutureObject*>(type->tp_alloc(type, 0));
+  if (!f) return nullptr;
+  f->result = f->exc = f->cancel_msg = f->cb0 = f->ctx0 = f->more = nullptr;
+  f->state = 0;
+  f->blocking = 0;
+  if (!loop || loop == Py_None) {
+    f->loop = PyObject_CallNoArgs(g_get_running_loop);
+    if (!f->loop) {
+      Py_DECREF(f);
+      return nullptr;
+    }
+  } else {
+    Py_INCREF(loop);
+    f->loop = loop;
+  }
+  return reinterpret_cast<PyObject*>(f);
+}
+
+PyObject* make_cancelled(IOFutureObject* f) {
+  if (f->cancel_msg) return PyObject_CallOneArg(g_cancelled_error, f->cancel_msg);
+  return PyObject_CallNoArgs(g_cancelled_error);
+}
+
+// Schedules fn(self) with loop.call_soon(fn, self, context=ctx).
+int schedule_cb(IOFutureObject* f, PyObject* fn, PyObject* ctx) {
+  PyObject* call_soon = PyObject_GetAttr(f->loop, s_call_soon);
+  if (!call_soon) return -1;
+  PyObject* args = PyTuple_Pack(2, fn, reinterpret_cast<PyObject*>(f));
+  if (!args) {
+    Py_DECREF(call_soon);
+    return -1;
+  }
+  PyObject* kw = nullptr;
+  if (ctx) {
+    kw = PyDict_New();
+    if (!kw || PyDict_SetItemString(kw, "context", ctx) < 0) {
+      Py_XDECREF(kw);
+      Py_DECREF(args);
+      Py_DECREF(call_soon);
+      return -1;
+    }
+  }
+  PyObject* h = PyObject_Call(call_soon, args, kw);
+  Py_XDECREF(kw);
+  Py_DECREF(args);
+  Py_DECREF(call_soon);
+  if (!h) return -1;
+  Py_DECREF(h);
+  return 0;
+}
+
+// Runs fn(self) now (Driver callbacks on the synchronous path). Exception subclasses go to
+// the loop's exception handler, as asyncio does for callbacks; anything else propagates.
+int call_now(IOFutureObject* f, PyObject* fn) {
+  PyObject* r = PyObject_CallOneArg(fn, reinterpret_cast<PyObject*>(f));
+  if (r) {
+    Py_DECREF(r);
+    return 0;
+  }
+  if (!PyErr_ExceptionMatches(PyExc_Exception)) return -1;
+  PyObject* e = fetch_exc();
+  PyObject* ctx = Py_BuildValue("{s:s,s:O,s:O}", "message", "Exception in IOFuture done callback", "exception",
+                                e ? e : Py_None, "future", reinterpret_cast<PyObject*>(f));
+  Py_XDECREF(e);
+  if (!ctx) return -1;
+  PyObject* h = PyObject_CallMethodOneArg(f->loop, s_call_exception_handler, ctx);
+  Py_DECREF(ctx);
+  if (!h) return -1;
+  Py_DECREF(h);
+  return 0;
+}
+
+// Fires the callbacks after a state change. sync: Driver callbacks run immediately.
+int fire(IOFutureObject* f, bool sync) {
+  PyObject* fn = f->cb0;
+  PyObject* ctx = f->ctx0;
+  PyObject* more = f->more;
+  f->cb0 = f->ctx0 = f->more = nullptr;
+  int rc = 0;
+  if (fn) {
+    if (sync && Py_TYPE(fn) == &DriverType)
+      rc = call_now(f, fn);
+    else
+      rc = schedule_cb(f, fn, ctx);
+    Py_DECREF(fn);
+    Py_XDECREF(ctx);
+  }
+  if (more) {
+    Py_ssize_t n = PyList_GET_SIZE(more);
+    for (Py_ssize_t i = 0; i < n && rc == 0; ++i) {
+      PyObject* pair = PyList_GET_ITEM(more, i);
+      PyObject* fn2 = PyTuple_GET_ITEM(pair, 0);
+      PyObject* ctx2 = PyTuple_GET_ITEM(pair, 1);
+      if (sync && Py_TYPE(fn2) == &DriverType)
+        rc = call_now(f, fn2);
+      else
+        rc = schedule_cb(f, fn2, ctx2 == Py_None ? nullptr : ctx2);
+    }
+    Py_DECREF(more);
+  }
+  return rc;
+}
+
+PyObject* invalid_state(const char* msg) {
+  PyErr_SetString(g_invalid_state, msg);
+  return nullptr;
+}
+
+PyObject* iof_finish_result(IOFutureObject* f, PyObject* v, bool sync) {
+  if (f->state) return invalid_state("invalid state");
+  Py_INCREF(v);
+  f->result = v;
+  f->state = 1;
+  if (fire(f, sync) < 0) return nullptr;
+  Py_RETURN_NONE;
+}
+
+PyObject* iof_finish_exc(IOFutureObject* f, PyObject* e, bool sync) {
+  if (f->state) return invalid_state("invalid state");
+  PyObject* inst = e;
+  if (PyType_Check(e)) {
+    inst = PyObject_CallNoArgs(e);
+    if (!inst) return nullptr;
+  } else {
+    Py_INCREF(inst);
+  }
+  if (!PyExceptionInstance_Check(inst)) {
+    Py_DECREF(inst);
+    PyErr_SetString(PyExc_TypeError, "invalid exception object");
+    return nullptr;
+  }
+  if (PyErr_GivenExceptionMatches(inst, PyExc_StopIteration)) {
+    Py_DECREF(inst);
+    PyErr_SetString(PyExc_TypeError, "StopIteration interacts badly with generators and cannot be raised into a Future");
+    return nullptr;
+  }
+  f->exc = inst;
+  f->state = 1;
+  if (fire(f, sync) < 0) return nullptr;
+  Py_RETURN_NONE;
+}
+
+PyObject* iof_set_result(IOFutureObject* f, PyObject* v) { return iof_finish_result(f, v, false); }
+PyObject* iof_resolve(IOFutureObject* f, PyObject* v) { return iof_finish_result(f, v, true); }
+PyObject* iof_set_exception(IOFutureObject* f, PyObject* e) { return iof_finish_exc(f, e, false); }
+PyObject* iof_reject(IOFutureObject* f, PyObject* e) { return iof_finish_exc(f, e, true); }
+
+PyObject* iof_cancel(IOFutureObject* f, PyObject* args, PyObject* kwds) {
+  static const char* kwlist[] = {"msg", nullptr};
+  PyObject* msg = Py_None;
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "|O", const_cast<char**>(kwlist), &msg)) return nullptr;
+  if (f->state) Py_RETURN_FALSE;
+  f->state = 2;
+  if (msg != Py_None) {
+    Py_INCREF(msg);
+    f->cancel_msg = msg;
+  }
+  if (fire(f, false) < 0) return nullptr;
+  Py_RETURN_TRUE;
+}
+
+PyObject* iof_result(IOFutureObject* f, PyObject*) {
+  if (f->state == 2) {
+    PyObject* e = make_cancelled(f);
+    if (!e) return nullptr;
+    PyErr_SetObject(g_cancelled_error, e);
+    Py_DECREF(e);
+    return nullptr;
+  }
+  if (!f->state) return invalid_state("Result is not ready.");
+  if (f->exc) {
+    PyErr_SetObject(reinterpret_cast<PyObject*>(Py_TYPE(f->exc)), f->exc);
+    return nullptr;
+  }
+  Py_INCREF(f->result);
+  return f->result;
+}
+
+PyObject* iof_exception(IOFutureObject* f, PyObject*) {
+  if (f->state == 2) {
+    PyObject* e = make_cancelled(f);
+    if (!e) return nullptr;
+    PyErr_SetObject(g_cancelled_error, e);
+    Py_DECREF(e);
+    return nullptr;
+  }
+  if (!f->state) return invalid_state("Exception is not set.");
+  PyObject* e = f->exc ? f->exc : Py_None;
+  Py_INCREF(e);
+  return e;
+}
+
+PyObject* iof_add_done_callback(IOFutureObject* f, PyObject* args, PyObject* kwds) {
+  static const char* kwlist[] = {"fn", "context", nullptr};
+  PyObject *fn, *ctx = Py_None;
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "O|$O", const_cast<char**>(kwlist), &fn, &ctx)) return nullptr;
+  PyObject* c = ctx == Py_None ? nullptr : ctx;
+  if (f->state) {
+    if (schedule_cb(f, fn, c) < 0) return nullptr;
+    Py_RETURN_NONE;
+  }
+  if (!f->cb0) {
+    Py_INCREF(fn);
+    f->cb0 = fn;
+    Py_XINCREF(c);
+    f->ctx0 = c;
+    Py_RETURN_NONE;
+  }
+  if (!f->more && !(f->more = PyList_New(0))) return nullptr;
+  PyObject* pair = PyTuple_Pack(2, fn, c ? c : Py_None);
+  if (!pair) return nullptr;
+  int rc = PyList_Append(f->more, pair);
+  Py_DECREF(pair);
+  if (rc < 0) return nullptr;
+  Py_RETURN_NONE;
+}
+
+PyObject* iof_remove_done_callback(IOFutureObject* f, PyObject* fn) {
+  Py_ssize_t removed = 0;
+  if (f->cb0) {
+    int eq = PyObject_RichCompareBool(f->cb0, fn, Py_EQ);
+    if (eq < 0) return nullptr;
+    if (eq) {
+      Py_CLEAR(f->cb0);
+      Py_CLEAR(f->ctx0);
+      ++removed;
+    }
+  }
+  if (f->more) {
+    PyObject* keep = PyList_New(0);
+    if (!keep) return nullptr;
+    for (Py_ssize_t i = 0; i < PyList_GET_SIZE(f->more); ++i) {
+      PyObject* pair = PyList_GET_ITEM(f->more, i);
+      int eq = PyObject_RichCompareBool(PyTuple_GET_ITEM(pair, 0), fn, Py_EQ);
+      if (eq < 0) {
+        Py_DECREF(keep);
+        return nullptr;
+      }
+      if (eq) {
+        ++removed;
+      } else if (PyList_Append(keep, pair) < 0) {
+        Py_DECREF(keep);
+        return nullptr;
+      }
+    }
+    Py_SETREF(f->more, keep);
+  }
+  return PyLong_FromSsize_t(removed);
+}
+
+PyObject* iof_done(IOFutureObject* f, PyObject*) { return PyBool_FromLong(f->state != 0); }
+PyObject* iof_cancelled(IOFutureObject* f, PyObject*) { return PyBool_FromLong(f->state == 2); }
+PyObject* iof_get_loop(IOFutureObject* f, PyObject*) {
+  Py_INCREF(f->loop);
+  return f->loop;
+}
+PyObject* iof_make_cancelled_error(IOFutureObject* f, PyObject*) { return make_cancelled(f); }
+
+PyObject* iof_get_blocking(IOFutureObject* f, void*) { return PyBool_FromLong(f->blocking); }
+int iof_set_blocking(IOFutureObject* f, PyObject* v, void*) {
+  if (!v) {
+    PyErr_SetString(PyExc_AttributeError, "cannot delete _asyncio_future_blocking");
+    return -1;
+  }
+  int b = PyObject_IsTrue(v);
+  if (b < 0) return -1;
+  f->blocking = uint8_t(b);
+  return 0;
+}
+PyObject* iof_get_log_tb(IOFutureObject*, void*) { Py_RETURN_FALSE; }
+int iof_set_log_tb(IOFutureObject*, PyObject*, void*) { return 0; }
+
+// await protocol: the future is its own iterator (one awaiter at a time, as in our clients)
+PyObject* iof_await(IOFutureObject* f) {
+  Py_INCREF(f);
+  return reinterpret_cast<PyObject*>(f);
+}
+
+PySendResult iof_am_send(IOFutureObject* f, PyObject*, PyObject** out) {
+  if (!f->state) {
+    f->blocking = 1;
+    Py_INCREF(f);
+    *out = reinterpret_cast<PyObject*>(f);
+    return PYGEN_NEXT;
+  }
+  PyObject* r = iof_result(f, nullptr);
+  if (!r) {
+    *out = nullptr;
+    return PYGEN_ERROR;
+  }
+  *out = r;
+  return PYGEN_RETURN;
+}
+
+PyObject* iof_iternext(IOFutureObject* f) {
+  PyObject* out;
+  PySendResult r = iof_am_send(f, Py_None, &out);
+  if (r == PYGEN_NEXT) return out;
+  if (r == PYGEN_ERROR) return nullptr;
+  // return value -> StopIteration(value)
+  if (out == Py_None) {
+    Py_DECREF(out);
+    PyErr_SetNone(PyExc_StopIteration);
+  } else {
+    PyObject* e = PyObject_CallOneArg(PyExc_StopIteration, out);
+    Py_DECREF(out);
+    if (!e) return nullptr;
+    PyErr_SetObject(PyExc_StopIteration, e);
+    Py_DECREF(e);
+  }
+  return nullptr;
+}
+
+PyObject* iof_send(IOFutureObject* f, PyObject*) { return iof_iternext(f); }
+PyObject* iof_await_method(IOFutureObject* f, PyObject*) { return iof_await(f); }
+
+PyObject* iof_throw(IOFutureObject*, PyObject* args) {
+  PyObject *t, *v = nullptr, *tb = nullptr;
+  if (!PyArg_ParseTuple(args, "O|OO", &t, &v, &tb)) return nullptr;
+  if (PyExceptionInstance_Check(t))
+    PyErr_SetObject(reinterpret_cast<PyObject*>(Py_TYPE(t)), t);
+  else
+    PyErr_SetObject(t, v ? v : Py_None);
+  return nullptr;
+}
+
+PyAsyncMethods iof_async = {reinterpret_cast<unaryfunc>(iof_await), nullptr, nullptr,
+                            reinterpret_cast<sendfunc>(iof_am_send)};
+
+PyMethodDef iof_methods[] = {
+    {"get_loop", reinterpret_cast<PyCFunction>(iof_get_loop), METH_NOARGS, nullptr},
+    {"done", reinterpret_cast<PyCFunction>(iof_done), METH_NOARGS, nullptr},
+    {"cancelled", reinterpret_cast<PyCFunction>(iof_cancelled), METH_NOARGS, nullptr},
+    {"result", reinterpret_cast<PyCFunction>(iof_result), METH_NOARGS, nullptr},
+    {"exception", reinterpret_cast<PyCFunction>(iof_exception), METH_NOARGS, nullptr},
+    {"add_done_callback", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(iof_add_done_callback)),
+     METH_VARARGS | METH_KEYWORDS, nullptr},
+    {"remove_done_callback", reinterpret_cast<PyCFunction>(iof_remove_done_callback), METH_O, nullptr},
+    {"cancel", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(iof_cancel)),
+     METH_VARARGS | METH_KEYWORDS, nullptr},
+    {"set_result", reinterpret_cast<PyCFunction>(iof_set_result), METH_O, "set_result(v): callbacks via call_soon"},
+    {"set_exception", reinterpret_cast<PyCFunction>(iof_set_exception), METH_O, nullptr},
+    {"resolve", reinterpret_cast<PyCFunction>(iof_resolve), METH_O,
+     "resolve(v): like set_result, but a waiting Driver resumes immediately (protocol callbacks only)"},
+    {"reject", reinterpret_cast<PyCFunction>(iof_reject), METH_O,
+     "reject(exc): like set_exception, but a waiting Driver resumes immediately"},
+    {"_make_cancelled_error", reinterpret_cast<PyCFunction>(iof_make_cancelled_error), METH_NOARGS, nullptr},
+    {"send", reinterpret_cast<PyCFunction>(iof_send), METH_O, nullptr},
+    {"throw", reinterpret_cast<PyCFunction>(iof_throw), METH_VARARGS, nullptr},
+    {"__await__", reinterpret_cast<PyCFunction>(iof_await_method), METH_NOARGS, nullptr},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyGetSetDef iof_getset[] = {
+    {"_asyncio_future_blocking", reinterpret_cast<getter>(iof_get_blocking),
+     reinterpret_cast<setter>(iof_set_blocking), nullptr, nullptr},
+    {"_log_traceback", reinterpret_cast<getter>(iof_get_log_tb), reinterpret_cast<setter>(iof_set_log_tb), nullptr,
+     nullptr},
+    {nullptr, nullptr, nullptr, nullptr, nullptr}};
+
 }  // namespace
 
 int init_driver_types(PyObject* m) {
@@ -345,7 +762,31 @@ int init_driver_types(PyObject* m) {
   DriverType.tp_getset = driver_getset;
   if (PyType_Ready(&DriverType) < 0) return -1;
   Py_INCREF(&DriverType);
-  return PyModule_AddObject(m, "Driver", reinterpret_cast<PyObject*>(&DriverType));
+  if (PyModule_AddObject(m, "Driver", reinterpret_cast<PyObject*>(&DriverType)) < 0) return -1;
+
+  PyObject* aio2 = PyImport_ImportModule("asyncio");
+  if (!aio2) return -1;
+  g_invalid_state = PyObject_GetAttrString(aio2, "InvalidStateError");
+  Py_DECREF(aio2);
+  if (!g_invalid_state) return -1;
+  s_call_exception_handler = PyUnicode_InternFromString("call_exception_handler");
+  if (!s_call_exception_handler) return -1;
+  IOFutureType.tp_name = "beholder_amd.ops._native.IOFuture";
+  IOFutureType.tp_basicsize = sizeof(IOFutureObject);
+  IOFutureType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC;
+  IOFutureType.tp_doc = "IOFuture(loop=None): asyncio-compatible reply future with synchronous Driver wake-up";
+  IOFutureType.tp_new = iof_new;
+  IOFutureType.tp_dealloc = reinterpret_cast<destructor>(iof_dealloc);
+  IOFutureType.tp_traverse = reinterpret_cast<traverseproc>(iof_traverse);
+  IOFutureType.tp_clear = reinterpret_cast<inquiry>(iof_clear);
+  IOFutureType.tp_as_async = &iof_async;
+  IOFutureType.tp_iter = reinterpret_cast<getiterfunc>(iof_await);
+  IOFutureType.tp_iternext = reinterpret_cast<iternextfunc>(iof_iternext);
+  IOFutureType.tp_methods = iof_methods;
+  IOFutureType.tp_getset = iof_getset;
+  if (PyType_Ready(&IOFutureType) < 0) return -1;
+  Py_INCREF(&IOFutureType);
+  return PyModule_AddObject(m, "IOFuture", reinterpret_cast<PyObject*>(&IOFutureType));
 }
 
 }  // namespace beholder

@@ -36,6 +36,7 @@ from typing import Deque, Dict, Optional, Tuple
 from urllib.parse import quote, unquote, urljoin
 
 from ..ops import H1Parser
+from ..ops import IOFuture as _IOFuture
 from .http import HttpClient, HttpError, HttpResponse, redact, with_query
 
 _IDEMPOTENT = frozenset(("GET", "HEAD", "PUT", "DELETE", "OPTIONS"))
@@ -84,7 +85,7 @@ class _Conn(asyncio.Protocol):
             if w is None or w.done():
                 self.abort()  # unsolicited response
             else:
-                w.set_result(r)
+                w.resolve(r)  # a handler waiting on it (native Driver) resumes right here
 
     def eof_received(self):
         return False  # let the transport close; connection_lost completes the response
@@ -338,7 +339,7 @@ class H1Client(HttpClient):
                 raise HttpError(_connect_error(e, o)) from None
             reused = c.uses > 0
             c.uses += 1
-            w = loop.create_future()
+            w = _IOFuture(loop)
             c.waiter = w
             c.deadline = deadline
             c.what = (m, cur)

@@ -34,6 +34,7 @@ import struct
 from typing import Any, Deque, Dict, List, Optional, Sequence, Tuple
 from urllib.parse import parse_qs, unquote, urlsplit
 
+from ..ops import IOFuture as _IOFuture
 from ..ops import PgReader
 from ..ops import native as _native
 
@@ -211,9 +212,9 @@ class PgConnection(asyncio.Protocol):
                     if new_sql is not None and not parse_ok and self._stmts.get(new_sql) == name:
                         del self._stmts[new_sql]
                     if not fut.done():
-                        fut.set_exception(PgError(err))
+                        fut.reject(PgError(err))
                 elif not fut.done():
-                    fut.set_result((rows, tag))
+                    fut.resolve((rows, tag))  # a handler waiting on it resumes right here
             else:
                 self._message(it[0], it[1])
 
@@ -355,7 +356,9 @@ class PgConnection(asyncio.Protocol):
 
     def execute(self, sql: str, params: Sequence[Any] = ()) -> "asyncio.Future[Tuple[List[Tuple], str]]":
         """Queue one statement with ``$n`` parameters; the returned future resolves to
-        ``(rows, command_tag)`` or raises :class:`PgError`."""
+        ``(rows, command_tag)`` or raises :class:`PgError`. It is an ``ops.IOFuture``: a
+        handler awaiting it through the native Driver resumes inside ``data_received``, with no
+        event-loop round trip per reply."""
         if self.closed:
             raise PgProtocolError("connection is closed")
         out = self._out
@@ -370,7 +373,7 @@ class PgConnection(asyncio.Protocol):
             out.append(b"P" + _PACK_LEN(len(pbody) + 4) + pbody)
         out.append(_pg_bind(name, params))  # Bind + Describe + Execute + Sync (ops/csrc/py_pg.cpp)
         loop = asyncio.get_running_loop()
-        fut = loop.create_future()
+        fut = _IOFuture(loop)
         self._pending.append((fut, new_sql, name))
         if self._flush_handle is None:
             self._flush_handle = loop.call_soon(self._flush)
