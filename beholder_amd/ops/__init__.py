@@ -69,6 +69,9 @@ if os.environ.get("BEHOLDER_IOFUTURE", "1") == "0":  # A/B switch: plain asyncio
     import asyncio as _asyncio
 
     class IOFuture(_asyncio.Future):  # type: ignore[no-redef]
+        def __init__(self, loop=None):
+            super().__init__(loop=loop)
+
         resolve = _asyncio.Future.set_result
         reject = _asyncio.Future.set_exception
 AckBatcher = native.AckBatcher
