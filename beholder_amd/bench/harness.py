@@ -267,6 +267,21 @@ def run_config(name: str, *, duration_s: Optional[float] = None, events: Optiona
     return res
 
 
+async def _wait_acked(settler, n: int, task, stall_s: float = 15.0) -> None:
+    """Until n deliveries are settled one way or another (acked, or abandoned under Q1), the
+    service stops, or nothing moves for ``stall_s`` (a broken run must not hang the bench)."""
+    last, t_last = -1, time.monotonic()
+    while not task.done():
+        done = settler.acked + settler.abandoned + settler.nacked + settler.rejected
+        if done >= n:
+            return
+        if done != last:
+            last, t_last = done, time.monotonic()
+        elif time.monotonic() - t_last > stall_s:
+            return
+        await asyncio.sleep(0.001)
+
+
 def _spawn(module: str, copies: int = 1, args=()) -> "tuple":
     """Starts ``copies`` of a bench endpoint process sharing one port (SO_REUSEPORT).
     Returns ``(port, procs)``; each process printed ``READY <port>``."""
@@ -367,8 +382,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2) -> dict:
             ru0 = resource.getrusage(resource.RUSAGE_SELF)
             t0 = time.perf_counter()
             task = asyncio.ensure_future(svc.run())
-            while src.settler.acked < n and not task.done():
-                await asyncio.sleep(0.001)
+            await _wait_acked(src.settler, n, task)
             elapsed = time.perf_counter() - t0
             ru1 = resource.getrusage(resource.RUSAGE_SELF)
             await asyncio.sleep(0.05)  # let the last acks flush
@@ -431,8 +445,7 @@ def _amqp(n: int) -> dict:
             ru0 = resource.getrusage(resource.RUSAGE_SELF)
             t0 = time.perf_counter()
             task = asyncio.ensure_future(svc.run())
-            while src.settler.acked < n:
-                await asyncio.sleep(0.001)
+            await _wait_acked(src.settler, n, task)
             elapsed = time.perf_counter() - t0
             ru1 = resource.getrusage(resource.RUSAGE_SELF)
             await asyncio.sleep(0.05)  # let the last acks flush
