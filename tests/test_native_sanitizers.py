@@ -21,5 +21,9 @@ def test_ring_stress_under_sanitizer(target):
     assert b.returncode == 0, b.stderr
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1", ASAN_OPTIONS="detect_leaks=1")
     r = subprocess.run([os.path.join(HERE, target)], capture_output=True, text=True, timeout=300, env=env)
+    if "unexpected memory mapping" in r.stderr:
+        # TSan's shadow layout clashes with some kernels' mmap randomisation (seen on the GPU
+        # box image): an environment limit, not a finding
+        pytest.skip("ThreadSanitizer cannot map its shadow memory on this kernel")
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
     assert "ALL OK" in r.stdout
