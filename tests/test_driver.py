@@ -163,3 +163,92 @@ def test_no_reference_leaks():
     ref, _ = run(go())
     gc.collect()
     assert ref() is None
+
+
+# ---------------------------------------------------------------- IOFuture ---
+
+def test_iofuture_is_an_asyncio_future_for_tasks_gather_and_wait_for():
+    from beholder_amd.ops import native
+    IOFuture = native.IOFuture
+
+    async def go():
+        loop = asyncio.get_running_loop()
+        f = IOFuture(loop)
+        assert asyncio.isfuture(f) and not f.done() and f.get_loop() is loop
+        with pytest.raises(asyncio.InvalidStateError):
+            f.result()
+        loop.call_soon(f.set_result, 42)
+        assert await f == 42 and f.done()
+        e = IOFuture()
+        loop.call_soon(e.set_exception, KeyError("k"))
+        with pytest.raises(KeyError):
+            await e
+        fs = [IOFuture() for _ in range(3)]
+        for i, x in enumerate(fs):
+            loop.call_soon(x.resolve, i)  # outside a Driver, resolve behaves like set_result
+        assert await asyncio.gather(*fs) == [0, 1, 2]
+        slow = IOFuture()
+        with pytest.raises(asyncio.TimeoutError):
+            await asyncio.wait_for(slow, 0.01)
+        assert slow.cancelled()
+        with pytest.raises(asyncio.CancelledError):
+            slow.result()
+        late = []
+        done = IOFuture()
+        done.set_result(1)
+        done.add_done_callback(lambda fut: late.append(fut.result()))  # already done: scheduled
+        assert late == []
+        await asyncio.sleep(0)
+        cb = late.append
+        g = IOFuture()
+        g.add_done_callback(cb)
+        g.add_done_callback(cb)
+        assert g.remove_done_callback(cb) == 2
+        with pytest.raises(asyncio.InvalidStateError):
+            done.set_result(2)
+        return late
+    assert run(go()) == [1]
+
+
+def test_iofuture_resolve_resumes_a_driver_synchronously():
+    from beholder_amd.ops import native
+    order = []
+
+    async def handler(fut):
+        v = await fut
+        order.append(("resumed", v))
+
+    async def go():
+        f = native.IOFuture()
+        coro = handler(f)
+        Driver(coro, lambda drv, exc: order.append(("done", exc))).start(coro.send(None))
+        f.resolve("row")
+        order.append("after resolve")
+        g = native.IOFuture()
+        coro = handler(g)
+        Driver(coro, lambda drv, exc: order.append(("done", type(exc).__name__))).start(coro.send(None))
+        g.reject(ValueError("bad"))
+        order.append("after reject")
+    run(go())
+    assert order == [("resumed", "row"), ("done", None), "after resolve", ("done", "ValueError"), "after reject"]
+
+
+def test_iofuture_sync_callback_errors_go_to_the_loop_handler():
+    from beholder_amd.ops import native
+    seen = []
+
+    async def handler(fut):
+        await fut
+
+    async def go():
+        loop = asyncio.get_running_loop()
+        loop.set_exception_handler(lambda lp, ctx: seen.append(type(ctx.get("exception")).__name__))
+        f = native.IOFuture()
+        coro = handler(f)
+
+        def on_done(drv, exc):
+            raise RuntimeError("on_done failed")
+        Driver(coro, on_done).start(coro.send(None))
+        f.resolve(1)  # must not raise into the protocol callback that resolves it
+    run(go())
+    assert seen == ["RuntimeError"]
