@@ -25,7 +25,8 @@ def test_native_runtime_is_in_tree_and_loaded():
     assert ops.native.ABI_VERSION == 1
     # every hot-path entry point is native
     for name in ("MessageCodec", "Ingest", "Delivery", "Settler", "Histogram", "format_line", "encode_query",
-                 "AmqpDemux", "H1Parser", "PgReader", "Driver", "dispatch_batch", "pg_bind"):
+                 "AmqpDemux", "H1Parser", "PgReader", "Driver", "IOFuture", "AckBatcher", "Buckets",
+                 "dispatch_batch", "pg_bind"):
         assert hasattr(ops.native, name), name
 
 
