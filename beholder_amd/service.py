@@ -499,9 +499,6 @@ class Service:
         if self.serializer is not None:  # per-media ordering (opt-in)
             out["ordering"] = {"active_keys": self.serializer.active_keys,
                                "serialized": self.serializer.serialized, "max_chain": self.serializer.max_chain}
-        if self.serializer is not None:  # per-media ordering (opt-in)
-            out["ordering"] = {"active_keys": self.serializer.active_keys,
-                               "serialized": self.serializer.serialized, "max_chain": self.serializer.max_chain}
         http_stats = getattr(self._http, "stats", None)
         if callable(http_stats):  # keep-alive pool accounting (sinks/h1.py)
             out["http"] = http_stats()

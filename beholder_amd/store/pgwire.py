@@ -115,10 +115,11 @@ def encode_param(v: Any) -> Optional[bytes]:
 class _Scram:
     """SCRAM-SHA-256 client (RFC 5802 / RFC 7677), no channel binding."""
 
-    def __init__(self, user: str, password: str):
+    def __init__(self, user: str, password: str, nonce: Optional[str] = None, send_user: bool = False):
         self.password = password
-        self.nonce = base64.b64encode(os.urandom(18)).decode()
-        self.first_bare = f"n=,r={self.nonce}"  # Postgres ignores the SCRAM user name
+        self.nonce = nonce or base64.b64encode(os.urandom(18)).decode()
+        # Postgres ignores the SCRAM user name (the startup message carries it); RFC 7677 sends it
+        self.first_bare = f"n={user if send_user else ''},r={self.nonce}"
         self.server_sig = b""
 
     def client_first(self) -> bytes:
@@ -328,6 +329,8 @@ class PgConnection(asyncio.Protocol):
                     scram = _Scram(p["user"], pw)
                     first = scram.client_first()
                     self._send(b"p", b"SCRAM-SHA-256\x00" + struct.pack("!i", len(first)) + first)
+                elif code in (11, 12) and scram is None:
+                    raise PgProtocolError(f"SASL message {code} before SASL negotiation")
                 elif code == 11:
                     self._send(b"p", scram.client_final(body[4:]))
                 elif code == 12:
