@@ -66,6 +66,8 @@ SERVICE_DEFAULTS: dict = {
         "gc_freeze": True,
         # per-message trace span at debug level (needs log.level: debug)
         "trace": False,
+        # handlers compiled to native state machines (ops/csrc/py_handlers.cpp); false = handlers.py
+        "native_handlers": True,
     }
 }
 

@@ -211,23 +211,32 @@ class TelemetryHandlers:
                 await self.trello.make_request("put", f"/1/cards/{js_str(media.creatorId)}",
                                                {"idList": list_pointer, "pos": 2})
             else:  # Q5
-                log.warn("unable to find list for status", status, f"({js_str(status_text)})",
-                         f"avail ([{','.join(str(k) for k in lists.keys())}])")
+                self._warn_missing_list(status, status_text)
 
         try:  # index.js:92-122 (Q3, Q4)
             if media.status == self.deployed:
-                tg_on, chat_id, tg_token, emby_on, emby_host, emby_key = self._hooks_plan()
-                if tg_on:
-                    log.info(f"informing telegram that media '{js_str(media_id)}' is available")
-                    await self.telegram.send_message(chat_id, deployed_text(media.name, media.metadataId),
-                                                     "markdown", token=tg_token())
-                if emby_on:
-                    log.info(f"telling emby to refresh at {js_str(emby_host)}")
-                    await self.emby.refresh_library(host=emby_host, api_key=emby_key)
+                await self._deployed_hooks(media, media_id)
         except Exception as err:  # noqa: BLE001 — reference catches everything here
             log.warn("failed to run deployed hooks:", err_message(err))
 
         return rmsg.ack()  # index.js:124
+
+    def _warn_missing_list(self, status: Any, status_text: Optional[str]) -> None:
+        """index.js:88 (Q5)."""
+        self.log.warn("unable to find list for status", status, f"({js_str(status_text)})",
+                      f"avail ([{','.join(str(k) for k in self.lists.keys())}])")
+
+    async def _deployed_hooks(self, media, media_id: Any) -> None:
+        """Body of the DEPLOYED branch, index.js:95-118 (the caller holds the try of index.js:92)."""
+        log = self.log
+        tg_on, chat_id, tg_token, emby_on, emby_host, emby_key = self._hooks_plan()
+        if tg_on:
+            log.info(f"informing telegram that media '{js_str(media_id)}' is available")
+            await self.telegram.send_message(chat_id, deployed_text(media.name, media.metadataId),
+                                             "markdown", token=tg_token())
+        if emby_on:
+            log.info(f"telling emby to refresh at {js_str(emby_host)}")
+            await self.emby.refresh_library(host=emby_host, api_key=emby_key)
 
     # ----------------------------------------------------------------- C11 ---
     async def on_progress(self, rmsg) -> Any:
@@ -264,6 +273,21 @@ class TelemetryHandlers:
             return rmsg.ack()
 
         return rmsg.ack()  # index.js:154
+
+
+def native_handlers(handlers: TelemetryHandlers):
+    """The compiled handlers (``ops/csrc/py_handlers.cpp``) bound to ``handlers``, or None.
+
+    They run index.js:62-155 as native state machines with the same dependencies
+    (logger, decoders, store, sinks, counters), so behaviour is identical to the
+    methods above; ``tests/test_handlers.py`` runs every case against both, and
+    ``tests/test_native_handlers.py`` fuzzes them against each other. A subclass
+    that overrides a handler method keeps the Python path.
+    """
+    if type(handlers) is not TelemetryHandlers:
+        return None
+    from .ops import native
+    return native.NativeHandlers(handlers)
 
 
 def _decoder(ptype) -> Callable:

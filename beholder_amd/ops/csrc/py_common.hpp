@@ -97,5 +97,6 @@ int init_http_types(PyObject* m);
 int init_pg_types(PyObject* m);
 int init_driver_types(PyObject* m);
 int init_ack_types(PyObject* m);
+int init_handler_types(PyObject* m);
 
 }  // namespace beholder

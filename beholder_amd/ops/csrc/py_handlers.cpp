@@ -1,0 +1,979 @@
+// NativeHandlers: the reference's two queue handlers (index.js:62-125 status,
+// index.js:127-155 progress) as native state machines.
+//
+// `NativeHandlers(handlers)` binds to a beholder_amd.handlers.TelemetryHandlers
+// and uses the same dependencies: its logger, decoders, enum tables, counters,
+// config lists, store and sink clients. `on_status(rmsg)` / `on_progress(rmsg)`
+// return a HandlerCall. It is an awaitable iterator (am_send, send, throw, close)
+// that dispatch_batch, the Driver and `await` all drive like the coroutine of
+// the Python method. Every step runs in C, up to the first await that really
+// suspends. An await on the store or a sink delegates to the Python awaitable
+// (`yield from` semantics). A store or sink that completes synchronously (the
+// in-memory store, buffered sinks) never leaves C.
+//
+// Branch and quirk mapping is the Python method's, line for line:
+//   status:   decode (errors escape: Q1) -> log -> updateStatus -> NO_TRELLO ack (Q2)
+//             -> enumToString -> getByID -> Trello move / missing-list warn (Q5, Q6)
+//             -> try { DEPLOYED hooks (Q3, Q4; TelemetryHandlers._deployed_hooks) } -> ack
+//   progress: try { decode -> log -> enumToString + counter (Q6) -> getByID ->
+//             comment (Q8) } catch -> warn -> ack (Q7)
+// The rare branches (missing-list warning, DEPLOYED hooks) call the Python helpers that the
+// Python method calls too, so their text and ordering come from one place.
+#include <string>
+
+#include "py_common.hpp"
+
+namespace beholder {
+
+bool text_js_str_append(std::string& out, PyObject* v);
+bool is_native_logger(PyObject* logger);
+bool logcore_emit(PyObject* logger, bool native, long lvl, PyObject* const* args, Py_ssize_t nargs);
+
+namespace {
+
+// interned attribute / literal strings
+PyObject *s_ack, *s_message, *s_content, *s_mediaId, *s_status, *s_progress, *s_host, *s_creator, *s_creatorId,
+    *s_get_nowait, *s_update_nowait, *s_store, *s_get_by_id, *s_update_status, *s_trello, *s_make_request, *s_post,
+    *s_put, *s_text, *s_idList, *s_pos, *s_deployed_hooks, *s_warn_missing_list, *s_child_for, *s_inc, *s_lower,
+    *s_throw, *s_close, *s_lists, *s_no_trello, *s_deployed, *s_trello_creator, *s_log, *s_decode_status,
+    *s_decode_progress, *s_status_names_s, *s_status_names_p, *s_progress_counter, *s_comment_inc;
+// log message literals (index.js:51,133,150)
+PyObject *m_progress, *m_status_kw, *m_percent, *m_creating, *m_with_text, *m_failed_progress, *m_failed_hooks;
+
+struct HandlersObject {
+  PyObject_HEAD PyObject* h;  // the TelemetryHandlers
+  PyObject* hdict;            // h.__dict__ (store / sinks are read per call: swappable)
+  PyObject* log;
+  PyObject* decode_s;
+  PyObject* decode_p;
+  PyObject* names_s;        // dict: status number -> enum name (index.js:74)
+  PyObject* names_p;        // (index.js:134)
+  PyObject* progress_plan;  // dict: status -> (statusText, counter child inc)
+  PyObject* progress_counter;
+  PyObject* comment_inc;
+  PyObject* deployed;
+  PyObject* trello_creator;
+  PyObject* lists;
+  PyObject* get_fn;         // handlers._get (JS property read on config nodes)
+  PyObject* err_message;    // handlers.err_message
+  PyObject* js_type_error;  // handlers.JsTypeError
+  PyObject* fallback;       // COMMENT_FALLBACK (index.js:54)
+  PyObject* one;            // TRELLO_CREATOR (index.js:79)
+  PyObject* two;            // pos: 2 (index.js:85)
+  uint64_t completed_sync;
+  uint64_t suspended;
+  uint8_t no_trello;
+  uint8_t native_log;
+};
+
+enum : uint8_t { K_STATUS = 0, K_PROGRESS = 1 };
+
+struct CallObject {
+  PyObject_HEAD HandlersObject* hs;
+  PyObject* rmsg;
+  PyObject* sub;  // awaitable iterator currently delegated to
+  PyObject* media_id;
+  PyObject* status;
+  PyObject* status_text;  // NULL = undefined
+  PyObject* progress;
+  PyObject* host;
+  PyObject* media;
+  uint8_t kind;
+  uint8_t state;
+  uint8_t started;
+  uint8_t done;
+  uint8_t did_suspend;
+};
+
+PyTypeObject HandlersType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+PyTypeObject CallType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+// ---------------------------------------------------------------- helpers ---
+bool js_truthy(PyObject* v, int* out) {
+  if (v == Py_None || v == Py_False) {
+    *out = 0;
+  } else if (v == Py_True) {
+    *out = 1;
+  } else if (PyUnicode_Check(v)) {
+    *out = PyUnicode_GET_LENGTH(v) != 0;
+  } else if (PyLong_Check(v)) {
+    *out = Py_SIZE(v) != 0;
+  } else if (PyFloat_Check(v)) {
+    double d = PyFloat_AS_DOUBLE(v);
+    *out = d == d && d != 0.0;
+  } else {
+    *out = 1;  // objects / arrays, even empty ones
+  }
+  return true;
+}
+
+PyObject* unicode_from(const std::string& s) { return PyUnicode_DecodeUTF8(s.data(), Py_ssize_t(s.size()), "strict"); }
+
+bool log_line(HandlersObject* hs, long lvl, PyObject* const* args, Py_ssize_t n) {
+  return logcore_emit(hs->log, hs->native_log != 0, lvl, args, n);
+}
+
+// rmsg.message.content
+PyObject* content_of(PyObject* rmsg) {
+  if (Py_TYPE(rmsg) == &DeliveryType) {
+    PyObject* c = reinterpret_cast<DeliveryObject*>(rmsg)->content;
+    Py_INCREF(c);
+    return c;
+  }
+  PyObject* m = PyObject_GetAttr(rmsg, s_message);
+  if (!m) return nullptr;
+  PyObject* c = PyObject_GetAttr(m, s_content);
+  Py_DECREF(m);
+  return c;
+}
+
+// instance attribute of the handlers object (store / sinks / sync accessors), borrowed
+PyObject* hattr(HandlersObject* hs, PyObject* name) {
+  PyObject* v = PyDict_GetItemWithError(hs->hdict, name);
+  if (!v && !PyErr_Occurred()) PyErr_Format(PyExc_AttributeError, "handlers have no attribute %U", name);
+  return v;
+}
+
+// Starts awaiting `aw` (reference stolen). 1 = finished synchronously (*out = result),
+// 0 = suspended (*out = the yielded future, c->sub set), -1 = raised.
+int await_start(CallObject* c, PyObject* aw, PyObject** out) {
+  PyObject* it;
+  if (PyCoro_CheckExact(aw)) {
+    it = aw;
+  } else {
+    unaryfunc getter = Py_TYPE(aw)->tp_as_async ? Py_TYPE(aw)->tp_as_async->am_await : nullptr;
+    if (!getter) {
+      PyErr_Format(PyExc_TypeError, "object %.100s can't be used in 'await' expression", Py_TYPE(aw)->tp_name);
+      Py_DECREF(aw);
+      return -1;
+    }
+    it = getter(aw);
+    Py_DECREF(aw);
+    if (!it) return -1;
+  }
+  PyObject* y = nullptr;
+  PySendResult r = PyIter_Send(it, Py_None, &y);
+  if (r == PYGEN_RETURN) {
+    Py_DECREF(it);
+    *out = y;
+    return 1;
+  }
+  if (r == PYGEN_ERROR) {
+    Py_DECREF(it);
+    return -1;
+  }
+  c->sub = it;
+  c->did_suspend = 1;
+  *out = y;
+  return 0;
+}
+
+// `except Exception as err: log.warn(text, err_message(err))`. Returns false when the
+// pending exception is not an Exception (CancelledError, KeyboardInterrupt) or logging failed.
+bool catch_and_warn(HandlersObject* hs, PyObject* text) {
+  if (!PyErr_ExceptionMatches(PyExc_Exception)) return false;
+  PyObject *et, *ev, *tb;
+  PyErr_Fetch(&et, &ev, &tb);
+  PyErr_NormalizeException(&et, &ev, &tb);
+  Py_XDECREF(tb);
+  Py_XDECREF(et);
+  if (ev) PyException_SetTraceback(ev, Py_None);  // drop frames (and the delivery they hold)
+  PyObject* msg = PyObject_CallOneArg(hs->err_message, ev ? ev : Py_None);
+  Py_XDECREF(ev);
+  if (!msg) return false;
+  PyObject* args[2] = {text, msg};
+  bool ok = log_line(hs, 40, args, 2);
+  Py_DECREF(msg);
+  return ok;
+}
+
+PySendResult finish_ack(CallObject* c, PyObject** result) {
+  c->done = 1;
+  PyObject* r = PyObject_CallMethodNoArgs(c->rmsg, s_ack);
+  if (!r) return PYGEN_ERROR;
+  *result = r;
+  return PYGEN_RETURN;
+}
+
+PySendResult fail(CallObject* c) {
+  c->done = 1;
+  return PYGEN_ERROR;
+}
+
+bool raise_to_lower_case(HandlersObject* hs) {
+  PyErr_SetString(hs->js_type_error, "Cannot read property 'toLowerCase' of undefined");
+  return false;
+}
+
+// media = await db.getByID(mediaId): nowait accessor when the store has one
+int get_media(CallObject* c, PyObject** out) {
+  HandlersObject* hs = c->hs;
+  PyObject* get = hattr(hs, s_get_nowait);
+  if (!get) return -1;
+  if (get != Py_None) {
+    PyObject* m = PyObject_CallOneArg(get, c->media_id);
+    if (!m) return -1;
+    *out = m;
+    return 1;
+  }
+  PyObject* store = hattr(hs, s_store);
+  if (!store) return -1;
+  PyObject* aw = PyObject_CallMethodOneArg(store, s_get_by_id, c->media_id);
+  if (!aw) return -1;
+  return await_start(c, aw, out);
+}
+
+// await trello.makeRequest(method, path, options)
+int trello_request(CallObject* c, PyObject* method, PyObject* path, PyObject* options, PyObject** out) {
+  PyObject* trello = hattr(c->hs, s_trello);
+  if (!trello) return -1;
+  PyObject* args[4] = {trello, method, path, options};
+  PyObject* aw = PyObject_VectorcallMethod(s_make_request, args, 4, nullptr);
+  if (!aw) return -1;
+  return await_start(c, aw, out);
+}
+
+// ------------------------------------------------------ progress handler ---
+// index.js:127-155. state: 0 start, 1 after getByID, 2 after the Trello comment.
+PySendResult step_progress(CallObject* c, PyObject* value, PyObject** result) {
+  HandlersObject* hs = c->hs;
+  int k;
+  PyObject* v = nullptr;
+  switch (c->state) {
+    case 0: {
+      PyObject* content = content_of(c->rmsg);
+      if (!content) goto catch_;
+      PyObject* msg = PyObject_CallOneArg(hs->decode_p, content);  // index.js:129
+      Py_DECREF(content);
+      if (!msg) goto catch_;
+      c->media_id = PyObject_GetAttr(msg, s_mediaId);
+      c->status = c->media_id ? PyObject_GetAttr(msg, s_status) : nullptr;
+      c->progress = c->status ? PyObject_GetAttr(msg, s_progress) : nullptr;
+      c->host = c->progress ? PyObject_GetAttr(msg, s_host) : nullptr;
+      Py_DECREF(msg);
+      if (!c->host) goto catch_;
+      {  // index.js:133
+        PyObject* args[6] = {m_progress, c->media_id, m_status_kw, c->status, m_percent, c->progress};
+        if (!log_line(hs, 30, args, 6)) goto catch_;
+      }
+      PyObject* plan = PyDict_GetItemWithError(hs->progress_plan, c->status);
+      if (!plan) {
+        if (PyErr_Occurred()) goto catch_;
+        PyObject* text = PyDict_GetItemWithError(hs->names_p, c->status);  // index.js:134
+        if (!text) {
+          if (!PyErr_Occurred()) raise_to_lower_case(hs);  // Q6
+          goto catch_;
+        }
+        PyObject* lower = PyObject_CallMethodNoArgs(text, s_lower);
+        if (!lower) goto catch_;
+        PyObject* child = PyObject_CallMethodOneArg(hs->progress_counter, s_child_for, lower);
+        Py_DECREF(lower);
+        if (!child) goto catch_;
+        PyObject* inc = PyObject_GetAttr(child, s_inc);
+        Py_DECREF(child);
+        if (!inc) goto catch_;
+        plan = PyTuple_Pack(2, text, inc);
+        Py_DECREF(inc);
+        if (!plan) goto catch_;
+        int rc = PyDict_SetItem(hs->progress_plan, c->status, plan);
+        Py_DECREF(plan);  // the dict holds it
+        if (rc < 0) goto catch_;
+      }
+      c->status_text = PyTuple_GET_ITEM(plan, 0);
+      Py_INCREF(c->status_text);
+      PyObject* r = PyObject_CallNoArgs(PyTuple_GET_ITEM(plan, 1));  // index.js:136-138
+      if (!r) goto catch_;
+      Py_DECREF(r);
+      k = get_media(c, &v);  // index.js:140
+      if (k < 0) goto catch_;
+      if (k == 0) {
+        c->state = 1;
+        *result = v;
+        return PYGEN_NEXT;
+      }
+      c->media = v;
+      goto have_media;
+    }
+    case 1:
+      if (!value) goto catch_;
+      c->media = value;
+    have_media: {
+      PyObject* creator = PyObject_GetAttr(c->media, s_creator);
+      if (!creator) goto catch_;
+      int is_trello = PyObject_RichCompareBool(creator, hs->trello_creator, Py_EQ);  // index.js:142
+      Py_DECREF(creator);
+      if (is_trello < 0) goto catch_;
+      if (!is_trello) goto finish;
+      std::string s;  // index.js:143-146 (Q8)
+      if (!text_js_str_append(s, c->status_text)) goto catch_;
+      s += ": Progress **";
+      if (!text_js_str_append(s, c->progress)) goto catch_;
+      s += "%**";
+      int has_host;
+      js_truthy(c->host, &has_host);
+      if (has_host) {
+        s += " (_";
+        if (!text_js_str_append(s, c->host)) goto catch_;
+        s += "_)";
+      }
+      PyObject* text = unicode_from(s);
+      if (!text) goto catch_;
+      PyObject* card = PyObject_GetAttr(c->media, s_creatorId);
+      if (!card) {
+        Py_DECREF(text);
+        goto catch_;
+      }
+      // comment(cardId, text), index.js:50-58
+      PyObject* largs[4] = {m_creating, card, m_with_text, text};
+      bool ok = log_line(hs, 30, largs, 4);
+      std::string path = "/1/cards/";
+      ok = ok && text_js_str_append(path, card);
+      Py_DECREF(card);
+      if (!ok) {
+        Py_DECREF(text);
+        goto catch_;
+      }
+      path += "/actions/comments";
+      PyObject* pathobj = unicode_from(path);
+      int truthy;
+      js_truthy(text, &truthy);
+      PyObject* options = pathobj ? PyDict_New() : nullptr;
+      if (!options || PyDict_SetItem(options, s_text, truthy ? text : hs->fallback) < 0) {
+        Py_XDECREF(options);
+        Py_XDECREF(pathobj);
+        Py_DECREF(text);
+        goto catch_;
+      }
+      Py_DECREF(text);
+      k = trello_request(c, s_post, pathobj, options, &v);  // index.js:53-55
+      Py_DECREF(pathobj);
+      Py_DECREF(options);
+      if (k < 0) goto catch_;
+      if (k == 0) {
+        c->state = 2;
+        *result = v;
+        return PYGEN_NEXT;
+      }
+      Py_DECREF(v);
+      goto commented;
+    }
+    case 2:
+      if (!value) goto catch_;
+      Py_DECREF(value);
+    commented: {
+      PyObject* r = PyObject_CallNoArgs(hs->comment_inc);  // index.js:57
+      if (!r) goto catch_;
+      Py_DECREF(r);
+      goto finish;
+    }
+    default:
+      PyErr_SetString(PyExc_RuntimeError, "HandlerCall: bad state");
+      return fail(c);
+  }
+catch_:  // index.js:149-151 (Q7)
+  if (!catch_and_warn(hs, m_failed_progress)) return fail(c);
+finish:
+  return finish_ack(c, result);  // index.js:151 / 154
+}
+
+// -------------------------------------------------------- status handler ---
+// index.js:62-125. Errors outside the hooks try escape (Q1).
+// state: 0 start, 1 after updateStatus, 2 after getByID, 3 after the card move, 4 after hooks.
+PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
+  HandlersObject* hs = c->hs;
+  int k;
+  PyObject* v = nullptr;
+  switch (c->state) {
+    case 0: {
+      PyObject* content = content_of(c->rmsg);
+      if (!content) return fail(c);
+      PyObject* msg = PyObject_CallOneArg(hs->decode_s, content);  // index.js:63
+      Py_DECREF(content);
+      if (!msg) return fail(c);
+      c->media_id = PyObject_GetAttr(msg, s_mediaId);
+      c->status = c->media_id ? PyObject_GetAttr(msg, s_status) : nullptr;
+      Py_DECREF(msg);
+      if (!c->status) return fail(c);
+      std::string s = "processing status update for media ";  // index.js:66
+      if (!text_js_str_append(s, c->media_id)) return fail(c);
+      s += ", status: ";
+      if (!text_js_str_append(s, c->status)) return fail(c);
+      PyObject* line = unicode_from(s);
+      if (!line) return fail(c);
+      bool ok = log_line(hs, 30, &line, 1);
+      Py_DECREF(line);
+      if (!ok) return fail(c);
+      PyObject* upd = hattr(hs, s_update_nowait);  // index.js:68
+      if (!upd) return fail(c);
+      if (upd != Py_None) {
+        PyObject* args[2] = {c->media_id, c->status};
+        PyObject* r = PyObject_Vectorcall(upd, args, 2, nullptr);
+        if (!r) return fail(c);
+        Py_DECREF(r);
+        goto updated;
+      }
+      PyObject* store = hattr(hs, s_store);
+      if (!store) return fail(c);
+      PyObject* args[3] = {store, c->media_id, c->status};
+      PyObject* aw = PyObject_VectorcallMethod(s_update_status, args, 3, nullptr);
+      if (!aw) return fail(c);
+      k = await_start(c, aw, &v);
+      if (k < 0) return fail(c);
+      if (k == 0) {
+        c->state = 1;
+        *result = v;
+        return PYGEN_NEXT;
+      }
+      Py_DECREF(v);
+      goto updated;
+    }
+    case 1:
+      if (!value) return fail(c);
+      Py_DECREF(value);
+    updated: {
+      if (hs->no_trello) return finish_ack(c, result);  // index.js:70-72 (Q2)
+      PyObject* text = PyDict_GetItemWithError(hs->names_s, c->status);  // index.js:74
+      if (!text && PyErr_Occurred()) return fail(c);
+      Py_XINCREF(text);
+      c->status_text = text;
+      k = get_media(c, &v);  // index.js:76
+      if (k < 0) return fail(c);
+      if (k == 0) {
+        c->state = 2;
+        *result = v;
+        return PYGEN_NEXT;
+      }
+      c->media = v;
+      goto have_media;
+    }
+    case 2:
+      if (!value) return fail(c);
+      c->media = value;
+    have_media: {  // TRELLO Movement, index.js:78-90
+      PyObject* creator = PyObject_GetAttr(c->media, s_creator);
+      if (!creator) return fail(c);
+      int is_trello = PyObject_RichCompareBool(creator, hs->one, Py_EQ);  // index.js:79
+      Py_DECREF(creator);
+      if (is_trello < 0) return fail(c);
+      if (!is_trello) goto hooks;
+      if (!c->status_text) {  // `statusText.toLowerCase()` on undefined (Q6)
+        raise_to_lower_case(hs);
+        return fail(c);
+      }
+      PyObject* lower = PyObject_CallMethodNoArgs(c->status_text, s_lower);
+      if (!lower) return fail(c);
+      PyObject* lp;  // index.js:80
+      if (PyDict_CheckExact(hs->lists)) {
+        lp = PyDict_GetItemWithError(hs->lists, lower);
+        if (!lp && PyErr_Occurred()) {
+          Py_DECREF(lower);
+          return fail(c);
+        }
+        lp = lp ? lp : Py_None;
+        Py_INCREF(lp);
+      } else {
+        lp = PyObject_CallFunctionObjArgs(hs->get_fn, hs->lists, lower, nullptr);
+      }
+      Py_DECREF(lower);
+      if (!lp) return fail(c);
+      int truthy;
+      js_truthy(lp, &truthy);
+      if (!truthy) {  // Q5
+        Py_DECREF(lp);
+        PyObject* text = c->status_text;
+        PyObject* r = PyObject_CallMethodObjArgs(hs->h, s_warn_missing_list, c->status, text, nullptr);
+        if (!r) return fail(c);
+        Py_DECREF(r);
+        goto hooks;
+      }
+      PyObject* card = PyObject_GetAttr(c->media, s_creatorId);
+      if (!card) {
+        Py_DECREF(lp);
+        return fail(c);
+      }
+      std::string s = "moving media card ";  // index.js:82
+      bool ok = text_js_str_append(s, c->media_id);
+      s += " (card id ";
+      ok = ok && text_js_str_append(s, card);
+      s += ")";
+      std::string path = "/1/cards/";
+      ok = ok && text_js_str_append(path, card);
+      Py_DECREF(card);
+      PyObject* line = ok ? unicode_from(s) : nullptr;
+      ok = line && log_line(hs, 30, &line, 1);
+      Py_XDECREF(line);
+      PyObject* pathobj = ok ? unicode_from(path) : nullptr;
+      PyObject* options = pathobj ? PyDict_New() : nullptr;
+      if (!options || PyDict_SetItem(options, s_idList, lp) < 0 || PyDict_SetItem(options, s_pos, hs->two) < 0) {
+        Py_XDECREF(options);
+        Py_XDECREF(pathobj);
+        Py_DECREF(lp);
+        return fail(c);
+      }
+      Py_DECREF(lp);
+      k = trello_request(c, s_put, pathobj, options, &v);  // index.js:83-86
+      Py_DECREF(pathobj);
+      Py_DECREF(options);
+      if (k < 0) return fail(c);
+      if (k == 0) {
+        c->state = 3;
+        *result = v;
+        return PYGEN_NEXT;
+      }
+      Py_DECREF(v);
+      goto hooks;
+    }
+    case 3:
+      if (!value) return fail(c);
+      Py_DECREF(value);
+    hooks: {  // try { ... } catch, index.js:92-122
+      PyObject* ms = PyObject_GetAttr(c->media, s_status);
+      if (!ms) goto hooks_catch;
+      int deployed = PyObject_RichCompareBool(ms, hs->deployed, Py_EQ);  // index.js:94 (Q3)
+      Py_DECREF(ms);
+      if (deployed < 0) goto hooks_catch;
+      if (!deployed) return finish_ack(c, result);
+      PyObject* aw = PyObject_CallMethodObjArgs(hs->h, s_deployed_hooks, c->media, c->media_id, nullptr);
+      if (!aw) goto hooks_catch;
+      k = await_start(c, aw, &v);
+      if (k < 0) goto hooks_catch;
+      if (k == 0) {
+        c->state = 4;
+        *result = v;
+        return PYGEN_NEXT;
+      }
+      Py_DECREF(v);
+      return finish_ack(c, result);
+    }
+    case 4:
+      if (!value) goto hooks_catch;
+      Py_DECREF(value);
+      return finish_ack(c, result);  // index.js:124
+    default:
+      PyErr_SetString(PyExc_RuntimeError, "HandlerCall: bad state");
+      return fail(c);
+  }
+hooks_catch:  // index.js:120-122 (Q4)
+  if (!catch_and_warn(hs, m_failed_hooks)) return fail(c);
+  return finish_ack(c, result);
+}
+
+PySendResult step(CallObject* c, PyObject* value, PyObject** result) {
+  PySendResult r = c->kind == K_STATUS ? step_status(c, value, result) : step_progress(c, value, result);
+  if (r != PYGEN_NEXT) {
+    c->done = 1;
+    if (c->did_suspend)
+      c->hs->suspended++;
+    else
+      c->hs->completed_sync++;
+  }
+  return r;
+}
+
+// ------------------------------------------------------ HandlerCall type ---
+PySendResult call_am_send(CallObject* c, PyObject* arg, PyObject** result) {
+  if (c->done) {
+    PyErr_SetString(PyExc_RuntimeError, "cannot reuse already awaited handler call");
+    return PYGEN_ERROR;
+  }
+  if (!c->started) {
+    if (arg != Py_None) {
+      PyErr_SetString(PyExc_TypeError, "can't send non-None value to a just-started handler call");
+      return PYGEN_ERROR;
+    }
+    c->started = 1;
+    return step(c, nullptr, result);
+  }
+  if (!c->sub) {
+    PyErr_SetString(PyExc_RuntimeError, "handler call is not suspended");
+    return PYGEN_ERROR;
+  }
+  PyObject* y = nullptr;
+  PySendResult r = PyIter_Send(c->sub, arg, &y);
+  if (r == PYGEN_NEXT) {
+    *result = y;
+    return PYGEN_NEXT;
+  }
+  Py_CLEAR(c->sub);
+  return step(c, r == PYGEN_RETURN ? y : nullptr, result);
+}
+
+// Converts an am_send outcome to the iterator-protocol return (value or NULL + StopIteration).
+PyObject* as_iter_result(PySendResult r, PyObject* res) {
+  if (r == PYGEN_NEXT) return res;
+  if (r == PYGEN_RETURN) {
+    if (res != Py_None) _PyGen_SetStopIterationValue(res);
+    else PyErr_SetNone(PyExc_StopIteration);
+    Py_DECREF(res);
+  }
+  return nullptr;
+}
+
+PyObject* call_iternext(CallObject* c) {
+  PyObject* res = nullptr;
+  PySendResult r = call_am_send(c, Py_None, &res);
+  if (r == PYGEN_RETURN) {  // tp_iternext: plain NULL (no exception) means StopIteration(None)
+    if (res == Py_None) {
+      Py_DECREF(res);
+      return nullptr;
+    }
+  }
+  return as_iter_result(r, res);
+}
+
+PyObject* call_send(CallObject* c, PyObject* arg) {
+  PyObject* res = nullptr;
+  PySendResult r = call_am_send(c, arg, &res);
+  return as_iter_result(r, res);
+}
+
+// throw(exc) / throw(type, value=None, tb=None): raise at the current await
+PyObject* call_throw(CallObject* c, PyObject* const* a, Py_ssize_t n) {
+  if (n < 1 || n > 3) {
+    PyErr_SetString(PyExc_TypeError, "throw expected 1 to 3 arguments");
+    return nullptr;
+  }
+  PyObject* exc = a[0];
+  if (c->sub) {
+    PyObject* meth = PyObject_GetAttr(c->sub, s_throw);
+    PyObject* y = nullptr;
+    if (meth) {
+      y = PyObject_Vectorcall(meth, a, size_t(n), nullptr);
+      Py_DECREF(meth);
+      if (y) return y;  // the delegate handled it and is still suspended
+    } else {
+      PyErr_Clear();
+      if (PyExceptionInstance_Check(exc))
+        PyErr_SetObject(reinterpret_cast<PyObject*>(Py_TYPE(exc)), exc);
+      else
+        PyErr_SetObject(exc, n > 1 ? a[1] : nullptr);
+    }
+    Py_CLEAR(c->sub);
+    PyObject* value = nullptr;
+    if (PyErr_ExceptionMatches(PyExc_StopIteration)) {
+      if (_PyGen_FetchStopIterationValue(&value) < 0) value = nullptr;
+    }
+    PyObject* res = nullptr;
+    PySendResult r = step(c, value, &res);
+    return as_iter_result(r, res);
+  }
+  c->done = 1;  // not suspended in a delegate: the exception ends the call, like a fresh coroutine
+  if (PyExceptionInstance_Check(exc))
+    PyErr_SetObject(reinterpret_cast<PyObject*>(Py_TYPE(exc)), exc);
+  else
+    PyErr_SetObject(exc, n > 1 ? a[1] : nullptr);
+  return nullptr;
+}
+
+PyObject* call_close(CallObject* c, PyObject*) {
+  c->done = 1;
+  if (c->sub) {
+    PyObject* sub = c->sub;
+    c->sub = nullptr;
+    PyObject* r = PyObject_CallMethodNoArgs(sub, s_close);
+    Py_DECREF(sub);
+    if (!r) {
+      if (!PyErr_ExceptionMatches(PyExc_AttributeError)) return nullptr;
+      PyErr_Clear();
+    } else {
+      Py_DECREF(r);
+    }
+  }
+  Py_RETURN_NONE;
+}
+
+PyObject* call_await(CallObject* c) {
+  Py_INCREF(c);
+  return reinterpret_cast<PyObject*>(c);
+}
+
+int call_traverse(CallObject* c, visitproc visit, void* arg) {
+  Py_VISIT(c->hs);
+  Py_VISIT(c->rmsg);
+  Py_VISIT(c->sub);
+  Py_VISIT(c->media_id);
+  Py_VISIT(c->status);
+  Py_VISIT(c->status_text);
+  Py_VISIT(c->progress);
+  Py_VISIT(c->host);
+  Py_VISIT(c->media);
+  return 0;
+}
+
+int call_clear(CallObject* c) {
+  Py_CLEAR(c->hs);
+  Py_CLEAR(c->rmsg);
+  Py_CLEAR(c->sub);
+  Py_CLEAR(c->media_id);
+  Py_CLEAR(c->status);
+  Py_CLEAR(c->status_text);
+  Py_CLEAR(c->progress);
+  Py_CLEAR(c->host);
+  Py_CLEAR(c->media);
+  return 0;
+}
+
+void call_dealloc(CallObject* c) {
+  PyObject_GC_UnTrack(c);
+  call_clear(c);
+  Py_TYPE(c)->tp_free(reinterpret_cast<PyObject*>(c));
+}
+
+PyObject* call_get_state(CallObject* c, void*) { return PyLong_FromLong(c->state); }
+PyObject* call_get_done(CallObject* c, void*) { return PyBool_FromLong(c->done); }
+
+PyMethodDef call_methods[] = {
+    {"send", reinterpret_cast<PyCFunction>(call_send), METH_O, "send(value): resume at the current await"},
+    {"throw", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(call_throw)), METH_FASTCALL,
+     "throw(exc): raise at the current await"},
+    {"close", reinterpret_cast<PyCFunction>(call_close), METH_NOARGS, "close(): abandon the call"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyGetSetDef call_getset[] = {
+    {"state", reinterpret_cast<getter>(call_get_state), nullptr, "resume point (per-handler numbering)", nullptr},
+    {"done", reinterpret_cast<getter>(call_get_done), nullptr, "finished (returned or raised)", nullptr},
+    {nullptr, nullptr, nullptr, nullptr, nullptr}};
+
+PyAsyncMethods call_async = {reinterpret_cast<unaryfunc>(call_await), nullptr, nullptr,
+                             reinterpret_cast<sendfunc>(call_am_send)};
+
+PyObject* make_call(HandlersObject* hs, PyObject* rmsg, uint8_t kind) {
+  CallObject* c = PyObject_GC_New(CallObject, &CallType);
+  if (!c) return nullptr;
+  Py_INCREF(hs);
+  c->hs = hs;
+  Py_INCREF(rmsg);
+  c->rmsg = rmsg;
+  c->sub = c->media_id = c->status = c->status_text = c->progress = c->host = c->media = nullptr;
+  c->kind = kind;
+  c->state = 0;
+  c->started = c->done = c->did_suspend = 0;
+  PyObject_GC_Track(c);
+  return reinterpret_cast<PyObject*>(c);
+}
+
+// ---------------------------------------------------- NativeHandlers type ---
+PyObject* hs_on_status(HandlersObject* hs, PyObject* rmsg) { return make_call(hs, rmsg, K_STATUS); }
+PyObject* hs_on_progress(HandlersObject* hs, PyObject* rmsg) { return make_call(hs, rmsg, K_PROGRESS); }
+
+PyObject* hs_stats(HandlersObject* hs, PyObject*) {
+  return Py_BuildValue("{s:K,s:K,s:O}", "completed_sync", static_cast<unsigned long long>(hs->completed_sync),
+                       "suspended", static_cast<unsigned long long>(hs->suspended), "native_log",
+                       hs->native_log ? Py_True : Py_False);
+}
+
+int hs_traverse(HandlersObject* hs, visitproc visit, void* arg) {
+  Py_VISIT(hs->h);
+  Py_VISIT(hs->hdict);
+  Py_VISIT(hs->log);
+  Py_VISIT(hs->decode_s);
+  Py_VISIT(hs->decode_p);
+  Py_VISIT(hs->names_s);
+  Py_VISIT(hs->names_p);
+  Py_VISIT(hs->progress_plan);
+  Py_VISIT(hs->progress_counter);
+  Py_VISIT(hs->comment_inc);
+  Py_VISIT(hs->deployed);
+  Py_VISIT(hs->trello_creator);
+  Py_VISIT(hs->lists);
+  Py_VISIT(hs->get_fn);
+  Py_VISIT(hs->err_message);
+  Py_VISIT(hs->js_type_error);
+  Py_VISIT(hs->fallback);
+  return 0;
+}
+
+int hs_clear(HandlersObject* hs) {
+  Py_CLEAR(hs->h);
+  Py_CLEAR(hs->hdict);
+  Py_CLEAR(hs->log);
+  Py_CLEAR(hs->decode_s);
+  Py_CLEAR(hs->decode_p);
+  Py_CLEAR(hs->names_s);
+  Py_CLEAR(hs->names_p);
+  Py_CLEAR(hs->progress_plan);
+  Py_CLEAR(hs->progress_counter);
+  Py_CLEAR(hs->comment_inc);
+  Py_CLEAR(hs->deployed);
+  Py_CLEAR(hs->trello_creator);
+  Py_CLEAR(hs->lists);
+  Py_CLEAR(hs->get_fn);
+  Py_CLEAR(hs->err_message);
+  Py_CLEAR(hs->js_type_error);
+  Py_CLEAR(hs->fallback);
+  return 0;
+}
+
+void hs_dealloc(HandlersObject* hs) {
+  PyObject_GC_UnTrack(hs);
+  hs_clear(hs);
+  Py_XDECREF(hs->one);
+  Py_XDECREF(hs->two);
+  Py_TYPE(hs)->tp_free(reinterpret_cast<PyObject*>(hs));
+}
+
+PyObject* hs_new(PyTypeObject* type, PyObject*, PyObject*) {
+  HandlersObject* hs = reinterpret_cast<HandlersObject*>(type->tp_alloc(type, 0));
+  if (!hs) return nullptr;
+  hs->one = PyLong_FromLong(1);
+  hs->two = PyLong_FromLong(2);
+  return reinterpret_cast<PyObject*>(hs);
+}
+
+// fetch `name` from the module of the handlers' class (beholder_amd.handlers)
+PyObject* module_attr(PyObject* h, const char* name) {
+  PyObject* modname = PyObject_GetAttrString(reinterpret_cast<PyObject*>(Py_TYPE(h)), "__module__");
+  if (!modname) return nullptr;
+  PyObject* mod = PyImport_Import(modname);
+  Py_DECREF(modname);
+  if (!mod) return nullptr;
+  PyObject* v = PyObject_GetAttrString(mod, name);
+  Py_DECREF(mod);
+  return v;
+}
+
+// NativeHandlers(handlers)
+int hs_init(HandlersObject* hs, PyObject* args, PyObject* kwds) {
+  PyObject* h;
+  static const char* kwlist[] = {"handlers", nullptr};
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "O", const_cast<char**>(kwlist), &h)) return -1;
+  hs_clear(hs);
+  Py_INCREF(h);
+  hs->h = h;
+  hs->hdict = PyObject_GenericGetDict(h, nullptr);
+  if (!hs->hdict) return -1;
+  struct {
+    PyObject** slot;
+    PyObject* name;
+  } attrs[] = {{&hs->log, s_log},
+               {&hs->decode_s, s_decode_status},
+               {&hs->decode_p, s_decode_progress},
+               {&hs->names_s, s_status_names_s},
+               {&hs->names_p, s_status_names_p},
+               {&hs->progress_counter, s_progress_counter},
+               {&hs->comment_inc, s_comment_inc},
+               {&hs->deployed, s_deployed},
+               {&hs->trello_creator, s_trello_creator},
+               {&hs->lists, s_lists}};
+  for (auto& a : attrs) {
+    *a.slot = PyObject_GetAttr(h, a.name);
+    if (!*a.slot) return -1;
+  }
+  if (!PyDict_CheckExact(hs->names_s) || !PyDict_CheckExact(hs->names_p)) {
+    PyErr_SetString(PyExc_TypeError, "enum name tables must be dicts");
+    return -1;
+  }
+  PyObject* nt = PyObject_GetAttr(h, s_no_trello);
+  if (!nt) return -1;
+  int t = PyObject_IsTrue(nt);
+  Py_DECREF(nt);
+  if (t < 0) return -1;
+  hs->no_trello = uint8_t(t);
+  hs->native_log = is_native_logger(hs->log) ? 1 : 0;
+  hs->progress_plan = PyDict_New();
+  hs->get_fn = module_attr(h, "_get");
+  hs->err_message = hs->get_fn ? module_attr(h, "err_message") : nullptr;
+  hs->js_type_error = hs->err_message ? module_attr(h, "JsTypeError") : nullptr;
+  hs->fallback = hs->js_type_error ? module_attr(h, "COMMENT_FALLBACK") : nullptr;
+  if (!hs->progress_plan || !hs->fallback || !hs->one || !hs->two) return -1;
+  return 0;
+}
+
+PyMethodDef hs_methods[] = {
+    {"on_status", reinterpret_cast<PyCFunction>(hs_on_status), METH_O,
+     "on_status(rmsg) -> awaitable: the v1.telemetry.status handler (index.js:62-125)"},
+    {"on_progress", reinterpret_cast<PyCFunction>(hs_on_progress), METH_O,
+     "on_progress(rmsg) -> awaitable: the v1.telemetry.progress handler (index.js:127-155)"},
+    {"stats", reinterpret_cast<PyCFunction>(hs_stats), METH_NOARGS, "calls finished without / after suspending"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyObject* intern(const char* s) { return PyUnicode_InternFromString(s); }
+
+}  // namespace
+
+int init_handler_types(PyObject* m) {
+  struct {
+    PyObject** slot;
+    const char* text;
+  } strs[] = {{&s_ack, "ack"},
+              {&s_message, "message"},
+              {&s_content, "content"},
+              {&s_mediaId, "mediaId"},
+              {&s_status, "status"},
+              {&s_progress, "progress"},
+              {&s_host, "host"},
+              {&s_creator, "creator"},
+              {&s_creatorId, "creatorId"},
+              {&s_get_nowait, "_get_nowait"},
+              {&s_update_nowait, "_update_nowait"},
+              {&s_store, "_store"},
+              {&s_get_by_id, "get_by_id"},
+              {&s_update_status, "update_status"},
+              {&s_trello, "trello"},
+              {&s_make_request, "make_request"},
+              {&s_post, "post"},
+              {&s_put, "put"},
+              {&s_text, "text"},
+              {&s_idList, "idList"},
+              {&s_pos, "pos"},
+              {&s_deployed_hooks, "_deployed_hooks"},
+              {&s_warn_missing_list, "_warn_missing_list"},
+              {&s_child_for, "child_for"},
+              {&s_inc, "inc"},
+              {&s_lower, "lower"},
+              {&s_throw, "throw"},
+              {&s_close, "close"},
+              {&s_lists, "lists"},
+              {&s_no_trello, "no_trello"},
+              {&s_deployed, "deployed"},
+              {&s_trello_creator, "trello_creator"},
+              {&s_log, "log"},
+              {&s_decode_status, "decode_status"},
+              {&s_decode_progress, "decode_progress"},
+              {&s_status_names_s, "_status_names_s"},
+              {&s_status_names_p, "_status_names_p"},
+              {&s_progress_counter, "progress_counter"},
+              {&s_comment_inc, "_comment_inc"},
+              {&m_progress, "processing progress update on media"},
+              {&m_status_kw, "status"},
+              {&m_percent, "percent"},
+              {&m_creating, "creating comment on"},
+              {&m_with_text, "with text:"},
+              {&m_failed_progress, "failed to update media progress"},
+              {&m_failed_hooks, "failed to run deployed hooks:"}};
+  for (auto& s : strs)
+    if (!(*s.slot = intern(s.text))) return -1;
+
+  CallType.tp_name = "beholder_amd.ops._native.HandlerCall";
+  CallType.tp_basicsize = sizeof(CallObject);
+  CallType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC;
+  CallType.tp_doc = "one native handler invocation: an awaitable iterator (send / throw / close)";
+  CallType.tp_dealloc = reinterpret_cast<destructor>(call_dealloc);
+  CallType.tp_traverse = reinterpret_cast<traverseproc>(call_traverse);
+  CallType.tp_clear = reinterpret_cast<inquiry>(call_clear);
+  CallType.tp_as_async = &call_async;
+  CallType.tp_iter = PyObject_SelfIter;
+  CallType.tp_iternext = reinterpret_cast<iternextfunc>(call_iternext);
+  CallType.tp_methods = call_methods;
+  CallType.tp_getset = call_getset;
+  if (PyType_Ready(&CallType) < 0) return -1;
+
+  HandlersType.tp_name = "beholder_amd.ops._native.NativeHandlers";
+  HandlersType.tp_basicsize = sizeof(HandlersObject);
+  HandlersType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC;
+  HandlersType.tp_doc = "NativeHandlers(handlers): the status / progress handlers compiled to native state machines";
+  HandlersType.tp_new = hs_new;
+  HandlersType.tp_init = reinterpret_cast<initproc>(hs_init);
+  HandlersType.tp_dealloc = reinterpret_cast<destructor>(hs_dealloc);
+  HandlersType.tp_traverse = reinterpret_cast<traverseproc>(hs_traverse);
+  HandlersType.tp_clear = reinterpret_cast<inquiry>(hs_clear);
+  HandlersType.tp_methods = hs_methods;
+  if (PyType_Ready(&HandlersType) < 0) return -1;
+  Py_INCREF(&HandlersType);
+  if (PyModule_AddObject(m, "NativeHandlers", reinterpret_cast<PyObject*>(&HandlersType)) < 0) return -1;
+  Py_INCREF(&CallType);
+  if (PyModule_AddObject(m, "HandlerCall", reinterpret_cast<PyObject*>(&CallType)) < 0) return -1;
+  return 0;
+}
+
+}  // namespace beholder

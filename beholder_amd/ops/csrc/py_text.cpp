@@ -817,6 +817,41 @@ PyMethodDef text_methods[] = {
 
 }  // namespace
 
+// ---- used by the native handlers (py_handlers.cpp) ---------------------------
+bool text_js_str_append(std::string& out, PyObject* v) { return js_str_append(out, v); }
+
+bool is_native_logger(PyObject* logger) {
+  // the level methods must be LogCore's own (a subclass overriding them keeps its override)
+  if (!PyObject_TypeCheck(logger, &LogCoreType)) return false;
+  static PyObject* names[3] = {nullptr, nullptr, nullptr};
+  static const char* raw[3] = {"info", "warn", "error"};
+  for (int i = 0; i < 3; ++i) {
+    if (!names[i] && !(names[i] = PyUnicode_InternFromString(raw[i]))) {
+      PyErr_Clear();
+      return false;
+    }
+    PyObject* mine = _PyType_Lookup(Py_TYPE(logger), names[i]);
+    PyObject* base = _PyType_Lookup(&LogCoreType, names[i]);
+    if (!mine || mine != base) return false;
+  }
+  return true;
+}
+
+bool logcore_emit(PyObject* logger, bool native, long lvl, PyObject* const* args, Py_ssize_t nargs) {
+  PyObject* r;
+  if (native) {
+    r = core_log(reinterpret_cast<LogCoreObject*>(logger), lvl, args, nargs);
+  } else {
+    PyObject* meth = PyObject_GetAttrString(logger, level_name(lvl));
+    if (!meth) return false;
+    r = PyObject_Vectorcall(meth, args, size_t(nargs), nullptr);
+    Py_DECREF(meth);
+  }
+  if (!r) return false;
+  Py_DECREF(r);
+  return true;
+}
+
 int init_text_functions(PyObject* m) {
   LogSinkType.tp_name = "beholder_amd.ops._native.LogSink";
   LogSinkType.tp_basicsize = sizeof(LogSinkObject);

@@ -37,7 +37,7 @@ from typing import Any, Callable, Dict, List, Optional
 
 from . import topics as T
 from .config import Config
-from .handlers import TelemetryHandlers, err_message
+from .handlers import TelemetryHandlers, err_message, native_handlers
 from .metrics import MetricsServer, NativeHistogramView, Registry, default_metrics
 from .metrics.registry import Gauge
 from .parallel.ordering import KeyedSerializer
@@ -121,6 +121,7 @@ class Service:
         self._running = False
         self._initialized = False
         self.handlers: Optional[TelemetryHandlers] = None
+        self.handler_impl: Any = None  # handlers or their compiled form (ops.NativeHandlers)
         self.serializer: Optional[KeyedSerializer] = None
         self.started_at = 0.0
         self.received = array.array("Q", [0] * len(T.TOPIC_NAMES_BY_ID))
@@ -189,9 +190,13 @@ class Service:
             progress_counter=self.progress_updates_total, comments_counter=self.trello_comments_total,
             logger=self.log)
 
-        # 8. listeners (index.js:62,127)
-        self.listen(T.STATUS, self.handlers.on_status)
-        self.listen(T.PROGRESS, self.handlers.on_progress)
+        # 8. listeners (index.js:62,127): the compiled handlers unless disabled (same semantics)
+        impl = self.handlers
+        if svc.get("native_handlers", True) and os.environ.get("BEHOLDER_NATIVE_HANDLERS", "1") != "0":
+            impl = native_handlers(self.handlers) or self.handlers
+        self.handler_impl = impl
+        self.listen(T.STATUS, impl.on_status)
+        self.listen(T.PROGRESS, impl.on_progress)
         await self._source.start([t for t in T.TOPIC_IDS if self._routes[T.TOPIC_IDS[t]] is not None])
         if self.ordering == "per_media":
             self.serializer = KeyedSerializer(self._dispatch_now, self._media_key)

@@ -6,7 +6,7 @@ import copy
 from typing import Optional
 
 from beholder_amd.config import Config
-from beholder_amd.handlers import TelemetryHandlers
+from beholder_amd.handlers import TelemetryHandlers, native_handlers
 from beholder_amd.metrics import Registry
 from beholder_amd.models import proto
 from beholder_amd.ops import Delivery, Settler
@@ -51,6 +51,15 @@ def progress_msg(media_id: str, status, progress=0, host: str = "") -> bytes:
     return proto.encode(PROGRESS, {"mediaId": media_id, "status": s, "progress": progress, "host": host})
 
 
+# which handler implementation Rig drives: "python" (handlers.py) or "native" (py_handlers.cpp);
+# tests/test_handlers.py runs every case under both
+HANDLER_IMPL = "python"
+
+
+async def _await(aw):
+    return await aw
+
+
 class Rig:
     """Handlers wired to an in-memory store, a recording HTTP client and a captured log."""
 
@@ -75,6 +84,7 @@ class Rig:
             progress_counter=self.progress, comments_counter=self.comments, logger=self.log,
             no_trello=no_trello)
         self.settler = Settler()
+        self.impl = self.h if HANDLER_IMPL == "python" else native_handlers(self.h)
 
     def delivery(self, topic_id: int, body: bytes) -> Delivery:
         return Delivery(body, topic_id, 1, self.settler)
@@ -83,14 +93,14 @@ class Rig:
         d = self.delivery(STATUS_ID, body)
         exc = None
         try:
-            asyncio.run(self.h.on_status(d))
+            asyncio.run(_await(self.impl.on_status(d)))
         except Exception as e:  # noqa: BLE001
             exc = e
         return d, exc
 
     def progress_(self, body: bytes):
         d = self.delivery(PROGRESS_ID, body)
-        asyncio.run(self.h.on_progress(d))
+        asyncio.run(_await(self.impl.on_progress(d)))
         return d
 
     def calls(self):

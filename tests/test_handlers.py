@@ -4,6 +4,7 @@ Each test names the reference lines / quirk it pins.
 """
 import pytest
 
+import helpers
 from beholder_amd.handlers import JsTypeError, js_truthy
 from beholder_amd.sinks import HttpError
 from beholder_amd.store import MediaNotFound, MemoryStore
@@ -11,6 +12,13 @@ from beholder_amd.store import MediaNotFound, MemoryStore
 from helpers import ENUM, Rig, api_media, cfg, progress_msg, status_msg, trello_media
 
 TRELLO = "https://api.trello.com"
+
+
+@pytest.fixture(autouse=True, params=["python", "native"])
+def impl(request, monkeypatch):
+    """Every case runs against the Python handlers and the compiled ones (ops/csrc/py_handlers.cpp)."""
+    monkeypatch.setattr(helpers, "HANDLER_IMPL", request.param)
+    return request.param
 
 
 # ----------------------------------------------------------------- status ----

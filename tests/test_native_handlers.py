@@ -1,0 +1,261 @@
+"""Compiled handlers (ops/csrc/py_handlers.cpp) against the Python handlers (handlers.py).
+
+tests/test_handlers.py runs every branch test under both implementations. This file
+fuzzes them against each other. Random media tables, configs, event streams
+(including undecodable bytes and unknown enum values), sink faults and store failures
+go through the same rig twice, once per implementation. The two runs must produce
+the same observable trace:
+
+* every delivery's final state, and the exception a status handler raised (Q1);
+* log lines (level + text, in order);
+* HTTP requests (method + full URL, in order);
+* counter values and the store contents.
+
+Stores and sinks that really suspend exercise the native state machine's resume
+points. Concurrent runs (asyncio.gather) check that suspension interleaves identically.
+"""
+from __future__ import annotations
+
+import asyncio
+import gc
+
+import pytest
+from hypothesis import HealthCheck, given, settings, strategies as st
+
+import helpers
+from beholder_amd.handlers import native_handlers
+from beholder_amd.ops import native
+from beholder_amd.store import Media, MemoryStore
+from helpers import Rig, cfg, progress_msg, status_msg
+
+
+class SuspendingStore(MemoryStore):
+    """Every access awaits a real loop iteration (a network store's shape)."""
+
+    async def update_status(self, media_id, status):
+        await asyncio.sleep(0)
+        MemoryStore.update_status_nowait(self, media_id, status)
+
+    async def get_by_id(self, media_id):
+        await asyncio.sleep(0)
+        return MemoryStore.get_by_id_nowait(self, media_id)
+
+
+class FlakyStore(MemoryStore):
+    """Raises for ids starting with "x" (driver / connection errors)."""
+
+    async def update_status(self, media_id, status):
+        if str(media_id).startswith("x"):
+            raise ConnectionError(f"update failed for {media_id}")
+        MemoryStore.update_status_nowait(self, media_id, status)
+
+    async def get_by_id(self, media_id):
+        if str(media_id).startswith("x"):
+            raise ConnectionError(f"read failed for {media_id}")
+        return MemoryStore.get_by_id_nowait(self, media_id)
+
+
+STORES = {"memory": MemoryStore, "suspending": SuspendingStore, "flaky": FlakyStore}
+
+ids = st.sampled_from(["m0", "m1", "m2", "m3", "x1", "missing", ""])
+medias = st.lists(st.builds(
+    Media, id=st.sampled_from(["m0", "m1", "m2", "m3", "x1"]), name=st.sampled_from(["Cowboy Bebop", "Ü & ?", ""]),
+    creator=st.sampled_from([0, 1, 2]), creatorId=st.sampled_from(["card1", "c/2", "", "ü"]),
+    metadataId=st.sampled_from(["1", "42", ""]), status=st.integers(0, 6)), max_size=6)
+events = st.lists(st.one_of(
+    st.tuples(st.just("status"), ids, st.integers(-1, 7)),
+    st.tuples(st.just("progress"), ids, st.integers(-1, 7), st.integers(-5, 150),
+              st.sampled_from(["", "worker-1", "ünï", "a b&c"])),
+    st.tuples(st.sampled_from(["status", "progress"]), st.just("garbage"), st.binary(max_size=12)),
+), min_size=1, max_size=12)
+configs = st.fixed_dictionaries({
+    "instance": st.fixed_dictionaries({
+        "flow_ids": st.dictionaries(st.sampled_from(["queued", "downloading", "converting", "uploading", "deployed"]),
+                                    st.sampled_from(["L1", "L2", "", 0, 7]), max_size=5),
+        "telegram": st.fixed_dictionaries({"enabled": st.booleans(), "channel": st.sampled_from(["-1001", 5])}),
+        "emby": st.fixed_dictionaries({"enabled": st.booleans(), "host": st.just("http://emby:8096")}),
+    }),
+})
+faults = st.lists(st.tuples(st.sampled_from(["POST", "PUT", "GET"]),
+                            st.sampled_from(["https://api.trello.com", "https://api.telegram.org", "http://emby"]),
+                            st.sampled_from([None, 404, 500])), max_size=2)
+
+
+def _encode(ev):
+    if ev[1] == "garbage":
+        return ev[2]
+    if ev[0] == "status":
+        return status_msg(ev[1], ev[2])
+    return progress_msg(ev[1], ev[2], ev[3], ev[4])
+
+
+def run_trace(impl, config, no_trello, rows, evs, fault_list, store_kind, concurrent):
+    helpers.HANDLER_IMPL = impl
+    try:
+        r = Rig(config=config, medias=rows, no_trello=no_trello)
+    finally:
+        helpers.HANDLER_IMPL = "python"
+    r.h.store = STORES[store_kind](list(rows))
+    for method, prefix, status in fault_list:
+        r.http.fail(method, prefix, status=status)
+    if impl == "native":
+        r.impl = native_handlers(r.h)
+    deliveries = [(ev[0], r.delivery(1 if ev[0] == "status" else 2, _encode(ev))) for ev in evs]
+
+    async def one(kind, d):
+        call = r.impl.on_status(d) if kind == "status" else r.impl.on_progress(d)
+        try:
+            await call
+            return None
+        except Exception as e:  # noqa: BLE001
+            return f"{type(e).__name__}: {e}"
+
+    async def go():
+        if concurrent:
+            return await asyncio.gather(*(one(k, d) for k, d in deliveries))
+        return [await one(k, d) for k, d in deliveries]
+
+    errors = asyncio.run(go())
+    r.log.flush()
+    return {
+        "deliveries": [(d.state, e) for (_, d), e in zip(deliveries, errors)],
+        "logs": [(rec["level"], rec["msg"]) for rec in r.stream.records()],
+        "http": list(r.http.calls),
+        "progress": sorted(r.progress.values().items()),
+        "comments": r.comments.get(),
+        "store": sorted(r.h.store.snapshot().items()),
+    }
+
+
+@settings(max_examples=300, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(config=configs, no_trello=st.booleans(), rows=medias, evs=events, fault_list=faults,
+       store_kind=st.sampled_from(sorted(STORES)), concurrent=st.booleans())
+def test_native_matches_python(config, no_trello, rows, evs, fault_list, store_kind, concurrent):
+    c = cfg(config)
+    c.data["instance"]["flow_ids"] = config["instance"]["flow_ids"]  # replace, not merge, the list map
+    args = (c, no_trello, rows, evs, fault_list, store_kind, concurrent)
+    assert run_trace("native", *args) == run_trace("python", *args)
+
+
+def test_native_handlers_selected_by_service_and_switchable(monkeypatch):
+    from beholder_amd.bench.generator import Workload, bench_config
+    from beholder_amd.config import Config
+    from beholder_amd.service import Service
+    from beholder_amd.sinks import RecordingHttpClient
+    from beholder_amd.transport.ingest import BytesSource
+
+    w = Workload(n_media=32, seed=5)
+    data = w.framed(200)
+
+    def run(env_value):
+        monkeypatch.setenv("BEHOLDER_NATIVE_HANDLERS", env_value)
+        http = RecordingHttpClient()
+        svc = Service(Config.from_dict(bench_config()), source=BytesSource(data), store=MemoryStore(w.media),
+                      http=http, serve_metrics=False, logger=helpers.Logger(stream=helpers.MemoryStream()))
+
+        async def go():
+            await svc.init()
+            st_ = await svc.run()
+            await svc.close()
+            return st_
+        st_ = asyncio.run(go())
+        return svc, st_, list(http.calls)
+
+    svc_n, st_n, calls_n = run("1")
+    svc_p, st_p, calls_p = run("0")
+    assert isinstance(svc_n.handler_impl, native.NativeHandlers)
+    assert svc_p.handler_impl is svc_p.handlers
+    assert svc_n.handler_impl.stats()["completed_sync"] == 200
+    assert st_n["source"]["acked"] == st_p["source"]["acked"] == 200
+    assert calls_n == calls_p and st_n["progress_updates"] == st_p["progress_updates"]
+
+
+def test_native_call_protocol():
+    """HandlerCall behaves like the coroutine of the Python method: send / throw / close / await."""
+    r = Rig(medias=[helpers.trello_media("m1")])
+    r.h.store = SuspendingStore([helpers.trello_media("m1")])
+    nh = native_handlers(r.h)
+
+    d = r.delivery(2, progress_msg("m1", "QUEUED", 5))
+    call = nh.on_progress(d)
+    fut = call.send(None)  # suspends in the store read (asyncio.sleep(0) yields None)
+    assert fut is None and call.state == 1 and not call.done
+    with pytest.raises(StopIteration):
+        call.send(None)
+    assert call.done and d.acked
+    with pytest.raises(RuntimeError):
+        call.send(None)
+
+    # throw at the await: the progress handler catches Exception (Q7) and still acks
+    d = r.delivery(2, progress_msg("m1", "QUEUED", 5))
+    call = nh.on_progress(d)
+    call.send(None)
+    with pytest.raises(StopIteration):
+        call.throw(ValueError("boom"))
+    assert d.acked and r.msgs(40)[-1] == "failed to update media progress boom"
+
+    # a CancelledError is not an Exception: it propagates and the delivery stays pending
+    d = r.delivery(2, progress_msg("m1", "QUEUED", 5))
+    call = nh.on_progress(d)
+    call.send(None)
+    with pytest.raises(asyncio.CancelledError):
+        call.throw(asyncio.CancelledError())
+    assert d.state == "pending"
+
+    # status errors escape (Q1)
+    d = r.delivery(1, b"\xff")
+    call = nh.on_status(d)
+    with pytest.raises(Exception):
+        call.send(None)
+    assert d.state == "pending" and call.done
+
+    # close() abandons a suspended call
+    d = r.delivery(2, progress_msg("m1", "QUEUED", 5))
+    call = nh.on_progress(d)
+    call.send(None)
+    call.close()
+    assert call.done and d.state == "pending"
+
+
+def test_native_calls_do_not_leak():
+    r = Rig(medias=[helpers.trello_media("m1"), helpers.api_media("m2")])
+    nh = native_handlers(r.h)
+
+    async def go(n):
+        for i in range(n):
+            await nh.on_progress(r.delivery(2, progress_msg("m1" if i % 2 else "m2", "CONVERTING", i % 100, "w")))
+            await nh.on_status(r.delivery(1, status_msg("m2", "QUEUED")))
+
+    asyncio.run(go(200))  # warm caches (counter children, interned strings)
+    gc.collect()
+    before = len(gc.get_objects())
+    asyncio.run(go(2000))
+    gc.collect()
+    assert len(gc.get_objects()) - before < 200
+    assert not [o for o in gc.get_objects() if type(o).__name__ == "HandlerCall"]
+
+
+def test_subclass_keeps_python_path():
+    from beholder_amd.handlers import TelemetryHandlers
+
+    class Custom(TelemetryHandlers):
+        pass
+
+    r = Rig()
+    r.h.__class__ = Custom
+    assert native_handlers(r.h) is None
+
+
+@pytest.mark.skipif(not __import__("os").path.exists("/root/reference/index.js") or
+                    not __import__("shutil").which("node"), reason="needs the reference checkout and node")
+def test_reference_node_harness_runs_the_reference():
+    """scripts/bench_reference_node.py: the reference index.js under in-process stand-ins acks every event."""
+    import json
+    import subprocess
+    import sys
+    out = subprocess.run([sys.executable, "scripts/bench_reference_node.py", "--procs", "1", "--steps", "2",
+                          "--warmup", "1", "--events-per-step", "2000", "--media", "200", "--skip-ours"],
+                         check=True, capture_output=True, text=True, timeout=120,
+                         cwd=__import__("os").path.dirname(__import__("os").path.dirname(__file__))).stdout
+    res = json.loads(out)["reference_node"]
+    assert res["events"] == 4000 and res["handler_errors"] == 0 and res["http_requests"] > 0
