@@ -75,6 +75,8 @@ if os.environ.get("BEHOLDER_IOFUTURE", "1") == "0":  # A/B switch: plain asyncio
         resolve = _asyncio.Future.set_result
         reject = _asyncio.Future.set_exception
 AckBatcher = native.AckBatcher
+SinkStats = native.SinkStats
+NativeHandlers = native.NativeHandlers
 dispatch_batch = native.dispatch_batch
 frame = native.frame
 frames = native.frames
@@ -130,7 +132,7 @@ def codec_for(ptype) -> Optional[object]:
 
 
 __all__ = [
-    "native", "AckBatcher", "AmqpDemux", "Driver", "IOFuture", "H1Parser", "PgReader", "MessageCodec", "Ingest", "Delivery", "Settler", "Counter", "Histogram",
+    "native", "NativeHandlers", "SinkStats", "AckBatcher", "AmqpDemux", "Driver", "IOFuture", "H1Parser", "PgReader", "MessageCodec", "Ingest", "Delivery", "Settler", "Counter", "Histogram",
     "frame", "frames", "mono_ns", "codec_for", "field_table", "format_line", "quick_format", "js_str",
     "js_number", "encode_query", "quote_component",
 ]

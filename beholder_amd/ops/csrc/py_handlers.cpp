@@ -22,12 +22,15 @@
 #include <string>
 
 #include "py_common.hpp"
+#include "ring.hpp"
 
 namespace beholder {
 
 bool text_js_str_append(std::string& out, PyObject* v);
 bool is_native_logger(PyObject* logger);
 bool logcore_emit(PyObject* logger, bool native, long lvl, PyObject* const* args, Py_ssize_t nargs);
+bool sink_stats_record(PyObject* stats, PyObject* status, double seconds);
+bool is_sink_stats(PyObject* o);
 
 namespace {
 
@@ -36,7 +39,9 @@ PyObject *s_ack, *s_message, *s_content, *s_mediaId, *s_status, *s_progress, *s_
     *s_get_nowait, *s_update_nowait, *s_store, *s_get_by_id, *s_update_status, *s_trello, *s_make_request, *s_post,
     *s_put, *s_text, *s_idList, *s_pos, *s_deployed_hooks, *s_warn_missing_list, *s_child_for, *s_inc, *s_lower,
     *s_throw, *s_close, *s_lists, *s_no_trello, *s_deployed, *s_trello_creator, *s_log, *s_decode_status,
-    *s_decode_progress, *s_status_names_s, *s_status_names_p, *s_progress_counter, *s_comment_inc;
+    *s_decode_progress, *s_status_names_s, *s_status_names_p, *s_progress_counter, *s_comment_inc, *s_key,
+    *s_token, *s_base_url, *s_http, *s_timeout, *s_strict, *s_stats, *s_request, *s_params, *s_POST, *s_PUT,
+    *s_record, *s_raise_for_status, *s_rows, *s_get_calls, *kw_params_timeout;
 // log message literals (index.js:51,133,150)
 PyObject *m_progress, *m_status_kw, *m_percent, *m_creating, *m_with_text, *m_failed_progress, *m_failed_hooks;
 
@@ -58,6 +63,9 @@ struct HandlersObject {
   PyObject* err_message;    // handlers.err_message
   PyObject* js_type_error;  // handlers.JsTypeError
   PyObject* fallback;       // COMMENT_FALLBACK (index.js:54)
+  PyObject* trello_cls;     // sinks.trello.TrelloClient (exact type: request built here)
+  PyObject* memory_cls;     // store.memory.MemoryStore (exact type: row read here)
+  PyObject* not_found;      // store.base.MediaNotFound
   PyObject* one;            // TRELLO_CREATOR (index.js:79)
   PyObject* two;            // pos: 2 (index.js:85)
   uint64_t completed_sync;
@@ -78,6 +86,10 @@ struct CallObject {
   PyObject* progress;
   PyObject* host;
   PyObject* media;
+  PyObject* req_stats;  // sink stats of the Trello request in flight (native path), may be NULL
+  int64_t req_t0;
+  uint8_t req_native;   // a Trello request built here is in flight: trello_finish() applies
+  uint8_t req_strict;
   uint8_t kind;
   uint8_t state;
   uint8_t started;
@@ -205,9 +217,34 @@ bool raise_to_lower_case(HandlersObject* hs) {
   return false;
 }
 
-// media = await db.getByID(mediaId): nowait accessor when the store has one
+// media = await db.getByID(mediaId). The in-memory store's row read (store/memory.py
+// get_by_id_nowait) runs inline; other stores go through their nowait accessor or the coroutine.
 int get_media(CallObject* c, PyObject** out) {
   HandlersObject* hs = c->hs;
+  PyObject* store = hattr(hs, s_store);
+  if (!store) return -1;
+  if (reinterpret_cast<PyObject*>(Py_TYPE(store)) == hs->memory_cls) {
+    PyObject** dp = _PyObject_GetDictPtr(store);
+    PyObject* sd = dp ? *dp : nullptr;
+    PyObject* rows = sd ? PyDict_GetItemWithError(sd, s_rows) : nullptr;
+    PyObject* calls = rows ? PyDict_GetItemWithError(sd, s_get_calls) : nullptr;
+    if (calls && PyDict_CheckExact(rows)) {
+      PyObject* n = PyNumber_Add(calls, hs->one);  // self.get_calls += 1
+      if (!n) return -1;
+      int rc = PyDict_SetItem(sd, s_get_calls, n);
+      Py_DECREF(n);
+      if (rc < 0) return -1;
+      PyObject* m = PyDict_GetItemWithError(rows, c->media_id);
+      if (!m) {
+        if (!PyErr_Occurred()) PyErr_SetObject(hs->not_found, c->media_id);
+        return -1;
+      }
+      Py_INCREF(m);
+      *out = m;
+      return 1;
+    }
+    if (PyErr_Occurred()) return -1;
+  }
   PyObject* get = hattr(hs, s_get_nowait);
   if (!get) return -1;
   if (get != Py_None) {
@@ -216,21 +253,142 @@ int get_media(CallObject* c, PyObject** out) {
     *out = m;
     return 1;
   }
-  PyObject* store = hattr(hs, s_store);
-  if (!store) return -1;
   PyObject* aw = PyObject_CallMethodOneArg(store, s_get_by_id, c->media_id);
   if (!aw) return -1;
   return await_start(c, aw, out);
 }
 
-// await trello.makeRequest(method, path, options)
-int trello_request(CallObject* c, PyObject* method, PyObject* path, PyObject* options, PyObject** out) {
-  PyObject* trello = hattr(c->hs, s_trello);
+bool record_stats(PyObject* stats, PyObject* status, double seconds) {
+  if (is_sink_stats(stats)) return sink_stats_record(stats, status, seconds);
+  PyObject* sec = PyFloat_FromDouble(seconds);
+  if (!sec) return false;
+  PyObject* r = PyObject_CallMethodObjArgs(stats, s_record, status, sec, nullptr);
+  Py_DECREF(sec);
+  if (!r) return false;
+  Py_DECREF(r);
+  return true;
+}
+
+// Completes a Trello request issued on the native path (sinks/trello.py make_request after its
+// await): per-sink stats, strict mode. Takes and returns the result reference; NULL = raised.
+PyObject* trello_finish(CallObject* c, PyObject* value) {
+  if (!c->req_native) return value;
+  c->req_native = 0;
+  PyObject* stats = c->req_stats;
+  c->req_stats = nullptr;
+  double dt = double(mono_ns() - c->req_t0) * 1e-9;
+  if (!value) {
+    if (stats) {  // stats.record(None, dt); raise
+      PyObject *et, *ev, *tb;
+      PyErr_Fetch(&et, &ev, &tb);
+      if (record_stats(stats, Py_None, dt)) {
+        PyErr_Restore(et, ev, tb);
+      } else {
+        Py_XDECREF(et);
+        Py_XDECREF(ev);
+        Py_XDECREF(tb);
+      }
+      Py_DECREF(stats);
+    }
+    return nullptr;
+  }
+  if (stats) {
+    PyObject* st = PyObject_GetAttr(value, s_status);
+    bool ok = st && record_stats(stats, st, dt);
+    Py_XDECREF(st);
+    Py_DECREF(stats);
+    if (!ok) {
+      Py_DECREF(value);
+      return nullptr;
+    }
+  }
+  if (c->req_strict) {
+    PyObject* r = PyObject_CallMethodNoArgs(value, s_raise_for_status);
+    if (!r) {
+      Py_DECREF(value);
+      return nullptr;
+    }
+    Py_DECREF(r);
+  }
+  return value;
+}
+
+// await trello.makeRequest(method, path, {keys[i]: vals[i]}). For the stock TrelloClient the
+// request is built here: query {key, token, ...options} handed to http.request, as
+// sinks/trello.py does, with stats recorded by trello_finish().
+int trello_request(CallObject* c, PyObject* method, PyObject* method_upper, PyObject* path, PyObject* const* keys,
+                   PyObject* const* vals, int nopt, PyObject** out) {
+  HandlersObject* hs = c->hs;
+  PyObject* trello = hattr(hs, s_trello);
   if (!trello) return -1;
-  PyObject* args[4] = {trello, method, path, options};
-  PyObject* aw = PyObject_VectorcallMethod(s_make_request, args, 4, nullptr);
-  if (!aw) return -1;
-  return await_start(c, aw, out);
+  bool fast = reinterpret_cast<PyObject*>(Py_TYPE(trello)) == hs->trello_cls;
+  PyObject** dp = fast ? _PyObject_GetDictPtr(trello) : nullptr;
+  PyObject* td = dp ? *dp : nullptr;
+  PyObject* query = PyDict_New();
+  if (!query) return -1;
+  if (td) {  // {"key": self.key, "token": self.token, **options}
+    PyObject* key = PyDict_GetItemWithError(td, s_key);
+    PyObject* token = key ? PyDict_GetItemWithError(td, s_token) : nullptr;
+    if (!token || PyDict_SetItem(query, s_key, key) < 0 || PyDict_SetItem(query, s_token, token) < 0) {
+      Py_DECREF(query);
+      if (PyErr_Occurred()) return -1;
+      td = nullptr;  // unexpected layout: generic path
+      query = PyDict_New();
+      if (!query) return -1;
+    }
+  }
+  for (int i = 0; i < nopt; ++i) {
+    if (PyDict_SetItem(query, keys[i], vals[i]) < 0) {
+      Py_DECREF(query);
+      return -1;
+    }
+  }
+  PyObject* aw;
+  if (!td) {
+    PyObject* args[4] = {trello, method, path, query};
+    aw = PyObject_VectorcallMethod(s_make_request, args, 4, nullptr);
+    Py_DECREF(query);
+    if (!aw) return -1;
+    return await_start(c, aw, out);
+  }
+  PyObject* base = PyDict_GetItemWithError(td, s_base_url);
+  PyObject* http = base ? PyDict_GetItemWithError(td, s_http) : nullptr;
+  PyObject* timeout = http ? PyDict_GetItemWithError(td, s_timeout) : nullptr;
+  PyObject* strict = timeout ? PyDict_GetItemWithError(td, s_strict) : nullptr;
+  PyObject* stats = strict ? PyDict_GetItemWithError(td, s_stats) : nullptr;
+  if (!stats) {
+    Py_DECREF(query);
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_AttributeError, "TrelloClient attributes missing");
+    return -1;
+  }
+  int is_strict = PyObject_IsTrue(strict);
+  if (is_strict < 0) {
+    Py_DECREF(query);
+    return -1;
+  }
+  PyObject* url = PyUnicode_Concat(base, path);  // self.base_url + path
+  if (!url) {
+    Py_DECREF(query);
+    return -1;
+  }
+  c->req_t0 = mono_ns();
+  PyObject* args[5] = {http, method_upper, url, query, timeout};
+  aw = PyObject_VectorcallMethod(s_request, args, 3, kw_params_timeout);  // http.request(M, url, params=, timeout=)
+  Py_DECREF(url);
+  Py_DECREF(query);
+  c->req_native = 1;
+  c->req_strict = uint8_t(is_strict);
+  if (stats != Py_None) {
+    Py_INCREF(stats);
+    c->req_stats = stats;
+  }
+  int k = aw ? await_start(c, aw, out) : -1;
+  if (k != 0) {  // finished (or failed) without suspending
+    PyObject* v = trello_finish(c, k == 1 ? *out : nullptr);
+    if (!v) return -1;
+    *out = v;
+  }
+  return k;
 }
 
 // ------------------------------------------------------ progress handler ---
@@ -335,19 +493,17 @@ PySendResult step_progress(CallObject* c, PyObject* value, PyObject** result) {
       }
       path += "/actions/comments";
       PyObject* pathobj = unicode_from(path);
-      int truthy;
-      js_truthy(text, &truthy);
-      PyObject* options = pathobj ? PyDict_New() : nullptr;
-      if (!options || PyDict_SetItem(options, s_text, truthy ? text : hs->fallback) < 0) {
-        Py_XDECREF(options);
-        Py_XDECREF(pathobj);
+      if (!pathobj) {
         Py_DECREF(text);
         goto catch_;
       }
-      Py_DECREF(text);
-      k = trello_request(c, s_post, pathobj, options, &v);  // index.js:53-55
+      int truthy;
+      js_truthy(text, &truthy);
+      PyObject* okeys[1] = {s_text};
+      PyObject* ovals[1] = {truthy ? text : hs->fallback};
+      k = trello_request(c, s_post, s_POST, pathobj, okeys, ovals, 1, &v);  // index.js:53-55
       Py_DECREF(pathobj);
-      Py_DECREF(options);
+      Py_DECREF(text);
       if (k < 0) goto catch_;
       if (k == 0) {
         c->state = 2;
@@ -358,6 +514,7 @@ PySendResult step_progress(CallObject* c, PyObject* value, PyObject** result) {
       goto commented;
     }
     case 2:
+      value = trello_finish(c, value);
       if (!value) goto catch_;
       Py_DECREF(value);
     commented: {
@@ -503,17 +660,15 @@ PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
       ok = line && log_line(hs, 30, &line, 1);
       Py_XDECREF(line);
       PyObject* pathobj = ok ? unicode_from(path) : nullptr;
-      PyObject* options = pathobj ? PyDict_New() : nullptr;
-      if (!options || PyDict_SetItem(options, s_idList, lp) < 0 || PyDict_SetItem(options, s_pos, hs->two) < 0) {
-        Py_XDECREF(options);
-        Py_XDECREF(pathobj);
+      if (!pathobj) {
         Py_DECREF(lp);
         return fail(c);
       }
-      Py_DECREF(lp);
-      k = trello_request(c, s_put, pathobj, options, &v);  // index.js:83-86
+      PyObject* okeys[2] = {s_idList, s_pos};
+      PyObject* ovals[2] = {lp, hs->two};
+      k = trello_request(c, s_put, s_PUT, pathobj, okeys, ovals, 2, &v);  // index.js:83-86
       Py_DECREF(pathobj);
-      Py_DECREF(options);
+      Py_DECREF(lp);
       if (k < 0) return fail(c);
       if (k == 0) {
         c->state = 3;
@@ -524,6 +679,7 @@ PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
       goto hooks;
     }
     case 3:
+      value = trello_finish(c, value);
       if (!value) return fail(c);
       Py_DECREF(value);
     hooks: {  // try { ... } catch, index.js:92-122
@@ -697,6 +853,7 @@ int call_traverse(CallObject* c, visitproc visit, void* arg) {
   Py_VISIT(c->progress);
   Py_VISIT(c->host);
   Py_VISIT(c->media);
+  Py_VISIT(c->req_stats);
   return 0;
 }
 
@@ -710,6 +867,7 @@ int call_clear(CallObject* c) {
   Py_CLEAR(c->progress);
   Py_CLEAR(c->host);
   Py_CLEAR(c->media);
+  Py_CLEAR(c->req_stats);
   return 0;
 }
 
@@ -744,7 +902,9 @@ PyObject* make_call(HandlersObject* hs, PyObject* rmsg, uint8_t kind) {
   c->hs = hs;
   Py_INCREF(rmsg);
   c->rmsg = rmsg;
-  c->sub = c->media_id = c->status = c->status_text = c->progress = c->host = c->media = nullptr;
+  c->sub = c->media_id = c->status = c->status_text = c->progress = c->host = c->media = c->req_stats = nullptr;
+  c->req_t0 = 0;
+  c->req_native = c->req_strict = 0;
   c->kind = kind;
   c->state = 0;
   c->started = c->done = c->did_suspend = 0;
@@ -780,6 +940,9 @@ int hs_traverse(HandlersObject* hs, visitproc visit, void* arg) {
   Py_VISIT(hs->err_message);
   Py_VISIT(hs->js_type_error);
   Py_VISIT(hs->fallback);
+  Py_VISIT(hs->trello_cls);
+  Py_VISIT(hs->memory_cls);
+  Py_VISIT(hs->not_found);
   return 0;
 }
 
@@ -801,6 +964,9 @@ int hs_clear(HandlersObject* hs) {
   Py_CLEAR(hs->err_message);
   Py_CLEAR(hs->js_type_error);
   Py_CLEAR(hs->fallback);
+  Py_CLEAR(hs->trello_cls);
+  Py_CLEAR(hs->memory_cls);
+  Py_CLEAR(hs->not_found);
   return 0;
 }
 
@@ -826,6 +992,14 @@ PyObject* module_attr(PyObject* h, const char* name) {
   if (!modname) return nullptr;
   PyObject* mod = PyImport_Import(modname);
   Py_DECREF(modname);
+  if (!mod) return nullptr;
+  PyObject* v = PyObject_GetAttrString(mod, name);
+  Py_DECREF(mod);
+  return v;
+}
+
+PyObject* import_attr(const char* module, const char* name) {
+  PyObject* mod = PyImport_ImportModule(module);
   if (!mod) return nullptr;
   PyObject* v = PyObject_GetAttrString(mod, name);
   Py_DECREF(mod);
@@ -876,6 +1050,10 @@ int hs_init(HandlersObject* hs, PyObject* args, PyObject* kwds) {
   hs->js_type_error = hs->err_message ? module_attr(h, "JsTypeError") : nullptr;
   hs->fallback = hs->js_type_error ? module_attr(h, "COMMENT_FALLBACK") : nullptr;
   if (!hs->progress_plan || !hs->fallback || !hs->one || !hs->two) return -1;
+  hs->trello_cls = import_attr("beholder_amd.sinks.trello", "TrelloClient");
+  hs->memory_cls = hs->trello_cls ? import_attr("beholder_amd.store.memory", "MemoryStore") : nullptr;
+  hs->not_found = hs->memory_cls ? import_attr("beholder_amd.store.base", "MediaNotFound") : nullptr;
+  if (!hs->not_found) return -1;
   return 0;
 }
 
@@ -934,6 +1112,21 @@ int init_handler_types(PyObject* m) {
               {&s_status_names_p, "_status_names_p"},
               {&s_progress_counter, "progress_counter"},
               {&s_comment_inc, "_comment_inc"},
+              {&s_key, "key"},
+              {&s_token, "token"},
+              {&s_base_url, "base_url"},
+              {&s_http, "http"},
+              {&s_timeout, "timeout"},
+              {&s_strict, "strict"},
+              {&s_stats, "stats"},
+              {&s_request, "request"},
+              {&s_params, "params"},
+              {&s_POST, "POST"},
+              {&s_PUT, "PUT"},
+              {&s_record, "record"},
+              {&s_raise_for_status, "raise_for_status"},
+              {&s_rows, "_rows"},
+              {&s_get_calls, "get_calls"},
               {&m_progress, "processing progress update on media"},
               {&m_status_kw, "status"},
               {&m_percent, "percent"},
@@ -943,6 +1136,8 @@ int init_handler_types(PyObject* m) {
               {&m_failed_hooks, "failed to run deployed hooks:"}};
   for (auto& s : strs)
     if (!(*s.slot = intern(s.text))) return -1;
+  kw_params_timeout = PyTuple_Pack(2, s_params, s_timeout);
+  if (!kw_params_timeout) return -1;
 
   CallType.tp_name = "beholder_amd.ops._native.HandlerCall";
   CallType.tp_basicsize = sizeof(CallObject);

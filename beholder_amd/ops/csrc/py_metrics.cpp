@@ -341,7 +341,151 @@ PyMethodDef buckets_methods[] = {
     {"reset", reinterpret_cast<PyCFunction>(buckets_reset), METH_NOARGS, "zero everything"},
     {nullptr, nullptr, 0, nullptr}};
 
+// ---- SinkStats: per-sink request accounting (sinks/http.py SinkObserver.child) --------
+// record(status, seconds): beholder_sink_requests_total{sink,code} += 1 (code = HTTP status,
+// or "error" for a transport failure) and beholder_sink_request_seconds{sink}.observe(seconds).
+struct SinkStatsObject {
+  PyObject_HEAD PyObject* requests;  // the labelled Counter metric (Python, labels(sink, code))
+  PyObject* hist;                    // histogram child for this sink (Buckets or any .observe)
+  PyObject* sink;                    // sink name (str)
+  PyObject* codes;                   // dict: status (int / None) -> counter child
+};
+
+PyTypeObject SinkStatsType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+bool observe_value(PyObject* hist, double v) {
+  if (Py_TYPE(hist) == &BucketsType) {
+    BucketsObject* b = reinterpret_cast<BucketsObject*>(hist);
+    Py_ssize_t lo = 0, hi = b->n;
+    while (lo < hi) {
+      Py_ssize_t mid = (lo + hi) >> 1;
+      if (b->bounds[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    if (lo < b->n && !(v != v)) b->counts[lo]++;
+    b->sum += v;
+    b->count++;
+    return true;
+  }
+  PyObject* f = PyFloat_FromDouble(v);
+  if (!f) return false;
+  PyObject* r = PyObject_CallMethod(hist, "observe", "O", f);
+  Py_DECREF(f);
+  if (!r) return false;
+  Py_DECREF(r);
+  return true;
+}
+
+bool sink_stats_record(PyObject* obj, PyObject* status, double seconds) {
+  SinkStatsObject* s = reinterpret_cast<SinkStatsObject*>(obj);
+  PyObject* c = PyDict_GetItemWithError(s->codes, status);
+  if (!c) {
+    if (PyErr_Occurred()) return false;
+    PyObject* code = status == Py_None ? PyUnicode_FromString("error") : PyObject_Str(status);
+    if (!code) return false;
+    c = PyObject_CallMethod(s->requests, "labels", "OO", s->sink, code);
+    Py_DECREF(code);
+    if (!c) return false;
+    int rc = PyDict_SetItem(s->codes, status, c);
+    Py_DECREF(c);  // the dict holds it
+    if (rc < 0) return false;
+  }
+  if (Py_TYPE(c) == &CounterType) {
+    reinterpret_cast<CounterObject*>(c)->value += 1.0;
+  } else {
+    PyObject* r = PyObject_CallMethod(c, "inc", nullptr);
+    if (!r) return false;
+    Py_DECREF(r);
+  }
+  return observe_value(s->hist, seconds);
+}
+
+bool is_sink_stats(PyObject* o) { return Py_TYPE(o) == &SinkStatsType; }
+
+namespace {
+
+PyObject* sinkstats_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
+  static const char* kwlist[] = {"requests", "hist", "sink", nullptr};
+  PyObject *req, *hist, *sink;
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "OOU", const_cast<char**>(kwlist), &req, &hist, &sink))
+    return nullptr;
+  SinkStatsObject* s = reinterpret_cast<SinkStatsObject*>(type->tp_alloc(type, 0));
+  if (!s) return nullptr;
+  Py_INCREF(req);
+  s->requests = req;
+  Py_INCREF(hist);
+  s->hist = hist;
+  Py_INCREF(sink);
+  s->sink = sink;
+  s->codes = PyDict_New();
+  if (!s->codes) {
+    Py_DECREF(s);
+    return nullptr;
+  }
+  return reinterpret_cast<PyObject*>(s);
+}
+
+int sinkstats_traverse(SinkStatsObject* s, visitproc visit, void* arg) {
+  Py_VISIT(s->requests);
+  Py_VISIT(s->hist);
+  Py_VISIT(s->codes);
+  return 0;
+}
+
+int sinkstats_clear(SinkStatsObject* s) {
+  Py_CLEAR(s->requests);
+  Py_CLEAR(s->hist);
+  Py_CLEAR(s->sink);
+  Py_CLEAR(s->codes);
+  return 0;
+}
+
+void sinkstats_dealloc(SinkStatsObject* s) {
+  PyObject_GC_UnTrack(s);
+  sinkstats_clear(s);
+  Py_TYPE(s)->tp_free(reinterpret_cast<PyObject*>(s));
+}
+
+PyObject* sinkstats_record(SinkStatsObject* s, PyObject* const* a, Py_ssize_t n) {
+  if (n != 2) {
+    PyErr_SetString(PyExc_TypeError, "record(status, seconds)");
+    return nullptr;
+  }
+  double sec = PyFloat_AsDouble(a[1]);
+  if (sec == -1.0 && PyErr_Occurred()) return nullptr;
+  if (!sink_stats_record(reinterpret_cast<PyObject*>(s), a[0], sec)) return nullptr;
+  Py_RETURN_NONE;
+}
+
+PyObject* sinkstats_get_sink(SinkStatsObject* s, void*) {
+  Py_INCREF(s->sink);
+  return s->sink;
+}
+
+PyMethodDef sinkstats_methods[] = {
+    {"record", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(sinkstats_record)), METH_FASTCALL,
+     "record(status or None, seconds)"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyGetSetDef sinkstats_getset[] = {{"sink", reinterpret_cast<getter>(sinkstats_get_sink), nullptr, "sink name", nullptr},
+                                  {nullptr, nullptr, nullptr, nullptr, nullptr}};
+
+}  // namespace
+
 int init_metric_types(PyObject* m) {
+  SinkStatsType.tp_name = "beholder_amd.ops._native.SinkStats";
+  SinkStatsType.tp_basicsize = sizeof(SinkStatsObject);
+  SinkStatsType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC;
+  SinkStatsType.tp_doc = "SinkStats(requests, hist, sink): per-sink request counter + latency histogram";
+  SinkStatsType.tp_new = sinkstats_new;
+  SinkStatsType.tp_dealloc = reinterpret_cast<destructor>(sinkstats_dealloc);
+  SinkStatsType.tp_traverse = reinterpret_cast<traverseproc>(sinkstats_traverse);
+  SinkStatsType.tp_clear = reinterpret_cast<inquiry>(sinkstats_clear);
+  SinkStatsType.tp_methods = sinkstats_methods;
+  SinkStatsType.tp_getset = sinkstats_getset;
+  if (PyType_Ready(&SinkStatsType) < 0) return -1;
+  Py_INCREF(&SinkStatsType);
+  if (PyModule_AddObject(m, "SinkStats", reinterpret_cast<PyObject*>(&SinkStatsType)) < 0) return -1;
+
   BucketsType.tp_name = "beholder_amd.ops._native.Buckets";
   BucketsType.tp_basicsize = sizeof(BucketsObject);
   BucketsType.tp_flags = Py_TPFLAGS_DEFAULT;

@@ -30,6 +30,7 @@ import time
 from typing import Any, Callable, Deque, Dict, List, Mapping, Optional, Tuple
 from urllib.parse import quote
 
+from .. import ops as _native_ops
 from ..ops import encode_query as _native_encode_query
 
 _SAFE = "-_.!~*'()"    # encodeURIComponent
@@ -265,30 +266,16 @@ class SinkObserver:
                                           ["sink"], buckets=(0.005, 0.01, 0.025, 0.05, 0.1, 0.25, 0.5, 1, 2.5, 5, 10))
 
     def child(self, sink: str) -> "SinkStats":
-        return SinkStats(self, sink)
+        return SinkStats(self.requests, self.seconds.labels(sink), sink)
 
     def __call__(self, sink: str, status: Optional[int], seconds: float) -> None:
         self.child(sink).record(status, seconds)
 
 
-class SinkStats:
-    """Hot-path handle for one sink: native counter per status code + histogram child."""
-
-    __slots__ = ("_obs", "_sink", "_codes", "_hist")
-
-    def __init__(self, obs: SinkObserver, sink: str):
-        self._obs = obs
-        self._sink = sink
-        self._codes = {}
-        self._hist = obs.seconds.labels(sink)
-
-    def record(self, status: Optional[int], seconds: float) -> None:
-        c = self._codes.get(status)
-        if c is None:
-            c = self._codes[status] = self._obs.requests.labels(self._sink, "error" if status is None
-                                                                else str(status))
-        c.inc()
-        self._hist.observe(seconds)
+# Hot-path handle for one sink (native, ops/csrc/py_metrics.cpp): record(status, seconds) bumps the
+# per-status counter child and observes the sink's histogram child in C. The compiled handlers
+# (ops/csrc/py_handlers.cpp) record through it without a Python call.
+SinkStats = _native_ops.SinkStats
 
 
 async def observed(stats: Optional["SinkStats"], coro):
