@@ -63,6 +63,12 @@ struct HandlersObject {
   PyObject* err_message;    // handlers.err_message
   PyObject* js_type_error;  // handlers.JsTypeError
   PyObject* fallback;       // COMMENT_FALLBACK (index.js:54)
+  PyObject* res_s;          // decoded-message types when the decoders are native codecs (else NULL)
+  PyObject* res_p;
+  Py_ssize_t ix_s[2];       // TelemetryStatus slots: mediaId, status
+  Py_ssize_t ix_p[4];       // TelemetryProgress slots: mediaId, status, progress, host
+  PyObject* media_cls;      // store.base.Media (a NamedTuple)
+  Py_ssize_t ix_m[3];       // Media slots: creator, creatorId, status
   PyObject* trello_cls;     // sinks.trello.TrelloClient (exact type: request built here)
   PyObject* memory_cls;     // store.memory.MemoryStore (exact type: row read here)
   PyObject* not_found;      // store.base.MediaNotFound
@@ -123,6 +129,31 @@ PyObject* unicode_from(const std::string& s) { return PyUnicode_DecodeUTF8(s.dat
 
 bool log_line(HandlersObject* hs, long lvl, PyObject* const* args, Py_ssize_t n) {
   return logcore_emit(hs->log, hs->native_log != 0, lvl, args, n);
+}
+
+// msg.<name>: tuple slot for the known decoded / row types, attribute lookup otherwise
+inline PyObject* field(PyObject* obj, PyObject* type, Py_ssize_t ix, PyObject* name) {
+  if (type && reinterpret_cast<PyObject*>(Py_TYPE(obj)) == type) {
+    PyObject* v = PyTuple_GET_ITEM(obj, ix);
+    Py_INCREF(v);
+    return v;
+  }
+  return PyObject_GetAttr(obj, name);
+}
+
+// counter.inc(): native Counter bumped in place, anything else called
+bool call_inc(PyObject* inc) {
+  if (PyCFunction_Check(inc)) {
+    PyObject* self = PyCFunction_GET_SELF(inc);
+    if (self && Py_TYPE(self) == &CounterType) {
+      reinterpret_cast<CounterObject*>(self)->value += 1.0;
+      return true;
+    }
+  }
+  PyObject* r = PyObject_CallNoArgs(inc);
+  if (!r) return false;
+  Py_DECREF(r);
+  return true;
 }
 
 // rmsg.message.content
@@ -404,10 +435,10 @@ PySendResult step_progress(CallObject* c, PyObject* value, PyObject** result) {
       PyObject* msg = PyObject_CallOneArg(hs->decode_p, content);  // index.js:129
       Py_DECREF(content);
       if (!msg) goto catch_;
-      c->media_id = PyObject_GetAttr(msg, s_mediaId);
-      c->status = c->media_id ? PyObject_GetAttr(msg, s_status) : nullptr;
-      c->progress = c->status ? PyObject_GetAttr(msg, s_progress) : nullptr;
-      c->host = c->progress ? PyObject_GetAttr(msg, s_host) : nullptr;
+      c->media_id = field(msg, hs->res_p, hs->ix_p[0], s_mediaId);
+      c->status = c->media_id ? field(msg, hs->res_p, hs->ix_p[1], s_status) : nullptr;
+      c->progress = c->status ? field(msg, hs->res_p, hs->ix_p[2], s_progress) : nullptr;
+      c->host = c->progress ? field(msg, hs->res_p, hs->ix_p[3], s_host) : nullptr;
       Py_DECREF(msg);
       if (!c->host) goto catch_;
       {  // index.js:133
@@ -439,9 +470,7 @@ PySendResult step_progress(CallObject* c, PyObject* value, PyObject** result) {
       }
       c->status_text = PyTuple_GET_ITEM(plan, 0);
       Py_INCREF(c->status_text);
-      PyObject* r = PyObject_CallNoArgs(PyTuple_GET_ITEM(plan, 1));  // index.js:136-138
-      if (!r) goto catch_;
-      Py_DECREF(r);
+      if (!call_inc(PyTuple_GET_ITEM(plan, 1))) goto catch_;  // index.js:136-138
       k = get_media(c, &v);  // index.js:140
       if (k < 0) goto catch_;
       if (k == 0) {
@@ -456,7 +485,7 @@ PySendResult step_progress(CallObject* c, PyObject* value, PyObject** result) {
       if (!value) goto catch_;
       c->media = value;
     have_media: {
-      PyObject* creator = PyObject_GetAttr(c->media, s_creator);
+      PyObject* creator = field(c->media, hs->media_cls, hs->ix_m[0], s_creator);
       if (!creator) goto catch_;
       int is_trello = PyObject_RichCompareBool(creator, hs->trello_creator, Py_EQ);  // index.js:142
       Py_DECREF(creator);
@@ -476,7 +505,7 @@ PySendResult step_progress(CallObject* c, PyObject* value, PyObject** result) {
       }
       PyObject* text = unicode_from(s);
       if (!text) goto catch_;
-      PyObject* card = PyObject_GetAttr(c->media, s_creatorId);
+      PyObject* card = field(c->media, hs->media_cls, hs->ix_m[1], s_creatorId);
       if (!card) {
         Py_DECREF(text);
         goto catch_;
@@ -518,9 +547,7 @@ PySendResult step_progress(CallObject* c, PyObject* value, PyObject** result) {
       if (!value) goto catch_;
       Py_DECREF(value);
     commented: {
-      PyObject* r = PyObject_CallNoArgs(hs->comment_inc);  // index.js:57
-      if (!r) goto catch_;
-      Py_DECREF(r);
+      if (!call_inc(hs->comment_inc)) goto catch_;  // index.js:57
       goto finish;
     }
     default:
@@ -547,8 +574,8 @@ PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
       PyObject* msg = PyObject_CallOneArg(hs->decode_s, content);  // index.js:63
       Py_DECREF(content);
       if (!msg) return fail(c);
-      c->media_id = PyObject_GetAttr(msg, s_mediaId);
-      c->status = c->media_id ? PyObject_GetAttr(msg, s_status) : nullptr;
+      c->media_id = field(msg, hs->res_s, hs->ix_s[0], s_mediaId);
+      c->status = c->media_id ? field(msg, hs->res_s, hs->ix_s[1], s_status) : nullptr;
       Py_DECREF(msg);
       if (!c->status) return fail(c);
       std::string s = "processing status update for media ";  // index.js:66
@@ -607,7 +634,7 @@ PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
       if (!value) return fail(c);
       c->media = value;
     have_media: {  // TRELLO Movement, index.js:78-90
-      PyObject* creator = PyObject_GetAttr(c->media, s_creator);
+      PyObject* creator = field(c->media, hs->media_cls, hs->ix_m[0], s_creator);
       if (!creator) return fail(c);
       int is_trello = PyObject_RichCompareBool(creator, hs->one, Py_EQ);  // index.js:79
       Py_DECREF(creator);
@@ -643,7 +670,7 @@ PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
         Py_DECREF(r);
         goto hooks;
       }
-      PyObject* card = PyObject_GetAttr(c->media, s_creatorId);
+      PyObject* card = field(c->media, hs->media_cls, hs->ix_m[1], s_creatorId);
       if (!card) {
         Py_DECREF(lp);
         return fail(c);
@@ -683,7 +710,7 @@ PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
       if (!value) return fail(c);
       Py_DECREF(value);
     hooks: {  // try { ... } catch, index.js:92-122
-      PyObject* ms = PyObject_GetAttr(c->media, s_status);
+      PyObject* ms = field(c->media, hs->media_cls, hs->ix_m[2], s_status);
       if (!ms) goto hooks_catch;
       int deployed = PyObject_RichCompareBool(ms, hs->deployed, Py_EQ);  // index.js:94 (Q3)
       Py_DECREF(ms);
@@ -940,6 +967,9 @@ int hs_traverse(HandlersObject* hs, visitproc visit, void* arg) {
   Py_VISIT(hs->err_message);
   Py_VISIT(hs->js_type_error);
   Py_VISIT(hs->fallback);
+  Py_VISIT(hs->res_s);
+  Py_VISIT(hs->res_p);
+  Py_VISIT(hs->media_cls);
   Py_VISIT(hs->trello_cls);
   Py_VISIT(hs->memory_cls);
   Py_VISIT(hs->not_found);
@@ -964,6 +994,9 @@ int hs_clear(HandlersObject* hs) {
   Py_CLEAR(hs->err_message);
   Py_CLEAR(hs->js_type_error);
   Py_CLEAR(hs->fallback);
+  Py_CLEAR(hs->res_s);
+  Py_CLEAR(hs->res_p);
+  Py_CLEAR(hs->media_cls);
   Py_CLEAR(hs->trello_cls);
   Py_CLEAR(hs->memory_cls);
   Py_CLEAR(hs->not_found);
@@ -996,6 +1029,46 @@ PyObject* module_attr(PyObject* h, const char* name) {
   PyObject* v = PyObject_GetAttrString(mod, name);
   Py_DECREF(mod);
   return v;
+}
+
+// index of each of `names` in the tuple of str `fields`; false if one is missing
+bool slots_of(PyObject* fields, const char* const* names, int n, Py_ssize_t* ix) {
+  if (!PyTuple_Check(fields)) return false;
+  for (int k = 0; k < n; ++k) {
+    ix[k] = -1;
+    for (Py_ssize_t i = 0; i < PyTuple_GET_SIZE(fields); ++i) {
+      PyObject* f = PyTuple_GET_ITEM(fields, i);
+      if (PyUnicode_Check(f) && PyUnicode_CompareWithASCIIString(f, names[k]) == 0) {
+        ix[k] = i;
+        break;
+      }
+    }
+    if (ix[k] < 0) return false;
+  }
+  return true;
+}
+
+// When `decoder` is a native MessageCodec's bound decode, *type = its result type (a struct
+// sequence) and ix = the slots of `names`; otherwise *type stays NULL (attribute reads).
+bool codec_slots(PyObject* decoder, const char* const* names, int n, PyObject** type, Py_ssize_t* ix) {
+  *type = nullptr;
+  if (!PyCFunction_Check(decoder)) return true;
+  PyObject* self = PyCFunction_GET_SELF(decoder);
+  if (!self || Py_TYPE(self) != &CodecType) return true;
+  PyObject* fields = PyObject_GetAttrString(self, "field_names");
+  PyObject* rt = fields ? PyObject_GetAttrString(self, "result_type") : nullptr;
+  if (!rt) {
+    Py_XDECREF(fields);
+    return false;
+  }
+  if (slots_of(fields, names, n, ix) && PyType_Check(rt) &&
+      PyType_IsSubtype(reinterpret_cast<PyTypeObject*>(rt), &PyTuple_Type)) {
+    *type = rt;
+  } else {
+    Py_DECREF(rt);
+  }
+  Py_DECREF(fields);
+  return true;
 }
 
 PyObject* import_attr(const char* module, const char* name) {
@@ -1054,6 +1127,21 @@ int hs_init(HandlersObject* hs, PyObject* args, PyObject* kwds) {
   hs->memory_cls = hs->trello_cls ? import_attr("beholder_amd.store.memory", "MemoryStore") : nullptr;
   hs->not_found = hs->memory_cls ? import_attr("beholder_amd.store.base", "MediaNotFound") : nullptr;
   if (!hs->not_found) return -1;
+  static const char* pnames[4] = {"mediaId", "status", "progress", "host"};
+  if (!codec_slots(hs->decode_s, pnames, 2, &hs->res_s, hs->ix_s) ||
+      !codec_slots(hs->decode_p, pnames, 4, &hs->res_p, hs->ix_p))
+    return -1;
+  hs->media_cls = import_attr("beholder_amd.store.base", "Media");
+  if (!hs->media_cls) return -1;
+  static const char* mnames[3] = {"creator", "creatorId", "status"};
+  PyObject* mfields = PyObject_GetAttrString(hs->media_cls, "_fields");
+  if (!mfields) return -1;
+  bool ok = PyType_Check(hs->media_cls) &&
+            PyType_IsSubtype(reinterpret_cast<PyTypeObject*>(hs->media_cls), &PyTuple_Type) &&
+            slots_of(mfields, mnames, 3, hs->ix_m);
+  Py_DECREF(mfields);
+  if (PyErr_Occurred()) return -1;
+  if (!ok) Py_CLEAR(hs->media_cls);  // unexpected layout: attribute reads
   return 0;
 }
 

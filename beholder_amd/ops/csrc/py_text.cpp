@@ -101,6 +101,20 @@ void js_number_append(std::string& out, double x) {
   }
 }
 
+// Decimal text of a 64-bit integer (the hot log / query path: no snprintf).
+void append_i64(std::string& out, long long x) {
+  char buf[24];
+  char* e = buf + sizeof buf;
+  char* p = e;
+  unsigned long long u = x < 0 ? 0ULL - static_cast<unsigned long long>(x) : static_cast<unsigned long long>(x);
+  do {
+    *--p = char('0' + u % 10);
+    u /= 10;
+  } while (u);
+  if (x < 0) *--p = '-';
+  out.append(p, size_t(e - p));
+}
+
 // Appends String(v). Returns false with a Python error set on failure.
 bool js_str_append(std::string& out, PyObject* v) {
   if (PyUnicode_CheckExact(v)) {
@@ -126,9 +140,7 @@ bool js_str_append(std::string& out, PyObject* v) {
     int overflow = 0;
     long long x = PyLong_AsLongLongAndOverflow(v, &overflow);
     if (!overflow) {
-      char buf[32];
-      int len = snprintf(buf, sizeof buf, "%lld", x);
-      out.append(buf, size_t(len));
+      append_i64(out, x);
       return true;
     }
   }
@@ -303,9 +315,11 @@ bool quick_format_append(std::string& out, PyObject* const* args, Py_ssize_t nar
 // Appends one pino line for `args` to `out`. Returns false with a Python error set.
 bool append_line(std::string& out, long lvl, long long t, const char* prefix, Py_ssize_t plen, PyObject* extra,
                  PyObject* const* argv, Py_ssize_t nargs) {
-  char head[64];
-  int hl = snprintf(head, sizeof head, "{\"level\":%ld,\"time\":%lld,", lvl, t);
-  out.append(head, size_t(hl));
+  out += "{\"level\":";
+  append_i64(out, lvl);
+  out += ",\"time\":";
+  append_i64(out, t);
+  out += ',';
   out.append(prefix, size_t(plen));
   if (extra && extra != Py_None) {
     Py_ssize_t el;
@@ -314,8 +328,8 @@ bool append_line(std::string& out, long lvl, long long t, const char* prefix, Py
     out.append(ex, size_t(el));
   }
   if (nargs) {
-    std::string msg;
-    msg.reserve(128);
+    static thread_local std::string msg;  // scratch: no allocation per line
+    msg.clear();
     if (!quick_format_append(msg, argv, nargs)) return false;
     out += ",\"msg\":\"";
     json_escape_append(out, msg.data(), msg.size());

@@ -8,7 +8,8 @@ triton-core/{config,dynamics,amqp,db,proto,prom}). The stand-ins do the same wor
 repo's bench fakes: protobuf decode, the JSON log line per log call, URL + query-string
 construction per sink request, label-hashed counters, an in-memory media table. Each is
 at most as expensive as the real library (the log sink is buffered, where pino@5 writes
-synchronously). The Node number is therefore an upper bound for the reference.
+synchronously; ``--pino-sync`` adds a run with that behaviour). The buffered Node number is
+therefore an upper bound for the reference, and ``speedup`` is taken against it.
 
 Both sides consume identical event streams: the same generator and seeds as bench.py, one
 stream per process. They use the same step size and warm-up, and the same number of
@@ -50,7 +51,7 @@ def write_inputs(d: str, i: int, seed: int, a) -> dict:
     return paths
 
 
-def run_node(a) -> dict:
+def run_node(a, pino_sync: bool = False) -> dict:
     env = dict(os.environ, NODE_PATH=os.path.join(HERE, "stubs"))
     env.pop("NO_TRELLO", None)
     with tempfile.TemporaryDirectory() as d:
@@ -59,7 +60,7 @@ def run_node(a) -> dict:
             p = write_inputs(d, i, a.seed + 104729 * i, a)
             cmd = [a.node, os.path.join(HERE, "harness.js"), "--index", a.index, "--config", p["config"],
                    "--media", p["media"], "--events", p["events"], "--events-per-step", str(a.events_per_step),
-                   "--warmup", str(a.warmup), "--steps", str(a.steps), "--wait-go"]
+                   "--warmup", str(a.warmup), "--steps", str(a.steps), "--wait-go"] + (["--pino-sync"] if pino_sync else [])
             procs.append(subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, env=env, text=True))
         for p in procs:
             line = p.stdout.readline()
@@ -102,12 +103,16 @@ def main() -> int:
     ap.add_argument("--media", type=int, default=10000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--skip-ours", action="store_true")
+    ap.add_argument("--pino-sync", action="store_true",
+                    help="also run the reference with one write(2) per log line (pino@5's default destination)")
     ap.add_argument("--out")
     a = ap.parse_args()
     if not os.path.exists(a.index):
         print(f"reference index.js not found at {a.index}", file=sys.stderr)
         return 2
     res = {"reference_node": run_node(a)}
+    if a.pino_sync:
+        res["reference_node_pino_sync"] = run_node(a, pino_sync=True)
     if not a.skip_ours:
         ours = run_ours(a)
         res["ours"] = {k: ours[k] for k in ("value", "events_per_proc_per_sec", "p50_handle_latency_us",

@@ -5,8 +5,10 @@
 // (handler call -> rmsg.ack()).
 //
 //   node harness.js --index /root/reference/index.js --config cfg.json --media media.json \
-//        --events events.bin --events-per-step E --warmup W --steps K [--wait-go]
+//        --events events.bin --events-per-step E --warmup W --steps K [--wait-go] [--pino-sync]
 //
+// --pino-sync writes every log line with its own write(2), as pino@5's default destination does;
+// without it lines are buffered (cheaper than the real library).
 // With --wait-go it prints "ready" after the warm-up steps and waits for a line on stdin before
 // the timed steps (the Python driver starts several processes together this way).
 const fs = require('fs')
@@ -19,12 +21,17 @@ function arg (name, def) {
 }
 
 class Sink {
-  constructor (fd) {
+  constructor (fd, sync) {
     this.fd = fd
+    this.sync = sync
     this.buf = ''
   }
 
   write (s) {
+    if (this.sync) {
+      fs.writeSync(this.fd, s)
+      return
+    }
     this.buf += s
     if (this.buf.length >= 65536) this.flush()
   }
@@ -41,7 +48,7 @@ const h = global.__beholderHarness = {
   config: JSON.parse(fs.readFileSync(arg('config'), 'utf8')),
   media: new Map(),
   listeners: {},
-  logSink: new Sink(fs.openSync(arg('log', '/dev/null'), 'w')),
+  logSink: new Sink(fs.openSync(arg('log', '/dev/null'), 'w'), process.argv.includes('--pino-sync')),
   logLevel: arg('log-level', 'info'),
   calls: 0,
   recent: new Array(16),

@@ -1,8 +1,9 @@
 'use strict'
 // In-process stand-in for pino@5 (yarn.lock:1438-1448): the same JSON line envelope the
-// reference writes ({"level","time","pid","hostname","name","msg","v":1}), buffered into a
-// 64 KiB sink on /dev/null. Real pino@5 defaults to one synchronous write(2) per line; the
-// buffer makes this stand-in cheaper than the real library, never dearer.
+// reference writes ({"level","time","pid","hostname","name","msg","v":1}) into a sink on
+// /dev/null. By default the sink buffers 64 KiB per write(2), which is cheaper than the real
+// library. pino@5's default destination (sonic-boom, sync) issues one write(2) per line; the
+// harness's --pino-sync mode reproduces that.
 const os = require('os')
 const h = global.__beholderHarness
 
