@@ -68,6 +68,10 @@ SERVICE_DEFAULTS: dict = {
         "trace": False,
         # handlers compiled to native state machines (ops/csrc/py_handlers.cpp); false = handlers.py
         "native_handlers": True,
+        # Jaeger spans per delivery (utils/tracing.py); JAEGER_* env variables override
+        "tracing": {"enabled": False, "service_name": "beholder",
+                    "sampler": {"type": "const", "param": 1},
+                    "agent": {"host": "127.0.0.1", "port": 6831}},
     }
 }
 

@@ -36,6 +36,7 @@ struct Pending {
   bool redelivered = false;
   int topic = 0;
   PyObject* extra = nullptr;  // borrowed from ConsumerInfo (kept alive by the map)
+  std::string headers;        // raw `headers` field table (u32 length + body) when captured
 };
 
 // RabbitMQ's hard upper bound for a message body (max_message_size <= 512 MiB).
@@ -48,6 +49,7 @@ struct AmqpDemuxObject {
   std::map<std::pair<uint16_t, std::string>, ConsumerInfo>* consumers;
   uint32_t frame_max;
   uint64_t deliveries, frames, passthrough, heartbeats;
+  uint8_t capture_headers;  // keep the `headers` property of deliveries (trace context)
 };
 
 inline uint16_t be16(const uint8_t* p) { return uint16_t((p[0] << 8) | p[1]); }
@@ -184,6 +186,15 @@ bool emit_delivery(AmqpDemuxObject* self, PyObject* out, Pending& pd, int64_t no
     Py_INCREF(pd.extra);
     reinterpret_cast<DeliveryObject*>(d)->extra = pd.extra;
   }
+  if (!pd.headers.empty()) {
+    PyObject* h = PyBytes_FromStringAndSize(pd.headers.data(), Py_ssize_t(pd.headers.size()));
+    if (!h) {
+      Py_DECREF(d);
+      return false;
+    }
+    reinterpret_cast<DeliveryObject*>(d)->headers = h;
+    pd.headers.clear();
+  }
   int r = PyList_Append(out, d);
   Py_DECREF(d);
   pd.mode = Pending::NONE;
@@ -259,6 +270,25 @@ bool handle_frame(AmqpDemuxObject* self, PyObject* out, uint8_t type, uint16_t c
     }
     pd.have_header = true;
     pd.size = be64(p + 4);
+    pd.headers.clear();
+    if (self->capture_headers) {
+      // property flags (bit 15 content-type, 14 content-encoding, 13 headers), then the values
+      uint16_t flags = be16(p + 12);
+      uint32_t off = 14;
+      bool ok = true;
+      for (uint16_t bit : {uint16_t(0x8000), uint16_t(0x4000)}) {
+        if (!(flags & bit)) continue;
+        if (off + 1 > n || off + 1 + p[off] > n) {
+          ok = false;
+          break;
+        }
+        off += 1 + p[off];
+      }
+      if (ok && (flags & 0x2000) && off + 4 <= n) {
+        uint32_t tl = be32(p + off);
+        if (uint64_t(off) + 4 + tl <= n) pd.headers.assign(reinterpret_cast<const char*>(p + off), 4 + size_t(tl));
+      }
+    }
     if (pd.size > kMaxBody) {
       PyErr_Format(PyExc_ValueError, "content body size %llu exceeds the %llu byte limit",
                    (unsigned long long)pd.size, (unsigned long long)kMaxBody);
@@ -361,7 +391,17 @@ PyObject* demux_get_passthrough(AmqpDemuxObject* self, void*) {
   return PyLong_FromUnsignedLongLong(self->passthrough);
 }
 
+PyObject* demux_get_capture(AmqpDemuxObject* self, void*) { return PyBool_FromLong(self->capture_headers); }
+int demux_set_capture(AmqpDemuxObject* self, PyObject* v, void*) {
+  int t = v ? PyObject_IsTrue(v) : 0;
+  if (t < 0) return -1;
+  self->capture_headers = uint8_t(t);
+  return 0;
+}
+
 PyGetSetDef demux_getset[] = {
+    {"capture_headers", reinterpret_cast<getter>(demux_get_capture), reinterpret_cast<setter>(demux_set_capture),
+     "attach each delivery's raw `headers` field table (Delivery.headers)", nullptr},
     {"passthrough", reinterpret_cast<getter>(demux_get_passthrough), nullptr,
      "frames handed to Python so far (unchanged across a feed() = the result holds only deliveries)", nullptr},
     {nullptr, nullptr, nullptr, nullptr, nullptr}};

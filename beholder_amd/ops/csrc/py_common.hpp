@@ -68,6 +68,7 @@ struct DeliveryObject {
   PyObject_HEAD PyObject* content;  // bytes
   SettlerObject* settler;           // may be NULL
   PyObject* extra;                  // transport-specific payload, may be NULL
+  PyObject* headers;                // message headers (dict, or raw AMQP field-table bytes), may be NULL
   uint64_t tag;
   int64_t recv_ns;
   int64_t start_ns;

@@ -173,6 +173,7 @@ PyObject* delivery_new(PyObject* content, uint8_t topic, uint64_t tag, int64_t r
   d->settler = settler;
   Py_XINCREF(settler);
   d->extra = nullptr;
+  d->headers = nullptr;
   d->tag = tag;
   d->recv_ns = recv_ns;
   d->start_ns = 0;
@@ -259,6 +260,7 @@ void delivery_dealloc(DeliveryObject* self) {
   }
   Py_XDECREF(self->content);
   Py_XDECREF(self->extra);
+  Py_XDECREF(self->headers);
   Py_XDECREF(s);
   PyObject_Del(self);
 }
@@ -361,6 +363,23 @@ int delivery_set_extra(DeliveryObject* self, PyObject* v, void*) {
   return 0;
 }
 
+PyObject* delivery_get_headers(DeliveryObject* self, void*) {
+  PyObject* h = self->headers ? self->headers : Py_None;
+  Py_INCREF(h);
+  return h;
+}
+int delivery_set_headers(DeliveryObject* self, PyObject* v, void*) {
+  PyObject* old = self->headers;
+  if (v == nullptr || v == Py_None) {
+    self->headers = nullptr;
+  } else {
+    Py_INCREF(v);
+    self->headers = v;
+  }
+  Py_XDECREF(old);
+  return 0;
+}
+
 PyObject* delivery_repr(DeliveryObject* self) {
   return PyUnicode_FromFormat("<Delivery tag=%llu topic=%d state=%s bytes=%zd>", (unsigned long long)self->tag,
                               int(self->topic), state_name(self->state), PyBytes_GET_SIZE(self->content));
@@ -391,6 +410,8 @@ PyGetSetDef delivery_getset[] = {
     {"redelivered", reinterpret_cast<getter>(delivery_get_redelivered), nullptr, nullptr, nullptr},
     {"extra", reinterpret_cast<getter>(delivery_get_extra), reinterpret_cast<setter>(delivery_set_extra),
      "transport-specific data (must not reference the delivery)", nullptr},
+    {"headers", reinterpret_cast<getter>(delivery_get_headers), reinterpret_cast<setter>(delivery_set_headers),
+     "message headers: dict, raw AMQP field-table bytes (native demux), or None", nullptr},
     {nullptr, nullptr, nullptr, nullptr, nullptr}};
 
 }  // namespace

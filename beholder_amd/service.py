@@ -46,11 +46,12 @@ from .store import MediaStore, open_store
 from .transport.base import Source
 from .ops import Driver, dispatch_batch
 from .utils.log import Logger
+from .utils.tracing import extract as extract_trace_context, tracer_from_config
 
 Handler = Callable[[Any], Any]
 
 
-def build_source(config: Config, logger: Optional[Logger] = None) -> Source:
+def build_source(config: Config, logger: Optional[Logger] = None, capture_headers: bool = False) -> Source:
     """Construct the ingest transport from ``service.transport``."""
     tcfg = config.data["service"]["transport"]
     kind = (tcfg.get("kind") or "amqp").lower()
@@ -79,7 +80,7 @@ def build_source(config: Config, logger: Optional[Logger] = None) -> Source:
         url = tcfg.get("url") or dyn("rabbitmq", env=config.env, config=config)
         hb = tcfg.get("heartbeat")
         return AmqpSource(url, prefetch=prefetch, retries=int(config.data["service"]["retries"]),
-                          logger=logger, heartbeat=None if hb is None else int(hb))
+                          logger=logger, heartbeat=None if hb is None else int(hb), capture_headers=capture_headers)
     raise ValueError(f"unknown transport kind {kind!r} (amqp|stdin|file)")
 
 
@@ -113,6 +114,8 @@ class Service:
         self.grace_s = float(svc["shutdown_grace_s"])
         # per-message trace spans (SURVEY.md §5 tracing): one debug line per handled delivery
         self.trace = bool(svc.get("trace", False))
+        # Jaeger spans per delivery (utils/tracing.py): service.tracing or JAEGER_* env
+        self.tracer = tracer_from_config(svc.get("tracing"), env=config.env)
         self._routes: List[Optional[Handler]] = [None] * len(T.TOPIC_NAMES_BY_ID)
         self._inflight: set = set()
         self._slot_free: Optional[asyncio.Event] = None
@@ -182,7 +185,7 @@ class Service:
 
         # 6. transport (index.js:43-44)
         if self._source is None:
-            self._source = build_source(cfg, self.log)
+            self._source = build_source(cfg, self.log, capture_headers=self.tracer is not None)
 
         # 7. proto types + handlers (index.js:46-60)
         self.handlers = TelemetryHandlers(
@@ -325,7 +328,7 @@ class Service:
         sleep = asyncio.sleep
         # native fast path: the per-delivery loop runs in C (ops.dispatch_batch); per-media
         # ordering and trace spans keep the Python loop
-        native = (self.serializer is None and not self.trace
+        native = (self.serializer is None and not self.trace and self.tracer is None
                   and os.environ.get("BEHOLDER_NATIVE_DISPATCH", "1") != "0")
         native_dispatch = dispatch_batch
         routes = tuple(routes)
@@ -369,6 +372,8 @@ class Service:
             while True:
                 await asyncio.sleep(every_s)
                 self.log.flush()
+                if self.tracer is not None:
+                    self.tracer.flush()
         except asyncio.CancelledError:
             pass
 
@@ -378,32 +383,60 @@ class Service:
                         "handle_us": (now - d.start_ns) // 1000, "outcome": outcome, "state": d.state},
                        "handled")
 
+    def _trace_start(self, d):
+        """A Jaeger span for this delivery (None when not sampled). Called after ``d.start()``."""
+        topic = d.topic or str(d.topic_id)
+        return self.tracer.start_span(topic, child_of=extract_trace_context(d.headers), tags={
+            "span.kind": "consumer", "component": "beholder", "message_bus.destination": topic,
+            "amqp.delivery_tag": d.tag, "amqp.redelivered": d.redelivered,
+            "beholder.queue_us": max(0, d.start_ns - d.recv_ns) // 1000})
+
+    def _trace_finish(self, span, d, exc: Optional[BaseException]) -> None:
+        h = self.handlers
+        try:
+            dec = h.decode_status if d.topic_id == T.STATUS_ID else h.decode_progress
+            span.set_tag("mediaId", dec(d.content).mediaId)
+        except Exception:  # noqa: BLE001 — undecodable message: the error tag says why
+            pass
+        span.set_tag("beholder.outcome", d.state)  # pending = left un-acked (quirk Q1)
+        if exc is not None:
+            span.set_tag("error", True)
+            span.log_kv({"event": "error", "error.kind": type(exc).__name__, "message": err_message(exc)})
+        span.finish()
+
     def _dispatch_now(self, d, on_finish: Optional[Callable[[], None]] = None) -> bool:
         """Python dispatch path (per-media ordering, trace spans). Returns True when the handler
         finished synchronously; otherwise a Driver finishes it and calls ``on_finish()`` then."""
         handler = self._routes[d.topic_id]
         d.start()
+        span = self._trace_start(d) if self.tracer is not None else None
         coro = handler(d)
         try:
             first = coro.send(None)
         except StopIteration:
             if self.trace:
                 self._span(d, "ok" if d.settled else "unsettled")
+            if span is not None:
+                self._trace_finish(span, d, None)
             return True
         except BaseException as exc:  # noqa: BLE001 — handler errors are data here
             self._on_handler_error(d, exc)
+            if span is not None:
+                self._trace_finish(span, d, exc)
             exc = None  # the traceback reaches this frame via f_back: don't keep a cycle alive
             if self.trace:
                 self._span(d, "ok" if d.settled else "unsettled")
             return True
-        if on_finish is None and not self.trace:
+        if on_finish is None and not self.trace and span is None:
             self._on_suspend(d, coro, first)
             return False
 
-        def done(drv, exc, on_finish=on_finish, d=d):
+        def done(drv, exc, on_finish=on_finish, d=d, span=span):
             self._driver_done(drv, exc)
             if self.trace:
                 self._span(d, "ok" if d.settled else "unsettled")
+            if span is not None:
+                self._trace_finish(span, d, exc)
             if on_finish is not None:
                 on_finish()
         drv = Driver(coro, done, d)
@@ -485,6 +518,8 @@ class Service:
             await self._http.close()
         if self.metrics_server is not None:
             await self.metrics_server.stop()
+        if self.tracer is not None:
+            self.tracer.close()
         self.log.flush()
 
     # ---------------------------------------------------------------- stats ---
@@ -504,6 +539,8 @@ class Service:
         if self.serializer is not None:  # per-media ordering (opt-in)
             out["ordering"] = {"active_keys": self.serializer.active_keys,
                                "serialized": self.serializer.serialized, "max_chain": self.serializer.max_chain}
+        if self.tracer is not None:
+            out["tracing"] = self.tracer.reporter.stats()
         http_stats = getattr(self._http, "stats", None)
         if callable(http_stats):  # keep-alive pool accounting (sinks/h1.py)
             out["http"] = http_stats()

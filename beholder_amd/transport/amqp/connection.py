@@ -289,7 +289,8 @@ class Channel:
 class Connection:
     def __init__(self, url: str, *, heartbeat: Optional[int] = None, connect_timeout: float = 10.0,
                  logger=None, on_lost: Optional[Callable[[Optional[BaseException]], None]] = None,
-                 native_settler=None, on_deliveries: Optional[Callable[[List[Any]], None]] = None):
+                 native_settler=None, on_deliveries: Optional[Callable[[List[Any]], None]] = None,
+                 capture_headers: bool = False):
         """``native_settler`` + ``on_deliveries`` enable the native delivery path
         (:class:`~beholder_amd.ops.AmqpDemux`): deliveries for consumers
         registered with ``native_topic`` arrive as native ``Delivery`` objects
@@ -330,6 +331,7 @@ class Connection:
         if native_settler is not None and on_deliveries is not None:
             from ...ops import AmqpDemux
             self._demux = AmqpDemux(native_settler, 0)
+            self._demux.capture_headers = capture_headers  # Delivery.headers (trace context)
 
     # ------------------------------------------------------------- open ----
     async def open(self) -> "Connection":

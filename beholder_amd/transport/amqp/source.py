@@ -38,8 +38,9 @@ class AmqpSource(Source):
     def __init__(self, url: str, prefetch: int = 100, retries: int = 2, *, logger=None,
                  durable: bool = True, heartbeat: Optional[int] = None, backoff_initial: float = 0.25,
                  backoff_max: float = 30.0, connect_timeout: float = 10.0, native: bool = True,
-                 coalesce_acks: bool = True):
+                 coalesce_acks: bool = True, capture_headers: bool = False):
         self.url = url
+        self.capture_headers = capture_headers  # keep message headers on deliveries (trace context)
         self._prefetch = int(prefetch)
         self.retries = int(retries)
         self.log = logger
@@ -102,7 +103,8 @@ class AmqpSource(Source):
         conn = Connection(self.url, heartbeat=self.heartbeat, connect_timeout=self.connect_timeout,
                           logger=self.log, on_lost=self._on_lost,
                           native_settler=self._settler if self.native else None,
-                          on_deliveries=self._on_native_deliveries if self.native else None)
+                          on_deliveries=self._on_native_deliveries if self.native else None,
+                          capture_headers=self.capture_headers)
         await conn.open()
         try:
             ch = await conn.channel()
@@ -124,6 +126,8 @@ class AmqpSource(Source):
     def _on_message(self, ch: Channel, method, props, body: bytes) -> None:
         tid = self._tag_topic.get(method.consumer_tag, 0)
         d = Delivery(body, tid, method.delivery_tag, self._settler, None, method.redelivered, ch)
+        if self.capture_headers:
+            d.headers = props.get("headers")
         self._on_native_deliveries([d])
 
     def _on_native_deliveries(self, ds) -> None:
