@@ -392,6 +392,15 @@ int trello_request(CallObject* c, PyObject* method, PyObject* method_upper, PyOb
     if (!PyErr_Occurred()) PyErr_SetString(PyExc_AttributeError, "TrelloClient attributes missing");
     return -1;
   }
+  // own them: the calls below may run Python code that rebinds the client's attributes
+  PyObject* held[5] = {base, http, timeout, strict, stats};
+  for (PyObject* o : held) Py_INCREF(o);
+  struct Release {
+    PyObject** objs;
+    ~Release() {
+      for (int i = 0; i < 5; ++i) Py_DECREF(objs[i]);
+    }
+  } release{held};
   int is_strict = PyObject_IsTrue(strict);
   if (is_strict < 0) {
     Py_DECREF(query);
