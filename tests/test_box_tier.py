@@ -26,8 +26,53 @@ def test_native_runtime_is_in_tree_and_loaded():
     # every hot-path entry point is native
     for name in ("MessageCodec", "Ingest", "Delivery", "Settler", "Histogram", "format_line", "encode_query",
                  "AmqpDemux", "H1Parser", "PgReader", "Driver", "IOFuture", "AckBatcher", "Buckets",
-                 "dispatch_batch", "pg_bind"):
+                 "dispatch_batch", "pg_bind", "NativeHandlers", "HandlerCall", "SinkStats"):
         assert hasattr(ops.native, name), name
+
+
+def test_compiled_handlers_match_python_on_the_box():
+    """The compiled handlers are the service default, and they agree with handlers.py on the
+    target image: the same 20k-event stream through both gives identical sink requests, counters
+    and store contents."""
+    import asyncio
+
+    from beholder_amd.bench.generator import Workload, bench_config
+    from beholder_amd.config import Config
+    from beholder_amd.ops import native
+    from beholder_amd.service import Service
+    from beholder_amd.sinks import RecordingHttpClient
+    from beholder_amd.store import MemoryStore
+    from beholder_amd.transport.ingest import BytesSource
+    from beholder_amd.utils.log import Logger, MemoryStream
+
+    w = Workload(n_media=500, seed=11, unknown_media_fraction=0.01)
+    data = w.framed(20_000)
+
+    def run(native_on):
+        cfg = bench_config()
+        cfg["service"]["native_handlers"] = native_on
+        http, store, stream = RecordingHttpClient(), MemoryStore(w.media), MemoryStream()
+        svc = Service(Config.from_dict(cfg), source=BytesSource(data), store=store, http=http,
+                      logger=Logger(stream=stream), serve_metrics=False)
+
+        async def go():
+            await svc.init()
+            st = await svc.run()
+            await svc.close()
+            return st
+        st = asyncio.run(go())
+        import gc
+        gc.collect()  # un-acked (Q1) deliveries are counted abandoned when freed
+        st["source"] = svc.source.settler.stats()
+        return svc, st, list(http.calls), sorted(store.snapshot().items()), [
+            (r["level"], r["msg"]) for r in stream.records()]
+
+    a = run(True)
+    b = run(False)
+    assert isinstance(a[0].handler_impl, native.NativeHandlers) and b[0].handler_impl is b[0].handlers
+    assert a[1]["source"]["acked"] == b[1]["source"]["acked"] and a[1]["source"]["abandoned"] == b[1]["source"]["abandoned"]
+    assert a[1]["progress_updates"] == b[1]["progress_updates"] and a[1]["trello_comments"] == b[1]["trello_comments"]
+    assert a[2] == b[2] and a[3] == b[3] and a[4] == b[4]
 
 
 def test_bench_single_rank_full_path():
