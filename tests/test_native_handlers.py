@@ -17,6 +17,8 @@ points. Concurrent runs (asyncio.gather) check that suspension interleaves ident
 from __future__ import annotations
 
 import asyncio
+import os
+import shutil
 import gc
 
 import pytest
@@ -127,7 +129,8 @@ def run_trace(impl, config, no_trello, rows, evs, fault_list, store_kind, concur
     }
 
 
-@settings(max_examples=300, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@settings(max_examples=int(os.environ.get("BEHOLDER_FUZZ_EXAMPLES", "300")), deadline=None,
+          suppress_health_check=[HealthCheck.too_slow])
 @given(config=configs, no_trello=st.booleans(), rows=medias, evs=events, fault_list=faults,
        store_kind=st.sampled_from(sorted(STORES)), concurrent=st.booleans())
 def test_native_matches_python(config, no_trello, rows, evs, fault_list, store_kind, concurrent):
@@ -246,8 +249,8 @@ def test_subclass_keeps_python_path():
     assert native_handlers(r.h) is None
 
 
-@pytest.mark.skipif(not __import__("os").path.exists("/root/reference/index.js") or
-                    not __import__("shutil").which("node"), reason="needs the reference checkout and node")
+@pytest.mark.skipif(not os.path.exists("/root/reference/index.js") or not shutil.which("node"),
+                    reason="needs the reference checkout and node")
 def test_reference_node_harness_runs_the_reference():
     """scripts/bench_reference_node.py: the reference index.js under in-process stand-ins acks every event."""
     import json
@@ -256,6 +259,6 @@ def test_reference_node_harness_runs_the_reference():
     out = subprocess.run([sys.executable, "scripts/bench_reference_node.py", "--procs", "1", "--steps", "2",
                           "--warmup", "1", "--events-per-step", "2000", "--media", "200", "--skip-ours"],
                          check=True, capture_output=True, text=True, timeout=120,
-                         cwd=__import__("os").path.dirname(__import__("os").path.dirname(__file__))).stdout
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__)))).stdout
     res = json.loads(out)["reference_node"]
     assert res["events"] == 4000 and res["handler_errors"] == 0 and res["http_requests"] > 0
