@@ -19,7 +19,8 @@ steps run untimed, then exactly ``K`` steps are timed.
 
 Scale-out is the reference's: competing consumers, one process each
 (SURVEY.md §2.3). Each rank runs ``--procs-per-rank`` consumer processes
-(default: its share of the host CPUs minus one, at most 16) on independent streams.
+(default: the CPU share of one GPU slot minus one, at most 16; the same for every N) on
+independent streams.
 Timing: every consumer finishes its warm-up and parks on a barrier; the
 rank's coordinator passes a gloo barrier across ranks, releases its
 consumers and starts the clock; it stops the clock when all of its
@@ -79,6 +80,27 @@ def available_cpus() -> int:
     return max(1, n)
 
 
+def gpus_on_node() -> int:
+    """GPUs visible on this node, counted without initialising HIP (0 if torch is unavailable)."""
+    try:
+        import torch
+        return int(torch.cuda.device_count())
+    except Exception:  # noqa: BLE001 — CPU-only environments
+        return 0
+
+
+def default_procs(local_world: int) -> int:
+    """Consumer processes per rank: the CPU share of one GPU slot minus one, at most 16.
+
+    The share is the node's CPUs divided by the number of GPU slots on the node (at least the
+    local world size). It does not depend on how many ranks run, so per-rank work stays fixed
+    as N grows (weak scaling): on an 8-GPU node with 16 CPUs per GPU, N=1 and N=8 both run 15
+    consumers per rank.
+    """
+    slots = max(1, local_world, gpus_on_node())
+    return max(1, min(16, available_cpus() // slots - 1))
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=1, help="number of ranks (one process group member per GPU slot)")
@@ -86,7 +108,7 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--events-per-step", type=int, default=65536, help="events per step per consumer process")
     ap.add_argument("--procs-per-rank", type=int, default=0,
-                    help="consumer processes per rank (0 = min(16, CPUs per rank - 1))")
+                    help="consumer processes per rank (0 = min(16, CPUs per GPU slot - 1))")
     ap.add_argument("--media", type=int, default=10000)
     ap.add_argument("--log-level", default="info")
     ap.add_argument("--seed", type=int, default=0)
@@ -275,7 +297,7 @@ def main(argv=None) -> int:
     if dist.world == 1 and a.gpus > 1:
         print(f"bench.py: --gpus {a.gpus} requires torch.distributed.run; running 1 rank", file=sys.stderr)
         n = 1
-    procs = a.procs_per_rank or max(1, min(16, available_cpus() // max(1, dist.local_world) - 1))
+    procs = a.procs_per_rank or default_procs(dist.local_world)
     gc.collect()
     res = run_rank(a, dist, procs)
     dist.barrier()
@@ -312,6 +334,8 @@ def main(argv=None) -> int:
                 "parallelism": f"dp{n} x {procs} consumer procs/rank (competing consumers)",
             },
             "procs_per_rank": procs,
+            "cpus_available": available_cpus(),
+            "gpus_on_node": gpus_on_node(),
             "events_per_proc_per_sec": round(value / total_procs, 1),
             "p50_handle_latency_us": round(hh.percentile(50) / 1e3, 3),
             "p99_handle_latency_us": round(hh.percentile(99) / 1e3, 3),
