@@ -41,7 +41,7 @@ PyObject *s_ack, *s_message, *s_content, *s_mediaId, *s_status, *s_progress, *s_
     *s_throw, *s_close, *s_lists, *s_no_trello, *s_deployed, *s_trello_creator, *s_log, *s_decode_status,
     *s_decode_progress, *s_status_names_s, *s_status_names_p, *s_progress_counter, *s_comment_inc, *s_key,
     *s_token, *s_base_url, *s_http, *s_timeout, *s_strict, *s_stats, *s_request, *s_params, *s_POST, *s_PUT,
-    *s_record, *s_raise_for_status, *s_rows, *s_get_calls, *kw_params_timeout;
+    *s_record, *s_raise_for_status, *s_rows, *s_get_calls, *s_limiter, *s_retry, *kw_params_timeout;
 // log message literals (index.js:51,133,150)
 PyObject *m_progress, *m_status_kw, *m_percent, *m_creating, *m_with_text, *m_failed_progress, *m_failed_hooks;
 
@@ -355,6 +355,12 @@ int trello_request(CallObject* c, PyObject* method, PyObject* method_upper, PyOb
   bool fast = reinterpret_cast<PyObject*>(Py_TYPE(trello)) == hs->trello_cls;
   PyObject** dp = fast ? _PyObject_GetDictPtr(trello) : nullptr;
   PyObject* td = dp ? *dp : nullptr;
+  if (td) {  // a rate limit or 429 retries (sinks/ratelimit.py): the client's own make_request
+    PyObject* lim = PyDict_GetItemWithError(td, s_limiter);
+    PyObject* rty = !PyErr_Occurred() ? PyDict_GetItemWithError(td, s_retry) : nullptr;
+    if (PyErr_Occurred()) return -1;
+    if ((lim && lim != Py_None) || (rty && rty != Py_None)) td = nullptr;
+  }
   PyObject* query = PyDict_New();
   if (!query) return -1;
   if (td) {  // {"key": self.key, "token": self.token, **options}
@@ -1224,6 +1230,8 @@ int init_handler_types(PyObject* m) {
               {&s_raise_for_status, "raise_for_status"},
               {&s_rows, "_rows"},
               {&s_get_calls, "get_calls"},
+              {&s_limiter, "limiter"},
+              {&s_retry, "retry"},
               {&m_progress, "processing progress update on media"},
               {&m_status_kw, "status"},
               {&m_percent, "percent"},

@@ -42,6 +42,7 @@ from .metrics import MetricsServer, NativeHistogramView, Registry, default_metri
 from .metrics.registry import Gauge
 from .parallel.ordering import KeyedSerializer
 from .sinks import AiohttpClient, EmbyClient, H1Client, HttpClient, SinkObserver, TelegramClient, TrelloClient
+from .sinks.ratelimit import from_config as sink_policy
 from .store import MediaStore, open_store
 from .transport.base import Source
 from .ops import Driver, dispatch_batch
@@ -155,10 +156,15 @@ class Service:
             self.registry = Registry("beholder")
         reg = self.registry
         observer = SinkObserver(reg) if svc["metrics"].get("sink_metrics", True) else None
+        sinks = svc.get("sinks") or {}
+        tl, tr = sink_policy(sinks.get("trello"))  # opt-in rate limits / 429 retries (sinks/ratelimit.py)
+        gl, gr = sink_policy(sinks.get("telegram"))
+        el, er = sink_policy(sinks.get("emby"))
         self.trello = TrelloClient(keys.get("key"), keys.get("token"), self._http, base_url=endpoints["trello"],
-                                   observer=observer)
-        self.telegram = TelegramClient(None, self._http, base_url=endpoints["telegram"], observer=observer)
-        self.emby = EmbyClient(None, None, self._http, observer=observer)
+                                   observer=observer, limiter=tl, retry=tr)
+        self.telegram = TelegramClient(None, self._http, base_url=endpoints["telegram"], observer=observer,
+                                       limiter=gl, retry=gr)
+        self.emby = EmbyClient(None, None, self._http, observer=observer, limiter=el, retry=er)
 
         self.progress_updates_total = reg.counter(
             "beholder_progress_updates_total", "Total number of messages processed in this processes lifetime",
@@ -541,6 +547,12 @@ class Service:
                                "serialized": self.serializer.serialized, "max_chain": self.serializer.max_chain}
         if self.tracer is not None:
             out["tracing"] = self.tracer.reporter.stats()
+        limits = {name: c.limiter.stats() for name, c in (("trello", getattr(self, "trello", None)),
+                                                          ("telegram", getattr(self, "telegram", None)),
+                                                          ("emby", getattr(self, "emby", None)))
+                  if c is not None and c.limiter is not None}
+        if limits:
+            out["rate_limits"] = limits
         http_stats = getattr(self._http, "stats", None)
         if callable(http_stats):  # keep-alive pool accounting (sinks/h1.py)
             out["http"] = http_stats()

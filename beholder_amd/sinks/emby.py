@@ -4,12 +4,15 @@ from __future__ import annotations
 from typing import Any, Optional
 
 from .http import HttpClient, HttpResponse, observed, with_query
+from .ratelimit import guarded
 from ..utils.log import js_str
 
 
 class EmbyClient:
     def __init__(self, host: Optional[str], api_key: Optional[str], http: HttpClient, timeout: Optional[float] = None,
-                 observer=None):
+                 observer=None, limiter=None, retry=None):
+        self.limiter = limiter  # opt-in rate limit / 429 retries (sinks/ratelimit.py)
+        self.retry = retry
         self.host = host
         self.api_key = api_key
         self.http = http
@@ -21,5 +24,9 @@ class EmbyClient:
         k = self.api_key if api_key is ... else api_key
         url = f"{js_str(h)}/emby/library/refresh"
         full = with_query(url, {"api_key": k}, rfc3986=True)  # request `qs` -> qs 6.5 encoding
-        r = await observed(self.stats, self.http.request("GET", full, timeout=self.timeout))
+        if self.limiter is not None or self.retry is not None:
+            r = await guarded(self.limiter, self.retry,
+                              lambda: observed(self.stats, self.http.request("GET", full, timeout=self.timeout)))
+        else:
+            r = await observed(self.stats, self.http.request("GET", full, timeout=self.timeout))
         return r.raise_for_status()

@@ -4,6 +4,7 @@ from __future__ import annotations
 from typing import Any, Optional
 
 from .http import HttpClient, HttpResponse, observed, with_query
+from .ratelimit import guarded
 from ..utils.log import js_str
 
 
@@ -14,7 +15,9 @@ def deployed_text(name: Any, metadata_id: Any) -> str:
 
 class TelegramClient:
     def __init__(self, token: Optional[str], http: HttpClient, base_url: str = "https://api.telegram.org",
-                 timeout: Optional[float] = None, observer=None):
+                 timeout: Optional[float] = None, observer=None, limiter=None, retry=None):
+        self.limiter = limiter  # opt-in rate limit / 429 retries (sinks/ratelimit.py)
+        self.retry = retry
         self.token = token
         self.http = http
         self.base_url = base_url.rstrip("/")
@@ -28,5 +31,9 @@ class TelegramClient:
         url = f"{self.base_url}/bot{js_str(tok)}/sendMessage"
         # request-promise `qs` option -> qs 6.5 (RFC 3986 strict) query encoding
         full = with_query(url, {"chat_id": chat_id, "text": text, "parse_mode": parse_mode}, rfc3986=True)
-        r = await observed(self.stats, self.http.request("GET", full, timeout=self.timeout))
+        if self.limiter is not None or self.retry is not None:
+            r = await guarded(self.limiter, self.retry,
+                              lambda: observed(self.stats, self.http.request("GET", full, timeout=self.timeout)))
+        else:
+            r = await observed(self.stats, self.http.request("GET", full, timeout=self.timeout))
         return r.raise_for_status()  # request-promise: reject on non-2xx

@@ -17,6 +17,7 @@ import time
 from typing import Any, Mapping, Optional
 
 from .http import HttpClient, HttpError, HttpResponse
+from .ratelimit import guarded
 
 COMMENT_FALLBACK = "Failed to retrieve comment text."  # index.js:54
 
@@ -26,7 +27,9 @@ _METHODS = {"get": "GET", "post": "POST", "put": "PUT", "delete": "DELETE"}
 class TrelloClient:
     def __init__(self, key: Optional[str], token: Optional[str], http: HttpClient,
                  base_url: str = "https://api.trello.com", strict: bool = False, timeout: Optional[float] = None,
-                 observer=None):
+                 observer=None, limiter=None, retry=None):
+        self.limiter = limiter  # opt-in rate limit / 429 retries (sinks/ratelimit.py)
+        self.retry = retry
         self.key = key
         self.token = token
         self.http = http
@@ -47,19 +50,25 @@ class TrelloClient:
             raise HttpError("Path must start with /")
         query = {"key": self.key, "token": self.token, **options} if options else \
             {"key": self.key, "token": self.token}
-        stats = self.stats
-        if stats is None:
-            r = await self.http.request(m, self.base_url + path, params=query, timeout=self.timeout)
+        if self.limiter is not None or self.retry is not None:
+            r = await guarded(self.limiter, self.retry, lambda: self._send(m, path, query))
         else:
-            t0 = time.perf_counter()
-            try:
-                r = await self.http.request(m, self.base_url + path, params=query, timeout=self.timeout)
-            except Exception:
-                stats.record(None, time.perf_counter() - t0)
-                raise
-            stats.record(r.status, time.perf_counter() - t0)
+            r = await self._send(m, path, query)
         if self.strict:
             r.raise_for_status()
+        return r
+
+    async def _send(self, m: str, path: str, query: dict) -> HttpResponse:
+        stats = self.stats
+        if stats is None:
+            return await self.http.request(m, self.base_url + path, params=query, timeout=self.timeout)
+        t0 = time.perf_counter()
+        try:
+            r = await self.http.request(m, self.base_url + path, params=query, timeout=self.timeout)
+        except Exception:
+            stats.record(None, time.perf_counter() - t0)
+            raise
+        stats.record(r.status, time.perf_counter() - t0)
         return r
 
     makeRequest = make_request  # noqa: N815 (reference name)
