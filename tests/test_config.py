@@ -90,3 +90,20 @@ def test_repo_has_no_unused_imports():
     r = subprocess.run([sys.executable, os.path.join(root, "scripts", "lint.py"), "beholder_amd", "tests",
                         "bench.py", "__graft_entry__.py", "scripts"], capture_output=True, text=True, cwd=root)
     assert r.returncode == 0, r.stdout
+
+
+def test_kubernetes_example_config_loads(tmp_path):
+    """deploy/kubernetes.yaml: the ConfigMap's events.yaml plus the Secret's env overrides make a
+    valid config (keys reach the reference's key paths, index.js:25,100,110,115)."""
+    import os
+    import yaml
+    from beholder_amd.config import Config
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    docs = list(yaml.safe_load_all(open(os.path.join(root, "deploy", "kubernetes.yaml"))))
+    cm = next(d for d in docs if d["kind"] == "ConfigMap")
+    secret = next(d for d in docs if d["kind"] == "Secret")
+    (tmp_path / "events.yaml").write_text(cm["data"]["events.yaml"])
+    cfg = Config.load("events", path=str(tmp_path / "events.yaml"), env=dict(secret["stringData"]))
+    assert cfg.root.require("keys.trello").get("token") == "<trello token>"
+    assert cfg.keys.emby.token == "<emby api key>" and cfg.flow_ids["deployed"] == "<list id>"
+    assert cfg.data["service"]["prefetch"] == 100
