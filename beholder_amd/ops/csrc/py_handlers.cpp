@@ -41,7 +41,8 @@ PyObject *s_ack, *s_message, *s_content, *s_mediaId, *s_status, *s_progress, *s_
     *s_throw, *s_close, *s_lists, *s_no_trello, *s_deployed, *s_trello_creator, *s_log, *s_decode_status,
     *s_decode_progress, *s_status_names_s, *s_status_names_p, *s_progress_counter, *s_comment_inc, *s_key,
     *s_token, *s_base_url, *s_http, *s_timeout, *s_strict, *s_stats, *s_request, *s_params, *s_POST, *s_PUT,
-    *s_record, *s_raise_for_status, *s_rows, *s_get_calls, *s_limiter, *s_retry, *kw_params_timeout;
+    *s_record, *s_raise_for_status, *s_rows, *s_get_calls, *s_update_calls, *s_limiter, *s_retry,
+    *kw_params_timeout;
 // log message literals (index.js:51,133,150)
 PyObject *m_progress, *m_status_kw, *m_percent, *m_creating, *m_with_text, *m_failed_progress, *m_failed_hooks;
 
@@ -287,6 +288,59 @@ int get_media(CallObject* c, PyObject** out) {
   PyObject* aw = PyObject_CallMethodOneArg(store, s_get_by_id, c->media_id);
   if (!aw) return -1;
   return await_start(c, aw, out);
+}
+
+// db.updateStatus(mediaId, status) on the stock in-memory store, inline (store/memory.py
+// update_status_nowait: count the call, replace the row with status = int(status)).
+// 1 = done, 0 = not the stock store (caller uses the store's API), -1 = raised.
+int update_inline(CallObject* c) {
+  HandlersObject* hs = c->hs;
+  PyObject* store = hattr(hs, s_store);
+  if (!store) return -1;
+  if (reinterpret_cast<PyObject*>(Py_TYPE(store)) != hs->memory_cls || !hs->media_cls ||
+      !PyLong_CheckExact(c->status))
+    return 0;
+  PyObject** dp = _PyObject_GetDictPtr(store);
+  PyObject* sd = dp ? *dp : nullptr;
+  PyObject* rows = sd ? PyDict_GetItemWithError(sd, s_rows) : nullptr;
+  PyObject* calls = rows ? PyDict_GetItemWithError(sd, s_update_calls) : nullptr;
+  if (!calls || !PyDict_CheckExact(rows)) return PyErr_Occurred() ? -1 : 0;
+  PyObject* n = PyNumber_Add(calls, hs->one);  // self.update_calls += 1
+  if (!n) return -1;
+  int rc = PyDict_SetItem(sd, s_update_calls, n);
+  Py_DECREF(n);
+  if (rc < 0) return -1;
+  PyObject* m = PyDict_GetItemWithError(rows, c->media_id);
+  if (!m) return PyErr_Occurred() ? -1 : 1;  // unknown media: nothing to update
+  if (reinterpret_cast<PyObject*>(Py_TYPE(m)) != hs->media_cls) {  // foreign row type: m._replace(status=...)
+    PyObject* kw = Py_BuildValue("{s:O}", "status", c->status);
+    PyObject* meth = kw ? PyObject_GetAttrString(m, "_replace") : nullptr;
+    PyObject* nm = meth ? PyObject_Call(meth, PyTuple_New(0), kw) : nullptr;
+    Py_XDECREF(meth);
+    Py_XDECREF(kw);
+    if (!nm) return -1;
+    rc = PyDict_SetItem(rows, c->media_id, nm);
+    Py_DECREF(nm);
+    return rc < 0 ? -1 : 1;
+  }
+  // Media is a NamedTuple: a copy with the status slot replaced, same type
+  Py_ssize_t len = PyTuple_GET_SIZE(m);
+  PyObject* items = PyTuple_New(len);
+  if (!items) return -1;
+  for (Py_ssize_t i = 0; i < len; ++i) {
+    PyObject* v = i == hs->ix_m[2] ? c->status : PyTuple_GET_ITEM(m, i);
+    Py_INCREF(v);
+    PyTuple_SET_ITEM(items, i, v);
+  }
+  PyObject* args = PyTuple_Pack(1, items);
+  Py_DECREF(items);
+  if (!args) return -1;
+  PyObject* nm = PyTuple_Type.tp_new(reinterpret_cast<PyTypeObject*>(hs->media_cls), args, nullptr);
+  Py_DECREF(args);
+  if (!nm) return -1;
+  rc = PyDict_SetItem(rows, c->media_id, nm);
+  Py_DECREF(nm);
+  return rc < 0 ? -1 : 1;
 }
 
 bool record_stats(PyObject* stats, PyObject* status, double seconds) {
@@ -602,7 +656,10 @@ PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
       bool ok = log_line(hs, 30, &line, 1);
       Py_DECREF(line);
       if (!ok) return fail(c);
-      PyObject* upd = hattr(hs, s_update_nowait);  // index.js:68
+      int inl = update_inline(c);  // index.js:68
+      if (inl < 0) return fail(c);
+      if (inl) goto updated;
+      PyObject* upd = hattr(hs, s_update_nowait);
       if (!upd) return fail(c);
       if (upd != Py_None) {
         PyObject* args[2] = {c->media_id, c->status};
@@ -1230,6 +1287,7 @@ int init_handler_types(PyObject* m) {
               {&s_raise_for_status, "raise_for_status"},
               {&s_rows, "_rows"},
               {&s_get_calls, "get_calls"},
+              {&s_update_calls, "update_calls"},
               {&s_limiter, "limiter"},
               {&s_retry, "retry"},
               {&m_progress, "processing progress update on media"},
