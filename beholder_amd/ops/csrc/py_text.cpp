@@ -379,13 +379,15 @@ struct LogSinkObject {
   PyObject* flush_cb;
   std::string* buf;
   size_t limit;
+  bool binary;  // write() takes bytes (UTF-8): no decode here and no encode in a text layer
   unsigned long long counts[7];  // trace..fatal by level/10 - 1, [6] other
   unsigned long long bytes;
 };
 
 int sink_drain(LogSinkObject* self) {
   if (self->buf->empty()) return 0;
-  PyObject* s = PyUnicode_DecodeUTF8(self->buf->data(), Py_ssize_t(self->buf->size()), "replace");
+  PyObject* s = self->binary ? PyBytes_FromStringAndSize(self->buf->data(), Py_ssize_t(self->buf->size()))
+                             : PyUnicode_DecodeUTF8(self->buf->data(), Py_ssize_t(self->buf->size()), "replace");
   self->bytes += self->buf->size();
   self->buf->clear();
   if (!s) return -1;
@@ -403,17 +405,21 @@ PyObject* sink_new(PyTypeObject* type, PyObject*, PyObject*) {
   self->flush_cb = nullptr;
   self->buf = new std::string();
   self->limit = 65536;
+  self->binary = false;
   memset(self->counts, 0, sizeof self->counts);
   self->bytes = 0;
   return reinterpret_cast<PyObject*>(self);
 }
 
 int sink_init(LogSinkObject* self, PyObject* args, PyObject* kwds) {
-  static const char* kwlist[] = {"write", "flush", "buffer_bytes", nullptr};
+  static const char* kwlist[] = {"write", "flush", "buffer_bytes", "binary", nullptr};
   PyObject* w;
   PyObject* f = Py_None;
   Py_ssize_t lim = 65536;
-  if (!PyArg_ParseTupleAndKeywords(args, kwds, "O|On", const_cast<char**>(kwlist), &w, &f, &lim)) return -1;
+  int binary = 0;
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "O|Onp", const_cast<char**>(kwlist), &w, &f, &lim, &binary))
+    return -1;
+  self->binary = binary != 0;
   if (!PyCallable_Check(w)) {
     PyErr_SetString(PyExc_TypeError, "write must be callable");
     return -1;
@@ -497,11 +503,12 @@ PyObject* sink_emit_impl(LogSinkObject* self, PyObject* const* a, Py_ssize_t n) 
   Py_RETURN_NONE;
 }
 
-// retarget(write, flush=None): flush, then send future lines elsewhere
+// retarget(write, flush=None, binary=False): flush, then send future lines elsewhere
 PyObject* sink_retarget(LogSinkObject* self, PyObject* args) {
   PyObject* w;
   PyObject* f = Py_None;
-  if (!PyArg_ParseTuple(args, "O|O", &w, &f)) return nullptr;
+  int binary = 0;
+  if (!PyArg_ParseTuple(args, "O|Op", &w, &f, &binary)) return nullptr;
   if (!PyCallable_Check(w)) {
     PyErr_SetString(PyExc_TypeError, "write must be callable");
     return nullptr;
@@ -509,6 +516,7 @@ PyObject* sink_retarget(LogSinkObject* self, PyObject* args) {
   if (sink_drain(self) < 0) return nullptr;
   Py_INCREF(w);
   Py_XSETREF(self->write, w);
+  self->binary = binary != 0;
   if (f == Py_None) {
     Py_CLEAR(self->flush_cb);
   } else {
@@ -539,7 +547,8 @@ PyMethodDef sink_methods[] = {
     {"emit", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(sink_emit)), METH_FASTCALL,
      "emit(level, prefix, extra, args): format one pino line into the buffer"},
     {"flush", reinterpret_cast<PyCFunction>(sink_flush), METH_NOARGS, "write out buffered lines"},
-    {"retarget", reinterpret_cast<PyCFunction>(sink_retarget), METH_VARARGS, "retarget(write, flush=None)"},
+    {"retarget", reinterpret_cast<PyCFunction>(sink_retarget), METH_VARARGS,
+     "retarget(write, flush=None, binary=False)"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyGetSetDef sink_getset[] = {
@@ -870,7 +879,9 @@ int init_text_functions(PyObject* m) {
   LogSinkType.tp_name = "beholder_amd.ops._native.LogSink";
   LogSinkType.tp_basicsize = sizeof(LogSinkObject);
   LogSinkType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC;
-  LogSinkType.tp_doc = "LogSink(write, flush=None, buffer_bytes=65536): buffered pino JSON-lines writer";
+  LogSinkType.tp_doc =
+      "LogSink(write, flush=None, buffer_bytes=65536, binary=False): buffered pino JSON-lines writer "
+      "(binary: write() gets UTF-8 bytes)";
   LogSinkType.tp_new = sink_new;
   LogSinkType.tp_init = reinterpret_cast<initproc>(sink_init);
   LogSinkType.tp_dealloc = reinterpret_cast<destructor>(sink_dealloc);

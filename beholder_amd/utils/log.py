@@ -21,6 +21,7 @@ message text matches the reference's template literals (``45`` not ``45.0``,
 """
 from __future__ import annotations
 
+import codecs
 import json
 import math
 import os
@@ -169,6 +170,27 @@ from ..ops import native as _native  # noqa: E402  (after js_str: ops configures
 _native.configure_text(js_str, lambda v: json.dumps(v, separators=(",", ":"), ensure_ascii=False, default=js_str))
 
 
+def _writer(stream):
+    """``(write, binary)`` for the native sink. A UTF-8 text file with a binary buffer
+    (``sys.stdout``, ``open(path, "w")``) takes the formatted bytes directly. The text layer is
+    flushed first, so lines never reorder against other writers of the same stream. Anything
+    else gets ``str`` through its own ``write``."""
+    raw = getattr(stream, "buffer", None)
+    enc = getattr(stream, "encoding", None)
+    try:
+        utf8 = enc is not None and codecs.lookup(enc).name == "utf-8"
+    except LookupError:
+        utf8 = False
+    if raw is None or not utf8 or not callable(getattr(raw, "write", None)):
+        return stream.write, False
+    text_flush, raw_write = stream.flush, raw.write
+
+    def write(data: bytes) -> int:
+        text_flush()
+        return raw_write(data)
+    return write, True
+
+
 class _Shared:
     """State shared by a logger and its children: one native sink, one stream."""
 
@@ -178,7 +200,8 @@ class _Shared:
         self.stream = stream
         self.pid = os.getpid()
         self.hostname = socket.gethostname()
-        self.sink = _native.LogSink(stream.write, getattr(stream, "flush", None), buffer_bytes)
+        write, binary = _writer(stream)
+        self.sink = _native.LogSink(write, getattr(stream, "flush", None), buffer_bytes, binary)
 
 
 class Logger(_native.LogCore):
@@ -228,7 +251,8 @@ class Logger(_native.LogCore):
     @stream.setter
     def stream(self, s: TextIO) -> None:
         self._shared.stream = s
-        self._shared.sink.retarget(s.write, getattr(s, "flush", None))
+        write, binary = _writer(s)
+        self._shared.sink.retarget(write, getattr(s, "flush", None), binary)
 
     @property
     def counts(self) -> Dict[str, int]:

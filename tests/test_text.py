@@ -1,4 +1,5 @@
 """Native JS-semantics text helpers vs their Python reference implementations."""
+import io
 import json
 import math
 import random
@@ -88,3 +89,23 @@ def test_native_log_line_matches_python_formatter():
         want = lg.py_line(30, args, time_ms=1234)
         got = native.format_line(30, 1234, lg._prefix, None, args)
         assert got == want, args
+
+
+def test_logger_writes_utf8_bytes_to_files_in_order(tmp_path):
+    """A UTF-8 text file gets the formatted bytes directly (no decode/encode round trip);
+    text written to the same stream between flushes stays in order."""
+    from beholder_amd.utils.log import Logger, _writer
+    p = tmp_path / "log.jsonl"
+    with open(p, "w", encoding="utf-8") as f:
+        assert _writer(f)[1] is True
+        log = Logger(stream=f)
+        log.info("first ü", 1)
+        log.flush()
+        f.write("between\n")
+        log.info("second", "✓")
+        log.flush()
+    lines = p.read_text(encoding="utf-8").splitlines()
+    assert [json.loads(lines[0])["msg"], lines[1], json.loads(lines[2])["msg"]] == ["first ü 1", "between", "second ✓"]
+    with open(tmp_path / "latin.txt", "w", encoding="latin-1") as g:
+        assert _writer(g)[1] is False  # other encodings keep the text path
+    assert _writer(io.StringIO())[1] is False
