@@ -163,10 +163,30 @@ bool js_str_append(std::string& out, PyObject* v) {
 }
 
 // JSON string body escaping, json.dumps(ensure_ascii=False) compatible.
+// true when one of the 8 bytes of `w` is < 0x20, '"' or '\\' (SWAR; bytes >= 0x80 never match)
+inline bool word_needs_escape(uint64_t w) {
+  constexpr uint64_t ones = 0x0101010101010101ULL, highs = 0x8080808080808080ULL;
+  uint64_t ctl = (w - ones * 0x20) & ~w & highs;
+  uint64_t q = w ^ (ones * '"'), b = w ^ (ones * '\\');
+  uint64_t quote = (q - ones) & ~q & highs, bslash = (b - ones) & ~b & highs;
+  return (ctl | quote | bslash) != 0;
+}
+
 void json_escape_append(std::string& out, const char* s, size_t n) {
   static const char* hex = "0123456789abcdef";
+  size_t i = 0;
+  while (i + 8 <= n) {  // clean prefix, 8 bytes at a time (the common case: nothing to escape)
+    uint64_t w;
+    memcpy(&w, s + i, 8);
+    if (word_needs_escape(w)) break;
+    i += 8;
+  }
+  if (i == n) {
+    out.append(s, n);
+    return;
+  }
   size_t run = 0;
-  for (size_t i = 0; i < n; ++i) {
+  for (; i < n; ++i) {
     unsigned char c = static_cast<unsigned char>(s[i]);
     if (c >= 0x20 && c != '"' && c != '\\') continue;
     out.append(s + run, i - run);

@@ -109,3 +109,17 @@ def test_logger_writes_utf8_bytes_to_files_in_order(tmp_path):
     with open(tmp_path / "latin.txt", "w", encoding="latin-1") as g:
         assert _writer(g)[1] is False  # other encodings keep the text path
     assert _writer(io.StringIO())[1] is False
+
+
+@settings(max_examples=400, deadline=None)
+@given(st.lists(st.one_of(st.text(alphabet=st.characters(min_codepoint=0, max_codepoint=0x2FF,
+                                                         blacklist_categories=("Cs",)), max_size=40),
+                          st.integers(-10**6, 10**6)), min_size=1, max_size=4))
+def test_native_log_line_escaping_matches_json(args):
+    """JSON escaping (8-byte SWAR scan + per-byte tail) equals json.dumps for any text: control
+    characters, quotes and backslashes at every offset, multi-byte UTF-8."""
+    from beholder_amd.ops import native
+    from beholder_amd.utils.log import Logger, NullStream
+    lg = Logger(stream=NullStream())
+    args = tuple(args) if isinstance(args[0], str) else ("x",) + tuple(args)
+    assert native.format_line(30, 1234, lg._prefix, None, args) == lg.py_line(30, args, time_ms=1234)
