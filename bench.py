@@ -28,9 +28,9 @@ consumers report their K steps done, then passes another gloo barrier. The
 elapsed time is the MAX over ranks and ``value`` is whole-job events/s.
 Per-consumer work is fixed as N grows: weak scaling. The service has no
 device work (the reference has none), so nothing runs on the GPU. The
-timed region is bracketed by barriers, but not by torch.cuda.synchronize():
-no kernel is ever queued, and initialising HIP in a rank process that then
-spawns consumer processes would only add start-up cost.
+timed region is bracketed by the barriers and by torch.cuda.synchronize()
+(no kernel is ever queued). HIP is initialised in a rank process only after
+its consumer processes have been spawned.
 
 Prints ONE JSON line on rank 0.
 """
@@ -118,6 +118,34 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+class _Device:
+    """``torch.cuda.synchronize()`` around the timed region, as the driver contract asks.
+
+    The service queues no device work, so this only orders the (empty) stream. HIP is
+    initialised lazily on the first :meth:`sync`. Callers make that happen only after every
+    consumer process has been spawned, because a process that initialised the GPU must not start
+    programs (spawn = fork + exec).
+    """
+
+    def __init__(self, local_rank: int):
+        self.local_rank = local_rank
+        self._torch = None
+        self._ready = False
+
+    def sync(self) -> None:
+        if not self._ready:
+            self._ready = True
+            try:
+                import torch
+                if torch.cuda.device_count() > 0 and torch.cuda.is_available():
+                    torch.cuda.set_device(self.local_rank % torch.cuda.device_count())
+                    self._torch = torch
+            except Exception:  # noqa: BLE001 — CPU-only environments: nothing to synchronize
+                self._torch = None
+        if self._torch is not None:
+            self._torch.cuda.synchronize()
+
+
 class _Dist:
     """gloo process group when launched under torch.distributed.run, no-op otherwise."""
 
@@ -156,8 +184,8 @@ class _Dist:
             self.dist.destroy_process_group()
 
 
-async def run_consumer(a, seed: int, go) -> dict:
-    """One consumer process: build the service, warm up, ``go()``, time K steps."""
+async def run_consumer(a, seed: int, go, stop=None) -> dict:
+    """One consumer process: build the service, warm up, ``go()``, time K steps, ``stop()``."""
     from beholder_amd.bench.generator import Workload, bench_config
     from beholder_amd.config import Config
     from beholder_amd.service import Service
@@ -211,6 +239,8 @@ async def run_consumer(a, seed: int, go) -> dict:
         th = write_step(i)
         await wait_settled((i + 1) * E)
         th.join()
+    if stop is not None:
+        stop()
     elapsed = time.perf_counter() - t0
     os.close(wfd)
     await run_task
@@ -250,10 +280,12 @@ def _consumer_entry(a, seed, barrier, results, cpu=None):
 def run_rank(a, dist: _Dist, procs: int) -> dict:
     """Coordinator for one rank's consumer processes; returns the rank's merged result."""
     base_seed = a.seed + 7919 * dist.rank
-    if procs == 1:
+    dev = _Device(dist.local_rank)
+    if procs == 1:  # the consumer runs in this process, which starts no other program
         def go():
             dist.barrier()
-        res = asyncio.run(run_consumer(a, base_seed, go))
+            dev.sync()
+        res = asyncio.run(run_consumer(a, base_seed, go, dev.sync))
         res["procs"] = 1
         return res
     ctx = mp.get_context("spawn")
@@ -268,11 +300,13 @@ def run_rank(a, dist: _Dist, procs: int) -> dict:
                             daemon=True) for i in range(procs)]
     for c in children:
         c.start()
-    barrier.wait()          # every consumer has warmed up
+    barrier.wait()          # every consumer has warmed up (all spawned: HIP may be initialised now)
     dist.barrier()          # ... on every rank
+    dev.sync()
     t0 = time.perf_counter()
     # releasing the barrier is the consumers' go signal (they were parked in it)
     got = [results.get() for _ in range(procs)]
+    dev.sync()
     t1 = time.perf_counter()
     for c in children:
         c.join(60)
