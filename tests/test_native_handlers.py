@@ -11,8 +11,8 @@ the same observable trace:
 * HTTP requests (method + full URL, in order);
 * counter values and the store contents.
 
-Stores and sinks that really suspend exercise the native state machine's resume
-points. Concurrent runs (asyncio.gather) check that suspension interleaves identically.
+Stores and sinks that really suspend (an awaiting store, an HTTP recorder with latency) exercise
+the native state machine's resume points. Concurrent runs (asyncio.gather) check that suspension interleaves identically.
 """
 from __future__ import annotations
 
@@ -27,6 +27,7 @@ from hypothesis import HealthCheck, given, settings, strategies as st
 import helpers
 from beholder_amd.handlers import native_handlers
 from beholder_amd.ops import native
+from beholder_amd.sinks import RecordingHttpClient
 from beholder_amd.store import Media, MemoryStore
 from helpers import Rig, cfg, progress_msg, status_msg
 
@@ -91,10 +92,11 @@ def _encode(ev):
     return progress_msg(ev[1], ev[2], ev[3], ev[4])
 
 
-def run_trace(impl, config, no_trello, rows, evs, fault_list, store_kind, concurrent):
+def run_trace(impl, config, no_trello, rows, evs, fault_list, store_kind, concurrent, http_delay=0.0):
     helpers.HANDLER_IMPL = impl
     try:
-        r = Rig(config=config, medias=rows, no_trello=no_trello)
+        r = Rig(config=config, medias=rows, no_trello=no_trello,
+                http=RecordingHttpClient(delay_s=http_delay) if http_delay else None)
     finally:
         helpers.HANDLER_IMPL = "python"
     r.h.store = STORES[store_kind](list(rows))
@@ -132,11 +134,12 @@ def run_trace(impl, config, no_trello, rows, evs, fault_list, store_kind, concur
 @settings(max_examples=int(os.environ.get("BEHOLDER_FUZZ_EXAMPLES", "300")), deadline=None,
           suppress_health_check=[HealthCheck.too_slow])
 @given(config=configs, no_trello=st.booleans(), rows=medias, evs=events, fault_list=faults,
-       store_kind=st.sampled_from(sorted(STORES)), concurrent=st.booleans())
-def test_native_matches_python(config, no_trello, rows, evs, fault_list, store_kind, concurrent):
+       store_kind=st.sampled_from(sorted(STORES)), concurrent=st.booleans(),
+       http_delay=st.sampled_from([0.0, 0.0, 0.0005]))
+def test_native_matches_python(config, no_trello, rows, evs, fault_list, store_kind, concurrent, http_delay):
     c = cfg(config)
     c.data["instance"]["flow_ids"] = config["instance"]["flow_ids"]  # replace, not merge, the list map
-    args = (c, no_trello, rows, evs, fault_list, store_kind, concurrent)
+    args = (c, no_trello, rows, evs, fault_list, store_kind, concurrent, http_delay)
     assert run_trace("native", *args) == run_trace("python", *args)
 
 
