@@ -27,6 +27,7 @@
 namespace beholder {
 
 bool text_js_str_append(std::string& out, PyObject* v);
+bool text_query_pair_append(std::string& out, PyObject* k, PyObject* v, bool* first, bool rfc3986);
 bool is_native_logger(PyObject* logger);
 bool logcore_emit(PyObject* logger, bool native, long lvl, PyObject* const* args, Py_ssize_t nargs);
 bool sink_stats_record(PyObject* stats, PyObject* status, double seconds);
@@ -42,7 +43,8 @@ PyObject *s_ack, *s_message, *s_content, *s_mediaId, *s_status, *s_progress, *s_
     *s_decode_progress, *s_status_names_s, *s_status_names_p, *s_progress_counter, *s_comment_inc, *s_key,
     *s_token, *s_base_url, *s_http, *s_timeout, *s_strict, *s_stats, *s_request, *s_params, *s_POST, *s_PUT,
     *s_record, *s_raise_for_status, *s_rows, *s_get_calls, *s_update_calls, *s_limiter, *s_retry,
-    *kw_params_timeout;
+    *s_hooks_plan, *s_telegram, *s_emby, *s_name, *s_metadataId, *s_GET, *s_chat_id, *s_parse_mode,
+    *s_markdown, *s_api_key, *s_send_message, *s_refresh_library, *kw_params_timeout, *kw_timeout;
 // log message literals (index.js:51,133,150)
 PyObject *m_progress, *m_status_kw, *m_percent, *m_creating, *m_with_text, *m_failed_progress, *m_failed_hooks;
 
@@ -71,6 +73,8 @@ struct HandlersObject {
   PyObject* media_cls;      // store.base.Media (a NamedTuple)
   Py_ssize_t ix_m[3];       // Media slots: creator, creatorId, status
   PyObject* trello_cls;     // sinks.trello.TrelloClient (exact type: request built here)
+  PyObject* telegram_cls;   // sinks.telegram.TelegramClient (exact type: request built here)
+  PyObject* emby_cls;       // sinks.emby.EmbyClient (exact type: request built here)
   PyObject* memory_cls;     // store.memory.MemoryStore (exact type: row read here)
   PyObject* not_found;      // store.base.MediaNotFound
   PyObject* one;            // TRELLO_CREATOR (index.js:79)
@@ -93,9 +97,10 @@ struct CallObject {
   PyObject* progress;
   PyObject* host;
   PyObject* media;
-  PyObject* req_stats;  // sink stats of the Trello request in flight (native path), may be NULL
+  PyObject* plan;       // DEPLOYED-hooks plan (handlers._hooks_plan()) while the hooks run natively
+  PyObject* req_stats;  // sink stats of the request in flight (native path), may be NULL
   int64_t req_t0;
-  uint8_t req_native;   // a Trello request built here is in flight: trello_finish() applies
+  uint8_t req_native;   // a sink request built here is in flight: request_finish() applies
   uint8_t req_strict;
   uint8_t kind;
   uint8_t state;
@@ -354,9 +359,10 @@ bool record_stats(PyObject* stats, PyObject* status, double seconds) {
   return true;
 }
 
-// Completes a Trello request issued on the native path (sinks/trello.py make_request after its
-// await): per-sink stats, strict mode. Takes and returns the result reference; NULL = raised.
-PyObject* trello_finish(CallObject* c, PyObject* value) {
+// Completes a sink request issued on the native path (after its await): per-sink stats, then
+// strict mode (Trello's `strict`; Telegram / Emby always raise_for_status, like request-promise).
+// Takes and returns the result reference; NULL = raised.
+PyObject* request_finish(CallObject* c, PyObject* value) {
   if (!c->req_native) return value;
   c->req_native = 0;
   PyObject* stats = c->req_stats;
@@ -400,7 +406,7 @@ PyObject* trello_finish(CallObject* c, PyObject* value) {
 
 // await trello.makeRequest(method, path, {keys[i]: vals[i]}). For the stock TrelloClient the
 // request is built here: query {key, token, ...options} handed to http.request, as
-// sinks/trello.py does, with stats recorded by trello_finish().
+// sinks/trello.py does, with stats recorded by request_finish().
 int trello_request(CallObject* c, PyObject* method, PyObject* method_upper, PyObject* path, PyObject* const* keys,
                    PyObject* const* vals, int nopt, PyObject** out) {
   HandlersObject* hs = c->hs;
@@ -484,11 +490,176 @@ int trello_request(CallObject* c, PyObject* method, PyObject* method_upper, PyOb
   }
   int k = aw ? await_start(c, aw, out) : -1;
   if (k != 0) {  // finished (or failed) without suspending
-    PyObject* v = trello_finish(c, k == 1 ? *out : nullptr);
+    PyObject* v = request_finish(c, k == 1 ? *out : nullptr);
     if (!v) return -1;
     *out = v;
   }
   return k;
+}
+
+// Stock Telegram / Emby client without a rate limit or retry policy: its instance dict, else NULL.
+PyObject* plain_client_dict(PyObject* client, PyObject* cls) {
+  if (reinterpret_cast<PyObject*>(Py_TYPE(client)) != cls) return nullptr;
+  PyObject** dp = _PyObject_GetDictPtr(client);
+  PyObject* d = dp ? *dp : nullptr;
+  if (!d) return nullptr;
+  PyObject* lim = PyDict_GetItemWithError(d, s_limiter);
+  PyObject* rty = PyDict_GetItemWithError(d, s_retry);
+  if (PyErr_Occurred()) {
+    PyErr_Clear();
+    return nullptr;
+  }
+  if ((lim && lim != Py_None) || (rty && rty != Py_None)) return nullptr;
+  return d;
+}
+
+// `await observed(stats, http.request("GET", with_query(url, pairs, rfc3986=True), timeout=...))`
+// then raise_for_status() in request_finish: sinks/telegram.py send_message, sinks/emby.py
+// refresh_library. `url` is the base URL text; `cd` the client's instance dict.
+int sink_get(CallObject* c, PyObject* cd, std::string& url, PyObject* const* keys, PyObject* const* vals, int n,
+             PyObject** out) {
+  std::string q;
+  bool first = true;
+  for (int i = 0; i < n; ++i)
+    if (!text_query_pair_append(q, keys[i], vals[i], &first, true)) return -1;
+  if (!q.empty()) {
+    url += url.find('?') == std::string::npos ? '?' : '&';
+    url += q;
+  }
+  PyObject* http = PyDict_GetItemWithError(cd, s_http);
+  PyObject* timeout = http ? PyDict_GetItemWithError(cd, s_timeout) : nullptr;
+  PyObject* stats = timeout ? PyDict_GetItemWithError(cd, s_stats) : nullptr;
+  if (!stats) {
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_AttributeError, "sink client attributes missing");
+    return -1;
+  }
+  PyObject* held[3] = {http, timeout, stats};
+  for (PyObject* o : held) Py_INCREF(o);
+  struct Release {
+    PyObject** objs;
+    ~Release() {
+      for (int i = 0; i < 3; ++i) Py_DECREF(objs[i]);
+    }
+  } release{held};
+  PyObject* full = unicode_from(url);
+  if (!full) return -1;
+  PyObject* args[4] = {http, s_GET, full, timeout};
+  PyObject* aw = PyObject_VectorcallMethod(s_request, args, 3, kw_timeout);  // http.request("GET", full, timeout=)
+  Py_DECREF(full);
+  c->req_t0 = mono_ns();
+  c->req_native = 1;
+  c->req_strict = 1;
+  if (stats != Py_None) {
+    Py_INCREF(stats);
+    c->req_stats = stats;
+  }
+  int k = aw ? await_start(c, aw, out) : -1;
+  if (k != 0) {
+    PyObject* v = request_finish(c, k == 1 ? *out : nullptr);
+    if (!v) return -1;
+    *out = v;
+  }
+  return k;
+}
+
+// Telegram step of the DEPLOYED hooks (index.js:97-107). 2 = nothing to send, else as await_start.
+int hook_telegram(CallObject* c, PyObject** out) {
+  HandlersObject* hs = c->hs;
+  PyObject* plan = c->plan;
+  int on = PyObject_IsTrue(PyTuple_GET_ITEM(plan, 0));
+  if (on <= 0) return on < 0 ? -1 : 2;
+  std::string line = "informing telegram that media '";
+  if (!text_js_str_append(line, c->media_id)) return -1;
+  line += "' is available";
+  PyObject* lo = unicode_from(line);
+  bool ok = lo && log_line(hs, 30, &lo, 1);
+  Py_XDECREF(lo);
+  if (!ok) return -1;
+  // arguments in the order Python evaluates them: chat_id, deployed_text(name, metadataId), token
+  PyObject* name = PyObject_GetAttr(c->media, s_name);
+  PyObject* meta = name ? PyObject_GetAttr(c->media, s_metadataId) : nullptr;
+  std::string text = "*New Anime:* ";
+  ok = meta && text_js_str_append(text, name);
+  text += "\nKitsu: https://kitsu.io/anime/";
+  ok = ok && text_js_str_append(text, meta);
+  Py_XDECREF(name);
+  Py_XDECREF(meta);
+  if (!ok) return -1;
+  PyObject* textobj = unicode_from(text);
+  if (!textobj) return -1;
+  PyObject* tok = PyObject_CallNoArgs(PyTuple_GET_ITEM(plan, 2));  // config.keys.telegram.token (may throw)
+  if (!tok) {
+    Py_DECREF(textobj);
+    return -1;
+  }
+  PyObject* tg = hattr(hs, s_telegram);
+  PyObject* cd = tg ? plain_client_dict(tg, hs->telegram_cls) : nullptr;
+  int k;
+  if (!cd) {  // another client, or a rate limit / retries: its own send_message
+    if (!tg) {
+      Py_DECREF(textobj);
+      Py_DECREF(tok);
+      return -1;
+    }
+    PyObject* args[5] = {tg, PyTuple_GET_ITEM(plan, 1), textobj, s_markdown, tok};
+    PyObject* kw = PyTuple_Pack(1, s_token);
+    PyObject* aw = kw ? PyObject_VectorcallMethod(s_send_message, args, 4, kw) : nullptr;
+    Py_XDECREF(kw);
+    Py_DECREF(textobj);
+    Py_DECREF(tok);
+    if (!aw) return -1;
+    return await_start(c, aw, out);
+  }
+  PyObject* base = PyDict_GetItemWithError(cd, s_base_url);
+  std::string url;
+  ok = base && text_js_str_append(url, base);
+  url += "/bot";
+  ok = ok && text_js_str_append(url, tok);
+  url += "/sendMessage";
+  Py_DECREF(tok);
+  if (!ok) {
+    Py_DECREF(textobj);
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_AttributeError, "TelegramClient.base_url missing");
+    return -1;
+  }
+  PyObject* keys[3] = {s_chat_id, s_text, s_parse_mode};
+  PyObject* vals[3] = {PyTuple_GET_ITEM(plan, 1), textobj, s_markdown};
+  k = sink_get(c, cd, url, keys, vals, 3, out);
+  Py_DECREF(textobj);
+  return k;
+}
+
+// Emby step of the DEPLOYED hooks (index.js:110-118). 2 = nothing to send, else as await_start.
+int hook_emby(CallObject* c, PyObject** out) {
+  HandlersObject* hs = c->hs;
+  PyObject* plan = c->plan;
+  int on = PyObject_IsTrue(PyTuple_GET_ITEM(plan, 3));
+  if (on <= 0) return on < 0 ? -1 : 2;
+  PyObject* host = PyTuple_GET_ITEM(plan, 4);
+  PyObject* key = PyTuple_GET_ITEM(plan, 5);
+  std::string line = "telling emby to refresh at ";
+  if (!text_js_str_append(line, host)) return -1;
+  PyObject* lo = unicode_from(line);
+  bool ok = lo && log_line(hs, 30, &lo, 1);
+  Py_XDECREF(lo);
+  if (!ok) return -1;
+  PyObject* em = hattr(hs, s_emby);
+  PyObject* cd = em ? plain_client_dict(em, hs->emby_cls) : nullptr;
+  if (!cd) {
+    if (!em) return -1;
+    PyObject* args[3] = {em, host, key};
+    PyObject* kw = PyTuple_Pack(2, s_host, s_api_key);
+    PyObject* aw = kw ? PyObject_VectorcallMethod(s_refresh_library, args, 1, kw) : nullptr;
+    Py_XDECREF(kw);
+    if (!aw) return -1;
+    return await_start(c, aw, out);
+  }
+  std::string url;
+  if (!text_js_str_append(url, host)) return -1;
+  url += "/emby/library/refresh";
+  PyObject* keys[1] = {s_api_key};
+  PyObject* vals[1] = {key};
+  return sink_get(c, cd, url, keys, vals, 1, out);
 }
 
 // ------------------------------------------------------ progress handler ---
@@ -612,7 +783,7 @@ PySendResult step_progress(CallObject* c, PyObject* value, PyObject** result) {
       goto commented;
     }
     case 2:
-      value = trello_finish(c, value);
+      value = request_finish(c, value);
       if (!value) goto catch_;
       Py_DECREF(value);
     commented: {
@@ -631,7 +802,8 @@ finish:
 
 // -------------------------------------------------------- status handler ---
 // index.js:62-125. Errors outside the hooks try escape (Q1).
-// state: 0 start, 1 after updateStatus, 2 after getByID, 3 after the card move, 4 after hooks.
+// state: 0 start, 1 after updateStatus, 2 after getByID, 3 after the card move,
+// 5 after the Telegram message, 6 after the Emby refresh.
 PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
   HandlersObject* hs = c->hs;
   int k;
@@ -778,7 +950,7 @@ PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
       goto hooks;
     }
     case 3:
-      value = trello_finish(c, value);
+      value = request_finish(c, value);
       if (!value) return fail(c);
       Py_DECREF(value);
     hooks: {  // try { ... } catch, index.js:92-122
@@ -788,19 +960,46 @@ PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
       Py_DECREF(ms);
       if (deployed < 0) goto hooks_catch;
       if (!deployed) return finish_ack(c, result);
-      PyObject* aw = PyObject_CallMethodObjArgs(hs->h, s_deployed_hooks, c->media, c->media_id, nullptr);
-      if (!aw) goto hooks_catch;
-      k = await_start(c, aw, &v);
+      // the DEPLOYED branch: handlers._deployed_hooks, step by step (config plan from the same helper)
+      PyObject* plan = PyObject_CallMethodNoArgs(hs->h, s_hooks_plan);
+      if (!plan) goto hooks_catch;
+      if (!PyTuple_Check(plan) || PyTuple_GET_SIZE(plan) != 6) {
+        Py_DECREF(plan);
+        PyErr_SetString(PyExc_TypeError, "_hooks_plan() must return a 6-tuple");
+        goto hooks_catch;
+      }
+      c->plan = plan;
+      k = hook_telegram(c, &v);
       if (k < 0) goto hooks_catch;
       if (k == 0) {
-        c->state = 4;
+        c->state = 5;
         *result = v;
         return PYGEN_NEXT;
       }
-      Py_DECREF(v);
-      return finish_ack(c, result);
+      if (k == 1) Py_DECREF(v);
+      goto emby;
     }
-    case 4:
+    case 4:  // (unused since the hooks run here; kept for the numbering in the header comment)
+      if (!value) goto hooks_catch;
+      Py_DECREF(value);
+      return finish_ack(c, result);
+    case 5:
+      value = request_finish(c, value);
+      if (!value) goto hooks_catch;
+      Py_DECREF(value);
+    emby: {
+      k = hook_emby(c, &v);
+      if (k < 0) goto hooks_catch;
+      if (k == 0) {
+        c->state = 6;
+        *result = v;
+        return PYGEN_NEXT;
+      }
+      if (k == 1) Py_DECREF(v);
+      return finish_ack(c, result);  // index.js:124
+    }
+    case 6:
+      value = request_finish(c, value);
       if (!value) goto hooks_catch;
       Py_DECREF(value);
       return finish_ack(c, result);  // index.js:124
@@ -953,6 +1152,7 @@ int call_traverse(CallObject* c, visitproc visit, void* arg) {
   Py_VISIT(c->host);
   Py_VISIT(c->media);
   Py_VISIT(c->req_stats);
+  Py_VISIT(c->plan);
   return 0;
 }
 
@@ -967,6 +1167,7 @@ int call_clear(CallObject* c) {
   Py_CLEAR(c->host);
   Py_CLEAR(c->media);
   Py_CLEAR(c->req_stats);
+  Py_CLEAR(c->plan);
   return 0;
 }
 
@@ -1002,6 +1203,7 @@ PyObject* make_call(HandlersObject* hs, PyObject* rmsg, uint8_t kind) {
   Py_INCREF(rmsg);
   c->rmsg = rmsg;
   c->sub = c->media_id = c->status = c->status_text = c->progress = c->host = c->media = c->req_stats = nullptr;
+  c->plan = nullptr;
   c->req_t0 = 0;
   c->req_native = c->req_strict = 0;
   c->kind = kind;
@@ -1043,6 +1245,8 @@ int hs_traverse(HandlersObject* hs, visitproc visit, void* arg) {
   Py_VISIT(hs->res_p);
   Py_VISIT(hs->media_cls);
   Py_VISIT(hs->trello_cls);
+  Py_VISIT(hs->telegram_cls);
+  Py_VISIT(hs->emby_cls);
   Py_VISIT(hs->memory_cls);
   Py_VISIT(hs->not_found);
   return 0;
@@ -1070,6 +1274,8 @@ int hs_clear(HandlersObject* hs) {
   Py_CLEAR(hs->res_p);
   Py_CLEAR(hs->media_cls);
   Py_CLEAR(hs->trello_cls);
+  Py_CLEAR(hs->telegram_cls);
+  Py_CLEAR(hs->emby_cls);
   Py_CLEAR(hs->memory_cls);
   Py_CLEAR(hs->not_found);
   return 0;
@@ -1196,7 +1402,9 @@ int hs_init(HandlersObject* hs, PyObject* args, PyObject* kwds) {
   hs->fallback = hs->js_type_error ? module_attr(h, "COMMENT_FALLBACK") : nullptr;
   if (!hs->progress_plan || !hs->fallback || !hs->one || !hs->two) return -1;
   hs->trello_cls = import_attr("beholder_amd.sinks.trello", "TrelloClient");
-  hs->memory_cls = hs->trello_cls ? import_attr("beholder_amd.store.memory", "MemoryStore") : nullptr;
+  hs->telegram_cls = hs->trello_cls ? import_attr("beholder_amd.sinks.telegram", "TelegramClient") : nullptr;
+  hs->emby_cls = hs->telegram_cls ? import_attr("beholder_amd.sinks.emby", "EmbyClient") : nullptr;
+  hs->memory_cls = hs->emby_cls ? import_attr("beholder_amd.store.memory", "MemoryStore") : nullptr;
   hs->not_found = hs->memory_cls ? import_attr("beholder_amd.store.base", "MediaNotFound") : nullptr;
   if (!hs->not_found) return -1;
   static const char* pnames[4] = {"mediaId", "status", "progress", "host"};
@@ -1289,6 +1497,18 @@ int init_handler_types(PyObject* m) {
               {&s_get_calls, "get_calls"},
               {&s_update_calls, "update_calls"},
               {&s_limiter, "limiter"},
+              {&s_hooks_plan, "_hooks_plan"},
+              {&s_telegram, "telegram"},
+              {&s_emby, "emby"},
+              {&s_name, "name"},
+              {&s_metadataId, "metadataId"},
+              {&s_GET, "GET"},
+              {&s_chat_id, "chat_id"},
+              {&s_parse_mode, "parse_mode"},
+              {&s_markdown, "markdown"},
+              {&s_api_key, "api_key"},
+              {&s_send_message, "send_message"},
+              {&s_refresh_library, "refresh_library"},
               {&s_retry, "retry"},
               {&m_progress, "processing progress update on media"},
               {&m_status_kw, "status"},
@@ -1300,7 +1520,8 @@ int init_handler_types(PyObject* m) {
   for (auto& s : strs)
     if (!(*s.slot = intern(s.text))) return -1;
   kw_params_timeout = PyTuple_Pack(2, s_params, s_timeout);
-  if (!kw_params_timeout) return -1;
+  kw_timeout = PyTuple_Pack(1, s_timeout);
+  if (!kw_params_timeout || !kw_timeout) return -1;
 
   CallType.tp_name = "beholder_amd.ops._native.HandlerCall";
   CallType.tp_basicsize = sizeof(CallObject);

@@ -863,6 +863,18 @@ PyMethodDef text_methods[] = {
 // ---- used by the native handlers (py_handlers.cpp) ---------------------------
 bool text_js_str_append(std::string& out, PyObject* v) { return js_str_append(out, v); }
 
+// one `key=value` pair of encode_query() (None values omitted; `first` tracks the '&')
+bool text_query_pair_append(std::string& out, PyObject* k, PyObject* v, bool* first, bool rfc3986) {
+  if (v == Py_None) return true;
+  if (!*first) out += '&';
+  *first = false;
+  std::string ks;
+  if (!js_str_append(ks, k)) return false;
+  quote_append(out, ks.data(), ks.size(), rfc3986);
+  out += '=';
+  return qs_value_append(out, v, rfc3986);
+}
+
 bool is_native_logger(PyObject* logger) {
   // the level methods must be LogCore's own (a subclass overriding them keeps its override)
   if (!PyObject_TypeCheck(logger, &LogCoreType)) return false;

@@ -65,9 +65,11 @@ medias = st.lists(st.builds(
     Media, id=st.sampled_from(["m0", "m1", "m2", "m3", "x1"]), name=st.sampled_from(["Cowboy Bebop", "Ü & ?", ""]),
     creator=st.sampled_from([0, 1, 2]), creatorId=st.sampled_from(["card1", "c/2", "", "ü"]),
     metadataId=st.sampled_from(["1", "42", ""]), status=st.integers(0, 6)), max_size=6)
+# status values: DEPLOYED (4) weighted up so the hooks branch (index.js:92-122) is reached often
+statuses = st.one_of(st.sampled_from([4, 4, 2]), st.integers(-1, 7))
 events = st.lists(st.one_of(
-    st.tuples(st.just("status"), ids, st.integers(-1, 7)),
-    st.tuples(st.just("progress"), ids, st.integers(-1, 7), st.integers(-5, 150),
+    st.tuples(st.just("status"), ids, statuses),
+    st.tuples(st.just("progress"), ids, statuses, st.integers(-5, 150),
               st.sampled_from(["", "worker-1", "ünï", "a b&c"])),
     st.tuples(st.sampled_from(["status", "progress"]), st.just("garbage"), st.binary(max_size=12)),
 ), min_size=1, max_size=12)
@@ -133,7 +135,8 @@ def run_trace(impl, config, no_trello, rows, evs, fault_list, store_kind, concur
 
 @settings(max_examples=int(os.environ.get("BEHOLDER_FUZZ_EXAMPLES", "300")), deadline=None,
           suppress_health_check=[HealthCheck.too_slow])
-@given(config=configs, no_trello=st.booleans(), rows=medias, evs=events, fault_list=faults,
+@given(config=configs, no_trello=st.sampled_from([False, False, False, True]), rows=medias, evs=events,
+       fault_list=faults,
        store_kind=st.sampled_from(sorted(STORES)), concurrent=st.booleans(),
        http_delay=st.sampled_from([0.0, 0.0, 0.0005]))
 def test_native_matches_python(config, no_trello, rows, evs, fault_list, store_kind, concurrent, http_delay):
