@@ -21,9 +21,9 @@ Scale-out is the reference's: competing consumers, one process each
 (SURVEY.md §2.3). Each rank runs ``--procs-per-rank`` consumer processes
 (default: the CPU share of one GPU slot minus one, at most 16; the same for every N) on
 independent streams.
-Timing: every consumer finishes its warm-up and parks on a barrier; the
-rank's coordinator passes a gloo barrier across ranks, releases its
-consumers and starts the clock; it stops the clock when all of its
+Timing: every consumer finishes its warm-up and reports ready; the rank's
+coordinator passes a gloo barrier across ranks and synchronizes the device, then
+releases its consumers through a second barrier and starts the clock; it stops the clock when all of its
 consumers report their K steps done, then passes another gloo barrier. The
 elapsed time is the MAX over ranks and ``value`` is whole-job events/s.
 Per-consumer work is fixed as N grows: weak scaling. The service has no
@@ -258,21 +258,27 @@ async def run_consumer(a, seed: int, go, stop=None) -> dict:
     }
 
 
-def _consumer_entry(a, seed, barrier, results, cpu=None):
-    """Spawned consumer process."""
+def _consumer_entry(a, seed, ready, go, results, cpu=None):
+    """Spawned consumer process: warm up, report ready, wait for the go signal, time K steps."""
     if cpu is not None:
         try:
             os.sched_setaffinity(0, {cpu})
         except OSError:
             pass
+
+    def start():
+        ready.wait()  # warmed up
+        go.wait()     # released by the coordinator, which starts its clock at the same moment
+
     try:
-        res = asyncio.run(run_consumer(a, seed, barrier.wait))
+        res = asyncio.run(run_consumer(a, seed, start))
         results.put(res)
     except BaseException as e:  # report, never hang the coordinator
-        try:
-            barrier.abort()
-        except Exception:  # noqa: BLE001
-            pass
+        for b in (ready, go):
+            try:
+                b.abort()
+            except Exception:  # noqa: BLE001
+                pass
         results.put({"error": f"{type(e).__name__}: {e}"})
         raise
 
@@ -289,22 +295,23 @@ def run_rank(a, dist: _Dist, procs: int) -> dict:
         res["procs"] = 1
         return res
     ctx = mp.get_context("spawn")
-    barrier = ctx.Barrier(procs + 1)
+    ready = ctx.Barrier(procs + 1)
+    go = ctx.Barrier(procs + 1)
     results = ctx.Queue()
     cpus = sorted(os.sched_getaffinity(0)) if a.pin and hasattr(os, "sched_getaffinity") else []
     first = dist.local_rank * procs
 
     def cpu_for(i):
         return cpus[(first + i) % len(cpus)] if cpus else None
-    children = [ctx.Process(target=_consumer_entry, args=(a, base_seed + 104729 * i, barrier, results, cpu_for(i)),
+    children = [ctx.Process(target=_consumer_entry, args=(a, base_seed + 104729 * i, ready, go, results, cpu_for(i)),
                             daemon=True) for i in range(procs)]
     for c in children:
         c.start()
-    barrier.wait()          # every consumer has warmed up (all spawned: HIP may be initialised now)
+    ready.wait()            # every consumer has warmed up (all spawned: HIP may be initialised now)
     dist.barrier()          # ... on every rank
-    dev.sync()
+    dev.sync()              # nothing is timed yet: the consumers wait at `go`
+    go.wait()               # releases the consumers; the clock starts with them
     t0 = time.perf_counter()
-    # releasing the barrier is the consumers' go signal (they were parked in it)
     got = [results.get() for _ in range(procs)]
     dev.sync()
     t1 = time.perf_counter()
@@ -318,7 +325,10 @@ def run_rank(a, dist: _Dist, procs: int) -> dict:
     for g in got:
         hh.merge_bytes(g["handle_hist"])
         ih.merge_bytes(g["ingest_hist"])
-    return {"elapsed": t1 - t0, "events": sum(g["events"] for g in got), "handle_hist": hh.to_bytes(),
+    # each consumer also clocks its own K steps from the go signal; the rank's elapsed time is never
+    # shorter than the slowest consumer's (guards against any head start before t0)
+    elapsed = max(t1 - t0, max(g["elapsed"] for g in got))
+    return {"elapsed": elapsed, "events": sum(g["events"] for g in got), "handle_hist": hh.to_bytes(),
             "ingest_hist": ih.to_bytes(), "http_calls": sum(g["http_calls"] for g in got),
             "errors": sum(g["errors"] for g in got), "abandoned": sum(g["abandoned"] for g in got),
             "procs": procs, "max_consumer_elapsed": max(g["elapsed"] for g in got)}
