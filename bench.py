@@ -22,7 +22,7 @@ Scale-out is the reference's: competing consumers, one process each
 (default: the CPU share of one GPU slot minus one, at most 16; the same for every N) on
 independent streams.
 Timing: every consumer finishes its warm-up and reports ready; the rank's
-coordinator passes a gloo barrier across ranks and synchronizes the device, then
+coordinator synchronizes the device, passes a gloo barrier across ranks, then
 releases its consumers through a second barrier and starts the clock; it stops the clock when all of its
 consumers report their K steps done, then passes another gloo barrier. The
 elapsed time is the MAX over ranks and ``value`` is whole-job events/s.
@@ -289,8 +289,8 @@ def run_rank(a, dist: _Dist, procs: int) -> dict:
     dev = _Device(dist.local_rank)
     if procs == 1:  # the consumer runs in this process, which starts no other program
         def go():
-            dist.barrier()
             dev.sync()
+            dist.barrier()
         res = asyncio.run(run_consumer(a, base_seed, go, dev.sync))
         res["procs"] = 1
         return res
@@ -308,8 +308,8 @@ def run_rank(a, dist: _Dist, procs: int) -> dict:
     for c in children:
         c.start()
     ready.wait()            # every consumer has warmed up (all spawned: HIP may be initialised now)
-    dist.barrier()          # ... on every rank
     dev.sync()              # nothing is timed yet: the consumers wait at `go`
+    dist.barrier()          # every rank is ready (after its device init, so ranks start together)
     go.wait()               # releases the consumers; the clock starts with them
     t0 = time.perf_counter()
     got = [results.get() for _ in range(procs)]
