@@ -328,7 +328,7 @@ def run_rank(a, dist: _Dist, procs: int) -> dict:
     # each consumer also clocks its own K steps from the go signal; the rank's elapsed time is never
     # shorter than the slowest consumer's (guards against any head start before t0)
     elapsed = max(t1 - t0, max(g["elapsed"] for g in got))
-    return {"elapsed": elapsed, "events": sum(g["events"] for g in got), "handle_hist": hh.to_bytes(),
+    return {"elapsed": elapsed, "coordinator_elapsed": t1 - t0, "events": sum(g["events"] for g in got), "handle_hist": hh.to_bytes(),
             "ingest_hist": ih.to_bytes(), "http_calls": sum(g["http_calls"] for g in got),
             "errors": sum(g["errors"] for g in got), "abandoned": sum(g["abandoned"] for g in got),
             "procs": procs, "max_consumer_elapsed": max(g["elapsed"] for g in got)}

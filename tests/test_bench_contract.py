@@ -48,3 +48,26 @@ def test_bench_multiprocess_rank():
     assert out["procs_per_rank"] == 2 and out["config"]["global_batch"] == 8192
     assert out["value"] == pytest.approx(8192 * 2 / (out["ms_per_step"] * 2 / 1000), rel=0.01)
     assert out["handler_errors"] == 0
+
+
+def test_consumers_get_no_head_start(monkeypatch):
+    """Slow device initialisation before the clock must not let consumers start early: the
+    coordinator's clock and each consumer's own clock cover the same K steps."""
+    import time as _time
+
+    import bench
+    calls = []
+
+    def slow_first_sync(self):  # device initialisation happens on the first sync only
+        calls.append(1)
+        if len(calls) == 1:
+            _time.sleep(0.5)
+    monkeypatch.setattr(bench._Device, "sync", slow_first_sync)
+    a = bench.parse(["--procs-per-rank", "2", "--steps", "2", "--warmup", "1", "--events-per-step", "4096",
+                     "--media", "200"])
+    res = bench.run_rank(a, bench._Dist(), 2)
+    assert res["events"] == 2 * 2 * 4096
+    # with a head start the consumers would finish ~0.5 s of work before the coordinator's t0
+    assert res["coordinator_elapsed"] >= res["max_consumer_elapsed"] - 0.05, res
+    assert res["coordinator_elapsed"] < res["max_consumer_elapsed"] + 0.3, res
+    assert len(calls) == 2  # before t0 and before t1
