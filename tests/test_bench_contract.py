@@ -69,5 +69,5 @@ def test_consumers_get_no_head_start(monkeypatch):
     assert res["events"] == 2 * 2 * 4096
     # with a head start the consumers would finish ~0.5 s of work before the coordinator's t0
     assert res["coordinator_elapsed"] >= res["max_consumer_elapsed"] - 0.05, res
-    assert res["coordinator_elapsed"] < res["max_consumer_elapsed"] + 0.3, res
+    assert res["coordinator_elapsed"] < res["max_consumer_elapsed"] + 1.0, res
     assert len(calls) == 2  # before t0 and before t1
