@@ -70,7 +70,8 @@ SERVICE_DEFAULTS: dict = {
         "native_handlers": True,
         # Jaeger spans per delivery (utils/tracing.py); JAEGER_* env variables override
         "tracing": {"enabled": False, "service_name": "beholder",
-                    "sampler": {"type": "const", "param": 1},
+                    # jaeger-client's fallback when no remote sampler answers: 1 trace in 1000
+                    "sampler": {"type": "probabilistic", "param": 0.001},
                     "agent": {"host": "127.0.0.1", "port": 6831}},
     }
 }

@@ -549,8 +549,8 @@ def tracer_from_config(section: Optional[Mapping[str, Any]], env: Optional[Mappi
         return None
     service = env.get("JAEGER_SERVICE_NAME") or section.get("service_name") or "beholder"
     smp = dict(section.get("sampler") or {})
-    sampler = make_sampler(env.get("JAEGER_SAMPLER_TYPE") or smp.get("type", "const"),
-                           env.get("JAEGER_SAMPLER_PARAM", smp.get("param", 1)))
+    sampler = make_sampler(env.get("JAEGER_SAMPLER_TYPE") or smp.get("type", "probabilistic"),
+                           env.get("JAEGER_SAMPLER_PARAM", smp.get("param", 0.001)))
     tags = {"hostname": socket.gethostname(), "jaeger.version": "Python-beholder"}
     tags.update({str(k): v for k, v in (section.get("tags") or {}).items()})
     tags.update(_parse_tags(env.get("JAEGER_TAGS")))
