@@ -334,14 +334,40 @@ class Service:
         sleep = asyncio.sleep
         # native fast path: the per-delivery loop runs in C (ops.dispatch_batch); per-media
         # ordering and trace spans keep the Python loop
-        native = (self.serializer is None and not self.trace and self.tracer is None
+        native = (self.serializer is None and not self.trace
                   and os.environ.get("BEHOLDER_NATIVE_DISPATCH", "1") != "0")
+        tracer = self.tracer
         native_dispatch = dispatch_batch
         routes = tuple(routes)
         on_error, on_suspend, on_unroutable = self._on_handler_error, self._on_suspend, self._unroutable
         try:
             async for batch in self.source.batches():
-                if native:
+                if native and tracer is not None:
+                    # sampled deliveries alone through the traced Python path, every run of
+                    # unsampled ones through the native dispatch loop
+                    i, n = 0, len(batch)
+                    while i < n:
+                        j, decision = self._next_sampled(batch, i)
+                        while i < j:
+                            sub = batch[i:j] if i or j < n else batch
+                            k, m = 0, len(sub)
+                            while k < m:
+                                k = native_dispatch(sub, k, routes, received, on_error, on_suspend, on_unroutable)
+                                if k < m or len(inflight) >= prefetch:
+                                    await self._wait_slots()
+                            i = j
+                        if j < n:
+                            d = batch[j]
+                            tid = d.topic_id
+                            if tid >= nroutes or routes[tid] is None:
+                                self._unroutable(d)
+                            else:
+                                received[tid] += 1
+                                self._dispatch_now(d, decision=decision)
+                                if inflight and len(inflight) >= prefetch:
+                                    await self._wait_slots()
+                            i = j + 1
+                elif native:
                     i, n = 0, len(batch)
                     while i < n:
                         i = native_dispatch(batch, i, routes, received, on_error, on_suspend, on_unroutable)
@@ -389,13 +415,28 @@ class Service:
                         "handle_us": (now - d.start_ns) // 1000, "outcome": outcome, "state": d.state},
                        "handled")
 
-    def _trace_start(self, d):
+    def _next_sampled(self, batch, i: int):
+        """``(j, decision)``: the first delivery at or after ``i`` whose trace is sampled, with
+        its sampling decision (``j == len(batch)``, None when there is none)."""
+        sample = self.tracer.sample
+        n = len(batch)
+        while i < n:
+            h = batch[i].headers
+            decision = sample(extract_trace_context(h) if h is not None else None)
+            if decision is not None:
+                return i, decision
+            i += 1
+        return n, None
+
+    def _trace_start(self, d, decision=None):
         """A Jaeger span for this delivery (None when not sampled). Called after ``d.start()``."""
         topic = d.topic or str(d.topic_id)
-        return self.tracer.start_span(topic, child_of=extract_trace_context(d.headers), tags={
-            "span.kind": "consumer", "component": "beholder", "message_bus.destination": topic,
-            "amqp.delivery_tag": d.tag, "amqp.redelivered": d.redelivered,
-            "beholder.queue_us": max(0, d.start_ns - d.recv_ns) // 1000})
+        tags = {"span.kind": "consumer", "component": "beholder", "message_bus.destination": topic,
+                "amqp.delivery_tag": d.tag, "amqp.redelivered": d.redelivered,
+                "beholder.queue_us": max(0, d.start_ns - d.recv_ns) // 1000}
+        if decision is not None:
+            return self.tracer.start_sampled(decision, topic, tags=tags)
+        return self.tracer.start_span(topic, child_of=extract_trace_context(d.headers), tags=tags)
 
     def _trace_finish(self, span, d, exc: Optional[BaseException]) -> None:
         h = self.handlers
@@ -410,12 +451,13 @@ class Service:
             span.log_kv({"event": "error", "error.kind": type(exc).__name__, "message": err_message(exc)})
         span.finish()
 
-    def _dispatch_now(self, d, on_finish: Optional[Callable[[], None]] = None) -> bool:
+    def _dispatch_now(self, d, on_finish: Optional[Callable[[], None]] = None, decision=None) -> bool:
         """Python dispatch path (per-media ordering, trace spans). Returns True when the handler
-        finished synchronously; otherwise a Driver finishes it and calls ``on_finish()`` then."""
+        finished synchronously; otherwise a Driver finishes it and calls ``on_finish()`` then.
+        ``decision``: a sampling decision already taken (``Tracer.sample``) for this delivery."""
         handler = self._routes[d.topic_id]
         d.start()
-        span = self._trace_start(d) if self.tracer is not None else None
+        span = self._trace_start(d, decision) if self.tracer is not None else None
         coro = handler(d)
         try:
             first = coro.send(None)

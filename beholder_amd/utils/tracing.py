@@ -98,6 +98,8 @@ def extract(headers: Any) -> Optional[SpanContext]:
     if headers is None:
         return None
     if isinstance(headers, (bytes, bytearray)):
+        if b"uber-trace-id" not in headers and b"traceparent" not in headers.lower():
+            return None  # no trace context: skip decoding the table
         from ..transport.amqp.wire import AmqpError, _Reader
         try:
             headers = _Reader(bytes(headers)).table()
@@ -495,25 +497,34 @@ class Tracer:
             v = self._rng.getrandbits(bits)
         return v
 
-    def start_span(self, operation: str, child_of: Optional[SpanContext] = None, start_us: Optional[int] = None,
-                   tags: Optional[Dict[str, TagValue]] = None) -> Optional[Span]:
-        """A recording span, or None when this trace is not sampled (nothing to do then)."""
-        span_id = self._id()
+    def sample(self, child_of: Optional[SpanContext] = None):
+        """The sampling decision alone: ``(context, references, root_tags)`` for a span to
+        record, or None. Cheap enough to run for every message; only sampled ones pay for a Span."""
         if child_of is not None:
             if not child_of.sampled:
                 return None  # the upstream decision wins (jaeger-client semantics)
-            ctx = SpanContext(child_of.trace_id, span_id, child_of.span_id, child_of.flags)
-            refs = [(REF_CHILD_OF, child_of)]
-            span_tags = dict(tags or {})
-        else:
-            trace_id = self._id()
-            if not self.sampler.is_sampled(trace_id):
-                return None
-            ctx = SpanContext(trace_id, span_id, 0, 1)
-            refs = []
-            span_tags = {"sampler.type": self.sampler.type, "sampler.param": self.sampler.param}
-            span_tags.update(tags or {})
+            return (SpanContext(child_of.trace_id, self._id(), child_of.span_id, child_of.flags),
+                    [(REF_CHILD_OF, child_of)], None)
+        trace_id = self._id()
+        if not self.sampler.is_sampled(trace_id):
+            return None
+        return (SpanContext(trace_id, self._id(), 0, 1), [],
+                {"sampler.type": self.sampler.type, "sampler.param": self.sampler.param})
+
+    def start_sampled(self, decision, operation: str, start_us: Optional[int] = None,
+                      tags: Optional[Dict[str, TagValue]] = None) -> Span:
+        ctx, refs, root_tags = decision
+        span_tags = dict(root_tags or {})
+        span_tags.update(tags or {})
         return Span(self, ctx, operation, start_us if start_us is not None else _now_us(), refs, span_tags)
+
+    def start_span(self, operation: str, child_of: Optional[SpanContext] = None, start_us: Optional[int] = None,
+                   tags: Optional[Dict[str, TagValue]] = None) -> Optional[Span]:
+        """A recording span, or None when this trace is not sampled (nothing to do then)."""
+        decision = self.sample(child_of)
+        if decision is None:
+            return None
+        return self.start_sampled(decision, operation, start_us, tags)
 
     def flush(self) -> None:
         self.reporter.flush()

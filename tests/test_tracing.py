@@ -267,3 +267,44 @@ def test_service_spans_join_upstream_traces_over_amqp(native_demux):
     assert len(err) == 1 and err[0].tags["beholder.outcome"] == "pending" and err[0].logs[0][1]["event"] == "error"
     assert ok[0].context.parent_id == 0 and ok[0].tags["sampler.type"] == "const"
     assert len(rep.spans) == 7
+
+
+def test_unsampled_deliveries_stay_on_the_native_dispatch_path():
+    """With a sampler that says no, only deliveries whose upstream trace is sampled get spans;
+    the rest run through the native dispatch loop in batches. Every delivery is acked."""
+    rep = tr.InMemoryReporter()
+
+    async def go():
+        broker = await AmqpBroker().start()
+        try:
+            d = {k: v for k, v in BASE_CFG.items()}
+            d["service"] = {"metrics": {"enabled": False}, "tracing": {"enabled": True}}
+            svc = Service(Config.from_dict(d, env={}), source=AmqpSource(broker.url, capture_headers=True),
+                          store=MemoryStore([trello_media("m1", card="C1")]), http=RecordingHttpClient(),
+                          logger=Logger(stream=MemoryStream()))
+            svc.tracer = tr.Tracer("beholder", tr.ConstSampler(False), rep)
+            calls = []
+            orig = svc._dispatch_now
+            svc._dispatch_now = lambda *a, **kw: calls.append(1) or orig(*a, **kw)
+            await svc.init()
+            task = asyncio.ensure_future(svc.run())
+            for i in range(50):
+                props = {"headers": {"uber-trace-id": f"{0x5000 + i:x}:{0x10 + i:x}:0:1"}} if i % 17 == 3 else \
+                    {"headers": {"x-other": "y"}}
+                broker.publish(PROGRESS, progress_msg("m1", "UPLOADING", i), properties=props)
+            for _ in range(300):
+                if broker.stats(PROGRESS)["acked"] == 50:
+                    break
+                await asyncio.sleep(0.02)
+            svc.request_stop()
+            await task
+            await svc.close()
+            return broker.stats(PROGRESS), calls
+        finally:
+            await broker.stop()
+
+    st, calls = asyncio.run(asyncio.wait_for(go(), 60))
+    assert st["acked"] == 50
+    traced = sorted(s.context.trace_id for s in rep.spans)
+    assert traced == [0x5000 + i for i in range(50) if i % 17 == 3]
+    assert len(calls) == len(traced)  # only the sampled ones took the Python dispatch path
