@@ -67,3 +67,34 @@ def test_ingest_feed_random_bytes(data):
             break
         got.extend(b)
     assert sum(len(d.content) + 5 for d in got) <= len(data)
+
+
+@settings(max_examples=300, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(st.dictionaries(st.text(max_size=8), st.one_of(st.text(max_size=30), st.integers(-5, 5), st.booleans()),
+                       max_size=4),
+       st.sampled_from([None, "application/protobuf"]), st.sampled_from([None, "gzip"]),
+       st.integers(0, 10_000), st.integers(0, 255), st.booleans())
+def test_demux_header_capture(headers, ctype, cenc, pos, byte, mutate):
+    """capture_headers: the raw `headers` table of each delivery equals wire.encode_table (any
+    preceding content-type / content-encoding properties skipped); corrupted header frames
+    never crash and never yield a table that overruns the frame."""
+    props = {"headers": headers or None, "content_type": ctype, "content_encoding": cenc, "delivery_mode": 2}
+    data = bytearray(wire.encode_method(1, "basic.deliver", consumer_tag="c", delivery_tag=1, redelivered=False,
+                                        exchange="", routing_key="q")
+                     + wire.encode_content(1, 60, b"body", props, 4096))
+    if mutate:
+        data[pos % len(data)] = byte
+    dm = AmqpDemux(Settler(), 0)
+    dm.capture_headers = True
+    dm.add_consumer(1, "c", 2, None)
+    try:
+        out = dm.feed(bytes(data))
+    except ValueError:
+        return
+    ds = [it for it in out if not isinstance(it, tuple)]
+    for d in ds:
+        if d.headers is not None:
+            assert len(d.headers) >= 4 and len(d.headers) <= len(data)
+    if not mutate:
+        assert len(ds) == 1
+        assert ds[0].headers == (wire.encode_table(headers) if headers else None)
