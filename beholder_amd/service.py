@@ -333,46 +333,19 @@ class Service:
         prefetch = self.prefetch
         sleep = asyncio.sleep
         # native fast path: the per-delivery loop runs in C (ops.dispatch_batch); per-media
-        # ordering and trace spans keep the Python loop
+        # ordering and debug-line spans keep the Python loop; with Jaeger tracing only the
+        # sampled deliveries leave it
         native = (self.serializer is None and not self.trace
                   and os.environ.get("BEHOLDER_NATIVE_DISPATCH", "1") != "0")
         tracer = self.tracer
-        native_dispatch = dispatch_batch
         routes = tuple(routes)
         on_error, on_suspend, on_unroutable = self._on_handler_error, self._on_suspend, self._unroutable
         try:
             async for batch in self.source.batches():
                 if native and tracer is not None:
-                    # sampled deliveries alone through the traced Python path, every run of
-                    # unsampled ones through the native dispatch loop
-                    i, n = 0, len(batch)
-                    while i < n:
-                        j, decision = self._next_sampled(batch, i)
-                        while i < j:
-                            sub = batch[i:j] if i or j < n else batch
-                            k, m = 0, len(sub)
-                            while k < m:
-                                k = native_dispatch(sub, k, routes, received, on_error, on_suspend, on_unroutable)
-                                if k < m or len(inflight) >= prefetch:
-                                    await self._wait_slots()
-                            i = j
-                        if j < n:
-                            d = batch[j]
-                            tid = d.topic_id
-                            if tid >= nroutes or routes[tid] is None:
-                                self._unroutable(d)
-                            else:
-                                received[tid] += 1
-                                self._dispatch_now(d, decision=decision)
-                                if inflight and len(inflight) >= prefetch:
-                                    await self._wait_slots()
-                            i = j + 1
+                    await self._dispatch_sampled(batch, routes, on_error, on_suspend, on_unroutable)
                 elif native:
-                    i, n = 0, len(batch)
-                    while i < n:
-                        i = native_dispatch(batch, i, routes, received, on_error, on_suspend, on_unroutable)
-                        if i < n or len(inflight) >= prefetch:
-                            await self._wait_slots()  # at most `prefetch` handlers suspended (index.js:43)
+                    await self._dispatch_native(batch, routes, on_error, on_suspend, on_unroutable)
                 else:
                     for d in batch:
                         tid = d.topic_id
@@ -397,6 +370,37 @@ class Service:
                 log.error(f"ingest source failed: {err}")
             log.flush()
         return self.stats()
+
+    async def _dispatch_native(self, batch, routes, on_error, on_suspend, on_unroutable) -> None:
+        """The per-delivery loop in C (ops.dispatch_batch), pausing while `prefetch` handlers
+        are suspended (index.js:43)."""
+        i, n = 0, len(batch)
+        inflight, prefetch = self._inflight, self.prefetch
+        while i < n:
+            i = dispatch_batch(batch, i, routes, self.received, on_error, on_suspend, on_unroutable)
+            if i < n or len(inflight) >= prefetch:
+                await self._wait_slots()
+
+    async def _dispatch_sampled(self, batch, routes, on_error, on_suspend, on_unroutable) -> None:
+        """Tracing on: each run of unsampled deliveries goes through the native loop, and each
+        sampled delivery through the Python path that opens and closes its span."""
+        i, n = 0, len(batch)
+        while i < n:
+            j, decision = self._next_sampled(batch, i)
+            if i < j:
+                await self._dispatch_native(batch[i:j] if i or j < n else batch, routes, on_error, on_suspend,
+                                            on_unroutable)
+            if j < n:
+                d = batch[j]
+                tid = d.topic_id
+                if tid >= len(routes) or routes[tid] is None:
+                    self._unroutable(d)
+                else:
+                    self.received[tid] += 1
+                    self._dispatch_now(d, decision=decision)
+                    if self._inflight and len(self._inflight) >= self.prefetch:
+                        await self._wait_slots()
+            i = j + 1
 
     async def _flush_logs_periodically(self, every_s: float = 0.1) -> None:
         """Lines logged outside the batch loop (reconnects, idle periods) reach the stream within 100 ms."""
