@@ -64,6 +64,7 @@ AmqpDemux = native.AmqpDemux
 H1Parser = native.H1Parser
 PgReader = native.PgReader
 Driver = native.Driver
+Window = native.Window
 IOFuture = native.IOFuture
 if os.environ.get("BEHOLDER_IOFUTURE", "1") == "0":  # A/B switch: plain asyncio futures for I/O replies
     import asyncio as _asyncio
@@ -132,7 +133,7 @@ def codec_for(ptype) -> Optional[object]:
 
 
 __all__ = [
-    "native", "NativeHandlers", "SinkStats", "AckBatcher", "AmqpDemux", "Driver", "IOFuture", "H1Parser", "PgReader", "MessageCodec", "Ingest", "Delivery", "Settler", "Counter", "Histogram",
+    "native", "NativeHandlers", "SinkStats", "AckBatcher", "AmqpDemux", "Driver", "Window", "IOFuture", "H1Parser", "PgReader", "MessageCodec", "Ingest", "Delivery", "Settler", "Counter", "Histogram",
     "frame", "frames", "mono_ns", "codec_for", "field_table", "format_line", "quick_format", "js_str",
     "js_number", "encode_query", "quote_component",
 ]

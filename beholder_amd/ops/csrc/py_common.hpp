@@ -100,4 +100,8 @@ int init_driver_types(PyObject* m);
 int init_ack_types(PyObject* m);
 int init_handler_types(PyObject* m);
 
+// ---- Window (py_driver.cpp): the in-flight set dispatch_batch hands suspended handlers to ----
+bool is_window(PyObject* o);
+PyObject* window_suspend_c(PyObject* w, PyObject* payload, PyObject* coro, PyObject* first);
+
 }  // namespace beholder

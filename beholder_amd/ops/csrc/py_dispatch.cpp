@@ -8,9 +8,10 @@
 // back into Python:
 //   on_error(delivery, exc)            handler raised (quirk Q1 policy lives in Python)
 //   on_suspend(delivery, coro, fut) -> bool
-//                                      handler awaited real I/O: Python wraps the
-//                                      started coroutine in a Task; returning True
-//                                      means "prefetch window full, stop here"
+//                                      handler awaited real I/O: a Driver resumes the
+//                                      started coroutine; returning True means
+//                                      "prefetch window full, stop here". A native
+//                                      Window (py_driver.cpp) does this in C.
 //   on_unroutable(delivery)            no handler for the topic id
 // Returns the index of the first delivery not dispatched (len(batch) when done).
 #include "py_common.hpp"
@@ -102,8 +103,9 @@ PyObject* mod_dispatch_batch(PyObject*, PyObject* const* a, Py_ssize_t n) {
       Py_DECREF(r);
       continue;
     }
-    // PYGEN_NEXT: suspended on real I/O
-    PyObject* r = PyObject_CallFunctionObjArgs(on_suspend, item, coro, result, nullptr);
+    // PYGEN_NEXT: suspended on real I/O (a native Window takes it without a Python call)
+    PyObject* r = is_window(on_suspend) ? window_suspend_c(on_suspend, item, coro, result)
+                                        : PyObject_CallFunctionObjArgs(on_suspend, item, coro, result, nullptr);
     Py_DECREF(coro);
     Py_XDECREF(result);
     if (!r) goto done;

@@ -116,6 +116,39 @@ PyObject* fetch_exc() {
   return v;
 }
 
+// ---- Window: the set of handlers suspended on I/O (at most `limit`: the prefetch window,
+// index.js:43). A Driver whose on_done is a Window reports to it in C.
+struct WindowObject {
+  PyObject_HEAD PyObject* drivers;  // set of live Drivers
+  PyObject* on_error;               // callable(payload, exc): a handler raised
+  PyObject* on_wake;                // callable(): a slot freed after the window was full, or it emptied
+  Py_ssize_t limit;
+  uint64_t suspended;
+  uint64_t wakes;
+};
+
+PyTypeObject WindowType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+// A driver finished (`exc` borrowed, may be NULL): forget it, report errors, wake waiters on the
+// transitions that matter. 0, or -1 with an exception set.
+int window_done(WindowObject* w, DriverObject* drv, PyObject* exc) {
+  Py_ssize_t before = PySet_GET_SIZE(w->drivers);
+  if (PySet_Discard(w->drivers, reinterpret_cast<PyObject*>(drv)) < 0) return -1;
+  if (exc && exc != Py_None && !drv->cancelled && w->on_error != Py_None) {
+    PyObject* r = PyObject_CallFunctionObjArgs(w->on_error, drv->payload ? drv->payload : Py_None, exc, nullptr);
+    if (!r) return -1;
+    Py_DECREF(r);
+  }
+  Py_ssize_t n = PySet_GET_SIZE(w->drivers);
+  if (((before >= w->limit && n < w->limit) || n == 0) && w->on_wake != Py_None) {
+    ++w->wakes;
+    PyObject* r = PyObject_CallNoArgs(w->on_wake);
+    if (!r) return -1;
+    Py_DECREF(r);
+  }
+  return 0;
+}
+
 // The coroutine is finished: report once. Returns 0, or -1 with an exception set
 // (on_done raised, or a KeyboardInterrupt/SystemExit that must reach the loop).
 int finish(DriverObject* s, PyObject* exc) {
@@ -126,7 +159,12 @@ int finish(DriverObject* s, PyObject* exc) {
   if (exc && PyErr_GivenExceptionMatches(exc, g_cancelled_error)) s->cancelled = 1;
   PyObject* cb = s->on_done;
   s->on_done = nullptr;
-  PyObject* r = PyObject_CallFunctionObjArgs(cb, reinterpret_cast<PyObject*>(s), exc ? exc : Py_None, nullptr);
+  PyObject* r;
+  if (Py_TYPE(cb) == &WindowType) {
+    r = window_done(reinterpret_cast<WindowObject*>(cb), s, exc) < 0 ? nullptr : Py_NewRef(Py_None);
+  } else {
+    r = PyObject_CallFunctionObjArgs(cb, reinterpret_cast<PyObject*>(s), exc ? exc : Py_None, nullptr);
+  }
   Py_DECREF(cb);
   Py_CLEAR(s->payload);  // release the delivery promptly (an un-acked one is then counted as abandoned)
   if (!r) return -1;
@@ -731,7 +769,151 @@ PyGetSetDef iof_getset[] = {
      nullptr},
     {nullptr, nullptr, nullptr, nullptr, nullptr}};
 
+// ---- Window methods ------------------------------------------------------------
+PyObject* window_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
+  static const char* kwlist[] = {"limit", "on_error", "on_wake", nullptr};
+  Py_ssize_t limit;
+  PyObject* on_error = Py_None;
+  PyObject* on_wake = Py_None;
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "n|OO", const_cast<char**>(kwlist), &limit, &on_error, &on_wake))
+    return nullptr;
+  if (limit < 1) {
+    PyErr_SetString(PyExc_ValueError, "limit must be >= 1");
+    return nullptr;
+  }
+  WindowObject* w = reinterpret_cast<WindowObject*>(type->tp_alloc(type, 0));
+  if (!w) return nullptr;
+  w->drivers = PySet_New(nullptr);
+  if (!w->drivers) {
+    Py_DECREF(w);
+    return nullptr;
+  }
+  Py_INCREF(on_error);
+  w->on_error = on_error;
+  Py_INCREF(on_wake);
+  w->on_wake = on_wake;
+  w->limit = limit;
+  return reinterpret_cast<PyObject*>(w);
+}
+
+int window_traverse(WindowObject* w, visitproc visit, void* arg) {
+  Py_VISIT(w->drivers);
+  Py_VISIT(w->on_error);
+  Py_VISIT(w->on_wake);
+  return 0;
+}
+
+int window_clear(WindowObject* w) {
+  Py_CLEAR(w->drivers);
+  Py_CLEAR(w->on_error);
+  Py_CLEAR(w->on_wake);
+  return 0;
+}
+
+void window_dealloc(WindowObject* w) {
+  PyObject_GC_UnTrack(w);
+  window_clear(w);
+  Py_TYPE(w)->tp_free(reinterpret_cast<PyObject*>(w));
+}
+
+Py_ssize_t window_len(WindowObject* w) { return w->drivers ? PySet_GET_SIZE(w->drivers) : 0; }
+
+PyObject* window_iter(WindowObject* w) {
+  PyObject* lst = PySequence_List(w->drivers);  // a snapshot: drivers may finish while iterating
+  if (!lst) return nullptr;
+  PyObject* it = PyObject_GetIter(lst);
+  Py_DECREF(lst);
+  return it;
+}
+
+// suspend(payload, coro, first_yield) -> bool: a Driver resumes `coro` (reporting here);
+// True when the window is now full.
+PyObject* window_suspend_impl(WindowObject* w, PyObject* payload, PyObject* coro, PyObject* first) {
+  DriverObject* drv = reinterpret_cast<DriverObject*>(driver_new(&DriverType, nullptr, nullptr));
+  if (!drv) return nullptr;
+  Py_INCREF(coro);
+  drv->coro = coro;
+  Py_INCREF(reinterpret_cast<PyObject*>(w));
+  drv->on_done = reinterpret_cast<PyObject*>(w);
+  Py_INCREF(payload);
+  drv->payload = payload;
+  if (PySet_Add(w->drivers, reinterpret_cast<PyObject*>(drv)) < 0) {
+    Py_DECREF(drv);
+    return nullptr;
+  }
+  ++w->suspended;
+  PyObject* r = driver_start(drv, first);
+  if (!r) {
+    PyObject *et, *ev, *tb;
+    PyErr_Fetch(&et, &ev, &tb);
+    PySet_Discard(w->drivers, reinterpret_cast<PyObject*>(drv));
+    PyErr_Restore(et, ev, tb);
+    Py_DECREF(drv);
+    return nullptr;
+  }
+  Py_DECREF(r);
+  Py_DECREF(drv);  // the set (and the awaited future's callback) keep it alive
+  return PyBool_FromLong(PySet_GET_SIZE(w->drivers) >= w->limit);
+}
+
+PyObject* window_suspend(WindowObject* w, PyObject* const* a, Py_ssize_t n) {
+  if (n != 3) {
+    PyErr_SetString(PyExc_TypeError, "suspend(payload, coro, first_yield)");
+    return nullptr;
+  }
+  return window_suspend_impl(w, a[0], a[1], a[2]);
+}
+
+// track(driver): a Driver created elsewhere (with its own on_done) counts against the window
+PyObject* window_track(WindowObject* w, PyObject* drv) {
+  if (Py_TYPE(drv) != &DriverType) {
+    PyErr_SetString(PyExc_TypeError, "track() takes a Driver");
+    return nullptr;
+  }
+  if (PySet_Add(w->drivers, drv) < 0) return nullptr;
+  ++w->suspended;
+  Py_RETURN_NONE;
+}
+
+// release(driver, exc=None): the tracked driver finished (its own on_done calls this)
+PyObject* window_release(WindowObject* w, PyObject* const* a, Py_ssize_t n) {
+  if (n < 1 || n > 2 || Py_TYPE(a[0]) != &DriverType) {
+    PyErr_SetString(PyExc_TypeError, "release(driver, exc=None)");
+    return nullptr;
+  }
+  if (window_done(w, reinterpret_cast<DriverObject*>(a[0]), n == 2 ? a[1] : nullptr) < 0) return nullptr;
+  Py_RETURN_NONE;
+}
+
+PyObject* window_stats(WindowObject* w, PyObject*) {
+  return Py_BuildValue("{s:n,s:n,s:K,s:K}", "inflight", window_len(w), "limit", w->limit, "suspended",
+                       static_cast<unsigned long long>(w->suspended), "wakes",
+                       static_cast<unsigned long long>(w->wakes));
+}
+
+PyObject* window_get_limit(WindowObject* w, void*) { return PyLong_FromSsize_t(w->limit); }
+
+PyMethodDef window_methods[] = {
+    {"suspend", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(window_suspend)), METH_FASTCALL,
+     "suspend(payload, coro, first_yield) -> bool: resume coro with a Driver; True = window full"},
+    {"track", reinterpret_cast<PyCFunction>(window_track), METH_O, "track(driver)"},
+    {"release", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(window_release)), METH_FASTCALL,
+     "release(driver, exc=None)"},
+    {"stats", reinterpret_cast<PyCFunction>(window_stats), METH_NOARGS, "counters"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyGetSetDef window_getset[] = {{"limit", reinterpret_cast<getter>(window_get_limit), nullptr, "capacity", nullptr},
+                               {nullptr, nullptr, nullptr, nullptr, nullptr}};
+
+PySequenceMethods window_seq = {};
+
 }  // namespace
+
+bool is_window(PyObject* o) { return Py_TYPE(o) == &WindowType; }
+
+PyObject* window_suspend_c(PyObject* w, PyObject* payload, PyObject* coro, PyObject* first) {
+  return window_suspend_impl(reinterpret_cast<WindowObject*>(w), payload, coro, first);
+}
 
 int init_driver_types(PyObject* m) {
   PyObject* aio = PyImport_ImportModule("asyncio");
@@ -763,6 +945,25 @@ int init_driver_types(PyObject* m) {
   if (PyType_Ready(&DriverType) < 0) return -1;
   Py_INCREF(&DriverType);
   if (PyModule_AddObject(m, "Driver", reinterpret_cast<PyObject*>(&DriverType)) < 0) return -1;
+
+  window_seq.sq_length = reinterpret_cast<lenfunc>(window_len);
+  WindowType.tp_name = "beholder_amd.ops._native.Window";
+  WindowType.tp_basicsize = sizeof(WindowObject);
+  WindowType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC;
+  WindowType.tp_doc =
+      "Window(limit, on_error=None, on_wake=None): handlers suspended on I/O (the prefetch window); "
+      "Drivers started by suspend() report back in C";
+  WindowType.tp_new = window_new;
+  WindowType.tp_dealloc = reinterpret_cast<destructor>(window_dealloc);
+  WindowType.tp_traverse = reinterpret_cast<traverseproc>(window_traverse);
+  WindowType.tp_clear = reinterpret_cast<inquiry>(window_clear);
+  WindowType.tp_as_sequence = &window_seq;
+  WindowType.tp_iter = reinterpret_cast<getiterfunc>(window_iter);
+  WindowType.tp_methods = window_methods;
+  WindowType.tp_getset = window_getset;
+  if (PyType_Ready(&WindowType) < 0) return -1;
+  Py_INCREF(&WindowType);
+  if (PyModule_AddObject(m, "Window", reinterpret_cast<PyObject*>(&WindowType)) < 0) return -1;
 
   PyObject* aio2 = PyImport_ImportModule("asyncio");
   if (!aio2) return -1;

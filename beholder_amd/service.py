@@ -45,7 +45,7 @@ from .sinks import AiohttpClient, EmbyClient, H1Client, HttpClient, SinkObserver
 from .sinks.ratelimit import from_config as sink_policy
 from .store import MediaStore, open_store
 from .transport.base import Source
-from .ops import Driver, dispatch_batch
+from .ops import Driver, Window, dispatch_batch
 from .utils.log import Logger
 from .utils.tracing import extract as extract_trace_context, tracer_from_config
 
@@ -118,7 +118,8 @@ class Service:
         # Jaeger spans per delivery (utils/tracing.py): service.tracing or JAEGER_* env
         self.tracer = tracer_from_config(svc.get("tracing"), env=config.env)
         self._routes: List[Optional[Handler]] = [None] * len(T.TOPIC_NAMES_BY_ID)
-        self._inflight: set = set()
+        # handlers suspended on I/O, at most `prefetch` (index.js:43); drivers report back in C
+        self._inflight = Window(self.prefetch, self._on_handler_error, self._on_wake)
         self._slot_free: Optional[asyncio.Event] = None
         self._idle: Optional[asyncio.Event] = None  # set when the last suspended handler finishes
         self._stop = False
@@ -339,7 +340,7 @@ class Service:
                   and os.environ.get("BEHOLDER_NATIVE_DISPATCH", "1") != "0")
         tracer = self.tracer
         routes = tuple(routes)
-        on_error, on_suspend, on_unroutable = self._on_handler_error, self._on_suspend, self._unroutable
+        on_error, on_suspend, on_unroutable = self._on_handler_error, self._inflight, self._unroutable
         try:
             async for batch in self.source.batches():
                 if native and tracer is not None:
@@ -480,11 +481,11 @@ class Service:
                 self._span(d, "ok" if d.settled else "unsettled")
             return True
         if on_finish is None and not self.trace and span is None:
-            self._on_suspend(d, coro, first)
+            self._inflight.suspend(d, coro, first)
             return False
 
         def done(drv, exc, on_finish=on_finish, d=d, span=span):
-            self._driver_done(drv, exc)
+            self._inflight.release(drv, exc)
             if self.trace:
                 self._span(d, "ok" if d.settled else "unsettled")
             if span is not None:
@@ -492,28 +493,15 @@ class Service:
             if on_finish is not None:
                 on_finish()
         drv = Driver(coro, done, d)
-        self._inflight.add(drv)
+        self._inflight.track(drv)
         drv.start(first)
         return False
 
-    def _on_suspend(self, d, coro, first_yield) -> bool:
-        """A handler awaited real I/O: a native Driver resumes it when the awaited future
-        completes (no asyncio.Task). True = prefetch window full."""
-        drv = Driver(coro, self._driver_done, d)
-        inflight = self._inflight
-        inflight.add(drv)
-        drv.start(first_yield)
-        return len(inflight) >= self.prefetch
-
-    def _driver_done(self, drv, exc) -> None:
-        inflight = self._inflight
-        inflight.discard(drv)
-        if exc is not None and not drv.cancelled:
-            self._on_handler_error(drv.payload, exc)
-        n = len(inflight)
-        if n < self.prefetch and self._slot_free is not None:
+    def _on_wake(self) -> None:
+        """From the native Window: a slot freed after the window was full, or it emptied."""
+        if self._slot_free is not None:
             self._slot_free.set()
-        if not n and self._idle is not None:
+        if not len(self._inflight) and self._idle is not None:
             self._idle.set()
 
     async def _wait_slots(self) -> None:

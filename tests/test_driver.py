@@ -252,3 +252,98 @@ def test_iofuture_sync_callback_errors_go_to_the_loop_handler():
         f.resolve(1)  # must not raise into the protocol callback that resolves it
     run(go())
     assert seen == ["RuntimeError"]
+
+
+# ---- Window: the native in-flight set (the prefetch window) -------------------------
+def test_window_suspend_full_flag_errors_and_wakes():
+    from beholder_amd.ops import Window
+    errors, wakes = [], []
+
+    async def h(fut, fail=False):
+        await fut
+        if fail:
+            raise ValueError("boom")
+
+    async def go():
+        loop = asyncio.get_running_loop()
+        w = Window(3, lambda p, e: errors.append((p, str(e))), lambda: wakes.append(len(w)))
+        futs = [loop.create_future() for _ in range(4)]
+        full = []
+        for i, f in enumerate(futs[:3]):
+            c = h(f, fail=(i == 1))
+            full.append(w.suspend(f"d{i}", c, c.send(None)))
+        assert full == [False, False, True] and len(w) == 3 and w.limit == 3
+        assert sorted(d.payload for d in w) == ["d0", "d1", "d2"]  # iteration is a snapshot
+        futs[1].set_result(None)
+        await asyncio.sleep(0)
+        assert errors == [("d1", "boom")] and wakes == [2]  # full -> not full
+        c = h(futs[3])
+        assert w.suspend("d3", c, c.send(None)) is True
+        futs[0].set_result(None)
+        futs[2].set_result(None)
+        await asyncio.sleep(0)
+        assert wakes == [2, 2]  # one more full -> not full transition, 1 left: no wake
+        futs[3].set_result(None)
+        await asyncio.sleep(0)
+        assert len(w) == 0 and wakes == [2, 2, 0]  # emptied
+        assert w.stats()["suspended"] == 4
+        return w
+
+    w = run(go())
+    assert not w
+
+
+def test_window_cancelled_drivers_are_not_errors_and_tracked_drivers_release():
+    from beholder_amd.ops import Window
+    errors, wakes = [], []
+
+    async def h(fut):
+        await fut
+
+    async def go():
+        loop = asyncio.get_running_loop()
+        w = Window(10, lambda p, e: errors.append(p), lambda: wakes.append(len(w)))
+        f = loop.create_future()
+        c = h(f)
+        w.suspend("a", c, c.send(None))
+        (drv,) = list(w)
+        drv.cancel()
+        await asyncio.sleep(0)
+        assert len(w) == 0 and errors == [] and drv.cancelled  # CancelledError is not a handler error
+        # a Driver with its own on_done, counted against the window via track/release
+        f2 = loop.create_future()
+        c2 = h(f2)
+        done = []
+        d2 = Driver(c2, lambda d, e: (w.release(d, e), done.append(e)), "b")
+        w.track(d2)
+        d2.start(c2.send(None))
+        assert len(w) == 1
+        f2.set_exception(RuntimeError("x"))
+        await asyncio.sleep(0)
+        assert len(w) == 0 and errors == ["b"] and isinstance(done[0], RuntimeError)
+
+    run(go())
+    with pytest.raises(ValueError):
+        __import__("beholder_amd.ops", fromlist=["Window"]).Window(0)
+
+
+def test_window_drops_finished_drivers():
+    from beholder_amd.ops import Window
+
+    async def h(fut):
+        await fut
+
+    async def go():
+        loop = asyncio.get_running_loop()
+        w = Window(100)
+        for _ in range(50):
+            f = loop.create_future()
+            c = h(f)
+            w.suspend(None, c, c.send(None))
+            f.set_result(1)
+        await asyncio.sleep(0)
+        assert len(w) == 0
+
+    run(go())
+    gc.collect()
+    assert not [o for o in gc.get_objects() if type(o).__name__ == "Driver"]
