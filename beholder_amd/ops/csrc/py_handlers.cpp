@@ -44,7 +44,8 @@ PyObject *s_ack, *s_message, *s_content, *s_mediaId, *s_status, *s_progress, *s_
     *s_token, *s_base_url, *s_http, *s_timeout, *s_strict, *s_stats, *s_request, *s_params, *s_POST, *s_PUT,
     *s_record, *s_raise_for_status, *s_rows, *s_get_calls, *s_update_calls, *s_limiter, *s_retry,
     *s_hooks_plan, *s_telegram, *s_emby, *s_name, *s_metadataId, *s_GET, *s_chat_id, *s_parse_mode,
-    *s_markdown, *s_api_key, *s_send_message, *s_refresh_library, *kw_params_timeout, *kw_timeout;
+    *s_markdown, *s_api_key, *s_send_message, *s_refresh_library, *s_pool, *s_select, *s_update,
+    *s_execute, *kw_params_timeout, *kw_timeout;
 // log message literals (index.js:51,133,150)
 PyObject *m_progress, *m_status_kw, *m_percent, *m_creating, *m_with_text, *m_failed_progress, *m_failed_hooks;
 
@@ -76,6 +77,8 @@ struct HandlersObject {
   PyObject* telegram_cls;   // sinks.telegram.TelegramClient (exact type: request built here)
   PyObject* emby_cls;       // sinks.emby.EmbyClient (exact type: request built here)
   PyObject* memory_cls;     // store.memory.MemoryStore (exact type: row read here)
+  PyObject* pg_cls;         // store.postgres.PostgresStore (exact type: queries issued here)
+  PyObject* row_to_media;   // store.postgres.row_to_media (rows that are not all-int / NULL-free)
   PyObject* not_found;      // store.base.MediaNotFound
   PyObject* one;            // TRELLO_CREATOR (index.js:79)
   PyObject* two;            // pos: 2 (index.js:85)
@@ -101,6 +104,7 @@ struct CallObject {
   PyObject* req_stats;  // sink stats of the request in flight (native path), may be NULL
   int64_t req_t0;
   uint8_t req_native;   // a sink request built here is in flight: request_finish() applies
+  uint8_t pg_get;       // a Postgres getByID issued here is in flight: pg_media() applies
   uint8_t req_strict;
   uint8_t kind;
   uint8_t state;
@@ -254,6 +258,61 @@ bool raise_to_lower_case(HandlersObject* hs) {
   return false;
 }
 
+// The stock Postgres store with an open pool: `pool.execute(sql, params)` issued here (the
+// store's own coroutine is skipped). 2 = not applicable (use the store's API), else as await_start.
+int pg_execute(CallObject* c, PyObject* store, PyObject* sql_name, PyObject* params, PyObject** out) {
+  HandlersObject* hs = c->hs;
+  if (reinterpret_cast<PyObject*>(Py_TYPE(store)) != hs->pg_cls) return 2;
+  PyObject** dp = _PyObject_GetDictPtr(store);
+  PyObject* sd = dp ? *dp : nullptr;
+  PyObject* pool = sd ? PyDict_GetItemWithError(sd, s_pool) : nullptr;
+  PyObject* sql = pool ? PyDict_GetItemWithError(sd, sql_name) : nullptr;
+  if (PyErr_Occurred()) return -1;
+  if (!pool || pool == Py_None || !sql) return 2;  // not connected yet: the store connects first
+  PyObject* args[3] = {pool, sql, params};
+  Py_INCREF(pool);  // the call may drop the store's reference (a reconnect)
+  PyObject* aw = PyObject_VectorcallMethod(s_execute, args, 3, nullptr);
+  Py_DECREF(pool);
+  if (!aw) return -1;
+  return await_start(c, aw, out);
+}
+
+// (rows, tag) of the media SELECT -> Media (store/postgres.py get_by_id + row_to_media).
+// Takes and returns a reference; NULL = raised.
+PyObject* pg_media(CallObject* c, PyObject* res) {
+  HandlersObject* hs = c->hs;
+  PyObject* rows = PyTuple_Check(res) && PyTuple_GET_SIZE(res) == 2 ? PyTuple_GET_ITEM(res, 0) : nullptr;
+  if (!rows || !PyList_Check(rows)) {
+    Py_DECREF(res);
+    PyErr_SetString(PyExc_TypeError, "unexpected Postgres result");
+    return nullptr;
+  }
+  if (PyList_GET_SIZE(rows) == 0) {
+    Py_DECREF(res);
+    PyErr_SetObject(hs->not_found, c->media_id);
+    return nullptr;
+  }
+  PyObject* r = PyList_GET_ITEM(rows, 0);
+  Py_INCREF(r);
+  Py_DECREF(res);
+  bool fast = hs->media_cls && PyTuple_CheckExact(r) && PyTuple_GET_SIZE(r) == 10;
+  for (Py_ssize_t i = 0; fast && i < 10; ++i) {
+    PyObject* v = PyTuple_GET_ITEM(r, i);
+    bool is_int_col = i == 2 || i == 4 || i == 5 || i == 7 || i == 9;
+    if (v == Py_None || (is_int_col && !PyLong_CheckExact(v))) fast = false;
+  }
+  PyObject* m;
+  if (fast) {  // Media._make(r)
+    PyObject* args = PyTuple_Pack(1, r);
+    m = args ? PyTuple_Type.tp_new(reinterpret_cast<PyTypeObject*>(hs->media_cls), args, nullptr) : nullptr;
+    Py_XDECREF(args);
+  } else {
+    m = PyObject_CallOneArg(hs->row_to_media, r);
+  }
+  Py_DECREF(r);
+  return m;
+}
+
 // media = await db.getByID(mediaId). The in-memory store's row read (store/memory.py
 // get_by_id_nowait) runs inline; other stores go through their nowait accessor or the coroutine.
 int get_media(CallObject* c, PyObject** out) {
@@ -281,6 +340,15 @@ int get_media(CallObject* c, PyObject** out) {
       return 1;
     }
     if (PyErr_Occurred()) return -1;
+  }
+  PyObject* params = PyTuple_Pack(1, c->media_id);
+  if (!params) return -1;
+  int k = pg_execute(c, store, s_select, params, out);
+  Py_DECREF(params);
+  if (k != 2) {
+    if (k == 0) c->pg_get = 1;
+    if (k == 1 && !(*out = pg_media(c, *out))) return -1;
+    return k;
   }
   PyObject* get = hattr(hs, s_get_nowait);
   if (!get) return -1;
@@ -722,6 +790,10 @@ PySendResult step_progress(CallObject* c, PyObject* value, PyObject** result) {
       goto have_media;
     }
     case 1:
+      if (c->pg_get) {
+        c->pg_get = 0;
+        if (value) value = pg_media(c, value);
+      }
       if (!value) goto catch_;
       c->media = value;
     have_media: {
@@ -831,6 +903,24 @@ PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
       int inl = update_inline(c);  // index.js:68
       if (inl < 0) return fail(c);
       if (inl) goto updated;
+      if (PyLong_CheckExact(c->status)) {  // Postgres: UPDATE ... SET status = int(status)
+        PyObject* store = hattr(hs, s_store);
+        if (!store) return fail(c);
+        PyObject* params = PyTuple_Pack(2, c->status, c->media_id);
+        if (!params) return fail(c);
+        k = pg_execute(c, store, s_update, params, &v);
+        Py_DECREF(params);
+        if (k < 0) return fail(c);
+        if (k == 0) {
+          c->state = 1;
+          *result = v;
+          return PYGEN_NEXT;
+        }
+        if (k == 1) {
+          Py_DECREF(v);
+          goto updated;
+        }
+      }
       PyObject* upd = hattr(hs, s_update_nowait);
       if (!upd) return fail(c);
       if (upd != Py_None) {
@@ -875,6 +965,10 @@ PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
       goto have_media;
     }
     case 2:
+      if (c->pg_get) {
+        c->pg_get = 0;
+        if (value) value = pg_media(c, value);
+      }
       if (!value) return fail(c);
       c->media = value;
     have_media: {  // TRELLO Movement, index.js:78-90
@@ -1206,6 +1300,7 @@ PyObject* make_call(HandlersObject* hs, PyObject* rmsg, uint8_t kind) {
   c->plan = nullptr;
   c->req_t0 = 0;
   c->req_native = c->req_strict = 0;
+  c->pg_get = 0;
   c->kind = kind;
   c->state = 0;
   c->started = c->done = c->did_suspend = 0;
@@ -1248,6 +1343,8 @@ int hs_traverse(HandlersObject* hs, visitproc visit, void* arg) {
   Py_VISIT(hs->telegram_cls);
   Py_VISIT(hs->emby_cls);
   Py_VISIT(hs->memory_cls);
+  Py_VISIT(hs->pg_cls);
+  Py_VISIT(hs->row_to_media);
   Py_VISIT(hs->not_found);
   return 0;
 }
@@ -1277,6 +1374,8 @@ int hs_clear(HandlersObject* hs) {
   Py_CLEAR(hs->telegram_cls);
   Py_CLEAR(hs->emby_cls);
   Py_CLEAR(hs->memory_cls);
+  Py_CLEAR(hs->pg_cls);
+  Py_CLEAR(hs->row_to_media);
   Py_CLEAR(hs->not_found);
   return 0;
 }
@@ -1406,6 +1505,9 @@ int hs_init(HandlersObject* hs, PyObject* args, PyObject* kwds) {
   hs->emby_cls = hs->telegram_cls ? import_attr("beholder_amd.sinks.emby", "EmbyClient") : nullptr;
   hs->memory_cls = hs->emby_cls ? import_attr("beholder_amd.store.memory", "MemoryStore") : nullptr;
   hs->not_found = hs->memory_cls ? import_attr("beholder_amd.store.base", "MediaNotFound") : nullptr;
+  hs->pg_cls = hs->not_found ? import_attr("beholder_amd.store.postgres", "PostgresStore") : nullptr;
+  hs->row_to_media = hs->pg_cls ? import_attr("beholder_amd.store.postgres", "row_to_media") : nullptr;
+  if (!hs->row_to_media) return -1;
   if (!hs->not_found) return -1;
   static const char* pnames[4] = {"mediaId", "status", "progress", "host"};
   if (!codec_slots(hs->decode_s, pnames, 2, &hs->res_s, hs->ix_s) ||
@@ -1509,6 +1611,10 @@ int init_handler_types(PyObject* m) {
               {&s_api_key, "api_key"},
               {&s_send_message, "send_message"},
               {&s_refresh_library, "refresh_library"},
+              {&s_pool, "_pool"},
+              {&s_select, "_select"},
+              {&s_update, "_update"},
+              {&s_execute, "execute"},
               {&s_retry, "retry"},
               {&m_progress, "processing progress update on media"},
               {&m_status_kw, "status"},

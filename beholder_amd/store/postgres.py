@@ -23,6 +23,15 @@ _COLS = "id, name, creator, creator_id, type, source, source_uri, metadata, meta
 _IDENT = re.compile(r"^[A-Za-z_][A-Za-z0-9_]*(\.[A-Za-z_][A-Za-z0-9_]*)?$")
 
 
+def row_to_media(r) -> Media:
+    """One ``SELECT {_COLS}`` row as a Media (NULL text -> "", NULL/str numbers -> int). The
+    compiled handlers (ops/csrc/py_handlers.cpp) take the all-int, no-NULL case themselves."""
+    if None not in r and type(r[2]) is type(r[4]) is type(r[5]) is type(r[7]) is type(r[9]) is int:
+        return Media._make(r)  # int columns arrived as int4/int8: no per-field conversion
+    return Media(*(("" if v is None else v) if i in (0, 1, 3, 6, 8) else (0 if v is None else int(v))
+                   for i, v in enumerate(r)))
+
+
 class PostgresStore(MediaStore):
     name = "postgres"
 
@@ -73,11 +82,7 @@ class PostgresStore(MediaStore):
         rows, _ = await pool.execute(self._select, (media_id,))
         if not rows:
             raise MediaNotFound(media_id)
-        r = rows[0]
-        if None not in r and type(r[2]) is type(r[4]) is type(r[5]) is type(r[7]) is type(r[9]) is int:
-            return Media._make(r)  # int columns arrived as int4/int8: no per-field conversion
-        return Media(*(("" if v is None else v) if i in (0, 1, 3, 6, 8) else (0 if v is None else int(v))
-                       for i, v in enumerate(r)))
+        return row_to_media(rows[0])
 
     async def upsert(self, media: Media) -> None:
         await self._exec(

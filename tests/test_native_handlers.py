@@ -268,3 +268,62 @@ def test_reference_node_harness_runs_the_reference():
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__)))).stdout
     res = json.loads(out)["reference_node"]
     assert res["events"] == 4000 and res["handler_errors"] == 0 and res["http_requests"] > 0
+
+
+@pytest.mark.parametrize("concurrent", [False, True])
+def test_native_matches_python_over_postgres(concurrent):
+    """The compiled handlers issue the store's UPDATE / SELECT themselves on the stock Postgres
+    store (no store coroutine). Same stream, same rows, over the wire protocol (tests/pg_fake.py):
+    identical deliveries, log lines, HTTP calls, counters and final table contents."""
+    from pg_fake import FakePg
+    from beholder_amd.store.postgres import PostgresStore
+    from helpers import api_media, trello_media
+
+    rows = [trello_media("m1", "UPLOADING", card="C1"), api_media("m2", "QUEUED"),
+            trello_media("m3", "DEPLOYED", card="C3", name="Ü & ?")]
+    evs = [("status", "m1", 4), ("progress", "m1", 2, 40, "w1"), ("progress", "m2", 1, 5, ""),
+           ("status", "m2", 4), ("status", "missing", 1), ("progress", "missing", 1, 1, ""),
+           ("status", "m3", 7), ("progress", "m3", 9, 3, "h"), ("status", "garbage", b"\x08\xff"),
+           ("progress", "m1", 3, 100, "w2"), ("status", "m3", 1)]
+
+    async def trace(impl):
+        pg = await FakePg(auth="trust").start()
+        try:
+            st = PostgresStore(pg.dsn, create_schema=True)
+            await st.connect()
+            for m in rows:
+                await st.upsert(m)
+            helpers.HANDLER_IMPL = impl
+            try:
+                r = Rig(medias=[])
+            finally:
+                helpers.HANDLER_IMPL = "python"
+            r.h.store = st
+            target = native_handlers(r.h) if impl == "native" else r.h
+            ds = [(ev[0], r.delivery(1 if ev[0] == "status" else 2, _encode(ev))) for ev in evs]
+
+            async def one(kind, d):
+                try:
+                    await (target.on_status(d) if kind == "status" else target.on_progress(d))
+                except Exception as e:  # noqa: BLE001
+                    return f"{type(e).__name__}: {e}"
+            if concurrent:
+                errs = await asyncio.gather(*(one(k, d) for k, d in ds))
+            else:
+                errs = [await one(k, d) for k, d in ds]
+            table = sorted([await st.get_by_id(m.id) for m in rows])
+            stats = target.stats() if impl == "native" else None
+            await st.close()
+            r.log.flush()
+            return {"deliveries": [(d.state, e) for (_, d), e in zip(ds, errs)],
+                    "logs": [(x["level"], x["msg"]) for x in r.stream.records()], "http": list(r.http.calls),
+                    "progress": sorted(r.progress.values().items()), "comments": r.comments.get(),
+                    "table": table}, stats
+        finally:
+            await pg.stop()
+
+    got, stats = asyncio.run(trace("native"))
+    want, _ = asyncio.run(trace("python"))
+    assert got == want
+    assert stats["suspended"] > 0  # the native path really waited on the wire
+    assert any(e and "MediaNotFound" in e for _, e in got["deliveries"])
