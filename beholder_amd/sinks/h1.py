@@ -328,8 +328,21 @@ class H1Client(HttpClient):
             if o.auth:
                 head += f"Authorization: {o.auth}\r\n"
             req = head.encode("latin-1") + (self._tail_cl0 if m in _BODY_METHODS else self._tail)
+            c = None
+            if not fresh:  # fast path of _acquire: a live idle keep-alive connection, no await
+                idle = o.idle
+                if idle:
+                    now = time.monotonic()
+                    while idle:
+                        cand = idle.pop()
+                        if not cand.closed and now - cand.last_used < self.keepalive_s:
+                            counts["reused"] += 1
+                            c = cand
+                            break
+                        self._drop(cand)
             try:
-                c = await self._acquire(o, deadline, fresh)
+                if c is None:
+                    c = await self._acquire(o, deadline, fresh)
             except asyncio.TimeoutError:
                 counts["timeouts"] += 1
                 counts["errors"] += 1
@@ -379,7 +392,7 @@ class H1Client(HttpClient):
                     cur = urljoin(cur, loc)
                     fresh = False
                     continue
-            return HttpResponse(status, body, url=full, raw_headers=raw)
+            return HttpResponse(status, body, None, full, raw)
 
     def stats(self) -> Dict[str, int]:
         out = dict(self.counts)
