@@ -37,7 +37,8 @@ from urllib.parse import quote, unquote, urljoin
 
 from ..ops import H1Parser
 from ..ops import IOFuture as _IOFuture
-from .http import HttpClient, HttpError, HttpResponse, redact, with_query
+from ..ops import encode_query as _encode_query
+from .http import HttpClient, HttpError, HttpResponse, encode_query, redact, with_query
 
 _IDEMPOTENT = frozenset(("GET", "HEAD", "PUT", "DELETE", "OPTIONS"))
 _BODY_METHODS = frozenset(("POST", "PUT", "PATCH", "DELETE"))
@@ -174,6 +175,7 @@ class H1Client(HttpClient):
         self.max_redirects = int(max_redirects)
         self._ssl = ssl_context
         self._origins: Dict[str, _Origin] = {}
+        self._routes: Dict[str, Tuple[_Origin, str, str]] = {}
         self._closed = False
         self._busy: set = set()
         self._sweeper = None
@@ -307,11 +309,46 @@ class H1Client(HttpClient):
             self._arm(loop)
 
     # -- request -------------------------------------------------------------
+    def _resolve(self, url: str) -> Tuple[_Origin, str, str]:
+        """``(origin, request target, rest of the request line + Host/Authorization lines)``."""
+        key, target = _split_url(url)
+        o = self._origin(key)
+        if not target.isascii() or " " in target:
+            target = quote(target, safe=_PATH_SAFE)
+        rest = f" HTTP/1.1\r\nHost: {o.host_header}\r\n"
+        if o.auth:
+            rest += f"Authorization: {o.auth}\r\n"
+        return o, target, rest
+
+    def _route(self, url: str) -> Tuple[_Origin, str, str]:
+        """:meth:`_resolve` of a URL without query or fragment, cached per client (a sink calls
+        a handful of base URLs; the per-event part rides in ``params``)."""
+        r = self._routes.get(url)
+        if r is None:
+            r = self._resolve(url)
+            if len(self._routes) >= 4096:
+                self._routes.clear()
+            self._routes[url] = r
+        return r
+
+    def _prepare(self, url: str, params) -> Tuple[str, _Origin, str, str]:
+        """``(full URL, *_resolve(full URL))`` for ``url`` + ``params``."""
+        if "?" in url or "#" in url:
+            full = with_query(url, params)
+            return (full, *self._resolve(full))
+        # the sinks' shape: a cached route + an encodeURIComponent query (ASCII, no spaces: the
+        # quoting of _resolve would leave it as is)
+        o, target, rest = self._route(url)
+        q = _encode_query(params) if type(params) is dict and params else encode_query(params)
+        if q:
+            return f"{url}?{q}", o, f"{target}?{q}", rest
+        return url, o, target, rest
+
     async def request(self, method, url, *, params=None, timeout=None) -> HttpResponse:
         if self._closed:
             raise HttpError("client closed")
         m = method.upper()
-        full = with_query(url, params)
+        full, o, target, rest = self._prepare(url, params)
         loop = asyncio.get_running_loop()
         deadline = loop.time() + (timeout or self.timeout_s)
         counts = self.counts
@@ -320,14 +357,7 @@ class H1Client(HttpClient):
         redirects = 0
         fresh = False
         while True:
-            key, target = _split_url(cur)
-            o = self._origin(key)
-            if not target.isascii() or " " in target:
-                target = quote(target, safe=_PATH_SAFE)
-            head = f"{m} {target} HTTP/1.1\r\nHost: {o.host_header}\r\n"
-            if o.auth:
-                head += f"Authorization: {o.auth}\r\n"
-            req = head.encode("latin-1") + (self._tail_cl0 if m in _BODY_METHODS else self._tail)
+            req = f"{m} {target}{rest}".encode("latin-1") + (self._tail_cl0 if m in _BODY_METHODS else self._tail)
             c = None
             if not fresh:  # fast path of _acquire: a live idle keep-alive connection, no await
                 idle = o.idle
@@ -390,6 +420,7 @@ class H1Client(HttpClient):
                         counts["errors"] += 1
                         raise HttpError(f"Exceeded maxRedirects. Probably stuck in a redirect loop {redact(cur)}")
                     cur = urljoin(cur, loc)
+                    o, target, rest = self._resolve(cur)
                     fresh = False
                     continue
             return HttpResponse(status, body, None, full, raw)

@@ -12,7 +12,7 @@ from hypothesis import given, settings, strategies as st
 
 from beholder_amd.ops import H1Parser
 from beholder_amd.sinks import H1Client, HttpError
-from beholder_amd.sinks.http import parse_raw_headers
+from beholder_amd.sinks.http import parse_raw_headers, with_query
 
 
 def run(coro):
@@ -468,3 +468,25 @@ def test_service_uses_h1_client_by_default():
     from beholder_amd.sinks import AiohttpClient
     assert isinstance(make_http_client({}), H1Client)
     assert isinstance(make_http_client({"client": "aiohttp"}), AiohttpClient)
+
+
+@settings(max_examples=400, deadline=None)
+@given(st.sampled_from(["http://h", "https://u:p@h:8443", "http://[::1]:80"]),
+       st.text(alphabet="/ab c%é#?&=-_", max_size=12),
+       st.one_of(st.none(), st.dictionaries(st.sampled_from(["text", "key", "a b", "é"]),
+                                            st.one_of(st.text(max_size=8), st.integers(), st.none()), max_size=3)))
+def test_cached_route_gives_the_uncached_request_target(origin, path, params):
+    """The per-URL route cache (query appended after the cached, already quoted path) builds the
+    same URL, origin and request line as resolving the full URL from scratch."""
+    c = H1Client()
+    url = origin + path
+    try:
+        want = c._resolve(with_query(url, params))
+    except HttpError:  # e.g. "https://u:p@h:8443=": both ways refuse it
+        with pytest.raises(HttpError):
+            c._prepare(url, params)
+        return
+    for _ in range(2):  # second time from the cache
+        full, o, target, rest = c._prepare(url, params)
+        assert full == with_query(url, params)
+        assert (o, target, rest) == want
