@@ -244,6 +244,52 @@ def test_native_calls_do_not_leak():
     assert not [o for o in gc.get_objects() if type(o).__name__ == "HandlerCall"]
 
 
+@pytest.mark.parametrize("store_kind", sorted(STORES))
+def test_native_error_paths_do_not_leak_memory(store_kind):
+    """tracemalloc over every branch, failures included: sink errors (raised and HTTP 500),
+    DEPLOYED hooks, missing media, undecodable bodies, store errors that escape (Q1), suspension.
+    Unlike the object count above, this also sees leaked strings, bytes and floats."""
+    import tracemalloc
+
+    from beholder_amd.utils.log import Logger, NullStream
+
+    c = cfg({"instance": {"telegram": {"enabled": True, "channel": "-1001"},
+                          "emby": {"enabled": True, "host": "http://emby:8096"}}})
+    rows = [helpers.trello_media("m1"), helpers.api_media("m2"), helpers.trello_media("x1")]
+    r = Rig(config=c, medias=rows, http=RecordingHttpClient(keep=16))
+    r.h.store = STORES[store_kind](rows)
+    r.h.log = Logger(stream=NullStream())
+    r.http.fail("POST", "https://api.trello.com")  # comment raises (Q7: logged, acked)
+    r.http.fail("GET", "https://api.telegram.org", status=500)  # hook error is swallowed
+    nh = native_handlers(r.h)
+    bodies = [(2, progress_msg("m1", "UPLOADING", 7, "w")), (2, progress_msg("missing", "QUEUED", 1)),
+              (2, b"\xff\x01"), (1, status_msg("m1", "DEPLOYED")), (1, status_msg("m2", "DEPLOYED")),
+              (1, status_msg("x1", "CONVERTING")), (1, status_msg("missing", "QUEUED")), (1, b"\xff")]
+
+    async def go(n):
+        for i in range(n):
+            t, b = bodies[i % len(bodies)]
+            call = nh.on_status(r.delivery(t, b)) if t == 1 else nh.on_progress(r.delivery(t, b))
+            try:
+                await call
+            except Exception:  # noqa: BLE001 - status errors escape by design (Q1)
+                pass
+
+    asyncio.run(go(800))  # warm caches
+    gc.collect()
+    tracemalloc.start()
+    try:
+        asyncio.run(go(800))
+        gc.collect()
+        base = tracemalloc.get_traced_memory()[0]
+        asyncio.run(go(8000))
+        gc.collect()
+        grown = tracemalloc.get_traced_memory()[0] - base
+    finally:
+        tracemalloc.stop()
+    assert grown < 64 * 1024, f"{grown} bytes kept after 8000 more calls"
+
+
 def test_subclass_keeps_python_path():
     from beholder_amd.handlers import TelemetryHandlers
 
