@@ -1,9 +1,12 @@
-"""Build the native runtime in-tree (``beholder_amd/ops/_native*.so``).
+"""Build the native runtime in-tree (``beholder_amd/ops/_native*.so``) and the HIP offload
+probe (``beholder_amd/ops/hip/libbeholder_hip.so``, gfx950).
 
 Beholder's runtime around the Python handlers (ingest reader thread, ring,
 codec, deliveries, histograms) is C++ — see ``csrc/``. The service has no
-device kernels (the reference has none), so this is a host
-build with the system C++ compiler; ``__graft_entry__.build()`` calls it.
+device kernels in its event path (the reference has none), so the runtime is a
+host build with the system C++ compiler. ``build_hip`` compiles the batched-decode kernel that
+``scripts/gpu_offload_probe.py`` measures against it (``ops/gpu_decode.py``).
+``__graft_entry__.build()`` calls both.
 
 Usage: ``python -m beholder_amd.ops.build [--debug] [--sanitize=address,undefined]`` (thin CLI over this module)
 """
@@ -89,14 +92,59 @@ def build(force: bool = False, debug: bool = False, sanitize: str = "", cxx: str
     return TARGET
 
 
+HIP_DIR = os.path.join(HERE, "hip")
+HIP_TARGET = os.path.join(HIP_DIR, "libbeholder_hip.so")
+HIP_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
+             "-Wall", "-Wextra"]
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC", ""), "/opt/rocm/bin/hipcc"):
+        if c and os.path.exists(c):
+            return c
+    import shutil
+    return shutil.which("hipcc") or ""
+
+
+def build_hip(force: bool = False, verbose: bool = False) -> str:
+    """Compile ``ops/hip/*.hip`` for gfx950 into one shared library (cached by source hash)."""
+    cc = hipcc()
+    if not cc:
+        raise RuntimeError("hipcc not found (ROCm is required to build the HIP extension)")
+    srcs = sorted(glob.glob(os.path.join(HIP_DIR, "*.hip")))
+    h = hashlib.sha256(" ".join(HIP_FLAGS).encode())
+    for p in srcs:
+        with open(p, "rb") as f:
+            h.update(os.path.basename(p).encode())
+            h.update(f.read())
+    digest = h.hexdigest()
+    stamp = HIP_TARGET + ".srchash"
+    if not force and os.path.exists(HIP_TARGET) and os.path.exists(stamp):
+        with open(stamp) as f:
+            if f.read().strip() == digest:
+                return HIP_TARGET
+    tmp = HIP_TARGET + ".tmp"
+    cmd = [cc, *HIP_FLAGS, *srcs, "-o", tmp]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, HIP_TARGET)
+    with open(stamp, "w") as f:
+        f.write(digest)
+    return HIP_TARGET
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--sanitize", default="")
     ap.add_argument("--cxx", default="")
+    ap.add_argument("--no-hip", action="store_true", help="skip the gfx950 HIP extension")
     a = ap.parse_args(argv)
     print(build(force=a.force, debug=a.debug, sanitize=a.sanitize, cxx=a.cxx, verbose=True))
+    if not a.no_hip and not a.sanitize:
+        print(build_hip(force=a.force, verbose=True))
     return 0
 
 

@@ -1,0 +1,162 @@
+"""Batched telemetry decode on the GPU (``ops/hip/telemetry_decode.hip``): the offload probe.
+
+The service decodes each event on the CPU as it arrives (``ops/csrc/py_codec.cpp``; the
+``decode`` of index.js:63,129). This module is the measured alternative. It packs a batch of
+message bodies, copies it to the device, decodes every message in one kernel (one lane per
+message) and returns an ``(n, 8)`` int32 table:
+``[id_off, id_len, status, progress, host_off, host_len, ok, fields_seen]``.
+
+``scripts/gpu_offload_probe.py`` prices this path against the CPU decode; docs/DESIGN.md
+("Why there are no HIP kernels") cites the result. :func:`reference_decode` is the plain-Python
+definition of the table, and the GPU tests compare the kernel against it.
+
+The extension is built in-tree by ``beholder_amd._build.build_hip`` (hipcc, gfx950) and loaded
+with ctypes after ``import torch``. torch's HIP runtime has the same soname, so the kernel
+launches on torch's runtime and stream. A missing library raises; there is no CPU fallback
+behind :func:`decode_batch`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "hip", "libbeholder_hip.so")
+FIELDS = ("id_off", "id_len", "status", "progress", "host_off", "host_len", "ok", "seen")
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """The HIP extension (raises if it was not built: no silent fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m beholder_amd.ops.build`")
+        import torch  # noqa: F401  load torch's libamdhip64 first so the kernel shares its runtime
+        _lib = ctypes.CDLL(LIB_PATH)
+        _lib.bh_decode_telemetry.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                             ctypes.c_void_p]
+        _lib.bh_decode_telemetry.restype = ctypes.c_int
+    return _lib
+
+
+def pack(bodies: Sequence[bytes]) -> Tuple[bytes, np.ndarray]:
+    """Concatenated bodies and their ``n + 1`` int32 boundaries."""
+    offs = np.zeros(len(bodies) + 1, dtype=np.int32)
+    np.cumsum([len(b) for b in bodies], out=offs[1:])
+    return b"".join(bodies), offs
+
+
+def check_layout(nbytes: int, offs: np.ndarray) -> None:
+    """The kernel trusts ``offs``: validate it on the host before any launch."""
+    if offs.ndim != 1 or offs.dtype != np.int32 or len(offs) < 1:
+        raise ValueError("offs must be a 1-D int32 array of n + 1 boundaries")
+    if offs[0] != 0 or offs[-1] != nbytes or (len(offs) > 1 and np.any(np.diff(offs) < 0)):
+        raise ValueError("offs must start at 0, never decrease and end at len(buf)")
+    if nbytes >= 2 ** 31:
+        raise ValueError("batch too large for int32 offsets")
+
+
+def decode_batch(buf_dev, offs_dev, n: int, out_dev=None):
+    """Decode ``n`` messages already on the device (uint8 ``buf_dev``, int32 ``offs_dev`` of
+    ``n + 1`` host-checked boundaries) on the current torch stream. Returns the ``(n, 8)`` int32
+    table (``out_dev`` if given)."""
+    import torch
+    if buf_dev.dtype != torch.uint8 or offs_dev.dtype != torch.int32 or offs_dev.numel() != n + 1:
+        raise ValueError("decode_batch needs uint8 buf, int32 offs of n + 1")
+    if not (buf_dev.is_cuda and offs_dev.is_cuda and buf_dev.is_contiguous() and offs_dev.is_contiguous()):
+        raise ValueError("decode_batch needs contiguous device tensors")
+    if out_dev is None:
+        out_dev = torch.empty((n, 8), dtype=torch.int32, device=buf_dev.device)
+    elif out_dev.shape != (n, 8) or out_dev.dtype != torch.int32 or not out_dev.is_contiguous():
+        raise ValueError("out must be a contiguous (n, 8) int32 tensor")
+    if n == 0:
+        return out_dev
+    stream = torch.cuda.current_stream(buf_dev.device).cuda_stream
+    err = lib().bh_decode_telemetry(buf_dev.data_ptr(), offs_dev.data_ptr(), n, out_dev.data_ptr(), stream)
+    if err:
+        raise RuntimeError(f"bh_decode_telemetry launch failed: hipError {err}")
+    return out_dev
+
+
+def decode_bodies(bodies: Sequence[bytes], device="cuda"):
+    """Host bodies → host ``(n, 8)`` numpy table through the GPU (tests; the probe times the steps)."""
+    import torch
+    buf, offs = pack(bodies)
+    check_layout(len(buf), offs)
+    b = torch.frombuffer(bytearray(buf), dtype=torch.uint8).to(device) if buf else \
+        torch.zeros(1, dtype=torch.uint8, device=device)
+    o = torch.from_numpy(offs).to(device)
+    out = decode_batch(b, o, len(bodies))
+    return out.cpu().numpy()
+
+
+def _varint(p: bytes, i: int, end: int):
+    v = 0
+    for shift in range(0, 70, 7):
+        if i >= end:
+            return None, i
+        b = p[i]
+        i += 1
+        v |= (b & 0x7F) << shift
+        if not b & 0x80:
+            return v & 0xFFFFFFFFFFFFFFFF, i  # the kernel's uint64 keeps the low 64 bits
+    return None, i
+
+
+def _i32(v: int) -> int:
+    v &= 0xFFFFFFFF
+    return v - (1 << 32) if v >= 1 << 31 else v
+
+
+def reference_decode(buf: bytes, start: int, end: int) -> List[int]:
+    """Plain-Python definition of one kernel output row (same rules as the kernel's header)."""
+    i = start
+    r = [0, 0, 0, 0, 0, 0, 1, 0]
+    while i < end:
+        key, i = _varint(buf, i, end)
+        if key is None or key >> 3 == 0:
+            r[6] = 0
+            break
+        field, wt = key >> 3, key & 7
+        if wt == 0:
+            v, i = _varint(buf, i, end)
+            if v is None:
+                r[6] = 0
+                break
+            if field == 2:
+                r[2] = _i32(v)
+                r[7] |= 2
+            elif field == 3:
+                r[3] = _i32(v)
+                r[7] |= 4
+        elif wt == 2:
+            n, i = _varint(buf, i, end)
+            if n is None or n > end - i:
+                r[6] = 0
+                break
+            if field == 1:
+                r[0], r[1] = i, n
+                r[7] |= 1
+            elif field == 4:
+                r[4], r[5] = i, n
+                r[7] |= 8
+            i += n
+        elif wt in (1, 5):
+            w = 8 if wt == 1 else 4
+            if end - i < w:
+                r[6] = 0
+                break
+            i += w
+        else:
+            r[6] = 0
+            break
+    return r
+
+
+def reference_table(bodies: Sequence[bytes]) -> np.ndarray:
+    buf, offs = pack(bodies)
+    return np.array([reference_decode(buf, int(offs[k]), int(offs[k + 1])) for k in range(len(bodies))],
+                    dtype=np.int32).reshape(len(bodies), 8)

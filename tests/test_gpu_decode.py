@@ -1,0 +1,106 @@
+"""The HIP batched decode (ops/hip/telemetry_decode.hip, ops/gpu_decode.py), the GPU-offload probe.
+
+CPU tests pin the plain-Python row definition (``reference_decode``) to the service's own codec
+on valid messages and check the host-side guards. GPU tests compare the kernel's table against
+that reference on valid, random and truncated inputs."""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+import pytest
+from hypothesis import given, settings, strategies as st
+
+from beholder_amd import ops
+from beholder_amd.bench.generator import Workload
+from beholder_amd.models import proto
+from beholder_amd.ops import gpu_decode as gd
+
+PROGRESS = ops.codec_for(proto.load("api.TelemetryProgress"))
+STATUS = ops.codec_for(proto.load("api.TelemetryStatus"))
+
+messages = st.builds(
+    lambda mid, status, progress, host: PROGRESS.encode(
+        {"mediaId": mid, "status": status, "progress": progress, "host": host}),
+    st.text(max_size=40), st.integers(0, 5), st.integers(-2 ** 31, 2 ** 31 - 1), st.text(max_size=12))
+
+
+def _fields(buf: bytes, row) -> tuple:
+    io, il, status, progress, ho, hl, ok, _ = (int(x) for x in row)
+    return buf[io:io + il].decode(), status, progress, buf[ho:ho + hl].decode(), ok
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.lists(messages, min_size=1, max_size=6))
+def test_reference_row_matches_the_service_codec(bodies):
+    buf, offs = gd.pack(bodies)
+    for k, b in enumerate(bodies):
+        m = PROGRESS.decode(b)
+        row = gd.reference_decode(buf, int(offs[k]), int(offs[k + 1]))
+        assert _fields(buf, row) == (m.mediaId, m.status, m.progress, m.host, 1)
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.lists(st.binary(max_size=24), max_size=6))
+def test_reference_never_reads_past_its_message(bodies):
+    buf, offs = gd.pack(bodies)
+    for k in range(len(bodies)):
+        io, il, _, _, ho, hl, _, _ = gd.reference_decode(buf, int(offs[k]), int(offs[k + 1]))
+        for off, ln in ((io, il), (ho, hl)):
+            assert ln == 0 or offs[k] <= off and off + ln <= offs[k + 1]
+
+
+def test_layout_guards_and_loud_missing_library(monkeypatch):
+    buf, offs = gd.pack([b"\n\x01a", b""])
+    gd.check_layout(len(buf), offs)
+    for bad in (np.array([1, 3, 3], np.int32), np.array([0, 3, 2], np.int32), np.array([0, 2, 2], np.int32),
+                np.array([0, 3, 3], np.int64)):
+        with pytest.raises(ValueError):
+            gd.check_layout(len(buf), bad)
+    monkeypatch.setattr(gd, "LIB_PATH", "/nonexistent/libbeholder_hip.so")
+    monkeypatch.setattr(gd, "_lib", None)
+    with pytest.raises(RuntimeError, match="missing"):
+        gd.lib()
+
+
+def _corpus(rng: random.Random) -> list:
+    w = Workload(n_media=64, seed=5)
+    bodies = [b for _, b in w.events(3000)]
+    bodies += [STATUS.encode({"mediaId": f"m{i}", "status": i % 7}) for i in range(200)]
+    for _ in range(500):  # truncations, garbage, unknown fields, empty
+        b = rng.choice(bodies)
+        bodies.append(b[:rng.randrange(len(b) + 1)])
+        bodies.append(bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 30))))
+        bodies.append(b + bytes([0x28, rng.randrange(128), 0x35, 1, 2, 3, 4, 0x39]) + bytes(8))
+    bodies.append(b"")
+    return bodies
+
+
+@pytest.mark.gpu
+def test_kernel_matches_reference_on_valid_random_and_truncated_messages():
+    bodies = _corpus(random.Random(11))
+    got = gd.decode_bodies(bodies)
+    want = gd.reference_table(bodies)
+    assert got.shape == want.shape == (len(bodies), 8)
+    bad = np.nonzero(np.any(got != want, axis=1))[0]
+    assert len(bad) == 0, [(bodies[i], got[i].tolist(), want[i].tolist()) for i in bad[:5]]
+    assert want[:3000, 6].all()  # the workload's messages all decode
+
+
+@pytest.mark.gpu
+def test_kernel_large_batch_and_argument_checks():
+    import torch
+    w = Workload(n_media=256, seed=9)
+    bodies = [b for _, b in w.events(200_000)]
+    got = gd.decode_bodies(bodies)
+    buf, offs = gd.pack(bodies)
+    sample = range(0, len(bodies), 997)
+    for k in sample:
+        assert got[k].tolist() == gd.reference_decode(buf, int(offs[k]), int(offs[k + 1]))
+    assert got[:, 6].all()
+    dev = torch.zeros(4, dtype=torch.uint8, device="cuda")
+    with pytest.raises(ValueError):
+        gd.decode_batch(dev, torch.zeros(3, dtype=torch.int64, device="cuda"), 2)
+    with pytest.raises(ValueError):
+        gd.decode_batch(dev.cpu(), torch.zeros(3, dtype=torch.int32), 2)
+    assert gd.decode_batch(dev, torch.zeros(1, dtype=torch.int32, device="cuda"), 0).shape == (0, 8)
