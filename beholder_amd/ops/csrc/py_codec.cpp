@@ -498,6 +498,66 @@ PyGetSetDef codec_getset[] = {
     {"type_name", reinterpret_cast<getter>(codec_get_type_name), nullptr, "message type name", nullptr},
     {nullptr, nullptr, nullptr, nullptr, nullptr}};
 
+// materialise_table(buf, table) -> [(mediaId, status, progress, host), ...]
+// Host half of the GPU-offload probe (ops/gpu_decode.py): turns the kernel's (n, 8) int32 field
+// table back into the Python values the handlers use. Rows with ok == 0 give None. Offsets are
+// re-checked against len(buf): the table comes from a device and is not trusted.
+PyObject* mod_materialise_table(PyObject*, PyObject* const* a, Py_ssize_t n) {
+  if (n != 2) {
+    PyErr_SetString(PyExc_TypeError, "materialise_table(buf, table)");
+    return nullptr;
+  }
+  Py_buffer b, t;
+  if (PyObject_GetBuffer(a[0], &b, PyBUF_SIMPLE) < 0) return nullptr;
+  if (PyObject_GetBuffer(a[1], &t, PyBUF_FORMAT | PyBUF_C_CONTIGUOUS) < 0) {
+    PyBuffer_Release(&b);
+    return nullptr;
+  }
+  PyObject* out = nullptr;
+  if (t.itemsize != 4 || t.len % 32 != 0) {
+    PyErr_SetString(PyExc_TypeError, "table must be a contiguous (n, 8) int32 buffer");
+  } else {
+    const Py_ssize_t rows = t.len / 32;
+    const int32_t* tab = static_cast<const int32_t*>(t.buf);
+    const char* base = static_cast<const char*>(b.buf);
+    out = PyList_New(rows);
+    for (Py_ssize_t k = 0; out && k < rows; ++k) {
+      const int32_t* r = tab + 8 * k;
+      PyObject* item;
+      if (!r[6]) {
+        item = Py_NewRef(Py_None);
+      } else if (r[0] < 0 || r[1] < 0 || r[4] < 0 || r[5] < 0 || r[0] + int64_t(r[1]) > b.len ||
+                 r[4] + int64_t(r[5]) > b.len) {
+        PyErr_Format(PyExc_ValueError, "row %zd points outside the batch", k);
+        item = nullptr;
+      } else {
+        PyObject* id = PyUnicode_DecodeUTF8(base + r[0], r[1], "replace");
+        PyObject* host = PyUnicode_DecodeUTF8(base + r[4], r[5], "replace");
+        PyObject* st = PyLong_FromLong(r[2]);
+        PyObject* pr = PyLong_FromLong(r[3]);
+        item = (id && host && st && pr) ? PyTuple_Pack(4, id, st, pr, host) : nullptr;
+        Py_XDECREF(id);
+        Py_XDECREF(host);
+        Py_XDECREF(st);
+        Py_XDECREF(pr);
+      }
+      if (!item) {
+        Py_CLEAR(out);
+        break;
+      }
+      PyList_SET_ITEM(out, k, item);
+    }
+  }
+  PyBuffer_Release(&t);
+  PyBuffer_Release(&b);
+  return out;
+}
+
+PyMethodDef codec_functions[] = {
+    {"materialise_table", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(mod_materialise_table)),
+     METH_FASTCALL, "materialise_table(buf, table) -> list of (mediaId, status, progress, host) or None"},
+    {nullptr, nullptr, 0, nullptr}};
+
 }  // namespace
 
 PyTypeObject CodecType = {PyVarObject_HEAD_INIT(nullptr, 0)};
@@ -515,7 +575,7 @@ int init_codec_types(PyObject* m) {
   if (PyType_Ready(&CodecType) < 0) return -1;
   Py_INCREF(&CodecType);
   if (PyModule_AddObject(m, "MessageCodec", reinterpret_cast<PyObject*>(&CodecType)) < 0) return -1;
-  return 0;
+  return PyModule_AddFunctions(m, codec_functions);
 }
 
 }  // namespace beholder

@@ -93,6 +93,13 @@ def decode_bodies(bodies: Sequence[bytes], device="cuda"):
     return out.cpu().numpy()
 
 
+def materialise(buf: bytes, table) -> list:
+    """Table rows → ``(mediaId, status, progress, host)`` tuples (None for ok == 0), in C
+    (``materialise_table``, ops/csrc/py_codec.cpp): the host work any offload still has to do."""
+    from . import native
+    return native.materialise_table(buf, np.ascontiguousarray(table, dtype=np.int32))
+
+
 def _varint(p: bytes, i: int, end: int):
     v = 0
     for shift in range(0, 70, 7):

@@ -50,6 +50,20 @@ def test_reference_never_reads_past_its_message(bodies):
             assert ln == 0 or offs[k] <= off and off + ln <= offs[k + 1]
 
 
+def test_native_materialise_gives_the_codec_values():
+    bodies = [b for _, b in Workload(n_media=8, seed=2).events(200)] + [b"\xff", b""]
+    buf, _ = gd.pack(bodies)
+    got = gd.materialise(buf, gd.reference_table(bodies))
+    for b, row in zip(bodies[:200], got):
+        m = PROGRESS.decode(b)
+        assert row == (m.mediaId, m.status, m.progress, m.host)
+    assert got[200] is None and got[201] == ("", 0, 0, "")
+    bad = gd.reference_table(bodies[:1])
+    bad[0, 1] = len(buf) + 1
+    with pytest.raises(ValueError, match="outside"):
+        gd.materialise(buf, bad)
+
+
 def test_layout_guards_and_loud_missing_library(monkeypatch):
     buf, offs = gd.pack([b"\n\x01a", b""])
     gd.check_layout(len(buf), offs)
