@@ -118,3 +118,14 @@ def test_kernel_large_batch_and_argument_checks():
     with pytest.raises(ValueError):
         gd.decode_batch(dev.cpu(), torch.zeros(3, dtype=torch.int32), 2)
     assert gd.decode_batch(dev, torch.zeros(1, dtype=torch.int32, device="cuda"), 0).shape == (0, 8)
+
+
+@pytest.mark.gpu
+def test_kernel_long_fields_and_mixed_sizes():
+    """Multi-byte length varints (fields of 128 bytes and up, one of 40,000) at every alignment."""
+    rng = random.Random(3)
+    bodies = [PROGRESS.encode({"mediaId": "x" * rng.randrange(0, 400), "status": 2, "progress": k,
+                               "host": "h" * rng.randrange(0, 40)}) for k in range(3000)]
+    bodies[700] = PROGRESS.encode({"mediaId": "y" * 40000, "status": 4})
+    got = gd.decode_bodies(bodies)
+    assert np.array_equal(got, gd.reference_table(bodies))
