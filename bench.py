@@ -80,6 +80,33 @@ def available_cpus() -> int:
     return max(1, n)
 
 
+def cpu_share() -> dict:
+    """What the CPU budget is made of: affinity CPUs, the cgroup quota (CPUs, None = no quota)
+    and the distinct physical cores behind the affinity CPUs (SMT siblings share a core, so the
+    same 16-CPU share can be 16 or 8 cores; box-to-box variance of the all-process number
+    follows this)."""
+    try:
+        aff = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = list(range(os.cpu_count() or 1))
+    cores = set()
+    for c in aff:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            with open(base + "physical_package_id") as f1, open(base + "core_id") as f2:
+                cores.add((f1.read().strip(), f2.read().strip()))
+        except OSError:
+            cores.add(("?", str(c)))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"affinity_cpus": len(aff), "quota_cpus": quota, "physical_cores": len(cores)}
+
+
 def gpus_on_node() -> int:
     """GPUs visible on this node, counted without initialising HIP (0 if torch is unavailable)."""
     try:
@@ -379,6 +406,7 @@ def main(argv=None) -> int:
             },
             "procs_per_rank": procs,
             "cpus_available": available_cpus(),
+            "cpu_share": cpu_share(),
             "gpus_on_node": gpus_on_node(),
             "events_per_proc_per_sec": round(value / total_procs, 1),
             "p50_handle_latency_us": round(hh.percentile(50) / 1e3, 3),
