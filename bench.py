@@ -82,9 +82,9 @@ def available_cpus() -> int:
 
 def cpu_share() -> dict:
     """What the CPU budget is made of: affinity CPUs, the cgroup quota (CPUs, None = no quota)
-    and the distinct physical cores behind the affinity CPUs (SMT siblings share a core, so the
-    same 16-CPU share can be 16 or 8 cores; box-to-box variance of the all-process number
-    follows this)."""
+    and the distinct physical cores behind the affinity CPUs. On the MI355X pool the share is a
+    16-CPU quota over all 256 hardware threads, so consumers run next to other tenants' work and
+    the all-process number moves with host load (profiles/box_r1_share/)."""
     try:
         aff = sorted(os.sched_getaffinity(0))
     except (AttributeError, OSError):
