@@ -8,7 +8,8 @@ RUN useradd --uid 999 --create-home --home-dir /home/beholder beholder && chown 
 COPY --chown=999:999 pyproject.toml /stack/
 RUN pip install --no-cache-dir protobuf pyyaml
 COPY --chown=999:999 . /stack
-# native runtime (ingest ring, codec, deliveries, metrics, text) built in-tree
+# native runtime (ingest ring, codec, deliveries, metrics, text) built in-tree; the optional gfx950
+# HIP probe library is skipped here (no hipcc in this image)
 RUN python -m beholder_amd.ops.build --force && chown -R 999:999 /stack
 
 USER 999

@@ -8,7 +8,12 @@ host build with the system C++ compiler. ``build_hip`` compiles the batched-deco
 ``scripts/gpu_offload_probe.py`` measures against it (``ops/gpu_decode.py``).
 ``__graft_entry__.build()`` calls both.
 
-Usage: ``python -m beholder_amd.ops.build [--debug] [--sanitize=address,undefined]`` (thin CLI over this module)
+The HIP library is optional for the service: ``main`` builds it only when ``hipcc`` is present
+(``--hip`` makes it required, ``--no-hip`` skips it), so the deployment image and CI, which have
+no ROCm, build the runtime alone.
+
+Usage: ``python -m beholder_amd.ops.build [--debug] [--sanitize=address,undefined] [--hip|--no-hip]``
+(thin CLI over this module)
 """
 from __future__ import annotations
 
@@ -140,11 +145,18 @@ def main(argv=None) -> int:
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--sanitize", default="")
     ap.add_argument("--cxx", default="")
-    ap.add_argument("--no-hip", action="store_true", help="skip the gfx950 HIP extension")
+    g = ap.add_mutually_exclusive_group()
+    g.add_argument("--hip", action="store_true", help="require the gfx950 HIP extension (fail without hipcc)")
+    g.add_argument("--no-hip", action="store_true", help="skip the gfx950 HIP extension")
     a = ap.parse_args(argv)
     print(build(force=a.force, debug=a.debug, sanitize=a.sanitize, cxx=a.cxx, verbose=True))
-    if not a.no_hip and not a.sanitize:
-        print(build_hip(force=a.force, verbose=True))
+    if a.no_hip or a.sanitize:
+        return 0
+    if not a.hip and not hipcc():
+        print("hipcc not found: skipping the optional gfx950 HIP extension (ops/hip); the service does not use it",
+              file=sys.stderr)
+        return 0
+    print(build_hip(force=a.force, verbose=True))
     return 0
 
 

@@ -326,7 +326,7 @@ def _reap(procs) -> Dict[str, int]:
     return total
 
 
-def _http_tcp(w: Workload, n: int, servers: int = 3) -> dict:
+def _http_tcp(w: Workload, n: int, servers: int = 3, clients=("h1", "aiohttp")) -> dict:
     """Sinks over real TCP: n events through the service with the production HTTP client
     (``h1``) and with ``aiohttp``, against ``servers`` fake endpoint processes sharing one
     port. About half the events make a Trello / Telegram / Emby request. ``prefetch`` (100)
@@ -339,6 +339,8 @@ def _http_tcp(w: Workload, n: int, servers: int = 3) -> dict:
         url = f"http://127.0.0.1:{port}"
         evs = w.events(n)
         for kind, cls in (("h1", H1Client), ("aiohttp", AiohttpClient)):
+            if kind not in clients:
+                continue
             out[kind] = asyncio.run(_run_inproc(evs, 0, media=w.media, http=cls(timeout_s=30), sink_url=url))
     finally:
         out["server_requests_total"] = _reap(procs).get("requests", 0)

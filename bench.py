@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Headline benchmark: metric-events/sec ingested + p50 handle latency (BASELINE.json ``metric``).
 
-One *step* = ``--events-per-step`` synthetic telemetry events (90% progress /
-10% status, protobuf-encoded, framed) pushed through the **whole** service
-path of each consumer process:
+BASELINE.json's configs are all **single process**, so ``value`` is the ingest rate of ONE
+consumer process per rank (for N ranks: N such consumers, whole-job events/s; weak scaling).
+One *step* = ``--events-per-step`` synthetic telemetry events (90% progress / 10% status,
+protobuf-encoded, framed) pushed through the **whole** service path of the consumer:
 
     producer thread -> OS pipe -> native reader thread (framing, ring)
       -> event loop: Delivery batches -> eager handler dispatch
@@ -14,23 +15,25 @@ path of each consumer process:
       -> pino JSON log line per reference log call (info level, to /dev/null)
       -> ack (latency recorded natively)
 
-A step ends when every event of the step has been settled. ``W`` warm-up
-steps run untimed, then exactly ``K`` steps are timed.
+A step ends when every event of the step has been settled. ``W`` warm-up steps run untimed,
+then exactly ``K`` steps are timed, bracketed by a gloo barrier and ``torch.cuda.synchronize()``
+on both sides (the service queues no device work: the reference has none).
+The elapsed time is the MAX over ranks.
 
-Scale-out is the reference's: competing consumers, one process each
-(SURVEY.md §2.3). Each rank runs ``--procs-per-rank`` consumer processes
-(default: the CPU share of one GPU slot minus one, at most 16; the same for every N) on
-independent streams.
-Timing: every consumer finishes its warm-up and reports ready; the rank's
-coordinator synchronizes the device, passes a gloo barrier across ranks, then
-releases its consumers through a second barrier and starts the clock; it stops the clock when all of its
-consumers report their K steps done, then passes another gloo barrier. The
-elapsed time is the MAX over ranks and ``value`` is whole-job events/s.
-Per-consumer work is fixed as N grows: weak scaling. The service has no
-device work (the reference has none), so nothing runs on the GPU. The
-timed region is bracketed by the barriers and by torch.cuda.synchronize()
-(no kernel is ever queued). HIP is initialised in a rank process only after
-its consumer processes have been spawned.
+The same run also measures, as extra keys of the one JSON line (rank 0, outside the timed
+region):
+
+* ``all_procs_*``: every CPU of the rank's share busy: ``--procs-per-rank`` consumer processes
+  (competing consumers) on independent streams. This moves with the host's load.
+* ``rate_10k_*``: BASELINE config 3, 10k events/s paced for 1 s: p50/p99 receive→ack latency.
+* ``soak_*``: BASELINE config 5, 1M events unpaced: RSS growth and GC pauses.
+* ``overload_*``: BASELINE config 4, unpaced into a 4096-event ring with ``drop_newest``.
+* ``tcp_e2e_*`` / ``http_tcp_h1_*``: the production-shaped path, every dependency over TCP (an
+  AMQP replay broker, a Postgres fake and HTTP fakes in their own processes).
+
+Order of the phases: everything that starts child processes (the TCP fakes, the all-process
+consumers) runs before the headline phase, whose ``torch.cuda.synchronize()`` is the first HIP
+call of this process (a process that initialised the GPU must not start programs).
 
 Prints ONE JSON line on rank 0.
 """
@@ -50,82 +53,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+from beholder_amd.utils.hostinfo import available_cpus, cpu_share, default_procs, gpus_on_node  # noqa: E402
+
 BASELINE_METRIC = "metric_events_ingested_per_sec"
-
-
-def available_cpus() -> int:
-    """CPUs this process may use: affinity mask, capped by a cgroup v2/v1 CPU quota."""
-    try:
-        n = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        n = os.cpu_count() or 1
-    quota = None
-    try:
-        with open("/sys/fs/cgroup/cpu.max") as f:
-            q, p = f.read().split()[:2]
-            if q != "max":
-                quota = int(q) / int(p)
-    except (OSError, ValueError):
-        try:
-            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
-                q = int(f.read())
-            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
-                p = int(f.read())
-            if q > 0:
-                quota = q / p
-        except (OSError, ValueError):
-            pass
-    if quota is not None:
-        n = min(n, max(1, int(quota)))
-    return max(1, n)
-
-
-def cpu_share() -> dict:
-    """What the CPU budget is made of: affinity CPUs, the cgroup quota (CPUs, None = no quota)
-    and the distinct physical cores behind the affinity CPUs. On the MI355X pool the share is a
-    16-CPU quota over all 256 hardware threads, so consumers run next to other tenants' work and
-    the all-process number moves with host load (profiles/box_r1_share/)."""
-    try:
-        aff = sorted(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        aff = list(range(os.cpu_count() or 1))
-    cores = set()
-    for c in aff:
-        try:
-            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
-            with open(base + "physical_package_id") as f1, open(base + "core_id") as f2:
-                cores.add((f1.read().strip(), f2.read().strip()))
-        except OSError:
-            cores.add(("?", str(c)))
-    quota = None
-    try:
-        with open("/sys/fs/cgroup/cpu.max") as f:
-            q, per = f.read().split()[:2]
-            quota = None if q == "max" else round(int(q) / int(per), 2)
-    except (OSError, ValueError):
-        pass
-    return {"affinity_cpus": len(aff), "quota_cpus": quota, "physical_cores": len(cores)}
-
-
-def gpus_on_node() -> int:
-    """GPUs visible on this node, counted without initialising HIP (0 if torch is unavailable)."""
-    try:
-        import torch
-        return int(torch.cuda.device_count())
-    except Exception:  # noqa: BLE001 — CPU-only environments
-        return 0
-
-
-def default_procs(local_world: int) -> int:
-    """Consumer processes per rank: the CPU share of one GPU slot minus one, at most 16.
-
-    The share is the node's CPUs divided by the number of GPU slots on the node (at least the
-    local world size). It does not depend on how many ranks run, so per-rank work stays fixed
-    as N grows (weak scaling): on an 8-GPU node with 16 CPUs per GPU, N=1 and N=8 both run 15
-    consumers per rank.
-    """
-    slots = max(1, local_world, gpus_on_node())
-    return max(1, min(16, available_cpus() // slots - 1))
 
 
 def parse(argv=None):
@@ -135,13 +65,19 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--events-per-step", type=int, default=65536, help="events per step per consumer process")
     ap.add_argument("--procs-per-rank", type=int, default=0,
-                    help="consumer processes per rank (0 = min(16, CPUs per GPU slot - 1))")
+                    help="consumer processes per rank in the all-process phase (0 = min(16, CPUs per GPU slot - 1))")
+    ap.add_argument("--all-procs-steps", type=int, default=10,
+                    help="timed steps of the all-process phase (0 = skip it)")
+    ap.add_argument("--no-extras", dest="extras", action="store_false",
+                    help="skip the rate_10k / soak / overload / TCP measurements")
+    ap.add_argument("--io-events", type=int, default=50000, help="events of each TCP measurement")
+    ap.add_argument("--soak-events", type=int, default=1_000_000)
     ap.add_argument("--media", type=int, default=10000)
     ap.add_argument("--log-level", default="info")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--ordering", default="none", choices=["none", "per_media"])
     ap.add_argument("--pin", action="store_true",
-                    help="pin each consumer process to its own CPU of the rank's affinity mask")
+                    help="pin each all-process consumer to its own CPU of the rank's affinity mask")
     return ap.parse_args(argv)
 
 
@@ -149,9 +85,8 @@ class _Device:
     """``torch.cuda.synchronize()`` around the timed region, as the driver contract asks.
 
     The service queues no device work, so this only orders the (empty) stream. HIP is
-    initialised lazily on the first :meth:`sync`. Callers make that happen only after every
-    consumer process has been spawned, because a process that initialised the GPU must not start
-    programs (spawn = fork + exec).
+    initialised lazily on the first :meth:`sync`, which ``main`` reaches only after every child
+    process of the run has been started.
     """
 
     def __init__(self, local_rank: int):
@@ -171,6 +106,10 @@ class _Device:
                 self._torch = None
         if self._torch is not None:
             self._torch.cuda.synchronize()
+
+    @property
+    def initialised(self) -> bool:
+        return self._ready
 
 
 class _Dist:
@@ -211,8 +150,8 @@ class _Dist:
             self.dist.destroy_process_group()
 
 
-async def run_consumer(a, seed: int, go, stop=None) -> dict:
-    """One consumer process: build the service, warm up, ``go()``, time K steps, ``stop()``."""
+async def run_consumer(a, seed: int, go, stop=None, *, steps: int = None, warmup: int = None) -> dict:
+    """One consumer: build the service, warm up, ``go()``, time ``steps`` steps, ``stop()``."""
     from beholder_amd.bench.generator import Workload, bench_config
     from beholder_amd.config import Config
     from beholder_amd.service import Service
@@ -221,8 +160,10 @@ async def run_consumer(a, seed: int, go, stop=None) -> dict:
     from beholder_amd.transport.ingest import FdSource
     from beholder_amd.utils.log import Logger
 
+    steps = a.steps if steps is None else steps
+    warmup = a.warmup if warmup is None else warmup
     E = a.events_per_step
-    total_steps = a.warmup + a.steps
+    total_steps = warmup + steps
     w = Workload(n_media=a.media, seed=seed)
     step_bytes = [w.framed(E) for _ in range(total_steps)]
 
@@ -259,7 +200,7 @@ async def run_consumer(a, seed: int, go, stop=None) -> dict:
 
     t0 = 0.0
     for i in range(total_steps):
-        if i == a.warmup:
+        if i == warmup:
             settler.reset_latency()
             go()
             t0 = time.perf_counter()
@@ -276,7 +217,7 @@ async def run_consumer(a, seed: int, go, stop=None) -> dict:
     st = svc.stats()
     return {
         "elapsed": elapsed,
-        "events": E * a.steps,
+        "events": E * steps,
         "handle_hist": settler.handle_latency.to_bytes(),
         "ingest_hist": settler.ingest_latency.to_bytes(),
         "http_calls": http.count,
@@ -285,8 +226,19 @@ async def run_consumer(a, seed: int, go, stop=None) -> dict:
     }
 
 
-def _consumer_entry(a, seed, ready, go, results, cpu=None):
-    """Spawned consumer process: warm up, report ready, wait for the go signal, time K steps."""
+def run_solo(a, dist: _Dist, dev: _Device) -> dict:
+    """The headline: one consumer in this process, K steps timed between barrier+sync pairs."""
+    def go():
+        dev.sync()
+        dist.barrier()
+
+    res = asyncio.run(run_consumer(a, a.seed + 7919 * dist.rank, go, dev.sync))
+    res["procs"] = 1
+    return res
+
+
+def _consumer_entry(a, seed, steps, warmup, ready, go, results, cpu=None):
+    """Spawned consumer process: warm up, report ready, wait for the go signal, time its steps."""
     if cpu is not None:
         try:
             os.sched_setaffinity(0, {cpu})
@@ -298,7 +250,7 @@ def _consumer_entry(a, seed, ready, go, results, cpu=None):
         go.wait()     # released by the coordinator, which starts its clock at the same moment
 
     try:
-        res = asyncio.run(run_consumer(a, seed, start))
+        res = asyncio.run(run_consumer(a, seed, start, steps=steps, warmup=warmup))
         results.put(res)
     except BaseException as e:  # report, never hang the coordinator
         for b in (ready, go):
@@ -310,17 +262,10 @@ def _consumer_entry(a, seed, ready, go, results, cpu=None):
         raise
 
 
-def run_rank(a, dist: _Dist, procs: int) -> dict:
-    """Coordinator for one rank's consumer processes; returns the rank's merged result."""
-    base_seed = a.seed + 7919 * dist.rank
-    dev = _Device(dist.local_rank)
-    if procs == 1:  # the consumer runs in this process, which starts no other program
-        def go():
-            dev.sync()
-            dist.barrier()
-        res = asyncio.run(run_consumer(a, base_seed, go, dev.sync))
-        res["procs"] = 1
-        return res
+def run_procs(a, dist: _Dist, procs: int, steps: int, warmup: int = 1) -> dict:
+    """All-process phase: ``procs`` spawned consumers on independent streams, released together
+    after a barrier across ranks. Runs before this process touches HIP (it starts programs)."""
+    base_seed = a.seed + 7919 * dist.rank + 1
     ctx = mp.get_context("spawn")
     ready = ctx.Barrier(procs + 1)
     go = ctx.Barrier(procs + 1)
@@ -330,35 +275,82 @@ def run_rank(a, dist: _Dist, procs: int) -> dict:
 
     def cpu_for(i):
         return cpus[(first + i) % len(cpus)] if cpus else None
-    children = [ctx.Process(target=_consumer_entry, args=(a, base_seed + 104729 * i, ready, go, results, cpu_for(i)),
+    children = [ctx.Process(target=_consumer_entry,
+                            args=(a, base_seed + 104729 * i, steps, warmup, ready, go, results, cpu_for(i)),
                             daemon=True) for i in range(procs)]
     for c in children:
         c.start()
-    ready.wait()            # every consumer has warmed up (all spawned: HIP may be initialised now)
-    dev.sync()              # nothing is timed yet: the consumers wait at `go`
-    dist.barrier()          # every rank is ready (after its device init, so ranks start together)
+    ready.wait()            # every consumer has warmed up
+    dist.barrier()          # every rank is ready
     go.wait()               # releases the consumers; the clock starts with them
     t0 = time.perf_counter()
     got = [results.get() for _ in range(procs)]
-    dev.sync()
     t1 = time.perf_counter()
     for c in children:
         c.join(60)
     errs = [g["error"] for g in got if "error" in g]
     if errs:
         raise RuntimeError("consumer failed: " + "; ".join(errs))
-    from beholder_amd.ops import Histogram
-    hh, ih = Histogram(), Histogram()
-    for g in got:
-        hh.merge_bytes(g["handle_hist"])
-        ih.merge_bytes(g["ingest_hist"])
-    # each consumer also clocks its own K steps from the go signal; the rank's elapsed time is never
+    # each consumer also clocks its own steps from the go signal; the rank's elapsed time is never
     # shorter than the slowest consumer's (guards against any head start before t0)
     elapsed = max(t1 - t0, max(g["elapsed"] for g in got))
-    return {"elapsed": elapsed, "coordinator_elapsed": t1 - t0, "events": sum(g["events"] for g in got), "handle_hist": hh.to_bytes(),
-            "ingest_hist": ih.to_bytes(), "http_calls": sum(g["http_calls"] for g in got),
-            "errors": sum(g["errors"] for g in got), "abandoned": sum(g["abandoned"] for g in got),
-            "procs": procs, "max_consumer_elapsed": max(g["elapsed"] for g in got)}
+    return {"elapsed": elapsed, "coordinator_elapsed": t1 - t0, "events": sum(g["events"] for g in got),
+            "errors": sum(g["errors"] for g in got), "procs": procs,
+            "max_consumer_elapsed": max(g["elapsed"] for g in got)}
+
+
+def _r(x, nd=3):
+    return None if x is None else round(float(x), nd)
+
+
+def io_extras(a) -> dict:
+    """Production-shaped TCP path (starts the fake endpoints as child processes)."""
+    from beholder_amd.bench import harness
+    from beholder_amd.bench.generator import Workload
+    out = {}
+    e2e = harness._tcp_e2e(a.io_events)
+    hl = e2e.get("handle_latency_us", {})
+    out.update({"tcp_e2e_events_per_sec": _r(e2e.get("ingest_rate_eps"), 1),
+                "tcp_e2e_cpu_us_per_event": _r(e2e.get("cpu_us_per_event")),
+                "tcp_e2e_p50_handle_latency_us": _r(hl.get("p50")),
+                "tcp_e2e_p999_handle_latency_us": _r(hl.get("p999")),
+                "tcp_e2e_errors": e2e.get("errors")})
+    h = harness._http_tcp(Workload(n_media=10000, seed=a.seed), a.io_events, clients=("h1",))["h1"]
+    hl = h["handle_latency_us"]
+    out.update({"http_tcp_h1_events_per_sec": _r(h["ingest_rate_eps"], 1),
+                "http_tcp_h1_p99_handle_latency_us": _r(hl.get("p99")),
+                "http_tcp_h1_p999_handle_latency_us": _r(hl.get("p999"))})
+    return out
+
+
+def inproc_extras(a) -> dict:
+    """BASELINE configs 3, 4 and 5 in this process (no child processes)."""
+    import resource
+
+    from beholder_amd.bench import harness
+    from beholder_amd.bench.generator import Workload
+    w = Workload(n_media=10000, seed=a.seed)
+    out = {}
+    r = asyncio.run(harness._run_inproc(w.events(10000), 10000, media=w.media))
+    out.update({"rate_10k_acked": r["acked"],
+                "rate_10k_p50_ingest_latency_us": _r(r["ingest_latency_us"].get("p50")),
+                "rate_10k_p99_ingest_latency_us": _r(r["ingest_latency_us"].get("p99"))})
+    r = asyncio.run(harness._run_inproc(w.events(200_000), 0, policy="drop_newest", capacity_events=4096,
+                                        media=w.media))
+    out.update({"overload_offered": r["offered"], "overload_accepted": r["accepted"],
+                "overload_dropped": r["dropped"]})
+    evs = w.events(a.soak_events)
+    probe: list = []
+    g = harness.GcPauses()
+    r = asyncio.run(harness._run_inproc(evs, 0, media=w.media, rss_probe=probe, gc_probe=g))
+    del evs
+    gs = g.summary()
+    out.update({"soak_events": r["acked"], "soak_events_per_sec": _r(r["ingest_rate_eps"], 1),
+                "soak_rss_growth_mb": _r(probe[1] - probe[0], 2),
+                "soak_rss_peak_mb": _r(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024, 1),
+                "soak_gc_pauses": gs.get("count", 0), "soak_gc_max_pause_us": _r(gs.get("max_us")),
+                "soak_gc_p99_pause_us": _r(gs.get("p99_us"))})
+    return out
 
 
 def main(argv=None) -> int:
@@ -369,20 +361,38 @@ def main(argv=None) -> int:
         print(f"bench.py: --gpus {a.gpus} requires torch.distributed.run; running 1 rank", file=sys.stderr)
         n = 1
     procs = a.procs_per_rank or default_procs(dist.local_world)
+    dev = _Device(dist.local_rank)
+    extras: dict = {}
+
+    # 1. phases that start child processes (before any HIP call in this process)
+    if a.extras and dist.rank == 0:
+        extras.update(io_extras(a))
+    dist.barrier()
+    allp = None
+    if a.all_procs_steps > 0 and procs > 1:
+        allp = run_procs(a, dist, procs, a.all_procs_steps)
+    allp_elapsed = dist.max(allp["elapsed"] if allp else 0.0)
+    allp_events = sum(dist.gather(allp["events"] if allp else 0))
+
+    # 2. the headline: one consumer per rank, K timed steps
     gc.collect()
-    res = run_rank(a, dist, procs)
+    res = run_solo(a, dist, dev)
     dist.barrier()
     elapsed = dist.max(res["elapsed"])
     parts = dist.gather({k: res[k] for k in ("handle_hist", "ingest_hist", "http_calls", "errors", "abandoned",
-                                             "events", "procs")})
+                                             "events")})
+
+    # 3. in-process BASELINE configs (no child processes: HIP may be initialised now)
+    if a.extras and dist.rank == 0:
+        extras.update(inproc_extras(a))
+    dist.barrier()
+
     if dist.rank == 0:
         from beholder_amd.ops import Histogram
-        hh, ih = Histogram(), Histogram()
+        hh = Histogram()
         for p in parts:
             hh.merge_bytes(p["handle_hist"])
-            ih.merge_bytes(p["ingest_hist"])
         total_events = sum(p["events"] for p in parts)
-        total_procs = sum(p["procs"] for p in parts)
         value = total_events / elapsed
         out = {
             "metric": BASELINE_METRIC,
@@ -400,22 +410,24 @@ def main(argv=None) -> int:
                     "Trello/Telegram/Emby stubbed in-process, info logs to /dev/null",
             "config": {
                 "model": "beholder telemetry consumer (status+progress handlers, index.js:62-155)",
-                "global_batch": a.events_per_step * total_procs,
+                "global_batch": a.events_per_step * n,
                 "seq_len": None,
-                "parallelism": f"dp{n} x {procs} consumer procs/rank (competing consumers)",
+                "parallelism": f"dp{n} x 1 consumer proc/rank (BASELINE: single process per consumer)",
             },
-            "procs_per_rank": procs,
+            "events_per_proc_per_sec": round(value / n, 1),
+            "p50_handle_latency_us": round(hh.percentile(50) / 1e3, 3),
+            "p99_handle_latency_us": round(hh.percentile(99) / 1e3, 3),
+            "http_requests": sum(p["http_calls"] for p in parts),
+            "handler_errors": sum(p["errors"] for p in parts),
+            "all_procs_per_rank": procs if allp is not None else 0,
+            "all_procs_events_per_sec": round(allp_events / allp_elapsed, 1) if allp_elapsed else None,
             "cpus_available": available_cpus(),
             "cpu_share": cpu_share(),
             "gpus_on_node": gpus_on_node(),
-            "events_per_proc_per_sec": round(value / total_procs, 1),
-            "p50_handle_latency_us": round(hh.percentile(50) / 1e3, 3),
-            "p99_handle_latency_us": round(hh.percentile(99) / 1e3, 3),
-            "p50_ingest_latency_us": round(ih.percentile(50) / 1e3, 3),
-            "http_requests": sum(p["http_calls"] for p in parts),
-            "handler_errors": sum(p["errors"] for p in parts),
-            "notes": "CPU event-consumer workload (the reference has no device compute; see docs/DESIGN.md); "
-                     "each consumer process runs the full service path on its own synthetic stream",
+            **extras,
+            "notes": "CPU event-consumer workload (the reference has no device compute; see docs/DESIGN.md). "
+                     "value = one consumer process per rank; all_procs_* = every CPU of the share busy; "
+                     "rate_10k/overload/soak = BASELINE configs 3-5; tcp_e2e/http_tcp = every dependency over TCP",
         }
         print(json.dumps(out), flush=True)
     dist.close()

@@ -1,4 +1,5 @@
-"""bench.py driver contract: one JSON line, required keys, multi-rank launch via torch.distributed.run."""
+"""bench.py driver contract: one JSON line, required keys, multi-rank launch via torch.distributed.run,
+the single-process headline (BASELINE.json configs are single process) and the extra keys."""
 import json
 import os
 import subprocess
@@ -9,6 +10,10 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
             "vs_baseline", "dtype", "data", "config"}
+EXTRAS = {"all_procs_events_per_sec", "rate_10k_p50_ingest_latency_us", "rate_10k_p99_ingest_latency_us",
+          "soak_rss_growth_mb", "soak_gc_max_pause_us", "overload_dropped", "tcp_e2e_events_per_sec",
+          "http_tcp_h1_p999_handle_latency_us", "p50_handle_latency_us"}
+SMALL = ["--steps", "2", "--warmup", "1", "--events-per-step", "4096", "--media", "500"]
 
 
 def _last_json(stdout: str) -> dict:
@@ -18,56 +23,98 @@ def _last_json(stdout: str) -> dict:
 
 
 def test_bench_single_rank_contract():
-    r = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--events-per-step", "4096",
-                        "--procs-per-rank", "1"], cwd=ROOT, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr
+    r = subprocess.run([sys.executable, "bench.py", *SMALL, "--procs-per-rank", "2", "--all-procs-steps", "1",
+                        "--io-events", "2000", "--soak-events", "20000"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
     out = _last_json(r.stdout)
     assert REQUIRED <= set(out) and out["n_gpus"] == 1 and out["steps"] == 2 and out["warmup"] == 1
     assert {"model", "global_batch", "seq_len", "parallelism"} <= set(out["config"])
+    assert EXTRAS <= set(out), EXTRAS - set(out)
+    # the headline is ONE consumer process (BASELINE.json configs are single process)
+    assert out["config"]["global_batch"] == 4096 and "1 consumer proc/rank" in out["config"]["parallelism"]
     assert out["value"] > 0 and out["handler_errors"] == 0
     assert out["value"] == pytest.approx(4096 * 2 / (out["ms_per_step"] * 2 / 1000), rel=0.01)
+    assert out["all_procs_per_rank"] == 2 and out["all_procs_events_per_sec"] > 0
+    assert out["rate_10k_acked"] == 10000 and out["soak_events"] == 20000 and out["tcp_e2e_errors"] == 0
+    assert out["overload_accepted"] + out["overload_dropped"] == out["overload_offered"]
 
 
 def test_bench_two_ranks_gloo():
+    pytest.importorskip("torch")  # torch.distributed.run launches the ranks
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", "29561", "bench.py", "--gpus", "2",
-                        "--steps", "2", "--warmup", "1", "--events-per-step", "4096", "--procs-per-rank", "1"],
+                        *SMALL, "--procs-per-rank", "2", "--all-procs-steps", "1", "--no-extras"],
                        cwd=ROOT, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     out = _last_json(r.stdout)
     assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 8192
     assert out["config"]["parallelism"].startswith("dp2")
-
-
-def test_bench_multiprocess_rank():
-    """Consumer processes per rank: events add up, value = total events / coordinator time."""
-    r = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--events-per-step", "4096",
-                        "--procs-per-rank", "2"], cwd=ROOT, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-3000:]
-    out = _last_json(r.stdout)
-    assert out["procs_per_rank"] == 2 and out["config"]["global_batch"] == 8192
     assert out["value"] == pytest.approx(8192 * 2 / (out["ms_per_step"] * 2 / 1000), rel=0.01)
-    assert out["handler_errors"] == 0
+    assert out["all_procs_per_rank"] == 2 and out["all_procs_events_per_sec"] > 0
+    assert "tcp_e2e_events_per_sec" not in out
+
+
+def test_all_procs_phase_adds_up():
+    """Consumer processes of the all-process phase: events add up over the spawned consumers."""
+    import bench
+    a = bench.parse([*SMALL, "--procs-per-rank", "2"])
+    res = bench.run_procs(a, bench._Dist(), 2, steps=2)
+    assert res["events"] == 2 * 2 * 4096 and res["errors"] == 0 and res["procs"] == 2
 
 
 def test_consumers_get_no_head_start(monkeypatch):
-    """Slow device initialisation before the clock must not let consumers start early: the
-    coordinator's clock and each consumer's own clock cover the same K steps."""
+    """A slow cross-rank barrier before the clock must not let consumers start early: the
+    coordinator's clock and each consumer's own clock cover the same steps."""
     import time as _time
 
     import bench
     calls = []
 
-    def slow_first_sync(self):  # device initialisation happens on the first sync only
+    def slow_first_barrier(self):
         calls.append(1)
         if len(calls) == 1:
             _time.sleep(0.5)
-    monkeypatch.setattr(bench._Device, "sync", slow_first_sync)
-    a = bench.parse(["--procs-per-rank", "2", "--steps", "2", "--warmup", "1", "--events-per-step", "4096",
-                     "--media", "200"])
-    res = bench.run_rank(a, bench._Dist(), 2)
+    monkeypatch.setattr(bench._Dist, "barrier", slow_first_barrier)
+    a = bench.parse([*SMALL, "--procs-per-rank", "2"])
+    res = bench.run_procs(a, bench._Dist(), 2, steps=2)
     assert res["events"] == 2 * 2 * 4096
     # with a head start the consumers would finish ~0.5 s of work before the coordinator's t0
     assert res["coordinator_elapsed"] >= res["max_consumer_elapsed"] - 0.05, res
     assert res["coordinator_elapsed"] < res["max_consumer_elapsed"] + 1.0, res
-    assert len(calls) == 2  # before t0 and before t1
+    assert len(calls) == 1
+
+
+def test_no_hip_before_child_processes(monkeypatch, capsys):
+    """Every child process (TCP fakes, all-process consumers) starts before the first device
+    synchronize, the first HIP call of the coordinator; torch has not initialised HIP then."""
+    import bench
+    from beholder_amd.bench import harness
+    order = []
+    orig_sync, orig_spawn, orig_procs = bench._Device.sync, harness._spawn, bench.run_procs
+
+    def spy_sync(self):
+        order.append("sync")
+        orig_sync(self)
+
+    def spy_spawn(*a, **k):
+        torch = sys.modules.get("torch")
+        assert torch is None or not torch.cuda.is_initialized()
+        order.append("spawn")
+        return orig_spawn(*a, **k)
+
+    def spy_procs(*a, **k):
+        torch = sys.modules.get("torch")
+        assert torch is None or not torch.cuda.is_initialized()
+        order.append("procs")
+        return orig_procs(*a, **k)
+    monkeypatch.setattr(bench._Device, "sync", spy_sync)
+    monkeypatch.setattr(harness, "_spawn", spy_spawn)
+    monkeypatch.setattr(bench, "run_procs", spy_procs)
+    assert bench.main([*SMALL, "--procs-per-rank", "2", "--all-procs-steps", "1", "--io-events", "1000",
+                       "--soak-events", "5000"]) == 0
+    out = _last_json(capsys.readouterr().out)
+    assert out["value"] > 0
+    assert "spawn" in order and "procs" in order and "sync" in order
+    first = order.index("sync")
+    assert all(x == "sync" for x in order[first:]), order

@@ -7,14 +7,15 @@ from __future__ import annotations
 
 import random
 
-import numpy as np
 import pytest
 from hypothesis import given, settings, strategies as st
 
 from beholder_amd import ops
 from beholder_amd.bench.generator import Workload
 from beholder_amd.models import proto
-from beholder_amd.ops import gpu_decode as gd
+
+np = pytest.importorskip("numpy")  # the probe's host tables are numpy; the service never imports it
+from beholder_amd.ops import gpu_decode as gd  # noqa: E402
 
 PROGRESS = ops.codec_for(proto.load("api.TelemetryProgress"))
 STATUS = ops.codec_for(proto.load("api.TelemetryStatus"))
