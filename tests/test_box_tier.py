@@ -107,12 +107,13 @@ def test_bench_two_ranks_torchrun_on_box():
     """The driver's multi-GPU launch path (torch.distributed.run, gloo barriers, MAX over ranks)."""
     out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                           "--master-addr", "127.0.0.1", "--master-port", "29571", os.path.join(ROOT, "bench.py"),
-                          "--gpus", "2", "--steps", "3", "--warmup", "1", "--procs-per-rank", "2"],
+                          "--gpus", "2", "--steps", "3", "--warmup", "1", "--procs-per-rank", "2", "--no-extras"],
                          capture_output=True, text=True, timeout=900, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     r = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
-    assert r["n_gpus"] == 2 and r["procs_per_rank"] == 2 and r["handler_errors"] == 0
-    assert r["config"]["global_batch"] == 4 * 65536
+    assert r["n_gpus"] == 2 and r["all_procs_per_rank"] == 2 and r["handler_errors"] == 0
+    # value = one consumer per rank (BASELINE configs are single process); all_procs_* = 2 per rank
+    assert r["config"]["global_batch"] == 2 * 65536
 
 
 def test_io_bound_concurrency_reaches_prefetch():
