@@ -517,7 +517,9 @@ class Service:
         # Drop the traceback: it references the handler frame (and so the delivery). Freeing it
         # promptly lets an un-acked delivery be reported as abandoned right away (Q1 accounting).
         exc.__traceback__ = None
-        if d.settled:
+        if d.settled or d.topic_id != T.STATUS_ID:
+            # `service.on_status_error` is the Q1 knob (a throwing status handler); any other
+            # handler's error leaves its delivery as the reference would (un-acked)
             return
         policy = self.on_status_error
         try:

@@ -47,6 +47,11 @@ _TICK = 0.05  # deadline sweep period (s): timeouts fire at most this late
 _PATH_SAFE = "".join(chr(c) for c in range(0x21, 0x7F) if chr(c) not in '"<>\\^`{|}')
 
 
+def _is_token_text(s: str) -> bool:
+    """Every character in 0x21-0x7E (printable ASCII, no space): safe in a request line."""
+    return s.isascii() and s.isprintable() and " " not in s
+
+
 class _Reset(Exception):
     """The connection closed before the response completed (``started``: bytes of it seen)."""
 
@@ -189,6 +194,8 @@ class H1Client(HttpClient):
         if o is not None:
             return o
         scheme, _, authority = key.partition("://")
+        if not _is_token_text(authority):  # CR/LF/SP would end up in the Host line
+            raise HttpError(f"Invalid URI \"{redact(key)}\"")
         scheme = scheme.lower()
         if scheme not in ("http", "https"):
             raise HttpError(f"Invalid protocol: {scheme}:")
@@ -313,7 +320,9 @@ class H1Client(HttpClient):
         """``(origin, request target, rest of the request line + Host/Authorization lines)``."""
         key, target = _split_url(url)
         o = self._origin(key)
-        if not target.isascii() or " " in target:
+        if not _is_token_text(target):
+            # any byte outside 0x21-0x7E is percent-encoded: a CR/LF in a DB-sourced path
+            # segment (Trello's /1/cards/{creatorId}) must not split the request
             target = quote(target, safe=_PATH_SAFE)
         rest = f" HTTP/1.1\r\nHost: {o.host_header}\r\n"
         if o.auth:

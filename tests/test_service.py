@@ -11,6 +11,7 @@ from beholder_amd.service import Service
 from beholder_amd.sinks import RecordingHttpClient
 from beholder_amd.store import MemoryStore
 from beholder_amd.topics import PROGRESS, STATUS
+from beholder_amd import topics as T
 from beholder_amd.transport.amqp import AmqpBroker, AmqpSource
 from beholder_amd.transport.memory import MemoryBroker
 from beholder_amd.utils.log import Logger, MemoryStream
@@ -311,3 +312,27 @@ def test_transport_metrics_exposed():
     m = run(go())
     assert m['beholder_transport{kind="amqp",field="connected"}'] == 1
     assert m['beholder_transport{kind="amqp",field="reconnects"}'] == 0
+
+
+class _FakeDelivery:
+    def __init__(self, topic_id):
+        self.topic_id, self.topic, self.settled, self.nacks = topic_id, T.TOPIC_NAMES_BY_ID[topic_id], False, []
+
+    def nack(self, requeue):
+        self.nacks.append(requeue)
+        self.settled = True
+
+
+@pytest.mark.parametrize("policy", ["nack_drop", "nack_requeue"])
+def test_on_status_error_policy_applies_to_status_only(policy):
+    """`service.on_status_error` is the Q1 knob: a progress handler error (it only raises on
+    something like cancellation, Q7) leaves its delivery as the reference would."""
+    async def go():
+        svc = make_service(MemoryBroker().consumer(), [], on_status_error=policy)
+        await svc.init()
+        svc._on_handler_error(st, RuntimeError("boom"))
+        svc._on_handler_error(pr, RuntimeError("boom"))
+        await svc.close()
+    st, pr = _FakeDelivery(T.STATUS_ID), _FakeDelivery(T.PROGRESS_ID)
+    run(go())
+    assert st.nacks == [policy == "nack_requeue"] and pr.nacks == [] and not pr.settled

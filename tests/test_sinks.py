@@ -143,3 +143,41 @@ def test_aiohttp_client_works_under_the_native_driver(server):
         await http.close()
         return exc
     assert run(go()) is None
+
+
+@pytest.mark.parametrize("impl", ["python", "native"])
+def test_crlf_in_db_sourced_path_is_percent_encoded(server, impl, monkeypatch):
+    """A creatorId holding CR/LF (it comes from the media table, index.js:83) must not split the
+    request line toward Trello: the H1 client percent-encodes every byte outside 0x21-0x7E, for
+    the Python handlers and for the compiled ones (which issue the request through the same
+    client)."""
+    import helpers
+    from helpers import Rig, status_msg, trello_media
+    monkeypatch.setattr(helpers, "HANDLER_IMPL", impl)
+    evil = "abc\r\nX-Evil:1\r\nY:"  # no space: the old check only quoted on SP / non-ASCII
+
+    async def go():
+        http = H1Client(timeout_s=5)
+        rig = Rig(medias=[trello_media("m1", "QUEUED", card=evil)], http=http)
+        rig.h.trello = TrelloClient("KEY", "TOK", http, base_url=server.url)
+        if impl == "native":
+            from beholder_amd.handlers import native_handlers
+            rig.impl = native_handlers(rig.h)
+        await rig.impl.on_status(rig.delivery(helpers.STATUS_ID, status_msg("m1", "DOWNLOADING")))
+        await http.close()
+    run(go())
+    assert len(server.requests) == 1
+    method, path, query = server.requests[0]
+    assert method == "PUT" and path == "/1/cards/abc%0D%0AX-Evil:1%0D%0AY:"
+    assert query["key"] == "KEY" and query["token"] == "TOK"
+
+
+def test_control_characters_in_authority_are_rejected():
+    async def go():
+        http = H1Client(timeout_s=1)
+        try:
+            with pytest.raises(HttpError):
+                await http.request("GET", "http://127.0.0.1\r\nX: 1/path")
+        finally:
+            await http.close()
+    run(go())
