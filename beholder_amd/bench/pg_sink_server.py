@@ -93,7 +93,7 @@ class _Proto(asyncio.Protocol):
                 continue
             elif t == b"P":
                 name, rest = body.split(b"\x00", 1)
-                sql = rest.split(b"\x00", 1)[0].decode().strip().upper()
+                sql = rest.split(b"\x00", 1)[0].decode().strip().upper().replace('"', "")
                 if sql.startswith("SELECT") and "WHERE ID = $1" in sql:
                     self.stmts[name] = "select"
                 elif sql.startswith("UPDATE") and "SET STATUS = $1" in sql:

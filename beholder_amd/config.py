@@ -44,8 +44,14 @@ SERVICE_DEFAULTS: dict = {
         # index.js:43 — third AMQP arg; we use it as the reconnect/redelivery retry budget.
         "retries": 2,
         "transport": {"kind": "amqp", "url": None},
+        # AMQP consume topology (transport/amqp/topology.py); triton-core/amqp is not vendored, the
+        # default is our guess: a durable queue per topic on the default exchange
+        "amqp": {"exchange": "", "exchange_type": "topic", "exchange_durable": True, "queue_names": {},
+                 "routing_keys": {}, "durable": True, "passive_declare": False, "queue_arguments": {}},
         # index.js:42 `new Storage()` is always Postgres (triton-core/db); dsn default: dyn('postgres')
-        "store": {"backend": "postgres", "dsn": None, "pool_size": 4, "create_schema": False},
+        # table/columns: triton-core/db's schema is not vendored; defaults are our guess (store/schema.py)
+        "store": {"backend": "postgres", "dsn": None, "pool_size": 4, "create_schema": False,
+                  "table": "media", "columns": {}},
         # index.js:28 — Prom.expose(); port/host are [inferred] (triton-core not vendored).
         "metrics": {"enabled": True, "host": "0.0.0.0", "port": 3000, "default_metrics": True},
         # index.js:11-13 — pino logger named after the file basename.
@@ -281,6 +287,17 @@ class Config:
             raise ConfigError("service.on_status_error must be leave_unacked|nack_requeue|nack_drop")
         if svc["http"].get("client", "h1") not in ("h1", "aiohttp"):
             raise ConfigError("service.http.client must be 'h1' or 'aiohttp'")
+        from .store.schema import MediaSchema
+        from .transport.amqp.topology import Topology
+        try:
+            Topology.from_config(svc.get("amqp"))
+        except (TypeError, ValueError) as e:
+            raise ConfigError(f"service.amqp: {e}") from None
+        st = svc.get("store") or {}
+        try:
+            MediaSchema(st.get("table") or "media", st.get("columns") or {})
+        except (TypeError, ValueError) as e:
+            raise ConfigError(f"service.store: {e}") from None
         fl = self._data.get("instance", {}).get("flow_ids") if isinstance(self._data.get("instance"), Mapping) else None
         if fl is not None and not isinstance(fl, Mapping):
             raise ConfigError("instance.flow_ids must be a mapping of status -> list id")

@@ -80,8 +80,10 @@ def build_source(config: Config, logger: Optional[Logger] = None, capture_header
         from .transport.amqp import AmqpSource
         url = tcfg.get("url") or dyn("rabbitmq", env=config.env, config=config)
         hb = tcfg.get("heartbeat")
+        from .transport.amqp.topology import Topology
         return AmqpSource(url, prefetch=prefetch, retries=int(config.data["service"]["retries"]),
-                          logger=logger, heartbeat=None if hb is None else int(hb), capture_headers=capture_headers)
+                          logger=logger, heartbeat=None if hb is None else int(hb), capture_headers=capture_headers,
+                          topology=Topology.from_config(config.data["service"].get("amqp")))
     raise ValueError(f"unknown transport kind {kind!r} (amqp|stdin|file)")
 
 
@@ -185,8 +187,9 @@ class Service:
         if self._store is None:
             st = svc["store"]
             backend = st.get("backend", "postgres")
-            kw = ({"pool_size": int(st.get("pool_size", 4)), "create_schema": bool(st.get("create_schema", False))}
-                  if backend in ("postgres", "postgresql", "pg") else {})
+            kw = {"table": st.get("table") or "media", "columns": dict(st.get("columns") or {})}
+            if backend in ("postgres", "postgresql", "pg"):
+                kw.update(pool_size=int(st.get("pool_size", 4)), create_schema=bool(st.get("create_schema", False)))
             self._store = open_store(backend, st.get("dsn"), **kw)
         await self._store.connect()
 
@@ -220,6 +223,9 @@ class Service:
             gc.collect()
             gc.freeze()
         self.log.info("initialized")
+        # the unpinned parts (triton-core's queue layout and media table are not vendored), stated
+        # once so a mismatch with the real deployment is visible in the log
+        self.log.info(f"consuming from {self._source.describe()}; store {self._store.describe()}")
         return self
 
     def _media_key(self, d) -> Any:

@@ -63,6 +63,10 @@ class MediaStore(abc.ABC):
     async def close(self) -> None:
         """Release resources."""
 
+    def describe(self) -> str:
+        """What the store reads and writes, for the startup log line (``service.py``)."""
+        return self.name
+
     @abc.abstractmethod
     async def update_status(self, media_id: str, status: int) -> None:
         """``db.updateStatus`` (index.js:68)."""
@@ -103,6 +107,7 @@ def open_store(backend: str, dsn: Optional[str] = None, **kw) -> MediaStore:
     backend = (backend or "memory").lower()
     if backend == "memory":
         from .memory import MemoryStore
+        kw.pop("table", None), kw.pop("columns", None)  # no table: nothing to map
         return MemoryStore(**kw)
     if backend == "sqlite":
         from .sqlite import SqliteStore

@@ -25,6 +25,9 @@ class MemoryStore(MediaStore):
         for m in medias or ():
             self._rows[m.id] = m
 
+    def describe(self) -> str:
+        return f"memory ({len(self._rows)} rows)"
+
     def update_status_nowait(self, media_id: str, status: int) -> None:
         self.update_calls += 1
         m = self._rows.get(media_id)

@@ -1,6 +1,6 @@
 """Postgres media store — ``triton-core/db`` (index.js:42,68,76,140) over :mod:`.pgwire`.
 
-Table layout (our documented assumption; triton-core's migrations are not
+Table layout: :mod:`.schema` (our documented default guess, triton-core's migrations are not
 vendored)::
 
     CREATE TABLE media (
@@ -8,24 +8,22 @@ vendored)::
         source_uri TEXT, metadata INT, metadata_id TEXT, status INT)
 
 ``service.store.dsn`` is a ``postgres://`` URL (default ``dyn('postgres')``);
-``service.store.table`` overrides the table name; ``create_schema: true``
-creates it if missing.
+``service.store.table`` and ``service.store.columns`` override the table and column names;
+``create_schema: true`` creates the table if missing.
 """
 from __future__ import annotations
 
-import re
-from typing import Iterable, Optional
+from typing import Iterable, Mapping, Optional
 
 from .base import Media, MediaNotFound, MediaStore
 from .pgwire import Pool
-
-_COLS = "id, name, creator, creator_id, type, source, source_uri, metadata, metadata_id, status"
-_IDENT = re.compile(r"^[A-Za-z_][A-Za-z0-9_]*(\.[A-Za-z_][A-Za-z0-9_]*)?$")
+from .schema import MediaSchema, pg_ph
 
 
 def row_to_media(r) -> Media:
-    """One ``SELECT {_COLS}`` row as a Media (NULL text -> "", NULL/str numbers -> int). The
-    compiled handlers (ops/csrc/py_handlers.cpp) take the all-int, no-NULL case themselves."""
+    """One ``SELECT`` row (Media field order) as a Media (NULL text -> "", NULL/str numbers ->
+    int). The compiled handlers (ops/csrc/py_handlers.cpp) take the all-int, no-NULL case
+    themselves."""
     if None not in r and type(r[2]) is type(r[4]) is type(r[5]) is type(r[7]) is type(r[9]) is int:
         return Media._make(r)  # int columns arrived as int4/int8: no per-field conversion
     return Media(*(("" if v is None else v) if i in (0, 1, 3, 6, 8) else (0 if v is None else int(v))
@@ -36,30 +34,29 @@ class PostgresStore(MediaStore):
     name = "postgres"
 
     def __init__(self, dsn: Optional[str] = None, table: str = "media", pool_size: int = 4,
-                 create_schema: bool = False):
+                 create_schema: bool = False, columns: Optional[Mapping[str, str]] = None):
         if dsn is None:
             from ..dynamics import dyn
             dsn = dyn("postgres")
-        if not _IDENT.match(table):
-            raise ValueError(f"invalid table name {table!r}")
+        self.schema = MediaSchema(table, columns)
         self.dsn = dsn
         self.table = table
         self.pool_size = pool_size
         self.create_schema = create_schema
         self._pool: Optional[Pool] = None
-        self._select = f"SELECT {_COLS} FROM {table} WHERE id = $1"
-        self._update = f"UPDATE {table} SET status = $1 WHERE id = $2"
+        # the compiled handlers issue these two texts themselves (py_handlers.cpp pg_execute)
+        self._select = self.schema.select_by_id(pg_ph)
+        self._update = self.schema.update_status(pg_ph)
+        self._upsert = self.schema.upsert(pg_ph)
+
+    def describe(self) -> str:
+        return f"postgres {self.schema.describe()}"
 
     async def connect(self) -> None:
         if self._pool is None:
             self._pool = await Pool(self.dsn, self.pool_size).open()
             if self.create_schema:
-                await self._pool.execute(
-                    f"CREATE TABLE IF NOT EXISTS {self.table} (id TEXT PRIMARY KEY, name TEXT NOT NULL DEFAULT '', "
-                    "creator INTEGER NOT NULL DEFAULT 0, creator_id TEXT NOT NULL DEFAULT '', "
-                    "type INTEGER NOT NULL DEFAULT 0, source INTEGER NOT NULL DEFAULT 0, "
-                    "source_uri TEXT NOT NULL DEFAULT '', metadata INTEGER NOT NULL DEFAULT 0, "
-                    "metadata_id TEXT NOT NULL DEFAULT '', status INTEGER NOT NULL DEFAULT 0)")
+                await self._pool.execute(self.schema.create_table())
 
     async def close(self) -> None:
         if self._pool is not None:
@@ -85,17 +82,12 @@ class PostgresStore(MediaStore):
         return row_to_media(rows[0])
 
     async def upsert(self, media: Media) -> None:
-        await self._exec(
-            f"INSERT INTO {self.table} ({_COLS}) VALUES ($1,$2,$3,$4,$5,$6,$7,$8,$9,$10) "
-            "ON CONFLICT (id) DO UPDATE SET name = EXCLUDED.name, creator = EXCLUDED.creator, "
-            "creator_id = EXCLUDED.creator_id, type = EXCLUDED.type, source = EXCLUDED.source, "
-            "source_uri = EXCLUDED.source_uri, metadata = EXCLUDED.metadata, "
-            "metadata_id = EXCLUDED.metadata_id, status = EXCLUDED.status", tuple(media))
+        await self._exec(self._upsert, tuple(media))
 
     async def upsert_many(self, medias: Iterable[Media]) -> None:
         for m in medias:
             await self.upsert(m)
 
     async def count(self) -> int:
-        rows, _ = await self._exec(f"SELECT COUNT(*) FROM {self.table}")
+        rows, _ = await self._exec(self.schema.count())
         return int(rows[0][0])

@@ -12,37 +12,29 @@ import sqlite3
 from typing import Optional
 
 from .base import Media, MediaNotFound, MediaStore
-
-SCHEMA = """
-CREATE TABLE IF NOT EXISTS media (
-    id          TEXT PRIMARY KEY,
-    name        TEXT NOT NULL DEFAULT '',
-    creator     INTEGER NOT NULL DEFAULT 0,
-    creator_id  TEXT NOT NULL DEFAULT '',
-    type        INTEGER NOT NULL DEFAULT 0,
-    source      INTEGER NOT NULL DEFAULT 0,
-    source_uri  TEXT NOT NULL DEFAULT '',
-    metadata    INTEGER NOT NULL DEFAULT 0,
-    metadata_id TEXT NOT NULL DEFAULT '',
-    status      INTEGER NOT NULL DEFAULT 0
-)
-"""
-_COLS = "id, name, creator, creator_id, type, source, source_uri, metadata, metadata_id, status"
-
+from .schema import MediaSchema, sqlite_ph
 
 class SqliteStore(MediaStore):
     name = "sqlite"
 
-    def __init__(self, path: str = ":memory:"):
+    def __init__(self, path: str = ":memory:", table: str = "media", columns=None):
         self.path = path
+        self.schema = sc = MediaSchema(table, columns)
+        self._select = sc.select_by_id(sqlite_ph)
+        self._update = sc.update_status(sqlite_ph)
+        self._upsert = sc.upsert(sqlite_ph, excluded="excluded")
+        self._replace = self._upsert.split(" ON CONFLICT", 1)[0].replace("INSERT INTO", "INSERT OR REPLACE INTO", 1)
         self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="sqlite")
         self._conn: Optional[sqlite3.Connection] = None
 
     def _open(self) -> None:
         conn = sqlite3.connect(self.path, check_same_thread=False, isolation_level=None)
         conn.execute("PRAGMA journal_mode=WAL") if self.path != ":memory:" else None
-        conn.execute(SCHEMA)
+        conn.execute(self.schema.create_table())
         self._conn = conn
+
+    def describe(self) -> str:
+        return f"sqlite {self.path} {self.schema.describe()}"
 
     async def _run(self, fn, *args):
         loop = asyncio.get_running_loop()
@@ -65,12 +57,12 @@ class SqliteStore(MediaStore):
 
     async def update_status(self, media_id: str, status: int) -> None:
         def q():
-            self._need().execute("UPDATE media SET status = ? WHERE id = ?", (int(status), media_id))
+            self._need().execute(self._update, (int(status), media_id))
         await self._run(q)
 
     async def get_by_id(self, media_id: str) -> Media:
         def q():
-            return self._need().execute(f"SELECT {_COLS} FROM media WHERE id = ?", (media_id,)).fetchone()
+            return self._need().execute(self._select, (media_id,)).fetchone()
         row = await self._run(q)
         if row is None:
             raise MediaNotFound(media_id)
@@ -78,13 +70,7 @@ class SqliteStore(MediaStore):
 
     async def upsert(self, media: Media) -> None:
         def q():
-            self._need().execute(
-                f"INSERT INTO media ({_COLS}) VALUES (?,?,?,?,?,?,?,?,?,?) "
-                "ON CONFLICT(id) DO UPDATE SET name=excluded.name, creator=excluded.creator, "
-                "creator_id=excluded.creator_id, type=excluded.type, source=excluded.source, "
-                "source_uri=excluded.source_uri, metadata=excluded.metadata, "
-                "metadata_id=excluded.metadata_id, status=excluded.status",
-                tuple(getattr(media, f) for f in Media._fields))
+            self._need().execute(self._upsert, tuple(media))
         await self._run(q)
 
     async def upsert_many(self, medias) -> None:
@@ -93,11 +79,11 @@ class SqliteStore(MediaStore):
         def q():
             c = self._need()
             c.execute("BEGIN")
-            c.executemany(f"INSERT OR REPLACE INTO media ({_COLS}) VALUES (?,?,?,?,?,?,?,?,?,?)", rows)
+            c.executemany(self._replace, rows)
             c.execute("COMMIT")
         await self._run(q)
 
     async def count(self) -> int:
         def q():
-            return self._need().execute("SELECT COUNT(*) FROM media").fetchone()[0]
+            return self._need().execute(self.schema.count()).fetchone()[0]
         return await self._run(q)

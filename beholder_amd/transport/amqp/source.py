@@ -7,8 +7,9 @@ Reference usage (index.js:43-44,62,127)::
     amqp.listen('v1.telemetry.status', async rmsg => { ... rmsg.ack() })
 
 :class:`AmqpSource` does the same: one channel with ``basic.qos(prefetch)``
-(100), a durable queue per topic (named after the topic, so publishers use
-the default exchange with ``routing_key = topic``), manual acks.
+(100), one queue per topic, manual acks. Queue names, exchange and bindings come from
+:class:`.topology.Topology` (``service.amqp``); the default is a durable queue per topic,
+named after the topic, on the default exchange (publishers use ``routing_key = topic``).
 
 Reliability (amqp-connection-manager parity):
 
@@ -29,6 +30,7 @@ from ...ops import AckBatcher, Delivery, Settler
 from ...topics import TOPIC_IDS, topic_id
 from ..base import Source
 from .connection import Channel, Connection
+from .topology import Topology
 from .wire import AmqpError
 
 
@@ -38,8 +40,10 @@ class AmqpSource(Source):
     def __init__(self, url: str, prefetch: int = 100, retries: int = 2, *, logger=None,
                  durable: bool = True, heartbeat: Optional[int] = None, backoff_initial: float = 0.25,
                  backoff_max: float = 30.0, connect_timeout: float = 10.0, native: bool = True,
-                 coalesce_acks: bool = True, capture_headers: bool = False):
+                 coalesce_acks: bool = True, capture_headers: bool = False,
+                 topology: Optional[Topology] = None):
         self.url = url
+        self.topology = topology if topology is not None else Topology(durable=durable)
         self.capture_headers = capture_headers  # keep message headers on deliveries (trace context)
         self._prefetch = int(prefetch)
         self.retries = int(retries)
@@ -110,9 +114,10 @@ class AmqpSource(Source):
             ch = await conn.channel()
             await ch.basic_qos(self._prefetch)
             tags = {}
+            topo = self.topology
+            await topo.declare(ch, self._topics)
             for t in self._topics:
-                await ch.queue_declare(t, durable=self.durable)
-                tag = await ch.basic_consume(t, self._on_message, native_topic=TOPIC_IDS[t])
+                tag = await ch.basic_consume(topo.queue(t), self._on_message, native_topic=TOPIC_IDS[t])
                 tags[tag] = TOPIC_IDS[t]
         except BaseException:
             await conn.close()
@@ -218,6 +223,10 @@ class AmqpSource(Source):
         if self._event is not None:
             self._event.set()
 
+    def describe(self) -> str:
+        from ...sinks.http import redact
+        return f"amqp {redact(self.url)} prefetch={self._prefetch} {self.topology.describe(self._topics)}"
+
     def ready(self) -> bool:
         return self._ch is not None and self._ch.is_open and not self._closing
 
@@ -283,10 +292,13 @@ class AmqpSource(Source):
 
 
 class AmqpPublisher:
-    """``amqp.publish(topic, buffer)`` — what the other triton services call (default exchange)."""
+    """``amqp.publish(topic, buffer)`` — what the other triton services call. Routes through
+    ``topology`` (default: the default exchange, ``routing_key = topic``)."""
 
-    def __init__(self, url: str, confirm: bool = True, durable: bool = True, persistent: bool = True):
+    def __init__(self, url: str, confirm: bool = True, durable: bool = True, persistent: bool = True,
+                 topology: Optional[Topology] = None):
         self.url = url
+        self.topology = topology if topology is not None else Topology(durable=durable)
         self.confirm = confirm
         self.durable = durable
         self.persistent = persistent
@@ -303,10 +315,12 @@ class AmqpPublisher:
 
     async def publish(self, topic: str, body: bytes, wait: bool = False):
         if topic not in self._declared:
-            await self._ch.queue_declare(topic, durable=self.durable)
+            await self.topology.declare(self._ch, [topic])  # messages published before a consumer exists are kept
             self._declared.add(topic)
+        exchange, key = self.topology.publish_target(topic)
         props = {"delivery_mode": 2} if self.persistent else None
-        return await self._ch.basic_publish(body, routing_key=topic, properties=props, wait_confirm=wait)
+        return await self._ch.basic_publish(body, routing_key=key, exchange=exchange, properties=props,
+                                            wait_confirm=wait)
 
     async def flush(self) -> None:
         if self._ch is not None:
@@ -320,11 +334,11 @@ class AmqpPublisher:
             await self._conn.close()
 
 
-async def publish_frames(url: str, data: bytes) -> int:
+async def publish_frames(url: str, data: bytes, topology: Optional[Topology] = None) -> int:
     """Publish every frame of a framed stream to its topic queue (CLI ``publish``)."""
     from ...topics import topic_name
     from ..framing import iter_frames
-    pub = await AmqpPublisher(url).connect()
+    pub = await AmqpPublisher(url, topology=topology).connect()
     n = 0
     try:
         for tid, payload in iter_frames(data):

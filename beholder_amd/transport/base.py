@@ -54,6 +54,10 @@ class Source(abc.ABC):
     def stats(self) -> Dict:
         return {}
 
+    def describe(self) -> str:
+        """What the source consumes from, for the startup log line (service.py)."""
+        return self.kind
+
     def ready(self) -> bool:
         return True
 

@@ -70,10 +70,15 @@ class FdSource(Source):
         self._dl_lock = threading.Lock()
         self.abandoned_frames = 0
         self._settler = Settler(on_abandon=self._on_abandon)
+        self.policy = policy
         self._ingest = Ingest(capacity_bytes=capacity_bytes, capacity_events=capacity_events,
                               policy=policy, settler=self._settler)
         self._started = False
         self._closed = False
+
+    def describe(self) -> str:
+        where = self._path if self._path is not None else ("stdin" if self._fd == 0 else f"fd {self._fd}")
+        return f"{self.kind} {where} (framed; policy {self.policy})"
 
     # -- Source API -------------------------------------------------------------
     async def start(self, topics: Sequence[str] = ()) -> None:

@@ -37,6 +37,8 @@ def test_run_stdin_plumbing(tmp_path):
     assert stats["source"]["acked"] == 30  # progress handler always acks (Q7), even with Trello down
     lines = [json.loads(x) for x in r.stdout.decode().splitlines()]
     assert lines[0]["msg"] == "initialized" and lines[0]["name"] == "index.js"
+    # the unpinned transport / store layout is stated once, after index.js:157's line
+    assert lines[1]["msg"].startswith("consuming from fd stdin") and "store memory (4 rows)" in lines[1]["msg"]
 
 
 def test_run_config_error_exit_code(tmp_path):
