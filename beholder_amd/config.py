@@ -55,7 +55,8 @@ SERVICE_DEFAULTS: dict = {
         # index.js:28 — Prom.expose(); port/host are [inferred] (triton-core not vendored).
         "metrics": {"enabled": True, "host": "0.0.0.0", "port": 3000, "default_metrics": True},
         # index.js:11-13 — pino logger named after the file basename.
-        "log": {"level": "info", "name": "index.js"},
+        # positional_args: append (Q11 fix, extra args kept) | drop (pino@5's exact msg text)
+        "log": {"level": "info", "name": "index.js", "positional_args": "append"},
         # outbound sink HTTP: `h1` = native-parsed keep-alive client (sinks/h1.py), `aiohttp` = library client
         "http": {"timeout_s": 30.0, "client": "h1", "max_per_host": 100, "keepalive_s": 4.0},
         # SURVEY §5 race detection: opt-in per-mediaId serialisation (default off = parity, Q9).
@@ -285,6 +286,8 @@ class Config:
             raise ConfigError("service.ordering must be 'none' or 'per_media'")
         if svc["on_status_error"] not in ("leave_unacked", "nack_requeue", "nack_drop"):
             raise ConfigError("service.on_status_error must be leave_unacked|nack_requeue|nack_drop")
+        if svc["log"].get("positional_args", "append") not in ("append", "drop"):
+            raise ConfigError("service.log.positional_args must be 'append' or 'drop'")
         if svc["http"].get("client", "h1") not in ("h1", "aiohttp"):
             raise ConfigError("service.http.client must be 'h1' or 'aiohttp'")
         from .store.schema import MediaSchema

@@ -269,11 +269,12 @@ bool number_like(PyObject* v, double* d) {
 }
 
 // quick-format-unescaped (pino v5) + appended extra args. args = all positional args.
-bool quick_format_append(std::string& out, PyObject* const* args, Py_ssize_t nargs) {
+// drop_extra: pino@5 exactly (args with no specifier are dropped, quirk Q11 kept).
+bool quick_format_append(std::string& out, PyObject* const* args, Py_ssize_t nargs, bool drop_extra) {
   if (nargs == 0) return true;
   PyObject* f = args[0];
   if (!PyUnicode_CheckExact(f)) {
-    for (Py_ssize_t i = 0; i < nargs; ++i) {
+    for (Py_ssize_t i = 0; i < (drop_extra ? 1 : nargs); ++i) {
       if (i) out += ' ';
       if (!js_str_append(out, args[i])) return false;
     }
@@ -325,6 +326,7 @@ bool quick_format_append(std::string& out, PyObject* const* args, Py_ssize_t nar
     ++i;
   }
   out.append(fs + last, size_t(flen) - last);
+  if (drop_extra) return true;
   for (; ai < nargs; ++ai) {
     out += ' ';
     if (!js_str_append(out, args[ai])) return false;
@@ -334,7 +336,7 @@ bool quick_format_append(std::string& out, PyObject* const* args, Py_ssize_t nar
 
 // Appends one pino line for `args` to `out`. Returns false with a Python error set.
 bool append_line(std::string& out, long lvl, long long t, const char* prefix, Py_ssize_t plen, PyObject* extra,
-                 PyObject* const* argv, Py_ssize_t nargs) {
+                 PyObject* const* argv, Py_ssize_t nargs, bool drop_extra) {
   out += "{\"level\":";
   append_i64(out, lvl);
   out += ",\"time\":";
@@ -350,7 +352,7 @@ bool append_line(std::string& out, long lvl, long long t, const char* prefix, Py
   if (nargs) {
     static thread_local std::string msg;  // scratch: no allocation per line
     msg.clear();
-    if (!quick_format_append(msg, argv, nargs)) return false;
+    if (!quick_format_append(msg, argv, nargs, drop_extra)) return false;
     out += ",\"msg\":\"";
     json_escape_append(out, msg.data(), msg.size());
     out += '"';
@@ -385,7 +387,7 @@ PyObject* mod_format_line_impl(PyObject*, PyObject* const* a, Py_ssize_t n) {
   if (!prefix) return nullptr;
   std::string out;
   out.reserve(192);
-  if (!append_line(out, lvl, t, prefix, plen, a[3], &PyTuple_GET_ITEM(a[4], 0), PyTuple_GET_SIZE(a[4])))
+  if (!append_line(out, lvl, t, prefix, plen, a[3], &PyTuple_GET_ITEM(a[4], 0), PyTuple_GET_SIZE(a[4]), false))
     return nullptr;
   return PyUnicode_DecodeUTF8(out.data(), Py_ssize_t(out.size()), "strict");
 }
@@ -400,6 +402,7 @@ struct LogSinkObject {
   std::string* buf;
   size_t limit;
   bool binary;  // write() takes bytes (UTF-8): no decode here and no encode in a text layer
+  bool drop_extra;  // service.log.positional_args == "drop": pino@5's message text exactly
   unsigned long long counts[7];  // trace..fatal by level/10 - 1, [6] other
   unsigned long long bytes;
 };
@@ -426,20 +429,23 @@ PyObject* sink_new(PyTypeObject* type, PyObject*, PyObject*) {
   self->buf = new std::string();
   self->limit = 65536;
   self->binary = false;
+  self->drop_extra = false;
   memset(self->counts, 0, sizeof self->counts);
   self->bytes = 0;
   return reinterpret_cast<PyObject*>(self);
 }
 
 int sink_init(LogSinkObject* self, PyObject* args, PyObject* kwds) {
-  static const char* kwlist[] = {"write", "flush", "buffer_bytes", "binary", nullptr};
+  static const char* kwlist[] = {"write", "flush", "buffer_bytes", "binary", "drop_extra", nullptr};
   PyObject* w;
   PyObject* f = Py_None;
   Py_ssize_t lim = 65536;
   int binary = 0;
-  if (!PyArg_ParseTupleAndKeywords(args, kwds, "O|Onp", const_cast<char**>(kwlist), &w, &f, &lim, &binary))
+  int drop = 0;
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "O|Onpp", const_cast<char**>(kwlist), &w, &f, &lim, &binary, &drop))
     return -1;
   self->binary = binary != 0;
+  self->drop_extra = drop != 0;
   if (!PyCallable_Check(w)) {
     PyErr_SetString(PyExc_TypeError, "write must be callable");
     return -1;
@@ -484,7 +490,7 @@ void sink_dealloc(LogSinkObject* self) {
 bool sink_emit_core(LogSinkObject* self, long lvl, const char* prefix, Py_ssize_t plen, PyObject* extra,
                     PyObject* const* argv, Py_ssize_t nargs) {
   size_t before = self->buf->size();
-  if (!append_line(*self->buf, lvl, wall_ms(), prefix, plen, extra, argv, nargs)) {
+  if (!append_line(*self->buf, lvl, wall_ms(), prefix, plen, extra, argv, nargs, self->drop_extra)) {
     self->buf->resize(before);
     return false;
   }
@@ -562,6 +568,13 @@ PyObject* sink_get_counts(LogSinkObject* self, void*) {
 }
 PyObject* sink_get_pending(LogSinkObject* self, void*) { return PyLong_FromSize_t(self->buf->size()); }
 PyObject* sink_get_bytes(LogSinkObject* self, void*) { return PyLong_FromUnsignedLongLong(self->bytes); }
+PyObject* sink_get_drop(LogSinkObject* self, void*) { return PyBool_FromLong(self->drop_extra); }
+int sink_set_drop(LogSinkObject* self, PyObject* v, void*) {
+  int t = v ? PyObject_IsTrue(v) : 0;
+  if (t < 0) return -1;
+  self->drop_extra = t != 0;
+  return 0;
+}
 
 PyMethodDef sink_methods[] = {
     {"emit", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(sink_emit)), METH_FASTCALL,
@@ -575,6 +588,8 @@ PyGetSetDef sink_getset[] = {
     {"counts", reinterpret_cast<getter>(sink_get_counts), nullptr, "lines emitted per level", nullptr},
     {"pending_bytes", reinterpret_cast<getter>(sink_get_pending), nullptr, "buffered bytes", nullptr},
     {"bytes_written", reinterpret_cast<getter>(sink_get_bytes), nullptr, "bytes handed to write()", nullptr},
+    {"drop_extra", reinterpret_cast<getter>(sink_get_drop), reinterpret_cast<setter>(sink_set_drop),
+     "drop positional args that no format specifier consumes (pino@5 exactly)", nullptr},
     {nullptr, nullptr, nullptr, nullptr, nullptr}};
 
 PyTypeObject LogSinkType = {PyVarObject_HEAD_INIT(nullptr, 0)};
@@ -587,8 +602,17 @@ PyObject* mod_quick_format(PyObject*, PyObject* args) {
 
 PyObject* mod_quick_format_impl(PyObject*, PyObject* args) {
   std::string msg;
-  if (!quick_format_append(msg, &PyTuple_GET_ITEM(args, 0), PyTuple_GET_SIZE(args))) return nullptr;
+  if (!quick_format_append(msg, &PyTuple_GET_ITEM(args, 0), PyTuple_GET_SIZE(args), false)) return nullptr;
   return PyUnicode_DecodeUTF8(msg.data(), Py_ssize_t(msg.size()), "strict");
+}
+
+PyObject* mod_quick_format_drop(PyObject*, PyObject* args) {
+  BEHOLDER_TRY {
+    std::string msg;
+    if (!quick_format_append(msg, &PyTuple_GET_ITEM(args, 0), PyTuple_GET_SIZE(args), true)) return nullptr;
+    return PyUnicode_DecodeUTF8(msg.data(), Py_ssize_t(msg.size()), "strict");
+  }
+  BEHOLDER_CATCH(nullptr)
 }
 
 PyObject* mod_js_str_impl(PyObject*, PyObject* v);
@@ -849,6 +873,8 @@ PyMethodDef text_methods[] = {
     {"format_line", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(mod_format_line)), METH_FASTCALL,
      "format_line(level, time_ms, prefix, extra, args) -> pino JSON line"},
     {"quick_format", mod_quick_format, METH_VARARGS, "quick_format(*args) -> message text"},
+    {"quick_format_drop", mod_quick_format_drop, METH_VARARGS,
+     "quick_format_drop(*args) -> pino@5's message text (unconsumed positional args dropped)"},
     {"js_str", mod_js_str, METH_O, "JavaScript String(v)"},
     {"js_number", mod_js_number, METH_O, "JavaScript Number::toString"},
     {"quote_component", mod_quote_component, METH_O, "encodeURIComponent(String(v))"},

@@ -104,7 +104,8 @@ class Service:
                  logger: Optional[Logger] = None, serve_metrics: Optional[bool] = None):
         self.config = config
         svc = config.data["service"]
-        self.log = logger or Logger(name=svc["log"]["name"], level=svc["log"]["level"])
+        self.log = logger or Logger(name=svc["log"]["name"], level=svc["log"]["level"],
+                                    positional_args=svc["log"].get("positional_args", "append"))
         self._source = source
         self._store = store
         self._http = http

@@ -12,8 +12,10 @@ Message formatting follows pino's ``quick-format-unescaped`` for ``%s %d %i
 %f %j %o %O %%``. **Documented fix of quirk Q11** (SURVEY.md §2.6): pino v5
 silently *drops* positional arguments that have no format specifier, so the
 reference's ``logger.info('creating comment on', cardId, 'with text:', text)``
-(index.js:51) logs only ``"creating comment on"``. We append such extra
-arguments space-separated (like ``util.format``) so the information survives.
+(index.js:51) logs only ``"creating comment on"``. By default we append such extra
+arguments space-separated (like ``util.format``) so the information survives;
+``service.log.positional_args: drop`` (``Logger(positional_args="drop")``) keeps
+pino@5's exact message text, for log-based alerts written against the reference.
 
 Values are rendered with JavaScript's ``String()`` rules (:func:`js_str`), so
 message text matches the reference's template literals (``45`` not ``45.0``,
@@ -107,14 +109,18 @@ def _json_safe(v: Any) -> Any:
         return js_str(v)
 
 
-def quick_format(args: tuple) -> str:
-    """Format positional args like pino v5 (see module doc for the Q11 fix)."""
+POSITIONAL_ARGS = ("append", "drop")
+
+
+def quick_format(args: tuple, drop: bool = False) -> str:
+    """Format positional args like pino v5 (see module doc for the Q11 fix; ``drop``: pino v5
+    exactly, arguments no format specifier consumes are dropped)."""
     if not args:
         return ""
     f = args[0]
     rest = args[1:]
     if not isinstance(f, str):
-        return " ".join(js_str(a) for a in args)
+        return js_str(f) if drop else " ".join(js_str(a) for a in args)
     if not rest:
         return f
     out = []
@@ -160,7 +166,7 @@ def quick_format(args: tuple) -> str:
         i += 1
     out.append(f[last:])
     s = "".join(out)
-    if ai < len(rest):
+    if ai < len(rest) and not drop:
         s += " " + " ".join(js_str(a) for a in rest[ai:])
     return s
 
@@ -196,12 +202,12 @@ class _Shared:
 
     __slots__ = ("stream", "pid", "hostname", "sink")
 
-    def __init__(self, stream, buffer_bytes: int):
+    def __init__(self, stream, buffer_bytes: int, drop_extra: bool = False):
         self.stream = stream
         self.pid = os.getpid()
         self.hostname = socket.gethostname()
         write, binary = _writer(stream)
-        self.sink = _native.LogSink(write, getattr(stream, "flush", None), buffer_bytes, binary)
+        self.sink = _native.LogSink(write, getattr(stream, "flush", None), buffer_bytes, binary, drop_extra)
 
 
 class Logger(_native.LogCore):
@@ -216,12 +222,16 @@ class Logger(_native.LogCore):
     """
 
     def __init__(self, name: str = "index.js", level: str = "info", stream: Optional[TextIO] = None,
-                 bindings: Optional[dict] = None, _shared: Optional[_Shared] = None, buffer_bytes: int = 65536):
+                 bindings: Optional[dict] = None, _shared: Optional[_Shared] = None, buffer_bytes: int = 65536,
+                 positional_args: str = "append"):
         super().__init__()
         if level not in LEVELS:
             raise ValueError(f"unknown log level {level!r}")
+        if positional_args not in POSITIONAL_ARGS:
+            raise ValueError(f"positional_args must be append|drop, not {positional_args!r}")
         self.name = name
-        self._shared = _shared or _Shared(stream if stream is not None else sys.stdout, buffer_bytes)
+        self._shared = _shared or _Shared(stream if stream is not None else sys.stdout, buffer_bytes,
+                                          positional_args == "drop")
         self._bindings = dict(bindings or {})
         self._prefix = self._make_prefix()
         self.set_level(level)
@@ -255,6 +265,17 @@ class Logger(_native.LogCore):
         self._shared.sink.retarget(write, getattr(s, "flush", None), binary)
 
     @property
+    def positional_args(self) -> str:
+        """``append`` (Q11 fix) or ``drop`` (pino@5's text); shared with children."""
+        return "drop" if self._shared.sink.drop_extra else "append"
+
+    @positional_args.setter
+    def positional_args(self, mode: str) -> None:
+        if mode not in POSITIONAL_ARGS:
+            raise ValueError(f"positional_args must be append|drop, not {mode!r}")
+        self._shared.sink.drop_extra = mode == "drop"
+
+    @property
     def counts(self) -> Dict[str, int]:
         """Lines emitted per level (a logger and its children share one table)."""
         return dict(self._shared.sink.counts)
@@ -285,7 +306,7 @@ class Logger(_native.LogCore):
                  self._prefix]
         if args:
             parts.append(',"msg":')
-            parts.append(json.dumps(quick_format(args), ensure_ascii=False))
+            parts.append(json.dumps(quick_format(args, self._shared.sink.drop_extra), ensure_ascii=False))
         parts.append(',"v":1}\n')
         return "".join(parts)
 

@@ -64,12 +64,12 @@ class Rig:
     """Handlers wired to an in-memory store, a recording HTTP client and a captured log."""
 
     def __init__(self, config: Optional[Config] = None, medias=(), no_trello: Optional[bool] = None,
-                 http: Optional[RecordingHttpClient] = None):
+                 http: Optional[RecordingHttpClient] = None, positional_args: str = "append"):
         self.config = config or cfg()
         self.http = http or RecordingHttpClient()
         self.store = MemoryStore(list(medias))
         self.stream = MemoryStream()
-        self.log = Logger(stream=self.stream)
+        self.log = Logger(stream=self.stream, positional_args=positional_args)
         self.registry = Registry()
         self.progress = self.registry.counter("beholder_progress_updates_total",
                                               "Total number of messages processed in this processes lifetime",
