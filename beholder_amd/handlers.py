@@ -25,7 +25,9 @@ Q8  card moves use ``pos: 2``; comment text is
 Q9  no per-media ordering (opt-in serialisation lives in
     :mod:`beholder_amd.parallel.ordering`).
 
-Log messages are the reference's text, rendered with JS ``String()`` rules.
+Log messages are the reference's text, rendered with JS ``String()`` rules. Every
+reference-visible string (log text, sink paths and bodies, query names) comes from
+:data:`beholder_amd.texts.TEXTS`, which the compiled handlers read too.
 """
 from __future__ import annotations
 
@@ -35,6 +37,16 @@ from .models import proto
 from .sinks.trello import COMMENT_FALLBACK
 from .sinks.telegram import deployed_text
 from .ops import js_str
+from .texts import TEXTS, Template
+
+_LOG_STATUS, _LOG_MOVE = Template("log_status"), Template("log_move")
+_LOG_TELEGRAM, _LOG_EMBY = Template("log_telegram"), Template("log_emby")
+_LOG_COMMENT, _LOG_PROGRESS, _LOG_MISSING = TEXTS["log_comment"], TEXTS["log_progress"], TEXTS["log_missing_list"]
+_WARN_HOOKS, _WARN_PROGRESS = TEXTS["warn_hooks"], TEXTS["warn_progress"]
+_COMMENT, _COMMENT_HOST = Template("comment"), Template("comment_host")
+_PATH_COMMENT, _PATH_CARD = Template("path_comment"), Template("path_card")
+_Q_TEXT, _Q_LIST, _Q_POS = TEXTS["q_text"], TEXTS["q_list"], TEXTS["q_pos"]
+_MOVE_POS, _PARSE_MODE, _ERR_TO_LOWER = TEXTS["trello_move_pos"], TEXTS["telegram_parse_mode"], TEXTS["err_to_lower"]
 
 TRELLO_CREATOR = 1  # index.js:79 compares `media.creator === 1`
 
@@ -171,9 +183,8 @@ class TelemetryHandlers:
     # ------------------------------------------------------------------ C8 ---
     async def comment(self, card_id: Any, text: Optional[str]) -> None:
         """index.js:50-58."""
-        self.log.info("creating comment on", card_id, "with text:", text)
-        await self.trello.make_request("post", f"/1/cards/{js_str(card_id)}/actions/comments",
-                                       {"text": text or COMMENT_FALLBACK})
+        self.log.info(_LOG_COMMENT[0], card_id, _LOG_COMMENT[1], text)
+        await self.trello.make_request("post", _PATH_COMMENT(card_id), {_Q_TEXT: text or COMMENT_FALLBACK})
         self._comment_inc()
 
     # ----------------------------------------------------------------- C10 ---
@@ -184,7 +195,7 @@ class TelemetryHandlers:
         media_id = msg.mediaId
         status = msg.status
 
-        log.info(f"processing status update for media {js_str(media_id)}, status: {js_str(status)}")
+        log.info(_LOG_STATUS(media_id, status))
 
         upd = self._update_nowait
         if upd is not None:
@@ -203,13 +214,13 @@ class TelemetryHandlers:
         # TRELLO Movement (index.js:78-90)
         if media.creator == TRELLO_CREATOR:
             if status_text is None:  # `statusText.toLowerCase()` on undefined (Q6)
-                raise JsTypeError("Cannot read property 'toLowerCase' of undefined")
+                raise JsTypeError(_ERR_TO_LOWER)
             lists = self.lists
             list_pointer = _get(lists, status_text.lower())
             if js_truthy(list_pointer):
-                log.info(f"moving media card {js_str(media_id)} (card id {js_str(media.creatorId)})")
-                await self.trello.make_request("put", f"/1/cards/{js_str(media.creatorId)}",
-                                               {"idList": list_pointer, "pos": 2})
+                log.info(_LOG_MOVE(media_id, media.creatorId))
+                await self.trello.make_request("put", _PATH_CARD(media.creatorId),
+                                               {_Q_LIST: list_pointer, _Q_POS: _MOVE_POS})
             else:  # Q5
                 self._warn_missing_list(status, status_text)
 
@@ -217,25 +228,26 @@ class TelemetryHandlers:
             if media.status == self.deployed:
                 await self._deployed_hooks(media, media_id)
         except Exception as err:  # noqa: BLE001 — reference catches everything here
-            log.warn("failed to run deployed hooks:", err_message(err))
+            log.warn(_WARN_HOOKS, err_message(err))
 
         return rmsg.ack()  # index.js:124
 
     def _warn_missing_list(self, status: Any, status_text: Optional[str]) -> None:
         """index.js:88 (Q5)."""
-        self.log.warn("unable to find list for status", status, f"({js_str(status_text)})",
-                      f"avail ([{','.join(str(k) for k in self.lists.keys())}])")
+        text, paren, avail = _LOG_MISSING
+        self.log.warn(text, status, paren.replace("{}", js_str(status_text)),
+                      avail.replace("{}", ",".join(str(k) for k in self.lists.keys())))
 
     async def _deployed_hooks(self, media, media_id: Any) -> None:
         """Body of the DEPLOYED branch, index.js:95-118 (the caller holds the try of index.js:92)."""
         log = self.log
         tg_on, chat_id, tg_token, emby_on, emby_host, emby_key = self._hooks_plan()
         if tg_on:
-            log.info(f"informing telegram that media '{js_str(media_id)}' is available")
+            log.info(_LOG_TELEGRAM(media_id))
             await self.telegram.send_message(chat_id, deployed_text(media.name, media.metadataId),
-                                             "markdown", token=tg_token())
+                                             _PARSE_MODE, token=tg_token())
         if emby_on:
-            log.info(f"telling emby to refresh at {js_str(emby_host)}")
+            log.info(_LOG_EMBY(emby_host))
             await self.emby.refresh_library(host=emby_host, api_key=emby_key)
 
     # ----------------------------------------------------------------- C11 ---
@@ -249,12 +261,12 @@ class TelemetryHandlers:
             progress = msg.progress
             host = msg.host
 
-            log.info("processing progress update on media", media_id, "status", status, "percent", progress)
+            log.info(_LOG_PROGRESS[0], media_id, _LOG_PROGRESS[1], status, _LOG_PROGRESS[2], progress)
             plan = self._progress_plan.get(status)
             if plan is None:
                 status_text = self._status_names_p.get(status)  # index.js:134
                 if status_text is None:  # Q6
-                    raise JsTypeError("Cannot read property 'toLowerCase' of undefined")
+                    raise JsTypeError(_ERR_TO_LOWER)
                 plan = self._progress_plan[status] = (status_text,
                                                       self.progress_counter.child_for(status_text.lower()).inc)
             status_text, count = plan
@@ -264,12 +276,12 @@ class TelemetryHandlers:
             media = get(media_id) if get is not None else await self.store.get_by_id(media_id)  # index.js:140
 
             if media.creator == self.trello_creator:  # index.js:142
-                comment_text = f"{status_text}: Progress **{js_str(progress)}%**"  # Q8
+                comment_text = _COMMENT(status_text, progress)  # Q8
                 if js_truthy(host):
-                    comment_text += f" (_{js_str(host)}_)"
+                    comment_text += _COMMENT_HOST(host)
                 await self.comment(media.creatorId, comment_text)
         except Exception as err:  # noqa: BLE001 — index.js:149-151
-            log.warn("failed to update media progress", err_message(err))
+            log.warn(_WARN_PROGRESS, err_message(err))
             return rmsg.ack()
 
         return rmsg.ack()  # index.js:154

@@ -20,6 +20,7 @@
 // The rare branches (missing-list warning, DEPLOYED hooks) call the Python helpers that the
 // Python method calls too, so their text and ordering come from one place.
 #include <string>
+#include <vector>
 
 #include "py_common.hpp"
 #include "ring.hpp"
@@ -38,16 +39,66 @@ namespace {
 // interned attribute / literal strings
 PyObject *s_ack, *s_message, *s_content, *s_mediaId, *s_status, *s_progress, *s_host, *s_creator, *s_creatorId,
     *s_get_nowait, *s_update_nowait, *s_store, *s_get_by_id, *s_update_status, *s_trello, *s_make_request, *s_post,
-    *s_put, *s_text, *s_idList, *s_pos, *s_deployed_hooks, *s_warn_missing_list, *s_child_for, *s_inc, *s_lower,
+    *s_put, *s_deployed_hooks, *s_warn_missing_list, *s_child_for, *s_inc, *s_lower,
     *s_throw, *s_close, *s_lists, *s_no_trello, *s_deployed, *s_trello_creator, *s_log, *s_decode_status,
     *s_decode_progress, *s_status_names_s, *s_status_names_p, *s_progress_counter, *s_comment_inc, *s_key,
     *s_token, *s_base_url, *s_http, *s_timeout, *s_strict, *s_stats, *s_request, *s_params, *s_POST, *s_PUT,
     *s_record, *s_raise_for_status, *s_rows, *s_get_calls, *s_update_calls, *s_limiter, *s_retry,
-    *s_hooks_plan, *s_telegram, *s_emby, *s_name, *s_metadataId, *s_GET, *s_chat_id, *s_parse_mode,
-    *s_markdown, *s_api_key, *s_send_message, *s_refresh_library, *s_pool, *s_select, *s_update,
+    *s_hooks_plan, *s_telegram, *s_emby, *s_name, *s_metadataId, *s_GET,
+    *s_api_key, *s_send_message, *s_refresh_library, *s_pool, *s_select, *s_update,
     *s_execute, *kw_params_timeout, *kw_timeout;
-// log message literals (index.js:51,133,150)
-PyObject *m_progress, *m_status_kw, *m_percent, *m_creating, *m_with_text, *m_failed_progress, *m_failed_hooks;
+
+// Reference-visible text: read from beholder_amd/texts.py TEXTS when a NativeHandlers is built
+// (the same table handlers.py and the sink clients read; no such string is spelled here).
+enum TextObj : int {
+  X_LOG_COMMENT_0, X_LOG_COMMENT_1,                        // index.js:51
+  X_LOG_PROGRESS_0, X_LOG_PROGRESS_1, X_LOG_PROGRESS_2,    // index.js:133
+  X_WARN_HOOKS, X_WARN_PROGRESS,                           // index.js:121,150
+  X_COMMENT_FALLBACK, X_PARSE_MODE, X_MOVE_POS,            // index.js:54,105,85
+  X_Q_KEY, X_Q_TOKEN, X_Q_TEXT, X_Q_LIST, X_Q_POS, X_Q_CHAT, X_Q_PARSE_MODE, X_Q_API_KEY,
+  X_ERR_TO_LOWER,                                          // index.js:80,134 (Q6)
+  X_N
+};
+struct TextSpec {
+  int slot;
+  const char* key;
+  int item;  // index into a tuple value, -1 = the value itself
+  bool is_int;
+};
+const TextSpec kTextSpecs[] = {
+    {X_LOG_COMMENT_0, "log_comment", 0, false},   {X_LOG_COMMENT_1, "log_comment", 1, false},
+    {X_LOG_PROGRESS_0, "log_progress", 0, false}, {X_LOG_PROGRESS_1, "log_progress", 1, false},
+    {X_LOG_PROGRESS_2, "log_progress", 2, false}, {X_WARN_HOOKS, "warn_hooks", -1, false},
+    {X_WARN_PROGRESS, "warn_progress", -1, false}, {X_COMMENT_FALLBACK, "comment_fallback", -1, false},
+    {X_PARSE_MODE, "telegram_parse_mode", -1, false}, {X_MOVE_POS, "trello_move_pos", -1, true},
+    {X_Q_KEY, "q_trello_key", -1, false},          {X_Q_TOKEN, "q_trello_token", -1, false},
+    {X_Q_TEXT, "q_text", -1, false},               {X_Q_LIST, "q_list", -1, false},
+    {X_Q_POS, "q_pos", -1, false},                 {X_Q_CHAT, "q_chat", -1, false},
+    {X_Q_PARSE_MODE, "q_parse_mode", -1, false},   {X_Q_API_KEY, "q_api_key", -1, false},
+    {X_ERR_TO_LOWER, "err_to_lower", -1, false}};
+
+// templates: pieces between the `{}` holes
+enum Tpl : int {
+  T_LOG_STATUS, T_LOG_MOVE, T_LOG_TELEGRAM, T_LOG_EMBY,  // index.js:66,82,98,111
+  T_COMMENT, T_COMMENT_HOST,                             // index.js:143-146 (Q8)
+  T_TELEGRAM_TEXT,                                       // index.js:104
+  T_PATH_COMMENT, T_PATH_CARD, T_PATH_TELEGRAM, T_PATH_EMBY,
+  T_N
+};
+struct TplSpec {
+  int slot;
+  const char* key;
+  int holes;
+};
+const TplSpec kTplSpecs[] = {{T_LOG_STATUS, "log_status", 2},       {T_LOG_MOVE, "log_move", 2},
+                             {T_LOG_TELEGRAM, "log_telegram", 1},   {T_LOG_EMBY, "log_emby", 1},
+                             {T_COMMENT, "comment", 2},             {T_COMMENT_HOST, "comment_host", 1},
+                             {T_TELEGRAM_TEXT, "telegram_text", 2}, {T_PATH_COMMENT, "path_comment", 1},
+                             {T_PATH_CARD, "path_card", 1},         {T_PATH_TELEGRAM, "path_telegram", 1},
+                             {T_PATH_EMBY, "path_emby", 1}};
+struct Templates {
+  std::vector<std::string> t[T_N];
+};
 
 struct HandlersObject {
   PyObject_HEAD PyObject* h;  // the TelemetryHandlers
@@ -66,7 +117,8 @@ struct HandlersObject {
   PyObject* get_fn;         // handlers._get (JS property read on config nodes)
   PyObject* err_message;    // handlers.err_message
   PyObject* js_type_error;  // handlers.JsTypeError
-  PyObject* fallback;       // COMMENT_FALLBACK (index.js:54)
+  PyObject* x[X_N];         // TEXTS strings / constants (see TextObj)
+  Templates* tpl;           // TEXTS templates, split at their holes
   PyObject* res_s;          // decoded-message types when the decoders are native codecs (else NULL)
   PyObject* res_p;
   Py_ssize_t ix_s[2];       // TelemetryStatus slots: mediaId, status
@@ -81,12 +133,24 @@ struct HandlersObject {
   PyObject* row_to_media;   // store.postgres.row_to_media (rows that are not all-int / NULL-free)
   PyObject* not_found;      // store.base.MediaNotFound
   PyObject* one;            // TRELLO_CREATOR (index.js:79)
-  PyObject* two;            // pos: 2 (index.js:85)
   uint64_t completed_sync;
   uint64_t suspended;
   uint8_t no_trello;
   uint8_t native_log;
 };
+
+// out += template `t` with its holes filled by String(vals[i]) (as the reference's template literals)
+bool tpl_append(std::string& out, const HandlersObject* hs, int t, PyObject* v0, PyObject* v1 = nullptr) {
+  const std::vector<std::string>& p = hs->tpl->t[t];
+  out += p[0];
+  if (!text_js_str_append(out, v0)) return false;
+  out += p[1];
+  if (p.size() > 2) {
+    if (!text_js_str_append(out, v1)) return false;
+    out += p[2];
+  }
+  return true;
+}
 
 enum : uint8_t { K_STATUS = 0, K_PROGRESS = 1 };
 
@@ -254,7 +318,7 @@ PySendResult fail(CallObject* c) {
 }
 
 bool raise_to_lower_case(HandlersObject* hs) {
-  PyErr_SetString(hs->js_type_error, "Cannot read property 'toLowerCase' of undefined");
+  PyErr_SetObject(hs->js_type_error, hs->x[X_ERR_TO_LOWER]);
   return false;
 }
 
@@ -494,7 +558,7 @@ int trello_request(CallObject* c, PyObject* method, PyObject* method_upper, PyOb
   if (td) {  // {"key": self.key, "token": self.token, **options}
     PyObject* key = PyDict_GetItemWithError(td, s_key);
     PyObject* token = key ? PyDict_GetItemWithError(td, s_token) : nullptr;
-    if (!token || PyDict_SetItem(query, s_key, key) < 0 || PyDict_SetItem(query, s_token, token) < 0) {
+    if (!token || PyDict_SetItem(query, hs->x[X_Q_KEY], key) < 0 || PyDict_SetItem(query, hs->x[X_Q_TOKEN], token) < 0) {
       Py_DECREF(query);
       if (PyErr_Occurred()) return -1;
       td = nullptr;  // unexpected layout: generic path
@@ -636,9 +700,8 @@ int hook_telegram(CallObject* c, PyObject** out) {
   PyObject* plan = c->plan;
   int on = PyObject_IsTrue(PyTuple_GET_ITEM(plan, 0));
   if (on <= 0) return on < 0 ? -1 : 2;
-  std::string line = "informing telegram that media '";
-  if (!text_js_str_append(line, c->media_id)) return -1;
-  line += "' is available";
+  std::string line;
+  if (!tpl_append(line, hs, T_LOG_TELEGRAM, c->media_id)) return -1;
   PyObject* lo = unicode_from(line);
   bool ok = lo && log_line(hs, 30, &lo, 1);
   Py_XDECREF(lo);
@@ -646,10 +709,8 @@ int hook_telegram(CallObject* c, PyObject** out) {
   // arguments in the order Python evaluates them: chat_id, deployed_text(name, metadataId), token
   PyObject* name = PyObject_GetAttr(c->media, s_name);
   PyObject* meta = name ? PyObject_GetAttr(c->media, s_metadataId) : nullptr;
-  std::string text = "*New Anime:* ";
-  ok = meta && text_js_str_append(text, name);
-  text += "\nKitsu: https://kitsu.io/anime/";
-  ok = ok && text_js_str_append(text, meta);
+  std::string text;
+  ok = meta && tpl_append(text, hs, T_TELEGRAM_TEXT, name, meta);
   Py_XDECREF(name);
   Py_XDECREF(meta);
   if (!ok) return -1;
@@ -669,7 +730,7 @@ int hook_telegram(CallObject* c, PyObject** out) {
       Py_DECREF(tok);
       return -1;
     }
-    PyObject* args[5] = {tg, PyTuple_GET_ITEM(plan, 1), textobj, s_markdown, tok};
+    PyObject* args[5] = {tg, PyTuple_GET_ITEM(plan, 1), textobj, hs->x[X_PARSE_MODE], tok};
     PyObject* kw = PyTuple_Pack(1, s_token);
     PyObject* aw = kw ? PyObject_VectorcallMethod(s_send_message, args, 4, kw) : nullptr;
     Py_XDECREF(kw);
@@ -681,17 +742,15 @@ int hook_telegram(CallObject* c, PyObject** out) {
   PyObject* base = PyDict_GetItemWithError(cd, s_base_url);
   std::string url;
   ok = base && text_js_str_append(url, base);
-  url += "/bot";
-  ok = ok && text_js_str_append(url, tok);
-  url += "/sendMessage";
+  ok = ok && tpl_append(url, hs, T_PATH_TELEGRAM, tok);
   Py_DECREF(tok);
   if (!ok) {
     Py_DECREF(textobj);
     if (!PyErr_Occurred()) PyErr_SetString(PyExc_AttributeError, "TelegramClient.base_url missing");
     return -1;
   }
-  PyObject* keys[3] = {s_chat_id, s_text, s_parse_mode};
-  PyObject* vals[3] = {PyTuple_GET_ITEM(plan, 1), textobj, s_markdown};
+  PyObject* keys[3] = {hs->x[X_Q_CHAT], hs->x[X_Q_TEXT], hs->x[X_Q_PARSE_MODE]};
+  PyObject* vals[3] = {PyTuple_GET_ITEM(plan, 1), textobj, hs->x[X_PARSE_MODE]};
   k = sink_get(c, cd, url, keys, vals, 3, out);
   Py_DECREF(textobj);
   return k;
@@ -705,8 +764,8 @@ int hook_emby(CallObject* c, PyObject** out) {
   if (on <= 0) return on < 0 ? -1 : 2;
   PyObject* host = PyTuple_GET_ITEM(plan, 4);
   PyObject* key = PyTuple_GET_ITEM(plan, 5);
-  std::string line = "telling emby to refresh at ";
-  if (!text_js_str_append(line, host)) return -1;
+  std::string line;
+  if (!tpl_append(line, hs, T_LOG_EMBY, host)) return -1;
   PyObject* lo = unicode_from(line);
   bool ok = lo && log_line(hs, 30, &lo, 1);
   Py_XDECREF(lo);
@@ -723,9 +782,8 @@ int hook_emby(CallObject* c, PyObject** out) {
     return await_start(c, aw, out);
   }
   std::string url;
-  if (!text_js_str_append(url, host)) return -1;
-  url += "/emby/library/refresh";
-  PyObject* keys[1] = {s_api_key};
+  if (!tpl_append(url, hs, T_PATH_EMBY, host)) return -1;
+  PyObject* keys[1] = {hs->x[X_Q_API_KEY]};
   PyObject* vals[1] = {key};
   return sink_get(c, cd, url, keys, vals, 1, out);
 }
@@ -750,7 +808,8 @@ PySendResult step_progress(CallObject* c, PyObject* value, PyObject** result) {
       Py_DECREF(msg);
       if (!c->host) goto catch_;
       {  // index.js:133
-        PyObject* args[6] = {m_progress, c->media_id, m_status_kw, c->status, m_percent, c->progress};
+        PyObject* args[6] = {hs->x[X_LOG_PROGRESS_0], c->media_id, hs->x[X_LOG_PROGRESS_1], c->status,
+                             hs->x[X_LOG_PROGRESS_2], c->progress};
         if (!log_line(hs, 30, args, 6)) goto catch_;
       }
       PyObject* plan = PyDict_GetItemWithError(hs->progress_plan, c->status);
@@ -804,17 +863,10 @@ PySendResult step_progress(CallObject* c, PyObject* value, PyObject** result) {
       if (is_trello < 0) goto catch_;
       if (!is_trello) goto finish;
       std::string s;  // index.js:143-146 (Q8)
-      if (!text_js_str_append(s, c->status_text)) goto catch_;
-      s += ": Progress **";
-      if (!text_js_str_append(s, c->progress)) goto catch_;
-      s += "%**";
+      if (!tpl_append(s, hs, T_COMMENT, c->status_text, c->progress)) goto catch_;
       int has_host;
       js_truthy(c->host, &has_host);
-      if (has_host) {
-        s += " (_";
-        if (!text_js_str_append(s, c->host)) goto catch_;
-        s += "_)";
-      }
+      if (has_host && !tpl_append(s, hs, T_COMMENT_HOST, c->host)) goto catch_;
       PyObject* text = unicode_from(s);
       if (!text) goto catch_;
       PyObject* card = field(c->media, hs->media_cls, hs->ix_m[1], s_creatorId);
@@ -823,16 +875,15 @@ PySendResult step_progress(CallObject* c, PyObject* value, PyObject** result) {
         goto catch_;
       }
       // comment(cardId, text), index.js:50-58
-      PyObject* largs[4] = {m_creating, card, m_with_text, text};
+      PyObject* largs[4] = {hs->x[X_LOG_COMMENT_0], card, hs->x[X_LOG_COMMENT_1], text};
       bool ok = log_line(hs, 30, largs, 4);
-      std::string path = "/1/cards/";
-      ok = ok && text_js_str_append(path, card);
+      std::string path;
+      ok = ok && tpl_append(path, hs, T_PATH_COMMENT, card);
       Py_DECREF(card);
       if (!ok) {
         Py_DECREF(text);
         goto catch_;
       }
-      path += "/actions/comments";
       PyObject* pathobj = unicode_from(path);
       if (!pathobj) {
         Py_DECREF(text);
@@ -840,8 +891,8 @@ PySendResult step_progress(CallObject* c, PyObject* value, PyObject** result) {
       }
       int truthy;
       js_truthy(text, &truthy);
-      PyObject* okeys[1] = {s_text};
-      PyObject* ovals[1] = {truthy ? text : hs->fallback};
+      PyObject* okeys[1] = {hs->x[X_Q_TEXT]};
+      PyObject* ovals[1] = {truthy ? text : hs->x[X_COMMENT_FALLBACK]};
       k = trello_request(c, s_post, s_POST, pathobj, okeys, ovals, 1, &v);  // index.js:53-55
       Py_DECREF(pathobj);
       Py_DECREF(text);
@@ -867,7 +918,7 @@ PySendResult step_progress(CallObject* c, PyObject* value, PyObject** result) {
       return fail(c);
   }
 catch_:  // index.js:149-151 (Q7)
-  if (!catch_and_warn(hs, m_failed_progress)) return fail(c);
+  if (!catch_and_warn(hs, hs->x[X_WARN_PROGRESS])) return fail(c);
 finish:
   return finish_ack(c, result);  // index.js:151 / 154
 }
@@ -891,10 +942,8 @@ PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
       c->status = c->media_id ? field(msg, hs->res_s, hs->ix_s[1], s_status) : nullptr;
       Py_DECREF(msg);
       if (!c->status) return fail(c);
-      std::string s = "processing status update for media ";  // index.js:66
-      if (!text_js_str_append(s, c->media_id)) return fail(c);
-      s += ", status: ";
-      if (!text_js_str_append(s, c->status)) return fail(c);
+      std::string s;  // index.js:66
+      if (!tpl_append(s, hs, T_LOG_STATUS, c->media_id, c->status)) return fail(c);
       PyObject* line = unicode_from(s);
       if (!line) return fail(c);
       bool ok = log_line(hs, 30, &line, 1);
@@ -1013,13 +1062,10 @@ PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
         Py_DECREF(lp);
         return fail(c);
       }
-      std::string s = "moving media card ";  // index.js:82
-      bool ok = text_js_str_append(s, c->media_id);
-      s += " (card id ";
-      ok = ok && text_js_str_append(s, card);
-      s += ")";
-      std::string path = "/1/cards/";
-      ok = ok && text_js_str_append(path, card);
+      std::string s;  // index.js:82
+      bool ok = tpl_append(s, hs, T_LOG_MOVE, c->media_id, card);
+      std::string path;
+      ok = ok && tpl_append(path, hs, T_PATH_CARD, card);
       Py_DECREF(card);
       PyObject* line = ok ? unicode_from(s) : nullptr;
       ok = line && log_line(hs, 30, &line, 1);
@@ -1029,8 +1075,8 @@ PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
         Py_DECREF(lp);
         return fail(c);
       }
-      PyObject* okeys[2] = {s_idList, s_pos};
-      PyObject* ovals[2] = {lp, hs->two};
+      PyObject* okeys[2] = {hs->x[X_Q_LIST], hs->x[X_Q_POS]};
+      PyObject* ovals[2] = {lp, hs->x[X_MOVE_POS]};
       k = trello_request(c, s_put, s_PUT, pathobj, okeys, ovals, 2, &v);  // index.js:83-86
       Py_DECREF(pathobj);
       Py_DECREF(lp);
@@ -1102,7 +1148,7 @@ PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
       return fail(c);
   }
 hooks_catch:  // index.js:120-122 (Q4)
-  if (!catch_and_warn(hs, m_failed_hooks)) return fail(c);
+  if (!catch_and_warn(hs, hs->x[X_WARN_HOOKS])) return fail(c);
   return finish_ack(c, result);
 }
 
@@ -1335,7 +1381,7 @@ int hs_traverse(HandlersObject* hs, visitproc visit, void* arg) {
   Py_VISIT(hs->get_fn);
   Py_VISIT(hs->err_message);
   Py_VISIT(hs->js_type_error);
-  Py_VISIT(hs->fallback);
+  for (PyObject* o : hs->x) Py_VISIT(o);
   Py_VISIT(hs->res_s);
   Py_VISIT(hs->res_p);
   Py_VISIT(hs->media_cls);
@@ -1366,7 +1412,7 @@ int hs_clear(HandlersObject* hs) {
   Py_CLEAR(hs->get_fn);
   Py_CLEAR(hs->err_message);
   Py_CLEAR(hs->js_type_error);
-  Py_CLEAR(hs->fallback);
+  for (PyObject*& o : hs->x) Py_CLEAR(o);
   Py_CLEAR(hs->res_s);
   Py_CLEAR(hs->res_p);
   Py_CLEAR(hs->media_cls);
@@ -1384,7 +1430,7 @@ void hs_dealloc(HandlersObject* hs) {
   PyObject_GC_UnTrack(hs);
   hs_clear(hs);
   Py_XDECREF(hs->one);
-  Py_XDECREF(hs->two);
+  delete hs->tpl;
   Py_TYPE(hs)->tp_free(reinterpret_cast<PyObject*>(hs));
 }
 
@@ -1392,7 +1438,7 @@ PyObject* hs_new(PyTypeObject* type, PyObject*, PyObject*) {
   HandlersObject* hs = reinterpret_cast<HandlersObject*>(type->tp_alloc(type, 0));
   if (!hs) return nullptr;
   hs->one = PyLong_FromLong(1);
-  hs->two = PyLong_FromLong(2);
+  hs->tpl = new Templates();
   return reinterpret_cast<PyObject*>(hs);
 }
 
@@ -1456,6 +1502,50 @@ PyObject* import_attr(const char* module, const char* name) {
   return v;
 }
 
+// TEXTS (beholder_amd/texts.py) -> hs->x / hs->tpl. Shapes are checked: a template with the
+// wrong number of holes fails construction instead of rendering wrong text.
+int load_texts(HandlersObject* hs) {
+  PyObject* table = import_attr("beholder_amd.texts", "TEXTS");
+  if (!table) return -1;
+  if (!PyDict_Check(table)) {
+    Py_DECREF(table);
+    PyErr_SetString(PyExc_TypeError, "texts.TEXTS must be a dict");
+    return -1;
+  }
+  for (const TextSpec& sp : kTextSpecs) {
+    PyObject* v = PyDict_GetItemString(table, sp.key);
+    if (v && sp.item >= 0) v = PyTuple_Check(v) && PyTuple_GET_SIZE(v) > sp.item ? PyTuple_GET_ITEM(v, sp.item) : nullptr;
+    if (!v || (sp.is_int ? !PyLong_CheckExact(v) : !PyUnicode_CheckExact(v))) {
+      Py_DECREF(table);
+      PyErr_Format(PyExc_TypeError, "texts.TEXTS[%s]: missing or of the wrong type", sp.key);
+      return -1;
+    }
+    Py_INCREF(v);
+    Py_XSETREF(hs->x[sp.slot], v);
+  }
+  for (const TplSpec& sp : kTplSpecs) {
+    PyObject* v = PyDict_GetItemString(table, sp.key);
+    Py_ssize_t n = 0;
+    const char* u = v && PyUnicode_CheckExact(v) ? PyUnicode_AsUTF8AndSize(v, &n) : nullptr;
+    std::vector<std::string>& out = hs->tpl->t[sp.slot];
+    out.clear();
+    if (u) {
+      std::string str(u, size_t(n));
+      size_t at = 0;
+      for (size_t h; (h = str.find("{}", at)) != std::string::npos; at = h + 2) out.push_back(str.substr(at, h - at));
+      out.push_back(str.substr(at));
+    }
+    if (!u || int(out.size()) != sp.holes + 1) {
+      Py_DECREF(table);
+      if (!PyErr_Occurred())
+        PyErr_Format(PyExc_ValueError, "texts.TEXTS[%s]: expected a str with %d holes", sp.key, sp.holes);
+      return -1;
+    }
+  }
+  Py_DECREF(table);
+  return 0;
+}
+
 // NativeHandlers(handlers)
 int hs_init(HandlersObject* hs, PyObject* args, PyObject* kwds) {
   PyObject* h;
@@ -1498,8 +1588,7 @@ int hs_init(HandlersObject* hs, PyObject* args, PyObject* kwds) {
   hs->get_fn = module_attr(h, "_get");
   hs->err_message = hs->get_fn ? module_attr(h, "err_message") : nullptr;
   hs->js_type_error = hs->err_message ? module_attr(h, "JsTypeError") : nullptr;
-  hs->fallback = hs->js_type_error ? module_attr(h, "COMMENT_FALLBACK") : nullptr;
-  if (!hs->progress_plan || !hs->fallback || !hs->one || !hs->two) return -1;
+  if (!hs->progress_plan || !hs->js_type_error || !hs->one || load_texts(hs) < 0) return -1;
   hs->trello_cls = import_attr("beholder_amd.sinks.trello", "TrelloClient");
   hs->telegram_cls = hs->trello_cls ? import_attr("beholder_amd.sinks.telegram", "TelegramClient") : nullptr;
   hs->emby_cls = hs->telegram_cls ? import_attr("beholder_amd.sinks.emby", "EmbyClient") : nullptr;
@@ -1561,9 +1650,6 @@ int init_handler_types(PyObject* m) {
               {&s_make_request, "make_request"},
               {&s_post, "post"},
               {&s_put, "put"},
-              {&s_text, "text"},
-              {&s_idList, "idList"},
-              {&s_pos, "pos"},
               {&s_deployed_hooks, "_deployed_hooks"},
               {&s_warn_missing_list, "_warn_missing_list"},
               {&s_child_for, "child_for"},
@@ -1605,9 +1691,6 @@ int init_handler_types(PyObject* m) {
               {&s_name, "name"},
               {&s_metadataId, "metadataId"},
               {&s_GET, "GET"},
-              {&s_chat_id, "chat_id"},
-              {&s_parse_mode, "parse_mode"},
-              {&s_markdown, "markdown"},
               {&s_api_key, "api_key"},
               {&s_send_message, "send_message"},
               {&s_refresh_library, "refresh_library"},
@@ -1615,14 +1698,8 @@ int init_handler_types(PyObject* m) {
               {&s_select, "_select"},
               {&s_update, "_update"},
               {&s_execute, "execute"},
-              {&s_retry, "retry"},
-              {&m_progress, "processing progress update on media"},
-              {&m_status_kw, "status"},
-              {&m_percent, "percent"},
-              {&m_creating, "creating comment on"},
-              {&m_with_text, "with text:"},
-              {&m_failed_progress, "failed to update media progress"},
-              {&m_failed_hooks, "failed to run deployed hooks:"}};
+              {&s_retry, "retry"}};
+
   for (auto& s : strs)
     if (!(*s.slot = intern(s.text))) return -1;
   kw_params_timeout = PyTuple_Pack(2, s_params, s_timeout);

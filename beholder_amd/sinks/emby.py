@@ -5,7 +5,10 @@ from typing import Any, Optional
 
 from .http import HttpClient, HttpResponse, observed, with_query
 from .ratelimit import guarded
-from ..utils.log import js_str
+from ..texts import TEXTS, Template
+
+_PATH = Template("path_emby")
+_Q_KEY = TEXTS["q_api_key"]
 
 
 class EmbyClient:
@@ -22,8 +25,8 @@ class EmbyClient:
     async def refresh_library(self, host: Any = ..., api_key: Any = ...) -> HttpResponse:
         h = self.host if host is ... else host
         k = self.api_key if api_key is ... else api_key
-        url = f"{js_str(h)}/emby/library/refresh"
-        full = with_query(url, {"api_key": k}, rfc3986=True)  # request `qs` -> qs 6.5 encoding
+        url = _PATH(h)
+        full = with_query(url, {_Q_KEY: k}, rfc3986=True)  # request `qs` -> qs 6.5 encoding
         if self.limiter is not None or self.retry is not None:
             r = await guarded(self.limiter, self.retry,
                               lambda: observed(self.stats, self.http.request("GET", full, timeout=self.timeout)))

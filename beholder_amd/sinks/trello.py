@@ -18,8 +18,11 @@ from typing import Any, Mapping, Optional
 
 from .http import HttpClient, HttpError, HttpResponse
 from .ratelimit import guarded
+from ..texts import TEXTS, Template
 
-COMMENT_FALLBACK = "Failed to retrieve comment text."  # index.js:54
+COMMENT_FALLBACK = TEXTS["comment_fallback"]  # index.js:54
+_K, _T = TEXTS["q_trello_key"], TEXTS["q_trello_token"]
+_COMMENT_PATH, _CARD_PATH = Template("path_comment"), Template("path_card")
 
 _METHODS = {"get": "GET", "post": "POST", "put": "PUT", "delete": "DELETE"}
 
@@ -39,7 +42,7 @@ class TrelloClient:
         self.stats = observer.child("trello") if observer is not None else None
 
     def create_query(self) -> dict:
-        return {"key": self.key, "token": self.token}
+        return {_K: self.key, _T: self.token}
 
     async def make_request(self, method: str, path: str, options: Optional[Mapping[str, Any]] = None) -> HttpResponse:
         """``trello.makeRequest(requestMethod, path, options)``."""
@@ -48,8 +51,7 @@ class TrelloClient:
             raise HttpError("Unsupported requestMethod. Pass one of these methods: POST, GET, PUT, DELETE.")
         if not path.startswith("/"):
             raise HttpError("Path must start with /")
-        query = {"key": self.key, "token": self.token, **options} if options else \
-            {"key": self.key, "token": self.token}
+        query = {_K: self.key, _T: self.token, **options} if options else {_K: self.key, _T: self.token}
         if self.limiter is not None or self.retry is not None:
             r = await guarded(self.limiter, self.retry, lambda: self._send(m, path, query))
         else:
@@ -74,8 +76,7 @@ class TrelloClient:
     makeRequest = make_request  # noqa: N815 (reference name)
 
     async def add_comment(self, card_id: str, text: Optional[str]) -> HttpResponse:
-        return await self.make_request("post", f"/1/cards/{card_id}/actions/comments",
-                                       {"text": text or COMMENT_FALLBACK})
+        return await self.make_request("post", _COMMENT_PATH(card_id), {TEXTS["q_text"]: text or COMMENT_FALLBACK})
 
-    async def move_card(self, card_id: str, list_id: str, pos: Any = 2) -> HttpResponse:
-        return await self.make_request("put", f"/1/cards/{card_id}", {"idList": list_id, "pos": pos})
+    async def move_card(self, card_id: str, list_id: str, pos: Any = TEXTS["trello_move_pos"]) -> HttpResponse:
+        return await self.make_request("put", _CARD_PATH(card_id), {TEXTS["q_list"]: list_id, TEXTS["q_pos"]: pos})
