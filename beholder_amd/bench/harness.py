@@ -125,7 +125,8 @@ class _Producer(threading.Thread):
 async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_events: int = 0,
                       n_media: int = 10000, media=None, log_level: str = "info", rss_probe=None,
                       sink_delay_s: float = 0.0, gc_probe: "Optional[GcPauses]" = None,
-                      http=None, sink_url: Optional[str] = None, prefetch: Optional[int] = None) -> dict:
+                      http=None, sink_url: Optional[str] = None, prefetch: Optional[int] = None,
+                      reset_latency_after: int = 0) -> dict:
     from ..config import Config
     from ..service import Service
     from ..sinks import RecordingHttpClient
@@ -171,10 +172,20 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
         gc_probe.__enter__()  # steady state only: init's own collect+freeze is not a run pause
     if rss_probe is not None:
         sampler = asyncio.ensure_future(sample_rss())
+    cold: dict = {}
+    if reset_latency_after:  # warm-up (connection pools filling) kept out of the latency histograms
+        async def reset_later():
+            while _settled(src.settler) < reset_latency_after:
+                await asyncio.sleep(0.001)
+            cold.update(src.settler.handle_latency.summary())
+            src.settler.reset_latency()
+        resetter = asyncio.ensure_future(reset_later())
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
     prod.start()
     stats = await svc.run()
+    if reset_latency_after:
+        resetter.cancel()
     elapsed = time.perf_counter() - t0
     ru1 = resource.getrusage(resource.RUSAGE_SELF)
     cpu_s = (ru1.ru_utime + ru1.ru_stime) - (ru0.ru_utime + ru0.ru_stime)
@@ -204,6 +215,9 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
         "cpu_us_per_event": cpu_s / s["acked"] * 1e6 if s["acked"] else None,
         "error_samples": sink.samples,
         **({"rss_curve_mb": rss_curve} if rss_probe is not None else {}),
+        **({"warmup_events": reset_latency_after,
+            "warmup_handle_latency_us": {k: v / 1e3 for k, v in cold.items() if k.startswith("p")}}
+           if reset_latency_after else {}),
     }
 
 
@@ -267,12 +281,16 @@ def run_config(name: str, *, duration_s: Optional[float] = None, events: Optiona
     return res
 
 
+def _settled(settler) -> int:
+    return settler.acked + settler.abandoned + settler.nacked + settler.rejected
+
+
 async def _wait_acked(settler, n: int, task, stall_s: float = 15.0) -> None:
     """Until n deliveries are settled one way or another (acked, or abandoned under Q1), the
     service stops, or nothing moves for ``stall_s`` (a broken run must not hang the bench)."""
     last, t_last = -1, time.monotonic()
     while not task.done():
-        done = settler.acked + settler.abandoned + settler.nacked + settler.rejected
+        done = _settled(settler)
         if done >= n:
             return
         if done != last:
@@ -341,7 +359,8 @@ def _http_tcp(w: Workload, n: int, servers: int = 3, clients=("h1", "aiohttp")) 
         for kind, cls in (("h1", H1Client), ("aiohttp", AiohttpClient)):
             if kind not in clients:
                 continue
-            out[kind] = asyncio.run(_run_inproc(evs, 0, media=w.media, http=cls(timeout_s=30), sink_url=url))
+            out[kind] = asyncio.run(_run_inproc(evs, 0, media=w.media, http=cls(timeout_s=30), sink_url=url,
+                                                reset_latency_after=min(5000, n // 10)))
     finally:
         out["server_requests_total"] = _reap(procs).get("requests", 0)
     return out
@@ -360,6 +379,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2) -> dict:
     from ..transport.amqp import AmqpSource
     from ..utils.log import Logger
 
+    warm = min(5000, n // 10)
     bport, bprocs = _spawn("beholder_amd.bench.replay_broker", 1, ("--events", str(n)))
     procs = list(bprocs)
     out: dict = {"events": n, "prefetch": 100}
@@ -381,12 +401,19 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2) -> dict:
             svc = Service(Config.from_dict(cfgd), source=src, store=store, http=http, logger=Logger(stream=sink),
                           serve_metrics=False)
             await svc.init()
+            task = asyncio.ensure_future(svc.run())
+            # warm-up: connection pools fill (up to prefetch sink connections, the PG pool), code
+            # paths get hot; then the latency histograms restart and the clock starts
+            await _wait_acked(src.settler, warm, task)
+            cold = dict(src.settler.handle_latency.summary())
+            src.settler.reset_latency()
+            settled0 = _settled(src.settler)
             ru0 = resource.getrusage(resource.RUSAGE_SELF)
             t0 = time.perf_counter()
-            task = asyncio.ensure_future(svc.run())
             await _wait_acked(src.settler, n, task)
             elapsed = time.perf_counter() - t0
             ru1 = resource.getrusage(resource.RUSAGE_SELF)
+            measured = _settled(src.settler) - settled0
             await asyncio.sleep(0.05)  # let the last acks flush
             svc.request_stop()
             await task
@@ -396,15 +423,17 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2) -> dict:
             await svc.close()
             sink.close()
             cpu = (ru1.ru_utime + ru1.ru_stime) - (ru0.ru_utime + ru0.ru_stime)
-            return elapsed, stats, cpu, ru1.ru_stime - ru0.ru_stime, pg_conns, http_stats
+            return elapsed, stats, cpu, ru1.ru_stime - ru0.ru_stime, pg_conns, http_stats, measured, cold
 
-        elapsed, stats, cpu, sys_s, pg_conns, http_stats = asyncio.run(go())
+        elapsed, stats, cpu, sys_s, pg_conns, http_stats, m, cold = asyncio.run(go())
         acked = stats["source"]["acked"]
         out.update({
-            "acked": acked, "elapsed_s": elapsed, "ingest_rate_eps": acked / elapsed,
-            "cpu_us_per_event": cpu / acked * 1e6 if acked else None,
-            "sys_cpu_us_per_event": sys_s / acked * 1e6 if acked else None,
+            "acked": acked, "warmup_events": warm, "measured_events": m, "elapsed_s": elapsed,
+            "ingest_rate_eps": m / elapsed if elapsed > 0 else None,
+            "cpu_us_per_event": cpu / m * 1e6 if m else None,
+            "sys_cpu_us_per_event": sys_s / m * 1e6 if m else None,
             "handle_latency_us": {k: v / 1e3 for k, v in stats["handle_latency_ns"].items() if k.startswith("p")},
+            "warmup_handle_latency_us": {k: v / 1e3 for k, v in cold.items() if k.startswith("p")},
             "errors": sum(stats.get("handler_errors", {}).values()),
             "pg_connections": pg_conns, "http": http_stats,
         })
@@ -444,12 +473,19 @@ def _amqp(n: int) -> dict:
             svc = Service(Config.from_dict(bench_config()), source=src, store=MemoryStore(w.media),
                           http=RecordingHttpClient(keep=8), logger=Logger(stream=sink), serve_metrics=False)
             await svc.init()
+            task = asyncio.ensure_future(svc.run())
+            # warm-up: connection pools fill (up to prefetch sink connections, the PG pool), code
+            # paths get hot; then the latency histograms restart and the clock starts
+            await _wait_acked(src.settler, warm, task)
+            cold = dict(src.settler.handle_latency.summary())
+            src.settler.reset_latency()
+            settled0 = _settled(src.settler)
             ru0 = resource.getrusage(resource.RUSAGE_SELF)
             t0 = time.perf_counter()
-            task = asyncio.ensure_future(svc.run())
             await _wait_acked(src.settler, n, task)
             elapsed = time.perf_counter() - t0
             ru1 = resource.getrusage(resource.RUSAGE_SELF)
+            measured = _settled(src.settler) - settled0
             await asyncio.sleep(0.05)  # let the last acks flush
             svc.request_stop()
             await task

@@ -990,4 +990,35 @@ int init_driver_types(PyObject* m) {
   return PyModule_AddObject(m, "IOFuture", reinterpret_cast<PyObject*>(&IOFutureType));
 }
 
+// C-level IOFuture access for other translation units (py_netconn.cpp): reply futures created
+// and completed without a Python-level call.
+PyObject* iofuture_new(PyObject* loop) {
+  PyObject* args = PyTuple_Pack(1, loop);
+  if (!args) return nullptr;
+  PyObject* f = iof_new(&IOFutureType, args, nullptr);
+  Py_DECREF(args);
+  return f;
+}
+
+bool iofuture_done(PyObject* f) { return reinterpret_cast<IOFutureObject*>(f)->state != 0; }
+
+// resolve / reject unless already finished: 0 ok (or already done), -1 error
+int iofuture_resolve(PyObject* f, PyObject* v) {
+  if (iofuture_done(f)) return 0;
+  PyObject* r = iof_finish_result(reinterpret_cast<IOFutureObject*>(f), v, true);
+  if (!r) return -1;
+  Py_DECREF(r);
+  return 0;
+}
+
+int iofuture_reject(PyObject* f, PyObject* exc) {
+  if (iofuture_done(f)) return 0;
+  PyObject* r = iof_finish_exc(reinterpret_cast<IOFutureObject*>(f), exc, true);
+  if (!r) return -1;
+  Py_DECREF(r);
+  return 0;
+}
+
+bool is_iofuture(PyObject* o) { return Py_TYPE(o) == &IOFutureType; }
+
 }  // namespace beholder

@@ -1,0 +1,696 @@
+// NetConn: a plain-TCP client socket driven straight from the asyncio loop, with the wire
+// protocol handled here.
+//
+// The production path (every status event does up to 2 Postgres round trips
+// and 3 HTTP requests, index.js:68,76,83,99,112; every progress event 1 + 1, index.js:53,140)
+// spends most of its CPU in asyncio's Python-level transport machinery: per reply a
+// `_read_ready` -> `_read_ready__data_received` -> `Protocol.data_received` chain, per request
+// a `transport.write`. A NetConn replaces that for plain TCP connections once they are
+// established (handshakes, TLS and authentication stay on asyncio transports):
+//
+//   c = NetConn(fd, loop, kind, owner, parser, ...)
+//       the loop's selector calls c's bound on_readable for the fd (loop.add_reader): one
+//       recv(2), the bytes fed to the native parser (H1Parser / PgReader), completed replies
+//       resolve their IOFuture here (ops.IOFuture.resolve: a handler waiting through the
+//       native Driver resumes in the same call).
+//   c.write(data)          send(2) now; what the kernel does not take is kept and sent from
+//                          on_writable (loop.add_writer), in order.
+//
+// kind "h1": one request in flight (HTTP/1.1 keep-alive, no pipelining):
+//   c.request(data, waiter, head)   starts the parser, sets the waiter, writes the request.
+// kind "pg": pipelined extended-protocol queries (store/pgwire.py semantics):
+//   c.execute(sql, params) -> IOFuture   Parse (first use of sql on this connection) + Bind +
+//                          Describe + Execute + Sync appended to the output, flushed once per
+//                          loop iteration (loop.call_soon), replies matched FIFO.
+//
+// Rare paths call back into Python on `owner`: _net_lost(exc or None) when the peer closes or
+// the socket fails (the fd is already closed and unregistered), _net_error(exc) for a protocol
+// error or an unsolicited reply, _net_message(type, body) for out-of-band Postgres messages.
+#include <errno.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <deque>
+#include <string>
+
+#include "py_common.hpp"
+
+namespace beholder {
+
+PyObject* iofuture_new(PyObject* loop);
+bool iofuture_done(PyObject* f);
+int iofuture_resolve(PyObject* f, PyObject* v);
+int iofuture_reject(PyObject* f, PyObject* exc);
+int pg_bind_append(std::string& o, const char* name, size_t nlen, PyObject* params);
+
+namespace {
+
+PyObject *s_add_reader, *s_remove_reader, *s_add_writer, *s_remove_writer, *s_call_soon, *s_feed, *s_start,
+    *s_head, *s_net_lost, *s_net_error, *s_net_message;
+
+enum : uint8_t { K_H1 = 0, K_PG = 1 };
+constexpr size_t kReadSize = 256 * 1024;
+
+struct PgPending {
+  PyObject* fut;
+  PyObject* new_sql;  // the statement text if this query carried its Parse, else NULL
+  PyObject* name;     // bytes
+};
+
+struct NetConnObject {
+  PyObject_HEAD int fd;
+  uint8_t kind;
+  uint8_t closed;
+  uint8_t writing;          // add_writer registered
+  uint8_t flush_scheduled;  // pg: a call_soon(flush) is pending
+  PyObject* loop;
+  PyObject* owner;
+  PyObject* on_readable;  // bound builtins handed to the loop
+  PyObject* on_writable;
+  PyObject* flush_cb;
+  PyObject* parser;  // H1Parser / PgReader
+  PyObject* feed;    // parser.feed
+  PyObject* start;   // h1: parser.start
+  PyObject* waiter;  // h1: the reply future of the request in flight
+  PyObject* stmts;   // pg: dict sql -> statement name (shared with store/pgwire.py)
+  PyObject* pg_error;
+  PyObject* closed_exc;  // raised by write/request/execute once closed
+  std::string* out;
+  std::deque<PgPending>* pending;
+  uint64_t n_stmts, bytes_in, bytes_out, recvs, sends;
+};
+
+PyTypeObject NetConnType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+char* read_buf() {
+  static char* buf = static_cast<char*>(PyMem_RawMalloc(kReadSize));  // one event-loop thread
+  return buf;
+}
+
+// Stops watching the fd and closes it (idempotent). Errors from the loop are swallowed: this
+// runs on teardown paths.
+void shut(NetConnObject* c) {
+  if (c->fd < 0) return;
+  PyObject *et, *ev, *tb;
+  PyErr_Fetch(&et, &ev, &tb);
+  PyObject* fdo = PyLong_FromLong(c->fd);
+  if (fdo && c->loop) {
+    PyObject* r = PyObject_CallMethodOneArg(c->loop, s_remove_reader, fdo);
+    if (!r) PyErr_Clear();
+    Py_XDECREF(r);
+    if (c->writing) {
+      r = PyObject_CallMethodOneArg(c->loop, s_remove_writer, fdo);
+      if (!r) PyErr_Clear();
+      Py_XDECREF(r);
+    }
+  }
+  Py_XDECREF(fdo);
+  PyErr_Clear();
+  PyErr_Restore(et, ev, tb);
+  ::close(c->fd);
+  c->fd = -1;
+  c->writing = 0;
+  c->closed = 1;
+  c->out->clear();
+}
+
+// owner.<name>(arg) for a rare path; the error (if any) is reported, never propagated into the loop
+void notify(NetConnObject* c, PyObject* name, PyObject* arg) {
+  if (!c->owner) return;
+  PyObject* r = PyObject_CallMethodOneArg(c->owner, name, arg ? arg : Py_None);
+  if (!r) {
+    PyErr_WriteUnraisable(c->owner);
+  } else {
+    Py_DECREF(r);
+  }
+}
+
+// Peer closed (exc NULL) or the socket failed: close, then tell the owner.
+void lost(NetConnObject* c, int err) {
+  shut(c);
+  if (err) {
+    errno = err;
+    PyErr_SetFromErrno(PyExc_OSError);
+    PyObject *et, *ev, *tb;
+    PyErr_Fetch(&et, &ev, &tb);
+    PyErr_NormalizeException(&et, &ev, &tb);
+    Py_XDECREF(et);
+    Py_XDECREF(tb);
+    notify(c, s_net_lost, ev);
+    Py_XDECREF(ev);
+  } else {
+    notify(c, s_net_lost, nullptr);
+  }
+}
+
+int watch_writes(NetConnObject* c) {
+  if (c->writing) return 0;
+  PyObject* fdo = PyLong_FromLong(c->fd);
+  if (!fdo) return -1;
+  PyObject* r = PyObject_CallMethodObjArgs(c->loop, s_add_writer, fdo, c->on_writable, nullptr);
+  Py_DECREF(fdo);
+  if (!r) return -1;
+  Py_DECREF(r);
+  c->writing = 1;
+  return 0;
+}
+
+// Sends c->out (after anything already queued). 0 ok, -1 Python error. A socket error closes
+// the connection and is reported to the owner (_net_lost) before this returns.
+int send_out(NetConnObject* c) {
+  std::string& o = *c->out;
+  size_t off = 0;
+  while (off < o.size()) {
+    ssize_t n = ::send(c->fd, o.data() + off, o.size() - off, MSG_NOSIGNAL);
+    if (n > 0) {
+      off += size_t(n);
+      c->bytes_out += uint64_t(n);
+      ++c->sends;
+      continue;
+    }
+    if (n < 0 && errno == EINTR) continue;
+    if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
+    int err = n < 0 ? errno : EPIPE;
+    o.clear();
+    lost(c, err);
+    return 0;
+  }
+  o.erase(0, off);
+  if (!o.empty()) return watch_writes(c);
+  if (c->writing) {
+    PyObject* fdo = PyLong_FromLong(c->fd);
+    if (!fdo) return -1;
+    PyObject* r = PyObject_CallMethodOneArg(c->loop, s_remove_writer, fdo);
+    Py_DECREF(fdo);
+    if (!r) return -1;
+    Py_DECREF(r);
+    c->writing = 0;
+  }
+  return 0;
+}
+
+int append_bytes(NetConnObject* c, PyObject* data) {
+  Py_buffer v;
+  if (PyObject_GetBuffer(data, &v, PyBUF_SIMPLE) < 0) return -1;
+  c->out->append(static_cast<const char*>(v.buf), size_t(v.len));
+  PyBuffer_Release(&v);
+  return 0;
+}
+
+PyObject* closed_error(NetConnObject* c) {
+  PyErr_SetString(c->closed_exc ? c->closed_exc : PyExc_ConnectionError, "connection is closed");
+  return nullptr;
+}
+
+// ---- reply dispatch -----------------------------------------------------------------------
+void on_h1_data(NetConnObject* c, PyObject* mv) {
+  PyObject* r = PyObject_CallOneArg(c->feed, mv);
+  if (!r) {  // malformed response: the owner fails the request and drops the connection
+    PyObject *et, *ev, *tb;
+    PyErr_Fetch(&et, &ev, &tb);
+    PyErr_NormalizeException(&et, &ev, &tb);
+    Py_XDECREF(et);
+    Py_XDECREF(tb);
+    notify(c, s_net_error, ev);
+    Py_XDECREF(ev);
+    return;
+  }
+  if (r == Py_None) {
+    Py_DECREF(r);
+    return;
+  }
+  PyObject* w = c->waiter;
+  c->waiter = nullptr;
+  if (!w || iofuture_done(w)) {
+    Py_XDECREF(w);
+    Py_DECREF(r);
+    notify(c, s_net_error, nullptr);  // unsolicited response
+    return;
+  }
+  if (iofuture_resolve(w, r) < 0) PyErr_WriteUnraisable(w);  // the waiting handler resumes here
+  Py_DECREF(w);
+  Py_DECREF(r);
+}
+
+void on_pg_data(NetConnObject* c, PyObject* mv) {
+  PyObject* items = PyObject_CallOneArg(c->feed, mv);
+  if (!items) {
+    PyObject *et, *ev, *tb;
+    PyErr_Fetch(&et, &ev, &tb);
+    PyErr_NormalizeException(&et, &ev, &tb);
+    Py_XDECREF(et);
+    Py_XDECREF(tb);
+    notify(c, s_net_error, ev);
+    Py_XDECREF(ev);
+    return;
+  }
+  Py_ssize_t n = PyList_GET_SIZE(items);
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* it = PyList_GET_ITEM(items, i);
+    if (PyTuple_GET_SIZE(it) != 4) {  // NoticeResponse / ParameterStatus / ...
+      PyObject* r = c->owner ? PyObject_CallMethodObjArgs(c->owner, s_net_message, PyTuple_GET_ITEM(it, 0),
+                                                          PyTuple_GET_ITEM(it, 1), nullptr)
+                             : (Py_INCREF(Py_None), Py_None);
+      if (!r) PyErr_WriteUnraisable(c->owner);
+      Py_XDECREF(r);
+      continue;
+    }
+    if (c->pending->empty()) {  // ReadyForQuery with nothing outstanding
+      notify(c, s_net_error, nullptr);
+      break;
+    }
+    PgPending p = c->pending->front();
+    c->pending->pop_front();
+    PyObject* rows = PyTuple_GET_ITEM(it, 0);
+    PyObject* tag = PyTuple_GET_ITEM(it, 1);
+    PyObject* err = PyTuple_GET_ITEM(it, 2);
+    int rc = 0;
+    if (err != Py_None) {
+      if (p.new_sql && PyTuple_GET_ITEM(it, 3) != Py_True) {  // failed Parse: forget the statement
+        PyObject* cur = PyDict_GetItemWithError(c->stmts, p.new_sql);
+        if (cur && PyObject_RichCompareBool(cur, p.name, Py_EQ) == 1) {
+          if (PyDict_DelItem(c->stmts, p.new_sql) < 0) PyErr_Clear();
+        }
+        PyErr_Clear();
+      }
+      PyObject* exc = PyObject_CallOneArg(c->pg_error, err);
+      rc = exc ? iofuture_reject(p.fut, exc) : -1;
+      Py_XDECREF(exc);
+    } else {
+      PyObject* res = PyTuple_Pack(2, rows, tag);
+      rc = res ? iofuture_resolve(p.fut, res) : -1;  // a handler waiting on it resumes here
+      Py_XDECREF(res);
+    }
+    if (rc < 0) PyErr_WriteUnraisable(p.fut);
+    Py_DECREF(p.fut);
+    Py_XDECREF(p.new_sql);
+    Py_DECREF(p.name);
+  }
+  Py_DECREF(items);
+}
+
+// ---- type ---------------------------------------------------------------------------------
+PyObject* nc_new(PyTypeObject* type, PyObject*, PyObject*) {
+  NetConnObject* c = reinterpret_cast<NetConnObject*>(type->tp_alloc(type, 0));
+  if (!c) return nullptr;
+  c->fd = -1;
+  c->closed = 1;
+  c->out = new (std::nothrow) std::string();
+  c->pending = new (std::nothrow) std::deque<PgPending>();
+  if (!c->out || !c->pending) {
+    Py_DECREF(c);
+    return PyErr_NoMemory();
+  }
+  return reinterpret_cast<PyObject*>(c);
+}
+
+void drop_pending(NetConnObject* c) {
+  while (!c->pending->empty()) {
+    PgPending p = c->pending->front();
+    c->pending->pop_front();
+    Py_DECREF(p.fut);
+    Py_XDECREF(p.new_sql);
+    Py_DECREF(p.name);
+  }
+}
+
+int nc_traverse(NetConnObject* c, visitproc visit, void* arg) {
+  Py_VISIT(c->loop);
+  Py_VISIT(c->owner);
+  Py_VISIT(c->on_readable);
+  Py_VISIT(c->on_writable);
+  Py_VISIT(c->flush_cb);
+  Py_VISIT(c->parser);
+  Py_VISIT(c->feed);
+  Py_VISIT(c->start);
+  Py_VISIT(c->waiter);
+  Py_VISIT(c->stmts);
+  Py_VISIT(c->pg_error);
+  Py_VISIT(c->closed_exc);
+  if (c->pending) {
+    for (const PgPending& p : *c->pending) {
+      Py_VISIT(p.fut);
+      Py_VISIT(p.new_sql);
+      Py_VISIT(p.name);
+    }
+  }
+  return 0;
+}
+
+int nc_clear(NetConnObject* c) {
+  Py_CLEAR(c->owner);
+  Py_CLEAR(c->on_readable);
+  Py_CLEAR(c->on_writable);
+  Py_CLEAR(c->flush_cb);
+  Py_CLEAR(c->parser);
+  Py_CLEAR(c->feed);
+  Py_CLEAR(c->start);
+  Py_CLEAR(c->waiter);
+  Py_CLEAR(c->stmts);
+  Py_CLEAR(c->pg_error);
+  Py_CLEAR(c->closed_exc);
+  if (c->pending) drop_pending(c);
+  return 0;
+}
+
+void nc_dealloc(NetConnObject* c) {
+  PyObject_GC_UnTrack(c);
+  if (c->fd >= 0) shut(c);  // normally closed by the owner first
+  nc_clear(c);
+  Py_CLEAR(c->loop);
+  delete c->out;
+  delete c->pending;
+  Py_TYPE(c)->tp_free(reinterpret_cast<PyObject*>(c));
+}
+
+PyObject* nc_on_readable(NetConnObject* c, PyObject*);
+PyObject* nc_on_writable(NetConnObject* c, PyObject*);
+PyObject* nc_flush(NetConnObject* c, PyObject*);
+
+// NetConn(fd, loop, kind, owner, parser, stmts=None, pg_error=None, closed_exc=ConnectionError):
+// takes ownership of fd (a connected TCP socket) and starts watching it.
+int nc_init(NetConnObject* c, PyObject* args, PyObject* kwds) {
+  static const char* kwlist[] = {"fd", "loop", "kind", "owner", "parser", "stmts", "pg_error", "closed_exc", nullptr};
+  int fd;
+  PyObject *loop, *owner, *parser, *stmts = Py_None, *pg_error = Py_None, *closed_exc = PyExc_ConnectionError;
+  const char* kind;
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "iOsOO|OOO", const_cast<char**>(kwlist), &fd, &loop, &kind, &owner,
+                                   &parser, &stmts, &pg_error, &closed_exc))
+    return -1;
+  if (!PyExceptionClass_Check(closed_exc)) {
+    PyErr_SetString(PyExc_TypeError, "closed_exc must be an exception class");
+    return -1;
+  }
+  if (c->fd >= 0 || c->loop) {
+    PyErr_SetString(PyExc_RuntimeError, "NetConn already initialised");
+    return -1;
+  }
+  if (strcmp(kind, "h1") == 0) {
+    c->kind = K_H1;
+  } else if (strcmp(kind, "pg") == 0) {
+    c->kind = K_PG;
+    if (!PyDict_Check(stmts) || pg_error == Py_None) {
+      PyErr_SetString(PyExc_TypeError, "kind 'pg' needs stmts (dict) and pg_error");
+      return -1;
+    }
+  } else {
+    PyErr_SetString(PyExc_ValueError, "kind must be 'h1' or 'pg'");
+    return -1;
+  }
+  if (fd < 0) {
+    PyErr_SetString(PyExc_ValueError, "invalid fd");
+    return -1;
+  }
+  Py_INCREF(loop);
+  c->loop = loop;
+  Py_INCREF(closed_exc);
+  c->closed_exc = closed_exc;
+  Py_INCREF(owner);
+  c->owner = owner;
+  Py_INCREF(parser);
+  c->parser = parser;
+  c->feed = PyObject_GetAttr(parser, s_feed);
+  if (!c->feed) return -1;
+  if (c->kind == K_H1) {
+    c->start = PyObject_GetAttr(parser, s_start);
+    if (!c->start) return -1;
+  } else {
+    Py_INCREF(stmts);
+    c->stmts = stmts;
+    Py_INCREF(pg_error);
+    c->pg_error = pg_error;
+  }
+  c->on_readable = PyObject_GetAttrString(reinterpret_cast<PyObject*>(c), "_on_readable");
+  c->on_writable = c->on_readable ? PyObject_GetAttrString(reinterpret_cast<PyObject*>(c), "_on_writable") : nullptr;
+  c->flush_cb = c->on_writable ? PyObject_GetAttrString(reinterpret_cast<PyObject*>(c), "flush") : nullptr;
+  if (!c->flush_cb) return -1;
+  PyObject* fdo = PyLong_FromLong(fd);
+  if (!fdo) return -1;
+  PyObject* r = PyObject_CallMethodObjArgs(loop, s_add_reader, fdo, c->on_readable, nullptr);
+  Py_DECREF(fdo);
+  if (!r) return -1;
+  Py_DECREF(r);
+  c->fd = fd;  // owned from here on
+  c->closed = 0;
+  return 0;
+}
+
+PyObject* nc_on_readable(NetConnObject* c, PyObject*) {
+  if (c->fd < 0) Py_RETURN_NONE;
+  char* buf = read_buf();
+  if (!buf) return PyErr_NoMemory();
+  ssize_t n;
+  do {
+    n = ::recv(c->fd, buf, kReadSize, 0);
+  } while (n < 0 && errno == EINTR);
+  if (n < 0) {
+    if (errno == EAGAIN || errno == EWOULDBLOCK) Py_RETURN_NONE;
+    lost(c, errno);
+    Py_RETURN_NONE;
+  }
+  if (n == 0) {
+    lost(c, 0);
+    Py_RETURN_NONE;
+  }
+  c->bytes_in += uint64_t(n);
+  ++c->recvs;
+  PyObject* mv = PyMemoryView_FromMemory(buf, Py_ssize_t(n), PyBUF_READ);
+  if (!mv) return nullptr;
+  Py_INCREF(c);  // a resumed handler may drop the last other reference
+  if (c->kind == K_H1) {
+    on_h1_data(c, mv);
+  } else {
+    on_pg_data(c, mv);
+  }
+  Py_DECREF(mv);
+  Py_DECREF(c);
+  Py_RETURN_NONE;
+}
+
+PyObject* nc_on_writable(NetConnObject* c, PyObject*) {
+  if (c->fd < 0) Py_RETURN_NONE;
+  if (send_out(c) < 0) return nullptr;
+  Py_RETURN_NONE;
+}
+
+// write(data): send now, keep the rest for on_writable
+PyObject* nc_write(NetConnObject* c, PyObject* data) {
+  BEHOLDER_TRY {
+    if (c->fd < 0) return closed_error(c);
+    if (append_bytes(c, data) < 0) return nullptr;
+    if (c->writing) Py_RETURN_NONE;  // queued behind earlier bytes
+    if (send_out(c) < 0) return nullptr;
+    Py_RETURN_NONE;
+  }
+  BEHOLDER_CATCH(nullptr)
+}
+
+// h1: request(data, waiter, head) — parser.start(head=head), waiter set, request written
+PyObject* nc_request(NetConnObject* c, PyObject* const* a, Py_ssize_t n) {
+  BEHOLDER_TRY {
+    if (n != 3 || c->kind != K_H1) {
+      PyErr_SetString(PyExc_TypeError, "request(data, waiter, head) on an h1 NetConn");
+      return nullptr;
+    }
+    if (c->fd < 0) return closed_error(c);
+    PyObject* kw = PyTuple_Pack(1, s_head);
+    if (!kw) return nullptr;
+    PyObject* args[1] = {a[2]};
+    PyObject* r = PyObject_Vectorcall(c->start, args, 0, kw);  // parser.start(head=head)
+    Py_DECREF(kw);
+    if (!r) return nullptr;
+    Py_DECREF(r);
+    Py_INCREF(a[1]);
+    Py_XSETREF(c->waiter, a[1]);
+    if (append_bytes(c, a[0]) < 0) return nullptr;
+    if (c->writing) Py_RETURN_NONE;
+    if (send_out(c) < 0) return nullptr;
+    Py_RETURN_NONE;
+  }
+  BEHOLDER_CATCH(nullptr)
+}
+
+// pg: execute(sql, params) -> IOFuture resolving to (rows, tag) or rejected with pg_error(fields)
+PyObject* nc_execute(NetConnObject* c, PyObject* const* a, Py_ssize_t n) {
+  BEHOLDER_TRY {
+    if (n < 1 || n > 2 || c->kind != K_PG) {
+      PyErr_SetString(PyExc_TypeError, "execute(sql, params=()) on a pg NetConn");
+      return nullptr;
+    }
+    if (c->fd < 0) return closed_error(c);
+    PyObject* sql = a[0];
+    PyObject* params = n > 1 ? a[1] : nullptr;
+    PyObject* name = PyDict_GetItemWithError(c->stmts, sql);
+    PyObject* new_sql = nullptr;
+    std::string& o = *c->out;
+    size_t mark = o.size();
+    if (name) {
+      Py_INCREF(name);
+    } else {
+      if (PyErr_Occurred()) return nullptr;
+      Py_ssize_t sl;
+      const char* st = PyUnicode_AsUTF8AndSize(sql, &sl);
+      if (!st) return nullptr;
+      name = PyBytes_FromFormat("b%zu", static_cast<size_t>(++c->n_stmts));
+      if (!name || PyDict_SetItem(c->stmts, sql, name) < 0) {
+        Py_XDECREF(name);
+        return nullptr;
+      }
+      new_sql = sql;
+      Py_INCREF(new_sql);
+      size_t nl = size_t(PyBytes_GET_SIZE(name));
+      uint32_t len = uint32_t(4 + nl + 1 + size_t(sl) + 1 + 2);
+      char hdr[5] = {'P', char(len >> 24), char(len >> 16), char(len >> 8), char(len)};
+      o.append(hdr, 5);
+      o.append(PyBytes_AS_STRING(name), nl);
+      o.push_back('\0');
+      o.append(st, size_t(sl));
+      o.append("\0\0\0", 3);  // terminator + no parameter types
+    }
+    PyObject* empty = nullptr;
+    if (!params) {
+      empty = PyTuple_New(0);
+      params = empty;
+    }
+    int rc = params ? pg_bind_append(o, PyBytes_AS_STRING(name), size_t(PyBytes_GET_SIZE(name)), params) : -1;
+    Py_XDECREF(empty);
+    PyObject* fut = rc < 0 ? nullptr : iofuture_new(c->loop);
+    if (!fut) {
+      o.resize(mark);
+      Py_DECREF(name);
+      Py_XDECREF(new_sql);
+      return nullptr;
+    }
+    Py_INCREF(fut);
+    c->pending->push_back({fut, new_sql, name});
+    if (!c->flush_scheduled) {
+      PyObject* h = PyObject_CallMethodOneArg(c->loop, s_call_soon, c->flush_cb);
+      if (!h) {
+        c->pending->pop_back();
+        o.resize(mark);
+        Py_DECREF(fut);
+        Py_DECREF(fut);
+        Py_DECREF(name);
+        Py_XDECREF(new_sql);
+        return nullptr;
+      }
+      Py_DECREF(h);
+      c->flush_scheduled = 1;
+    }
+    return fut;
+  }
+  BEHOLDER_CATCH(nullptr)
+}
+
+// flush(): write out what execute() queued (scheduled once per loop iteration)
+PyObject* nc_flush(NetConnObject* c, PyObject*) {
+  c->flush_scheduled = 0;
+  if (c->fd < 0 || c->out->empty() || c->writing) Py_RETURN_NONE;
+  if (send_out(c) < 0) return nullptr;
+  Py_RETURN_NONE;
+}
+
+// fail_all(exc): pg: every outstanding query fails with exc (connection gone)
+PyObject* nc_fail_all(NetConnObject* c, PyObject* exc) {
+  c->closed = 1;
+  while (!c->pending->empty()) {
+    PgPending p = c->pending->front();
+    c->pending->pop_front();
+    int rc = iofuture_reject(p.fut, exc);
+    Py_DECREF(p.fut);
+    Py_XDECREF(p.new_sql);
+    Py_DECREF(p.name);
+    if (rc < 0) return nullptr;
+  }
+  Py_RETURN_NONE;
+}
+
+// take_waiter(): h1: the pending reply future (or None), cleared
+PyObject* nc_take_waiter(NetConnObject* c, PyObject*) {
+  PyObject* w = c->waiter;
+  c->waiter = nullptr;
+  if (!w) Py_RETURN_NONE;
+  return w;
+}
+
+PyObject* nc_close(NetConnObject* c, PyObject*) {
+  c->flush_scheduled = 0;
+  if (c->fd >= 0 && !c->out->empty() && !c->writing) {  // best effort: what is queued goes out
+    ::send(c->fd, c->out->data(), c->out->size(), MSG_NOSIGNAL | MSG_DONTWAIT);
+  }
+  shut(c);
+  Py_RETURN_NONE;
+}
+
+PyObject* nc_abort(NetConnObject* c, PyObject*) {
+  shut(c);
+  Py_RETURN_NONE;
+}
+
+PyObject* nc_get_closed(NetConnObject* c, void*) { return PyBool_FromLong(c->closed || c->fd < 0); }
+PyObject* nc_get_fd(NetConnObject* c, void*) { return PyLong_FromLong(c->fd); }
+PyObject* nc_get_pending(NetConnObject* c, void*) { return PyLong_FromSize_t(c->pending->size()); }
+PyObject* nc_get_buffered(NetConnObject* c, void*) { return PyLong_FromSize_t(c->out->size()); }
+PyObject* nc_get_waiting(NetConnObject* c, void*) { return PyBool_FromLong(c->waiter != nullptr); }
+PyObject* nc_get_stats(NetConnObject* c, void*) {
+  return Py_BuildValue("{s:K,s:K,s:K,s:K}", "bytes_in", c->bytes_in, "bytes_out", c->bytes_out, "recvs", c->recvs,
+                       "sends", c->sends);
+}
+
+PyMethodDef nc_methods[] = {
+    {"_on_readable", reinterpret_cast<PyCFunction>(nc_on_readable), METH_NOARGS, "loop reader callback"},
+    {"_on_writable", reinterpret_cast<PyCFunction>(nc_on_writable), METH_NOARGS, "loop writer callback"},
+    {"write", reinterpret_cast<PyCFunction>(nc_write), METH_O, "write(data): send, queue what the kernel refuses"},
+    {"request", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(nc_request)), METH_FASTCALL,
+     "h1: request(data, waiter, head): start the parser, set the reply future, send"},
+    {"execute", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(nc_execute)), METH_FASTCALL,
+     "pg: execute(sql, params=()) -> IOFuture of (rows, tag)"},
+    {"flush", reinterpret_cast<PyCFunction>(nc_flush), METH_NOARGS, "pg: send the queued queries"},
+    {"fail_all", reinterpret_cast<PyCFunction>(nc_fail_all), METH_O, "pg: reject every outstanding query"},
+    {"take_waiter", reinterpret_cast<PyCFunction>(nc_take_waiter), METH_NOARGS, "h1: pop the reply future"},
+    {"close", reinterpret_cast<PyCFunction>(nc_close), METH_NOARGS, "send what is queued (best effort), close"},
+    {"abort", reinterpret_cast<PyCFunction>(nc_abort), METH_NOARGS, "close now"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyGetSetDef nc_getset[] = {
+    {"closed", reinterpret_cast<getter>(nc_get_closed), nullptr, "fd closed (or failed)", nullptr},
+    {"fd", reinterpret_cast<getter>(nc_get_fd), nullptr, "the socket fd, -1 once closed", nullptr},
+    {"pending", reinterpret_cast<getter>(nc_get_pending), nullptr, "pg: queries awaiting their reply", nullptr},
+    {"buffered", reinterpret_cast<getter>(nc_get_buffered), nullptr, "bytes not yet taken by the kernel", nullptr},
+    {"waiting", reinterpret_cast<getter>(nc_get_waiting), nullptr, "h1: a reply is awaited", nullptr},
+    {"stats", reinterpret_cast<getter>(nc_get_stats), nullptr, "bytes / syscall counters", nullptr},
+    {nullptr, nullptr, nullptr, nullptr, nullptr}};
+
+}  // namespace
+
+int init_netconn_types(PyObject* m) {
+  struct {
+    PyObject** slot;
+    const char* text;
+  } strs[] = {{&s_add_reader, "add_reader"},   {&s_remove_reader, "remove_reader"}, {&s_add_writer, "add_writer"},
+              {&s_remove_writer, "remove_writer"}, {&s_call_soon, "call_soon"},   {&s_feed, "feed"},
+              {&s_start, "start"},             {&s_head, "head"},                 {&s_net_lost, "_net_lost"},
+              {&s_net_error, "_net_error"},    {&s_net_message, "_net_message"}};
+  for (auto& s : strs)
+    if (!(*s.slot = PyUnicode_InternFromString(s.text))) return -1;
+  NetConnType.tp_name = "beholder_amd.ops._native.NetConn";
+  NetConnType.tp_basicsize = sizeof(NetConnObject);
+  NetConnType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC;
+  NetConnType.tp_doc =
+      "NetConn(fd, loop, kind, owner, parser, stmts=None, pg_error=None, closed_exc=ConnectionError): plain-TCP "
+      "client socket on the "
+      "asyncio loop with native reply dispatch (kind 'h1' or 'pg')";
+  NetConnType.tp_new = nc_new;
+  NetConnType.tp_init = reinterpret_cast<initproc>(nc_init);
+  NetConnType.tp_dealloc = reinterpret_cast<destructor>(nc_dealloc);
+  NetConnType.tp_traverse = reinterpret_cast<traverseproc>(nc_traverse);
+  NetConnType.tp_clear = reinterpret_cast<inquiry>(nc_clear);
+  NetConnType.tp_methods = nc_methods;
+  NetConnType.tp_getset = nc_getset;
+  if (PyType_Ready(&NetConnType) < 0) return -1;
+  Py_INCREF(&NetConnType);
+  if (PyModule_AddObject(m, "NetConn", reinterpret_cast<PyObject*>(&NetConnType)) < 0) return -1;
+  return 0;
+}
+
+}  // namespace beholder

@@ -436,22 +436,20 @@ int put_param(std::string& o, PyObject* v) {
   return 0;
 }
 
-// pg_bind(statement: bytes, params: sequence) -> Bind + Describe(portal) + Execute + Sync
-PyObject* pg_bind_impl(PyObject*, PyObject* args) {
-  const char* name;
-  Py_ssize_t nlen;
-  PyObject* params;
-  if (!PyArg_ParseTuple(args, "y#O", &name, &nlen, &params)) return nullptr;
+}  // namespace
+
+// Appends Bind + Describe(portal) + Execute + Sync for statement `name` to `o`. -1 on error.
+int pg_bind_append(std::string& o, const char* name, size_t nlen, PyObject* params) {
   PyObject* seq = PySequence_Fast(params, "params must be a sequence");
-  if (!seq) return nullptr;
+  if (!seq) return -1;
   Py_ssize_t np = PySequence_Fast_GET_SIZE(seq);
   if (np > 65535) {
     Py_DECREF(seq);
     PyErr_SetString(PyExc_ValueError, "too many parameters");
-    return nullptr;
+    return -1;
   }
-  std::string o;
-  o.reserve(size_t(64 + nlen + np * 48));
+  size_t start = o.size();
+  o.reserve(start + size_t(64 + nlen + np * 48));
   o.push_back('B');
   put32(o, 0);  // length, patched below
   o.push_back('\0');  // unnamed portal
@@ -464,20 +462,34 @@ PyObject* pg_bind_impl(PyObject*, PyObject* args) {
   for (Py_ssize_t i = 0; i < np; ++i) {
     if (put_param(o, items[i]) < 0) {
       Py_DECREF(seq);
-      return nullptr;
+      o.resize(start);
+      return -1;
     }
   }
   Py_DECREF(seq);
   o.append("\0\0", 2);  // no result format codes: all text
-  uint32_t blen = uint32_t(o.size() - 1);
-  o[1] = char(blen >> 24);
-  o[2] = char(blen >> 16);
-  o[3] = char(blen >> 8);
-  o[4] = char(blen);
+  uint32_t blen = uint32_t(o.size() - start - 1);
+  o[start + 1] = char(blen >> 24);
+  o[start + 2] = char(blen >> 16);
+  o[start + 3] = char(blen >> 8);
+  o[start + 4] = char(blen);
   static const char tail[] = {'D', 0, 0, 0, 6, 'P', 0,           // Describe portal ""
                               'E', 0, 0, 0, 9, 0, 0, 0, 0, 0,    // Execute "", no row limit
                               'S', 0, 0, 0, 4};                   // Sync
   o.append(tail, sizeof(tail));
+  return 0;
+}
+
+namespace {
+
+// pg_bind(statement: bytes, params: sequence) -> Bind + Describe(portal) + Execute + Sync
+PyObject* pg_bind_impl(PyObject*, PyObject* args) {
+  const char* name;
+  Py_ssize_t nlen;
+  PyObject* params;
+  if (!PyArg_ParseTuple(args, "y#O", &name, &nlen, &params)) return nullptr;
+  std::string o;
+  if (pg_bind_append(o, name, size_t(nlen), params) < 0) return nullptr;
   return PyBytes_FromStringAndSize(o.data(), Py_ssize_t(o.size()));
 }
 

@@ -38,6 +38,7 @@ from urllib.parse import quote, unquote, urljoin
 from ..ops import H1Parser
 from ..ops import IOFuture as _IOFuture
 from ..ops import encode_query as _encode_query
+from ..utils import netconn
 from .http import HttpClient, HttpError, HttpResponse, encode_query, redact, with_query
 
 _IDEMPOTENT = frozenset(("GET", "HEAD", "PUT", "DELETE", "OPTIONS"))
@@ -61,12 +62,18 @@ class _Reset(Exception):
 
 
 class _Conn(asyncio.Protocol):
-    __slots__ = ("origin", "parser", "transport", "waiter", "closed", "last_used", "uses", "deadline", "what")
+    """One keep-alive connection. A plain-TCP connection is handed to a native ``NetConn``
+    (``net``) once connected (utils/netconn.py): replies are then parsed and delivered in C and
+    the methods below only see its rare paths (``_net_lost``, ``_net_error``)."""
+
+    __slots__ = ("origin", "parser", "transport", "waiter", "closed", "last_used", "uses", "deadline", "what",
+                 "net")
 
     def __init__(self, origin: "_Origin"):
         self.origin = origin
         self.parser = H1Parser()
         self.transport = None
+        self.net = None
         self.waiter: Optional[asyncio.Future] = None
         self.closed = False
         self.last_used = 0.0
@@ -97,9 +104,24 @@ class _Conn(asyncio.Protocol):
         return False  # let the transport close; connection_lost completes the response
 
     def connection_lost(self, exc):
+        if self.net is not None:
+            return  # the transport was aborted when the socket was handed to the NetConn
         self.closed = True
         w = self.waiter
         self.waiter = None
+        self._complete_at_eof(w, exc)
+
+    # -- NetConn callbacks (rare paths) ----------------------------------------
+    def _net_lost(self, exc):
+        self.closed = True
+        self._complete_at_eof(self.net.take_waiter(), exc)
+
+    def _net_error(self, exc):
+        if exc is not None:
+            self._fail(HttpError(f"HPE_INVALID_RESPONSE: {exc}"))
+        self.abort()  # malformed or unsolicited response
+
+    def _complete_at_eof(self, w, exc) -> None:
         if w is None or w.done():
             return
         try:
@@ -114,15 +136,29 @@ class _Conn(asyncio.Protocol):
 
     # -- client side ---------------------------------------------------------
     def _fail(self, exc: BaseException) -> None:
-        w = self.waiter
-        self.waiter = None
+        if self.net is not None:
+            w = self.net.take_waiter()
+        else:
+            w = self.waiter
+            self.waiter = None
         if w is not None and not w.done():
             w.set_exception(exc)
 
     def abort(self) -> None:
         self.closed = True
-        if self.transport is not None:
+        if self.net is not None:
+            self.net.abort()
+        elif self.transport is not None:
             self.transport.abort()
+
+    def adopt(self, loop) -> bool:
+        """Hand a plain-TCP connection to a native NetConn (utils/netconn.py)."""
+        fd = netconn.adopt(self.transport)
+        if fd is None:
+            return False
+        self.net = netconn.NetConn(fd, loop, "h1", self, self.parser)
+        self.transport = None
+        return True
 
     def timed_out(self) -> None:
         m, url = self.what
@@ -236,6 +272,8 @@ class H1Client(HttpClient):
                 raise asyncio.TimeoutError
             kw = {"ssl": self._ssl_context(), "server_hostname": o.host} if o.tls else {}
             await asyncio.wait_for(loop.create_connection(lambda: conn, o.host, o.port, **kw), remaining)
+            if not o.tls:
+                conn.adopt(loop)
         except BaseException:
             o.open -= 1
             self._wake(o)
@@ -392,11 +430,15 @@ class H1Client(HttpClient):
             reused = c.uses > 0
             c.uses += 1
             w = _IOFuture(loop)
-            c.waiter = w
             c.deadline = deadline
             c.what = (m, cur)
-            c.parser.start(head=m == "HEAD")
-            c.transport.write(req)
+            net = c.net
+            if net is not None:
+                net.request(req, w, m == "HEAD")  # parser started, reply future set, request sent
+            else:
+                c.waiter = w
+                c.parser.start(head=m == "HEAD")
+                c.transport.write(req)
             busy = self._busy
             busy.add(c)
             if self._sweeper is None:

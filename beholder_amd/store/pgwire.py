@@ -31,12 +31,14 @@ import hashlib
 import hmac
 import os
 import struct
+import time
 from typing import Any, Deque, Dict, List, Optional, Sequence, Tuple
 from urllib.parse import parse_qs, unquote, urlsplit
 
 from ..ops import IOFuture as _IOFuture
 from ..ops import PgReader
 from ..ops import native as _native
+from ..utils import netconn
 
 PROTOCOL_V3 = 196608
 
@@ -182,6 +184,9 @@ class PgConnection(asyncio.Protocol):
         self._n_stmts = 0
         self._ssl_answer: Optional[asyncio.Future] = None
         self.tls = False
+        # plain TCP after startup: the socket belongs to a native NetConn (utils/netconn.py),
+        # which takes over execute() and the reply matching
+        self._net = None
 
     # -- protocol callbacks --------------------------------------------------
     def connection_made(self, transport):
@@ -230,6 +235,8 @@ class PgConnection(asyncio.Protocol):
         # b"A" NotificationResponse (LISTEN is never used here): ignored
 
     def connection_lost(self, exc):
+        if self._net is not None:
+            return  # the transport was aborted when the socket was handed to the NetConn
         self.closed = True
         if self._flush_handle is not None:
             self._flush_handle.cancel()
@@ -261,6 +268,10 @@ class PgConnection(asyncio.Protocol):
     async def connect(self) -> "PgConnection":
         p = self.params
         loop = asyncio.get_running_loop()
+        if self._net is not None:  # reconnecting this object: back to the asyncio path first
+            self._net.abort()
+            self._net = None
+            self.__dict__.pop("execute", None)
         self._reader = PgReader()
         self._startup = asyncio.Queue()
         self._stmts.clear()
@@ -284,7 +295,36 @@ class PgConnection(asyncio.Protocol):
         self._startup = None
         self._reader.query_mode = True
         self.closed = False
+        if not self.tls:
+            fd = netconn.adopt(self._transport)
+            if fd is not None:
+                self._net = netconn.NetConn(fd, loop, "pg", self, self._reader, self._stmts, PgError,
+                                            PgProtocolError)
+                self._transport = None
+                self.execute = self._net.execute  # native: Parse/Bind/Execute/Sync + IOFuture
         return self
+
+    def abort(self) -> None:
+        """Drop the connection now; outstanding queries fail with PgProtocolError."""
+        if self._net is not None:
+            self._net.abort()
+            self._net_lost(None)
+        elif self._transport is not None:
+            self._transport.abort()
+
+    # -- NetConn callbacks (rare paths) ----------------------------------------
+    def _net_lost(self, exc) -> None:
+        self.closed = True
+        self._net.fail_all(PgProtocolError(f"connection lost: {exc}" if exc else "connection lost"))
+
+    def _net_error(self, exc) -> None:
+        self.closed = True
+        self._net.abort()
+        self._net.fail_all(PgProtocolError(f"protocol error: {exc}" if exc is not None
+                                           else "unexpected ReadyForQuery"))
+
+    def _net_message(self, typ: bytes, body: bytes) -> None:
+        self._message(typ, body)
 
     async def _negotiate_tls(self, mode: str, p: Dict[str, Any]) -> None:
         """SSLRequest; on 'S' upgrade the transport in place (``loop.start_tls``)."""
@@ -355,7 +395,8 @@ class PgConnection(asyncio.Protocol):
     @property
     def pending(self) -> int:
         """Queries sent (or buffered) and not yet answered."""
-        return len(self._pending)
+        net = self._net
+        return net.pending if net is not None else len(self._pending)
 
     def execute(self, sql: str, params: Sequence[Any] = ()) -> "asyncio.Future[Tuple[List[Tuple], str]]":
         """Queue one statement with ``$n`` parameters; the returned future resolves to
@@ -390,6 +431,19 @@ class PgConnection(asyncio.Protocol):
             self._transport.write(data)
 
     async def close(self) -> None:
+        net = self._net
+        if net is not None:
+            if not self.closed:
+                deadline = time.monotonic() + self.connect_timeout
+                while net.pending and not net.closed and time.monotonic() < deadline:
+                    await asyncio.sleep(0.001)  # in-flight queries finish; a dead server cannot hang shutdown
+                if not net.closed:
+                    net.flush()
+                    net.write(b"X" + _PACK_LEN(4))  # Terminate
+                    net.close()
+                net.fail_all(PgProtocolError("connection closed"))
+            self.closed = True
+            return
         if self._transport is None or self.closed:
             self.closed = True
             return
@@ -447,7 +501,7 @@ class Pool:
         bp = 0
         for c in self._conns:
             if not c.closed:
-                n = len(c._pending)
+                n = c.pending
                 if best is None or n < bp:
                     best, bp = c, n
         if best is not None and (bp < self.spread_at or len(self._conns) >= self.size):
@@ -458,14 +512,14 @@ class Pool:
         async with self._lock:
             self._conns = [c for c in self._conns if not c.closed]
             live = self._conns
-            if len(live) < self.size and (not live or min(len(c._pending) for c in live) >= self.spread_at):
+            if len(live) < self.size and (not live or min(c.pending for c in live) >= self.spread_at):
                 try:
                     c = await PgConnection(self.dsn).connect()
                     live.append(c)
                 except (OSError, asyncio.TimeoutError, PgError, PgProtocolError):
                     if not live:
                         raise
-            c = min(live, key=lambda c: len(c._pending))
+            c = min(live, key=lambda c: c.pending)
         return await c.execute(sql, params)
 
     @property

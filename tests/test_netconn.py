@@ -1,0 +1,181 @@
+"""Native plain-TCP connections (ops/csrc/py_netconn.cpp, utils/netconn.py).
+
+The H1 sink client and the Postgres client hand their plain-TCP sockets to a NetConn once
+connected; tests/test_h1.py and tests/test_stores.py therefore exercise the native path. This
+file adds what only the native path has (multi-recv replies, send backpressure, fd ownership),
+and re-runs the network tests of both clients with BEHOLDER_NATIVE_NET=0, so the asyncio
+transport path (TLS connections always take it) stays covered too.
+"""
+import asyncio
+import inspect
+import os
+import socket
+
+import pytest
+
+import test_h1
+import test_stores
+from beholder_amd.ops import H1Parser, IOFuture
+from beholder_amd.sinks import H1Client
+from beholder_amd.store.pgwire import PgConnection
+from beholder_amd.utils import netconn
+
+from pg_fake import FakePg
+
+
+def run(coro):
+    return asyncio.run(asyncio.wait_for(coro, 30))
+
+
+def _no_arg_tests(mod, prefix):
+    return [f for n, f in sorted(vars(mod).items())
+            if n.startswith(prefix) and callable(f) and not inspect.signature(f).parameters]
+
+
+ASYNCIO_PATH = ([f for f in _no_arg_tests(test_h1, "test_")
+                 if "H1Client" in inspect.getsource(f) or "Scripted" in inspect.getsource(f)]
+                + [f for f in _no_arg_tests(test_stores, "test_")
+                   if any(k in inspect.getsource(f) for k in ("PgConnection", "PostgresStore", "Pool"))])
+
+
+@pytest.mark.parametrize("fn", ASYNCIO_PATH, ids=[f"{f.__module__}.{f.__name__}" for f in ASYNCIO_PATH])
+def test_asyncio_transport_path(fn, monkeypatch):
+    monkeypatch.setenv("BEHOLDER_NATIVE_NET", "0")
+    fn()
+
+
+def test_both_clients_adopt_plain_tcp_connections():
+    async def go():
+        s = await test_h1.Scripted(lambda n, m, t, h: test_h1.OK).start()
+        pg = await FakePg(auth="md5").start()
+        try:
+            c = H1Client(timeout_s=5)
+            await c.request("GET", f"http://127.0.0.1:{s.port}/x")
+            conn = next(iter(c._origins.values())).idle[0]
+            p = await PgConnection(pg.dsn).connect()
+            rows, tag = await p.execute("SELECT $1 + 1", (1,))
+            out = (type(conn.net).__name__, conn.transport, type(p._net).__name__, p._transport, rows, tag)
+            await c.close()
+            await p.close()
+            assert p.closed and conn.net.closed
+            return out
+        finally:
+            await s.stop()
+            await pg.stop()
+    assert run(go()) == ("NetConn", None, "NetConn", None, [(2,)], "SELECT 1")
+
+
+def test_large_response_spans_many_recvs():
+    body = os.urandom(3 << 20).hex().encode()  # 6 MiB: 24+ reads of 256 KiB
+
+    def respond(n, m, t, h):
+        return b"HTTP/1.1 200 OK\r\nContent-Length: %d\r\n\r\n" % len(body) + body
+
+    async def go():
+        s = await test_h1.Scripted(respond).start()
+        c = H1Client(timeout_s=10)
+        try:
+            r1 = await c.request("GET", f"http://127.0.0.1:{s.port}/a")
+            r2 = await c.request("GET", f"http://127.0.0.1:{s.port}/b")  # same connection, reused
+            conn = next(iter(c._origins.values())).idle[0]
+            return r1.body == body and r2.body == body, conn.net.stats, s.connections
+        finally:
+            await c.close()
+            await s.stop()
+    ok, stats, conns = run(go())
+    assert ok and conns == 1 and stats["recvs"] > 24 and stats["bytes_in"] > 2 * len(body)
+
+
+def test_write_backpressure_keeps_order():
+    """A peer that reads slowly: what the kernel refuses is queued and sent from the writer
+    callback, in order, and the fd is unregistered at close."""
+    payload = bytes(range(256)) * (64 << 10)  # 16 MiB
+
+    async def go():
+        loop = asyncio.get_running_loop()
+        a, b = socket.socketpair()
+        a.setblocking(False)
+        b.setblocking(False)
+        fd = os.dup(a.fileno())
+        a.close()
+        lost = []
+
+        class Owner:
+            def _net_lost(self, exc):
+                lost.append(exc)
+
+        nc = netconn.NetConn(fd, loop, "h1", Owner(), H1Parser())
+        nc.write(payload[: len(payload) // 2])
+        nc.write(payload[len(payload) // 2:])
+        assert nc.buffered > 0  # the socket buffer cannot hold 16 MiB
+        got = bytearray()
+        while len(got) < len(payload):
+            await asyncio.sleep(0.001)
+            try:
+                got += b.recv(1 << 20)
+            except BlockingIOError:
+                pass
+        assert nc.buffered == 0
+        nc.close()
+        b.close()
+        return bytes(got) == payload, nc.fd, nc.closed, lost
+    ok, fd, closed, lost = run(go())
+    assert ok and fd == -1 and closed and lost == []
+
+
+def test_peer_close_reports_loss_and_fails_the_waiter():
+    async def go():
+        loop = asyncio.get_running_loop()
+        a, b = socket.socketpair()
+        lost = []
+
+        class Owner:
+            def _net_lost(self, exc):
+                lost.append(exc)
+                w = nc.take_waiter()
+                if w is not None:
+                    w.set_exception(ConnectionResetError("peer closed"))
+
+        fd = os.dup(a.fileno())
+        a.close()
+        os.set_blocking(fd, False)
+        nc = netconn.NetConn(fd, loop, "h1", Owner(), H1Parser())
+        w = IOFuture(loop)
+        nc.request(b"GET / HTTP/1.1\r\n\r\n", w, False)
+        assert b.recv(100).startswith(b"GET /")
+        b.close()
+        with pytest.raises(ConnectionResetError):
+            await w
+        with pytest.raises(ConnectionError):
+            nc.write(b"x")
+        return lost, nc.closed
+    lost, closed = run(go())
+    assert lost == [None] and closed
+
+
+def test_bad_arguments():
+    async def go():
+        loop = asyncio.get_running_loop()
+        with pytest.raises(ValueError):
+            netconn.NetConn(0, loop, "smtp", object(), H1Parser())
+        with pytest.raises(TypeError):
+            netconn.NetConn(0, loop, "pg", object(), H1Parser())  # no stmts / pg_error
+        with pytest.raises(ValueError):
+            netconn.NetConn(-1, loop, "h1", object(), H1Parser())
+    run(go())
+
+
+def test_disabled_by_env(monkeypatch):
+    monkeypatch.setenv("BEHOLDER_NATIVE_NET", "0")
+
+    async def go():
+        pg = await FakePg(auth="trust").start()
+        try:
+            p = await PgConnection(pg.dsn).connect()
+            r = await p.execute("SELECT 1")
+            kind = p._net
+            await p.close()
+            return kind, r
+        finally:
+            await pg.stop()
+    assert run(go()) == (None, ([(1,)], "SELECT 1"))

@@ -205,7 +205,7 @@ def test_pool_spreads_load_and_replaces_broken_connections():
             res = await asyncio.gather(*[pool.execute("SELECT $1 + 0", (i,)) for i in range(30)])
             assert [r[0][0][0] for r in res] == list(range(30))
             spread = pool.connections
-            pool._conns[0]._transport.abort()  # a broken connection is dropped and replaced
+            pool._conns[0].abort()  # a broken connection is dropped and replaced
             await asyncio.sleep(0.01)
             res = await asyncio.gather(*[pool.execute("SELECT $1 + 0", (i,)) for i in range(10)])
             assert [r[0][0][0] for r in res] == list(range(10))
