@@ -1002,6 +1002,22 @@ PyObject* iofuture_new(PyObject* loop) {
 
 bool iofuture_done(PyObject* f) { return reinterpret_cast<IOFutureObject*>(f)->state != 0; }
 
+// 0 pending; 1 finished with a result (*result borrowed); 2 finished with an exception or cancelled
+int iofuture_peek(PyObject* f, PyObject** result) {
+  IOFutureObject* x = reinterpret_cast<IOFutureObject*>(f);
+  if (!x->state) return 0;
+  if (x->state == 2 || x->exc) return 2;
+  *result = x->result;
+  return 1;
+}
+
+// What an awaiter yields for a pending future: the future, with the asyncio blocking handshake set
+PyObject* iofuture_yield(PyObject* f) {
+  reinterpret_cast<IOFutureObject*>(f)->blocking = 1;
+  Py_INCREF(f);
+  return f;
+}
+
 // resolve / reject unless already finished: 0 ok (or already done), -1 error
 int iofuture_resolve(PyObject* f, PyObject* v) {
   if (iofuture_done(f)) return 0;

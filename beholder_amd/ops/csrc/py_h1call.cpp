@@ -1,0 +1,767 @@
+// H1 fast path: the common case of sinks/h1.py `H1Client.request` done in C.
+//
+// The production path issues one sink request per Trello-created progress event and up to
+// three per status event (index.js:53,83,99,112). In Python each costs a coroutine, the URL
+// split / route lookup, the request text, the idle-connection pop, the reply future, the
+// busy-set bookkeeping, the release to the pool and the HttpResponse: about 4 us of CPU on
+// the box, the largest Python cost left in `tcp_e2e` after the native NetConn.
+//
+//   call = h1_fast(client, method, url, params, timeout)   # None: take the Python path
+//   resp = await call
+//
+// h1_fast handles exactly the shape the sinks produce on a warm pool: a stock H1Client, an
+// ASCII URL whose origin is already known, a printable path (no fragment), params None or a
+// dict (encodeURIComponent query, the `request` library's qs.stringify), and a live idle
+// keep-alive connection on a native NetConn (utils/netconn.py). Anything else returns None
+// before any state is touched, and H1Client._request does the work as before.
+//
+// The returned H1Call is an awaitable iterator (send/throw/close). It yields the reply
+// IOFuture; a handler driven by the native Driver is resumed by the NetConn's reply callback.
+// A plain reply (not a redirect of a GET/HEAD) completes in C: the connection goes back to
+// the idle pool (or is dropped through H1Client._release), an HttpResponse is built. A failed
+// reply (reset, timeout, malformed) or a redirect is handed to H1Client._resume(m, full,
+// deadline, conn, fut, reused), which runs the Python request loop from that await on
+// (transparent retry on a fresh connection, redirects, error mapping), and the H1Call
+// delegates to it (yield from). The pool invariants of sinks/h1.py hold on every path:
+// counts, `uses`, `deadline`, `what`, the busy set and the deadline sweeper are updated as
+// the Python fast path does.
+#include <time.h>
+
+#include <string>
+
+#include "py_common.hpp"
+
+#include <structmember.h>
+
+namespace beholder {
+
+PyObject* iofuture_new(PyObject* loop);
+bool is_iofuture(PyObject* o);
+int iofuture_peek(PyObject* f, PyObject** result);
+PyObject* iofuture_yield(PyObject* f);
+bool is_netconn(PyObject* o);
+bool netconn_open(PyObject* o);
+int netconn_h1_request(PyObject* o, const std::string& data, PyObject* waiter, bool head);
+bool text_query_pair_append(std::string& out, PyObject* k, PyObject* v, bool* first, bool rfc3986);
+
+namespace {
+
+// Slot offsets of a __slots__ class, from its member descriptors (exact type only).
+struct Slots {
+  PyTypeObject* type = nullptr;
+  Py_ssize_t off[8] = {0};
+
+  bool resolve(PyObject* cls, const char* const* names, int n) {
+    if (!PyType_Check(cls)) {
+      PyErr_SetString(PyExc_TypeError, "h1_setup: expected a class");
+      return false;
+    }
+    for (int i = 0; i < n; ++i) {
+      PyObject* d = PyObject_GetAttrString(cls, names[i]);
+      if (!d) return false;
+      bool ok = Py_TYPE(d) == &PyMemberDescr_Type &&
+                reinterpret_cast<PyMemberDescrObject*>(d)->d_member->type == T_OBJECT_EX;
+      if (ok) off[i] = reinterpret_cast<PyMemberDescrObject*>(d)->d_member->offset;
+      Py_DECREF(d);
+      if (!ok) {
+        PyErr_Format(PyExc_TypeError, "h1_setup: %s.%s is not a __slots__ member",
+                     reinterpret_cast<PyTypeObject*>(cls)->tp_name, names[i]);
+        return false;
+      }
+    }
+    Py_INCREF(cls);
+    Py_XSETREF(type, reinterpret_cast<PyTypeObject*>(cls));
+    return true;
+  }
+  // borrowed; NULL when the slot is unset
+  PyObject* get(PyObject* o, int i) const { return *reinterpret_cast<PyObject**>(reinterpret_cast<char*>(o) + off[i]); }
+  // steals v
+  void set(PyObject* o, int i, PyObject* v) const {
+    PyObject** p = reinterpret_cast<PyObject**>(reinterpret_cast<char*>(o) + off[i]);
+    PyObject* old = *p;
+    *p = v;
+    Py_XDECREF(old);
+  }
+};
+
+// sinks/h1.py _Conn / _Origin and sinks/http.py HttpResponse slot indices
+enum { C_ORIGIN, C_PARSER, C_CLOSED, C_LAST_USED, C_USES, C_DEADLINE, C_WHAT, C_NET, C_N };
+const char* const kConnSlots[C_N] = {"origin", "parser", "closed", "last_used", "uses", "deadline", "what", "net"};
+enum { O_HOST_HEADER, O_AUTH, O_IDLE, O_WAITERS, O_N };
+const char* const kOriginSlots[O_N] = {"host_header", "auth", "idle", "waiters"};
+enum { R_STATUS, R_BODY, R_HEADERS, R_RAW, R_URL, R_N };
+const char* const kRespSlots[R_N] = {"status", "body", "_headers", "_raw", "url"};
+
+struct State {
+  Slots conn, origin, resp;
+  PyTypeObject* client_type = nullptr;
+  PyObject* get_running_loop = nullptr;
+  bool ready = false;
+} g;
+
+PyObject *s_closed_attr, *s_origins, *s_counts, *s_keepalive_s, *s_timeout_s, *s_busy, *s_sweeper, *s_tail,
+    *s_tail_cl0, *s_requests, *s_reused, *s_drop, *s_release, *s_arm, *s_resume, *s_time, *s_pop, *s_append,
+    *s_buffered, *s_throw, *s_close;
+
+double mono_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);  // time.monotonic()'s clock
+  return double(ts.tv_sec) + double(ts.tv_nsec) * 1e-9;
+}
+
+bool is_body_method(const char* m, Py_ssize_t n) {
+  auto eq = [&](const char* s) { return Py_ssize_t(strlen(s)) == n && memcmp(m, s, size_t(n)) == 0; };
+  return eq("POST") || eq("PUT") || eq("PATCH") || eq("DELETE");
+}
+
+bool is_get_or_head(const char* m, Py_ssize_t n) {
+  return (n == 3 && memcmp(m, "GET", 3) == 0) || (n == 4 && memcmp(m, "HEAD", 4) == 0);
+}
+
+// dict[key] += 1 (int counters of H1Client.counts)
+int bump(PyObject* d, PyObject* key) {
+  PyObject* v = PyDict_GetItemWithError(d, key);
+  if (!v) {
+    if (!PyErr_Occurred()) PyErr_SetObject(PyExc_KeyError, key);
+    return -1;
+  }
+  PyObject* one = PyLong_FromLong(1);
+  PyObject* n = one ? PyNumber_Add(v, one) : nullptr;
+  Py_XDECREF(one);
+  if (!n) return -1;
+  int rc = PyDict_SetItem(d, key, n);
+  Py_DECREF(n);
+  return rc;
+}
+
+// ---- H1Call ---------------------------------------------------------------------------------
+enum : uint8_t { ST_WAIT = 0, ST_DELEGATE = 1, ST_DONE = 2 };
+
+struct H1CallObject {
+  PyObject_HEAD PyObject* client;
+  PyObject* conn;
+  PyObject* fut;
+  PyObject* method;  // str, upper case
+  PyObject* full;    // str: the URL with its query (HttpResponse.url, error text)
+  PyObject* deadline;
+  PyObject* sub;  // the Python continuation (H1Client._resume) once delegated
+  uint8_t state;
+  uint8_t reused;  // the connection had served a request before (h1.py `reused`)
+};
+
+PyTypeObject H1CallType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+int call_traverse(H1CallObject* s, visitproc visit, void* arg) {
+  Py_VISIT(s->client);
+  Py_VISIT(s->conn);
+  Py_VISIT(s->fut);
+  Py_VISIT(s->method);
+  Py_VISIT(s->full);
+  Py_VISIT(s->deadline);
+  Py_VISIT(s->sub);
+  return 0;
+}
+
+int call_clear(H1CallObject* s) {
+  Py_CLEAR(s->client);
+  Py_CLEAR(s->conn);
+  Py_CLEAR(s->fut);
+  Py_CLEAR(s->method);
+  Py_CLEAR(s->full);
+  Py_CLEAR(s->deadline);
+  Py_CLEAR(s->sub);
+  return 0;
+}
+
+PyObject* client_attr(PyObject* client, PyObject* name) {  // borrowed, from the instance dict
+  PyObject** dp = _PyObject_GetDictPtr(client);
+  PyObject* v = dp && *dp ? PyDict_GetItemWithError(*dp, name) : nullptr;
+  if (!v && !PyErr_Occurred()) PyErr_SetObject(PyExc_AttributeError, name);
+  return v;
+}
+
+// `busy.discard(c); self._release(c, False)`: the request ended without a usable reply
+// (cancelled, closed, abandoned). Errors are reported, not raised (cleanup path).
+void abandon(H1CallObject* s) {
+  PyObject *et, *ev, *tb;
+  PyErr_Fetch(&et, &ev, &tb);
+  if (s->client && s->conn) {
+    PyObject* busy = client_attr(s->client, s_busy);
+    if (!busy || PySet_Discard(busy, s->conn) < 0) PyErr_WriteUnraisable(s->client);
+    PyObject* r = PyObject_CallMethodObjArgs(s->client, s_release, s->conn, Py_False, nullptr);
+    if (!r)
+      PyErr_WriteUnraisable(s->client);
+    else
+      Py_DECREF(r);
+  }
+  PyErr_Restore(et, ev, tb);
+}
+
+void call_finalize(H1CallObject* s) {
+  if (s->state == ST_WAIT) {  // never awaited to the end: like a closed coroutine
+    s->state = ST_DONE;
+    abandon(s);
+  } else if (s->state == ST_DELEGATE && s->sub) {
+    s->state = ST_DONE;
+    PyObject *et, *ev, *tb;
+    PyErr_Fetch(&et, &ev, &tb);
+    PyObject* r = PyObject_CallMethodNoArgs(s->sub, s_close);
+    if (!r)
+      PyErr_WriteUnraisable(s->sub);
+    else
+      Py_DECREF(r);
+    PyErr_Restore(et, ev, tb);
+  }
+}
+
+void call_dealloc(H1CallObject* s) {
+  if (PyObject_CallFinalizerFromDealloc(reinterpret_cast<PyObject*>(s)) < 0) return;  // resurrected
+  PyObject_GC_UnTrack(s);
+  call_clear(s);
+  Py_TYPE(s)->tp_free(reinterpret_cast<PyObject*>(s));
+}
+
+// The reply `res` arrived. 1 = finished here (*out = HttpResponse), 0 = the Python loop must
+// continue (a redirect to follow), -1 = error.
+int finish_fast(H1CallObject* s, PyObject* res, PyObject** out) {
+  if (!PyTuple_CheckExact(res) || PyTuple_GET_SIZE(res) != 5) return 0;
+  PyObject* status = PyTuple_GET_ITEM(res, 0);
+  if (!PyLong_CheckExact(status)) return 0;
+  long st = PyLong_AsLong(status);
+  if (st == -1 && PyErr_Occurred()) return -1;
+  if (st == 301 || st == 302 || st == 303 || st == 307 || st == 308) {
+    Py_ssize_t mn;
+    const char* m = PyUnicode_AsUTF8AndSize(s->method, &mn);
+    if (!m) return -1;
+    if (is_get_or_head(m, mn)) return 0;
+  }
+  PyObject* client = s->client;
+  PyObject* conn = s->conn;
+  PyObject* busy = client_attr(client, s_busy);
+  if (!busy || PySet_Discard(busy, conn) < 0) return -1;
+  // keep = keep-alive and c.parser.buffered == 0
+  int keep = PyObject_IsTrue(PyTuple_GET_ITEM(res, 4));
+  if (keep < 0) return -1;
+  if (keep) {
+    PyObject* parser = g.conn.get(conn, C_PARSER);
+    PyObject* b = parser ? PyObject_GetAttr(parser, s_buffered) : nullptr;
+    if (!b) return -1;
+    int zero = PyLong_Check(b) && PyLong_AsSsize_t(b) == 0;
+    Py_DECREF(b);
+    keep = zero;
+  }
+  PyObject* cclosed = client_attr(client, s_closed_attr);
+  if (!cclosed) return -1;
+  PyObject* o = g.conn.get(conn, C_ORIGIN);
+  PyObject* waiters = o && Py_TYPE(o) == g.origin.type ? g.origin.get(o, O_WAITERS) : nullptr;
+  PyObject* idle = waiters ? g.origin.get(o, O_IDLE) : nullptr;
+  Py_ssize_t nw = waiters ? PyObject_Size(waiters) : -1;
+  if (nw < 0 && PyErr_Occurred()) return -1;
+  if (keep && idle && nw == 0 && g.conn.get(conn, C_CLOSED) == Py_False && cclosed == Py_False) {
+    // H1Client._release(c, True) with no waiter: back to the idle pool
+    PyObject* t = PyFloat_FromDouble(mono_s());
+    if (!t) return -1;
+    g.conn.set(conn, C_LAST_USED, t);
+    PyObject* r = PyObject_CallMethodOneArg(idle, s_append, conn);
+    if (!r) return -1;
+    Py_DECREF(r);
+  } else {
+    PyObject* r = PyObject_CallMethodObjArgs(client, s_release, conn, keep ? Py_True : Py_False, nullptr);
+    if (!r) return -1;
+    Py_DECREF(r);
+  }
+  // HttpResponse(status, body, None, full, raw)
+  PyTypeObject* rt = g.resp.type;
+  PyObject* resp = rt->tp_alloc(rt, 0);
+  if (!resp) return -1;
+  PyObject* vals[R_N] = {status, PyTuple_GET_ITEM(res, 3), Py_None, PyTuple_GET_ITEM(res, 2), s->full};
+  for (int i = 0; i < R_N; ++i) {
+    Py_INCREF(vals[i]);
+    g.resp.set(resp, i, vals[i]);
+  }
+  *out = resp;
+  return 1;
+}
+
+PySendResult delegate_send(H1CallObject* s, PyObject* arg, PyObject** out) {
+  PySendResult r = PyIter_Send(s->sub, arg, out);
+  if (r != PYGEN_NEXT) {
+    s->state = ST_DONE;
+    Py_CLEAR(s->sub);
+  }
+  return r;
+}
+
+// The Python request loop takes over at the await: s->sub = client._resume(m, full, deadline,
+// conn, fut, reused, thrown), where `thrown` (or None) is an exception thrown in at the await.
+int start_delegate(H1CallObject* s, PyObject* thrown) {
+  PyObject* args[8] = {s->client,  s->method, s->full, s->deadline, s->conn, s->fut, s->reused ? Py_True : Py_False,
+                       thrown ? thrown : Py_None};
+  PyObject* sub = PyObject_VectorcallMethod(s_resume, args, 8, nullptr);
+  if (!sub) {
+    s->state = ST_DONE;
+    return -1;
+  }
+  PyObject* it = sub;
+  if (!PyCoro_CheckExact(sub)) {
+    unaryfunc getter = Py_TYPE(sub)->tp_as_async ? Py_TYPE(sub)->tp_as_async->am_await : nullptr;
+    it = getter ? getter(sub) : nullptr;
+    Py_DECREF(sub);
+    if (!it) {
+      if (!PyErr_Occurred()) PyErr_SetString(PyExc_TypeError, "H1Client._resume must return an awaitable");
+      s->state = ST_DONE;
+      return -1;
+    }
+  }
+  s->sub = it;
+  s->state = ST_DELEGATE;
+  return 0;
+}
+
+PySendResult call_am_send(H1CallObject* s, PyObject* arg, PyObject** out) {
+  if (s->state == ST_DELEGATE) return delegate_send(s, arg, out);
+  if (s->state == ST_DONE) {
+    PyErr_SetString(PyExc_RuntimeError, "cannot reuse already awaited H1 request");
+    *out = nullptr;
+    return PYGEN_ERROR;
+  }
+  PyObject* res = nullptr;
+  int st = iofuture_peek(s->fut, &res);
+  if (st == 0) {
+    *out = iofuture_yield(s->fut);
+    return PYGEN_NEXT;
+  }
+  if (st == 1) {
+    Py_INCREF(res);
+    int k = finish_fast(s, res, out);
+    Py_DECREF(res);
+    if (k != 0) {
+      s->state = ST_DONE;
+      if (k < 0) {
+        *out = nullptr;
+        return PYGEN_ERROR;
+      }
+      return PYGEN_RETURN;
+    }
+  }
+  // an error, a cancelled future or a redirect: the Python request loop takes over at the await
+  if (start_delegate(s, nullptr) < 0) {
+    *out = nullptr;
+    return PYGEN_ERROR;
+  }
+  return delegate_send(s, Py_None, out);
+}
+
+// iterator protocol on top of am_send: a return value becomes StopIteration(value)
+PyObject* call_result(PySendResult r, PyObject* out) {
+  if (r == PYGEN_NEXT) return out;
+  if (r == PYGEN_ERROR) return nullptr;
+  if (out == Py_None) {
+    Py_DECREF(out);
+    PyErr_SetNone(PyExc_StopIteration);
+    return nullptr;
+  }
+  PyObject* e = PyObject_CallOneArg(PyExc_StopIteration, out);
+  Py_DECREF(out);
+  if (!e) return nullptr;
+  PyErr_SetObject(PyExc_StopIteration, e);
+  Py_DECREF(e);
+  return nullptr;
+}
+
+PyObject* call_iternext(H1CallObject* s) {
+  PyObject* out = nullptr;
+  PySendResult r = call_am_send(s, Py_None, &out);
+  return call_result(r, out);
+}
+
+PyObject* call_send(H1CallObject* s, PyObject* v) {
+  PyObject* out = nullptr;
+  PySendResult r = call_am_send(s, v, &out);
+  return call_result(r, out);
+}
+
+PyObject* call_throw(H1CallObject* s, PyObject* args) {
+  PyObject *typ, *val = nullptr, *tb = nullptr;
+  if (!PyArg_UnpackTuple(args, "throw", 1, 3, &typ, &val, &tb)) return nullptr;
+  if (s->state == ST_DELEGATE) {
+    PyObject* r = PyObject_CallMethodObjArgs(s->sub, s_throw, typ, val, tb, nullptr);
+    if (!r) {  // finished (StopIteration) or raised
+      s->state = ST_DONE;
+      Py_CLEAR(s->sub);
+    }
+    return r;
+  }
+  PyObject* exc = nullptr;  // the thrown exception as an instance
+  if (PyExceptionInstance_Check(typ)) {
+    Py_INCREF(typ);
+    exc = typ;
+  } else if (PyExceptionClass_Check(typ)) {
+    exc = val && PyObject_TypeCheck(val, reinterpret_cast<PyTypeObject*>(typ)) ? (Py_INCREF(val), val)
+          : val && val != Py_None ? PyObject_CallOneArg(typ, val)
+                                  : PyObject_CallNoArgs(typ);
+    if (!exc) return nullptr;
+  } else {
+    PyErr_SetString(PyExc_TypeError, "exceptions must be classes or instances deriving from BaseException");
+    return nullptr;
+  }
+  if (s->state == ST_WAIT) {  // the request loop's except clauses see it at the await (h1.py _exchange)
+    int rc = start_delegate(s, exc);
+    Py_DECREF(exc);
+    if (rc < 0) return nullptr;
+    PyObject* out = nullptr;
+    PySendResult r = delegate_send(s, Py_None, &out);
+    return call_result(r, out);
+  }
+  PyErr_SetObject(reinterpret_cast<PyObject*>(Py_TYPE(exc)), exc);
+  Py_DECREF(exc);
+  return nullptr;
+}
+
+PyObject* call_close(H1CallObject* s, PyObject*) {
+  if (s->state == ST_DELEGATE) {
+    s->state = ST_DONE;
+    PyObject* sub = s->sub;
+    s->sub = nullptr;
+    PyObject* r = PyObject_CallMethodNoArgs(sub, s_close);
+    Py_DECREF(sub);
+    return r;
+  }
+  if (s->state == ST_WAIT) {
+    s->state = ST_DONE;
+    abandon(s);
+  }
+  Py_RETURN_NONE;
+}
+
+PyObject* call_await(H1CallObject* s) {
+  Py_INCREF(s);
+  return reinterpret_cast<PyObject*>(s);
+}
+
+PyAsyncMethods call_async = {reinterpret_cast<unaryfunc>(call_await), nullptr, nullptr,
+                             reinterpret_cast<sendfunc>(call_am_send)};
+
+PyMethodDef call_methods[] = {
+    {"send", reinterpret_cast<PyCFunction>(call_send), METH_O, nullptr},
+    {"throw", reinterpret_cast<PyCFunction>(call_throw), METH_VARARGS, nullptr},
+    {"close", reinterpret_cast<PyCFunction>(call_close), METH_NOARGS, nullptr},
+    {"__await__", reinterpret_cast<PyCFunction>(call_await), METH_NOARGS, nullptr},
+    {nullptr, nullptr, 0, nullptr}};
+
+// ---- h1_fast ----------------------------------------------------------------------------------
+// Everything that can decline does so before any pool state changes: the caller then runs the
+// Python path, which reproduces any error at its await.
+PyObject* h1_fast_impl(PyObject* client, PyObject* method, PyObject* url, PyObject* params, PyObject* timeout) {
+  if (!g.ready || Py_TYPE(client) != g.client_type) Py_RETURN_NONE;
+  if (!PyUnicode_CheckExact(method) || !PyUnicode_CheckExact(url) || !PyUnicode_IS_ASCII(method) ||
+      !PyUnicode_IS_ASCII(url))
+    Py_RETURN_NONE;
+  if (params == Py_None) params = nullptr;
+  if (params && !PyDict_CheckExact(params)) Py_RETURN_NONE;
+  if (timeout == Py_None) timeout = nullptr;
+  if (timeout && !PyFloat_CheckExact(timeout) && !PyLong_CheckExact(timeout)) Py_RETURN_NONE;
+  PyObject** dp = _PyObject_GetDictPtr(client);
+  PyObject* d = dp ? *dp : nullptr;
+  if (!d) Py_RETURN_NONE;
+  PyObject* cclosed = PyDict_GetItemWithError(d, s_closed_attr);
+  PyObject* origins = cclosed ? PyDict_GetItemWithError(d, s_origins) : nullptr;
+  PyObject* counts = origins ? PyDict_GetItemWithError(d, s_counts) : nullptr;
+  PyObject* keepalive = counts ? PyDict_GetItemWithError(d, s_keepalive_s) : nullptr;
+  PyObject* timeout_s = keepalive ? PyDict_GetItemWithError(d, s_timeout_s) : nullptr;
+  PyObject* busy = timeout_s ? PyDict_GetItemWithError(d, s_busy) : nullptr;
+  PyObject* tail = busy ? PyDict_GetItemWithError(d, s_tail) : nullptr;
+  PyObject* tail_cl0 = tail ? PyDict_GetItemWithError(d, s_tail_cl0) : nullptr;
+  if (!tail_cl0) {
+    if (PyErr_Occurred()) return nullptr;
+    Py_RETURN_NONE;
+  }
+  if (cclosed != Py_False || !PyDict_CheckExact(origins) || !PyDict_CheckExact(counts) || !PySet_CheckExact(busy) ||
+      !PyBytes_CheckExact(tail) || !PyBytes_CheckExact(tail_cl0) || !PyFloat_CheckExact(keepalive))
+    Py_RETURN_NONE;
+
+  // method: upper-case token
+  Py_ssize_t mn = PyUnicode_GET_LENGTH(method);
+  const char* m = reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(method));
+  if (mn == 0) Py_RETURN_NONE;
+  for (Py_ssize_t i = 0; i < mn; ++i)
+    if (m[i] < 'A' || m[i] > 'Z') Py_RETURN_NONE;
+
+  // url: scheme://authority[/path][?query], no fragment (h1.py _split_url)
+  Py_ssize_t un = PyUnicode_GET_LENGTH(url);
+  const char* u = reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(url));
+  Py_ssize_t i = 0;
+  while (i + 2 < un && !(u[i] == ':' && u[i + 1] == '/' && u[i + 2] == '/')) ++i;
+  if (i == 0 || i + 2 >= un) Py_RETURN_NONE;
+  Py_ssize_t k = i + 3;
+  while (k < un && u[k] != '/' && u[k] != '?' && u[k] != '#') ++k;
+  bool has_q = false;
+  for (Py_ssize_t j = k; j < un; ++j) {
+    unsigned char ch = static_cast<unsigned char>(u[j]);
+    if (ch < 0x21 || ch > 0x7E || ch == '#') Py_RETURN_NONE;  // _resolve would quote it
+    if (ch == '?') has_q = true;
+  }
+  if (params && has_q && PyDict_GET_SIZE(params)) Py_RETURN_NONE;  // with_query appends with '&'
+  PyObject* key = PyUnicode_FromStringAndSize(u, k);
+  if (!key) return nullptr;
+  PyObject* o = PyDict_GetItemWithError(origins, key);
+  Py_DECREF(key);
+  if (!o) {
+    if (PyErr_Occurred()) return nullptr;
+    Py_RETURN_NONE;  // first request to this origin: the Python path creates it
+  }
+  if (Py_TYPE(o) != g.origin.type) Py_RETURN_NONE;
+  PyObject* host = g.origin.get(o, O_HOST_HEADER);
+  PyObject* auth = g.origin.get(o, O_AUTH);
+  PyObject* idle = g.origin.get(o, O_IDLE);
+  if (!host || !auth || !idle || !PyUnicode_CheckExact(host) || !PyUnicode_IS_ASCII(host) ||
+      (auth != Py_None && (!PyUnicode_CheckExact(auth) || !PyUnicode_IS_ASCII(auth))))
+    Py_RETURN_NONE;
+
+  // request text: "M target HTTP/1.1\r\nHost: h\r\n[Authorization: a\r\n]" + User-Agent tail
+  std::string req;
+  req.reserve(size_t(un) + 256);
+  req.append(m, size_t(mn));
+  req += ' ';
+  if (k == un || u[k] != '/') req += '/';
+  req.append(u + k, size_t(un - k));
+  std::string q;
+  if (params && PyDict_GET_SIZE(params)) {
+    Py_ssize_t pos = 0;
+    PyObject *pk, *pv;
+    bool first = true;
+    while (PyDict_Next(params, &pos, &pk, &pv)) {
+      if (!text_query_pair_append(q, pk, pv, &first, false)) {
+        PyErr_Clear();  // the Python path raises it at the await
+        Py_RETURN_NONE;
+      }
+    }
+    if (!q.empty()) {
+      req += '?';
+      req += q;
+    }
+  }
+  req += " HTTP/1.1\r\nHost: ";
+  req.append(reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(host)), size_t(PyUnicode_GET_LENGTH(host)));
+  req += "\r\n";
+  if (auth != Py_None) {
+    req += "Authorization: ";
+    req.append(reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(auth)), size_t(PyUnicode_GET_LENGTH(auth)));
+    req += "\r\n";
+  }
+  PyObject* t = is_body_method(m, mn) ? tail_cl0 : tail;
+  req.append(PyBytes_AS_STRING(t), size_t(PyBytes_GET_SIZE(t)));
+
+  // a live idle keep-alive connection on a NetConn (the Python fast path's idle pop)
+  double ka = PyFloat_AS_DOUBLE(keepalive);
+  PyObject* conn = nullptr;
+  for (;;) {
+    Py_ssize_t n = PyObject_Size(idle);
+    if (n < 0) return nullptr;
+    if (n == 0) Py_RETURN_NONE;  // connect or wait for a slot: Python path
+    PyObject* cand = PyObject_CallMethodNoArgs(idle, s_pop);
+    if (!cand) return nullptr;
+    if (Py_TYPE(cand) != g.conn.type) {
+      PyObject* r = PyObject_CallMethodOneArg(idle, s_append, cand);  // put it back
+      Py_DECREF(cand);
+      if (!r) return nullptr;
+      Py_DECREF(r);
+      Py_RETURN_NONE;
+    }
+    PyObject* closed = g.conn.get(cand, C_CLOSED);
+    PyObject* last = g.conn.get(cand, C_LAST_USED);
+    double lu = last ? PyFloat_AsDouble(last) : -1e300;
+    if (lu == -1.0 && PyErr_Occurred()) {
+      Py_DECREF(cand);
+      return nullptr;
+    }
+    if (closed == Py_False && mono_s() - lu < ka) {
+      PyObject* net = g.conn.get(cand, C_NET);
+      if (!net || !is_netconn(net) || !netconn_open(net)) {  // TLS / asyncio transport: Python path
+        PyObject* r = PyObject_CallMethodOneArg(idle, s_append, cand);
+        Py_DECREF(cand);
+        if (!r) return nullptr;
+        Py_DECREF(r);
+        Py_RETURN_NONE;
+      }
+      conn = cand;
+      break;
+    }
+    PyObject* r = PyObject_CallMethodOneArg(client, s_drop, cand);  // stale: self._drop(cand)
+    Py_DECREF(cand);
+    if (!r) return nullptr;
+    Py_DECREF(r);
+  }
+
+  // committed: the request goes out on `conn`
+  struct Own {
+    PyObject* p;
+    ~Own() { Py_XDECREF(p); }
+  } own_conn{conn};
+  if (bump(counts, s_requests) < 0 || bump(counts, s_reused) < 0) return nullptr;
+  PyObject* uses = g.conn.get(conn, C_USES);
+  bool reused = true;
+  if (uses) {
+    int pos = PyObject_IsTrue(uses);  // reused = c.uses > 0 (an idle connection has served one)
+    if (pos < 0) return nullptr;
+    reused = pos != 0;
+    PyObject* one = PyLong_FromLong(1);
+    PyObject* nu = one ? PyNumber_Add(uses, one) : nullptr;
+    Py_XDECREF(one);
+    if (!nu) return nullptr;
+    g.conn.set(conn, C_USES, nu);
+  }
+  PyObject* loop = PyObject_CallNoArgs(g.get_running_loop);
+  if (!loop) return nullptr;
+  Own own_loop{loop};
+  PyObject* now = PyObject_CallMethodNoArgs(loop, s_time);
+  if (!now) return nullptr;
+  double dl = PyFloat_AsDouble(now);
+  Py_DECREF(now);
+  if (dl == -1.0 && PyErr_Occurred()) return nullptr;
+  PyObject* tmo = timeout;  // `timeout or self.timeout_s`
+  if (tmo) {
+    int truth = PyObject_IsTrue(tmo);
+    if (truth < 0) return nullptr;
+    if (!truth) tmo = nullptr;
+  }
+  double add = PyFloat_AsDouble(tmo ? tmo : timeout_s);
+  if (add == -1.0 && PyErr_Occurred()) return nullptr;
+  PyObject* deadline = PyFloat_FromDouble(dl + add);
+  if (!deadline) return nullptr;
+  Own own_deadline{deadline};
+  PyObject* full;
+  if (q.empty()) {
+    Py_INCREF(url);
+    full = url;
+  } else {
+    std::string f(u, size_t(un));
+    f += '?';
+    f += q;
+    full = PyUnicode_FromStringAndSize(f.data(), Py_ssize_t(f.size()));
+    if (!full) return nullptr;
+  }
+  Own own_full{full};
+  Py_INCREF(method);
+  PyObject* what = PyTuple_Pack(2, method, full);
+  Py_DECREF(method);
+  if (!what) return nullptr;
+  Py_INCREF(deadline);
+  g.conn.set(conn, C_DEADLINE, deadline);
+  g.conn.set(conn, C_WHAT, what);
+  PyObject* fut = iofuture_new(loop);
+  if (!fut) return nullptr;
+  Own own_fut{fut};
+  bool head = mn == 4 && memcmp(m, "HEAD", 4) == 0;
+  if (netconn_h1_request(g.conn.get(conn, C_NET), req, fut, head) < 0) return nullptr;
+  if (PySet_Add(busy, conn) < 0) return nullptr;
+  PyObject* sweeper = PyDict_GetItemWithError(d, s_sweeper);
+  if (!sweeper && PyErr_Occurred()) return nullptr;
+  if (!sweeper || sweeper == Py_None) {
+    PyObject* r = PyObject_CallMethodOneArg(client, s_arm, loop);
+    if (!r) return nullptr;
+    Py_DECREF(r);
+  }
+  H1CallObject* call = PyObject_GC_New(H1CallObject, &H1CallType);
+  if (!call) return nullptr;
+  Py_INCREF(client);
+  call->client = client;
+  call->conn = conn;
+  own_conn.p = nullptr;
+  call->fut = fut;
+  own_fut.p = nullptr;
+  Py_INCREF(method);
+  call->method = method;
+  call->full = full;
+  own_full.p = nullptr;
+  call->deadline = deadline;
+  own_deadline.p = nullptr;
+  call->sub = nullptr;
+  call->state = ST_WAIT;
+  call->reused = reused;
+  PyObject_GC_Track(call);
+  return reinterpret_cast<PyObject*>(call);
+}
+
+// h1_fast(client, method, url, params=None, timeout=None) -> H1Call or None
+PyObject* mod_h1_fast(PyObject*, PyObject* const* a, Py_ssize_t n) {
+  if (n < 3 || n > 5) {
+    PyErr_SetString(PyExc_TypeError, "h1_fast(client, method, url, params=None, timeout=None)");
+    return nullptr;
+  }
+  BEHOLDER_TRY { return h1_fast_impl(a[0], a[1], a[2], n > 3 ? a[3] : Py_None, n > 4 ? a[4] : Py_None); }
+  BEHOLDER_CATCH(nullptr)
+}
+
+// h1_setup(client_cls, conn_cls, origin_cls, response_cls, get_running_loop)
+PyObject* mod_h1_setup(PyObject*, PyObject* args) {
+  PyObject *client_cls, *conn_cls, *origin_cls, *resp_cls, *grl;
+  if (!PyArg_ParseTuple(args, "OOOOO", &client_cls, &conn_cls, &origin_cls, &resp_cls, &grl)) return nullptr;
+  g.ready = false;
+  if (!PyType_Check(client_cls)) {
+    PyErr_SetString(PyExc_TypeError, "h1_setup: client_cls must be a class");
+    return nullptr;
+  }
+  if (!g.conn.resolve(conn_cls, kConnSlots, C_N) || !g.origin.resolve(origin_cls, kOriginSlots, O_N) ||
+      !g.resp.resolve(resp_cls, kRespSlots, R_N))
+    return nullptr;
+  if (reinterpret_cast<PyTypeObject*>(resp_cls)->tp_dictoffset != 0) {
+    PyErr_SetString(PyExc_TypeError, "h1_setup: the response class must have __slots__ only");
+    return nullptr;
+  }
+  Py_INCREF(client_cls);
+  Py_XSETREF(g.client_type, reinterpret_cast<PyTypeObject*>(client_cls));
+  Py_INCREF(grl);
+  Py_XSETREF(g.get_running_loop, grl);
+  g.ready = true;
+  Py_RETURN_NONE;
+}
+
+PyObject* mod_h1_disable(PyObject*, PyObject*) {
+  g.ready = false;
+  Py_RETURN_NONE;
+}
+
+PyMethodDef h1_functions[] = {
+    {"h1_fast", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(mod_h1_fast)), METH_FASTCALL,
+     "h1_fast(client, method, url, params=None, timeout=None) -> awaitable H1Call, or None for the Python path "
+     "(sinks/h1.py)"},
+    {"h1_setup", mod_h1_setup, METH_VARARGS,
+     "h1_setup(H1Client, _Conn, _Origin, HttpResponse, get_running_loop): enable h1_fast for these classes"},
+    {"h1_disable", mod_h1_disable, METH_NOARGS, "h1_disable(): h1_fast always returns None"},
+    {nullptr, nullptr, 0, nullptr}};
+
+}  // namespace
+
+int init_h1call_types(PyObject* m) {
+  struct {
+    PyObject** slot;
+    const char* text;
+  } strs[] = {{&s_closed_attr, "_closed"},   {&s_origins, "_origins"},   {&s_counts, "counts"},
+              {&s_keepalive_s, "keepalive_s"}, {&s_timeout_s, "timeout_s"}, {&s_busy, "_busy"},
+              {&s_sweeper, "_sweeper"},       {&s_tail, "_tail"},         {&s_tail_cl0, "_tail_cl0"},
+              {&s_requests, "requests"},      {&s_reused, "reused"},      {&s_drop, "_drop"},
+              {&s_release, "_release"},       {&s_arm, "_arm"},           {&s_resume, "_resume"},
+              {&s_time, "time"},              {&s_pop, "pop"},            {&s_append, "append"},
+              {&s_buffered, "buffered"},      {&s_throw, "throw"},        {&s_close, "close"}};
+  for (auto& s : strs)
+    if (!(*s.slot = PyUnicode_InternFromString(s.text))) return -1;
+  H1CallType.tp_name = "beholder_amd.ops._native.H1Call";
+  H1CallType.tp_basicsize = sizeof(H1CallObject);
+  H1CallType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC;
+  H1CallType.tp_doc = "An HTTP/1.1 request in flight on the native fast path (awaitable; see h1_fast)";
+  H1CallType.tp_dealloc = reinterpret_cast<destructor>(call_dealloc);
+  H1CallType.tp_finalize = reinterpret_cast<destructor>(call_finalize);
+  H1CallType.tp_traverse = reinterpret_cast<traverseproc>(call_traverse);
+  H1CallType.tp_clear = reinterpret_cast<inquiry>(call_clear);
+  H1CallType.tp_as_async = &call_async;
+  H1CallType.tp_iter = PyObject_SelfIter;
+  H1CallType.tp_iternext = reinterpret_cast<iternextfunc>(call_iternext);
+  H1CallType.tp_methods = call_methods;
+  if (PyType_Ready(&H1CallType) < 0) return -1;
+  Py_INCREF(&H1CallType);
+  if (PyModule_AddObject(m, "H1Call", reinterpret_cast<PyObject*>(&H1CallType)) < 0) return -1;
+  return PyModule_AddFunctions(m, h1_functions);
+}
+
+}  // namespace beholder

@@ -663,6 +663,91 @@ PyGetSetDef nc_getset[] = {
 
 }  // namespace
 
+bool is_netconn(PyObject* o) { return Py_TYPE(o) == &NetConnType; }
+
+bool netconn_open(PyObject* o) {
+  NetConnObject* c = reinterpret_cast<NetConnObject*>(o);
+  return c->fd >= 0 && !c->closed;
+}
+
+// The h1 request of nc_request for a caller in C (sinks/h1.py fast path, py_h1call.cpp): parser
+// started, `waiter` set, the request bytes written. 0, or -1 with an exception set.
+int netconn_h1_request(PyObject* o, const std::string& data, PyObject* waiter, bool head) {
+  NetConnObject* c = reinterpret_cast<NetConnObject*>(o);
+  if (c->kind != K_H1) {
+    PyErr_SetString(PyExc_TypeError, "not an h1 NetConn");
+    return -1;
+  }
+  if (c->fd < 0) {
+    closed_error(c);
+    return -1;
+  }
+  PyObject* kw = PyTuple_Pack(1, s_head);
+  if (!kw) return -1;
+  PyObject* args[1] = {head ? Py_True : Py_False};
+  PyObject* r = PyObject_Vectorcall(c->start, args, 0, kw);  // parser.start(head=head)
+  Py_DECREF(kw);
+  if (!r) return -1;
+  Py_DECREF(r);
+  Py_INCREF(waiter);
+  Py_XSETREF(c->waiter, waiter);
+  c->out->append(data);
+  if (c->writing) return 0;
+  return send_out(c);
+}
+
+namespace {
+
+PyObject *s_closed_name, *s_net_name;
+
+// pg_pool_execute(conns, sql, params, spread_at, size) -> IOFuture, or None for the Python path.
+// store/pgwire.py Pool.execute for a pool whose open connections are all native: the open
+// connection with the fewest queries in flight (the first on ties) gets the query, unless every
+// one has `spread_at` or more in flight and the pool may still grow.
+PyObject* mod_pg_pool_execute(PyObject*, PyObject* const* a, Py_ssize_t n) {
+  if (n != 5 || !PyList_CheckExact(a[0])) {
+    PyErr_SetString(PyExc_TypeError, "pg_pool_execute(conns: list, sql, params, spread_at, size)");
+    return nullptr;
+  }
+  Py_ssize_t spread = PyLong_AsSsize_t(a[3]);
+  Py_ssize_t size = spread == -1 && PyErr_Occurred() ? -1 : PyLong_AsSsize_t(a[4]);
+  if (size == -1 && PyErr_Occurred()) return nullptr;
+  PyObject* conns = a[0];
+  Py_ssize_t nc = PyList_GET_SIZE(conns);
+  NetConnObject* best = nullptr;
+  size_t bp = 0;
+  for (Py_ssize_t i = 0; i < nc; ++i) {
+    PyObject* c = PyList_GET_ITEM(conns, i);
+    PyObject** dp = _PyObject_GetDictPtr(c);
+    PyObject* d = dp ? *dp : nullptr;
+    PyObject* closed = d ? PyDict_GetItemWithError(d, s_closed_name) : nullptr;
+    PyObject* net = closed ? PyDict_GetItemWithError(d, s_net_name) : nullptr;
+    if (!net) {
+      if (PyErr_Occurred()) return nullptr;
+      Py_RETURN_NONE;
+    }
+    if (closed == Py_True) continue;
+    if (closed != Py_False || Py_TYPE(net) != &NetConnType) Py_RETURN_NONE;  // asyncio transport: Python path
+    NetConnObject* nc_ = reinterpret_cast<NetConnObject*>(net);
+    if (nc_->kind != K_PG) Py_RETURN_NONE;
+    size_t p = nc_->pending->size();
+    if (!best || p < bp) {
+      best = nc_;
+      bp = p;
+    }
+  }
+  if (!best || !(bp < size_t(spread < 0 ? 0 : spread) || nc >= size)) Py_RETURN_NONE;
+  PyObject* args[2] = {a[1], a[2]};
+  return nc_execute(best, args, 2);
+}
+
+PyMethodDef pool_functions[] = {
+    {"pg_pool_execute", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(mod_pg_pool_execute)),
+     METH_FASTCALL, "pg_pool_execute(conns, sql, params, spread_at, size) -> IOFuture or None (store/pgwire.py Pool)"},
+    {nullptr, nullptr, 0, nullptr}};
+
+}  // namespace
+
 int init_netconn_types(PyObject* m) {
   struct {
     PyObject** slot;
@@ -690,7 +775,9 @@ int init_netconn_types(PyObject* m) {
   if (PyType_Ready(&NetConnType) < 0) return -1;
   Py_INCREF(&NetConnType);
   if (PyModule_AddObject(m, "NetConn", reinterpret_cast<PyObject*>(&NetConnType)) < 0) return -1;
-  return 0;
+  if (!(s_closed_name = PyUnicode_InternFromString("closed")) || !(s_net_name = PyUnicode_InternFromString("_net")))
+    return -1;
+  return PyModule_AddFunctions(m, pool_functions);
 }
 
 }  // namespace beholder

@@ -30,6 +30,7 @@ from __future__ import annotations
 import asyncio
 import base64
 import collections
+import os
 import ssl as _ssl
 import time
 from typing import Deque, Dict, Optional, Tuple
@@ -38,6 +39,7 @@ from urllib.parse import quote, unquote, urljoin
 from ..ops import H1Parser
 from ..ops import IOFuture as _IOFuture
 from ..ops import encode_query as _encode_query
+from ..ops import native as _native
 from ..utils import netconn
 from .http import HttpClient, HttpError, HttpResponse, encode_query, redact, with_query
 
@@ -391,65 +393,95 @@ class H1Client(HttpClient):
             return f"{url}?{q}", o, f"{target}?{q}", rest
         return url, o, target, rest
 
-    async def request(self, method, url, *, params=None, timeout=None) -> HttpResponse:
+    def request(self, method, url, *, params=None, timeout=None):
+        """Awaitable :class:`HttpResponse`. On a warm pool the native fast path
+        (``ops/csrc/py_h1call.cpp`` ``h1_fast``) sends the request right here and completes a
+        plain reply in C; every other case is :meth:`_request`."""
+        call = _h1_fast(self, method, url, params, timeout)
+        if call is not None:
+            return call
+        return self._request(method, url, params, timeout)
+
+    async def _request(self, method, url, params, timeout) -> HttpResponse:
         if self._closed:
             raise HttpError("client closed")
         m = method.upper()
         full, o, target, rest = self._prepare(url, params)
         loop = asyncio.get_running_loop()
         deadline = loop.time() + (timeout or self.timeout_s)
+        self.counts["requests"] += 1
+        return await self._exchange(m, full, o, target, rest, deadline, None, None, False, None)
+
+    async def _resume(self, m, full, deadline, c, w, reused, thrown) -> HttpResponse:
+        """The native fast path sent ``m full`` on the pooled connection ``c``. The reply future
+        ``w`` holds an error or a redirect, or ``thrown`` was thrown in at the await (a Task
+        waking on a failed or cancelled ``w``): the request loop continues from its await."""
+        o, target, rest = self._resolve(full)
+        return await self._exchange(m, full, o, target, rest, deadline, c, w, reused, thrown)
+
+    async def _exchange(self, m, full, o, target, rest, deadline, c, w, reused, thrown) -> HttpResponse:
+        """Send on a pooled connection, await the reply; one transparent retry on a fresh
+        connection for an idempotent request whose reused connection died before any response
+        byte; redirects for GET/HEAD. ``c``/``w``/``reused``: a request already on the wire;
+        ``thrown``: what its await raised."""
         counts = self.counts
-        counts["requests"] += 1
+        loop = asyncio.get_running_loop()
         cur = full
         redirects = 0
         fresh = False
         while True:
-            req = f"{m} {target}{rest}".encode("latin-1") + (self._tail_cl0 if m in _BODY_METHODS else self._tail)
-            c = None
-            if not fresh:  # fast path of _acquire: a live idle keep-alive connection, no await
-                idle = o.idle
-                if idle:
-                    now = time.monotonic()
-                    while idle:
-                        cand = idle.pop()
-                        if not cand.closed and now - cand.last_used < self.keepalive_s:
-                            counts["reused"] += 1
-                            c = cand
-                            break
-                        self._drop(cand)
-            try:
-                if c is None:
-                    c = await self._acquire(o, deadline, fresh)
-            except asyncio.TimeoutError:
-                counts["timeouts"] += 1
-                counts["errors"] += 1
-                raise HttpError(f"ETIMEDOUT: {m} {redact(cur)}") from None
-            except OSError as e:
-                counts["errors"] += 1
-                raise HttpError(_connect_error(e, o)) from None
-            reused = c.uses > 0
-            c.uses += 1
-            w = _IOFuture(loop)
-            c.deadline = deadline
-            c.what = (m, cur)
-            net = c.net
-            if net is not None:
-                net.request(req, w, m == "HEAD")  # parser started, reply future set, request sent
-            else:
-                c.waiter = w
-                c.parser.start(head=m == "HEAD")
-                c.transport.write(req)
+            if w is None:
+                req = f"{m} {target}{rest}".encode("latin-1") + (self._tail_cl0 if m in _BODY_METHODS else self._tail)
+                c = None
+                if not fresh:  # fast path of _acquire: a live idle keep-alive connection, no await
+                    idle = o.idle
+                    if idle:
+                        now = time.monotonic()
+                        while idle:
+                            cand = idle.pop()
+                            if not cand.closed and now - cand.last_used < self.keepalive_s:
+                                counts["reused"] += 1
+                                c = cand
+                                break
+                            self._drop(cand)
+                try:
+                    if c is None:
+                        c = await self._acquire(o, deadline, fresh)
+                except asyncio.TimeoutError:
+                    counts["timeouts"] += 1
+                    counts["errors"] += 1
+                    raise HttpError(f"ETIMEDOUT: {m} {redact(cur)}") from None
+                except OSError as e:
+                    counts["errors"] += 1
+                    raise HttpError(_connect_error(e, o)) from None
+                reused = c.uses > 0
+                c.uses += 1
+                w = _IOFuture(loop)
+                c.deadline = deadline
+                c.what = (m, cur)
+                net = c.net
+                if net is not None:
+                    net.request(req, w, m == "HEAD")  # parser started, reply future set, request sent
+                else:
+                    c.waiter = w
+                    c.parser.start(head=m == "HEAD")
+                    c.transport.write(req)
+                busy = self._busy
+                busy.add(c)
+                if self._sweeper is None:
+                    self._arm(loop)
             busy = self._busy
-            busy.add(c)
-            if self._sweeper is None:
-                self._arm(loop)
             try:
+                if thrown is not None:
+                    e, thrown = thrown, None
+                    raise e
                 status, _reason, raw, body, keep = await w
             except _Reset as e:
                 self._release(c, False)
                 if reused and not e.started and m in _IDEMPOTENT and not fresh:
                     counts["retries"] += 1
                     fresh = True
+                    w = None
                     continue
                 counts["errors"] += 1
                 raise HttpError(f"{e}: {m} {redact(cur)}") from None
@@ -462,6 +494,7 @@ class H1Client(HttpClient):
                 raise
             finally:
                 busy.discard(c)
+            w = None
             self._release(c, keep and c.parser.buffered == 0)
             if status in _REDIRECTS and m in ("GET", "HEAD"):
                 loc = _header(raw, b"location")
@@ -515,3 +548,16 @@ def _connect_error(e: OSError, o: "_Origin") -> str:
         return f"getaddrinfo ENOTFOUND {o.host}"
     name = errno.errorcode.get(e.errno or 0) if e.errno else None
     return f"connect {name or type(e).__name__} {o.host}:{o.port}"
+
+
+def _h1_python_only(client, method, url, params, timeout):
+    return None
+
+
+# Native fast path of H1Client.request (ops/csrc/py_h1call.cpp). BEHOLDER_NATIVE_H1=0 keeps every
+# request on the Python path (A/B runs, debugging); so does the plain-asyncio-future A/B switch.
+if os.environ.get("BEHOLDER_NATIVE_H1", "1") != "0" and _IOFuture is _native.IOFuture:
+    _native.h1_setup(H1Client, _Conn, _Origin, HttpResponse, asyncio.get_running_loop)
+    _h1_fast = _native.h1_fast
+else:
+    _h1_fast = _h1_python_only

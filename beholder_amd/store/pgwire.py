@@ -40,6 +40,15 @@ from ..ops import PgReader
 from ..ops import native as _native
 from ..utils import netconn
 
+
+def _pg_pool_python_only(conns, sql, params, spread_at, size):
+    return None
+
+
+# native pick + execute for a pool of native connections (ops/csrc/py_netconn.cpp); A/B switch
+_pg_pool_execute = (_native.pg_pool_execute if os.environ.get("BEHOLDER_NATIVE_POOL", "1") != "0"
+                    else _pg_pool_python_only)
+
 PROTOCOL_V3 = 196608
 
 
@@ -497,6 +506,9 @@ class Pool:
 
     def execute(self, sql: str, params: Sequence[Any] = ()):
         """Awaitable ``(rows, command_tag)`` (a future on the fast path)."""
+        f = _pg_pool_execute(self._conns, sql, params, self.spread_at, self.size)  # all connections native
+        if f is not None:
+            return f
         best = None
         bp = 0
         for c in self._conns:

@@ -1,0 +1,249 @@
+"""Native fast path of the keep-alive sink client (`ops/csrc/py_h1call.cpp` `h1_fast`, used by
+`sinks/h1.py` `H1Client.request` on a warm pool): the bytes on the wire, the responses, the
+pool accounting and every rare path (reset + retry, redirect, timeout, cancellation, abandon)
+must be those of the Python request loop (index.js:53,83,99,112 go through this client)."""
+import asyncio
+import random
+
+import pytest
+
+from beholder_amd.ops import native
+from beholder_amd.sinks import H1Client, HttpError
+from beholder_amd.sinks import h1 as h1mod
+
+
+def run(coro):
+    return asyncio.run(asyncio.wait_for(coro, 30))
+
+
+class Raw:
+    """HTTP/1.1 server that records every request's exact bytes; ``respond(target) -> bytes | None``
+    (None: drop the connection without answering; "hang": never answer)."""
+
+    def __init__(self, respond):
+        self.respond = respond
+        self.raw = []
+        self.connections = 0
+
+    async def start(self):
+        self.server = await asyncio.start_server(self._serve, "127.0.0.1", 0)
+        self.port = self.server.sockets[0].getsockname()[1]
+        return self
+
+    async def stop(self):
+        self.server.close()
+        await self.server.wait_closed()
+
+    async def _serve(self, r, w):
+        self.connections += 1
+        try:
+            while True:
+                try:
+                    head = await r.readuntil(b"\r\n\r\n")
+                except (asyncio.IncompleteReadError, ConnectionError):
+                    return
+                self.raw.append(head)
+                target = head.split(b" ", 2)[1].decode("latin-1")
+                out = self.respond(target)
+                if out == "hang":
+                    await asyncio.sleep(3600)
+                if out is None:
+                    w.transport.abort()
+                    return
+                w.write(out)
+                await w.drain()
+        finally:
+            w.close()
+
+
+OK = b"HTTP/1.1 200 OK\r\nContent-Length: 2\r\nX-A: 1\r\n\r\n{}"
+
+
+def _cases(port, n=150, seed=7):
+    rnd = random.Random(seed)
+    base = [f"http://127.0.0.1:{port}", f"http://u%40s:p%3Aw@127.0.0.1:{port}"]
+    paths = ["/1/cards/abc/actions/comments", "/bot123:XYZ/sendMessage?chat_id=5&text=a%20b", "/emby/library/refresh",
+             "", "/x y", "/é", "/a#frag", "?q=1", "/p?x=1", "/1/cards/C\r\nX-Evil:1/actions/comments"]
+    params = [None, {}, {"key": "k", "token": "t", "text": "DEPLOYED: **5%** (_x_) ü"}, {"a": None, "b": 1},
+              {"pos": 2, "idList": "L1"}, {"api_key": "x y&z"}, {"v": 1.5, "w": True}]
+    for _ in range(n):
+        yield (rnd.choice(["GET", "POST", "PUT", "get", "DELETE", "HEAD"]), rnd.choice(base) + rnd.choice(paths),
+               rnd.choice(params))
+
+
+async def _drive(port, fast: bool):
+    """Every case on one client, each after a warm-up request so a keep-alive connection is idle."""
+    saved = h1mod._h1_fast
+    if not fast:
+        h1mod._h1_fast = h1mod._h1_python_only
+    try:
+        c = H1Client(timeout_s=5)
+        out, kinds = [], []
+        for m, url, params in _cases(port):
+            try:
+                await c.request("GET", f"http://127.0.0.1:{port}/warm")
+                await c.request("GET", url.split("?")[0].split("#")[0] or url, params=None)
+            except HttpError:
+                pass
+            aw = c.request(m, url, params=params)
+            kinds.append(type(aw).__name__)
+            try:
+                r = await aw
+                out.append((r.status, r.body, r.headers, r.url))
+            except HttpError as e:
+                out.append(("error", str(e)))
+        counts = dict(c.counts)
+        await c.close()
+        return out, kinds, counts
+    finally:
+        h1mod._h1_fast = saved
+
+
+def test_fast_path_sends_the_same_bytes_and_returns_the_same_responses():
+    async def go():
+        res = {}
+        for fast in (True, False):
+            s = await Raw(lambda t: OK).start()
+            out, kinds, counts = await _drive(s.port, fast)
+            raw = [r.replace(str(s.port).encode(), b"PORT") for r in s.raw]
+            res[fast] = ([tuple(str(x).replace(str(s.port), "PORT") for x in o) for o in out], kinds, counts, raw,
+                         s.connections)
+            await s.stop()
+        return res
+    res = run(go())
+    f_out, f_kinds, f_counts, f_raw, f_conns = res[True]
+    p_out, p_kinds, p_counts, p_raw, p_conns = res[False]
+    assert f_raw == p_raw  # byte for byte, request line, Host, Authorization, User-Agent, Content-Length
+    assert f_out == p_out
+    assert f_counts == p_counts and f_conns == p_conns
+    assert "H1Call" in f_kinds and "H1Call" not in p_kinds
+    # the shapes the sinks produce take the native path; the others decline before any state changes
+    assert f_kinds.count("H1Call") > len(f_kinds) // 3
+
+
+def test_fast_path_declines_cold_pool_and_foreign_shapes():
+    async def go():
+        s = await Raw(lambda t: OK).start()
+        c = H1Client(timeout_s=5)
+        url = f"http://127.0.0.1:{s.port}/a"
+        first = c.request("GET", url)
+        kinds = [type(first).__name__]
+        await first
+        for args in (("GET", url), ("get", url), ("GET", url + "#f"), ("GET", url + "/é"), ("POST", url + "?a=1"),
+                     ("GET", f"http://127.0.0.1:{s.port + 1 if s.port < 65535 else 1}/b")):
+            aw = c.request(*args, params={"k": 1} if args[0] == "POST" else None)
+            kinds.append(type(aw).__name__)
+            try:
+                await aw
+            except HttpError:
+                pass
+        await c.close()
+        await s.stop()
+        return kinds
+    kinds = run(go())
+    assert kinds[0] == "coroutine"  # no idle connection yet
+    assert kinds[1] == "H1Call"
+    assert kinds[2:] == ["coroutine"] * 5
+
+
+def test_fast_path_reset_retry_redirect_and_errors_match_python():
+    def respond(t):
+        if t.startswith("/old"):
+            return b"HTTP/1.1 302 Found\r\nLocation: /new?a=1\r\nContent-Length: 0\r\n\r\n"
+        if t.startswith("/drop"):
+            return None
+        if t.startswith("/bad"):
+            return b"SMTP ready\r\n\r\n"
+        return b"HTTP/1.1 200 OK\r\nContent-Length: 3\r\n\r\nnew"
+
+    async def one(fast):
+        saved = h1mod._h1_fast
+        if not fast:
+            h1mod._h1_fast = h1mod._h1_python_only
+        try:
+            s = await Raw(respond).start()
+            c = H1Client(timeout_s=5)
+            base = f"http://127.0.0.1:{s.port}"
+            seen = []
+            for m, p in [("GET", "/new"), ("GET", "/old"), ("POST", "/old"), ("GET", "/drop"), ("POST", "/drop"),
+                         ("GET", "/bad"), ("GET", "/new")]:
+                await c.request("GET", base + "/new")  # warm: an idle connection for the fast path
+                try:
+                    r = await c.request(m, base + p)
+                    seen.append((r.status, r.body, r.url.replace(base, "")))
+                except HttpError as e:
+                    seen.append(str(e).replace(base, ""))
+            st = dict(c.counts)
+            await c.close()
+            await s.stop()
+            return seen, st, [r.split(b"\r\n")[0] for r in s.raw]
+        finally:
+            h1mod._h1_fast = saved
+
+    async def go():
+        return await one(True), await one(False)
+    fast, slow = run(go())
+    assert fast == slow
+    assert fast[1]["retries"] >= 1 and fast[1]["errors"] >= 2
+
+
+def test_fast_path_timeout_cancel_and_abandon_release_the_connection():
+    async def go():
+        s = await Raw(lambda t: "hang" if t.startswith("/slow") else OK).start()
+        c = H1Client(timeout_s=5)
+        base = f"http://127.0.0.1:{s.port}"
+        await c.request("GET", base + "/a")
+        aw = c.request("GET", base + "/slow", params={"token": "secret"}, timeout=0.2)
+        assert type(aw).__name__ == "H1Call"
+        with pytest.raises(HttpError, match=r"^ETIMEDOUT: GET http://127\.0\.0\.1:\d+/slow$"):
+            await aw
+        await c.request("GET", base + "/a")
+        t = asyncio.ensure_future(c.request("GET", base + "/slow"))
+        await asyncio.sleep(0.05)
+        t.cancel()
+        with pytest.raises(asyncio.CancelledError):
+            await t
+        await c.request("GET", base + "/a")
+        aw = c.request("GET", base + "/slow")
+        assert type(aw).__name__ == "H1Call"
+        aw.close()  # never awaited to the end: like closing the coroutine
+        busy = len(c._busy)
+        r = await c.request("GET", base + "/a")
+        st = dict(c.counts)
+        open_ = sum(o.open for o in c._origins.values())
+        await c.close()
+        await s.stop()
+        return busy, r.status, st, open_, s.connections
+    busy, status, st, open_, conns = run(go())
+    assert busy == 0 and status == 200
+    assert st["timeouts"] == 1 and st["errors"] == 1
+    assert open_ == 1 and conns == 4  # each abandoned request's connection was dropped, a new one opened
+
+
+def test_fast_path_under_native_driver_and_gather():
+    """Many concurrent requests through gather (Tasks) and through a native Driver."""
+    async def go():
+        s = await Raw(lambda t: OK).start()
+        c = H1Client(timeout_s=5, max_per_host=8)
+        base = f"http://127.0.0.1:{s.port}"
+        await asyncio.gather(*[c.request("GET", f"{base}/w{i}") for i in range(8)])
+        rs = await asyncio.gather(*[c.request("POST", f"{base}/p{i}", params={"i": i}) for i in range(200)])
+        done = []
+
+        async def handler(i):
+            r = await c.request("PUT", f"{base}/d{i}", params={"pos": 2})
+            done.append(r.status)
+
+        for i in range(50):
+            coro = handler(i)
+            first = coro.send(None)
+            native.Driver(coro, lambda d, e: None).start(first)
+        while len(done) < 50:
+            await asyncio.sleep(0.01)
+        st = dict(c.counts)
+        await c.close()
+        await s.stop()
+        return [r.status for r in rs], done, st, s.connections
+    statuses, done, st, conns = run(go())
+    assert statuses == [200] * 200 and done == [200] * 50
+    assert st["requests"] == 258 and conns <= 8

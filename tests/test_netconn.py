@@ -179,3 +179,38 @@ def test_disabled_by_env(monkeypatch):
         finally:
             await pg.stop()
     assert run(go()) == (None, ([(1,)], "SELECT 1"))
+
+
+def test_native_pool_pick_matches_python_pick(monkeypatch):
+    """store/pgwire.py Pool.execute: the native pick (ops pg_pool_execute) sends each query to the
+    same connection the Python loop would (fewest in flight, first on ties, grow only when every
+    open one has spread_at or more) and the answers are the same."""
+    from beholder_amd.store import pgwire
+
+    async def one(native_pick):
+        if not native_pick:
+            monkeypatch.setattr(pgwire, "_pg_pool_execute", pgwire._pg_pool_python_only)
+        else:
+            monkeypatch.setattr(pgwire, "_pg_pool_execute", pgwire._native.pg_pool_execute)
+        pg = await FakePg(auth="md5").start()
+        try:
+            pool = await pgwire.Pool(pg.dsn, size=3, spread_at=4).open()
+            seq, futs = [], []
+            for wave in range(3):
+                for i in range(10):
+                    futs.append(pool.execute("SELECT $1 * 2", (wave * 10 + i,)))
+                    seq.append(tuple(c.pending for c in pool._conns))
+                await asyncio.sleep(0)
+            res = await asyncio.gather(*futs)
+            kinds = {type(f).__name__ for f in futs}
+            await pool.close()
+            return seq, [r[0] for r in res], len(pool._conns), kinds
+        finally:
+            await pg.stop()
+
+    nat = run(one(True))
+    py = run(one(False))
+    assert nat[1] == py[1] == [[(2 * i,)] for i in range(30)]
+    assert nat[0] == py[0]
+    assert nat[2] == py[2]
+    assert "IOFuture" in nat[3]
