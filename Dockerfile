@@ -1,7 +1,7 @@
 # Reference: FROM tritonmedia/base; yarn; copy source into /stack as uid 999 (Dockerfile:1-6).
 FROM python:3.10-slim
 
-RUN apt-get update && apt-get install -y --no-install-recommends g++ && rm -rf /var/lib/apt/lists/*
+RUN apt-get update && apt-get install -y --no-install-recommends g++ libssl-dev && rm -rf /var/lib/apt/lists/*
 WORKDIR /stack
 RUN useradd --uid 999 --create-home --home-dir /home/beholder beholder && chown 999:999 /stack
 

@@ -32,6 +32,11 @@ TARGET = os.path.join(HERE, "_native" + EXT_SUFFIX)
 STAMP = TARGET + ".srchash"
 
 
+# OpenSSL for the native TLS connections (ops/csrc/py_tls.cpp): the same libssl the interpreter's
+# `ssl` module loads (headers from libssl-dev)
+LIBS = ["-lssl", "-lcrypto"]
+
+
 def sources() -> list:
     return sorted(glob.glob(os.path.join(CSRC, "*.cpp")))
 
@@ -66,7 +71,7 @@ def build(force: bool = False, debug: bool = False, sanitize: str = "", cxx: str
     cxx = cxx or os.environ.get("CXX") or "g++"
     flags = compile_flags(debug, sanitize)
     # hash path-independent flags so a snapshot copied elsewhere (GPU box) reuses the .so
-    digest = source_hash([f for f in flags if not f.startswith("-I")] + [cxx, sysconfig.get_config_var("SOABI") or ""])
+    digest = source_hash([f for f in flags if not f.startswith("-I")] + LIBS + [cxx, sysconfig.get_config_var("SOABI") or ""])
     if not force and os.path.exists(TARGET) and os.path.exists(STAMP):
         with open(STAMP) as f:
             if f.read().strip() == digest:
@@ -87,7 +92,7 @@ def build(force: bool = False, debug: bool = False, sanitize: str = "", cxx: str
             return obj
         with concurrent.futures.ThreadPoolExecutor(jobs) as ex:
             objs = list(ex.map(compile_one, sources()))
-        link = [cxx, *[f for f in flags if not f.startswith("-I") and not f.startswith("-W")], *objs, "-o", tmp]
+        link = [cxx, *[f for f in flags if not f.startswith("-I") and not f.startswith("-W")], *objs, *LIBS, "-o", tmp]
         if verbose:
             print(" ".join(link), file=sys.stderr)
         subprocess.run(link, check=True)

@@ -38,7 +38,7 @@ from typing import Dict, List, Optional
 
 from .generator import Workload, bench_config
 
-CONFIGS = ("plumbing", "firehose_1k", "rate_10k", "backpressure", "soak", "amqp", "io_bound", "io_bound_wide", "http_tcp", "tcp_e2e")
+CONFIGS = ("plumbing", "firehose_1k", "rate_10k", "backpressure", "soak", "amqp", "io_bound", "io_bound_wide", "http_tcp", "tcp_e2e", "tls_e2e")
 
 
 def _rss_mb() -> float:
@@ -260,6 +260,8 @@ def run_config(name: str, *, duration_s: Optional[float] = None, events: Optiona
         res = _http_tcp(w, events or 100_000)
     elif name == "tcp_e2e":
         res = _tcp_e2e(events or 100_000)
+    elif name == "tls_e2e":
+        res = _tcp_e2e(events or 100_000, http_servers=4, tls=True)  # TLS fakes cost more CPU per request
     elif name == "amqp":
         res = _amqp(events or 200_000)
     elif name == "soak":
@@ -366,12 +368,13 @@ def _http_tcp(w: Workload, n: int, servers: int = 3, clients=("h1", "aiohttp")) 
     return out
 
 
-def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2) -> dict:
+def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = False) -> dict:
     """Production-shaped: every dependency over real TCP. A replay AMQP broker streams n
     events (prefetch 100, index.js:43). Each handler reads / updates the media row in a
     fake Postgres (pipelined ``pgwire``). Every sink call goes to a fake HTTP endpoint
     (keep-alive ``h1`` client). The fakes are separate processes; the numbers describe
-    the consumer process."""
+    the consumer process. ``tls`` (config ``tls_e2e``): the sinks are HTTPS, as Trello and
+    Telegram are in production (certificate verified against the bench's own CA)."""
     from ..config import Config
     from ..service import Service
     from ..sinks import H1Client
@@ -384,11 +387,12 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2) -> dict:
     procs = list(bprocs)
     out: dict = {"events": n, "prefetch": 100}
     try:
-        hport, hp = _spawn("beholder_amd.bench.http_sink_server", http_servers)
+        hport, hp = _spawn("beholder_amd.bench.http_sink_server", http_servers, ("--tls",) if tls else ())
         procs += hp
         pport, pp = _spawn("beholder_amd.bench.pg_sink_server", pg_servers, ("--media", "10000", "--seed", "0"))
         procs += pp
-        url = f"http://127.0.0.1:{hport}"
+        url = f"{'https' if tls else 'http'}://127.0.0.1:{hport}"
+        out["tls"] = tls
 
         async def go():
             cfgd = bench_config()
@@ -397,7 +401,11 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2) -> dict:
             sink = open(os.devnull, "w", buffering=1 << 16)
             src = AmqpSource(f"amqp://guest:guest@127.0.0.1:{bport}/", prefetch=100)
             store = PostgresStore(f"postgres://beholder@127.0.0.1:{pport}/media", pool_size=4)
-            http = H1Client(timeout_s=30)
+            if tls:
+                from .http_sink_server import TLS_CERT
+                http = H1Client(timeout_s=30, ssl_cafile=TLS_CERT)
+            else:
+                http = H1Client(timeout_s=30)
             svc = Service(Config.from_dict(cfgd), source=src, store=store, http=http, logger=Logger(stream=sink),
                           serve_metrics=False)
             await svc.init()

@@ -27,6 +27,8 @@
 // the socket fails (the fd is already closed and unregistered), _net_error(exc) for a protocol
 // error or an unsolicited reply, _net_message(type, body) for out-of-band Postgres messages.
 #include <errno.h>
+#include <openssl/err.h>
+#include <openssl/ssl.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -42,6 +44,10 @@ bool iofuture_done(PyObject* f);
 int iofuture_resolve(PyObject* f, PyObject* v);
 int iofuture_reject(PyObject* f, PyObject* exc);
 int pg_bind_append(std::string& o, const char* name, size_t nlen, PyObject* params);
+bool is_tls_context(PyObject* o);
+SSL* tls_new_ssl(PyObject* ctx_obj, int fd, const char* host, int port);
+void tls_count_handshake(SSL* ssl);
+void tls_describe_failure(SSL* ssl, std::string& reason, std::string& message, bool& verify);
 
 namespace {
 
@@ -78,6 +84,13 @@ struct NetConnObject {
   std::string* out;
   std::deque<PgPending>* pending;
   uint64_t n_stmts, bytes_in, bytes_out, recvs, sends;
+  // TLS (py_tls.cpp): NULL ssl = plain TCP
+  SSL* ssl;
+  uint8_t tls_state;         // 0 plain, 1 handshaking, 2 established
+  uint8_t write_wants_read;  // an SSL_write needs the peer's next record first (renegotiation)
+  PyObject* tls_ctx;         // TlsContext (owns the SSL_CTX and the session cache)
+  PyObject* hs_fut;          // handshake IOFuture: None when established, rejected on failure
+  PyObject* tls_error;       // callable(reason, message, verify) -> exception for a failed handshake
 };
 
 PyTypeObject NetConnType = {PyVarObject_HEAD_INIT(nullptr, 0)};
@@ -107,11 +120,32 @@ void shut(NetConnObject* c) {
   Py_XDECREF(fdo);
   PyErr_Clear();
   PyErr_Restore(et, ev, tb);
+  if (c->ssl) {
+    // an established session stays resumable when its connection is dropped without close_notify
+    // (idle keep-alive expiry, peer reset): OpenSSL would otherwise mark the cached session
+    // not resumable in SSL_free
+    if (c->tls_state == 2) SSL_set_shutdown(c->ssl, SSL_SENT_SHUTDOWN | SSL_RECEIVED_SHUTDOWN);
+    SSL_free(c->ssl);
+    c->ssl = nullptr;
+  }
   ::close(c->fd);
   c->fd = -1;
   c->writing = 0;
   c->closed = 1;
   c->out->clear();
+}
+
+// Rejects a pending handshake future with `exc` (borrowed; NULL = ConnectionResetError).
+void hs_fail(NetConnObject* c, PyObject* exc) {
+  PyObject* f = c->hs_fut;
+  if (!f || iofuture_done(f)) return;
+  PyObject *et, *ev, *tb;
+  PyErr_Fetch(&et, &ev, &tb);
+  PyObject* own = nullptr;
+  if (!exc) exc = own = PyObject_CallFunction(PyExc_ConnectionResetError, "s", "connection closed during TLS handshake");
+  if (!exc || iofuture_reject(f, exc) < 0) PyErr_WriteUnraisable(f);
+  Py_XDECREF(own);
+  PyErr_Restore(et, ev, tb);
 }
 
 // owner.<name>(arg) for a rare path; the error (if any) is reported, never propagated into the loop
@@ -128,6 +162,7 @@ void notify(NetConnObject* c, PyObject* name, PyObject* arg) {
 // Peer closed (exc NULL) or the socket failed: close, then tell the owner.
 void lost(NetConnObject* c, int err) {
   shut(c);
+  hs_fail(c, nullptr);
   if (err) {
     errno = err;
     PyErr_SetFromErrno(PyExc_OSError);
@@ -157,7 +192,10 @@ int watch_writes(NetConnObject* c) {
 
 // Sends c->out (after anything already queued). 0 ok, -1 Python error. A socket error closes
 // the connection and is reported to the owner (_net_lost) before this returns.
+int send_out_tls(NetConnObject* c);
+
 int send_out(NetConnObject* c) {
+  if (c->ssl) return send_out_tls(c);
   std::string& o = *c->out;
   size_t off = 0;
   while (off < o.size()) {
@@ -186,6 +224,80 @@ int send_out(NetConnObject* c) {
     Py_DECREF(r);
     c->writing = 0;
   }
+  return 0;
+}
+
+int unwatch_writes(NetConnObject* c) {
+  if (!c->writing) return 0;
+  PyObject* fdo = PyLong_FromLong(c->fd);
+  if (!fdo) return -1;
+  PyObject* r = PyObject_CallMethodOneArg(c->loop, s_remove_writer, fdo);
+  Py_DECREF(fdo);
+  if (!r) return -1;
+  Py_DECREF(r);
+  c->writing = 0;
+  return 0;
+}
+
+// send_out over TLS: SSL_write what is queued (nothing before the handshake completes).
+int send_out_tls(NetConnObject* c) {
+  if (c->tls_state != 2) return 0;
+  std::string& o = *c->out;
+  size_t off = 0;
+  while (off < o.size()) {
+    ERR_clear_error();
+    size_t len = o.size() - off;
+    int n = SSL_write(c->ssl, o.data() + off, len > (1u << 30) ? int(1u << 30) : int(len));
+    if (n > 0) {
+      off += size_t(n);
+      c->bytes_out += uint64_t(n);
+      ++c->sends;
+      continue;
+    }
+    int e = SSL_get_error(c->ssl, n);
+    if (e == SSL_ERROR_WANT_WRITE) break;
+    if (e == SSL_ERROR_WANT_READ) {
+      c->write_wants_read = 1;
+      break;
+    }
+    int err = e == SSL_ERROR_SYSCALL && errno ? errno : EPIPE;
+    o.clear();
+    lost(c, err);
+    return 0;
+  }
+  o.erase(0, off);
+  if (!o.empty() && !c->write_wants_read) return watch_writes(c);
+  return unwatch_writes(c);
+}
+
+// Drives the handshake. On success: counted, the future resolved, queued output sent.
+// On failure: the future rejected with tls_error(reason, message, verify), the socket closed.
+int tls_handshake(NetConnObject* c) {
+  ERR_clear_error();
+  int r = SSL_do_handshake(c->ssl);
+  if (r == 1) {
+    c->tls_state = 2;
+    tls_count_handshake(c->ssl);
+    if (unwatch_writes(c) < 0) return -1;
+    PyObject* f = c->hs_fut;
+    if (f && !iofuture_done(f) && iofuture_resolve(f, Py_None) < 0) return -1;
+    if (c->fd >= 0 && !c->out->empty()) return send_out(c);
+    return 0;
+  }
+  int e = SSL_get_error(c->ssl, r);
+  if (e == SSL_ERROR_WANT_READ) return unwatch_writes(c);
+  if (e == SSL_ERROR_WANT_WRITE) return watch_writes(c);
+  std::string reason, message;
+  bool verify = false;
+  tls_describe_failure(c->ssl, reason, message, verify);
+  ERR_clear_error();
+  PyObject* exc = c->tls_error ? PyObject_CallFunction(c->tls_error, "ssO", reason.c_str(), message.c_str(),
+                                                       verify ? Py_True : Py_False)
+                               : PyObject_CallFunction(PyExc_ConnectionError, "s", message.c_str());
+  if (!exc) return -1;
+  shut(c);
+  hs_fail(c, exc);
+  Py_DECREF(exc);
   return 0;
 }
 
@@ -327,6 +439,9 @@ int nc_traverse(NetConnObject* c, visitproc visit, void* arg) {
   Py_VISIT(c->stmts);
   Py_VISIT(c->pg_error);
   Py_VISIT(c->closed_exc);
+  Py_VISIT(c->tls_ctx);
+  Py_VISIT(c->hs_fut);
+  Py_VISIT(c->tls_error);
   if (c->pending) {
     for (const PgPending& p : *c->pending) {
       Py_VISIT(p.fut);
@@ -349,6 +464,8 @@ int nc_clear(NetConnObject* c) {
   Py_CLEAR(c->stmts);
   Py_CLEAR(c->pg_error);
   Py_CLEAR(c->closed_exc);
+  Py_CLEAR(c->hs_fut);
+  Py_CLEAR(c->tls_error);
   if (c->pending) drop_pending(c);
   return 0;
 }
@@ -356,8 +473,13 @@ int nc_clear(NetConnObject* c) {
 void nc_dealloc(NetConnObject* c) {
   PyObject_GC_UnTrack(c);
   if (c->fd >= 0) shut(c);  // normally closed by the owner first
+  if (c->ssl) {  // set up but never owned the fd (init failed)
+    SSL_free(c->ssl);
+    c->ssl = nullptr;
+  }
   nc_clear(c);
   Py_CLEAR(c->loop);
+  Py_CLEAR(c->tls_ctx);  // after shut(): the SSL refers to it
   delete c->out;
   delete c->pending;
   Py_TYPE(c)->tp_free(reinterpret_cast<PyObject*>(c));
@@ -370,13 +492,21 @@ PyObject* nc_flush(NetConnObject* c, PyObject*);
 // NetConn(fd, loop, kind, owner, parser, stmts=None, pg_error=None, closed_exc=ConnectionError):
 // takes ownership of fd (a connected TCP socket) and starts watching it.
 int nc_init(NetConnObject* c, PyObject* args, PyObject* kwds) {
-  static const char* kwlist[] = {"fd", "loop", "kind", "owner", "parser", "stmts", "pg_error", "closed_exc", nullptr};
+  static const char* kwlist[] = {"fd",        "loop", "kind",       "owner",     "parser", "stmts", "pg_error",
+                                 "closed_exc", "tls",  "server_hostname", "port", "tls_error", nullptr};
   int fd;
   PyObject *loop, *owner, *parser, *stmts = Py_None, *pg_error = Py_None, *closed_exc = PyExc_ConnectionError;
+  PyObject *tls = Py_None, *tls_error = Py_None;
   const char* kind;
-  if (!PyArg_ParseTupleAndKeywords(args, kwds, "iOsOO|OOO", const_cast<char**>(kwlist), &fd, &loop, &kind, &owner,
-                                   &parser, &stmts, &pg_error, &closed_exc))
+  const char* host = nullptr;
+  int port = 0;
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "iOsOO|OOOOziO", const_cast<char**>(kwlist), &fd, &loop, &kind, &owner,
+                                   &parser, &stmts, &pg_error, &closed_exc, &tls, &host, &port, &tls_error))
     return -1;
+  if (tls != Py_None && (!is_tls_context(tls) || !host || strcmp(kind, "h1") != 0)) {
+    PyErr_SetString(PyExc_TypeError, "tls needs a TlsContext, server_hostname and kind 'h1'");
+    return -1;
+  }
   if (!PyExceptionClass_Check(closed_exc)) {
     PyErr_SetString(PyExc_TypeError, "closed_exc must be an exception class");
     return -1;
@@ -424,6 +554,18 @@ int nc_init(NetConnObject* c, PyObject* args, PyObject* kwds) {
   c->on_writable = c->on_readable ? PyObject_GetAttrString(reinterpret_cast<PyObject*>(c), "_on_writable") : nullptr;
   c->flush_cb = c->on_writable ? PyObject_GetAttrString(reinterpret_cast<PyObject*>(c), "flush") : nullptr;
   if (!c->flush_cb) return -1;
+  if (tls != Py_None) {  // set up before the fd is owned: a failure here leaves it to the caller
+    c->hs_fut = iofuture_new(loop);
+    if (!c->hs_fut) return -1;
+    c->ssl = tls_new_ssl(tls, fd, host, port);
+    if (!c->ssl) return -1;
+    Py_INCREF(tls);
+    c->tls_ctx = tls;
+    if (tls_error != Py_None) {
+      Py_INCREF(tls_error);
+      c->tls_error = tls_error;
+    }
+  }
   PyObject* fdo = PyLong_FromLong(fd);
   if (!fdo) return -1;
   PyObject* r = PyObject_CallMethodObjArgs(loop, s_add_reader, fdo, c->on_readable, nullptr);
@@ -432,13 +574,20 @@ int nc_init(NetConnObject* c, PyObject* args, PyObject* kwds) {
   Py_DECREF(r);
   c->fd = fd;  // owned from here on
   c->closed = 0;
+  if (c->ssl) {
+    c->tls_state = 1;
+    if (tls_handshake(c) < 0) return -1;  // ClientHello goes out now
+  }
   return 0;
 }
+
+PyObject* on_readable_tls(NetConnObject* c, char* buf);
 
 PyObject* nc_on_readable(NetConnObject* c, PyObject*) {
   if (c->fd < 0) Py_RETURN_NONE;
   char* buf = read_buf();
   if (!buf) return PyErr_NoMemory();
+  if (c->ssl) return on_readable_tls(c, buf);
   ssize_t n;
   do {
     n = ::recv(c->fd, buf, kReadSize, 0);
@@ -467,8 +616,73 @@ PyObject* nc_on_readable(NetConnObject* c, PyObject*) {
   Py_RETURN_NONE;
 }
 
+// TLS: records are decrypted until OpenSSL wants more bytes; each plaintext chunk goes to the
+// parser as on the plain path (a completed reply resumes its handler right here).
+PyObject* on_readable_tls(NetConnObject* c, char* buf) {
+  if (c->tls_state == 1) {
+    if (tls_handshake(c) < 0) return nullptr;
+    Py_RETURN_NONE;
+  }
+  Py_INCREF(c);  // a resumed handler may drop the last other reference
+  if (c->write_wants_read) {
+    c->write_wants_read = 0;
+    if (send_out(c) < 0) {
+      Py_DECREF(c);
+      return nullptr;
+    }
+  }
+  while (c->ssl && c->fd >= 0) {
+    ERR_clear_error();
+    int n = SSL_read(c->ssl, buf, int(kReadSize));
+    if (n > 0) {
+      c->bytes_in += uint64_t(n);
+      ++c->recvs;
+      PyObject* mv = PyMemoryView_FromMemory(buf, Py_ssize_t(n), PyBUF_READ);
+      if (!mv) {
+        Py_DECREF(c);
+        return nullptr;
+      }
+      if (c->kind == K_H1) {
+        on_h1_data(c, mv);
+      } else {
+        on_pg_data(c, mv);
+      }
+      Py_DECREF(mv);
+      // nothing buffered in OpenSSL: stop without the recv(2) that would only say EAGAIN (the
+      // loop's level-triggered poll comes back if the kernel holds more)
+      if (c->ssl && !SSL_has_pending(c->ssl)) break;
+      continue;
+    }
+    int e = SSL_get_error(c->ssl, n);
+    if (e == SSL_ERROR_WANT_READ) break;
+    if (e == SSL_ERROR_WANT_WRITE) {
+      if (watch_writes(c) < 0) {
+        Py_DECREF(c);
+        return nullptr;
+      }
+      break;
+    }
+    int err = 0;  // close_notify, or EOF without it: the peer closed
+    if (e == SSL_ERROR_SYSCALL) {
+      err = errno;
+    } else if (e == SSL_ERROR_SSL) {
+      unsigned long le = ERR_peek_last_error();
+      if (ERR_GET_REASON(le) != SSL_R_UNEXPECTED_EOF_WHILE_READING) err = EPROTO;
+    }
+    ERR_clear_error();
+    lost(c, err);
+    break;
+  }
+  Py_DECREF(c);
+  Py_RETURN_NONE;
+}
+
 PyObject* nc_on_writable(NetConnObject* c, PyObject*) {
   if (c->fd < 0) Py_RETURN_NONE;
+  if (c->ssl && c->tls_state == 1) {
+    if (tls_handshake(c) < 0) return nullptr;
+    Py_RETURN_NONE;
+  }
   if (send_out(c) < 0) return nullptr;
   Py_RETURN_NONE;
 }
@@ -615,15 +829,23 @@ PyObject* nc_take_waiter(NetConnObject* c, PyObject*) {
 
 PyObject* nc_close(NetConnObject* c, PyObject*) {
   c->flush_scheduled = 0;
-  if (c->fd >= 0 && !c->out->empty() && !c->writing) {  // best effort: what is queued goes out
+  if (c->ssl) {  // best effort: queued records, then close_notify
+    if (c->tls_state == 2) {
+      if (!c->out->empty() && !c->writing) SSL_write(c->ssl, c->out->data(), int(c->out->size()));
+      SSL_shutdown(c->ssl);
+    }
+    ERR_clear_error();
+  } else if (c->fd >= 0 && !c->out->empty() && !c->writing) {  // best effort: what is queued goes out
     ::send(c->fd, c->out->data(), c->out->size(), MSG_NOSIGNAL | MSG_DONTWAIT);
   }
   shut(c);
+  hs_fail(c, nullptr);
   Py_RETURN_NONE;
 }
 
 PyObject* nc_abort(NetConnObject* c, PyObject*) {
   shut(c);
+  hs_fail(c, nullptr);
   Py_RETURN_NONE;
 }
 
@@ -632,6 +854,16 @@ PyObject* nc_get_fd(NetConnObject* c, void*) { return PyLong_FromLong(c->fd); }
 PyObject* nc_get_pending(NetConnObject* c, void*) { return PyLong_FromSize_t(c->pending->size()); }
 PyObject* nc_get_buffered(NetConnObject* c, void*) { return PyLong_FromSize_t(c->out->size()); }
 PyObject* nc_get_waiting(NetConnObject* c, void*) { return PyBool_FromLong(c->waiter != nullptr); }
+PyObject* nc_get_handshake(NetConnObject* c, void*) {
+  if (!c->hs_fut) Py_RETURN_NONE;
+  Py_INCREF(c->hs_fut);
+  return c->hs_fut;
+}
+PyObject* nc_get_tls(NetConnObject* c, void*) {
+  if (c->tls_state == 0) Py_RETURN_NONE;
+  if (c->tls_state == 1 || !c->ssl) Py_RETURN_FALSE;
+  return PyUnicode_FromString(SSL_get_version(c->ssl));
+}
 PyObject* nc_get_stats(NetConnObject* c, void*) {
   return Py_BuildValue("{s:K,s:K,s:K,s:K}", "bytes_in", c->bytes_in, "bytes_out", c->bytes_out, "recvs", c->recvs,
                        "sends", c->sends);
@@ -659,6 +891,10 @@ PyGetSetDef nc_getset[] = {
     {"buffered", reinterpret_cast<getter>(nc_get_buffered), nullptr, "bytes not yet taken by the kernel", nullptr},
     {"waiting", reinterpret_cast<getter>(nc_get_waiting), nullptr, "h1: a reply is awaited", nullptr},
     {"stats", reinterpret_cast<getter>(nc_get_stats), nullptr, "bytes / syscall counters", nullptr},
+    {"handshake", reinterpret_cast<getter>(nc_get_handshake), nullptr, "TLS: the handshake future (None: plain TCP)",
+     nullptr},
+    {"tls", reinterpret_cast<getter>(nc_get_tls), nullptr,
+     "None (plain TCP), False (handshaking) or the negotiated protocol ('TLSv1.3')", nullptr},
     {nullptr, nullptr, nullptr, nullptr, nullptr}};
 
 }  // namespace

@@ -1,0 +1,227 @@
+// TlsContext: the client-side OpenSSL context of the native HTTPS path.
+//
+// The production sinks are HTTPS (api.trello.com, api.telegram.org; index.js:53,83,99). With
+// asyncio's SSL transport every request and reply also crosses asyncio's pure-Python
+// SSLProtocol (memory BIOs, several Python frames per record), which costs more CPU than the
+// whole plain-TCP request path. A TLS NetConn (py_netconn.cpp) runs the handshake and the
+// record layer on the socket with OpenSSL directly.
+//
+// The context mirrors what `ssl.create_default_context(cafile=...)` sets up for a client:
+// TLS 1.2 minimum, peer verification against `cafile` / `capath` or OpenSSL's default
+// verify paths (which honour SSL_CERT_FILE / SSL_CERT_DIR like Python's), the same cipher
+// string, no compression, hostname (or IP address) checked against the certificate, SNI sent
+// for names (not for IP literals). Only H1Client's own contexts (default or built from its
+// `ssl_cafile`) are mirrored: a caller-supplied ssl.SSLContext keeps the asyncio TLS path.
+//
+// Client sessions are cached per "host:port" (the last ticket each origin gave us), so a
+// reconnect after the server closed an idle keep-alive connection resumes instead of running
+// a full handshake.
+#include <arpa/inet.h>
+#include <openssl/err.h>
+#include <openssl/ssl.h>
+#include <openssl/x509v3.h>
+
+#include <map>
+#include <string>
+
+#include "py_common.hpp"
+
+namespace beholder {
+
+namespace {
+
+// Python 3.10's default cipher string for ssl.create_default_context (Lib/ssl.py / _ssl.c)
+constexpr const char* kCiphers = "@SECLEVEL=2:ECDH+AESGCM:ECDH+CHACHA20:ECDH+AES:DHE+AES:!aNULL:!eNULL:!aDSS:!SHA1:!AESCCM";
+
+struct TlsContextObject {
+  PyObject_HEAD SSL_CTX* ctx;
+  std::map<std::string, SSL_SESSION*>* sessions;  // "host:port" -> last session (one ref each)
+  uint64_t handshakes, resumed;
+};
+
+PyTypeObject TlsContextType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+int g_ex_index = -1;  // SSL ex_data: the TlsContextObject* of an SSL
+int g_key_index = -1;  // SSL ex_data: std::string* session-cache key
+
+std::string last_error_text() {
+  unsigned long e = ERR_peek_last_error();
+  char buf[256];
+  ERR_error_string_n(e, buf, sizeof buf);
+  return buf;
+}
+
+// new-session callback: keep the newest session of each origin (TLS 1.3 tickets arrive after
+// the handshake, in the first reads)
+int on_new_session(SSL* ssl, SSL_SESSION* sess) {
+  auto* self = static_cast<TlsContextObject*>(SSL_get_ex_data(ssl, g_ex_index));
+  auto* key = static_cast<std::string*>(SSL_get_ex_data(ssl, g_key_index));
+  if (!self || !key || !self->sessions) return 0;
+  auto it = self->sessions->find(*key);
+  if (it != self->sessions->end()) {
+    SSL_SESSION_free(it->second);
+    it->second = sess;
+  } else {
+    if (self->sessions->size() >= 1024) {  // bounded: forget everything, rebuild on demand
+      for (auto& kv : *self->sessions) SSL_SESSION_free(kv.second);
+      self->sessions->clear();
+    }
+    self->sessions->emplace(*key, sess);
+  }
+  return 1;  // we hold the reference
+}
+
+void free_key(void*, void* ptr, CRYPTO_EX_DATA*, int, long, void*) { delete static_cast<std::string*>(ptr); }
+
+PyObject* tc_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
+  static const char* kwlist[] = {"cafile", "capath", "verify", nullptr};
+  const char* cafile = nullptr;
+  const char* capath = nullptr;
+  int verify = 1;
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "|zzp", const_cast<char**>(kwlist), &cafile, &capath, &verify))
+    return nullptr;
+  TlsContextObject* s = reinterpret_cast<TlsContextObject*>(type->tp_alloc(type, 0));
+  if (!s) return nullptr;
+  s->ctx = nullptr;
+  s->sessions = new (std::nothrow) std::map<std::string, SSL_SESSION*>();
+  if (!s->sessions) {
+    Py_DECREF(s);
+    return PyErr_NoMemory();
+  }
+  ERR_clear_error();
+  SSL_CTX* ctx = SSL_CTX_new(TLS_client_method());
+  if (!ctx) {
+    Py_DECREF(s);
+    PyErr_Format(PyExc_RuntimeError, "SSL_CTX_new: %s", last_error_text().c_str());
+    return nullptr;
+  }
+  s->ctx = ctx;
+  SSL_CTX_set_min_proto_version(ctx, TLS1_2_VERSION);
+  SSL_CTX_set_options(ctx, SSL_OP_NO_COMPRESSION);
+  SSL_CTX_set_mode(ctx, SSL_MODE_ENABLE_PARTIAL_WRITE | SSL_MODE_ACCEPT_MOVING_WRITE_BUFFER);
+  SSL_CTX_set_read_ahead(ctx, 1);  // one recv(2) takes every record the kernel holds, not header + body
+  if (SSL_CTX_set_cipher_list(ctx, kCiphers) != 1) {
+    Py_DECREF(s);
+    PyErr_Format(PyExc_RuntimeError, "SSL_CTX_set_cipher_list: %s", last_error_text().c_str());
+    return nullptr;
+  }
+  if (verify) {
+    SSL_CTX_set_verify(ctx, SSL_VERIFY_PEER, nullptr);
+    int ok = (cafile || capath) ? SSL_CTX_load_verify_locations(ctx, cafile, capath)
+                                : SSL_CTX_set_default_verify_paths(ctx);
+    if (ok != 1) {
+      Py_DECREF(s);
+      PyErr_Format(PyExc_FileNotFoundError, "cannot load verify locations (%s): %s", cafile ? cafile : "default",
+                   last_error_text().c_str());
+      return nullptr;
+    }
+  } else {
+    SSL_CTX_set_verify(ctx, SSL_VERIFY_NONE, nullptr);
+  }
+  SSL_CTX_set_session_cache_mode(ctx, SSL_SESS_CACHE_CLIENT | SSL_SESS_CACHE_NO_INTERNAL_STORE);
+  SSL_CTX_sess_set_new_cb(ctx, on_new_session);
+  return reinterpret_cast<PyObject*>(s);
+}
+
+void tc_dealloc(TlsContextObject* s) {
+  if (s->sessions) {
+    for (auto& kv : *s->sessions) SSL_SESSION_free(kv.second);
+    delete s->sessions;
+  }
+  if (s->ctx) SSL_CTX_free(s->ctx);
+  Py_TYPE(s)->tp_free(reinterpret_cast<PyObject*>(s));
+}
+
+PyObject* tc_get_stats(TlsContextObject* s, void*) {
+  return Py_BuildValue("{s:K,s:K,s:n}", "handshakes", static_cast<unsigned long long>(s->handshakes), "resumed",
+                       static_cast<unsigned long long>(s->resumed), "cached_sessions",
+                       static_cast<Py_ssize_t>(s->sessions->size()));
+}
+
+PyGetSetDef tc_getset[] = {
+    {"stats", reinterpret_cast<getter>(tc_get_stats), nullptr, "handshakes, resumed, cached_sessions", nullptr},
+    {nullptr, nullptr, nullptr, nullptr, nullptr}};
+
+}  // namespace
+
+bool is_tls_context(PyObject* o) { return Py_TYPE(o) == &TlsContextType; }
+
+// A client SSL on connected socket `fd` for `host` (a name or an IP literal) and `port`:
+// verification target, SNI, a cached session of that origin. NULL with a Python error set.
+SSL* tls_new_ssl(PyObject* ctx_obj, int fd, const char* host, int port) {
+  TlsContextObject* tc = reinterpret_cast<TlsContextObject*>(ctx_obj);
+  ERR_clear_error();
+  SSL* ssl = SSL_new(tc->ctx);
+  if (!ssl) {
+    PyErr_Format(PyExc_RuntimeError, "SSL_new: %s", last_error_text().c_str());
+    return nullptr;
+  }
+  unsigned char addr[16];
+  bool is_ip = inet_pton(AF_INET, host, addr) == 1 || inet_pton(AF_INET6, host, addr) == 1;
+  bool ok = SSL_set_fd(ssl, fd) == 1;
+  if (ok && is_ip) {
+    ok = X509_VERIFY_PARAM_set1_ip_asc(SSL_get0_param(ssl), host) == 1;
+  } else if (ok) {
+    ok = SSL_set_tlsext_host_name(ssl, host) == 1 && SSL_set1_host(ssl, host) == 1;
+  }
+  std::string* key = ok ? new (std::nothrow) std::string(std::string(host) + ":" + std::to_string(port)) : nullptr;
+  if (!key || SSL_set_ex_data(ssl, g_ex_index, tc) != 1 || SSL_set_ex_data(ssl, g_key_index, key) != 1) {
+    if (key && SSL_get_ex_data(ssl, g_key_index) != key) delete key;
+    SSL_free(ssl);
+    PyErr_Format(PyExc_RuntimeError, "TLS setup for %s: %s", host, last_error_text().c_str());
+    return nullptr;
+  }
+  auto it = tc->sessions->find(*key);
+  if (it != tc->sessions->end()) SSL_set_session(ssl, it->second);
+  SSL_set_connect_state(ssl);
+  return ssl;
+}
+
+// Handshake finished on `ssl`: count it (resumed or full).
+void tls_count_handshake(SSL* ssl) {
+  auto* tc = static_cast<TlsContextObject*>(SSL_get_ex_data(ssl, g_ex_index));
+  if (!tc) return;
+  ++tc->handshakes;
+  if (SSL_session_reused(ssl)) ++tc->resumed;
+}
+
+// Description of a failed handshake, Python-ssl style: reason ("CERTIFICATE_VERIFY_FAILED",
+// "WRONG_VERSION_NUMBER", ...), message ("[SSL: REASON] text"), verify = certificate problem.
+void tls_describe_failure(SSL* ssl, std::string& reason, std::string& message, bool& verify) {
+  long vr = SSL_get_verify_result(ssl);
+  verify = vr != X509_V_OK;
+  if (verify) {
+    reason = "CERTIFICATE_VERIFY_FAILED";
+    message = std::string("[SSL: CERTIFICATE_VERIFY_FAILED] certificate verify failed: ") +
+              X509_verify_cert_error_string(vr);
+    return;
+  }
+  unsigned long e = ERR_peek_last_error();
+  const char* r = e ? ERR_reason_error_string(e) : nullptr;
+  std::string text = r ? r : "unexpected eof while reading";
+  reason.clear();
+  for (char ch : text) reason += ch == ' ' ? '_' : char(ch >= 'a' && ch <= 'z' ? ch - 32 : ch);
+  message = "[SSL: " + reason + "] " + text;
+}
+
+int init_tls_types(PyObject* m) {
+  g_ex_index = SSL_get_ex_new_index(0, nullptr, nullptr, nullptr, nullptr);
+  g_key_index = SSL_get_ex_new_index(0, nullptr, nullptr, nullptr, free_key);
+  if (g_ex_index < 0 || g_key_index < 0) {
+    PyErr_SetString(PyExc_RuntimeError, "SSL_get_ex_new_index failed");
+    return -1;
+  }
+  TlsContextType.tp_name = "beholder_amd.ops._native.TlsContext";
+  TlsContextType.tp_basicsize = sizeof(TlsContextObject);
+  TlsContextType.tp_flags = Py_TPFLAGS_DEFAULT;
+  TlsContextType.tp_doc =
+      "TlsContext(cafile=None, capath=None, verify=True): OpenSSL client context for TLS NetConns "
+      "(ssl.create_default_context semantics)";
+  TlsContextType.tp_new = tc_new;
+  TlsContextType.tp_dealloc = reinterpret_cast<destructor>(tc_dealloc);
+  TlsContextType.tp_getset = tc_getset;
+  if (PyType_Ready(&TlsContextType) < 0) return -1;
+  Py_INCREF(&TlsContextType);
+  return PyModule_AddObject(m, "TlsContext", reinterpret_cast<PyObject*>(&TlsContextType));
+}
+
+}  // namespace beholder

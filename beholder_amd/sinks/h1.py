@@ -69,7 +69,7 @@ class _Conn(asyncio.Protocol):
     the methods below only see its rare paths (``_net_lost``, ``_net_error``)."""
 
     __slots__ = ("origin", "parser", "transport", "waiter", "closed", "last_used", "uses", "deadline", "what",
-                 "net")
+                 "net", "adopt_plan", "adopt_error")
 
     def __init__(self, origin: "_Origin"):
         self.origin = origin
@@ -82,10 +82,24 @@ class _Conn(asyncio.Protocol):
         self.uses = 0
         self.deadline = 0.0
         self.what = ("", "")
+        self.adopt_plan = None  # True (plain TCP) or (TlsContext, host, port): adopt in connection_made
+        self.adopt_error: Optional[BaseException] = None
 
     # -- protocol callbacks --------------------------------------------------
     def connection_made(self, transport):
         self.transport = transport
+        plan = self.adopt_plan
+        if plan is not None:  # before asyncio starts reading: no byte can reach the asyncio transport
+            self.adopt_plan = None
+            loop = asyncio.get_running_loop()
+            try:
+                if plan is True:
+                    self.adopt(loop)
+                else:
+                    self.adopt_tls(loop, *plan)
+            except BaseException as e:  # re-raised by H1Client._connect
+                self.adopt_error = e
+                self.abort()
 
     def data_received(self, data):
         try:
@@ -162,6 +176,21 @@ class _Conn(asyncio.Protocol):
         self.transport = None
         return True
 
+    def adopt_tls(self, loop, ctx, host: str, port: int) -> bool:
+        """Hand a connected plain-TCP socket to a NetConn that runs TLS natively (ops TlsContext
+        ``ctx``); ``self.net.handshake`` completes when the session is established."""
+        fd = netconn.adopt(self.transport)
+        if fd is None:
+            return False
+        try:
+            self.net = netconn.NetConn(fd, loop, "h1", self, self.parser, tls=ctx, server_hostname=host, port=port,
+                                       tls_error=_tls_error)
+        except BaseException:
+            os.close(fd)
+            raise
+        self.transport = None
+        return True
+
     def timed_out(self) -> None:
         m, url = self.what
         self._fail(HttpError(f"ETIMEDOUT: {m} {redact(url)}"))
@@ -210,13 +239,18 @@ class H1Client(HttpClient):
 
     def __init__(self, timeout_s: float = 30.0, user_agent: str = "beholder/1.0", max_per_host: int = 100,
                  keepalive_s: float = 4.0, ssl_context: Optional[_ssl.SSLContext] = None,
-                 max_redirects: int = 10):
+                 max_redirects: int = 10, ssl_cafile: Optional[str] = None):
         self.timeout_s = float(timeout_s)
         self.user_agent = user_agent
         self.max_per_host = max(1, int(max_per_host))
         self.keepalive_s = float(keepalive_s)
         self.max_redirects = int(max_redirects)
+        self._own_ssl = ssl_context is None  # our own context: the native TLS path can mirror it
+        if ssl_context is None and ssl_cafile:
+            ssl_context = _ssl.create_default_context(cafile=ssl_cafile)
         self._ssl = ssl_context
+        self.ssl_cafile = ssl_cafile
+        self._ntls = None
         self._origins: Dict[str, _Origin] = {}
         self._routes: Dict[str, Tuple[_Origin, str, str]] = {}
         self._closed = False
@@ -259,6 +293,18 @@ class H1Client(HttpClient):
         self._origins[key] = o
         return o
 
+    def _native_tls(self):
+        """The native TLS context (ops TlsContext) mirroring this client's own SSL context: the
+        default one or the one built from ``ssl_cafile``. None for a caller-supplied
+        ``ssl_context`` (its settings cannot be mirrored) or with native connections off."""
+        t = self._ntls
+        if t is None:
+            t = False
+            if self._own_ssl and netconn.enabled() and os.environ.get("BEHOLDER_NATIVE_TLS", "1") != "0":
+                t = _native.TlsContext(cafile=self.ssl_cafile)
+            self._ntls = t
+        return t or None
+
     def _ssl_context(self) -> _ssl.SSLContext:
         if self._ssl is None:
             self._ssl = _ssl.create_default_context()
@@ -272,11 +318,21 @@ class H1Client(HttpClient):
             remaining = deadline - loop.time()
             if remaining <= 0:
                 raise asyncio.TimeoutError
-            kw = {"ssl": self._ssl_context(), "server_hostname": o.host} if o.tls else {}
+            ntls = self._native_tls() if o.tls else None
+            kw = {"ssl": self._ssl_context(), "server_hostname": o.host} if o.tls and ntls is None else {}
+            if ntls is not None:  # TLS in C on the socket (ops/csrc/py_tls.cpp)
+                conn.adopt_plan = (ntls, o.host, o.port)
+            elif not o.tls:
+                conn.adopt_plan = True
             await asyncio.wait_for(loop.create_connection(lambda: conn, o.host, o.port, **kw), remaining)
-            if not o.tls:
-                conn.adopt(loop)
+            if conn.adopt_error is not None:
+                raise conn.adopt_error
+            if ntls is not None:
+                if conn.net is None:
+                    raise HttpError(f"cannot start TLS to {o.host}:{o.port}")
+                await asyncio.wait_for(conn.net.handshake, max(deadline - loop.time(), 0.0))
         except BaseException:
+            conn.abort()
             o.open -= 1
             self._wake(o)
             raise
@@ -548,6 +604,15 @@ def _connect_error(e: OSError, o: "_Origin") -> str:
         return f"getaddrinfo ENOTFOUND {o.host}"
     name = errno.errorcode.get(e.errno or 0) if e.errno else None
     return f"connect {name or type(e).__name__} {o.host}:{o.port}"
+
+
+def _tls_error(reason: str, message: str, verify: bool) -> _ssl.SSLError:
+    """A failed native TLS handshake as the ``ssl`` module would raise it (``reason`` is what
+    :func:`_connect_error` reports, as for the asyncio TLS path)."""
+    e = (_ssl.SSLCertVerificationError if verify else _ssl.SSLError)(1, message)
+    e.reason = reason
+    e.library = "SSL"
+    return e
 
 
 def _h1_python_only(client, method, url, params, timeout):

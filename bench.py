@@ -30,6 +30,7 @@ region):
 * ``overload_*``: BASELINE config 4, unpaced into a 4096-event ring with ``drop_newest``.
 * ``tcp_e2e_*`` / ``http_tcp_h1_*``: the production-shaped path, every dependency over TCP (an
   AMQP replay broker, a Postgres fake and HTTP fakes in their own processes).
+* ``tls_e2e_*``: the same with HTTPS sinks, as Trello and Telegram are in production.
 
 Order of the phases: everything that starts child processes (the TCP fakes, the all-process
 consumers) runs before the headline phase, whose ``torch.cuda.synchronize()`` is the first HIP
@@ -315,6 +316,12 @@ def io_extras(a) -> dict:
                 "tcp_e2e_p50_handle_latency_us": _r(hl.get("p50")),
                 "tcp_e2e_p999_handle_latency_us": _r(hl.get("p999")),
                 "tcp_e2e_errors": e2e.get("errors")})
+    tls = harness._tcp_e2e(a.io_events, http_servers=4, tls=True)
+    hl = tls.get("handle_latency_us", {})
+    out.update({"tls_e2e_events_per_sec": _r(tls.get("ingest_rate_eps"), 1),
+                "tls_e2e_cpu_us_per_event": _r(tls.get("cpu_us_per_event")),
+                "tls_e2e_p999_handle_latency_us": _r(hl.get("p999")),
+                "tls_e2e_errors": tls.get("errors")})
     h = harness._http_tcp(Workload(n_media=10000, seed=a.seed), a.io_events, clients=("h1",))["h1"]
     hl = h["handle_latency_us"]
     out.update({"http_tcp_h1_events_per_sec": _r(h["ingest_rate_eps"], 1),
@@ -427,7 +434,7 @@ def main(argv=None) -> int:
             **extras,
             "notes": "CPU event-consumer workload (the reference has no device compute; see docs/DESIGN.md). "
                      "value = one consumer process per rank; all_procs_* = every CPU of the share busy; "
-                     "rate_10k/overload/soak = BASELINE configs 3-5; tcp_e2e/http_tcp = every dependency over TCP",
+                     "rate_10k/overload/soak = BASELINE configs 3-5; tcp_e2e/http_tcp = every dependency over TCP, tls_e2e = same with HTTPS sinks",
         }
         print(json.dumps(out), flush=True)
     dist.close()

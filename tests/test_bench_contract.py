@@ -12,7 +12,8 @@ REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step
             "vs_baseline", "dtype", "data", "config"}
 EXTRAS = {"all_procs_events_per_sec", "rate_10k_p50_ingest_latency_us", "rate_10k_p99_ingest_latency_us",
           "soak_rss_growth_mb", "soak_gc_max_pause_us", "overload_dropped", "tcp_e2e_events_per_sec",
-          "http_tcp_h1_p999_handle_latency_us", "p50_handle_latency_us"}
+          "http_tcp_h1_p999_handle_latency_us", "p50_handle_latency_us", "tls_e2e_events_per_sec",
+          "tls_e2e_cpu_us_per_event"}
 SMALL = ["--steps", "2", "--warmup", "1", "--events-per-step", "4096", "--media", "500"]
 
 
@@ -37,6 +38,7 @@ def test_bench_single_rank_contract():
     assert out["value"] == pytest.approx(4096 * 2 / (out["ms_per_step"] * 2 / 1000), rel=0.01)
     assert out["all_procs_per_rank"] == 2 and out["all_procs_events_per_sec"] > 0
     assert out["rate_10k_acked"] == 10000 and out["soak_events"] == 20000 and out["tcp_e2e_errors"] == 0
+    assert out["tls_e2e_errors"] == 0
     assert out["overload_accepted"] + out["overload_dropped"] == out["overload_offered"]
 
 

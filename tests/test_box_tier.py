@@ -133,6 +133,16 @@ def test_tcp_e2e_every_dependency_over_tcp():
     assert res["server_side"]["requests"] == res["http"]["requests"] and res["http"]["errors"] == 0
 
 
+def test_tls_e2e_https_sinks_on_native_tls():
+    """Production shape with HTTPS sinks (Trello / Telegram are HTTPS): every request on a
+    native TLS connection (ops TlsContext), certificates verified, every event acked."""
+    from beholder_amd.bench import harness
+    res = harness.run_config("tls_e2e", events=50_000)
+    assert res["tls"] is True and res["acked"] == 50_000 and res["errors"] == 0, res
+    assert res["server_side"]["requests"] == res["http"]["requests"] and res["http"]["errors"] == 0
+    assert res["http"]["connections"] <= 100  # keep-alive: no reconnect churn
+
+
 def test_http_tcp_both_clients_error_free():
     """Sinks over real TCP with the default keep-alive client and with aiohttp: every event
     acked, no handler errors (aiohttp under the native Driver needs its own task)."""

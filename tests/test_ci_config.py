@@ -44,3 +44,13 @@ def test_dockerfile_builds_without_rocm():
     assert "FROM python:3.10-slim" in text
     build = [ln for ln in text.splitlines() if "beholder_amd.ops.build" in ln]
     assert build and "--hip " not in build[0] + " "  # the HIP extra is never required in the image
+
+
+def test_dockerfile_has_the_native_build_dependencies():
+    """The native runtime links OpenSSL (ops/csrc/py_tls.cpp): the slim image needs its headers;
+    the CI image (python:3.10, buildpack-deps) ships them."""
+    from beholder_amd import _build
+    text = open(os.path.join(ROOT, "Dockerfile")).read()
+    apt = [ln for ln in text.splitlines() if "apt-get install" in ln]
+    assert apt and "g++" in apt[0] and "libssl-dev" in apt[0]
+    assert "-lssl" in _build.LIBS and "-lcrypto" in _build.LIBS

@@ -1,0 +1,227 @@
+"""Native TLS for the HTTPS sinks (`ops/csrc/py_tls.cpp` TlsContext, the TLS mode of
+`ops/csrc/py_netconn.cpp` NetConn, `sinks/h1.py` `_connect`). Trello and Telegram are HTTPS in
+production (index.js:53,83,99); with H1Client's own SSL context (the default one or
+``ssl_cafile``) the handshake and the record layer run in C on the socket. Every behaviour is
+checked against the asyncio TLS path (``BEHOLDER_NATIVE_TLS=0``)."""
+import asyncio
+import os
+import shutil
+import ssl
+import subprocess
+
+import pytest
+
+from beholder_amd.bench.http_sink_server import TLS_CERT, server_ssl_context
+from beholder_amd.sinks import H1Client, HttpError
+
+
+def run(coro):
+    return asyncio.run(asyncio.wait_for(coro, 30))
+
+
+class TlsServer:
+    """HTTPS keep-alive server; ``respond(target) -> bytes | None`` (None: close the connection
+    cleanly after reading the request); "hang" never answers."""
+
+    def __init__(self, respond, ctx=None, handshake=True):
+        self.respond = respond
+        self.ctx = ctx or server_ssl_context()
+        self.handshake = handshake
+        self.connections = 0
+        self.requests = []
+
+    async def start(self):
+        self.server = await asyncio.start_server(self._serve, "127.0.0.1", 0,
+                                                 ssl=self.ctx if self.handshake else None)
+        self.port = self.server.sockets[0].getsockname()[1]
+        return self
+
+    async def stop(self):
+        self.server.close()
+        await self.server.wait_closed()
+
+    async def _serve(self, r, w):
+        self.connections += 1
+        try:
+            if not self.handshake:  # accept TCP, never answer the ClientHello
+                await asyncio.sleep(3600)
+            while True:
+                try:
+                    head = await r.readuntil(b"\r\n\r\n")
+                except (asyncio.IncompleteReadError, ConnectionError, ssl.SSLError):
+                    return
+                self.requests.append(head)
+                out = self.respond(head.split(b" ", 2)[1].decode())
+                if out == "hang":
+                    await asyncio.sleep(3600)
+                if out is None:
+                    return
+                w.write(out)
+                await w.drain()
+        finally:
+            w.close()
+
+
+def ok(body=b"{}"):
+    return b"HTTP/1.1 200 OK\r\nContent-Length: %d\r\n\r\n" % len(body) + body
+
+
+def native_tls(c):
+    return [conn.net.tls for o in c._origins.values() for conn in o.idle if conn.net is not None]
+
+
+def test_native_tls_requests_take_the_fast_path():
+    async def go():
+        s = await TlsServer(lambda t: ok()).start()
+        c = H1Client(timeout_s=5, ssl_cafile=TLS_CERT)
+        url = f"https://127.0.0.1:{s.port}/1/cards/abc/actions/comments"
+        first = await c.request("POST", url, params={"text": "hi ü", "key": "k"})
+        aw = c.request("POST", url, params={"text": "again"})
+        kind = type(aw).__name__
+        second = await aw
+        tls = native_tls(c)
+        st = dict(c.counts)
+        await c.close()
+        await s.stop()
+        return first.status, second.status, kind, tls, st, s.connections, s.requests[0].split(b"\r\n")[0]
+    a, b, kind, tls, st, conns, line = run(go())
+    assert (a, b, kind, conns) == (200, 200, "H1Call", 1)
+    assert tls == ["TLSv1.3"] and st["reused"] == 1
+    assert line == b"POST /1/cards/abc/actions/comments?text=hi%20%C3%BC&key=k HTTP/1.1"
+
+
+def _both(fn):
+    """fn(native: bool) run with the native TLS path and with asyncio's; returns both results."""
+    out = {}
+    for native in (True, False):
+        old = os.environ.get("BEHOLDER_NATIVE_TLS")
+        os.environ["BEHOLDER_NATIVE_TLS"] = "1" if native else "0"
+        try:
+            out[native] = run(fn(native))
+        finally:
+            if old is None:
+                os.environ.pop("BEHOLDER_NATIVE_TLS", None)
+            else:
+                os.environ["BEHOLDER_NATIVE_TLS"] = old
+    return out[True], out[False]
+
+
+def test_large_bodies_and_many_requests_match_asyncio_tls():
+    big = os.urandom(700_000).hex().encode()  # 1.4 MB: ~90 TLS records, many reads
+
+    async def go(native):
+        s = await TlsServer(lambda t: ok(big if t.startswith("/big") else t.encode())).start()
+        c = H1Client(timeout_s=10, ssl_cafile=TLS_CERT)
+        base = f"https://127.0.0.1:{s.port}"
+        rs = await asyncio.gather(*[c.request("GET", f"{base}/p{i}", params={"i": i}) for i in range(60)])
+        b = await c.request("GET", base + "/big")
+        kinds = native_tls(c)
+        await c.close()
+        await s.stop()
+        return [(r.status, r.body) for r in rs], b.body == big, bool(kinds) and all(kinds)
+    nat, py = _both(go)
+    assert nat[0] == py[0] and nat[1] and py[1]
+    assert nat[2] is True and py[2] is False  # native connections only with the native path
+
+
+def test_verification_failures_match_asyncio_tls(tmp_path):
+    if shutil.which("openssl") is None:
+        pytest.skip("needs openssl")
+    key, crt = tmp_path / "k.pem", tmp_path / "c.pem"
+    r = subprocess.run(["openssl", "req", "-x509", "-newkey", "ec", "-pkeyopt", "ec_paramgen_curve:prime256v1",
+                        "-nodes", "-keyout", str(key), "-out", str(crt), "-days", "1", "-subj", "/CN=other.example",
+                        "-addext", "subjectAltName=DNS:other.example"], capture_output=True)
+    assert r.returncode == 0, r.stderr
+    wrong_name = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+    wrong_name.load_cert_chain(str(crt), str(key))
+
+    async def go(native):
+        errs = []
+        for ctx, cafile in ((None, None), (wrong_name, str(crt))):
+            s = await TlsServer(lambda t: ok(), ctx=ctx).start()
+            c = H1Client(timeout_s=5, ssl_cafile=cafile)  # no cafile: default trust, self-signed refused
+            try:
+                await c.request("GET", f"https://127.0.0.1:{s.port}/x")
+                errs.append("no error")
+            except HttpError as e:
+                errs.append(str(e))
+            await c.close()
+            await s.stop()
+        return errs
+    nat, py = _both(go)
+    assert nat == py == ["CERTIFICATE_VERIFY_FAILED", "CERTIFICATE_VERIFY_FAILED"]
+
+
+def test_plain_http_server_and_handshake_timeout():
+    async def plain(native):
+        s = await TlsServer(lambda t: ok(), handshake=True).start()
+        s.server.close()
+        await s.server.wait_closed()
+        srv = await asyncio.start_server(lambda r, w: w.write(b"HTTP/1.1 400 Bad\r\n\r\n"), "127.0.0.1", 0)
+        port = srv.sockets[0].getsockname()[1]
+        c = H1Client(timeout_s=5, ssl_cafile=TLS_CERT)
+        try:
+            await c.request("GET", f"https://127.0.0.1:{port}/x")
+            err = "no error"
+        except HttpError as e:
+            err = str(e)
+        await c.close()
+        srv.close()
+        await srv.wait_closed()
+        return err
+    nat, py = _both(plain)
+    assert nat == py and nat in ("WRONG_VERSION_NUMBER", "RECORD_LAYER_FAILURE", "PACKET_LENGTH_TOO_LONG")
+
+    async def silent():
+        s = await TlsServer(lambda t: ok(), handshake=False).start()
+        c = H1Client(timeout_s=5, ssl_cafile=TLS_CERT)
+        with pytest.raises(HttpError, match=r"^ETIMEDOUT: GET https://127\.0\.0\.1:\d+/x$"):
+            await c.request("GET", f"https://127.0.0.1:{s.port}/x", timeout=0.3)
+        open_ = sum(o.open for o in c._origins.values())
+        await c.close()
+        s.server.close()
+        return open_
+    assert run(silent()) == 0
+
+
+def test_server_close_then_reconnect_resumes_the_session():
+    async def go():
+        n = {"i": 0}
+
+        def respond(t):
+            n["i"] += 1
+            return ok() if n["i"] % 2 else None  # every second request: the server closes instead
+        s = await TlsServer(respond).start()
+        c = H1Client(timeout_s=5, ssl_cafile=TLS_CERT)
+        url = f"https://127.0.0.1:{s.port}/x"
+        statuses = []
+        for _ in range(6):
+            statuses.append((await c.request("GET", url)).status)  # GET: retried on a fresh connection
+            await asyncio.sleep(0.01)
+        stats = c._native_tls().stats
+        st = dict(c.counts)
+        await c.close()
+        await s.stop()
+        return statuses, stats, st, s.connections
+    statuses, stats, st, conns = run(go())
+    assert statuses == [200] * 6 and st["retries"] >= 4
+    assert stats["handshakes"] == conns and stats["resumed"] >= conns - 2  # tickets reused on reconnect
+
+
+def test_tls12_server_and_caller_context_keeps_asyncio_path():
+    ctx12 = server_ssl_context()
+    ctx12.maximum_version = ssl.TLSVersion.TLSv1_2
+
+    async def go():
+        s = await TlsServer(lambda t: ok(), ctx=ctx12).start()
+        c = H1Client(timeout_s=5, ssl_cafile=TLS_CERT)
+        r = await c.request("GET", f"https://127.0.0.1:{s.port}/x")
+        tls = native_tls(c)
+        await c.close()
+        own = H1Client(timeout_s=5, ssl_context=ssl.create_default_context(cafile=TLS_CERT))
+        r2 = await own.request("GET", f"https://127.0.0.1:{s.port}/y")
+        own_native = native_tls(own)
+        await own.close()
+        await s.stop()
+        return r.status, tls, r2.status, own_native
+    assert run(go()) == (200, ["TLSv1.2"], 200, [])
