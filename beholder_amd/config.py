@@ -290,6 +290,9 @@ class Config:
             raise ConfigError("service.log.positional_args must be 'append' or 'drop'")
         if svc["http"].get("client", "h1") not in ("h1", "aiohttp"):
             raise ConfigError("service.http.client must be 'h1' or 'aiohttp'")
+        ca = svc["http"].get("ca_file")
+        if ca is not None and (not isinstance(ca, str) or not os.path.isfile(ca)):
+            raise ConfigError(f"service.http.ca_file: not a readable file: {ca!r}")
         from .store.schema import MediaSchema
         from .transport.amqp.topology import Topology
         try:

@@ -653,7 +653,18 @@ PyObject* h1_fast_impl(PyObject* client, PyObject* method, PyObject* url, PyObje
   if (!fut) return nullptr;
   Own own_fut{fut};
   bool head = mn == 4 && memcmp(m, "HEAD", 4) == 0;
-  if (netconn_h1_request(g.conn.get(conn, C_NET), req, fut, head) < 0) return nullptr;
+  if (netconn_h1_request(g.conn.get(conn, C_NET), req, fut, head) < 0) {
+    // the connection left the idle pool: give it back to the pool accounting (dropped), then raise
+    PyObject *et, *ev, *tb;
+    PyErr_Fetch(&et, &ev, &tb);
+    PyObject* r = PyObject_CallMethodObjArgs(client, s_release, conn, Py_False, nullptr);
+    if (!r)
+      PyErr_WriteUnraisable(client);
+    else
+      Py_DECREF(r);
+    PyErr_Restore(et, ev, tb);
+    return nullptr;
+  }
   if (PySet_Add(busy, conn) < 0) return nullptr;
   PyObject* sweeper = PyDict_GetItemWithError(d, s_sweeper);
   if (!sweeper && PyErr_Occurred()) return nullptr;

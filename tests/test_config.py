@@ -107,3 +107,17 @@ def test_kubernetes_example_config_loads(tmp_path):
     assert cfg.root.require("keys.trello").get("token") == "<trello token>"
     assert cfg.keys.emby.token == "<emby api key>" and cfg.flow_ids["deployed"] == "<list id>"
     assert cfg.data["service"]["prefetch"] == 100
+
+
+def test_http_ca_file_reaches_the_native_tls_context(tmp_path):
+    """service.http.ca_file: validated at load, handed to H1Client (ssl_cafile), mirrored by the
+    native TLS context (sinks/h1.py _native_tls)."""
+    from beholder_amd.bench.http_sink_server import TLS_CERT
+    from beholder_amd.service import make_http_client
+    base = {"keys": {"trello": {}}, "instance": {"flow_ids": {}}}
+    with pytest.raises(ConfigError, match="ca_file"):
+        Config.from_dict({**base, "service": {"http": {"ca_file": str(tmp_path / "missing.pem")}}})
+    cfg = Config.from_dict({**base, "service": {"http": {"ca_file": TLS_CERT}}})
+    c = make_http_client(cfg.data["service"]["http"])
+    assert c.ssl_cafile == TLS_CERT and c._native_tls() is not None
+    assert make_http_client({}).ssl_cafile is None
