@@ -503,8 +503,8 @@ int nc_init(NetConnObject* c, PyObject* args, PyObject* kwds) {
   if (!PyArg_ParseTupleAndKeywords(args, kwds, "iOsOO|OOOOziO", const_cast<char**>(kwlist), &fd, &loop, &kind, &owner,
                                    &parser, &stmts, &pg_error, &closed_exc, &tls, &host, &port, &tls_error))
     return -1;
-  if (tls != Py_None && (!is_tls_context(tls) || !host || strcmp(kind, "h1") != 0)) {
-    PyErr_SetString(PyExc_TypeError, "tls needs a TlsContext, server_hostname and kind 'h1'");
+  if (tls != Py_None && (!is_tls_context(tls) || !host)) {
+    PyErr_SetString(PyExc_TypeError, "tls needs a TlsContext and server_hostname");
     return -1;
   }
   if (!PyExceptionClass_Check(closed_exc)) {

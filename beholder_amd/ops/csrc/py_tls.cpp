@@ -37,6 +37,7 @@ struct TlsContextObject {
   PyObject_HEAD SSL_CTX* ctx;
   std::map<std::string, SSL_SESSION*>* sessions;  // "host:port" -> last session (one ref each)
   uint64_t handshakes, resumed;
+  bool check_hostname;  // the certificate must name the host (verify-full / HTTPS)
 };
 
 PyTypeObject TlsContextType = {PyVarObject_HEAD_INIT(nullptr, 0)};
@@ -73,15 +74,17 @@ int on_new_session(SSL* ssl, SSL_SESSION* sess) {
 void free_key(void*, void* ptr, CRYPTO_EX_DATA*, int, long, void*) { delete static_cast<std::string*>(ptr); }
 
 PyObject* tc_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
-  static const char* kwlist[] = {"cafile", "capath", "verify", nullptr};
+  static const char* kwlist[] = {"cafile", "capath", "verify", "check_hostname", nullptr};
   const char* cafile = nullptr;
   const char* capath = nullptr;
-  int verify = 1;
-  if (!PyArg_ParseTupleAndKeywords(args, kwds, "|zzp", const_cast<char**>(kwlist), &cafile, &capath, &verify))
+  int verify = 1, check_hostname = 1;
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "|zzpp", const_cast<char**>(kwlist), &cafile, &capath, &verify,
+                                   &check_hostname))
     return nullptr;
   TlsContextObject* s = reinterpret_cast<TlsContextObject*>(type->tp_alloc(type, 0));
   if (!s) return nullptr;
   s->ctx = nullptr;
+  s->check_hostname = verify && check_hostname;
   s->sessions = new (std::nothrow) std::map<std::string, SSL_SESSION*>();
   if (!s->sessions) {
     Py_DECREF(s);
@@ -158,11 +161,9 @@ SSL* tls_new_ssl(PyObject* ctx_obj, int fd, const char* host, int port) {
   unsigned char addr[16];
   bool is_ip = inet_pton(AF_INET, host, addr) == 1 || inet_pton(AF_INET6, host, addr) == 1;
   bool ok = SSL_set_fd(ssl, fd) == 1;
-  if (ok && is_ip) {
-    ok = X509_VERIFY_PARAM_set1_ip_asc(SSL_get0_param(ssl), host) == 1;
-  } else if (ok) {
-    ok = SSL_set_tlsext_host_name(ssl, host) == 1 && SSL_set1_host(ssl, host) == 1;
-  }
+  if (ok && !is_ip) ok = SSL_set_tlsext_host_name(ssl, host) == 1;  // SNI for names only
+  if (ok && tc->check_hostname)
+    ok = is_ip ? X509_VERIFY_PARAM_set1_ip_asc(SSL_get0_param(ssl), host) == 1 : SSL_set1_host(ssl, host) == 1;
   std::string* key = ok ? new (std::nothrow) std::string(std::string(host) + ":" + std::to_string(port)) : nullptr;
   if (!key || SSL_set_ex_data(ssl, g_ex_index, tc) != 1 || SSL_set_ex_data(ssl, g_key_index, key) != 1) {
     if (key && SSL_get_ex_data(ssl, g_key_index) != key) delete key;
@@ -214,8 +215,9 @@ int init_tls_types(PyObject* m) {
   TlsContextType.tp_basicsize = sizeof(TlsContextObject);
   TlsContextType.tp_flags = Py_TPFLAGS_DEFAULT;
   TlsContextType.tp_doc =
-      "TlsContext(cafile=None, capath=None, verify=True): OpenSSL client context for TLS NetConns "
-      "(ssl.create_default_context semantics)";
+      "TlsContext(cafile=None, capath=None, verify=True, check_hostname=True): OpenSSL client context for TLS "
+      "NetConns (ssl.create_default_context semantics; verify=False = libpq sslmode require/prefer, "
+      "check_hostname=False = verify-ca)";
   TlsContextType.tp_new = tc_new;
   TlsContextType.tp_dealloc = reinterpret_cast<destructor>(tc_dealloc);
   TlsContextType.tp_getset = tc_getset;

@@ -85,6 +85,32 @@ def parse_dsn(dsn: str) -> Dict[str, Any]:
 SSL_MODES = ("disable", "prefer", "require", "verify-ca", "verify-full")
 
 
+_NATIVE_TLS: Dict[Tuple[str, Optional[str]], Any] = {}
+
+
+def _native_tls_context(mode: str, rootcert: Optional[str]):
+    """The native TLS context (ops TlsContext) for an sslmode, as :func:`_ssl_context` sets
+    up the ``ssl`` one; None when native connections or native TLS are off."""
+    if not netconn.enabled() or os.environ.get("BEHOLDER_NATIVE_TLS", "1") == "0":
+        return None
+    key = (mode, rootcert)
+    ctx = _NATIVE_TLS.get(key)
+    if ctx is None:
+        verify = mode not in ("prefer", "require")
+        ctx = _NATIVE_TLS[key] = _native.TlsContext(cafile=rootcert, verify=verify,
+                                                    check_hostname=mode == "verify-full")
+    return ctx
+
+
+def _tls_error(reason: str, message: str, verify: bool):
+    """A failed native TLS handshake as the ``ssl`` module raises it."""
+    import ssl
+    e = (ssl.SSLCertVerificationError if verify else ssl.SSLError)(1, message)
+    e.reason = reason
+    e.library = "SSL"
+    return e
+
+
 def _ssl_context(mode: str, rootcert: Optional[str]):
     import ssl
     ctx = ssl.create_default_context(cafile=rootcert) if rootcert else ssl.create_default_context()
@@ -272,7 +298,13 @@ class PgConnection(asyncio.Protocol):
         return item
 
     def _send(self, typ: bytes, body: bytes) -> None:
-        self._transport.write(typ + _PACK_LEN(len(body) + 4) + body)
+        self._write_raw(typ + _PACK_LEN(len(body) + 4) + body)
+
+    def _write_raw(self, data: bytes) -> None:
+        if self._net is not None:  # native TLS: startup and authentication over the NetConn
+            self._net.write(data)
+        else:
+            self._transport.write(data)
 
     async def connect(self) -> "PgConnection":
         p = self.params
@@ -295,16 +327,22 @@ class PgConnection(asyncio.Protocol):
                           (("user", p["user"]), ("database", p["database"]),
                            ("application_name", p["application_name"]), ("client_encoding", "UTF8")))
             body = struct.pack("!I", PROTOCOL_V3) + kv + b"\x00"
-            self._transport.write(_PACK_LEN(len(body) + 4) + body)
+            self._write_raw(_PACK_LEN(len(body) + 4) + body)
             await asyncio.wait_for(self._auth(), self.connect_timeout)
         except BaseException:
-            self._transport.abort()
+            if self._net is not None:
+                self._net.abort()
+                self._net = None
+            elif self._transport is not None:
+                self._transport.abort()
             self._startup = None
             raise
         self._startup = None
         self._reader.query_mode = True
         self.closed = False
-        if not self.tls:
+        if self._net is not None:  # native TLS since the SSLRequest
+            self.execute = self._net.execute
+        elif not self.tls:
             fd = netconn.adopt(self._transport)
             if fd is not None:
                 self._net = netconn.NetConn(fd, loop, "pg", self, self._reader, self._stmts, PgError,
@@ -324,6 +362,8 @@ class PgConnection(asyncio.Protocol):
     # -- NetConn callbacks (rare paths) ----------------------------------------
     def _net_lost(self, exc) -> None:
         self.closed = True
+        if self._startup is not None:
+            self._startup.put_nowait(_LOST)
         self._net.fail_all(PgProtocolError(f"connection lost: {exc}" if exc else "connection lost"))
 
     def _net_error(self, exc) -> None:
@@ -342,9 +382,22 @@ class PgConnection(asyncio.Protocol):
         ans = await self._ssl_answer
         self._ssl_answer = None
         if ans == b"S":
-            ctx = _ssl_context(mode, p.get("sslrootcert"))
-            self._transport = await asyncio.get_running_loop().start_tls(
-                self._transport, self, ctx, server_hostname=p["host"])
+            loop = asyncio.get_running_loop()
+            nctx = _native_tls_context(mode, p.get("sslrootcert"))
+            fd = netconn.adopt(self._transport) if nctx is not None else None
+            if fd is not None:  # TLS in C on the socket (ops/csrc/py_tls.cpp): handshake, then startup
+                try:
+                    self._net = netconn.NetConn(fd, loop, "pg", self, self._reader, self._stmts, PgError,
+                                                PgProtocolError, tls=nctx, server_hostname=p["host"],
+                                                port=int(p["port"]), tls_error=_tls_error)
+                except BaseException:
+                    os.close(fd)
+                    raise
+                self._transport = None
+                await self._net.handshake
+            else:
+                ctx = _ssl_context(mode, p.get("sslrootcert"))
+                self._transport = await loop.start_tls(self._transport, self, ctx, server_hostname=p["host"])
             self.tls = True
         elif ans == b"N":
             if mode != "prefer":

@@ -1,8 +1,9 @@
-"""Native TLS for the HTTPS sinks (`ops/csrc/py_tls.cpp` TlsContext, the TLS mode of
-`ops/csrc/py_netconn.cpp` NetConn, `sinks/h1.py` `_connect`). Trello and Telegram are HTTPS in
-production (index.js:53,83,99); with H1Client's own SSL context (the default one or
-``ssl_cafile``) the handshake and the record layer run in C on the socket. Every behaviour is
-checked against the asyncio TLS path (``BEHOLDER_NATIVE_TLS=0``)."""
+"""Native TLS (`ops/csrc/py_tls.cpp` TlsContext, the TLS mode of `ops/csrc/py_netconn.cpp`
+NetConn) for the HTTPS sinks (`sinks/h1.py` `_connect`) and for Postgres sslmodes
+(`store/pgwire.py` `_negotiate_tls`). Trello and Telegram are HTTPS in production
+(index.js:53,83,99); with H1Client's own SSL context (the default one or ``ssl_cafile``) the
+handshake and the record layer run in C on the socket. Every behaviour is checked against the
+asyncio TLS path (``BEHOLDER_NATIVE_TLS=0``)."""
 import asyncio
 import os
 import shutil
@@ -225,3 +226,44 @@ def test_tls12_server_and_caller_context_keeps_asyncio_path():
         await s.stop()
         return r.status, tls, r2.status, own_native
     assert run(go()) == (200, ["TLSv1.2"], 200, [])
+
+
+def test_postgres_sslmodes_on_native_tls():
+    """store/pgwire.py: after the SSLRequest's 'S' the socket goes to a TLS NetConn; startup,
+    authentication (SCRAM) and the pipelined queries run over it. sslmode require / verify-ca /
+    verify-full behave as libpq (and as the asyncio path)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from pg_fake import FakePg
+
+    from beholder_amd.store.pgwire import PgConnection, Pool
+
+    async def go(native):
+        srv = await FakePg(auth="scram", ssl_context=server_ssl_context()).start()
+        out = []
+        try:
+            for mode in ("require", f"verify-ca&sslrootcert={TLS_CERT}", f"verify-full&sslrootcert={TLS_CERT}"):
+                c = await PgConnection(f"{srv.dsn}?sslmode={mode}").connect()
+                rows = await asyncio.gather(*[c.execute("SELECT $1 + 1", (i,)) for i in range(50)])
+                out.append((mode.split("&")[0], c.tls, c._net.tls if c._net is not None else None,
+                            [r[0][0][0] for r in rows][:3]))
+                await c.close()
+            for mode in ("verify-full", "verify-ca"):  # unknown CA: refused before any query
+                try:
+                    await PgConnection(f"{srv.dsn}?sslmode={mode}").connect()
+                    out.append("no error")
+                except ssl.SSLError as e:
+                    out.append(e.reason)
+            pool = await Pool(f"{srv.dsn}?sslmode=verify-full&sslrootcert={TLS_CERT}", size=2).open()
+            res = await asyncio.gather(*[pool.execute("SELECT $1 * 3", (i,)) for i in range(40)])
+            out.append([r[0][0][0] for r in res][-1])
+            await pool.close()
+            return out, srv.tls_sessions
+        finally:
+            await srv.stop()
+    nat, py = _both(go)
+    assert [o if not isinstance(o, tuple) else (o[0], o[1], o[3]) for o in nat[0]] == \
+           [o if not isinstance(o, tuple) else (o[0], o[1], o[3]) for o in py[0]]
+    assert [o[2] for o in nat[0][:3]] == ["TLSv1.3"] * 3 and [o[2] for o in py[0][:3]] == [None] * 3
+    assert nat[0][3:5] == ["CERTIFICATE_VERIFY_FAILED"] * 2 and nat[0][5] == 117
+    assert nat[1] == py[1]
