@@ -85,11 +85,21 @@ def run_node(a, pino_sync: bool = False) -> dict:
 
 
 def run_ours(a) -> dict:
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--procs-per-rank", str(a.procs), "--steps", str(a.steps),
-           "--warmup", str(a.warmup), "--events-per-step", str(a.events_per_step), "--media", str(a.media),
-           "--seed", str(a.seed)]
-    out = subprocess.run(cmd, check=True, capture_output=True, text=True).stdout
-    return json.loads(out.strip().splitlines()[-1])
+    """bench.py on the same streams. One process: the headline (``value``, one consumer). N
+    processes: the all-process phase (``all_procs_*``), whose consumer i uses seed
+    ``--seed + 1 + 104729 * i``, hence ``--seed`` one lower than the Node side's."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(a.steps), "--warmup", str(a.warmup),
+           "--events-per-step", str(a.events_per_step), "--media", str(a.media), "--no-extras"]
+    if a.procs == 1:
+        cmd += ["--procs-per-rank", "1", "--all-procs-steps", "0", "--seed", str(a.seed)]
+    else:
+        cmd += ["--procs-per-rank", str(a.procs), "--all-procs-steps", str(a.steps), "--seed", str(a.seed - 1)]
+    out = json.loads(subprocess.run(cmd, check=True, capture_output=True, text=True).stdout.strip().splitlines()[-1])
+    if a.procs > 1:
+        out["value"] = out["all_procs_events_per_sec"]
+        out["events_per_proc_per_sec"] = round(out["value"] / a.procs, 1)
+    out["procs"] = a.procs
+    return out
 
 
 def main() -> int:
@@ -116,8 +126,7 @@ def main() -> int:
     if not a.skip_ours:
         ours = run_ours(a)
         res["ours"] = {k: ours[k] for k in ("value", "events_per_proc_per_sec", "p50_handle_latency_us",
-                                            "p99_handle_latency_us", "http_requests", "handler_errors",
-                                            "procs_per_rank")}
+                                            "p99_handle_latency_us", "http_requests", "handler_errors", "procs")}
         res["speedup"] = round(ours["value"] / res["reference_node"]["events_per_sec"], 2)
     res["config"] = {"procs": a.procs, "steps": a.steps, "warmup": a.warmup, "events_per_step": a.events_per_step,
                      "media": a.media, "seed": a.seed, "cpu": _cpu_model()}
