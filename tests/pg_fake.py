@@ -94,11 +94,12 @@ class FakePg:
             w.write(_msg(b"K", struct.pack("!II", 42, 7)))
             w.write(_msg(b"Z", b"I"))
             await self._loop(r, w)
-        except (asyncio.IncompleteReadError, ConnectionError):
+        except (asyncio.IncompleteReadError, ConnectionError, OSError):
             pass
         finally:
             self._writers.discard(w)
-            w.close()
+            if w.transport is not None:  # None: dropped while start_tls was upgrading it
+                w.close()
 
     async def _authenticate(self, r, w) -> bool:
         if self.auth == "trust":

@@ -18,6 +18,9 @@ outstanding when the run stops, un-acked and held by the broker for redelivery.
 import asyncio
 import random
 
+import pytest
+
+from beholder_amd.bench.http_sink_server import TLS_CERT, server_ssl_context
 from beholder_amd.service import Service
 from beholder_amd.sinks import H1Client
 from beholder_amd.store import Media
@@ -34,13 +37,15 @@ from pg_fake import FakePg
 class _HttpSink:
     """Keep-alive HTTP endpoint answering 200 {} that can drop all its connections."""
 
-    def __init__(self):
+    def __init__(self, tls: bool = False):
         self.requests = 0
         self.writers = set()
+        self.tls = tls
 
     async def start(self):
-        self.server = await asyncio.start_server(self._serve, "127.0.0.1", 0)
-        self.url = f"http://127.0.0.1:{self.server.sockets[0].getsockname()[1]}"
+        self.server = await asyncio.start_server(self._serve, "127.0.0.1", 0,
+                                                 ssl=server_ssl_context() if self.tls else None)
+        self.url = f"{'https' if self.tls else 'http'}://127.0.0.1:{self.server.sockets[0].getsockname()[1]}"
         return self
 
     async def _serve(self, r, w):
@@ -50,7 +55,7 @@ class _HttpSink:
                 await r.readuntil(b"\r\n\r\n")
                 self.requests += 1
                 w.write(b"HTTP/1.1 200 OK\r\nContent-Length: 2\r\n\r\n{}")
-        except (asyncio.IncompleteReadError, ConnectionError, asyncio.LimitOverrunError):
+        except (asyncio.IncompleteReadError, ConnectionError, asyncio.LimitOverrunError, OSError):
             pass
         finally:
             self.writers.discard(w)
@@ -65,7 +70,10 @@ class _HttpSink:
         await self.server.wait_closed()
 
 
-def test_chaos_every_dependency_drops_connections():
+@pytest.mark.parametrize("tls", [False, True], ids=["plain", "tls"])
+def test_chaos_every_dependency_drops_connections(tls):
+    """``tls``: HTTPS sinks and Postgres sslmode=verify-full, i.e. every sink and DB connection on
+    the native TLS path (ops/csrc/py_tls.cpp) while the chaos task drops them."""
     rng = random.Random(7)
     n_progress, n_status = 1500, 150
     medias = [Media(id=f"m{i}", name=f"Show {i}", creator=1, creatorId=f"card{i}", metadataId=str(i),
@@ -73,10 +81,11 @@ def test_chaos_every_dependency_drops_connections():
 
     async def go():
         broker = await AmqpBroker().start()
-        pg = await FakePg(auth="trust").start()
-        sink = await _HttpSink().start()
+        pg = await FakePg(auth="trust", ssl_context=server_ssl_context() if tls else None).start()
+        sink = await _HttpSink(tls).start()
         try:
-            store = PostgresStore(pg.dsn, create_schema=True, pool_size=2)
+            dsn = f"{pg.dsn}?sslmode=verify-full&sslrootcert={TLS_CERT}" if tls else pg.dsn
+            store = PostgresStore(dsn, create_schema=True, pool_size=2)
             await store.connect()
             for m in medias:
                 await store.upsert(m)
@@ -85,7 +94,8 @@ def test_chaos_every_dependency_drops_connections():
                                  "on_status_error": "leave_unacked"},
                      "instance": {"emby": {"host": sink.url}}})
             src = AmqpSource(broker.url, prefetch=50, backoff_initial=0.02, backoff_max=0.2)
-            svc = Service(c, source=src, store=store, http=H1Client(timeout_s=5), logger=Logger(stream=log),
+            http = H1Client(timeout_s=5, ssl_cafile=TLS_CERT if tls else None)
+            svc = Service(c, source=src, store=store, http=http, logger=Logger(stream=log),
                           serve_metrics=False)
             await svc.init()
             run = asyncio.ensure_future(svc.run())
@@ -125,6 +135,9 @@ def test_chaos_every_dependency_drops_connections():
                 if st["acked"] >= n_status:
                     break
                 await asyncio.sleep(0.05)
+            if tls:  # the sink and DB connections were native TLS ones
+                assert http._native_tls().stats["handshakes"] >= 1
+                assert all(c._net is not None and c._net.tls for c in store._pool._conns if not c.closed)
             svc.request_stop()
             stats = await asyncio.wait_for(run, 15)
             await svc.close()
