@@ -6,14 +6,16 @@
 // busy-set bookkeeping, the release to the pool and the HttpResponse: about 4 us of CPU on
 // the box, the largest Python cost left in `tcp_e2e` after the native NetConn.
 //
-//   call = h1_fast(client, method, url, params, timeout)   # None: take the Python path
+//   call = h1_fast(client, method, url, params, timeout)   # None: not a stock H1Client
 //   resp = await call
 //
-// h1_fast handles exactly the shape the sinks produce on a warm pool: a stock H1Client, an
+// Like a coroutine, an H1Call does nothing until it is first awaited. Then it handles exactly
+// the shape the sinks produce on a warm pool: a stock H1Client, an
 // ASCII URL whose origin is already known, a printable path (no fragment), params None or a
 // dict (encodeURIComponent query, the `request` library's qs.stringify), and a live idle
-// keep-alive connection on a native NetConn (utils/netconn.py). Anything else returns None
-// before any state is touched, and H1Client._request does the work as before.
+// keep-alive connection on a native NetConn (utils/netconn.py). Anything else is declined
+// before any state is touched, and the H1Call delegates the whole request to
+// H1Client._request (yield from).
 //
 // The returned H1Call is an awaitable iterator (send/throw/close). It yields the reply
 // IOFuture; a handler driven by the native Driver is resumed by the NetConn's reply callback.
@@ -101,7 +103,7 @@ struct State {
 
 PyObject *s_closed_attr, *s_origins, *s_counts, *s_keepalive_s, *s_timeout_s, *s_busy, *s_sweeper, *s_tail,
     *s_tail_cl0, *s_requests, *s_reused, *s_drop, *s_release, *s_arm, *s_resume, *s_time, *s_pop, *s_append,
-    *s_buffered, *s_throw, *s_close;
+    *s_buffered, *s_throw, *s_close, *s_request_py;
 
 double mono_s() {
   timespec ts;
@@ -135,18 +137,24 @@ int bump(PyObject* d, PyObject* key) {
 }
 
 // ---- H1Call ---------------------------------------------------------------------------------
-enum : uint8_t { ST_WAIT = 0, ST_DELEGATE = 1, ST_DONE = 2 };
+// ST_INIT: created, nothing done yet (like a coroutine before its first send: the request is
+// prepared and sent when the call is first awaited, so ordering under gather() and an
+// H1Call that is never awaited behave as H1Client._request would)
+enum : uint8_t { ST_WAIT = 0, ST_DELEGATE = 1, ST_DONE = 2, ST_INIT = 3 };
 
 struct H1CallObject {
   PyObject_HEAD PyObject* client;
   PyObject* conn;
   PyObject* fut;
-  PyObject* method;  // str, upper case
-  PyObject* full;    // str: the URL with its query (HttpResponse.url, error text)
+  PyObject* method;  // str as passed, then upper case once sent
+  PyObject* full;    // str: the URL as passed, then with its query (HttpResponse.url, error text)
   PyObject* deadline;
-  PyObject* sub;  // the Python continuation (H1Client._resume) once delegated
+  PyObject* params;   // ST_INIT: the call's params (or NULL)
+  PyObject* timeout;  // ST_INIT: the call's timeout (or NULL)
+  PyObject* sub;  // the Python continuation (H1Client._resume / _request) once delegated
   uint8_t state;
   uint8_t reused;  // the connection had served a request before (h1.py `reused`)
+  uint8_t path;    // 0 not started, 1 sent natively, 2 delegated to H1Client._request
 };
 
 PyTypeObject H1CallType = {PyVarObject_HEAD_INIT(nullptr, 0)};
@@ -158,6 +166,8 @@ int call_traverse(H1CallObject* s, visitproc visit, void* arg) {
   Py_VISIT(s->method);
   Py_VISIT(s->full);
   Py_VISIT(s->deadline);
+  Py_VISIT(s->params);
+  Py_VISIT(s->timeout);
   Py_VISIT(s->sub);
   return 0;
 }
@@ -169,6 +179,8 @@ int call_clear(H1CallObject* s) {
   Py_CLEAR(s->method);
   Py_CLEAR(s->full);
   Py_CLEAR(s->deadline);
+  Py_CLEAR(s->params);
+  Py_CLEAR(s->timeout);
   Py_CLEAR(s->sub);
   return 0;
 }
@@ -318,12 +330,57 @@ int start_delegate(H1CallObject* s, PyObject* thrown) {
   return 0;
 }
 
+int h1_start(H1CallObject* s);
+
+// The fast path declined at the first await: the whole request is H1Client._request's.
+int start_python(H1CallObject* s) {
+  PyObject* args[5] = {s->client, s->method, s->full, s->params ? s->params : Py_None,
+                       s->timeout ? s->timeout : Py_None};
+  PyObject* sub = PyObject_VectorcallMethod(s_request_py, args, 5, nullptr);
+  if (!sub) {
+    s->state = ST_DONE;
+    return -1;
+  }
+  if (!PyCoro_CheckExact(sub)) {
+    Py_DECREF(sub);
+    PyErr_SetString(PyExc_TypeError, "H1Client._request must be a coroutine function");
+    s->state = ST_DONE;
+    return -1;
+  }
+  s->sub = sub;
+  s->state = ST_DELEGATE;
+  return 0;
+}
+
 PySendResult call_am_send(H1CallObject* s, PyObject* arg, PyObject** out) {
   if (s->state == ST_DELEGATE) return delegate_send(s, arg, out);
   if (s->state == ST_DONE) {
     PyErr_SetString(PyExc_RuntimeError, "cannot reuse already awaited H1 request");
     *out = nullptr;
     return PYGEN_ERROR;
+  }
+  if (s->state == ST_INIT) {
+    int k;
+    try {
+      k = h1_start(s);
+    } catch (const std::bad_alloc&) {
+      PyErr_NoMemory();
+      k = -1;
+    }
+    if (k < 0) {
+      s->state = ST_DONE;
+      *out = nullptr;
+      return PYGEN_ERROR;
+    }
+    s->path = uint8_t(k == 1 ? 1 : 2);
+    if (k == 0) {
+      if (start_python(s) < 0) {
+        *out = nullptr;
+        return PYGEN_ERROR;
+      }
+      return delegate_send(s, Py_None, out);
+    }
+    s->state = ST_WAIT;
   }
   PyObject* res = nullptr;
   int st = iofuture_peek(s->fut, &res);
@@ -405,6 +462,7 @@ PyObject* call_throw(H1CallObject* s, PyObject* args) {
     PyErr_SetString(PyExc_TypeError, "exceptions must be classes or instances deriving from BaseException");
     return nullptr;
   }
+  if (s->state == ST_INIT) s->state = ST_DONE;  // like throw() into an unstarted coroutine
   if (s->state == ST_WAIT) {  // the request loop's except clauses see it at the await (h1.py _exchange)
     int rc = start_delegate(s, exc);
     Py_DECREF(exc);
@@ -431,6 +489,7 @@ PyObject* call_close(H1CallObject* s, PyObject*) {
     s->state = ST_DONE;
     abandon(s);
   }
+  s->state = ST_DONE;
   Py_RETURN_NONE;
 }
 
@@ -438,6 +497,16 @@ PyObject* call_await(H1CallObject* s) {
   Py_INCREF(s);
   return reinterpret_cast<PyObject*>(s);
 }
+
+PyObject* call_get_native(H1CallObject* s, void*) {
+  if (s->path == 0) Py_RETURN_NONE;
+  return PyBool_FromLong(s->path == 1);
+}
+
+PyGetSetDef call_getset[] = {
+    {"native", reinterpret_cast<getter>(call_get_native), nullptr,
+     "None before the first await; True if the request was sent on the native path", nullptr},
+    {nullptr, nullptr, nullptr, nullptr, nullptr}};
 
 PyAsyncMethods call_async = {reinterpret_cast<unaryfunc>(call_await), nullptr, nullptr,
                              reinterpret_cast<sendfunc>(call_am_send)};
@@ -450,20 +519,18 @@ PyMethodDef call_methods[] = {
     {nullptr, nullptr, 0, nullptr}};
 
 // ---- h1_fast ----------------------------------------------------------------------------------
-// Everything that can decline does so before any pool state changes: the caller then runs the
-// Python path, which reproduces any error at its await.
-PyObject* h1_fast_impl(PyObject* client, PyObject* method, PyObject* url, PyObject* params, PyObject* timeout) {
-  if (!g.ready || Py_TYPE(client) != g.client_type) Py_RETURN_NONE;
-  if (!PyUnicode_CheckExact(method) || !PyUnicode_CheckExact(url) || !PyUnicode_IS_ASCII(method) ||
-      !PyUnicode_IS_ASCII(url))
-    Py_RETURN_NONE;
-  if (params == Py_None) params = nullptr;
-  if (params && !PyDict_CheckExact(params)) Py_RETURN_NONE;
-  if (timeout == Py_None) timeout = nullptr;
-  if (timeout && !PyFloat_CheckExact(timeout) && !PyLong_CheckExact(timeout)) Py_RETURN_NONE;
+// At the first await: send the request on an idle pooled connection. 1 = sent (s->conn, fut,
+// method, full, deadline, reused set), 0 = declined before any pool state changed (the Python
+// path runs instead and reproduces any error at its await), -1 = error.
+int h1_start(H1CallObject* s) {
+  PyObject* client = s->client;
+  PyObject* method = s->method;
+  PyObject* url = s->full;
+  PyObject* params = s->params;
+  PyObject* timeout = s->timeout;
   PyObject** dp = _PyObject_GetDictPtr(client);
   PyObject* d = dp ? *dp : nullptr;
-  if (!d) Py_RETURN_NONE;
+  if (!d) return 0;
   PyObject* cclosed = PyDict_GetItemWithError(d, s_closed_attr);
   PyObject* origins = cclosed ? PyDict_GetItemWithError(d, s_origins) : nullptr;
   PyObject* counts = origins ? PyDict_GetItemWithError(d, s_counts) : nullptr;
@@ -473,50 +540,50 @@ PyObject* h1_fast_impl(PyObject* client, PyObject* method, PyObject* url, PyObje
   PyObject* tail = busy ? PyDict_GetItemWithError(d, s_tail) : nullptr;
   PyObject* tail_cl0 = tail ? PyDict_GetItemWithError(d, s_tail_cl0) : nullptr;
   if (!tail_cl0) {
-    if (PyErr_Occurred()) return nullptr;
-    Py_RETURN_NONE;
+    if (PyErr_Occurred()) return -1;
+    return 0;
   }
   if (cclosed != Py_False || !PyDict_CheckExact(origins) || !PyDict_CheckExact(counts) || !PySet_CheckExact(busy) ||
       !PyBytes_CheckExact(tail) || !PyBytes_CheckExact(tail_cl0) || !PyFloat_CheckExact(keepalive))
-    Py_RETURN_NONE;
+    return 0;
 
   // method: upper-case token
   Py_ssize_t mn = PyUnicode_GET_LENGTH(method);
   const char* m = reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(method));
-  if (mn == 0) Py_RETURN_NONE;
+  if (mn == 0) return 0;
   for (Py_ssize_t i = 0; i < mn; ++i)
-    if (m[i] < 'A' || m[i] > 'Z') Py_RETURN_NONE;
+    if (m[i] < 'A' || m[i] > 'Z') return 0;
 
   // url: scheme://authority[/path][?query], no fragment (h1.py _split_url)
   Py_ssize_t un = PyUnicode_GET_LENGTH(url);
   const char* u = reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(url));
   Py_ssize_t i = 0;
   while (i + 2 < un && !(u[i] == ':' && u[i + 1] == '/' && u[i + 2] == '/')) ++i;
-  if (i == 0 || i + 2 >= un) Py_RETURN_NONE;
+  if (i == 0 || i + 2 >= un) return 0;
   Py_ssize_t k = i + 3;
   while (k < un && u[k] != '/' && u[k] != '?' && u[k] != '#') ++k;
   bool has_q = false;
   for (Py_ssize_t j = k; j < un; ++j) {
     unsigned char ch = static_cast<unsigned char>(u[j]);
-    if (ch < 0x21 || ch > 0x7E || ch == '#') Py_RETURN_NONE;  // _resolve would quote it
+    if (ch < 0x21 || ch > 0x7E || ch == '#') return 0;  // _resolve would quote it
     if (ch == '?') has_q = true;
   }
-  if (params && has_q && PyDict_GET_SIZE(params)) Py_RETURN_NONE;  // with_query appends with '&'
+  if (params && has_q && PyDict_GET_SIZE(params)) return 0;  // with_query appends with '&'
   PyObject* key = PyUnicode_FromStringAndSize(u, k);
-  if (!key) return nullptr;
+  if (!key) return -1;
   PyObject* o = PyDict_GetItemWithError(origins, key);
   Py_DECREF(key);
   if (!o) {
-    if (PyErr_Occurred()) return nullptr;
-    Py_RETURN_NONE;  // first request to this origin: the Python path creates it
+    if (PyErr_Occurred()) return -1;
+    return 0;  // first request to this origin: the Python path creates it
   }
-  if (Py_TYPE(o) != g.origin.type) Py_RETURN_NONE;
+  if (Py_TYPE(o) != g.origin.type) return 0;
   PyObject* host = g.origin.get(o, O_HOST_HEADER);
   PyObject* auth = g.origin.get(o, O_AUTH);
   PyObject* idle = g.origin.get(o, O_IDLE);
   if (!host || !auth || !idle || !PyUnicode_CheckExact(host) || !PyUnicode_IS_ASCII(host) ||
       (auth != Py_None && (!PyUnicode_CheckExact(auth) || !PyUnicode_IS_ASCII(auth))))
-    Py_RETURN_NONE;
+    return 0;
 
   // request text: "M target HTTP/1.1\r\nHost: h\r\n[Authorization: a\r\n]" + User-Agent tail
   std::string req;
@@ -533,7 +600,7 @@ PyObject* h1_fast_impl(PyObject* client, PyObject* method, PyObject* url, PyObje
     while (PyDict_Next(params, &pos, &pk, &pv)) {
       if (!text_query_pair_append(q, pk, pv, &first, false)) {
         PyErr_Clear();  // the Python path raises it at the await
-        Py_RETURN_NONE;
+        return 0;
       }
     }
     if (!q.empty()) {
@@ -557,39 +624,39 @@ PyObject* h1_fast_impl(PyObject* client, PyObject* method, PyObject* url, PyObje
   PyObject* conn = nullptr;
   for (;;) {
     Py_ssize_t n = PyObject_Size(idle);
-    if (n < 0) return nullptr;
-    if (n == 0) Py_RETURN_NONE;  // connect or wait for a slot: Python path
+    if (n < 0) return -1;
+    if (n == 0) return 0;  // connect or wait for a slot: Python path
     PyObject* cand = PyObject_CallMethodNoArgs(idle, s_pop);
-    if (!cand) return nullptr;
+    if (!cand) return -1;
     if (Py_TYPE(cand) != g.conn.type) {
       PyObject* r = PyObject_CallMethodOneArg(idle, s_append, cand);  // put it back
       Py_DECREF(cand);
-      if (!r) return nullptr;
+      if (!r) return -1;
       Py_DECREF(r);
-      Py_RETURN_NONE;
+      return 0;
     }
     PyObject* closed = g.conn.get(cand, C_CLOSED);
     PyObject* last = g.conn.get(cand, C_LAST_USED);
     double lu = last ? PyFloat_AsDouble(last) : -1e300;
     if (lu == -1.0 && PyErr_Occurred()) {
       Py_DECREF(cand);
-      return nullptr;
+      return -1;
     }
     if (closed == Py_False && mono_s() - lu < ka) {
       PyObject* net = g.conn.get(cand, C_NET);
       if (!net || !is_netconn(net) || !netconn_open(net)) {  // TLS / asyncio transport: Python path
         PyObject* r = PyObject_CallMethodOneArg(idle, s_append, cand);
         Py_DECREF(cand);
-        if (!r) return nullptr;
+        if (!r) return -1;
         Py_DECREF(r);
-        Py_RETURN_NONE;
+        return 0;
       }
       conn = cand;
       break;
     }
     PyObject* r = PyObject_CallMethodOneArg(client, s_drop, cand);  // stale: self._drop(cand)
     Py_DECREF(cand);
-    if (!r) return nullptr;
+    if (!r) return -1;
     Py_DECREF(r);
   }
 
@@ -598,37 +665,37 @@ PyObject* h1_fast_impl(PyObject* client, PyObject* method, PyObject* url, PyObje
     PyObject* p;
     ~Own() { Py_XDECREF(p); }
   } own_conn{conn};
-  if (bump(counts, s_requests) < 0 || bump(counts, s_reused) < 0) return nullptr;
+  if (bump(counts, s_requests) < 0 || bump(counts, s_reused) < 0) return -1;
   PyObject* uses = g.conn.get(conn, C_USES);
   bool reused = true;
   if (uses) {
     int pos = PyObject_IsTrue(uses);  // reused = c.uses > 0 (an idle connection has served one)
-    if (pos < 0) return nullptr;
+    if (pos < 0) return -1;
     reused = pos != 0;
     PyObject* one = PyLong_FromLong(1);
     PyObject* nu = one ? PyNumber_Add(uses, one) : nullptr;
     Py_XDECREF(one);
-    if (!nu) return nullptr;
+    if (!nu) return -1;
     g.conn.set(conn, C_USES, nu);
   }
   PyObject* loop = PyObject_CallNoArgs(g.get_running_loop);
-  if (!loop) return nullptr;
+  if (!loop) return -1;
   Own own_loop{loop};
   PyObject* now = PyObject_CallMethodNoArgs(loop, s_time);
-  if (!now) return nullptr;
+  if (!now) return -1;
   double dl = PyFloat_AsDouble(now);
   Py_DECREF(now);
-  if (dl == -1.0 && PyErr_Occurred()) return nullptr;
+  if (dl == -1.0 && PyErr_Occurred()) return -1;
   PyObject* tmo = timeout;  // `timeout or self.timeout_s`
   if (tmo) {
     int truth = PyObject_IsTrue(tmo);
-    if (truth < 0) return nullptr;
+    if (truth < 0) return -1;
     if (!truth) tmo = nullptr;
   }
   double add = PyFloat_AsDouble(tmo ? tmo : timeout_s);
-  if (add == -1.0 && PyErr_Occurred()) return nullptr;
+  if (add == -1.0 && PyErr_Occurred()) return -1;
   PyObject* deadline = PyFloat_FromDouble(dl + add);
-  if (!deadline) return nullptr;
+  if (!deadline) return -1;
   Own own_deadline{deadline};
   PyObject* full;
   if (q.empty()) {
@@ -639,18 +706,18 @@ PyObject* h1_fast_impl(PyObject* client, PyObject* method, PyObject* url, PyObje
     f += '?';
     f += q;
     full = PyUnicode_FromStringAndSize(f.data(), Py_ssize_t(f.size()));
-    if (!full) return nullptr;
+    if (!full) return -1;
   }
   Own own_full{full};
   Py_INCREF(method);
   PyObject* what = PyTuple_Pack(2, method, full);
   Py_DECREF(method);
-  if (!what) return nullptr;
+  if (!what) return -1;
   Py_INCREF(deadline);
   g.conn.set(conn, C_DEADLINE, deadline);
   g.conn.set(conn, C_WHAT, what);
   PyObject* fut = iofuture_new(loop);
-  if (!fut) return nullptr;
+  if (!fut) return -1;
   Own own_fut{fut};
   bool head = mn == 4 && memcmp(m, "HEAD", 4) == 0;
   if (netconn_h1_request(g.conn.get(conn, C_NET), req, fut, head) < 0) {
@@ -663,35 +730,30 @@ PyObject* h1_fast_impl(PyObject* client, PyObject* method, PyObject* url, PyObje
     else
       Py_DECREF(r);
     PyErr_Restore(et, ev, tb);
-    return nullptr;
+    return -1;
   }
-  if (PySet_Add(busy, conn) < 0) return nullptr;
+  if (PySet_Add(busy, conn) < 0) return -1;
   PyObject* sweeper = PyDict_GetItemWithError(d, s_sweeper);
-  if (!sweeper && PyErr_Occurred()) return nullptr;
+  if (!sweeper && PyErr_Occurred()) return -1;
   if (!sweeper || sweeper == Py_None) {
     PyObject* r = PyObject_CallMethodOneArg(client, s_arm, loop);
-    if (!r) return nullptr;
+    if (!r) return -1;
     Py_DECREF(r);
   }
-  H1CallObject* call = PyObject_GC_New(H1CallObject, &H1CallType);
-  if (!call) return nullptr;
-  Py_INCREF(client);
-  call->client = client;
-  call->conn = conn;
   own_conn.p = nullptr;
-  call->fut = fut;
+  s->conn = conn;
   own_fut.p = nullptr;
+  s->fut = fut;
   Py_INCREF(method);
-  call->method = method;
-  call->full = full;
+  Py_SETREF(s->method, method);
   own_full.p = nullptr;
-  call->deadline = deadline;
+  Py_SETREF(s->full, full);
   own_deadline.p = nullptr;
-  call->sub = nullptr;
-  call->state = ST_WAIT;
-  call->reused = reused;
-  PyObject_GC_Track(call);
-  return reinterpret_cast<PyObject*>(call);
+  s->deadline = deadline;
+  s->reused = reused;
+  Py_CLEAR(s->params);
+  Py_CLEAR(s->timeout);
+  return 1;
 }
 
 // h1_fast(client, method, url, params=None, timeout=None) -> H1Call or None
@@ -700,8 +762,27 @@ PyObject* mod_h1_fast(PyObject*, PyObject* const* a, Py_ssize_t n) {
     PyErr_SetString(PyExc_TypeError, "h1_fast(client, method, url, params=None, timeout=None)");
     return nullptr;
   }
-  BEHOLDER_TRY { return h1_fast_impl(a[0], a[1], a[2], n > 3 ? a[3] : Py_None, n > 4 ? a[4] : Py_None); }
-  BEHOLDER_CATCH(nullptr)
+  if (!g.ready || Py_TYPE(a[0]) != g.client_type) Py_RETURN_NONE;
+  H1CallObject* call = PyObject_GC_New(H1CallObject, &H1CallType);
+  if (!call) return nullptr;
+  PyObject* params = n > 3 && a[3] != Py_None ? a[3] : nullptr;
+  PyObject* timeout = n > 4 && a[4] != Py_None ? a[4] : nullptr;
+  Py_INCREF(a[0]);
+  call->client = a[0];
+  Py_INCREF(a[1]);
+  call->method = a[1];
+  Py_INCREF(a[2]);
+  call->full = a[2];
+  Py_XINCREF(params);
+  call->params = params;
+  Py_XINCREF(timeout);
+  call->timeout = timeout;
+  call->conn = call->fut = call->deadline = call->sub = nullptr;
+  call->state = ST_INIT;
+  call->reused = 0;
+  call->path = 0;
+  PyObject_GC_Track(call);
+  return reinterpret_cast<PyObject*>(call);
 }
 
 // h1_setup(client_cls, conn_cls, origin_cls, response_cls, get_running_loop)
@@ -754,7 +835,8 @@ int init_h1call_types(PyObject* m) {
               {&s_requests, "requests"},      {&s_reused, "reused"},      {&s_drop, "_drop"},
               {&s_release, "_release"},       {&s_arm, "_arm"},           {&s_resume, "_resume"},
               {&s_time, "time"},              {&s_pop, "pop"},            {&s_append, "append"},
-              {&s_buffered, "buffered"},      {&s_throw, "throw"},        {&s_close, "close"}};
+              {&s_buffered, "buffered"},      {&s_throw, "throw"},        {&s_close, "close"},
+              {&s_request_py, "_request"}};
   for (auto& s : strs)
     if (!(*s.slot = PyUnicode_InternFromString(s.text))) return -1;
   H1CallType.tp_name = "beholder_amd.ops._native.H1Call";
@@ -769,6 +851,7 @@ int init_h1call_types(PyObject* m) {
   H1CallType.tp_iter = PyObject_SelfIter;
   H1CallType.tp_iternext = reinterpret_cast<iternextfunc>(call_iternext);
   H1CallType.tp_methods = call_methods;
+  H1CallType.tp_getset = call_getset;
   if (PyType_Ready(&H1CallType) < 0) return -1;
   Py_INCREF(&H1CallType);
   if (PyModule_AddObject(m, "H1Call", reinterpret_cast<PyObject*>(&H1CallType)) < 0) return -1;

@@ -86,12 +86,12 @@ async def _drive(port, fast: bool):
             except HttpError:
                 pass
             aw = c.request(m, url, params=params)
-            kinds.append(type(aw).__name__)
             try:
                 r = await aw
                 out.append((r.status, r.body, r.headers, r.url))
             except HttpError as e:
                 out.append(("error", str(e)))
+            kinds.append("native" if getattr(aw, "native", False) else "python")
         counts = dict(c.counts)
         await c.close()
         return out, kinds, counts
@@ -116,9 +116,9 @@ def test_fast_path_sends_the_same_bytes_and_returns_the_same_responses():
     assert f_raw == p_raw  # byte for byte, request line, Host, Authorization, User-Agent, Content-Length
     assert f_out == p_out
     assert f_counts == p_counts and f_conns == p_conns
-    assert "H1Call" in f_kinds and "H1Call" not in p_kinds
+    assert "native" in f_kinds and "native" not in p_kinds
     # the shapes the sinks produce take the native path; the others decline before any state changes
-    assert f_kinds.count("H1Call") > len(f_kinds) // 3
+    assert f_kinds.count("native") > len(f_kinds) // 3
 
 
 def test_fast_path_declines_cold_pool_and_foreign_shapes():
@@ -127,23 +127,24 @@ def test_fast_path_declines_cold_pool_and_foreign_shapes():
         c = H1Client(timeout_s=5)
         url = f"http://127.0.0.1:{s.port}/a"
         first = c.request("GET", url)
-        kinds = [type(first).__name__]
+        assert first.native is None  # nothing happens before the first await, as for a coroutine
         await first
+        kinds = [first.native]
         for args in (("GET", url), ("get", url), ("GET", url + "#f"), ("GET", url + "/é"), ("POST", url + "?a=1"),
                      ("GET", f"http://127.0.0.1:{s.port + 1 if s.port < 65535 else 1}/b")):
             aw = c.request(*args, params={"k": 1} if args[0] == "POST" else None)
-            kinds.append(type(aw).__name__)
             try:
                 await aw
             except HttpError:
                 pass
+            kinds.append(aw.native)
         await c.close()
         await s.stop()
         return kinds
     kinds = run(go())
-    assert kinds[0] == "coroutine"  # no idle connection yet
-    assert kinds[1] == "H1Call"
-    assert kinds[2:] == ["coroutine"] * 5
+    assert kinds[0] is False  # no idle connection yet
+    assert kinds[1] is True
+    assert kinds[2:] == [False] * 5
 
 
 def test_fast_path_reset_retry_redirect_and_errors_match_python():
@@ -194,9 +195,9 @@ def test_fast_path_timeout_cancel_and_abandon_release_the_connection():
         base = f"http://127.0.0.1:{s.port}"
         await c.request("GET", base + "/a")
         aw = c.request("GET", base + "/slow", params={"token": "secret"}, timeout=0.2)
-        assert type(aw).__name__ == "H1Call"
         with pytest.raises(HttpError, match=r"^ETIMEDOUT: GET http://127\.0\.0\.1:\d+/slow$"):
             await aw
+        assert aw.native is True
         await c.request("GET", base + "/a")
         t = asyncio.ensure_future(c.request("GET", base + "/slow"))
         await asyncio.sleep(0.05)
@@ -205,7 +206,7 @@ def test_fast_path_timeout_cancel_and_abandon_release_the_connection():
             await t
         await c.request("GET", base + "/a")
         aw = c.request("GET", base + "/slow")
-        assert type(aw).__name__ == "H1Call"
+        assert aw.send(None) is not None and aw.native is True  # sent, suspended on the reply
         aw.close()  # never awaited to the end: like closing the coroutine
         busy = len(c._busy)
         r = await c.request("GET", base + "/a")
@@ -247,3 +248,116 @@ def test_fast_path_under_native_driver_and_gather():
     statuses, done, st, conns = run(go())
     assert statuses == [200] * 200 and done == [200] * 50
     assert st["requests"] == 258 and conns <= 8
+
+
+def _script(seed):
+    """Server behaviour for the differential run: a function of the request's global index only
+    (the same in both runs when the client behaves the same)."""
+    rnd = random.Random(seed)
+    plan = []
+    for _ in range(120):
+        kind = rnd.choices(["ok", "cl", "chunked", "close", "redirect", "status", "drop", "drop_mid", "head204"],
+                           [30, 10, 10, 8, 6, 10, 6, 4, 4])[0]
+        plan.append((kind, rnd.randrange(0, 2000), rnd.choice([200, 201, 204, 404, 500, 503])))
+    return plan
+
+
+def _response(kind, n, status, target):
+    body = (b"x%d" % n) * (n % 7)
+    if kind == "ok":
+        return b"HTTP/1.1 200 OK\r\nContent-Length: %d\r\n\r\n" % len(body) + body
+    if kind == "cl":
+        return b"HTTP/1.1 %d S\r\nContent-Length: %d\r\nX-N: %d\r\n\r\n" % (status, len(body), n) + body
+    if kind == "chunked":
+        return (b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n" + b"%x\r\n" % len(body) + body
+                + b"\r\n" if body else b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n") + b"0\r\n\r\n"
+    if kind == "close":
+        return b"HTTP/1.1 200 OK\r\nConnection: close\r\nContent-Length: %d\r\n\r\n" % len(body) + body
+    if kind == "redirect":
+        return b"HTTP/1.1 302 Found\r\nLocation: /r%d\r\nContent-Length: 0\r\n\r\n" % n
+    if kind == "status":
+        return b"HTTP/1.1 %d X\r\nContent-Length: 0\r\n\r\n" % status
+    if kind == "head204":
+        return b"HTTP/1.1 204 No Content\r\n\r\n"
+    if kind == "drop_mid":
+        return (b"HTTP/1.1 200 OK\r\nContent-Length: 100\r\n\r\npartial", "close")
+    return None  # drop
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_differential_random_server_behaviour(seed):
+    """Random status codes, framings, Connection: close, redirects, drops before and in the
+    middle of a response: the fast path and the Python path see the same requests on the same
+    connections and produce the same outcomes and counters."""
+    plan = _script(seed)
+
+    class Srv(Raw):
+        def __init__(self):
+            super().__init__(None)
+            self.n = 0
+            self.trace = []
+
+        async def _serve(self, r, w):
+            self.connections += 1
+            conn = self.connections
+            try:
+                while True:
+                    try:
+                        head = await r.readuntil(b"\r\n\r\n")
+                    except (asyncio.IncompleteReadError, ConnectionError):
+                        return
+                    i = self.n
+                    self.n += 1
+                    kind, n, status = plan[i % len(plan)]
+                    target = head.split(b" ", 2)[1].decode()
+                    self.trace.append((conn, head.split(b" ", 1)[0].decode(), target, kind))
+                    if target.startswith("/r"):
+                        kind = "ok"  # redirect targets answer
+                    out = _response(kind, n, status, target)
+                    if out is None:
+                        w.transport.abort()
+                        return
+                    close = isinstance(out, tuple)
+                    w.write(out[0] if close else out)
+                    await w.drain()
+                    if close or kind == "close":
+                        return
+            finally:
+                w.close()
+
+    async def one(fast):
+        saved = h1mod._h1_fast
+        if not fast:
+            h1mod._h1_fast = h1mod._h1_python_only
+        try:
+            s = await Srv().start()
+            c = H1Client(timeout_s=5, max_per_host=4)
+            rnd = random.Random(seed + 100)
+            base = f"http://127.0.0.1:{s.port}"
+            out = []
+            for i in range(80):
+                m = rnd.choice(["GET", "POST", "PUT", "HEAD", "DELETE"])
+                params = rnd.choice([None, {"i": i}, {"text": "a b ü", "k": None}])
+                conc = rnd.choice([1, 1, 1, 3])
+                aws = [c.request(m, f"{base}/p{i}_{j}", params=params) for j in range(conc)]
+                res = await asyncio.gather(*aws, return_exceptions=True)
+                for r in res:
+                    if isinstance(r, HttpError):
+                        out.append(("err", str(r).replace(base, "")))
+                    elif isinstance(r, BaseException):
+                        raise r
+                    else:
+                        out.append((r.status, r.body, r.url.replace(base, ""), sorted(r.headers.items())))
+            st = dict(c.counts)
+            await c.close()
+            await s.stop()
+            return out, st, s.trace
+        finally:
+            h1mod._h1_fast = saved
+
+    async def go():
+        return await one(True), await one(False)
+    (fo, fs, ft), (po, ps, pt) = run(go())
+    assert ft == pt  # same requests, same connections, same order
+    assert fo == po
+    assert fs == ps
