@@ -15,12 +15,14 @@
 //
 // Client sessions are cached per "host:port" (the last ticket each origin gave us), so a
 // reconnect after the server closed an idle keep-alive connection resumes instead of running
-// a full handshake.
+// a full handshake. A TLS 1.3 ticket is used once (RFC 8446 C.4); the resumed connection's
+// own tickets take its place.
 #include <arpa/inet.h>
 #include <openssl/err.h>
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
 
+#include <deque>
 #include <map>
 #include <string>
 
@@ -35,7 +37,7 @@ constexpr const char* kCiphers = "@SECLEVEL=2:ECDH+AESGCM:ECDH+CHACHA20:ECDH+AES
 
 struct TlsContextObject {
   PyObject_HEAD SSL_CTX* ctx;
-  std::map<std::string, SSL_SESSION*>* sessions;  // "host:port" -> last session (one ref each)
+  std::map<std::string, std::deque<SSL_SESSION*>>* sessions;  // "host:port" -> newest sessions (one ref each)
   uint64_t handshakes, resumed;
   bool check_hostname;  // the certificate must name the host (verify-full / HTTPS)
 };
@@ -51,22 +53,29 @@ std::string last_error_text() {
   return buf;
 }
 
-// new-session callback: keep the newest session of each origin (TLS 1.3 tickets arrive after
-// the handshake, in the first reads)
+constexpr size_t kTicketsPerOrigin = 16;  // enough for a burst of reconnects to resume
+
+void free_all(TlsContextObject* tc) {
+  for (auto& kv : *tc->sessions)
+    for (SSL_SESSION* x : kv.second) SSL_SESSION_free(x);
+  tc->sessions->clear();
+}
+
+// new-session callback: keep the newest sessions of each origin (TLS 1.3 tickets arrive after
+// the handshake, in the first reads; servers usually send two)
 int on_new_session(SSL* ssl, SSL_SESSION* sess) {
   auto* self = static_cast<TlsContextObject*>(SSL_get_ex_data(ssl, g_ex_index));
   auto* key = static_cast<std::string*>(SSL_get_ex_data(ssl, g_key_index));
   if (!self || !key || !self->sessions) return 0;
   auto it = self->sessions->find(*key);
-  if (it != self->sessions->end()) {
-    SSL_SESSION_free(it->second);
-    it->second = sess;
-  } else {
-    if (self->sessions->size() >= 1024) {  // bounded: forget everything, rebuild on demand
-      for (auto& kv : *self->sessions) SSL_SESSION_free(kv.second);
-      self->sessions->clear();
-    }
-    self->sessions->emplace(*key, sess);
+  if (it == self->sessions->end()) {
+    if (self->sessions->size() >= 1024) free_all(self);  // bounded: rebuilt on demand
+    it = self->sessions->emplace(*key, std::deque<SSL_SESSION*>()).first;
+  }
+  it->second.push_back(sess);
+  if (it->second.size() > kTicketsPerOrigin) {
+    SSL_SESSION_free(it->second.front());
+    it->second.pop_front();
   }
   return 1;  // we hold the reference
 }
@@ -85,7 +94,7 @@ PyObject* tc_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
   if (!s) return nullptr;
   s->ctx = nullptr;
   s->check_hostname = verify && check_hostname;
-  s->sessions = new (std::nothrow) std::map<std::string, SSL_SESSION*>();
+  s->sessions = new (std::nothrow) std::map<std::string, std::deque<SSL_SESSION*>>();
   if (!s->sessions) {
     Py_DECREF(s);
     return PyErr_NoMemory();
@@ -127,7 +136,7 @@ PyObject* tc_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
 
 void tc_dealloc(TlsContextObject* s) {
   if (s->sessions) {
-    for (auto& kv : *s->sessions) SSL_SESSION_free(kv.second);
+    free_all(s);
     delete s->sessions;
   }
   if (s->ctx) SSL_CTX_free(s->ctx);
@@ -135,9 +144,10 @@ void tc_dealloc(TlsContextObject* s) {
 }
 
 PyObject* tc_get_stats(TlsContextObject* s, void*) {
+  Py_ssize_t n = 0;
+  for (auto& kv : *s->sessions) n += Py_ssize_t(kv.second.size());
   return Py_BuildValue("{s:K,s:K,s:n}", "handshakes", static_cast<unsigned long long>(s->handshakes), "resumed",
-                       static_cast<unsigned long long>(s->resumed), "cached_sessions",
-                       static_cast<Py_ssize_t>(s->sessions->size()));
+                       static_cast<unsigned long long>(s->resumed), "cached_sessions", n);
 }
 
 PyGetSetDef tc_getset[] = {
@@ -172,7 +182,15 @@ SSL* tls_new_ssl(PyObject* ctx_obj, int fd, const char* host, int port) {
     return nullptr;
   }
   auto it = tc->sessions->find(*key);
-  if (it != tc->sessions->end()) SSL_set_session(ssl, it->second);
+  if (it != tc->sessions->end() && !it->second.empty()) {
+    SSL_SESSION* sess = it->second.back();
+    SSL_set_session(ssl, sess);  // the SSL holds its own reference
+    if (SSL_SESSION_get_protocol_version(sess) == TLS1_3_VERSION) {
+      // TLS 1.3 tickets are single use (RFC 8446 C.4): the resumed connection brings new ones
+      SSL_SESSION_free(sess);
+      it->second.pop_back();
+    }
+  }
   SSL_set_connect_state(ssl);
   return ssl;
 }

@@ -267,3 +267,27 @@ def test_postgres_sslmodes_on_native_tls():
     assert [o[2] for o in nat[0][:3]] == ["TLSv1.3"] * 3 and [o[2] for o in py[0][:3]] == [None] * 3
     assert nat[0][3:5] == ["CERTIFICATE_VERIFY_FAILED"] * 2 and nat[0][5] == 117
     assert nat[1] == py[1]
+
+
+def test_tls13_tickets_are_single_use_and_a_reconnect_burst_resumes():
+    """Each TLS 1.3 ticket resumes one connection (RFC 8446 C.4); the origin's newest tickets
+    (servers send two per connection) let several concurrent reconnects resume."""
+    async def go():
+        s = await TlsServer(lambda t: ok()).start()
+        c = H1Client(timeout_s=5, ssl_cafile=TLS_CERT)
+        url = f"https://127.0.0.1:{s.port}/x"
+        await c.request("GET", url)
+        await asyncio.sleep(0.02)  # the tickets arrive after the handshake
+        t = c._native_tls()
+        cached0 = t.stats["cached_sessions"]
+        for o in c._origins.values():
+            while o.idle:
+                c._drop(o.idle.pop())
+        await asyncio.gather(*[c.request("GET", url) for _ in range(cached0)])
+        st = t.stats
+        await c.close()
+        await s.stop()
+        return cached0, st
+    cached0, st = run(go())
+    assert cached0 >= 2
+    assert st["handshakes"] == 1 + cached0 and st["resumed"] == cached0
