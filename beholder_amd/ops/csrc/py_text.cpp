@@ -649,27 +649,58 @@ bool unreserved(unsigned char c, bool rfc3986) {
   return !rfc3986 && (c == '!' || c == '*' || c == '\'' || c == '(' || c == ')');
 }
 
+// unreserved(c, rfc3986) as two 256-entry tables
+struct UnreservedTables {
+  bool t[2][256];
+  UnreservedTables() {
+    for (int m = 0; m < 2; ++m)
+      for (int c = 0; c < 256; ++c) t[m][c] = unreserved(static_cast<unsigned char>(c), m == 1);
+  }
+};
+const UnreservedTables kUnreserved;
+
+// Percent-encodes the UTF-8 bytes s[0..n) (every byte that is not unreserved), writing into
+// the output's buffer directly (one resize, no per-byte capacity checks).
 void quote_append(std::string& out, const char* s, size_t n, bool rfc3986 = false) {
   static const char* hex = "0123456789ABCDEF";
+  const bool* t = kUnreserved.t[rfc3986 ? 1 : 0];
+  size_t old = out.size();
+  out.resize(old + 3 * n);
+  char* p = &out[old];
   for (size_t i = 0; i < n; ++i) {
     unsigned char c = static_cast<unsigned char>(s[i]);
-    if (unreserved(c, rfc3986)) {
-      out += char(c);
+    if (t[c]) {
+      *p++ = char(c);
     } else {
-      out += '%';
-      out += hex[c >> 4];
-      out += hex[c & 15];
+      p[0] = '%';
+      p[1] = hex[c >> 4];
+      p[2] = hex[c & 15];
+      p += 3;
     }
   }
+  out.resize(size_t(p - out.data()));
+}
+
+// quote_append of String(v): a str is encoded from its UTF-8 form in place (a lone surrogate
+// raises, as encodeURIComponent throws URIError); other values through a scratch buffer.
+bool quote_js_str_append(std::string& out, PyObject* v, bool rfc3986) {
+  if (PyUnicode_CheckExact(v)) {
+    Py_ssize_t n;
+    const char* s = PyUnicode_AsUTF8AndSize(v, &n);
+    if (!s) return false;
+    quote_append(out, s, size_t(n), rfc3986);
+    return true;
+  }
+  std::string tmp;  // short (numbers, booleans): stays in the small-string buffer
+  if (!js_str_append(tmp, v)) return false;
+  quote_append(out, tmp.data(), tmp.size(), rfc3986);
+  return true;
 }
 
 // querystring value rendering: None -> "", bool -> true/false, numbers JS-style
 bool qs_value_append(std::string& out, PyObject* v, bool rfc3986 = false) {
-  std::string tmp;
   if (v == Py_None) return true;
-  if (!js_str_append(tmp, v)) return false;
-  quote_append(out, tmp.data(), tmp.size(), rfc3986);
-  return true;
+  return quote_js_str_append(out, v, rfc3986);
 }
 
 PyObject* mod_quote_component(PyObject*, PyObject* v) {
@@ -719,9 +750,7 @@ PyObject* mod_encode_query_impl(PyObject* m, bool rfc3986) {
     if (v == Py_None) continue;  // undefined: qs omits the key
     if (!first) out += '&';
     first = false;
-    std::string ks;
-    if (!js_str_append(ks, k)) return nullptr;
-    quote_append(out, ks.data(), ks.size(), rfc3986);
+    if (!quote_js_str_append(out, k, rfc3986)) return nullptr;
     out += '=';
     if (!qs_value_append(out, v, rfc3986)) return nullptr;
   }
@@ -894,9 +923,7 @@ bool text_query_pair_append(std::string& out, PyObject* k, PyObject* v, bool* fi
   if (v == Py_None) return true;
   if (!*first) out += '&';
   *first = false;
-  std::string ks;
-  if (!js_str_append(ks, k)) return false;
-  quote_append(out, ks.data(), ks.size(), rfc3986);
+  if (!quote_js_str_append(out, k, rfc3986)) return false;
   out += '=';
   return qs_value_append(out, v, rfc3986);
 }
