@@ -450,9 +450,10 @@ class H1Client(HttpClient):
         return url, o, target, rest
 
     def request(self, method, url, *, params=None, timeout=None):
-        """Awaitable :class:`HttpResponse`. On a warm pool the native fast path
-        (``ops/csrc/py_h1call.cpp`` ``h1_fast``) sends the request right here and completes a
-        plain reply in C; every other case is :meth:`_request`."""
+        """Awaitable :class:`HttpResponse`. For a stock client this is a native ``H1Call``
+        (``ops/csrc/py_h1call.cpp``): like a coroutine it does nothing until awaited; then, on a
+        warm pool, it sends the request and completes a plain reply in C, and in every other
+        case it delegates to :meth:`_request`."""
         call = _h1_fast(self, method, url, params, timeout)
         if call is not None:
             return call
