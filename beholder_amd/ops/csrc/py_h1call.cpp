@@ -43,6 +43,7 @@ int iofuture_peek(PyObject* f, PyObject** result);
 PyObject* iofuture_yield(PyObject* f);
 bool is_netconn(PyObject* o);
 bool netconn_open(PyObject* o);
+PyObject* netconn_loop(PyObject* o);
 int netconn_h1_request(PyObject* o, const std::string& data, PyObject* waiter, bool head);
 bool text_query_pair_append(std::string& out, PyObject* k, PyObject* v, bool* first, bool rfc3986);
 
@@ -98,6 +99,7 @@ struct State {
   Slots conn, origin, resp;
   PyTypeObject* client_type = nullptr;
   PyObject* get_running_loop = nullptr;
+  PyObject* base_time = nullptr;  // asyncio.BaseEventLoop.time (time.monotonic())
   bool ready = false;
 } g;
 
@@ -678,14 +680,20 @@ int h1_start(H1CallObject* s) {
     if (!nu) return -1;
     g.conn.set(conn, C_USES, nu);
   }
-  PyObject* loop = PyObject_CallNoArgs(g.get_running_loop);
-  if (!loop) return -1;
+  // the connection's loop (asyncio.get_running_loop() would cost a getpid(2) per request)
+  PyObject* loop = netconn_loop(g.conn.get(conn, C_NET));
+  Py_INCREF(loop);
   Own own_loop{loop};
-  PyObject* now = PyObject_CallMethodNoArgs(loop, s_time);
-  if (!now) return -1;
-  double dl = PyFloat_AsDouble(now);
-  Py_DECREF(now);
-  if (dl == -1.0 && PyErr_Occurred()) return -1;
+  double dl;
+  if (g.base_time && _PyType_Lookup(Py_TYPE(loop), s_time) == g.base_time) {
+    dl = mono_s();  // BaseEventLoop.time() is time.monotonic()
+  } else {
+    PyObject* now = PyObject_CallMethodNoArgs(loop, s_time);
+    if (!now) return -1;
+    dl = PyFloat_AsDouble(now);
+    Py_DECREF(now);
+    if (dl == -1.0 && PyErr_Occurred()) return -1;
+  }
   PyObject* tmo = timeout;  // `timeout or self.timeout_s`
   if (tmo) {
     int truth = PyObject_IsTrue(tmo);
@@ -805,6 +813,14 @@ PyObject* mod_h1_setup(PyObject*, PyObject* args) {
   Py_XSETREF(g.client_type, reinterpret_cast<PyTypeObject*>(client_cls));
   Py_INCREF(grl);
   Py_XSETREF(g.get_running_loop, grl);
+  PyObject* be = PyImport_ImportModule("asyncio.base_events");
+  PyObject* cls = be ? PyObject_GetAttrString(be, "BaseEventLoop") : nullptr;
+  Py_XDECREF(be);
+  if (!cls) return nullptr;
+  PyObject* bt = _PyType_Lookup(reinterpret_cast<PyTypeObject*>(cls), s_time);
+  Py_XINCREF(bt);
+  Py_XSETREF(g.base_time, bt);
+  Py_DECREF(cls);
   g.ready = true;
   Py_RETURN_NONE;
 }

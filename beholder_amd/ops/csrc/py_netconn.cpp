@@ -901,6 +901,8 @@ PyGetSetDef nc_getset[] = {
 
 bool is_netconn(PyObject* o) { return Py_TYPE(o) == &NetConnType; }
 
+PyObject* netconn_loop(PyObject* o) { return reinterpret_cast<NetConnObject*>(o)->loop; }
+
 bool netconn_open(PyObject* o) {
   NetConnObject* c = reinterpret_cast<NetConnObject*>(o);
   return c->fd >= 0 && !c->closed;
