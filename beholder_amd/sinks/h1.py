@@ -570,6 +570,10 @@ class H1Client(HttpClient):
         out = dict(self.counts)
         out["open"] = sum(o.open for o in self._origins.values())
         out["idle"] = sum(len(o.idle) for o in self._origins.values())
+        if self._ntls:  # native TLS: full and resumed handshakes (beholder_pool{pool="http"})
+            t = self._ntls.stats
+            out["tls_handshakes"] = t["handshakes"]
+            out["tls_resumed"] = t["resumed"]
         return out
 
     async def close(self) -> None:

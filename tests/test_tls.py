@@ -201,6 +201,8 @@ def test_server_close_then_reconnect_resumes_the_session():
             await asyncio.sleep(0.01)
         stats = c._native_tls().stats
         st = dict(c.counts)
+        cs = c.stats()
+        assert (cs["tls_handshakes"], cs["tls_resumed"]) == (stats["handshakes"], stats["resumed"])
         await c.close()
         await s.stop()
         return statuses, stats, st, s.connections
