@@ -293,3 +293,50 @@ def test_tls13_tickets_are_single_use_and_a_reconnect_burst_resumes():
     cached0, st = run(go())
     assert cached0 >= 2
     assert st["handshakes"] == 1 + cached0 and st["resumed"] == cached0
+
+
+def test_garbage_on_an_established_tls_connection():
+    """Bytes that are not TLS records on an established connection (a broken middlebox): the
+    connection is failed, the idempotent request is retried once on a fresh connection (as on
+    the asyncio path), a POST fails with an error, and the pool keeps working."""
+    state = {"n": 0}
+
+    class Broken(TlsServer):
+        async def _serve(self, r, w):
+            self.connections += 1
+            try:
+                while True:
+                    try:
+                        await r.readuntil(b"\r\n\r\n")
+                    except (asyncio.IncompleteReadError, ConnectionError, ssl.SSLError):
+                        return
+                    state["n"] += 1
+                    if state["n"] in (2, 4):  # raw bytes under the TLS layer instead of a record
+                        os.write(w.transport.get_extra_info("socket").fileno(), b"\x17\x03\x03\x00\x05junk!" * 3)
+                        await asyncio.sleep(0.05)
+                        w.transport.abort()
+                        return
+                    w.write(ok())
+                    await w.drain()
+            finally:
+                w.close()
+
+    async def go(native):
+        state["n"] = 0
+        s = await Broken(None).start()
+        c = H1Client(timeout_s=5, ssl_cafile=TLS_CERT)
+        url = f"https://127.0.0.1:{s.port}/x"
+        out = [(await c.request("GET", url)).status]
+        out.append((await c.request("GET", url)).status)  # 2nd answered with junk: retried
+        try:
+            await c.request("POST", url)  # 4th answered with junk: not replayed
+            out.append("no error")
+        except HttpError:
+            out.append("error")
+        out.append((await c.request("GET", url)).status)
+        st = dict(c.counts)
+        await c.close()
+        await s.stop()
+        return out, st["retries"], st["errors"]
+    nat, py = _both(go)
+    assert nat == py and nat[0] == [200, 200, "error", 200] and nat[1] == 1 and nat[2] == 1
