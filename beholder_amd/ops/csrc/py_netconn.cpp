@@ -29,6 +29,9 @@
 #include <errno.h>
 #include <openssl/err.h>
 #include <openssl/ssl.h>
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -69,6 +72,7 @@ struct NetConnObject {
   uint8_t closed;
   uint8_t writing;          // add_writer registered
   uint8_t flush_scheduled;  // pg: a call_soon(flush) is pending
+  uint8_t connecting;       // created by netconn_connect: the TCP connect is in progress
   PyObject* loop;
   PyObject* owner;
   PyObject* on_readable;  // bound builtins handed to the loop
@@ -195,6 +199,7 @@ int watch_writes(NetConnObject* c) {
 int send_out_tls(NetConnObject* c);
 
 int send_out(NetConnObject* c) {
+  if (c->connecting) return 0;  // queued until the connect completes
   if (c->ssl) return send_out_tls(c);
   std::string& o = *c->out;
   size_t off = 0;
@@ -574,7 +579,7 @@ int nc_init(NetConnObject* c, PyObject* args, PyObject* kwds) {
   Py_DECREF(r);
   c->fd = fd;  // owned from here on
   c->closed = 0;
-  if (c->ssl) {
+  if (c->ssl && !c->connecting) {
     c->tls_state = 1;
     if (tls_handshake(c) < 0) return -1;  // ClientHello goes out now
   }
@@ -583,8 +588,45 @@ int nc_init(NetConnObject* c, PyObject* args, PyObject* kwds) {
 
 PyObject* on_readable_tls(NetConnObject* c, char* buf);
 
+// The socket of a connecting NetConn became writable (or reported an error): finish the
+// connect. Failure: the ready future is rejected with the OSError and the socket closed.
+// Success: TLS starts its handshake; plain TCP resolves the ready future.
+int connect_done(NetConnObject* c) {
+  int err = 0;
+  socklen_t len = sizeof err;
+  if (getsockopt(c->fd, SOL_SOCKET, SO_ERROR, &err, &len) < 0) err = errno;
+  if (err == EINPROGRESS || err == EALREADY) return 0;  // spurious wake-up
+  c->connecting = 0;
+  if (err) {
+    errno = err;
+    PyErr_SetFromErrno(PyExc_OSError);
+    PyObject *et, *ev, *tb;
+    PyErr_Fetch(&et, &ev, &tb);
+    PyErr_NormalizeException(&et, &ev, &tb);
+    Py_XDECREF(et);
+    Py_XDECREF(tb);
+    shut(c);
+    hs_fail(c, ev);
+    Py_XDECREF(ev);
+    return 0;
+  }
+  if (unwatch_writes(c) < 0) return -1;
+  if (c->ssl) {
+    c->tls_state = 1;
+    return tls_handshake(c);
+  }
+  PyObject* f = c->hs_fut;
+  if (f && !iofuture_done(f) && iofuture_resolve(f, Py_None) < 0) return -1;
+  if (c->fd >= 0 && !c->out->empty()) return send_out(c);
+  return 0;
+}
+
 PyObject* nc_on_readable(NetConnObject* c, PyObject*) {
   if (c->fd < 0) Py_RETURN_NONE;
+  if (c->connecting) {
+    if (connect_done(c) < 0) return nullptr;
+    Py_RETURN_NONE;
+  }
   char* buf = read_buf();
   if (!buf) return PyErr_NoMemory();
   if (c->ssl) return on_readable_tls(c, buf);
@@ -679,6 +721,10 @@ PyObject* on_readable_tls(NetConnObject* c, char* buf) {
 
 PyObject* nc_on_writable(NetConnObject* c, PyObject*) {
   if (c->fd < 0) Py_RETURN_NONE;
+  if (c->connecting) {
+    if (connect_done(c) < 0) return nullptr;
+    Py_RETURN_NONE;
+  }
   if (c->ssl && c->tls_state == 1) {
     if (tls_handshake(c) < 0) return nullptr;
     Py_RETURN_NONE;
@@ -938,6 +984,93 @@ namespace {
 
 PyObject *s_closed_name, *s_net_name;
 
+// netconn_connect(ip, port, loop, kind, owner, parser, **NetConn keywords) -> NetConn
+// A non-blocking TCP connect to the IP literal `ip` (IPv4 or IPv6) made here, without an asyncio
+// transport: socket(2) + TCP_NODELAY + connect(2), then the NetConn watches for completion. Its
+// `handshake` future resolves once the connection is usable (after the TLS handshake for `tls=`),
+// or is rejected with the connect OSError (ECONNREFUSED, ...) or the TLS failure.
+PyObject* mod_netconn_connect(PyObject*, PyObject* args, PyObject* kwds) {
+  const char* ip;
+  int port;
+  PyObject *loop, *kind, *owner, *parser;
+  if (!PyArg_ParseTuple(args, "siOOOO", &ip, &port, &loop, &kind, &owner, &parser)) return nullptr;
+  sockaddr_storage ss;
+  socklen_t slen;
+  int family;
+  memset(&ss, 0, sizeof ss);
+  auto* s4 = reinterpret_cast<sockaddr_in*>(&ss);
+  auto* s6 = reinterpret_cast<sockaddr_in6*>(&ss);
+  if (inet_pton(AF_INET, ip, &s4->sin_addr) == 1) {
+    family = AF_INET;
+    s4->sin_family = AF_INET;
+    s4->sin_port = htons(uint16_t(port));
+    slen = sizeof *s4;
+  } else if (inet_pton(AF_INET6, ip, &s6->sin6_addr) == 1) {
+    family = AF_INET6;
+    s6->sin6_family = AF_INET6;
+    s6->sin6_port = htons(uint16_t(port));
+    slen = sizeof *s6;
+  } else {
+    PyErr_Format(PyExc_ValueError, "netconn_connect: not an IP address: %s", ip);
+    return nullptr;
+  }
+  if (port <= 0 || port > 65535) {
+    PyErr_SetString(PyExc_ValueError, "netconn_connect: bad port");
+    return nullptr;
+  }
+  int fd = ::socket(family, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+  if (fd < 0) return PyErr_SetFromErrno(PyExc_OSError);
+  int one = 1;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);  // small requests go out at once (as asyncio)
+  int rc;
+  do {
+    rc = ::connect(fd, reinterpret_cast<sockaddr*>(&ss), slen);
+  } while (rc < 0 && errno == EINTR);
+  int cerr = rc < 0 ? errno : 0;
+  if (cerr && cerr != EINPROGRESS) {
+    ::close(fd);
+    errno = cerr;
+    return PyErr_SetFromErrno(PyExc_OSError);
+  }
+  // NetConn(fd, loop, kind, owner, parser, **kwds) with the connect pending: the TLS handshake
+  // waits for connect_done()
+  PyObject* fdo = PyLong_FromLong(fd);
+  PyObject* a5 = fdo ? PyTuple_Pack(5, fdo, loop, kind, owner, parser) : nullptr;
+  Py_XDECREF(fdo);
+  if (!a5) {
+    ::close(fd);
+    return nullptr;
+  }
+  NetConnObject* c = reinterpret_cast<NetConnObject*>(NetConnType.tp_new(&NetConnType, a5, kwds));
+  if (!c) {
+    Py_DECREF(a5);
+    ::close(fd);
+    return nullptr;
+  }
+  c->connecting = 1;  // nc_init: no handshake yet
+  int ok = NetConnType.tp_init(reinterpret_cast<PyObject*>(c), a5, kwds);
+  Py_DECREF(a5);
+  if (ok < 0) {
+    if (c->fd < 0) ::close(fd);  // not owned yet
+    Py_DECREF(c);
+    return nullptr;
+  }
+  if (!c->hs_fut && !(c->hs_fut = iofuture_new(loop))) {
+    Py_DECREF(c);
+    return nullptr;
+  }
+  if (cerr == 0) {  // connected at once (loopback can): finish now
+    if (connect_done(c) < 0) {
+      Py_DECREF(c);
+      return nullptr;
+    }
+  } else if (watch_writes(c) < 0) {
+    Py_DECREF(c);
+    return nullptr;
+  }
+  return reinterpret_cast<PyObject*>(c);
+}
+
 // pg_pool_execute(conns, sql, params, spread_at, size) -> IOFuture, or None for the Python path.
 // store/pgwire.py Pool.execute for a pool whose open connections are all native: the open
 // connection with the fewest queries in flight (the first on ties) gets the query, unless every
@@ -980,6 +1113,10 @@ PyObject* mod_pg_pool_execute(PyObject*, PyObject* const* a, Py_ssize_t n) {
 }
 
 PyMethodDef pool_functions[] = {
+    {"netconn_connect", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(mod_netconn_connect)),
+     METH_VARARGS | METH_KEYWORDS,
+     "netconn_connect(ip, port, loop, kind, owner, parser, **NetConn keywords) -> NetConn; `handshake` resolves once "
+     "connected (and TLS established)"},
     {"pg_pool_execute", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(mod_pg_pool_execute)),
      METH_FASTCALL, "pg_pool_execute(conns, sql, params, spread_at, size) -> IOFuture or None (store/pgwire.py Pool)"},
     {nullptr, nullptr, 0, nullptr}};

@@ -30,7 +30,9 @@ from __future__ import annotations
 import asyncio
 import base64
 import collections
+import ipaddress
 import os
+import socket
 import ssl as _ssl
 import time
 from typing import Deque, Dict, Optional, Tuple
@@ -40,6 +42,8 @@ from ..ops import H1Parser
 from ..ops import IOFuture as _IOFuture
 from ..ops import encode_query as _encode_query
 from ..ops import native as _native
+
+_netconn_connect = _native.netconn_connect
 from ..utils import netconn
 from .http import HttpClient, HttpError, HttpResponse, encode_query, redact, with_query
 
@@ -64,12 +68,14 @@ class _Reset(Exception):
 
 
 class _Conn(asyncio.Protocol):
-    """One keep-alive connection. A plain-TCP connection is handed to a native ``NetConn``
-    (``net``) once connected (utils/netconn.py): replies are then parsed and delivered in C and
-    the methods below only see its rare paths (``_net_lost``, ``_net_error``)."""
+    """One keep-alive connection. Normally its socket is a native ``NetConn`` (``net``) that
+    connected it (and runs its TLS) in C (``ops netconn_connect``): replies are parsed and
+    delivered in C and the methods below only see its rare paths (``_net_lost``,
+    ``_net_error``). With native connections off, or a caller-supplied ``ssl.SSLContext``, it
+    is an asyncio protocol on an ordinary transport."""
 
     __slots__ = ("origin", "parser", "transport", "waiter", "closed", "last_used", "uses", "deadline", "what",
-                 "net", "adopt_plan", "adopt_error")
+                 "net")
 
     def __init__(self, origin: "_Origin"):
         self.origin = origin
@@ -82,24 +88,10 @@ class _Conn(asyncio.Protocol):
         self.uses = 0
         self.deadline = 0.0
         self.what = ("", "")
-        self.adopt_plan = None  # True (plain TCP) or (TlsContext, host, port): adopt in connection_made
-        self.adopt_error: Optional[BaseException] = None
 
-    # -- protocol callbacks --------------------------------------------------
+    # -- protocol callbacks (asyncio transports: BEHOLDER_NATIVE_NET=0, caller-supplied TLS) ------
     def connection_made(self, transport):
         self.transport = transport
-        plan = self.adopt_plan
-        if plan is not None:  # before asyncio starts reading: no byte can reach the asyncio transport
-            self.adopt_plan = None
-            loop = asyncio.get_running_loop()
-            try:
-                if plan is True:
-                    self.adopt(loop)
-                else:
-                    self.adopt_tls(loop, *plan)
-            except BaseException as e:  # re-raised by H1Client._connect
-                self.adopt_error = e
-                self.abort()
 
     def data_received(self, data):
         try:
@@ -167,30 +159,6 @@ class _Conn(asyncio.Protocol):
         elif self.transport is not None:
             self.transport.abort()
 
-    def adopt(self, loop) -> bool:
-        """Hand a plain-TCP connection to a native NetConn (utils/netconn.py)."""
-        fd = netconn.adopt(self.transport)
-        if fd is None:
-            return False
-        self.net = netconn.NetConn(fd, loop, "h1", self, self.parser)
-        self.transport = None
-        return True
-
-    def adopt_tls(self, loop, ctx, host: str, port: int) -> bool:
-        """Hand a connected plain-TCP socket to a NetConn that runs TLS natively (ops TlsContext
-        ``ctx``); ``self.net.handshake`` completes when the session is established."""
-        fd = netconn.adopt(self.transport)
-        if fd is None:
-            return False
-        try:
-            self.net = netconn.NetConn(fd, loop, "h1", self, self.parser, tls=ctx, server_hostname=host, port=port,
-                                       tls_error=_tls_error)
-        except BaseException:
-            os.close(fd)
-            raise
-        self.transport = None
-        return True
-
     def timed_out(self) -> None:
         m, url = self.what
         self._fail(HttpError(f"ETIMEDOUT: {m} {redact(url)}"))
@@ -251,6 +219,7 @@ class H1Client(HttpClient):
         self._ssl = ssl_context
         self.ssl_cafile = ssl_cafile
         self._ntls = None
+        self._literal: Dict[str, list] = {}  # hosts that are IP literals: no resolver call
         self._origins: Dict[str, _Origin] = {}
         self._routes: Dict[str, Tuple[_Origin, str, str]] = {}
         self._closed = False
@@ -319,18 +288,11 @@ class H1Client(HttpClient):
             if remaining <= 0:
                 raise asyncio.TimeoutError
             ntls = self._native_tls() if o.tls else None
-            kw = {"ssl": self._ssl_context(), "server_hostname": o.host} if o.tls and ntls is None else {}
-            if ntls is not None:  # TLS in C on the socket (ops/csrc/py_tls.cpp)
-                conn.adopt_plan = (ntls, o.host, o.port)
-            elif not o.tls:
-                conn.adopt_plan = True
-            await asyncio.wait_for(loop.create_connection(lambda: conn, o.host, o.port, **kw), remaining)
-            if conn.adopt_error is not None:
-                raise conn.adopt_error
-            if ntls is not None:
-                if conn.net is None:
-                    raise HttpError(f"cannot start TLS to {o.host}:{o.port}")
-                await asyncio.wait_for(conn.net.handshake, max(deadline - loop.time(), 0.0))
+            if netconn.enabled() and (ntls is not None or not o.tls):
+                await self._connect_native(conn, o, ntls, deadline, loop)
+            else:  # asyncio transport: native connections off, or a caller-supplied ssl.SSLContext
+                kw = {"ssl": self._ssl_context(), "server_hostname": o.host} if o.tls else {}
+                await asyncio.wait_for(loop.create_connection(lambda: conn, o.host, o.port, **kw), remaining)
         except BaseException:
             conn.abort()
             o.open -= 1
@@ -338,6 +300,44 @@ class H1Client(HttpClient):
             raise
         self.counts["connections"] += 1
         return conn
+
+    async def _connect_native(self, conn: _Conn, o: _Origin, ntls, deadline: float, loop) -> None:
+        """TCP connect, and TLS for ``ntls``, in C (``ops netconn_connect``): no asyncio transport
+        is made and dropped. Addresses are tried in order, as ``loop.create_connection`` does
+        (an IP literal as is, a name through ``loop.getaddrinfo``); a TLS failure is final."""
+        infos = self._literal.get(o.host)
+        if infos is None:
+            try:
+                ipaddress.ip_address(o.host)
+                infos = self._literal[o.host] = [o.host]
+            except ValueError:
+                infos = [ai[4][0] for ai in await loop.getaddrinfo(o.host, o.port, type=socket.SOCK_STREAM)]
+        errors = []
+        for ip in infos:
+            remaining = deadline - loop.time()
+            if remaining <= 0:
+                raise asyncio.TimeoutError
+            try:
+                net = _netconn_connect(ip, o.port, loop, "h1", conn, conn.parser, tls=ntls, server_hostname=o.host,
+                                       port=o.port, tls_error=_tls_error)
+            except OSError as e:
+                errors.append(e)
+                continue
+            conn.net = net
+            try:
+                await asyncio.wait_for(net.handshake, remaining)
+                return
+            except _ssl.SSLError:
+                raise
+            except OSError as e:
+                net.abort()
+                conn.net = None
+                errors.append(e)
+        if not errors:
+            raise OSError(f"getaddrinfo returned no addresses for {o.host}")
+        if len(errors) == 1 or all(str(e) == str(errors[0]) for e in errors):
+            raise errors[0]
+        raise OSError("Multiple exceptions: " + ", ".join(str(e) for e in errors))
 
     async def _acquire(self, o: _Origin, deadline: float, fresh: bool = False) -> _Conn:
         now = time.monotonic()

@@ -214,3 +214,42 @@ def test_native_pool_pick_matches_python_pick(monkeypatch):
     assert nat[0] == py[0]
     assert nat[2] == py[2]
     assert "IOFuture" in nat[3]
+
+
+def test_native_connect_refused_localhost_and_ready_future():
+    """ops netconn_connect: the TCP connect made in C (sinks/h1.py _connect_native). A refused
+    connect rejects the ready future with ECONNREFUSED (Node's message via _connect_error); a
+    name tries every resolved address in order (localhost: ::1 then 127.0.0.1 against a server
+    on 127.0.0.1 only); the connection in the pool is a NetConn with no asyncio transport."""
+    import errno as _errno
+
+    from beholder_amd.ops import native
+    from beholder_amd.sinks import HttpError
+
+    async def go():
+        loop = asyncio.get_running_loop()
+        probe = socket.socket()
+        probe.bind(("127.0.0.1", 0))
+        dead_port = probe.getsockname()[1]
+        probe.close()  # nothing listens there now
+        net = native.netconn_connect("127.0.0.1", dead_port, loop, "h1", None, H1Parser())
+        try:
+            await net.handshake
+            refused = None
+        except OSError as e:
+            refused = e.errno
+        s = await test_h1.Scripted(lambda n, m, t, h: test_h1.OK).start()
+        try:
+            c = H1Client(timeout_s=5)
+            r = await c.request("GET", f"http://localhost:{s.port}/x")
+            conn = next(iter(c._origins.values())).idle[0]
+            kinds = (type(conn.net).__name__, conn.transport, conn.net.tls)
+            with pytest.raises(HttpError, match=f"^connect ECONNREFUSED 127.0.0.1:{dead_port}$"):
+                await c.request("GET", f"http://127.0.0.1:{dead_port}/x")
+            await c.close()
+            return refused, r.status, kinds
+        finally:
+            await s.stop()
+    refused, status, kinds = run(go())
+    assert refused == _errno.ECONNREFUSED
+    assert status == 200 and kinds == ("NetConn", None, None)
