@@ -23,6 +23,10 @@
 //                          Describe + Execute + Sync appended to the output, flushed once per
 //                          loop iteration (loop.call_soon), replies matched FIFO.
 //
+// netconn_connect(ip, port, loop, kind, owner, parser, **kw) makes the TCP connection itself
+// (non-blocking connect; `handshake` resolves once it is usable, after TLS when `tls=` is given),
+// so an HTTP sink connection never has an asyncio transport at all.
+//
 // Rare paths call back into Python on `owner`: _net_lost(exc or None) when the peer closes or
 // the socket fails (the fd is already closed and unregistered), _net_error(exc) for a protocol
 // error or an unsolicited reply, _net_message(type, body) for out-of-band Postgres messages.

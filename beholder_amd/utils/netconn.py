@@ -1,5 +1,8 @@
 """Hand an established plain-TCP asyncio connection over to a native ``NetConn``.
 
+(HTTP sink connections do not go through here: they are connected by the NetConn itself,
+``ops.native.netconn_connect``; Postgres connections, authenticated on asyncio first, are.)
+
 ``ops/csrc/py_netconn.cpp`` drives a socket straight from the event loop's selector and does
 the protocol work (HTTP/1.1 response parsing, Postgres reply matching) in C, so a reply costs
 no Python-level transport / protocol frames. Connections are opened, TLS-wrapped and
