@@ -253,3 +253,29 @@ def test_native_connect_refused_localhost_and_ready_future():
     refused, status, kinds = run(go())
     assert refused == _errno.ECONNREFUSED
     assert status == 200 and kinds == ("NetConn", None, None)
+
+
+def test_native_connect_ipv6_literal():
+    """An IPv6 literal origin (``http://[::1]:port``) connects natively over AF_INET6."""
+    async def go():
+        async def serve(r, w):
+            await r.readuntil(b"\r\n\r\n")
+            w.write(b"HTTP/1.1 200 OK\r\nContent-Length: 2\r\n\r\nv6")
+            await w.drain()
+            w.close()
+        try:
+            srv = await asyncio.start_server(serve, "::1", 0)
+        except OSError:
+            return None
+        port = srv.sockets[0].getsockname()[1]
+        c = H1Client(timeout_s=5)
+        try:
+            r = await c.request("GET", f"http://[::1]:{port}/x")
+            return r.status, r.body
+        finally:
+            await c.close()
+            srv.close()
+    res = run(go())
+    if res is None:
+        pytest.skip("no IPv6 loopback")
+    assert res == (200, b"v6")
