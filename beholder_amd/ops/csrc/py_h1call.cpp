@@ -98,7 +98,6 @@ const char* const kRespSlots[R_N] = {"status", "body", "_headers", "_raw", "url"
 struct State {
   Slots conn, origin, resp;
   PyTypeObject* client_type = nullptr;
-  PyObject* get_running_loop = nullptr;
   PyObject* base_time = nullptr;  // asyncio.BaseEventLoop.time (time.monotonic())
   bool ready = false;
 } g;
@@ -793,10 +792,10 @@ PyObject* mod_h1_fast(PyObject*, PyObject* const* a, Py_ssize_t n) {
   return reinterpret_cast<PyObject*>(call);
 }
 
-// h1_setup(client_cls, conn_cls, origin_cls, response_cls, get_running_loop)
+// h1_setup(client_cls, conn_cls, origin_cls, response_cls)
 PyObject* mod_h1_setup(PyObject*, PyObject* args) {
-  PyObject *client_cls, *conn_cls, *origin_cls, *resp_cls, *grl;
-  if (!PyArg_ParseTuple(args, "OOOOO", &client_cls, &conn_cls, &origin_cls, &resp_cls, &grl)) return nullptr;
+  PyObject *client_cls, *conn_cls, *origin_cls, *resp_cls;
+  if (!PyArg_ParseTuple(args, "OOOO", &client_cls, &conn_cls, &origin_cls, &resp_cls)) return nullptr;
   g.ready = false;
   if (!PyType_Check(client_cls)) {
     PyErr_SetString(PyExc_TypeError, "h1_setup: client_cls must be a class");
@@ -811,8 +810,6 @@ PyObject* mod_h1_setup(PyObject*, PyObject* args) {
   }
   Py_INCREF(client_cls);
   Py_XSETREF(g.client_type, reinterpret_cast<PyTypeObject*>(client_cls));
-  Py_INCREF(grl);
-  Py_XSETREF(g.get_running_loop, grl);
   PyObject* be = PyImport_ImportModule("asyncio.base_events");
   PyObject* cls = be ? PyObject_GetAttrString(be, "BaseEventLoop") : nullptr;
   Py_XDECREF(be);
@@ -835,7 +832,7 @@ PyMethodDef h1_functions[] = {
      "h1_fast(client, method, url, params=None, timeout=None) -> awaitable H1Call, or None for the Python path "
      "(sinks/h1.py)"},
     {"h1_setup", mod_h1_setup, METH_VARARGS,
-     "h1_setup(H1Client, _Conn, _Origin, HttpResponse, get_running_loop): enable h1_fast for these classes"},
+     "h1_setup(H1Client, _Conn, _Origin, HttpResponse): enable h1_fast for these classes"},
     {"h1_disable", mod_h1_disable, METH_NOARGS, "h1_disable(): h1_fast always returns None"},
     {nullptr, nullptr, 0, nullptr}};
 

@@ -627,7 +627,7 @@ def _h1_python_only(client, method, url, params, timeout):
 # Native fast path of H1Client.request (ops/csrc/py_h1call.cpp). BEHOLDER_NATIVE_H1=0 keeps every
 # request on the Python path (A/B runs, debugging); so does the plain-asyncio-future A/B switch.
 if os.environ.get("BEHOLDER_NATIVE_H1", "1") != "0" and _IOFuture is _native.IOFuture:
-    _native.h1_setup(H1Client, _Conn, _Origin, HttpResponse, asyncio.get_running_loop)
+    _native.h1_setup(H1Client, _Conn, _Origin, HttpResponse)
     _h1_fast = _native.h1_fast
 else:
     _h1_fast = _h1_python_only
