@@ -1000,7 +1000,28 @@ PyObject* iofuture_new(PyObject* loop) {
   return f;
 }
 
-bool iofuture_done(PyObject* f) { return reinterpret_cast<IOFutureObject*>(f)->state != 0; }
+PyObject* interned(PyObject** slot, const char* text) {
+  if (!*slot) *slot = PyUnicode_InternFromString(text);
+  return *slot;
+}
+PyObject *g_done_name, *g_set_result_name, *g_set_exception_name;
+#define s_done_name interned(&g_done_name, "done")
+#define s_set_result_name interned(&g_set_result_name, "set_result")
+#define s_set_exception_name interned(&g_set_exception_name, "set_exception")
+
+// The helpers below also accept a foreign future (an asyncio.Future: the BEHOLDER_IOFUTURE=0
+// A/B switch hands those to a NetConn as reply waiters); it goes through its Python methods.
+bool iofuture_done(PyObject* f) {
+  if (Py_TYPE(f) == &IOFutureType) return reinterpret_cast<IOFutureObject*>(f)->state != 0;
+  PyObject* r = PyObject_CallMethodNoArgs(f, s_done_name);
+  int d = r ? PyObject_IsTrue(r) : -1;
+  Py_XDECREF(r);
+  if (d < 0) {
+    PyErr_WriteUnraisable(f);
+    return true;  // unusable: treat as finished (nothing is delivered to it)
+  }
+  return d != 0;
+}
 
 // 0 pending; 1 finished with a result (*result borrowed); 2 finished with an exception or cancelled
 int iofuture_peek(PyObject* f, PyObject** result) {
@@ -1021,7 +1042,8 @@ PyObject* iofuture_yield(PyObject* f) {
 // resolve / reject unless already finished: 0 ok (or already done), -1 error
 int iofuture_resolve(PyObject* f, PyObject* v) {
   if (iofuture_done(f)) return 0;
-  PyObject* r = iof_finish_result(reinterpret_cast<IOFutureObject*>(f), v, true);
+  PyObject* r = Py_TYPE(f) == &IOFutureType ? iof_finish_result(reinterpret_cast<IOFutureObject*>(f), v, true)
+                                            : PyObject_CallMethodOneArg(f, s_set_result_name, v);
   if (!r) return -1;
   Py_DECREF(r);
   return 0;
@@ -1029,7 +1051,8 @@ int iofuture_resolve(PyObject* f, PyObject* v) {
 
 int iofuture_reject(PyObject* f, PyObject* exc) {
   if (iofuture_done(f)) return 0;
-  PyObject* r = iof_finish_exc(reinterpret_cast<IOFutureObject*>(f), exc, true);
+  PyObject* r = Py_TYPE(f) == &IOFutureType ? iof_finish_exc(reinterpret_cast<IOFutureObject*>(f), exc, true)
+                                            : PyObject_CallMethodOneArg(f, s_set_exception_name, exc);
   if (!r) return -1;
   Py_DECREF(r);
   return 0;

@@ -11,6 +11,9 @@ from beholder_amd.ops import native
 from beholder_amd.sinks import H1Client, HttpError
 from beholder_amd.sinks import h1 as h1mod
 
+pytestmark = pytest.mark.skipif(h1mod._h1_fast is h1mod._h1_python_only,
+                                reason="native H1 path switched off (BEHOLDER_NATIVE_H1=0 / BEHOLDER_IOFUTURE=0)")
+
 
 def run(coro):
     return asyncio.run(asyncio.wait_for(coro, 30))

@@ -279,3 +279,16 @@ def test_native_connect_ipv6_literal():
     if res is None:
         pytest.skip("no IPv6 loopback")
     assert res == (200, b"v6")
+
+
+@pytest.mark.parametrize("env", ["BEHOLDER_IOFUTURE", "BEHOLDER_NATIVE_H1", "BEHOLDER_NATIVE_TLS"])
+def test_switched_off_paths_still_work(env):
+    """Each A/B switch (read at import) leaves a working client: the H1 and TLS suites pass with
+    it set to 0 (a NetConn then also completes plain asyncio futures as reply waiters)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-p", "no:cacheprovider", "-x",
+                        "tests/test_h1.py", "tests/test_tls.py"], cwd=root, capture_output=True, text=True,
+                       env=dict(os.environ, **{env: "0"}), timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
