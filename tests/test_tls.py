@@ -73,8 +73,8 @@ def native_tls(c):
 
 def test_native_tls_requests_take_the_fast_path():
     from beholder_amd.sinks import h1
-    if h1._h1_fast is h1._h1_python_only:
-        pytest.skip("native H1 path switched off (BEHOLDER_NATIVE_H1=0 / BEHOLDER_IOFUTURE=0)")
+    if h1._h1_fast is h1._h1_python_only or os.environ.get("BEHOLDER_NATIVE_TLS", "1") == "0":
+        pytest.skip("native H1 / TLS path switched off")
 
     async def go():
         s = await TlsServer(lambda t: ok()).start()
