@@ -63,6 +63,10 @@ class TlsServer:
             w.close()
 
 
+requires_native_tls = pytest.mark.skipif(os.environ.get("BEHOLDER_NATIVE_TLS", "1") == "0",
+                                         reason="inspects native TLS state; BEHOLDER_NATIVE_TLS=0")
+
+
 def ok(body=b"{}"):
     return b"HTTP/1.1 200 OK\r\nContent-Length: %d\r\n\r\n" % len(body) + body
 
@@ -189,6 +193,7 @@ def test_plain_http_server_and_handshake_timeout():
     assert run(silent()) == 0
 
 
+@requires_native_tls
 def test_server_close_then_reconnect_resumes_the_session():
     async def go():
         n = {"i": 0}
@@ -215,6 +220,7 @@ def test_server_close_then_reconnect_resumes_the_session():
     assert stats["handshakes"] == conns and stats["resumed"] >= conns - 2  # tickets reused on reconnect
 
 
+@requires_native_tls
 def test_tls12_server_and_caller_context_keeps_asyncio_path():
     ctx12 = server_ssl_context()
     ctx12.maximum_version = ssl.TLSVersion.TLSv1_2
@@ -275,6 +281,7 @@ def test_postgres_sslmodes_on_native_tls():
     assert nat[1] == py[1]
 
 
+@requires_native_tls
 def test_tls13_tickets_are_single_use_and_a_reconnect_burst_resumes():
     """Each TLS 1.3 ticket resumes one connection (RFC 8446 C.4); the origin's newest tickets
     (servers send two per connection) let several concurrent reconnects resume."""
