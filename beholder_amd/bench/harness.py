@@ -416,11 +416,15 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             cold = dict(src.settler.handle_latency.summary())
             src.settler.reset_latency()
             settled0 = _settled(src.settler)
+            gc.collect()
+            rss0 = _rss_mb()  # pools full, code paths warm: later growth would be a leak
             ru0 = resource.getrusage(resource.RUSAGE_SELF)
             t0 = time.perf_counter()
             await _wait_acked(src.settler, n, task)
             elapsed = time.perf_counter() - t0
             ru1 = resource.getrusage(resource.RUSAGE_SELF)
+            gc.collect()
+            rss1 = _rss_mb()
             measured = _settled(src.settler) - settled0
             await asyncio.sleep(0.05)  # let the last acks flush
             svc.request_stop()
@@ -431,9 +435,9 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             await svc.close()
             sink.close()
             cpu = (ru1.ru_utime + ru1.ru_stime) - (ru0.ru_utime + ru0.ru_stime)
-            return elapsed, stats, cpu, ru1.ru_stime - ru0.ru_stime, pg_conns, http_stats, measured, cold
+            return elapsed, stats, cpu, ru1.ru_stime - ru0.ru_stime, pg_conns, http_stats, measured, cold, rss1 - rss0
 
-        elapsed, stats, cpu, sys_s, pg_conns, http_stats, m, cold = asyncio.run(go())
+        elapsed, stats, cpu, sys_s, pg_conns, http_stats, m, cold, rss_growth = asyncio.run(go())
         acked = stats["source"]["acked"]
         out.update({
             "acked": acked, "warmup_events": warm, "measured_events": m, "elapsed_s": elapsed,
@@ -443,7 +447,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             "handle_latency_us": {k: v / 1e3 for k, v in stats["handle_latency_ns"].items() if k.startswith("p")},
             "warmup_handle_latency_us": {k: v / 1e3 for k, v in cold.items() if k.startswith("p")},
             "errors": sum(stats.get("handler_errors", {}).values()),
-            "pg_connections": pg_conns, "http": http_stats,
+            "pg_connections": pg_conns, "http": http_stats, "rss_growth_mb": round(rss_growth, 2),
         })
     finally:
         counters = _reap(procs)

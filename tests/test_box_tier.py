@@ -143,6 +143,16 @@ def test_tls_e2e_https_sinks_on_native_tls():
     assert res["http"]["connections"] <= 100  # keep-alive: no reconnect churn
 
 
+def test_tls_e2e_million_events_memory_flat():
+    """1M events over every native socket path (AMQP, Postgres NetConns, HTTPS sinks on native TLS
+    with H1Call): the process RSS after the run is within a few MB of the warm start (a leak of a
+    few bytes per request would show as tens of MB)."""
+    from beholder_amd.bench import harness
+    res = harness.run_config("tls_e2e", events=1_000_000)
+    assert res["acked"] == 1_000_000 and res["errors"] == 0, res
+    assert res["rss_growth_mb"] < 16, res["rss_growth_mb"]
+
+
 def test_http_tcp_both_clients_error_free():
     """Sinks over real TCP with the default keep-alive client and with aiohttp: every event
     acked, no handler errors (aiohttp under the native Driver needs its own task)."""
