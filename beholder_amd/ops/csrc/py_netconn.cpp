@@ -170,8 +170,9 @@ void notify(NetConnObject* c, PyObject* name, PyObject* arg) {
 // Peer closed (exc NULL) or the socket failed: close, then tell the owner.
 void lost(NetConnObject* c, int err) {
   shut(c);
-  hs_fail(c, nullptr);
   if (err) {
+    PyObject *et0, *ev0, *tb0;  // keep a pending exception of the caller intact
+    PyErr_Fetch(&et0, &ev0, &tb0);
     errno = err;
     PyErr_SetFromErrno(PyExc_OSError);
     PyObject *et, *ev, *tb;
@@ -179,9 +180,12 @@ void lost(NetConnObject* c, int err) {
     PyErr_NormalizeException(&et, &ev, &tb);
     Py_XDECREF(et);
     Py_XDECREF(tb);
+    PyErr_Restore(et0, ev0, tb0);
+    hs_fail(c, ev);  // a TLS handshake in progress fails with the socket error itself
     notify(c, s_net_lost, ev);
     Py_XDECREF(ev);
   } else {
+    hs_fail(c, nullptr);
     notify(c, s_net_lost, nullptr);
   }
 }
