@@ -645,7 +645,7 @@ int h1_start(H1CallObject* s) {
     }
     if (closed == Py_False && mono_s() - lu < ka) {
       PyObject* net = g.conn.get(cand, C_NET);
-      if (!net || !is_netconn(net) || !netconn_open(net)) {  // TLS / asyncio transport: Python path
+      if (!net || !is_netconn(net) || !netconn_open(net)) {  // asyncio transport: Python path
         PyObject* r = PyObject_CallMethodOneArg(idle, s_append, cand);
         Py_DECREF(cand);
         if (!r) return -1;
