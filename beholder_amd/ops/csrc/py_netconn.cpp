@@ -36,6 +36,7 @@
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <sys/epoll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -52,6 +53,10 @@ int iofuture_resolve(PyObject* f, PyObject* v);
 int iofuture_reject(PyObject* f, PyObject* exc);
 int pg_bind_append(std::string& o, const char* name, size_t nlen, PyObject* params);
 bool is_tls_context(PyObject* o);
+PyObject* netpoll_for(PyObject* loop);
+int netpoll_add(PyObject* po, int fd, PyObject* conn);
+int netpoll_set_write(PyObject* po, int fd, bool write);
+void netpoll_del(PyObject* po, int fd);
 SSL* tls_new_ssl(PyObject* ctx_obj, int fd, const char* host, int port);
 void tls_count_handshake(SSL* ssl);
 void tls_describe_failure(SSL* ssl, std::string& reason, std::string& message, bool& verify);
@@ -99,6 +104,7 @@ struct NetConnObject {
   PyObject* tls_ctx;         // TlsContext (owns the SSL_CTX and the session cache)
   PyObject* hs_fut;          // handshake IOFuture: None when established, rejected on failure
   PyObject* tls_error;       // callable(reason, message, verify) -> exception for a failed handshake
+  PyObject* poller;          // the loop's NetPoller (py_netpoll.cpp), or NULL: own loop.add_reader
 };
 
 PyTypeObject NetConnType = {PyVarObject_HEAD_INIT(nullptr, 0)};
@@ -114,18 +120,23 @@ void shut(NetConnObject* c) {
   if (c->fd < 0) return;
   PyObject *et, *ev, *tb;
   PyErr_Fetch(&et, &ev, &tb);
-  PyObject* fdo = PyLong_FromLong(c->fd);
-  if (fdo && c->loop) {
-    PyObject* r = PyObject_CallMethodOneArg(c->loop, s_remove_reader, fdo);
-    if (!r) PyErr_Clear();
-    Py_XDECREF(r);
-    if (c->writing) {
-      r = PyObject_CallMethodOneArg(c->loop, s_remove_writer, fdo);
+  if (c->poller) {
+    netpoll_del(c->poller, c->fd);
+    Py_CLEAR(c->poller);
+  } else {
+    PyObject* fdo = PyLong_FromLong(c->fd);
+    if (fdo && c->loop) {
+      PyObject* r = PyObject_CallMethodOneArg(c->loop, s_remove_reader, fdo);
       if (!r) PyErr_Clear();
       Py_XDECREF(r);
+      if (c->writing) {
+        r = PyObject_CallMethodOneArg(c->loop, s_remove_writer, fdo);
+        if (!r) PyErr_Clear();
+        Py_XDECREF(r);
+      }
     }
+    Py_XDECREF(fdo);
   }
-  Py_XDECREF(fdo);
   PyErr_Clear();
   PyErr_Restore(et, ev, tb);
   if (c->ssl) {
@@ -192,6 +203,11 @@ void lost(NetConnObject* c, int err) {
 
 int watch_writes(NetConnObject* c) {
   if (c->writing) return 0;
+  if (c->poller) {
+    if (netpoll_set_write(c->poller, c->fd, true) < 0) return -1;
+    c->writing = 1;
+    return 0;
+  }
   PyObject* fdo = PyLong_FromLong(c->fd);
   if (!fdo) return -1;
   PyObject* r = PyObject_CallMethodObjArgs(c->loop, s_add_writer, fdo, c->on_writable, nullptr);
@@ -205,6 +221,7 @@ int watch_writes(NetConnObject* c) {
 // Sends c->out (after anything already queued). 0 ok, -1 Python error. A socket error closes
 // the connection and is reported to the owner (_net_lost) before this returns.
 int send_out_tls(NetConnObject* c);
+int unwatch_writes(NetConnObject* c);
 
 int send_out(NetConnObject* c) {
   if (c->connecting) return 0;  // queued until the connect completes
@@ -228,20 +245,16 @@ int send_out(NetConnObject* c) {
   }
   o.erase(0, off);
   if (!o.empty()) return watch_writes(c);
-  if (c->writing) {
-    PyObject* fdo = PyLong_FromLong(c->fd);
-    if (!fdo) return -1;
-    PyObject* r = PyObject_CallMethodOneArg(c->loop, s_remove_writer, fdo);
-    Py_DECREF(fdo);
-    if (!r) return -1;
-    Py_DECREF(r);
-    c->writing = 0;
-  }
-  return 0;
+  return unwatch_writes(c);
 }
 
 int unwatch_writes(NetConnObject* c) {
   if (!c->writing) return 0;
+  if (c->poller) {
+    if (netpoll_set_write(c->poller, c->fd, false) < 0) return -1;
+    c->writing = 0;
+    return 0;
+  }
   PyObject* fdo = PyLong_FromLong(c->fd);
   if (!fdo) return -1;
   PyObject* r = PyObject_CallMethodOneArg(c->loop, s_remove_writer, fdo);
@@ -455,6 +468,7 @@ int nc_traverse(NetConnObject* c, visitproc visit, void* arg) {
   Py_VISIT(c->tls_ctx);
   Py_VISIT(c->hs_fut);
   Py_VISIT(c->tls_error);
+  Py_VISIT(c->poller);
   if (c->pending) {
     for (const PgPending& p : *c->pending) {
       Py_VISIT(p.fut);
@@ -479,6 +493,10 @@ int nc_clear(NetConnObject* c) {
   Py_CLEAR(c->closed_exc);
   Py_CLEAR(c->hs_fut);
   Py_CLEAR(c->tls_error);
+  if (c->poller) {  // registered: leave the epoll set first (the poller's reference cycle)
+    if (c->fd >= 0) netpoll_del(c->poller, c->fd);
+    Py_CLEAR(c->poller);
+  }
   if (c->pending) drop_pending(c);
   return 0;
 }
@@ -579,17 +597,31 @@ int nc_init(NetConnObject* c, PyObject* args, PyObject* kwds) {
       c->tls_error = tls_error;
     }
   }
-  PyObject* fdo = PyLong_FromLong(fd);
-  if (!fdo) return -1;
-  PyObject* r = PyObject_CallMethodObjArgs(loop, s_add_reader, fdo, c->on_readable, nullptr);
-  Py_DECREF(fdo);
-  if (!r) return -1;
-  Py_DECREF(r);
+  PyObject* poller = netpoll_for(loop);  // the loop's shared epoll set, or None
+  if (!poller) return -1;
+  if (poller != Py_None) {
+    if (netpoll_add(poller, fd, reinterpret_cast<PyObject*>(c)) < 0) {
+      Py_DECREF(poller);
+      return -1;
+    }
+    c->poller = poller;
+  } else {
+    Py_DECREF(poller);
+    PyObject* fdo = PyLong_FromLong(fd);
+    if (!fdo) return -1;
+    PyObject* r = PyObject_CallMethodObjArgs(loop, s_add_reader, fdo, c->on_readable, nullptr);
+    Py_DECREF(fdo);
+    if (!r) return -1;
+    Py_DECREF(r);
+  }
   c->fd = fd;  // owned from here on
   c->closed = 0;
   if (c->ssl && !c->connecting) {
     c->tls_state = 1;
-    if (tls_handshake(c) < 0) return -1;  // ClientHello goes out now
+    if (tls_handshake(c) < 0) {  // ClientHello goes out now
+      shut(c);  // unregistered and closed: the caller only gets the exception
+      return -1;
+    }
   }
   return 0;
 }
@@ -604,6 +636,11 @@ int connect_done(NetConnObject* c) {
   socklen_t len = sizeof err;
   if (getsockopt(c->fd, SOL_SOCKET, SO_ERROR, &err, &len) < 0) err = errno;
   if (err == EINPROGRESS || err == EALREADY) return 0;  // spurious wake-up
+  if (!err) {  // writable and no error: connected, unless the event was stale (fd reuse)
+    sockaddr_storage peer;
+    socklen_t plen = sizeof peer;
+    if (getpeername(c->fd, reinterpret_cast<sockaddr*>(&peer), &plen) < 0 && errno == ENOTCONN) return 0;
+  }
   c->connecting = 0;
   if (err) {
     errno = err;
@@ -955,6 +992,22 @@ PyGetSetDef nc_getset[] = {
 
 bool is_netconn(PyObject* o) { return Py_TYPE(o) == &NetConnType; }
 
+// The NetPoller's dispatch (py_netpoll.cpp): epoll `events` for this connection.
+PyObject* netconn_dispatch(PyObject* o, uint32_t events) {
+  NetConnObject* c = reinterpret_cast<NetConnObject*>(o);
+  if (events & (EPOLLIN | EPOLLERR | EPOLLHUP | EPOLLRDHUP)) {
+    PyObject* r = nc_on_readable(c, nullptr);
+    if (!r) return nullptr;
+    Py_DECREF(r);
+  }
+  if ((events & EPOLLOUT) && c->fd >= 0 && (c->writing || c->connecting)) {
+    PyObject* r = nc_on_writable(c, nullptr);
+    if (!r) return nullptr;
+    Py_DECREF(r);
+  }
+  Py_RETURN_NONE;
+}
+
 PyObject* netconn_loop(PyObject* o) { return reinterpret_cast<NetConnObject*>(o)->loop; }
 
 bool netconn_open(PyObject* o) {
@@ -1063,16 +1116,11 @@ PyObject* mod_netconn_connect(PyObject*, PyObject* args, PyObject* kwds) {
     Py_DECREF(c);
     return nullptr;
   }
-  if (!c->hs_fut && !(c->hs_fut = iofuture_new(loop))) {
-    Py_DECREF(c);
-    return nullptr;
-  }
-  if (cerr == 0) {  // connected at once (loopback can): finish now
-    if (connect_done(c) < 0) {
-      Py_DECREF(c);
-      return nullptr;
-    }
-  } else if (watch_writes(c) < 0) {
+  int rc2 = 0;
+  if (!c->hs_fut && !(c->hs_fut = iofuture_new(loop))) rc2 = -1;
+  if (rc2 == 0) rc2 = cerr == 0 ? connect_done(c) : watch_writes(c);  // connected at once: finish now
+  if (rc2 < 0) {
+    shut(c);  // registered with the loop: leave it before the reference goes
     Py_DECREF(c);
     return nullptr;
   }

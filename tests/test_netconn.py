@@ -281,7 +281,7 @@ def test_native_connect_ipv6_literal():
     assert res == (200, b"v6")
 
 
-@pytest.mark.parametrize("env", ["BEHOLDER_IOFUTURE", "BEHOLDER_NATIVE_H1", "BEHOLDER_NATIVE_TLS"])
+@pytest.mark.parametrize("env", ["BEHOLDER_IOFUTURE", "BEHOLDER_NATIVE_H1", "BEHOLDER_NATIVE_TLS", "BEHOLDER_NATIVE_POLLER"])
 def test_switched_off_paths_still_work(env):
     """Each A/B switch (read at import) leaves a working client: the H1 and TLS suites pass with
     it set to 0 (a NetConn then also completes plain asyncio futures as reply waiters)."""
@@ -292,3 +292,36 @@ def test_switched_off_paths_still_work(env):
                         "tests/test_h1.py", "tests/test_tls.py"], cwd=root, capture_output=True, text=True,
                        env=dict(os.environ, **{env: "0"}), timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+def test_netconns_share_one_epoll_set_per_loop():
+    """ops/csrc/py_netpoll.cpp: every NetConn of a loop sits in one epoll set whose fd is the only
+    one registered with the loop; it is closed (and leaves the loop) with its last socket."""
+    from beholder_amd.ops import native
+    if not native.netpoll_enabled():
+        pytest.skip("BEHOLDER_NATIVE_POLLER=0")
+
+    async def go():
+        loop = asyncio.get_running_loop()
+        s = await test_h1.Scripted(lambda n, m, t, h: test_h1.OK).start()
+        pg = await FakePg(auth="md5").start()
+        try:
+            c = H1Client(timeout_s=5)
+            await asyncio.gather(*[c.request("GET", f"http://127.0.0.1:{s.port}/{i}") for i in range(5)])
+            p = await PgConnection(pg.dsn).connect()
+            poller = loop._beholder_netpoller
+            sizes = [poller.size]
+            client_fds = {conn.net.fd for o in c._origins.values() for conn in o.idle} | {p._net.fd}
+            registered = set(loop._selector.get_map())
+            readers = (poller.fd in registered, bool(client_fds & registered))
+            await p.close()
+            sizes.append(poller.size)
+            await c.close()
+            sizes.append(poller.size)
+            return sizes, poller.fd, hasattr(loop, "_beholder_netpoller"), readers
+        finally:
+            await s.stop()
+            await pg.stop()
+    sizes, fd, attached, readers = run(go())
+    assert sizes == [6, 5, 0] and fd == -1 and not attached
+    assert readers == (True, False)  # the loop watches the epoll fd, not the client sockets
