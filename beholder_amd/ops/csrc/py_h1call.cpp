@@ -792,6 +792,17 @@ PyObject* mod_h1_fast(PyObject*, PyObject* const* a, Py_ssize_t n) {
   return reinterpret_cast<PyObject*>(call);
 }
 
+}  // namespace
+
+// h1_fast for a caller in C (the compiled handlers): an H1Call, or None when `client` is not a
+// stock H1Client (new reference either way), NULL on error.
+PyObject* h1_call_new(PyObject* client, PyObject* method, PyObject* url, PyObject* params, PyObject* timeout) {
+  PyObject* a[5] = {client, method, url, params, timeout};
+  return mod_h1_fast(nullptr, a, 5);
+}
+
+namespace {
+
 // h1_setup(client_cls, conn_cls, origin_cls, response_cls)
 PyObject* mod_h1_setup(PyObject*, PyObject* args) {
   PyObject *client_cls, *conn_cls, *origin_cls, *resp_cls;

@@ -29,6 +29,8 @@ namespace beholder {
 
 bool text_js_str_append(std::string& out, PyObject* v);
 bool text_query_pair_append(std::string& out, PyObject* k, PyObject* v, bool* first, bool rfc3986);
+PyObject* pg_pool_execute_c(PyObject* conns, PyObject* sql, PyObject* params, PyObject* spread_at, PyObject* size);
+PyObject* h1_call_new(PyObject* client, PyObject* method, PyObject* url, PyObject* params, PyObject* timeout);
 bool is_native_logger(PyObject* logger);
 bool logcore_emit(PyObject* logger, bool native, long lvl, PyObject* const* args, Py_ssize_t nargs);
 bool sink_stats_record(PyObject* stats, PyObject* status, double seconds);
@@ -46,7 +48,7 @@ PyObject *s_ack, *s_message, *s_content, *s_mediaId, *s_status, *s_progress, *s_
     *s_record, *s_raise_for_status, *s_rows, *s_get_calls, *s_update_calls, *s_limiter, *s_retry,
     *s_hooks_plan, *s_telegram, *s_emby, *s_name, *s_metadataId, *s_GET,
     *s_api_key, *s_send_message, *s_refresh_library, *s_pool, *s_select, *s_update,
-    *s_execute, *kw_params_timeout, *kw_timeout;
+    *s_execute, *s_conns, *s_spread_at, *s_size, *s_h1_fast_name, *kw_params_timeout, *kw_timeout;
 
 // Reference-visible text: read from beholder_amd/texts.py TEXTS when a NativeHandlers is built
 // (the same table handlers.py and the sink clients read; no such string is spelled here).
@@ -130,6 +132,9 @@ struct HandlersObject {
   PyObject* emby_cls;       // sinks.emby.EmbyClient (exact type: request built here)
   PyObject* memory_cls;     // store.memory.MemoryStore (exact type: row read here)
   PyObject* pg_cls;         // store.postgres.PostgresStore (exact type: queries issued here)
+  PyObject* pool_cls;       // store.pgwire.Pool when its native pick is on (connection picked here), else NULL
+  PyObject* h1_globals;     // sinks/h1.py module dict: `_h1_fast` is read per request (tests switch it)
+  PyObject* h1_fast_fn;     // ops._native.h1_fast: H1Client.request's native path, called directly
   PyObject* row_to_media;   // store.postgres.row_to_media (rows that are not all-int / NULL-free)
   PyObject* not_found;      // store.base.MediaNotFound
   PyObject* one;            // TRELLO_CREATOR (index.js:79)
@@ -333,6 +338,23 @@ int pg_execute(CallObject* c, PyObject* store, PyObject* sql_name, PyObject* par
   PyObject* sql = pool ? PyDict_GetItemWithError(sd, sql_name) : nullptr;
   if (PyErr_Occurred()) return -1;
   if (!pool || pool == Py_None || !sql) return 2;  // not connected yet: the store connects first
+  if (hs->pool_cls && reinterpret_cast<PyObject*>(Py_TYPE(pool)) == hs->pool_cls) {
+    // Pool.execute's fast path in C: the least-loaded native connection takes the query
+    PyObject** pdp = _PyObject_GetDictPtr(pool);
+    PyObject* pd = pdp ? *pdp : nullptr;
+    PyObject* conns = pd ? PyDict_GetItemWithError(pd, s_conns) : nullptr;
+    PyObject* spread = conns ? PyDict_GetItemWithError(pd, s_spread_at) : nullptr;
+    PyObject* size = spread ? PyDict_GetItemWithError(pd, s_size) : nullptr;
+    if (!size && PyErr_Occurred()) return -1;
+    if (size && PyList_CheckExact(conns)) {
+      Py_INCREF(conns);
+      PyObject* f = pg_pool_execute_c(conns, sql, params, spread, size);
+      Py_DECREF(conns);
+      if (!f) return -1;
+      if (f != Py_None) return await_start(c, f, out);
+      Py_DECREF(f);  // not all native / must grow: Pool.execute below
+    }
+  }
   PyObject* args[3] = {pool, sql, params};
   Py_INCREF(pool);  // the call may drop the store's reference (a reconnect)
   PyObject* aw = PyObject_VectorcallMethod(s_execute, args, 3, nullptr);
@@ -491,6 +513,26 @@ bool record_stats(PyObject* stats, PyObject* status, double seconds) {
   return true;
 }
 
+// http.request(method, url, params=params, timeout=timeout): for a stock H1Client whose native
+// path is on (sinks/h1.py `_h1_fast`), the H1Call is made here without the Python method frame.
+PyObject* http_request(HandlersObject* hs, PyObject* http, PyObject* method, PyObject* url, PyObject* params,
+                       PyObject* timeout) {
+  PyObject* cur = hs->h1_globals ? PyDict_GetItemWithError(hs->h1_globals, s_h1_fast_name) : nullptr;
+  if (cur && cur == hs->h1_fast_fn) {
+    PyObject* call = h1_call_new(http, method, url, params ? params : Py_None, timeout);
+    if (call != Py_None) return call;  // an H1Call, or NULL with an exception
+    Py_DECREF(call);  // not a stock H1Client
+  } else if (PyErr_Occurred()) {
+    return nullptr;
+  }
+  if (params) {
+    PyObject* args[5] = {http, method, url, params, timeout};
+    return PyObject_VectorcallMethod(s_request, args, 3, kw_params_timeout);
+  }
+  PyObject* args[4] = {http, method, url, timeout};
+  return PyObject_VectorcallMethod(s_request, args, 3, kw_timeout);
+}
+
 // Completes a sink request issued on the native path (after its await): per-sink stats, then
 // strict mode (Trello's `strict`; Telegram / Emby always raise_for_status, like request-promise).
 // Takes and returns the result reference; NULL = raised.
@@ -610,8 +652,7 @@ int trello_request(CallObject* c, PyObject* method, PyObject* method_upper, PyOb
     return -1;
   }
   c->req_t0 = mono_ns();
-  PyObject* args[5] = {http, method_upper, url, query, timeout};
-  aw = PyObject_VectorcallMethod(s_request, args, 3, kw_params_timeout);  // http.request(M, url, params=, timeout=)
+  aw = http_request(hs, http, method_upper, url, query, timeout);  // http.request(M, url, params=, timeout=)
   Py_DECREF(url);
   Py_DECREF(query);
   c->req_native = 1;
@@ -675,8 +716,7 @@ int sink_get(CallObject* c, PyObject* cd, std::string& url, PyObject* const* key
   } release{held};
   PyObject* full = unicode_from(url);
   if (!full) return -1;
-  PyObject* args[4] = {http, s_GET, full, timeout};
-  PyObject* aw = PyObject_VectorcallMethod(s_request, args, 3, kw_timeout);  // http.request("GET", full, timeout=)
+  PyObject* aw = http_request(c->hs, http, s_GET, full, nullptr, timeout);  // http.request("GET", full, timeout=)
   Py_DECREF(full);
   c->req_t0 = mono_ns();
   c->req_native = 1;
@@ -1390,6 +1430,9 @@ int hs_traverse(HandlersObject* hs, visitproc visit, void* arg) {
   Py_VISIT(hs->emby_cls);
   Py_VISIT(hs->memory_cls);
   Py_VISIT(hs->pg_cls);
+  Py_VISIT(hs->pool_cls);
+  Py_VISIT(hs->h1_globals);
+  Py_VISIT(hs->h1_fast_fn);
   Py_VISIT(hs->row_to_media);
   Py_VISIT(hs->not_found);
   return 0;
@@ -1421,6 +1464,9 @@ int hs_clear(HandlersObject* hs) {
   Py_CLEAR(hs->emby_cls);
   Py_CLEAR(hs->memory_cls);
   Py_CLEAR(hs->pg_cls);
+  Py_CLEAR(hs->pool_cls);
+  Py_CLEAR(hs->h1_globals);
+  Py_CLEAR(hs->h1_fast_fn);
   Py_CLEAR(hs->row_to_media);
   Py_CLEAR(hs->not_found);
   return 0;
@@ -1597,6 +1643,31 @@ int hs_init(HandlersObject* hs, PyObject* args, PyObject* kwds) {
   hs->pg_cls = hs->not_found ? import_attr("beholder_amd.store.postgres", "PostgresStore") : nullptr;
   hs->row_to_media = hs->pg_cls ? import_attr("beholder_amd.store.postgres", "row_to_media") : nullptr;
   if (!hs->row_to_media) return -1;
+  {  // Pool.execute's native pick, called directly (unless BEHOLDER_NATIVE_POOL=0 switched it off)
+    PyObject* pick = import_attr("beholder_amd.store.pgwire", "_pg_pool_execute");
+    PyObject* native_pick = pick ? import_attr("beholder_amd.ops._native", "pg_pool_execute") : nullptr;
+    if (!native_pick) {
+      Py_XDECREF(pick);
+      return -1;
+    }
+    if (pick == native_pick && !(hs->pool_cls = import_attr("beholder_amd.store.pgwire", "Pool"))) {
+      Py_DECREF(pick);
+      Py_DECREF(native_pick);
+      return -1;
+    }
+    Py_DECREF(pick);
+    Py_DECREF(native_pick);
+  }
+  {  // H1Client.request's native path, called directly while sinks/h1.py has it switched on
+    PyObject* mod = PyImport_ImportModule("beholder_amd.sinks.h1");
+    if (!mod) return -1;
+    PyObject* d = PyModule_GetDict(mod);
+    Py_XINCREF(d);
+    Py_DECREF(mod);
+    hs->h1_globals = d;
+    hs->h1_fast_fn = d ? import_attr("beholder_amd.ops._native", "h1_fast") : nullptr;
+    if (!hs->h1_fast_fn) return -1;
+  }
   if (!hs->not_found) return -1;
   static const char* pnames[4] = {"mediaId", "status", "progress", "host"};
   if (!codec_slots(hs->decode_s, pnames, 2, &hs->res_s, hs->ix_s) ||
@@ -1698,6 +1769,10 @@ int init_handler_types(PyObject* m) {
               {&s_select, "_select"},
               {&s_update, "_update"},
               {&s_execute, "execute"},
+              {&s_conns, "_conns"},
+              {&s_spread_at, "spread_at"},
+              {&s_size, "size"},
+              {&s_h1_fast_name, "_h1_fast"},
               {&s_retry, "retry"}};
 
   for (auto& s : strs)

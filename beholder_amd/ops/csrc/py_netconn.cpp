@@ -992,6 +992,7 @@ PyGetSetDef nc_getset[] = {
 
 bool is_netconn(PyObject* o) { return Py_TYPE(o) == &NetConnType; }
 
+
 // The NetPoller's dispatch (py_netpoll.cpp): epoll `events` for this connection.
 PyObject* netconn_dispatch(PyObject* o, uint32_t events) {
   NetConnObject* c = reinterpret_cast<NetConnObject*>(o);
@@ -1178,6 +1179,13 @@ PyMethodDef pool_functions[] = {
     {nullptr, nullptr, 0, nullptr}};
 
 }  // namespace
+
+// pg_pool_execute for a caller in C (the compiled handlers' Postgres queries): the same pick,
+// IOFuture or None (Python path), NULL on error.
+PyObject* pg_pool_execute_c(PyObject* conns, PyObject* sql, PyObject* params, PyObject* spread_at, PyObject* size) {
+  PyObject* a[5] = {conns, sql, params, spread_at, size};
+  return mod_pg_pool_execute(nullptr, a, 5);
+}
 
 int init_netconn_types(PyObject* m) {
   struct {

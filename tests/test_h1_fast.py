@@ -364,3 +364,51 @@ def test_differential_random_server_behaviour(seed):
     assert ft == pt  # same requests, same connections, same order
     assert fo == po
     assert fs == ps
+
+
+def test_compiled_handlers_make_h1_calls_directly(monkeypatch):
+    """The compiled handlers make the H1Call themselves (no H1Client.request frame); switching
+    sinks/h1.py's `_h1_fast` off at run time sends them back through the Python method."""
+    from beholder_amd.service import Service
+    from beholder_amd.store import MemoryStore
+    from beholder_amd.topics import PROGRESS
+    from beholder_amd.transport.memory import MemoryBroker
+    from beholder_amd.utils.log import Logger, MemoryStream
+
+    from helpers import cfg, progress_msg
+    from test_stores import M1
+
+    calls = []
+    orig = H1Client.request
+
+    def counting(self, *a, **k):
+        calls.append(a[0])
+        return orig(self, *a, **k)
+
+    monkeypatch.setattr(H1Client, "request", counting)
+
+    async def go(direct):
+        if not direct:
+            monkeypatch.setattr(h1mod, "_h1_fast", h1mod._h1_python_only)
+        s = await Raw(lambda t: OK).start()
+        b = MemoryBroker()
+        http = H1Client(timeout_s=5)
+        url = f"http://127.0.0.1:{s.port}"
+        svc = Service(cfg({"service": {"endpoints": {"trello": url, "telegram": url}}}), source=b.consumer(),
+                      store=MemoryStore([M1]), http=http, logger=Logger(stream=MemoryStream()), serve_metrics=False)
+        await svc.init()
+        run_ = asyncio.ensure_future(svc.run())
+        for i in range(20):
+            b.publish(PROGRESS, progress_msg("m1", "CONVERTING", i))
+        b.finish()
+        stats = await run_
+        await svc.close()
+        await http.close()
+        await s.stop()
+        return stats["source"]["acked"], len(s.raw), type(svc.handler_impl).__name__
+
+    calls.clear()
+    acked, served, impl = run(go(True))
+    assert (acked, served, impl) == (20, 20, "NativeHandlers") and calls == []
+    acked, served, _ = run(go(False))
+    assert (acked, served) == (20, 20) and calls.count("POST") == 20

@@ -384,3 +384,52 @@ def test_service_survives_a_postgres_restart():
     assert stats["source"]["acked"] == 60  # Q7: progress always acks, even on DB errors
     failed = [r for r in records if r["msg"].startswith("failed to update media progress")]
     assert comments + len(failed) == 60 and comments >= 50, (comments, len(failed))
+
+
+def test_compiled_handlers_pick_the_postgres_connection_in_c(monkeypatch):
+    """The compiled handlers issue the stock store's queries through the native pick
+    (ops pg_pool_execute, called directly): Pool.execute in Python runs only when the pick
+    declines (pool growth). The results are those of the Python pick."""
+    from beholder_amd.service import Service
+    from beholder_amd.sinks import RecordingHttpClient
+    from beholder_amd.store import pgwire
+    from beholder_amd.topics import PROGRESS
+    from beholder_amd.transport.memory import MemoryBroker
+    from beholder_amd.utils.log import Logger, MemoryStream
+
+    from helpers import cfg, progress_msg
+
+    calls = []
+    orig = pgwire.Pool.execute
+
+    def counting(self, sql, params=()):
+        calls.append(sql)
+        return orig(self, sql, params)
+
+    monkeypatch.setattr(pgwire.Pool, "execute", counting)
+
+    async def go():
+        pg = await FakePg(auth="trust").start()
+        try:
+            st = PostgresStore(pg.dsn, create_schema=True, pool_size=1)
+            await st.connect()
+            await st.upsert(M1)
+            calls.clear()
+            b = MemoryBroker()
+            http = RecordingHttpClient()
+            svc = Service(cfg(), source=b.consumer(), store=st, http=http, logger=Logger(stream=MemoryStream()),
+                          serve_metrics=False)
+            await svc.init()
+            run = asyncio.ensure_future(svc.run())
+            for i in range(30):
+                b.publish(PROGRESS, progress_msg("m1", "CONVERTING", i))
+            b.finish()
+            stats = await run
+            await svc.close()
+            return stats, http.count, svc.handler_impl
+        finally:
+            await pg.stop()
+    stats, comments, impl = run(go())
+    assert stats["source"]["acked"] == 30 and comments == 30
+    assert type(impl).__name__ == "NativeHandlers"
+    assert calls == []  # every lookup went through the direct native pick
