@@ -56,6 +56,7 @@ bool is_tls_context(PyObject* o);
 PyObject* netpoll_for(PyObject* loop);
 int netpoll_add(PyObject* po, int fd, PyObject* conn);
 int netpoll_set_write(PyObject* po, int fd, bool write);
+int netpoll_request_flush(PyObject* po, PyObject* conn);
 void netpoll_del(PyObject* po, int fd);
 SSL* tls_new_ssl(PyObject* ctx_obj, int fd, const char* host, int port);
 void tls_count_handshake(SSL* ssl);
@@ -869,7 +870,12 @@ PyObject* nc_execute(NetConnObject* c, PyObject* const* a, Py_ssize_t n) {
     Py_INCREF(fut);
     c->pending->push_back({fut, new_sql, name});
     if (!c->flush_scheduled) {
-      PyObject* h = PyObject_CallMethodOneArg(c->loop, s_call_soon, c->flush_cb);
+      // with a NetPoller: one flush for all its connections (at the end of its dispatch, or one
+      // call_soon), else a call_soon of this connection's flush
+      PyObject* h = c->poller ? (netpoll_request_flush(c->poller, reinterpret_cast<PyObject*>(c)) < 0
+                                     ? nullptr
+                                     : (Py_INCREF(Py_None), Py_None))
+                              : PyObject_CallMethodOneArg(c->loop, s_call_soon, c->flush_cb);
       if (!h) {
         c->pending->pop_back();
         o.resize(mark);
@@ -1179,6 +1185,15 @@ PyMethodDef pool_functions[] = {
     {nullptr, nullptr, 0, nullptr}};
 
 }  // namespace
+
+// The NetPoller's flush of a connection whose queries it collected.
+void netconn_flush(PyObject* o) {
+  PyObject* r = nc_flush(reinterpret_cast<NetConnObject*>(o), nullptr);
+  if (!r)
+    PyErr_WriteUnraisable(o);
+  else
+    Py_DECREF(r);
+}
 
 // pg_pool_execute for a caller in C (the compiled handlers' Postgres queries): the same pick,
 // IOFuture or None (Python path), NULL on error.

@@ -18,12 +18,14 @@
 #include <cstdlib>
 #include <cstring>
 #include <unordered_map>
+#include <vector>
 
 #include "py_common.hpp"
 
 namespace beholder {
 
 PyObject* netconn_dispatch(PyObject* conn, uint32_t events);
+void netconn_flush(PyObject* conn);
 
 namespace {
 
@@ -32,7 +34,10 @@ struct PollerObject {
   int running;    // nested _run depth: closing waits until it is 0
   PyObject* loop;
   PyObject* run_cb;                              // bound _run handed to loop.add_reader
+  PyObject* flush_cb;                            // bound _flush (call_soon)
   std::unordered_map<int, PyObject*>* conns;     // fd -> NetConn (strong)
+  std::vector<PyObject*>* to_flush;              // connections with queued queries (strong)
+  bool flush_scheduled;
 };
 
 PyTypeObject PollerType = {PyVarObject_HEAD_INIT(nullptr, 0)};
@@ -61,7 +66,22 @@ void poller_close(PollerObject* p) {
   PyErr_Restore(et, ev, tb);
 }
 
+void flush_all(PollerObject* p) {
+  if (!p->to_flush || p->to_flush->empty()) return;
+  std::vector<PyObject*> tmp;
+  tmp.swap(*p->to_flush);
+  for (PyObject* c : tmp) {
+    netconn_flush(c);
+    Py_DECREF(c);
+  }
+}
+
 void drop_all(PollerObject* p) {
+  if (p->to_flush) {
+    std::vector<PyObject*> tmp;
+    tmp.swap(*p->to_flush);
+    for (PyObject* c : tmp) Py_DECREF(c);
+  }
   if (!p->conns) return;
   std::unordered_map<int, PyObject*> tmp;
   tmp.swap(*p->conns);  // decrefs below may re-enter netpoll_del
@@ -71,6 +91,9 @@ void drop_all(PollerObject* p) {
 int poller_traverse(PollerObject* p, visitproc visit, void* arg) {
   Py_VISIT(p->loop);
   Py_VISIT(p->run_cb);
+  Py_VISIT(p->flush_cb);
+  if (p->to_flush)
+    for (PyObject* c : *p->to_flush) Py_VISIT(c);
   if (p->conns)
     for (auto& kv : *p->conns) Py_VISIT(kv.second);
   return 0;
@@ -79,6 +102,7 @@ int poller_traverse(PollerObject* p, visitproc visit, void* arg) {
 int poller_clear(PollerObject* p) {
   drop_all(p);
   Py_CLEAR(p->run_cb);
+  Py_CLEAR(p->flush_cb);
   Py_CLEAR(p->loop);
   return 0;
 }
@@ -91,8 +115,10 @@ void poller_dealloc(PollerObject* p) {
     p->epfd = -1;
   }
   Py_CLEAR(p->run_cb);
+  Py_CLEAR(p->flush_cb);
   Py_CLEAR(p->loop);
   delete p->conns;
+  delete p->to_flush;
   Py_TYPE(p)->tp_free(reinterpret_cast<PyObject*>(p));
 }
 
@@ -120,13 +146,24 @@ PyObject* poller_run(PollerObject* p, PyObject*) {
     Py_DECREF(c);
   }
   --p->running;
+  if (!p->running) flush_all(p);  // queries the resumed handlers issued go out now, batched
   if (!p->running && p->conns && p->conns->empty()) poller_close(p);
+  Py_DECREF(p);
+  Py_RETURN_NONE;
+}
+
+// _flush(): call_soon callback for queries queued outside a dispatch
+PyObject* poller_flush(PollerObject* p, PyObject*) {
+  p->flush_scheduled = false;
+  Py_INCREF(p);
+  flush_all(p);
   Py_DECREF(p);
   Py_RETURN_NONE;
 }
 
 PyMethodDef poller_methods[] = {
     {"_run", reinterpret_cast<PyCFunction>(poller_run), METH_NOARGS, "loop reader callback: dispatch ready sockets"},
+    {"_flush", reinterpret_cast<PyCFunction>(poller_flush), METH_NOARGS, "send the queued Postgres queries"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyObject* poller_get_size(PollerObject* p, void*) { return PyLong_FromSize_t(p->conns ? p->conns->size() : 0); }
@@ -163,10 +200,13 @@ PyObject* netpoll_for(PyObject* loop) {
   p->running = 0;
   p->loop = nullptr;
   p->run_cb = nullptr;
+  p->flush_cb = nullptr;
+  p->flush_scheduled = false;
   p->conns = new (std::nothrow) std::unordered_map<int, PyObject*>();
+  p->to_flush = new (std::nothrow) std::vector<PyObject*>();
   PyObject_GC_Track(p);
   PyObject* po = reinterpret_cast<PyObject*>(p);
-  if (!p->conns) {
+  if (!p->conns || !p->to_flush) {
     Py_DECREF(po);
     return PyErr_NoMemory();
   }
@@ -178,7 +218,8 @@ PyObject* netpoll_for(PyObject* loop) {
   Py_INCREF(loop);
   p->loop = loop;
   p->run_cb = PyObject_GetAttrString(po, "_run");
-  if (!p->run_cb) {
+  p->flush_cb = p->run_cb ? PyObject_GetAttrString(po, "_flush") : nullptr;
+  if (!p->flush_cb) {
     Py_DECREF(po);
     return nullptr;
   }
@@ -237,6 +278,26 @@ int netpoll_set_write(PyObject* po, int fd, bool write) {
     PyErr_SetFromErrno(PyExc_OSError);
     return -1;
   }
+  return 0;
+}
+
+// `conn` queued queries (its flush_scheduled flag is set by the caller): flushed at the end of the
+// dispatch in progress, else by one call_soon(_flush) shared by all connections. 0 or -1.
+int netpoll_request_flush(PyObject* po, PyObject* conn) {
+  PollerObject* p = reinterpret_cast<PollerObject*>(po);
+  if (!p->to_flush) {
+    PyErr_SetString(PyExc_RuntimeError, "NetPoller is closed");
+    return -1;
+  }
+  if (!p->running && !p->flush_scheduled) {
+    static PyObject* s_call_soon_p = PyUnicode_InternFromString("call_soon");
+    PyObject* h = s_call_soon_p && p->loop ? PyObject_CallMethodOneArg(p->loop, s_call_soon_p, p->flush_cb) : nullptr;
+    if (!h) return -1;
+    Py_DECREF(h);
+    p->flush_scheduled = true;
+  }
+  Py_INCREF(conn);
+  p->to_flush->push_back(conn);
   return 0;
 }
 
