@@ -397,6 +397,12 @@ class Connection:
             self._flush_scheduled = True
             asyncio.get_running_loop().call_soon(self._flush)
 
+    def _write_now(self, data: bytes) -> None:
+        """Append and send at once (with anything already queued, in order): the ack flush runs
+        once per loop iteration already, so it need not wait for another one."""
+        self._wbuf += data
+        self._flush()
+
     def _flush(self) -> None:
         self._flush_scheduled = False
         if not self._wbuf or self._writer is None:

@@ -152,7 +152,7 @@ class AmqpSource(Source):
         data = b.flush()
         ch = self._ch
         if data and ch is not None and ch.is_open and b.channel is ch:
-            ch.conn._write(data)
+            ch.conn._write_now(data)
 
     def _on_settle(self, d, kind: str, requeue: bool) -> None:
         """Settles the native batcher did not take: nack/reject, stale channels, no batching."""
