@@ -67,6 +67,7 @@ class AmqpSource(Source):
         self._ch: Optional[Channel] = None
         self._pending: List = []
         self._event: Optional[asyncio.Event] = None
+        self._loop: Optional[asyncio.AbstractEventLoop] = None  # set at start(): one lookup, not one per flush
         self._closing = False
         self._stopping = False
         self._reconnect_task: Optional[asyncio.Task] = None
@@ -90,6 +91,7 @@ class AmqpSource(Source):
             topic_id(t)
         self._topics = list(topics)
         self._event = asyncio.Event()
+        self._loop = asyncio.get_running_loop()
         delay = self.backoff_initial
         for attempt in range(self.retries + 1):
             try:
@@ -145,7 +147,10 @@ class AmqpSource(Source):
             self._event.set()
 
     def _schedule_ack_flush(self) -> None:
-        asyncio.get_running_loop().call_soon(self._flush_acks)
+        loop = self._loop
+        if loop is None:
+            loop = self._loop = asyncio.get_running_loop()
+        loop.call_soon(self._flush_acks)
 
     def _flush_acks(self) -> None:
         b = self._batcher
