@@ -41,7 +41,7 @@ struct PollerObject {
 };
 
 PyTypeObject PollerType = {PyVarObject_HEAD_INIT(nullptr, 0)};
-PyObject *s_attr, *s_add_reader_p, *s_remove_reader_p;
+PyObject *s_attr, *s_add_reader_p, *s_remove_reader_p, *s_call_soon_p;
 bool g_enabled = true;
 
 // Closes the epoll fd and leaves the loop (reader removed, attribute dropped). Errors are
@@ -290,8 +290,11 @@ int netpoll_request_flush(PyObject* po, PyObject* conn) {
     return -1;
   }
   if (!p->running && !p->flush_scheduled) {
-    static PyObject* s_call_soon_p = PyUnicode_InternFromString("call_soon");
-    PyObject* h = s_call_soon_p && p->loop ? PyObject_CallMethodOneArg(p->loop, s_call_soon_p, p->flush_cb) : nullptr;
+    if (!p->loop) {
+      PyErr_SetString(PyExc_RuntimeError, "NetPoller has no loop");
+      return -1;
+    }
+    PyObject* h = PyObject_CallMethodOneArg(p->loop, s_call_soon_p, p->flush_cb);
     if (!h) return -1;
     Py_DECREF(h);
     p->flush_scheduled = true;
@@ -319,7 +322,8 @@ int init_netpoll_types(PyObject* m) {
   g_enabled = !(env && strcmp(env, "0") == 0);
   if (!(s_attr = PyUnicode_InternFromString("_beholder_netpoller")) ||
       !(s_add_reader_p = PyUnicode_InternFromString("add_reader")) ||
-      !(s_remove_reader_p = PyUnicode_InternFromString("remove_reader")))
+      !(s_remove_reader_p = PyUnicode_InternFromString("remove_reader")) ||
+      !(s_call_soon_p = PyUnicode_InternFromString("call_soon")))
     return -1;
   PollerType.tp_name = "beholder_amd.ops._native.NetPoller";
   PollerType.tp_basicsize = sizeof(PollerObject);
