@@ -302,6 +302,23 @@ async def _wait_acked(settler, n: int, task, stall_s: float = 15.0) -> None:
         await asyncio.sleep(0.001)
 
 
+def _die_with_parent():
+    """preexec_fn: the endpoint gets SIGTERM when the process that started it dies (a bench
+    killed by a timeout must not leave its fakes running). Resolved before the fork."""
+    try:
+        import ctypes
+        prctl = ctypes.CDLL(None, use_errno=True).prctl
+    except (OSError, AttributeError):
+        return None
+    parent = os.getpid()
+
+    def arm():
+        prctl(1, 15, 0, 0, 0)  # PR_SET_PDEATHSIG, SIGTERM
+        if os.getppid() != parent:  # the parent died before the signal was armed
+            os._exit(1)
+    return arm
+
+
 def _spawn(module: str, copies: int = 1, args=()) -> "tuple":
     """Starts ``copies`` of a bench endpoint process sharing one port (SO_REUSEPORT).
     Returns ``(port, procs)``; each process printed ``READY <port>``."""
@@ -313,7 +330,8 @@ def _spawn(module: str, copies: int = 1, args=()) -> "tuple":
     try:
         for _ in range(copies):
             p = subprocess.Popen([sys.executable, "-m", module, "--port", str(port), *args],
-                                 stdout=subprocess.PIPE, text=True, env=env, cwd=root)
+                                 stdout=subprocess.PIPE, text=True, env=env, cwd=root,
+                                 preexec_fn=_die_with_parent())
             procs.append(p)
             line = p.stdout.readline().split()
             if not line or line[0] != "READY":
