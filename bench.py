@@ -42,6 +42,8 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import contextlib
+import ctypes
 import gc
 import json
 import multiprocessing as mp
@@ -113,6 +115,24 @@ class _Device:
         return self._ready
 
 
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """Points fd 1 at stderr for the block: native libraries' chatter (gloo's connection report)
+    must not land on stdout, where rank 0 prints the one JSON line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        try:
+            ctypes.CDLL(None).fflush(None)  # C stdio / std::cout output written inside the block
+        except (OSError, AttributeError):
+            pass
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 class _Dist:
     """gloo process group when launched under torch.distributed.run, no-op otherwise."""
 
@@ -124,7 +144,8 @@ class _Dist:
         self.dist = None
         if self.world > 1:
             import torch.distributed as dist
-            dist.init_process_group("gloo")
+            with _stdout_to_stderr():  # gloo prints "[Gloo] Rank r is connected to ..." on fd 1
+                dist.init_process_group("gloo")
             self.dist = dist
 
     def barrier(self):

@@ -18,8 +18,10 @@ SMALL = ["--steps", "2", "--warmup", "1", "--events-per-step", "4096", "--media"
 
 
 def _last_json(stdout: str) -> dict:
-    lines = [x for x in stdout.splitlines() if x.startswith("{")]
-    assert len(lines) == 1, stdout
+    """The driver reads rank 0's stdout: exactly one line, the JSON record (no library chatter
+    such as gloo's "[Gloo] Rank r is connected to ..." report)."""
+    lines = [x for x in stdout.splitlines() if x.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), stdout
     return json.loads(lines[0])
 
 
