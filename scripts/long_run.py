@@ -14,4 +14,5 @@ for c in ("tcp_e2e", "tls_e2e"):
     r = harness.run_config(c, events=n)
     out[c] = {k: r[k] for k in ("acked", "errors", "ingest_rate_eps", "cpu_us_per_event", "rss_growth_mb",
                                 "handle_latency_us", "http")}
+    print(f"{c}: {json.dumps(out[c])}", file=sys.stderr, flush=True)  # progress for long runs
 print(json.dumps(out))
