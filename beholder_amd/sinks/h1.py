@@ -310,8 +310,10 @@ class H1Client(HttpClient):
             try:
                 ipaddress.ip_address(o.host)
                 infos = self._literal[o.host] = [o.host]
-            except ValueError:
-                infos = [ai[4][0] for ai in await loop.getaddrinfo(o.host, o.port, type=socket.SOCK_STREAM)]
+            except ValueError:  # a name: resolved within the request's deadline, like create_connection
+                found = await asyncio.wait_for(loop.getaddrinfo(o.host, o.port, type=socket.SOCK_STREAM),
+                                               deadline - loop.time())
+                infos = [ai[4][0] for ai in found]
         errors = []
         for ip in infos:
             remaining = deadline - loop.time()

@@ -410,6 +410,28 @@ def test_connection_refused_and_bad_urls():
     run(go())
 
 
+def test_name_resolution_counts_against_the_request_timeout():
+    """A resolver that never answers ends in ETIMEDOUT at the request's deadline (the native
+    connect resolves names itself; asyncio's create_connection did it inside the timeout)."""
+    async def go():
+        loop = asyncio.get_running_loop()
+
+        async def stuck(*a, **k):
+            await asyncio.sleep(3600)
+        loop.getaddrinfo = stuck
+        c = H1Client(timeout_s=5)
+        t0 = loop.time()
+        with pytest.raises(HttpError, match="^ETIMEDOUT: GET http://resolver-hangs.example/x$"):
+            await c.request("GET", "http://resolver-hangs.example/x", timeout=0.2)
+        took = loop.time() - t0
+        st = dict(c.counts)
+        open_ = sum(o.open for o in c._origins.values())
+        await c.close()
+        return took, st, open_
+    took, st, open_ = run(go())
+    assert took < 2 and st["timeouts"] == 1 and open_ == 0
+
+
 def test_invalid_response_is_an_http_error():
     async def go():
         s = await Scripted(lambda n, m, t, h: b"SMTP ready\r\n\r\n").start()
