@@ -133,6 +133,56 @@ def test_large_bodies_and_many_requests_match_asyncio_tls():
     assert nat[2] is True and py[2] is False  # native connections only with the native path
 
 
+class DribbleServer(TlsServer):
+    """Answers in one-byte TLS records (one write + drain per byte) after reading the request
+    head slowly; the request targets may be far larger than a socket buffer."""
+
+    async def _serve(self, r, w):
+        self.connections += 1
+        try:
+            while True:
+                try:
+                    head = await r.readuntil(b"\r\n\r\n")
+                except (asyncio.IncompleteReadError, asyncio.LimitOverrunError, ConnectionError, ssl.SSLError):
+                    return
+                self.requests.append(len(head))
+                target = head.split(b" ", 2)[1]
+                body = b"%d:%s" % (len(target), target[-16:])
+                for i, ch in enumerate(ok(body)):
+                    w.write(bytes([ch]))
+                    if i % 7 == 0:
+                        await w.drain()
+                        await asyncio.sleep(0)
+                await w.drain()
+        finally:
+            w.close()
+
+
+def test_one_byte_records_and_requests_larger_than_the_socket_buffer():
+    """Replies split into one-byte records, and request heads of several MB (partial TLS writes
+    that wait for the socket to drain), on the native path and on asyncio's: same results."""
+    async def go(native):
+        s = DribbleServer(None)
+        s.server = await asyncio.start_server(s._serve, "127.0.0.1", 0, ssl=s.ctx, limit=16 * 1024 * 1024)
+        s.port = s.server.sockets[0].getsockname()[1]
+        c = H1Client(timeout_s=20, ssl_cafile=TLS_CERT)
+        base = f"https://127.0.0.1:{s.port}"
+        out = []
+        for i in range(6):
+            params = {"i": i, "text": ("x%d" % i) * (2_200_000 if i % 3 == 2 else 10)}
+            r = await c.request("POST", f"{base}/c{i}", params=params)
+            out.append((r.status, r.body))
+        kinds = native_tls(c)
+        st = dict(c.counts)
+        await c.close()
+        await s.stop()
+        return out, bool(kinds) and all(kinds), st["connections"], s.requests
+    nat, py = _both(go)
+    assert nat[0] == py[0] and nat[3] == py[3]
+    assert max(nat[3]) > 4_000_000 and nat[2] == py[2] == 1
+    assert nat[1] is True and py[1] is False
+
+
 def test_verification_failures_match_asyncio_tls(tmp_path):
     if shutil.which("openssl") is None:
         pytest.skip("needs openssl")
