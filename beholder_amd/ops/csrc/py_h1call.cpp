@@ -252,31 +252,37 @@ int finish_fast(H1CallObject* s, PyObject* res, PyObject** out) {
   PyObject* conn = s->conn;
   PyObject* busy = client_attr(client, s_busy);
   if (!busy || PySet_Discard(busy, conn) < 0) return -1;
+  // from here on the connection is out of `busy`: a failure must still hand it back (closed),
+  // or its origin would count it open forever
+  auto fail = [s]() {
+    abandon(s);
+    return -1;
+  };
   // keep = keep-alive and c.parser.buffered == 0
   int keep = PyObject_IsTrue(PyTuple_GET_ITEM(res, 4));
-  if (keep < 0) return -1;
+  if (keep < 0) return fail();
   if (keep) {
     PyObject* parser = g.conn.get(conn, C_PARSER);
     PyObject* b = parser ? PyObject_GetAttr(parser, s_buffered) : nullptr;
-    if (!b) return -1;
+    if (!b) return fail();
     int zero = PyLong_Check(b) && PyLong_AsSsize_t(b) == 0;
     Py_DECREF(b);
     keep = zero;
   }
   PyObject* cclosed = client_attr(client, s_closed_attr);
-  if (!cclosed) return -1;
+  if (!cclosed) return fail();
   PyObject* o = g.conn.get(conn, C_ORIGIN);
   PyObject* waiters = o && Py_TYPE(o) == g.origin.type ? g.origin.get(o, O_WAITERS) : nullptr;
   PyObject* idle = waiters ? g.origin.get(o, O_IDLE) : nullptr;
   Py_ssize_t nw = waiters ? PyObject_Size(waiters) : -1;
-  if (nw < 0 && PyErr_Occurred()) return -1;
+  if (nw < 0 && PyErr_Occurred()) return fail();
   if (keep && idle && nw == 0 && g.conn.get(conn, C_CLOSED) == Py_False && cclosed == Py_False) {
     // H1Client._release(c, True) with no waiter: back to the idle pool
     PyObject* t = PyFloat_FromDouble(mono_s());
-    if (!t) return -1;
+    if (!t) return fail();
     g.conn.set(conn, C_LAST_USED, t);
     PyObject* r = PyObject_CallMethodOneArg(idle, s_append, conn);
-    if (!r) return -1;
+    if (!r) return fail();
     Py_DECREF(r);
   } else {
     PyObject* r = PyObject_CallMethodObjArgs(client, s_release, conn, keep ? Py_True : Py_False, nullptr);
