@@ -535,6 +535,12 @@ int h1_start(H1CallObject* s) {
   PyObject* url = s->full;
   PyObject* params = s->params;
   PyObject* timeout = s->timeout;
+  // the shapes the sinks produce: str method and URL (ASCII: one byte per character, as read
+  // below), params a dict or absent; anything else takes the Python path, which raises or
+  // handles it (a Mapping that is not a dict, a non-ASCII host, a bytes method, ...)
+  if (!PyUnicode_CheckExact(method) || !PyUnicode_IS_ASCII(method) || !PyUnicode_CheckExact(url) ||
+      !PyUnicode_IS_ASCII(url) || (params && !PyDict_CheckExact(params)))
+    return 0;
   PyObject** dp = _PyObject_GetDictPtr(client);
   PyObject* d = dp ? *dp : nullptr;
   if (!d) return 0;

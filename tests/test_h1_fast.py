@@ -150,6 +150,47 @@ def test_fast_path_declines_cold_pool_and_foreign_shapes():
     assert kinds[2:] == [False] * 5
 
 
+def test_fast_path_declines_foreign_argument_types():
+    """Arguments outside the sinks' shapes (a Mapping that is not a dict, a non-ASCII host, a
+    bytes method) are the Python path's: same results and errors, no native read of them."""
+    import types
+
+    async def one(fast):
+        saved = h1mod._h1_fast
+        if not fast:
+            h1mod._h1_fast = h1mod._h1_python_only
+        try:
+            s = await Raw(lambda t: OK).start()
+            c = H1Client(timeout_s=5)
+            base = f"http://127.0.0.1:{s.port}"
+            seen = []
+            for m, url, params in [("POST", base + "/a", types.MappingProxyType({"k": "v w"})),
+                                   ("POST", base + "/b", [("x", 1)]),
+                                   ("GET", "http://café.invalid/x", None),
+                                   (b"GET", base + "/c", None),
+                                   ("GET", base + "/d", {"ok": 1})]:
+                await c.request("GET", base + "/warm")
+                aw = c.request(m, url, params=params)
+                try:
+                    r = await aw
+                    seen.append((r.status, r.url.replace(base, "")))
+                except Exception as e:  # noqa: BLE001 — the exact outcome is compared
+                    seen.append((type(e).__name__, str(e).replace(base, "")))
+                seen.append(getattr(aw, "native", None) is True)
+            await c.close()
+            await s.stop()
+            return seen, [r.split(b"\r\n")[0] for r in s.raw]
+        finally:
+            h1mod._h1_fast = saved
+
+    async def go():
+        return await one(True), await one(False)
+    (fast, fraw), (slow, sraw) = run(go())
+    assert [x for x in fast if not isinstance(x, bool)] == [x for x in slow if not isinstance(x, bool)]
+    assert fraw == sraw
+    assert fast[1::2] == [False, False, False, False, True]  # only the dict-shaped request is native
+
+
 def test_fast_path_reset_retry_redirect_and_errors_match_python():
     def respond(t):
         if t.startswith("/old"):
