@@ -862,7 +862,13 @@ PyObject* nc_execute(NetConnObject* c, PyObject* const* a, Py_ssize_t n) {
     Py_XDECREF(empty);
     PyObject* fut = rc < 0 ? nullptr : iofuture_new(c->loop);
     if (!fut) {
-      o.resize(mark);
+      o.resize(mark);  // the Parse of a new statement goes too: forget its name
+      if (new_sql) {
+        PyObject *et, *ev, *tb;
+        PyErr_Fetch(&et, &ev, &tb);
+        if (PyDict_DelItem(c->stmts, new_sql) < 0) PyErr_Clear();
+        PyErr_Restore(et, ev, tb);
+      }
       Py_DECREF(name);
       Py_XDECREF(new_sql);
       return nullptr;

@@ -69,6 +69,31 @@ def test_postgres_bad_password():
     run(go())
 
 
+def test_postgres_bad_params_do_not_poison_the_statement():
+    """Parameters that cannot be encoded fail that call only: the statement (first seen in that
+    call) is parsed again by the next one instead of being bound to a name never sent."""
+    class Unprintable:
+        def __str__(self):
+            raise ValueError("no text form")
+
+    async def go():
+        pg = await FakePg(auth="trust").start()
+        try:
+            c = await PgConnection(pg.dsn).connect()
+            with pytest.raises((TypeError, ValueError)):
+                await c.execute("SELECT 2 + $1", 5)  # not a sequence
+            with pytest.raises(ValueError):
+                await c.execute("SELECT 3 + $1", (Unprintable(),))
+            a = await c.execute("SELECT 2 + $1", (40,))
+            b = await c.execute("SELECT 3 + $1", (39,))
+            await c.close()
+            return a, b
+        finally:
+            await pg.stop()
+    a, b = run(go())
+    assert a == ([(42,)], "SELECT 1") and b == ([(42,)], "SELECT 1")
+
+
 def test_postgres_error_then_connection_still_usable():
     async def go():
         pg = await FakePg(auth="trust").start()
