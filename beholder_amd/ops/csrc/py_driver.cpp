@@ -1025,6 +1025,7 @@ bool iofuture_done(PyObject* f) {
 
 // 0 pending; 1 finished with a result (*result borrowed); 2 finished with an exception or cancelled
 int iofuture_peek(PyObject* f, PyObject** result) {
+  if (Py_TYPE(f) != &IOFutureType) return iofuture_done(f) ? 2 : 0;  // foreign: its owner reads it
   IOFutureObject* x = reinterpret_cast<IOFutureObject*>(f);
   if (!x->state) return 0;
   if (x->state == 2 || x->exc) return 2;
@@ -1034,7 +1035,11 @@ int iofuture_peek(PyObject* f, PyObject** result) {
 
 // What an awaiter yields for a pending future: the future, with the asyncio blocking handshake set
 PyObject* iofuture_yield(PyObject* f) {
-  reinterpret_cast<IOFutureObject*>(f)->blocking = 1;
+  if (Py_TYPE(f) == &IOFutureType) {
+    reinterpret_cast<IOFutureObject*>(f)->blocking = 1;
+  } else if (PyObject_SetAttrString(f, "_asyncio_future_blocking", Py_True) < 0) {
+    return nullptr;
+  }
   Py_INCREF(f);
   return f;
 }

@@ -393,7 +393,7 @@ PySendResult call_am_send(H1CallObject* s, PyObject* arg, PyObject** out) {
   int st = iofuture_peek(s->fut, &res);
   if (st == 0) {
     *out = iofuture_yield(s->fut);
-    return PYGEN_NEXT;
+    return *out ? PYGEN_NEXT : PYGEN_ERROR;
   }
   if (st == 1) {
     Py_INCREF(res);
