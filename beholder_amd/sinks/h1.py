@@ -506,6 +506,10 @@ class H1Client(HttpClient):
                 try:
                     if c is None:
                         c = await self._acquire(o, deadline, fresh)
+                        if self._closed:  # closed while this request connected or waited for a slot
+                            self._release(c, False)
+                            counts["errors"] += 1
+                            raise HttpError("client closed")
                 except asyncio.TimeoutError:
                     counts["timeouts"] += 1
                     counts["errors"] += 1
@@ -583,6 +587,12 @@ class H1Client(HttpClient):
         if self._sweeper is not None:
             self._sweeper.cancel()
             self._sweeper = None
+        # requests waiting for a reply end now (with the sweeper gone nothing would time them out);
+        # each request's own path then drops its connection
+        for c in list(self._busy):
+            self._busy.discard(c)
+            c._fail(HttpError("client closed"))
+            c.abort()
         for o in self._origins.values():
             while o.idle:
                 self._drop(o.idle.pop())

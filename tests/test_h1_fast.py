@@ -265,6 +265,35 @@ def test_fast_path_timeout_cancel_and_abandon_release_the_connection():
     assert open_ == 1 and conns == 4  # each abandoned request's connection was dropped, a new one opened
 
 
+def test_client_close_with_requests_in_flight_matches_python():
+    """close() while requests wait for their replies: every waiter ends (no hang), with the
+    same outcome on the native path and on the Python one, and nothing stays open."""
+    async def one(fast):
+        saved = h1mod._h1_fast
+        if not fast:
+            h1mod._h1_fast = h1mod._h1_python_only
+        try:
+            s = await Raw(lambda t: "hang" if t.startswith("/slow") else OK).start()
+            c = H1Client(timeout_s=5, max_per_host=4)
+            base = f"http://127.0.0.1:{s.port}"
+            await asyncio.gather(*[c.request("GET", f"{base}/w{i}") for i in range(4)])
+            tasks = [asyncio.ensure_future(c.request("POST", f"{base}/slow{i}", params={"i": i})) for i in range(4)]
+            await asyncio.sleep(0.05)
+            await c.close()
+            done = await asyncio.wait_for(asyncio.gather(*tasks, return_exceptions=True), 5)
+            open_ = sum(o.open for o in c._origins.values())
+            await s.stop()
+            return [type(x).__name__ + ":" + str(x).replace(base, "") for x in done], open_, len(c._busy)
+        finally:
+            h1mod._h1_fast = saved
+
+    async def go():
+        return await one(True), await one(False)
+    fast, slow = run(go())
+    assert fast == slow
+    assert fast[1] == 0 and fast[2] == 0
+
+
 def test_fast_path_under_native_driver_and_gather():
     """Many concurrent requests through gather (Tasks) and through a native Driver."""
     async def go():
