@@ -38,7 +38,8 @@ from typing import Dict, List, Optional
 
 from .generator import Workload, bench_config
 
-CONFIGS = ("plumbing", "firehose_1k", "rate_10k", "backpressure", "soak", "amqp", "io_bound", "io_bound_wide", "http_tcp", "tcp_e2e", "tls_e2e")
+CONFIGS = ("plumbing", "firehose_1k", "rate_10k", "backpressure", "soak", "amqp", "io_bound", "io_bound_wide", "http_tcp", "tcp_e2e", "tls_e2e",
+           "tcp_e2e_preconnect", "tls_e2e_preconnect")
 
 
 def _rss_mb() -> float:
@@ -262,6 +263,10 @@ def run_config(name: str, *, duration_s: Optional[float] = None, events: Optiona
         res = _tcp_e2e(events or 100_000)
     elif name == "tls_e2e":
         res = _tcp_e2e(events or 100_000, http_servers=4, tls=True)  # TLS fakes cost more CPU per request
+    elif name in ("tcp_e2e_preconnect", "tls_e2e_preconnect"):
+        # service.http.preconnect = prefetch: the warm-up no longer opens sink connections per delivery
+        tls = name.startswith("tls")
+        res = _tcp_e2e(events or 100_000, http_servers=4 if tls else 2, tls=tls, preconnect=100)
     elif name == "amqp":
         res = _amqp(events or 200_000)
     elif name == "soak":
@@ -386,13 +391,14 @@ def _http_tcp(w: Workload, n: int, servers: int = 3, clients=("h1", "aiohttp")) 
     return out
 
 
-def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = False) -> dict:
+def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = False, preconnect: int = 0) -> dict:
     """Production-shaped: every dependency over real TCP. A replay AMQP broker streams n
     events (prefetch 100, index.js:43). Each handler reads / updates the media row in a
     fake Postgres (pipelined ``pgwire``). Every sink call goes to a fake HTTP endpoint
     (keep-alive ``h1`` client). The fakes are separate processes; the numbers describe
     the consumer process. ``tls`` (config ``tls_e2e``): the sinks are HTTPS, as Trello and
-    Telegram are in production (certificate verified against the bench's own CA)."""
+    Telegram are in production (certificate verified against the bench's own CA). ``preconnect``:
+    ``service.http.preconnect`` (sink connections opened at init, before the clock)."""
     from ..config import Config
     from ..service import Service
     from ..sinks import H1Client
@@ -403,7 +409,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
     warm = min(5000, n // 10)
     bport, bprocs = _spawn("beholder_amd.bench.replay_broker", 1, ("--events", str(n)))
     procs = list(bprocs)
-    out: dict = {"events": n, "prefetch": 100}
+    out: dict = {"events": n, "prefetch": 100, "preconnect": preconnect}
     try:
         hport, hp = _spawn("beholder_amd.bench.http_sink_server", http_servers, ("--tls",) if tls else ())
         procs += hp
@@ -416,6 +422,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             cfgd = bench_config()
             cfgd["service"]["endpoints"] = {"trello": url, "telegram": url}
             cfgd["instance"]["emby"]["host"] = url
+            cfgd["service"].setdefault("http", {})["preconnect"] = preconnect
             sink = open(os.devnull, "w", buffering=1 << 16)
             src = AmqpSource(f"amqp://guest:guest@127.0.0.1:{bport}/", prefetch=100)
             store = PostgresStore(f"postgres://beholder@127.0.0.1:{pport}/media", pool_size=4)

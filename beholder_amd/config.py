@@ -58,7 +58,8 @@ SERVICE_DEFAULTS: dict = {
         # positional_args: append (Q11 fix, extra args kept) | drop (pino@5's exact msg text)
         "log": {"level": "info", "name": "index.js", "positional_args": "append"},
         # outbound sink HTTP: `h1` = native-parsed keep-alive client (sinks/h1.py), `aiohttp` = library client
-        "http": {"timeout_s": 30.0, "client": "h1", "max_per_host": 100, "keepalive_s": 4.0},
+        # preconnect: connections opened per sink origin at startup (0 = on demand, as the reference)
+        "http": {"timeout_s": 30.0, "client": "h1", "max_per_host": 100, "keepalive_s": 4.0, "preconnect": 0},
         # SURVEY §5 race detection: opt-in per-mediaId serialisation (default off = parity, Q9).
         "ordering": "none",
         # Q1: what to do with a status message whose handler threw.
@@ -290,6 +291,11 @@ class Config:
             raise ConfigError("service.log.positional_args must be 'append' or 'drop'")
         if svc["http"].get("client", "h1") not in ("h1", "aiohttp"):
             raise ConfigError("service.http.client must be 'h1' or 'aiohttp'")
+        pc = svc["http"].get("preconnect", 0)
+        if pc is None:
+            pc = 0
+        if isinstance(pc, bool) or not isinstance(pc, int) or pc < 0:
+            raise ConfigError(f"service.http.preconnect must be an integer >= 0, got {pc!r}")
         ca = svc["http"].get("ca_file")
         if ca is not None and (not isinstance(ca, str) or not os.path.isfile(ca)):
             raise ConfigError(f"service.http.ca_file: not a readable file: {ca!r}")

@@ -209,6 +209,9 @@ class Service:
         if svc.get("native_handlers", True) and os.environ.get("BEHOLDER_NATIVE_HANDLERS", "1") != "0":
             impl = native_handlers(self.handlers) or self.handlers
         self.handler_impl = impl
+        pc = int(svc["http"].get("preconnect") or 0)
+        if pc > 0:  # opt-in: sink connections made before the first delivery, not inside it
+            await self._preconnect(pc, endpoints)
         self.listen(T.STATUS, impl.on_status)
         self.listen(T.PROGRESS, impl.on_progress)
         await self._source.start([t for t in T.TOPIC_IDS if self._routes[T.TOPIC_IDS[t]] is not None])
@@ -228,6 +231,41 @@ class Service:
         # once so a mismatch with the real deployment is visible in the log
         self.log.info(f"consuming from {self._source.describe()}; store {self._store.describe()}")
         return self
+
+    async def _preconnect(self, n: int, endpoints) -> None:
+        """``service.http.preconnect``: ``n`` connections to each sink origin the handlers will
+        call (Trello; Telegram and Emby when their DEPLOYED hooks are on), all at once. A sink
+        that cannot be reached is warned about, never fatal: the reference only meets it on the
+        first event, and the handlers connect on demand as they always do."""
+        from .sinks.emby import _PATH as emby_path
+        from .sinks.http import redact
+        urls = [endpoints["trello"]]
+        try:
+            tg_on, _, _, emby_on, emby_host, _ = self.handlers._hooks_plan()
+            if tg_on:
+                urls.append(endpoints["telegram"])
+            if emby_on and emby_host:
+                urls.append(emby_path(emby_host))
+        except Exception:  # noqa: BLE001 -- a hook config the handler would reject at its own point
+            pass
+        seen, origins = set(), []
+        for u in urls:
+            o = str(u).split("/", 3)[:3]
+            key = "/".join(o).lower()
+            if key not in seen:
+                seen.add(key)
+                origins.append(str(u))
+        got = await asyncio.gather(*(self._http.preconnect(u, n) for u in origins), return_exceptions=True)
+        for u, r in zip(origins, got):
+            if isinstance(r, BaseException):
+                opened, err = 0, r
+            else:
+                opened, err = r
+            origin = redact("/".join(u.split("/", 3)[:3]))
+            if err is not None:
+                self.log.warn(f"preconnect to {origin}: {opened}/{n} connections ({type(err).__name__}: {err})")
+            else:
+                self.log.info(f"preconnect to {origin}: {opened} connections")
 
     def _media_key(self, d) -> Any:
         h = self.handlers

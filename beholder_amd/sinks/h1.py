@@ -371,6 +371,29 @@ class H1Client(HttpClient):
                 self._drop(c)
         return await self._connect(o, deadline)
 
+    async def preconnect(self, url: str, n: int) -> Tuple[int, Optional[BaseException]]:
+        """Open up to ``n`` connections to ``url``'s origin at once (never past ``max_per_host``)
+        and park them idle, so the first burst of requests after start reuses them instead of
+        each paying a connect (and TLS handshake) inside its handle latency. Connections left
+        unused for ``keepalive_s`` are dropped at the next acquire, as any idle one is."""
+        if self._closed or n <= 0:
+            return 0, None
+        o = self._origin(_split_url(url)[0])
+        want = min(int(n), self.max_per_host - o.open)
+        if want <= 0:
+            return 0, None
+        loop = asyncio.get_running_loop()
+        deadline = loop.time() + self.timeout_s
+        got = await asyncio.gather(*(self._connect(o, deadline) for _ in range(want)), return_exceptions=True)
+        opened, err = 0, None
+        for c in got:
+            if isinstance(c, BaseException):
+                err = err or c
+            else:
+                self._release(c, True)
+                opened += 1
+        return opened, err
+
     def _release(self, c: _Conn, keep: bool) -> None:
         o = c.origin
         if not keep or c.closed or self._closed:

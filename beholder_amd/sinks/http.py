@@ -155,6 +155,11 @@ class HttpClient(abc.ABC):
                       timeout: Optional[float] = None) -> HttpResponse:
         ...
 
+    async def preconnect(self, url: str, n: int) -> Tuple[int, Optional[BaseException]]:
+        """Open up to ``n`` keep-alive connections to ``url``'s origin ahead of the first request:
+        ``(connections opened, first error or None)``. Clients without a pool open none."""
+        return 0, None
+
     async def close(self) -> None:
         pass
 

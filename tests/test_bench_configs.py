@@ -9,7 +9,7 @@ from beholder_amd.bench import harness
 SMALL = {"firehose_1k": {"duration_s": 0.5}, "rate_10k": {"duration_s": 0.5}, "backpressure": {"duration_s": 0.2},
          "io_bound": {"events": 3000}, "io_bound_wide": {"events": 4000}, "http_tcp": {"events": 3000},
          "tcp_e2e": {"events": 4000}, "tls_e2e": {"events": 4000}, "amqp": {"events": 6000},
-         "soak": {"events": 20000}}
+         "soak": {"events": 20000}, "tcp_e2e_preconnect": {"events": 4000}, "tls_e2e_preconnect": {"events": 4000}}
 
 
 def test_every_config_is_covered():
@@ -27,6 +27,9 @@ def test_config_runs_small(name):
         assert res["accepted"] + res["dropped"] == res["offered"]
     elif "events" in SMALL[name]:
         assert res["acked"] == SMALL[name]["events"], res
-    if name in ("tcp_e2e", "tls_e2e", "amqp"):
+    if name in ("tcp_e2e", "tls_e2e", "amqp") or name.endswith("_preconnect"):
         assert res["ingest_rate_eps"] > 0 and res["cpu_us_per_event"] > 0
         assert 0 < res["measured_events"] <= res["acked"]
+    if name.endswith("_preconnect"):
+        assert res["preconnect"] == 100 and res["errors"] == 0
+        assert res["http"]["connections"] >= 100  # opened at init, before the first delivery

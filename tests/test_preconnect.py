@@ -1,0 +1,131 @@
+"""``service.http.preconnect``: sink connections opened at startup instead of inside the first
+deliveries' handle latency (the warm-up tail of ``tcp_e2e``, docs/STATUS.md open items)."""
+import asyncio
+import socket
+
+import pytest
+
+from beholder_amd.config import ConfigError
+from beholder_amd.service import Service
+from beholder_amd.sinks import H1Client, RecordingHttpClient
+from beholder_amd.store import MemoryStore
+from beholder_amd.topics import STATUS
+from beholder_amd.transport.memory import MemoryBroker
+from beholder_amd.utils.log import Logger, MemoryStream
+
+from helpers import cfg, status_msg, trello_media
+from test_h1 import OK, Scripted
+
+
+def run(coro, timeout=60):
+    return asyncio.run(asyncio.wait_for(coro, timeout))
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_preconnected_connections_serve_a_burst_without_new_connects():
+    async def go():
+        s = await Scripted(lambda n, m, t, h: OK).start()
+        c = H1Client(timeout_s=5)
+        base = f"http://127.0.0.1:{s.port}"
+        opened, err = await c.preconnect(base + "/1/cards", 8)
+        before = s.connections
+        rs = await asyncio.gather(*[c.request("GET", f"{base}/{i}") for i in range(8)])
+        st = c.stats()
+        await c.close()
+        await s.stop()
+        return opened, err, before, s.connections, rs, st
+    opened, err, before, after, rs, st = run(go())
+    assert (opened, err) == (8, None) and before == after == 8
+    assert all(r.status == 200 for r in rs) and st["reused"] == 8 and st["connections"] == 8
+
+
+def test_preconnect_never_exceeds_max_per_host():
+    async def go():
+        s = await Scripted(lambda n, m, t, h: OK).start()
+        c = H1Client(timeout_s=5, max_per_host=3)
+        base = f"http://127.0.0.1:{s.port}"
+        first = await c.preconnect(base, 10)
+        again = await c.preconnect(base, 10)  # the pool is full already
+        await c.close()
+        await s.stop()
+        return first, again, s.connections
+    first, again, conns = run(go())
+    assert first == (3, None) and again == (0, None) and conns == 3
+
+
+def test_preconnect_to_a_dead_origin_reports_instead_of_raising():
+    async def go():
+        c = H1Client(timeout_s=2)
+        url = f"http://127.0.0.1:{_free_port()}/x"
+        opened, err = await c.preconnect(url, 4)
+        open_after = c._origin(f"http://127.0.0.1:{url.split(':')[2].split('/')[0]}").open
+        await c.close()
+        return opened, err, open_after
+    opened, err, open_after = run(go())
+    assert opened == 0 and isinstance(err, OSError) and open_after == 0  # no pool slot leaked
+
+
+def test_preconnect_config_is_validated():
+    assert cfg().data["service"]["http"]["preconnect"] == 0
+    assert cfg({"service": {"http": {"preconnect": 50}}}).data["service"]["http"]["preconnect"] == 50
+    for bad in (-1, "10", 1.5, True):
+        with pytest.raises(ConfigError, match="preconnect"):
+            cfg({"service": {"http": {"preconnect": bad}}})
+
+
+def _service(c, http, medias=()):
+    return Service(c, source=MemoryBroker().consumer(prefetch=100), store=MemoryStore(list(medias)), http=http,
+                   logger=Logger(stream=MemoryStream()), serve_metrics=False)
+
+
+def test_service_preconnects_each_sink_origin_the_handlers_will_call():
+    async def go():
+        trello = await Scripted(lambda n, m, t, h: OK).start()
+        hooks = await Scripted(lambda n, m, t, h: OK).start()  # Telegram and Emby on one origin
+        dead = _free_port()
+        c = cfg({"service": {"http": {"preconnect": 3},
+                             "endpoints": {"trello": f"http://127.0.0.1:{trello.port}",
+                                           "telegram": f"http://127.0.0.1:{hooks.port}"}},
+                 "instance": {"emby": {"host": f"http://127.0.0.1:{dead}"}}})
+        http = H1Client(timeout_s=2)
+        svc = _service(c, http)
+        await svc.init()
+        await svc.close()  # flushes the log
+        msgs = [r["msg"] for r in svc.log.stream.records()]
+        levels = {r["msg"]: r["level"] for r in svc.log.stream.records()}
+        await http.close()
+        await trello.stop()
+        await hooks.stop()
+        return trello.connections, hooks.connections, msgs, levels, dead
+    t_conns, h_conns, msgs, levels, dead = run(go())
+    assert t_conns == 3 and h_conns == 3
+    pre = [m for m in msgs if m.startswith("preconnect to ")]
+    assert len(pre) == 3
+    bad = [m for m in pre if f":{dead}" in m]
+    assert len(bad) == 1 and "0/3 connections" in bad[0] and levels[bad[0]] == 40  # warn, startup went on
+    assert "initialized" in msgs
+
+
+def test_service_preconnect_is_harmless_for_clients_without_a_pool():
+    async def go():
+        b = MemoryBroker()
+        http = RecordingHttpClient()
+        c = cfg({"service": {"http": {"preconnect": 5}}})  # a client without a pool opens none
+        svc = Service(c, source=b.consumer(prefetch=100), store=MemoryStore([trello_media("m1", card="C1")]),
+                      http=http, logger=Logger(stream=MemoryStream()), serve_metrics=False)
+        await svc.init()
+        b.publish(STATUS, status_msg("m1", "DEPLOYED"))
+        b.finish()
+        stats = await svc.run()
+        await svc.close()
+        return stats, [r["msg"] for r in svc.log.stream.records()]
+    stats, msgs = run(go())
+    assert stats["received"][STATUS] == 1 and stats["source"]["acked"] == 1
+    assert sum(m.startswith("preconnect to ") for m in msgs) == 3  # trello, telegram, emby: 0 each, no error
