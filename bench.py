@@ -48,6 +48,7 @@ import gc
 import json
 import multiprocessing as mp
 import os
+import resource
 import sys
 import threading
 import time
@@ -221,17 +222,20 @@ async def run_consumer(a, seed: int, go, stop=None, *, steps: int = None, warmup
             await asyncio.sleep(0.0002)
 
     t0 = 0.0
+    ru0 = None
     for i in range(total_steps):
         if i == warmup:
             settler.reset_latency()
             go()
             t0 = time.perf_counter()
+            ru0 = resource.getrusage(resource.RUSAGE_SELF)
         th = write_step(i)
         await wait_settled((i + 1) * E)
         th.join()
     if stop is not None:
         stop()
     elapsed = time.perf_counter() - t0
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
     os.close(wfd)
     await run_task
     await svc.close()
@@ -245,6 +249,11 @@ async def run_consumer(a, seed: int, go, stop=None, *, steps: int = None, warmup
         "http_calls": http.count,
         "errors": sum(st.get("handler_errors", {}).values()),
         "abandoned": st["source"]["abandoned"],
+        # CPU of the timed steps (consumer + the thread feeding its pipe) and the times the kernel
+        # took the CPU away: a low rate with unchanged CPU per event and many involuntary switches
+        # is other load on the box, not the consumer
+        "cpu_s": (ru1.ru_utime + ru1.ru_stime) - (ru0.ru_utime + ru0.ru_stime) if ru0 else 0.0,
+        "nivcsw": ru1.ru_nivcsw - ru0.ru_nivcsw if ru0 else 0,
     }
 
 
@@ -408,7 +417,7 @@ def main(argv=None) -> int:
     dist.barrier()
     elapsed = dist.max(res["elapsed"])
     parts = dist.gather({k: res[k] for k in ("handle_hist", "ingest_hist", "http_calls", "errors", "abandoned",
-                                             "events")})
+                                             "events", "cpu_s", "nivcsw")})
 
     # 3. in-process BASELINE configs (no child processes: HIP may be initialised now)
     if a.extras and dist.rank == 0:
@@ -445,6 +454,8 @@ def main(argv=None) -> int:
             "events_per_proc_per_sec": round(value / n, 1),
             "p50_handle_latency_us": round(hh.percentile(50) / 1e3, 3),
             "p99_handle_latency_us": round(hh.percentile(99) / 1e3, 3),
+            "cpu_us_per_event": round(sum(p["cpu_s"] for p in parts) / total_events * 1e6, 3),
+            "involuntary_ctx_switches": sum(p["nivcsw"] for p in parts),
             "http_requests": sum(p["http_calls"] for p in parts),
             "handler_errors": sum(p["errors"] for p in parts),
             "all_procs_per_rank": procs if allp is not None else 0,
