@@ -537,14 +537,24 @@ def _fields(body: bytes) -> Dict[str, str]:
     return out
 
 
+_BACKGROUND_GROW = os.environ.get("BEHOLDER_PG_BACKGROUND_GROW", "1") != "0"
+
+
 class Pool:
     """Up to ``size`` pipelined :class:`PgConnection` s.
 
     A query goes to the open connection with the fewest queries in flight. A new
     connection is opened (up to ``size``) only when every open one already has
     ``spread_at`` or more in flight, so light load stays on one connection and one
-    ``write`` per loop iteration. Broken connections are dropped and replaced on demand.
+    ``write`` per loop iteration. The pool grows in the background: the query that finds
+    every connection busy is still sent at once on the least-loaded one, and the new
+    connection takes queries once its startup and authentication are done (a query never
+    waits for a connect while a connection is open; the warm-up tail of ``tcp_e2e``). A
+    failed grow is retried after ``GROW_RETRY_S``. Broken connections are dropped and
+    replaced on demand.
     """
+
+    GROW_RETRY_S = 1.0
 
     def __init__(self, dsn: str, size: int = 4, spread_at: int = 8):
         self.dsn = dsn
@@ -552,6 +562,11 @@ class Pool:
         self.spread_at = spread_at
         self._conns: List[PgConnection] = []
         self._lock = asyncio.Lock()
+        self._growing: Optional[asyncio.Future] = None
+        self._grow_after = 0.0
+        self._closed = False
+        self.grows = 0  # connections added by the background grow
+        self.grow_errors = 0
 
     async def open(self) -> "Pool":
         self._conns.append(await PgConnection(self.dsn).connect())  # fail fast on bad DSN/credentials
@@ -564,23 +579,54 @@ class Pool:
             return f
         best = None
         bp = 0
+        live = 0
         for c in self._conns:
             if not c.closed:
+                live += 1
                 n = c.pending
                 if best is None or n < bp:
                     best, bp = c, n
-        if best is not None and (bp < self.spread_at or len(self._conns) >= self.size):
-            return best.execute(sql, params)
-        return self._execute_slow(sql, params)
+        if best is None:
+            return self._execute_slow(sql, params)
+        if bp >= self.spread_at and live < self.size:
+            if not _BACKGROUND_GROW:  # BEHOLDER_PG_BACKGROUND_GROW=0: the query waits for the new connection
+                return self._execute_slow(sql, params)
+            self._grow()
+        return best.execute(sql, params)
+
+    def _grow(self) -> None:
+        if self._growing is not None or self._closed:
+            return
+        loop = asyncio.get_running_loop()
+        if loop.time() < self._grow_after:
+            return
+        self._growing = loop.create_task(self._grow_one())
+
+    async def _grow_one(self) -> None:
+        try:
+            c = await PgConnection(self.dsn).connect()
+        except (OSError, asyncio.TimeoutError, PgError, PgProtocolError):
+            self.grow_errors += 1
+            self._grow_after = asyncio.get_running_loop().time() + self.GROW_RETRY_S
+            return
+        finally:
+            self._growing = None
+        if self._closed:
+            await c.close()
+            return
+        self._conns[:] = [x for x in self._conns if not x.closed]
+        self._conns.append(c)  # in place: a connect in _execute_slow appends to the same list
+        self.grows += 1
 
     async def _execute_slow(self, sql: str, params: Sequence[Any]):
+        """No open connection (or the inline grow of ``BEHOLDER_PG_BACKGROUND_GROW=0``): connect
+        under the lock, so a burst makes one connection, then send."""
         async with self._lock:
-            self._conns = [c for c in self._conns if not c.closed]
+            self._conns[:] = [c for c in self._conns if not c.closed]
             live = self._conns
             if len(live) < self.size and (not live or min(c.pending for c in live) >= self.spread_at):
                 try:
-                    c = await PgConnection(self.dsn).connect()
-                    live.append(c)
+                    live.append(await PgConnection(self.dsn).connect())
                 except (OSError, asyncio.TimeoutError, PgError, PgProtocolError):
                     if not live:
                         raise
@@ -592,6 +638,14 @@ class Pool:
         return sum(1 for c in self._conns if not c.closed)
 
     async def close(self) -> None:
-        for c in self._conns:
+        self._closed = True
+        g = self._growing
+        if g is not None:
+            g.cancel()
+            try:
+                await g
+            except (asyncio.CancelledError, Exception):  # noqa: BLE001 -- closing anyway
+                pass
+        for c in list(self._conns):
             await c.close()
         self._conns = []

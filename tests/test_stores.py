@@ -1,5 +1,6 @@
 """Media stores (triton-core/db parity, index.js:42,68,76,140): memory, sqlite, postgres (wire protocol)."""
 import asyncio
+import os
 
 import pytest
 
@@ -227,9 +228,17 @@ def test_pool_spreads_load_and_replaces_broken_connections():
         try:
             pool = await Pool(pg.dsn, size=3, spread_at=2).open()
             assert pool.connections == 1
-            res = await asyncio.gather(*[pool.execute("SELECT $1 + 0", (i,)) for i in range(30)])
-            assert [r[0][0][0] for r in res] == list(range(30))
+            # the pool grows in the background, one connection at a time, while bursts keep
+            # every open connection at spread_at or more
+            for _ in range(50):
+                res = await asyncio.gather(*[pool.execute("SELECT $1 + 0", (i,)) for i in range(30)])
+                assert [r[0][0][0] for r in res] == list(range(30))
+                if pool.connections == 3:
+                    break
+                await asyncio.sleep(0.005)
             spread = pool.connections
+            from beholder_amd.store import pgwire
+            assert pool.grows == (2 if pgwire._BACKGROUND_GROW else 0) and pool.grow_errors == 0
             pool._conns[0].abort()  # a broken connection is dropped and replaced
             await asyncio.sleep(0.01)
             res = await asyncio.gather(*[pool.execute("SELECT $1 + 0", (i,)) for i in range(10)])
@@ -239,6 +248,69 @@ def test_pool_spreads_load_and_replaces_broken_connections():
         finally:
             await pg.stop()
     assert run(go()) == 3
+
+
+def test_pool_grow_never_delays_a_query_and_backs_off_after_a_failure(monkeypatch):
+    if os.environ.get("BEHOLDER_PG_BACKGROUND_GROW", "1") == "0":
+        pytest.skip("background pool grow switched off")
+    from beholder_amd.store import pgwire
+    from beholder_amd.store.pgwire import Pool
+
+    async def go():
+        pg = await FakePg(auth="trust").start()
+        try:
+            pool = await Pool(pg.dsn, size=4, spread_at=1).open()
+            real = pgwire.PgConnection.connect
+            gate = asyncio.Event()
+
+            async def slow_connect(self):  # a grow whose connect takes as long as the test wants
+                await gate.wait()
+                return await real(self)
+            monkeypatch.setattr(pgwire.PgConnection, "connect", slow_connect)
+            res = await asyncio.wait_for(asyncio.gather(*[pool.execute("SELECT $1 + 0", (i,)) for i in range(20)]), 5)
+            assert [r[0][0][0] for r in res] == list(range(20))  # served while the grow still waits
+            assert pool.connections == 1 and pool._growing is not None
+            gate.set()
+            await asyncio.sleep(0.05)
+            assert pool.connections == 2 and pool.grows == 1
+
+            async def failing_connect(self):
+                raise OSError("connection refused")
+            monkeypatch.setattr(pgwire.PgConnection, "connect", failing_connect)
+            await asyncio.gather(*[pool.execute("SELECT 1") for _ in range(10)])
+            await asyncio.sleep(0.01)
+            await asyncio.gather(*[pool.execute("SELECT 1") for _ in range(10)])
+            await asyncio.sleep(0.01)
+            errors = pool.grow_errors  # one failed attempt, then no retry inside GROW_RETRY_S
+            monkeypatch.setattr(pgwire.PgConnection, "connect", real)
+            await pool.close()
+            return errors, pool.connections
+        finally:
+            await pg.stop()
+    assert run(go()) == (1, 0)
+
+
+def test_pool_close_cancels_a_grow_in_progress(monkeypatch):
+    if os.environ.get("BEHOLDER_PG_BACKGROUND_GROW", "1") == "0":
+        pytest.skip("background pool grow switched off")
+    from beholder_amd.store import pgwire
+    from beholder_amd.store.pgwire import Pool
+
+    async def go():
+        pg = await FakePg(auth="trust").start()
+        try:
+            pool = await Pool(pg.dsn, size=2, spread_at=1).open()
+
+            async def never(self):
+                await asyncio.sleep(3600)
+            monkeypatch.setattr(pgwire.PgConnection, "connect", never)
+            await asyncio.gather(*[pool.execute("SELECT 1") for _ in range(4)])
+            assert pool._growing is not None
+            await asyncio.wait_for(pool.close(), 2)
+            return pool._growing, pool.connections
+        finally:
+            await pg.stop()
+    assert run(go()) == (None, 0)
 
 
 def test_pg_reader_decoding_matches_python_reference():
@@ -458,3 +530,15 @@ def test_compiled_handlers_pick_the_postgres_connection_in_c(monkeypatch):
     assert stats["source"]["acked"] == 30 and comments == 30
     assert type(impl).__name__ == "NativeHandlers"
     assert calls == []  # every lookup went through the direct native pick
+
+
+def test_inline_pool_grow_switch_still_works():
+    """BEHOLDER_PG_BACKGROUND_GROW=0 (read at import) keeps the earlier inline grow: the store
+    suite passes with it."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-p", "no:cacheprovider", "-x", "tests/test_stores.py",
+                        "-k", "not inline_pool_grow_switch"], cwd=root, capture_output=True, text=True,
+                       env=dict(os.environ, BEHOLDER_PG_BACKGROUND_GROW="0"), timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
