@@ -345,6 +345,7 @@ def io_extras(a) -> dict:
                 "tcp_e2e_cpu_us_per_event": _r(e2e.get("cpu_us_per_event")),
                 "tcp_e2e_p50_handle_latency_us": _r(hl.get("p50")),
                 "tcp_e2e_p999_handle_latency_us": _r(hl.get("p999")),
+                "tcp_e2e_warmup_p999_handle_latency_us": _r(e2e.get("warmup_handle_latency_us", {}).get("p999")),
                 "tcp_e2e_errors": e2e.get("errors")})
     tls = harness._tcp_e2e(a.io_events, http_servers=4, tls=True)
     hl = tls.get("handle_latency_us", {})
