@@ -255,7 +255,10 @@ class Service:
             if key not in seen:
                 seen.add(key)
                 origins.append(str(u))
-        got = await asyncio.gather(*(self._http.preconnect(u, n) for u in origins), return_exceptions=True)
+        pre = getattr(self._http, "preconnect", None)
+        if pre is None:  # a duck-typed client without the HttpClient base: nothing to open
+            return
+        got = await asyncio.gather(*(pre(u, n) for u in origins), return_exceptions=True)
         for u, r in zip(origins, got):
             if isinstance(r, BaseException):
                 opened, err = 0, r
