@@ -343,6 +343,10 @@ class Service:
             pool = getattr(self._store, "_pool", None)
             if pool is not None and hasattr(pool, "connections"):
                 g.set({"pool": "postgres", "field": "open"}, pool.connections)
+                for k in ("grows", "grow_errors"):  # background grow (store/pgwire.py Pool)
+                    v = getattr(pool, k, None)
+                    if isinstance(v, int):
+                        g.set({"pool": "postgres", "field": k}, v)
 
         reg.register(Gauge("beholder_pool", "Outbound connection pools (HTTP sinks, Postgres): open/idle "
                            "connections and request/connect/error counts", ["pool", "field"],

@@ -542,3 +542,30 @@ def test_inline_pool_grow_switch_still_works():
                         "-k", "not inline_pool_grow_switch"], cwd=root, capture_output=True, text=True,
                        env=dict(os.environ, BEHOLDER_PG_BACKGROUND_GROW="0"), timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+def test_pool_metrics_render_postgres_connections_and_grows():
+    from beholder_amd.metrics import parse_exposition
+    from beholder_amd.service import Service
+    from beholder_amd.sinks import RecordingHttpClient
+    from beholder_amd.transport.memory import MemoryBroker
+    from beholder_amd.utils.log import Logger, MemoryStream
+
+    from helpers import cfg
+
+    async def go():
+        pg = await FakePg().start()
+        try:
+            st = PostgresStore(pg.dsn, create_schema=True, pool_size=2)
+            svc = Service(cfg(), source=MemoryBroker().consumer(), store=st, http=RecordingHttpClient(),
+                          logger=Logger(stream=MemoryStream()), serve_metrics=False)
+            await svc.init()
+            text = svc.registry.render()
+            await svc.close()
+            return parse_exposition(text)
+        finally:
+            await pg.stop()
+    m = run(go())
+    assert m['beholder_pool{pool="postgres",field="open"}'] == 1
+    assert m['beholder_pool{pool="postgres",field="grows"}'] == 0
+    assert m['beholder_pool{pool="postgres",field="grow_errors"}'] == 0
