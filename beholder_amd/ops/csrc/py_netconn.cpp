@@ -1143,7 +1143,7 @@ PyObject* mod_netconn_connect(PyObject*, PyObject* args, PyObject* kwds) {
 // pg_pool_execute(conns, sql, params, spread_at, size) -> IOFuture, or None for the Python path.
 // store/pgwire.py Pool.execute for a pool whose open connections are all native: the open
 // connection with the fewest queries in flight (the first on ties) gets the query, unless every
-// one has `spread_at` or more in flight and the pool may still grow.
+// one has `spread_at` or more in flight and the pool may still grow (fewer than `size` open).
 PyObject* mod_pg_pool_execute(PyObject*, PyObject* const* a, Py_ssize_t n) {
   if (n != 5 || !PyList_CheckExact(a[0])) {
     PyErr_SetString(PyExc_TypeError, "pg_pool_execute(conns: list, sql, params, spread_at, size)");
@@ -1156,6 +1156,7 @@ PyObject* mod_pg_pool_execute(PyObject*, PyObject* const* a, Py_ssize_t n) {
   Py_ssize_t nc = PyList_GET_SIZE(conns);
   NetConnObject* best = nullptr;
   size_t bp = 0;
+  Py_ssize_t live = 0;  // open connections: a closed one left in the list does not fill the pool
   for (Py_ssize_t i = 0; i < nc; ++i) {
     PyObject* c = PyList_GET_ITEM(conns, i);
     PyObject** dp = _PyObject_GetDictPtr(c);
@@ -1170,13 +1171,14 @@ PyObject* mod_pg_pool_execute(PyObject*, PyObject* const* a, Py_ssize_t n) {
     if (closed != Py_False || Py_TYPE(net) != &NetConnType) Py_RETURN_NONE;  // asyncio transport: Python path
     NetConnObject* nc_ = reinterpret_cast<NetConnObject*>(net);
     if (nc_->kind != K_PG) Py_RETURN_NONE;
+    ++live;
     size_t p = nc_->pending->size();
     if (!best || p < bp) {
       best = nc_;
       bp = p;
     }
   }
-  if (!best || !(bp < size_t(spread < 0 ? 0 : spread) || nc >= size)) Py_RETURN_NONE;
+  if (!best || !(bp < size_t(spread < 0 ? 0 : spread) || live >= size)) Py_RETURN_NONE;
   PyObject* args[2] = {a[1], a[2]};
   return nc_execute(best, args, 2);
 }

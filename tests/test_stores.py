@@ -569,3 +569,35 @@ def test_pool_metrics_render_postgres_connections_and_grows():
     assert m['beholder_pool{pool="postgres",field="open"}'] == 1
     assert m['beholder_pool{pool="postgres",field="grows"}'] == 0
     assert m['beholder_pool{pool="postgres",field="grow_errors"}'] == 0
+
+
+def test_pool_regrows_after_a_connection_breaks():
+    """A broken connection left in the pool's list does not count toward ``size``: the next
+    burst that finds the open ones busy grows the pool back (native pick and Python path)."""
+    from beholder_amd.store.pgwire import Pool
+
+    async def go():
+        pg = await FakePg(auth="trust").start()
+        try:
+            pool = await Pool(pg.dsn, size=2, spread_at=1).open()
+            for _ in range(50):
+                await asyncio.gather(*[pool.execute("SELECT 1") for _ in range(4)])
+                if pool.connections == 2:
+                    break
+                await asyncio.sleep(0.005)
+            assert pool.connections == 2
+            pool._conns[1].abort()
+            await asyncio.sleep(0.01)
+            assert pool.connections == 1
+            for _ in range(50):
+                res = await asyncio.gather(*[pool.execute("SELECT $1 + 0", (i,)) for i in range(4)])
+                assert [r[0][0][0] for r in res] == list(range(4))
+                if pool.connections == 2:
+                    break
+                await asyncio.sleep(0.005)
+            n = pool.connections
+            await pool.close()
+            return n
+        finally:
+            await pg.stop()
+    assert run(go()) == 2
