@@ -50,7 +50,8 @@ SERVICE_DEFAULTS: dict = {
                  "routing_keys": {}, "durable": True, "passive_declare": False, "queue_arguments": {}},
         # index.js:42 `new Storage()` is always Postgres (triton-core/db); dsn default: dyn('postgres')
         # table/columns: triton-core/db's schema is not vendored; defaults are our guess (store/schema.py)
-        "store": {"backend": "postgres", "dsn": None, "pool_size": 4, "create_schema": False,
+        # spread_at: queries in flight on every open connection before the pool opens another
+        "store": {"backend": "postgres", "dsn": None, "pool_size": 4, "spread_at": 8, "create_schema": False,
                   "table": "media", "columns": {}},
         # index.js:28 — Prom.expose(); port/host are [inferred] (triton-core not vendored).
         "metrics": {"enabled": True, "host": "0.0.0.0", "port": 3000, "default_metrics": True},
@@ -306,6 +307,10 @@ class Config:
         except (TypeError, ValueError) as e:
             raise ConfigError(f"service.amqp: {e}") from None
         st = svc.get("store") or {}
+        for k in ("pool_size", "spread_at"):
+            v = st.get(k, 1)
+            if isinstance(v, bool) or not isinstance(v, int) or v < 1:
+                raise ConfigError(f"service.store.{k} must be an integer >= 1, got {v!r}")
         try:
             MediaSchema(st.get("table") or "media", st.get("columns") or {})
         except (TypeError, ValueError) as e:

@@ -34,7 +34,7 @@ class PostgresStore(MediaStore):
     name = "postgres"
 
     def __init__(self, dsn: Optional[str] = None, table: str = "media", pool_size: int = 4,
-                 create_schema: bool = False, columns: Optional[Mapping[str, str]] = None):
+                 create_schema: bool = False, columns: Optional[Mapping[str, str]] = None, spread_at: int = 8):
         if dsn is None:
             from ..dynamics import dyn
             dsn = dyn("postgres")
@@ -42,6 +42,7 @@ class PostgresStore(MediaStore):
         self.dsn = dsn
         self.table = table
         self.pool_size = pool_size
+        self.spread_at = spread_at  # queries in flight on every connection before the pool grows
         self.create_schema = create_schema
         self._pool: Optional[Pool] = None
         # the compiled handlers issue these two texts themselves (py_handlers.cpp pg_execute)
@@ -54,7 +55,7 @@ class PostgresStore(MediaStore):
 
     async def connect(self) -> None:
         if self._pool is None:
-            self._pool = await Pool(self.dsn, self.pool_size).open()
+            self._pool = await Pool(self.dsn, self.pool_size, self.spread_at).open()
             if self.create_schema:
                 await self._pool.execute(self.schema.create_table())
 

@@ -601,3 +601,32 @@ def test_pool_regrows_after_a_connection_breaks():
         finally:
             await pg.stop()
     assert run(go()) == 2
+
+
+def test_store_pool_knobs_reach_the_pool_and_are_validated():
+    from beholder_amd.config import ConfigError
+    from beholder_amd.service import Service
+    from beholder_amd.sinks import RecordingHttpClient
+    from beholder_amd.transport.memory import MemoryBroker
+    from beholder_amd.utils.log import Logger, MemoryStream
+
+    from helpers import cfg
+
+    for bad in ({"spread_at": 0}, {"pool_size": "4"}, {"spread_at": True}):
+        with pytest.raises(ConfigError, match="service.store"):
+            cfg({"service": {"store": bad}})
+
+    async def go():
+        pg = await FakePg(auth="trust").start()
+        try:
+            c = cfg({"service": {"store": {"dsn": pg.dsn, "pool_size": 3, "spread_at": 2}}})
+            svc = Service(c, source=MemoryBroker().consumer(), http=RecordingHttpClient(),
+                          logger=Logger(stream=MemoryStream()), serve_metrics=False)
+            await svc.init()
+            pool = svc.store._pool
+            got = (pool.size, pool.spread_at)
+            await svc.close()
+            return got
+        finally:
+            await pg.stop()
+    assert run(go()) == (3, 2)
