@@ -23,6 +23,8 @@ Additions over the reference:
   dies before any response byte arrives. This applies to idempotent methods only,
   so a POST (a Trello comment) is never sent twice;
 * a per-request deadline that covers connect, TLS, request and response;
+* :meth:`H1Client.preconnect` opens connections ahead of the first requests
+  (``service.http.preconnect``; one name lookup per batch);
 * HTTP proxies (``HTTP_PROXY``) are not supported.
 """
 from __future__ import annotations
@@ -279,7 +281,7 @@ class H1Client(HttpClient):
             self._ssl = _ssl.create_default_context()
         return self._ssl
 
-    async def _connect(self, o: _Origin, deadline: float) -> _Conn:
+    async def _connect(self, o: _Origin, deadline: float, infos=None) -> _Conn:
         loop = asyncio.get_running_loop()
         conn = _Conn(o)
         o.open += 1
@@ -289,7 +291,7 @@ class H1Client(HttpClient):
                 raise asyncio.TimeoutError
             ntls = self._native_tls() if o.tls else None
             if netconn.enabled() and (ntls is not None or not o.tls):
-                await self._connect_native(conn, o, ntls, deadline, loop)
+                await self._connect_native(conn, o, ntls, deadline, loop, infos)
             else:  # asyncio transport: native connections off, or a caller-supplied ssl.SSLContext
                 kw = {"ssl": self._ssl_context(), "server_hostname": o.host} if o.tls else {}
                 await asyncio.wait_for(loop.create_connection(lambda: conn, o.host, o.port, **kw), remaining)
@@ -301,11 +303,13 @@ class H1Client(HttpClient):
         self.counts["connections"] += 1
         return conn
 
-    async def _connect_native(self, conn: _Conn, o: _Origin, ntls, deadline: float, loop) -> None:
+    async def _connect_native(self, conn: _Conn, o: _Origin, ntls, deadline: float, loop, infos=None) -> None:
         """TCP connect, and TLS for ``ntls``, in C (``ops netconn_connect``): no asyncio transport
         is made and dropped. Addresses are tried in order, as ``loop.create_connection`` does
-        (an IP literal as is, a name through ``loop.getaddrinfo``); a TLS failure is final."""
-        infos = self._literal.get(o.host)
+        (an IP literal as is, a name through ``loop.getaddrinfo`` unless ``infos`` carries the
+        addresses already); a TLS failure is final."""
+        if infos is None:
+            infos = self._literal.get(o.host)
         if infos is None:
             try:
                 ipaddress.ip_address(o.host)
@@ -384,7 +388,18 @@ class H1Client(HttpClient):
             return 0, None
         loop = asyncio.get_running_loop()
         deadline = loop.time() + self.timeout_s
-        got = await asyncio.gather(*(self._connect(o, deadline) for _ in range(want)), return_exceptions=True)
+        infos = None
+        if netconn.enabled() and o.host not in self._literal:
+            try:
+                ipaddress.ip_address(o.host)
+            except ValueError:  # a name: one lookup for the whole batch, not one per connection
+                try:
+                    found = await asyncio.wait_for(loop.getaddrinfo(o.host, o.port, type=socket.SOCK_STREAM),
+                                                   self.timeout_s)
+                except (OSError, asyncio.TimeoutError) as e:
+                    return 0, e
+                infos = [ai[4][0] for ai in found]
+        got = await asyncio.gather(*(self._connect(o, deadline, infos) for _ in range(want)), return_exceptions=True)
         opened, err = 0, None
         for c in got:
             if isinstance(c, BaseException):

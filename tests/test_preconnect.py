@@ -129,3 +129,29 @@ def test_service_preconnect_is_harmless_for_clients_without_a_pool():
     stats, msgs = run(go())
     assert stats["received"][STATUS] == 1 and stats["source"]["acked"] == 1
     assert sum(m.startswith("preconnect to ") for m in msgs) == 3  # trello, telegram, emby: 0 each, no error
+
+
+def test_preconnect_resolves_a_host_name_once_for_the_batch(monkeypatch):
+    from beholder_amd.utils import netconn
+    if not netconn.enabled():
+        pytest.skip("native connections switched off")
+
+    async def go():
+        s = await Scripted(lambda n, m, t, h: OK).start()
+        loop = asyncio.get_running_loop()
+        real = loop.getaddrinfo
+        lookups = []
+
+        async def counting(host, *a, **kw):
+            lookups.append(host)
+            return await real("127.0.0.1", *a, **kw)
+        monkeypatch.setattr(loop, "getaddrinfo", counting)
+        c = H1Client(timeout_s=5)
+        opened, err = await c.preconnect(f"http://sink.invalid:{s.port}/", 6)
+        r = await c.request("GET", f"http://sink.invalid:{s.port}/x")
+        await c.close()
+        await s.stop()
+        return opened, err, lookups, r.status, s.connections
+    opened, err, lookups, status, conns = run(go())
+    assert (opened, err, status, conns) == (6, None, 200, 6)
+    assert lookups == ["sink.invalid"]  # one lookup for six connections; the request reused one
