@@ -352,6 +352,7 @@ def io_extras(a) -> dict:
     out.update({"tls_e2e_events_per_sec": _r(tls.get("ingest_rate_eps"), 1),
                 "tls_e2e_cpu_us_per_event": _r(tls.get("cpu_us_per_event")),
                 "tls_e2e_p999_handle_latency_us": _r(hl.get("p999")),
+                "tls_e2e_warmup_p999_handle_latency_us": _r(tls.get("warmup_handle_latency_us", {}).get("p999")),
                 "tls_e2e_errors": tls.get("errors")})
     h = harness._http_tcp(Workload(n_media=10000, seed=a.seed), a.io_events, clients=("h1",))["h1"]
     hl = h["handle_latency_us"]
