@@ -60,7 +60,8 @@ SERVICE_DEFAULTS: dict = {
         "log": {"level": "info", "name": "index.js", "positional_args": "append"},
         # outbound sink HTTP: `h1` = native-parsed keep-alive client (sinks/h1.py), `aiohttp` = library client
         # preconnect: connections opened per sink origin at startup (0 = on demand, as the reference)
-        "http": {"timeout_s": 30.0, "client": "h1", "max_per_host": 100, "keepalive_s": 4.0, "preconnect": 0},
+        "http": {"timeout_s": 30.0, "client": "h1", "max_per_host": 100, "keepalive_s": 4.0, "preconnect": 0,
+                 "preconnect_wait_s": 5.0},
         # SURVEY §5 race detection: opt-in per-mediaId serialisation (default off = parity, Q9).
         "ordering": "none",
         # Q1: what to do with a status message whose handler threw.
@@ -297,6 +298,9 @@ class Config:
             pc = 0
         if isinstance(pc, bool) or not isinstance(pc, int) or pc < 0:
             raise ConfigError(f"service.http.preconnect must be an integer >= 0, got {pc!r}")
+        pw = svc["http"].get("preconnect_wait_s", 5.0)
+        if isinstance(pw, bool) or not isinstance(pw, (int, float)) or pw < 0:
+            raise ConfigError(f"service.http.preconnect_wait_s must be a number >= 0, got {pw!r}")
         ca = svc["http"].get("ca_file")
         if ca is not None and (not isinstance(ca, str) or not os.path.isfile(ca)):
             raise ConfigError(f"service.http.ca_file: not a readable file: {ca!r}")

@@ -134,6 +134,7 @@ class Service:
         self.started_at = 0.0
         self.received = array.array("Q", [0] * len(T.TOPIC_NAMES_BY_ID))
         self.source_error: Optional[str] = None
+        self._preconnecting: set = set()  # preconnect tasks still running after startup
 
     # ------------------------------------------------------------ properties --
     @property
@@ -259,17 +260,33 @@ class Service:
         pre = getattr(self._http, "preconnect", None)
         if pre is None:  # a duck-typed client without the HttpClient base: nothing to open
             return
-        got = await asyncio.gather(*(pre(u, n) for u in origins), return_exceptions=True)
-        for u, r in zip(origins, got):
-            if isinstance(r, BaseException):
-                opened, err = 0, r
-            else:
-                opened, err = r
+
+        def report(u, t):
+            if t.cancelled():
+                return
+            e = t.exception()
+            opened, err = (0, e) if e is not None else t.result()
             origin = redact("/".join(u.split("/", 3)[:3]))
             if err is not None:
                 self.log.warn(f"preconnect to {origin}: {opened}/{n} connections ({type(err).__name__}: {err})")
             else:
                 self.log.info(f"preconnect to {origin}: {opened} connections")
+
+        tasks = []
+        for u in origins:
+            t = asyncio.ensure_future(pre(u, n))
+            t.add_done_callback(lambda t, u=u: report(u, t))
+            tasks.append(t)
+        # startup waits for the connections at most `preconnect_wait_s` (a sink that drops
+        # packets would otherwise hold it for the whole request timeout); the rest finish in
+        # the background and are parked in the pool as they come
+        wait_s = float(self.config.data["service"]["http"].get("preconnect_wait_s", 5.0))
+        _, pending = await asyncio.wait(tasks, timeout=wait_s)
+        if pending:
+            self.log.warn(f"preconnect: {len(pending)} origin(s) still connecting after {wait_s:g} s; "
+                          "continuing startup")
+            self._preconnecting = pending
+        await asyncio.sleep(0)  # the done callbacks of the finished ones log before `initialized`
 
     def _media_key(self, d) -> Any:
         h = self.handlers
@@ -605,6 +622,11 @@ class Service:
 
     async def close(self) -> None:
         """Release transport, store, HTTP client and the metrics server."""
+        for t in self._preconnecting:
+            t.cancel()
+        if self._preconnecting:
+            await asyncio.gather(*self._preconnecting, return_exceptions=True)
+            self._preconnecting = set()
         if self._source is not None:
             await self._source.close()
         if self._store is not None:

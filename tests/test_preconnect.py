@@ -155,3 +155,33 @@ def test_preconnect_resolves_a_host_name_once_for_the_batch(monkeypatch):
     opened, err, lookups, status, conns = run(go())
     assert (opened, err, status, conns) == (6, None, 200, 6)
     assert lookups == ["sink.invalid"]  # one lookup for six connections; the request reused one
+
+
+def test_startup_waits_for_preconnect_at_most_preconnect_wait_s():
+    """A sink that never answers the connect (dropped packets) holds startup for
+    ``preconnect_wait_s``, not for the request timeout; close() cancels what is still running."""
+    class Stuck(RecordingHttpClient):
+        cancelled = 0
+
+        async def preconnect(self, url, n):
+            try:
+                await asyncio.sleep(3600)
+            except asyncio.CancelledError:
+                Stuck.cancelled += 1
+                raise
+
+    async def go():
+        c = cfg({"service": {"http": {"preconnect": 4, "preconnect_wait_s": 0.2}}})
+        svc = _service(c, Stuck())
+        loop = asyncio.get_running_loop()
+        t0 = loop.time()
+        await svc.init()
+        dt = loop.time() - t0
+        pending = len(svc._preconnecting)
+        await svc.close()
+        return dt, pending, [r["msg"] for r in svc.log.stream.records()]
+    dt, pending, msgs = run(go())
+    assert 0.2 <= dt < 2.0 and pending == 3 and Stuck.cancelled == 3  # trello, telegram, emby
+    assert any("still connecting after 0.2 s" in m for m in msgs) and "initialized" in msgs
+    with pytest.raises(ConfigError, match="preconnect_wait_s"):
+        cfg({"service": {"http": {"preconnect_wait_s": -1}}})
