@@ -236,9 +236,10 @@ class Service:
 
     async def _preconnect(self, n: int, endpoints) -> None:
         """``service.http.preconnect``: ``n`` connections to each sink origin the handlers will
-        call (Trello; Telegram and Emby when their DEPLOYED hooks are on), all at once. A sink
-        that cannot be reached is warned about, never fatal: the reference only meets it on the
-        first event, and the handlers connect on demand as they always do."""
+        call (Trello; Telegram and Emby when their DEPLOYED hooks are on), all at once, with
+        startup held for at most ``preconnect_wait_s``. A sink that cannot be reached is warned
+        about, never fatal: the reference only meets it on the first event, and the handlers
+        connect on demand as they always do."""
         from .sinks.emby import _PATH as emby_path
         from .sinks.http import redact
         urls = [endpoints["trello"]]
