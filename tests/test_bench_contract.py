@@ -13,7 +13,8 @@ REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step
 EXTRAS = {"all_procs_events_per_sec", "rate_10k_p50_ingest_latency_us", "rate_10k_p99_ingest_latency_us",
           "soak_rss_growth_mb", "soak_gc_max_pause_us", "overload_dropped", "tcp_e2e_events_per_sec",
           "http_tcp_h1_p999_handle_latency_us", "p50_handle_latency_us", "tls_e2e_events_per_sec",
-          "tls_e2e_cpu_us_per_event"}
+          "tls_e2e_cpu_us_per_event", "cpu_us_per_event", "involuntary_ctx_switches",
+          "tcp_e2e_warmup_p999_handle_latency_us", "tls_e2e_warmup_p999_handle_latency_us"}
 SMALL = ["--steps", "2", "--warmup", "1", "--events-per-step", "4096", "--media", "500"]
 
 
