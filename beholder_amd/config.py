@@ -78,6 +78,10 @@ SERVICE_DEFAULTS: dict = {
         "trace": False,
         # handlers compiled to native state machines (ops/csrc/py_handlers.cpp); false = handlers.py
         "native_handlers": True,
+        # how inbound bodies are decoded (index.js:63,129): protobufjs = the reference library's reader
+        # (malformed input reads, fails and logs exactly as protobufjs 6.8.8 does, ops/csrc/pbjs.hpp);
+        # upb = google.protobuf's stricter acceptance rules
+        "proto": {"dialect": "protobufjs"},
         # Jaeger spans per delivery (utils/tracing.py); JAEGER_* env variables override
         "tracing": {"enabled": False, "service_name": "beholder",
                     # jaeger-client's fallback when no remote sampler answers: 1 trace in 1000
@@ -291,6 +295,8 @@ class Config:
             raise ConfigError("service.on_status_error must be leave_unacked|nack_requeue|nack_drop")
         if svc["log"].get("positional_args", "append") not in ("append", "drop"):
             raise ConfigError("service.log.positional_args must be 'append' or 'drop'")
+        if (svc.get("proto") or {}).get("dialect", "protobufjs") not in ("protobufjs", "upb"):
+            raise ConfigError("service.proto.dialect must be 'protobufjs' or 'upb'")
         if svc["http"].get("client", "h1") not in ("h1", "aiohttp"):
             raise ConfigError("service.http.client must be 'h1' or 'aiohttp'")
         pc = svc["http"].get("preconnect", 0)

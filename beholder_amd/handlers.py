@@ -76,6 +76,20 @@ def err_message(err: BaseException) -> str:
     return s if s else type(err).__name__
 
 
+def js_object_keys(obj: Mapping) -> list:
+    """``Object.keys(obj)`` as strings, in ECMAScript property order: array-index keys
+    (canonical integers below 2**32 - 1) ascending, then the other keys in insertion order."""
+    idx, rest = [], []
+    for k in obj.keys():
+        s = k if type(k) is str else js_str(k)
+        if s.isdigit() and s.isascii() and (s == "0" or s[0] != "0") and int(s) < 4294967295:
+            idx.append((int(s), s))
+        else:
+            rest.append(s)
+    idx.sort()
+    return [s for _, s in idx] + rest
+
+
 class JsTypeError(TypeError):
     """What V8 raises where the reference dereferences ``undefined``."""
 
@@ -120,8 +134,9 @@ class TelemetryHandlers:
         self.status_proto = proto.load("api.TelemetryStatus")      # index.js:47
         self.progress_proto = proto.load("api.TelemetryProgress")  # index.js:46
         self.media_proto = proto.load("api.Media")                 # index.js:48
-        self.decode_status = decode_status or _decoder(self.status_proto)
-        self.decode_progress = decode_progress or _decoder(self.progress_proto)
+        dialect = _dialect(config)
+        self.decode_status = decode_status or _decoder(self.status_proto, dialect)
+        self.decode_progress = decode_progress or _decoder(self.progress_proto, dialect)
 
         # enumToString tables (index.js:74,134): number -> name, first name wins
         self._status_names_s = self.status_proto.enum("TelemetryStatusEntry")[0]
@@ -236,7 +251,7 @@ class TelemetryHandlers:
         """index.js:88 (Q5)."""
         text, paren, avail = _LOG_MISSING
         self.log.warn(text, status, paren.replace("{}", js_str(status_text)),
-                      avail.replace("{}", ",".join(str(k) for k in self.lists.keys())))
+                      avail.replace("{}", ",".join(js_object_keys(self.lists))))  # `${Object.keys(lists)}`
 
     async def _deployed_hooks(self, media, media_id: Any) -> None:
         """Body of the DEPLOYED branch, index.js:95-118 (the caller holds the try of index.js:92)."""
@@ -302,10 +317,19 @@ def native_handlers(handlers: TelemetryHandlers):
     return native.NativeHandlers(handlers)
 
 
-def _decoder(ptype) -> Callable:
-    """Native decode if the schema is flat, else upb (same field names either way)."""
+def _dialect(config) -> str:
+    """``service.proto.dialect`` (default ``protobufjs``, the reference's reader)."""
+    try:
+        d = config.data.get("service", {}).get("proto", {}).get("dialect")
+    except AttributeError:
+        d = None
+    return d or "protobufjs"
+
+
+def _decoder(ptype, dialect: str = "protobufjs") -> Callable:
+    """Native decode if the schema is flat (in ``dialect``), else upb (same field names either way)."""
     from .ops import codec_for
-    codec = codec_for(ptype)
+    codec = codec_for(ptype, dialect) or codec_for(ptype)
     if codec is not None:
         return codec.decode
     return lambda data: proto.decode(ptype, data)

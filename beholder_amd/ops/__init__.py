@@ -102,7 +102,7 @@ _KIND_OF = {
     _FD.TYPE_SFIXED32: K_SFIXED32, _FD.TYPE_SFIXED64: K_SFIXED64,
 }
 
-_codecs: Dict[str, Optional[object]] = {}
+_codecs: Dict[tuple, Optional[object]] = {}
 
 
 def field_table(descriptor):
@@ -121,13 +121,27 @@ def field_table(descriptor):
     return out or None
 
 
-def codec_for(ptype) -> Optional[object]:
-    """Native ``MessageCodec`` for a :class:`~beholder_amd.models.proto.ProtoType` (cached)."""
-    key = ptype.full_name
+DIALECTS = ("upb", "protobufjs")
+
+
+def codec_for(ptype, dialect: str = "upb") -> Optional[object]:
+    """Native ``MessageCodec`` for a :class:`~beholder_amd.models.proto.ProtoType` (cached).
+
+    ``dialect`` picks how malformed input is read: ``upb`` (google.protobuf's rules, the test
+    oracle for tooling) or ``protobufjs`` (the reference's reader, ``csrc/pbjs.hpp``). Valid
+    input decodes identically. None when the schema is not flat, or when the protobufjs
+    dialect is asked for a 64-bit integer field it does not model."""
+    key = (ptype.full_name, dialect)
     if key in _codecs:
         return _codecs[key]
     table = field_table(ptype.descriptor)
-    codec = MessageCodec(ptype.full_name, table) if table else None
+    codec = None
+    if table:
+        try:
+            codec = MessageCodec(ptype.full_name, table, dialect)
+        except ValueError:
+            if dialect not in DIALECTS:
+                raise
     _codecs[key] = codec
     return codec
 

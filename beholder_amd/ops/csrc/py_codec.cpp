@@ -11,6 +11,7 @@
 #include <string>
 #include <vector>
 
+#include "pbjs.hpp"
 #include "py_common.hpp"
 #include "wire.hpp"
 
@@ -26,8 +27,15 @@ struct FieldSpec {
   int kind;
 };
 
+// Decode dialects: how malformed input is read (valid input decodes the same either way).
+enum Dialect : int {
+  D_UPB = 0,         // google.protobuf acceptance rules (wire.hpp), the tooling / test oracle
+  D_PROTOBUFJS = 1,  // protobufjs 6.8.8 BufferReader (pbjs.hpp), what the reference runs
+};
+
 struct CodecObject {
   PyObject_HEAD PyTypeObject* result_type;
+  int dialect;
   std::vector<int16_t>* by_number;  // field number -> slot (-1 = unknown)
   std::vector<FieldSpec>* fields;   // by slot
   PyObject* defaults;               // tuple, per slot
@@ -74,6 +82,7 @@ PyObject* codec_new(PyTypeObject* type, PyObject*, PyObject*) {
   CodecObject* self = reinterpret_cast<CodecObject*>(type->tp_alloc(type, 0));
   if (!self) return nullptr;
   self->result_type = nullptr;
+  self->dialect = D_UPB;
   self->by_number = nullptr;
   self->fields = nullptr;
   self->defaults = nullptr;
@@ -82,7 +91,7 @@ PyObject* codec_new(PyTypeObject* type, PyObject*, PyObject*) {
   return reinterpret_cast<PyObject*>(self);
 }
 
-// MessageCodec(type_name: str, fields: sequence of (number, name, kind))
+// MessageCodec(type_name: str, fields: sequence of (number, name, kind), dialect="upb")
 int codec_init_impl(CodecObject* self, PyObject* args, PyObject* kwds);
 int codec_init(CodecObject* self, PyObject* args, PyObject* kwds) {
   BEHOLDER_TRY { return codec_init_impl(self, args, kwds); }
@@ -90,11 +99,20 @@ int codec_init(CodecObject* self, PyObject* args, PyObject* kwds) {
 }
 
 int codec_init_impl(CodecObject* self, PyObject* args, PyObject* kwds) {
-  static const char* kwlist[] = {"type_name", "fields", nullptr};
+  static const char* kwlist[] = {"type_name", "fields", "dialect", nullptr};
   const char* tname;
   PyObject* fields;
-  if (!PyArg_ParseTupleAndKeywords(args, kwds, "sO", const_cast<char**>(kwlist), &tname, &fields))
+  const char* dialect = "upb";
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "sO|s", const_cast<char**>(kwlist), &tname, &fields, &dialect))
     return -1;
+  if (std::strcmp(dialect, "upb") == 0) {
+    self->dialect = D_UPB;
+  } else if (std::strcmp(dialect, "protobufjs") == 0) {
+    self->dialect = D_PROTOBUFJS;
+  } else {
+    PyErr_Format(PyExc_ValueError, "unknown dialect %s (upb|protobufjs)", dialect);
+    return -1;
+  }
   PyObject* seq = PySequence_Fast(fields, "fields must be a sequence");
   if (!seq) return -1;
   Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
@@ -123,6 +141,12 @@ int codec_init_impl(CodecObject* self, PyObject* args, PyObject* kwds) {
     }
     if (kind < wire::K_STRING || kind > wire::K_SFIXED64) {
       PyErr_Format(PyExc_ValueError, "unknown field kind %d", kind);
+      goto fail;
+    }
+    if (self->dialect == D_PROTOBUFJS && (kind == wire::K_INT64 || kind == wire::K_UINT64 || kind == wire::K_SINT64 ||
+                                          kind == wire::K_FIXED64 || kind == wire::K_SFIXED64)) {
+      // protobufjs returns Long objects for these; nothing in the telemetry schema uses them
+      PyErr_Format(PyExc_ValueError, "protobufjs dialect does not model 64-bit integer field %s", fname);
       goto fail;
     }
     for (auto& s : *specs) {
@@ -215,6 +239,51 @@ const char* decode_into(CodecObject* self, const uint8_t* data, size_t len, Slot
   return nullptr;
 }
 
+// protobufjs dialect (pbjs.hpp): the generated decoder's loop. Values are final (already
+// narrowed as protobufjs narrows them); strings hold their clamped byte range.
+bool decode_pbjs_into(CodecObject* self, pbjs::Reader& r, SlotVal* vals, bool* seen) {
+  const auto& bynum = *self->by_number;
+  const auto& specs = *self->fields;
+  while (r.pos < r.len) {
+    uint32_t t;
+    if (!r.uint32(&t)) return false;
+    uint32_t field = t >> 3;
+    int slot = field < bynum.size() ? bynum[field] : -1;
+    if (slot < 0) {
+      if (!r.skip_type(t & 7)) return false;
+      continue;
+    }
+    SlotVal& v = vals[slot];
+    switch (specs[slot].kind) {
+      case wire::K_STRING:
+        if (!r.string(&v.s.p, &v.s.n)) return false;
+        break;
+      case wire::K_BYTES:
+        if (!r.bytes(&v.s.p, &v.s.n)) return false;
+        break;
+      case wire::K_FLOAT:
+      case wire::K_FIXED32:
+      case wire::K_SFIXED32: {
+        uint32_t x;
+        if (!r.fixed32(&x)) return false;
+        v.u = x;
+        break;
+      }
+      case wire::K_DOUBLE:
+        if (!r.fixed64(&v.u)) return false;
+        break;
+      default: {  // int32 / enum / uint32 / sint32 / bool: Reader.uint32() and its narrowing
+        uint32_t x;
+        if (!r.uint32(&x)) return false;
+        v.u = x;
+        break;
+      }
+    }
+    seen[slot] = true;
+  }
+  return true;
+}
+
 PyObject* value_for(int kind, const SlotVal& v) {
   switch (kind) {
     case wire::K_STRING:
@@ -267,14 +336,27 @@ PyObject* codec_decode_raw(PyObject* self_obj, const uint8_t* data, size_t len) 
   const size_t n = self->fields->size();
   SlotVal vals[MAX_FIELDS];
   bool seen[MAX_FIELDS] = {false};
-  const char* err = decode_into(self, data, len, vals, seen);
-  if (err) return raise_decode(err, self->type_name);
+  const bool pbjs_dialect = self->dialect == D_PROTOBUFJS;
+  if (pbjs_dialect) {
+    pbjs::Reader r(data, len);
+    if (!decode_pbjs_into(self, r, vals, seen)) {
+      // protobufjs's own message: it is what `err.message` logs (index.js:150)
+      PyErr_SetString(g_state.decode_error ? g_state.decode_error : PyExc_ValueError, r.err);
+      return nullptr;
+    }
+  } else {
+    const char* err = decode_into(self, data, len, vals, seen);
+    if (err) return raise_decode(err, self->type_name);
+  }
   PyObject* out = PyStructSequence_New(self->result_type);
   if (!out) return nullptr;
   for (size_t i = 0; i < n; ++i) {
     PyObject* v;
     if (seen[i]) {
-      v = value_for((*self->fields)[i].kind, vals[i]);
+      const int kind = (*self->fields)[i].kind;
+      v = pbjs_dialect && (kind == wire::K_STRING) ? PyUnicode_DecodeUTF8(reinterpret_cast<const char*>(vals[i].s.p),
+                                                                          Py_ssize_t(vals[i].s.n), "replace")
+                                                   : value_for(kind, vals[i]);
       if (!v) {
         Py_DECREF(out);
         if (PyErr_ExceptionMatches(PyExc_UnicodeDecodeError)) {
@@ -484,6 +566,9 @@ PyObject* codec_get_type_name(CodecObject* self, void*) {
   Py_INCREF(self->type_name);
   return self->type_name;
 }
+PyObject* codec_get_dialect(CodecObject* self, void*) {
+  return PyUnicode_FromString(self->dialect == D_PROTOBUFJS ? "protobufjs" : "upb");
+}
 
 PyMethodDef codec_methods[] = {
     {"decode", reinterpret_cast<PyCFunction>(codec_decode), METH_O,
@@ -496,6 +581,7 @@ PyGetSetDef codec_getset[] = {
     {"result_type", reinterpret_cast<getter>(codec_get_result_type), nullptr, "decoded message type", nullptr},
     {"field_names", reinterpret_cast<getter>(codec_get_names), nullptr, "field names in slot order", nullptr},
     {"type_name", reinterpret_cast<getter>(codec_get_type_name), nullptr, "message type name", nullptr},
+    {"dialect", reinterpret_cast<getter>(codec_get_dialect), nullptr, "decode dialect: upb | protobufjs", nullptr},
     {nullptr, nullptr, nullptr, nullptr, nullptr}};
 
 // materialise_table(buf, table) -> [(mediaId, status, progress, host), ...]

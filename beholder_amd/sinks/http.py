@@ -132,7 +132,8 @@ class HttpResponse:
     def raise_for_status(self) -> "HttpResponse":
         if not self.ok:
             # request-promise StatusCodeError: `${statusCode} - ${JSON.stringify(body)}`
-            raise HttpError(f"{self.status} - {_json.dumps(self.text())}", self.status, self.body)
+            # (JSON.stringify leaves non-ASCII characters as they are: ensure_ascii=False)
+            raise HttpError(f"{self.status} - {_json.dumps(self.text(), ensure_ascii=False)}", self.status, self.body)
         return self
 
 
@@ -230,13 +231,14 @@ class RecordingHttpClient(HttpClient):
     def add_rule(self, method: str, url_prefix: str, fn) -> None:
         self.rules.append((method.upper(), url_prefix, fn))
 
-    def fail(self, method: str, url_prefix: str, status: Optional[int] = None, message: str = "ECONNREFUSED"):
+    def fail(self, method: str, url_prefix: str, status: Optional[int] = None, message: str = "ECONNREFUSED",
+             body: bytes = b'"error"'):
         if status is None:
             def boom(m, u):
                 raise HttpError(message)
             self.add_rule(method, url_prefix, boom)
         else:
-            self.add_rule(method, url_prefix, lambda m, u: HttpResponse(status, b'"error"', url=u))
+            self.add_rule(method, url_prefix, lambda m, u: HttpResponse(status, body, url=u))
 
     async def request(self, method, url, *, params=None, timeout=None) -> HttpResponse:
         m = method.upper()

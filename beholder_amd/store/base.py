@@ -22,7 +22,7 @@ from typing import Iterable, NamedTuple, Optional
 
 class MediaNotFound(LookupError):
     def __init__(self, media_id: str):
-        super().__init__(f"media {media_id!r} not found")
+        super().__init__(f"media {media_id} not found")  # the stand-in db.js text (tests/reference_oracle.py)
         self.media_id = media_id
 
 

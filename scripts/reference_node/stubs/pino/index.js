@@ -15,11 +15,24 @@ function render (a) {
   return String(a)
 }
 
-// positional args joined with spaces: the same text volume as the rebuilt service (quirk Q11 fix)
+// positional args joined with spaces: the rebuilt service's default (quirk Q11 fix,
+// service.log.positional_args: append)
 function format (args) {
   let s = render(args[0])
   for (let i = 1; i < args.length; i++) s += ' ' + render(args[i])
   return s
+}
+
+// pino@5 itself (positional_args: drop): the message is quick-format-unescaped(args[0], rest),
+// which keeps only what a %-specifier consumes. Every index.js call site that passes extra
+// arguments has a constant first argument without '%' (index.js:51,88,121,133,150), so the
+// text is args[0]; a '%' there would need the full formatter, which is not modelled here.
+function formatDrop (args) {
+  const f = args[0]
+  if (args.length > 1 && typeof f === 'string' && f.indexOf('%') !== -1) {
+    throw new Error('pino stub: %-specifiers with extra arguments are not modelled')
+  }
+  return render(f)
 }
 
 module.exports = function pino (opts) {
@@ -27,6 +40,7 @@ module.exports = function pino (opts) {
   const head = ',"pid":' + process.pid + ',"hostname":' + JSON.stringify(os.hostname()) +
     ',"name":' + JSON.stringify((opts && opts.name) || 'pino')
   const min = LEVELS[h.logLevel || 'info']
+  const fmt = h.positionalArgs === 'drop' ? formatDrop : format
   const logger = {}
   for (const name of Object.keys(LEVELS)) {
     const num = LEVELS[name]
@@ -34,7 +48,7 @@ module.exports = function pino (opts) {
       ? function () {}
       : function () {
         sink.write('{"level":' + num + ',"time":' + Date.now() + head + ',"msg":' +
-          JSON.stringify(format(arguments)) + ',"v":1}\n')
+          JSON.stringify(fmt(arguments)) + ',"v":1}\n')
       }
   }
   return logger

@@ -1,6 +1,8 @@
 'use strict'
 // In-process stand-in for request-promise-native@1.0.7 over request@2.88 (qs 6.5, RFC 3986
-// encoding): builds the GET URL from `url` + `qs`, records it and resolves with the body.
+// encoding): builds the GET URL from `url` + `qs`, records it and lets the harness answer
+// (h.reply): a transport error rejects with that error; a non-2xx status rejects with
+// request-promise's StatusCodeError (simple: true), message `${statusCode} - ${JSON.stringify(body)}`.
 const h = global.__beholderHarness
 
 function rfc3986 (s) {
@@ -18,6 +20,7 @@ module.exports = function request (opts) {
     }
     if (q) url += (url.indexOf('?') === -1 ? '?' : '&') + q
   }
-  h.record(opts.method || 'GET', url)
-  return Promise.resolve('{}')
+  const method = opts.method || 'GET'
+  h.record(method, url)
+  return h.reply('request', method, url)
 }

@@ -2,7 +2,9 @@
 // In-process stand-in for trello@0.9.1 (yarn.lock:1982-1989): makeRequest validates the method and
 // path, merges key/token with the options into the query string (restler + qs 1.2 encoding =
 // encodeURIComponent) and resolves without network I/O. The request is recorded, like the
-// rebuilt service's bench recorder.
+// rebuilt service's bench recorder, and answered by the harness (h.reply): trello@0.9.1's promise
+// rejects only on a transport error (restler 'complete' with an Error) and resolves with the
+// body on any HTTP status.
 const h = global.__beholderHarness
 const METHODS = { get: 'GET', post: 'POST', put: 'PUT', delete: 'DELETE' }
 
@@ -27,8 +29,9 @@ Trello.prototype.makeRequest = function (requestMethod, path, options) {
     if (query[k] === undefined) continue
     qs += (qs ? '&' : '') + encodeURIComponent(k) + '=' + encodeURIComponent(query[k])
   }
-  h.record(method, this.uri + path + '?' + qs)
-  return Promise.resolve({})
+  const url = this.uri + path + '?' + qs
+  h.record(method, url)
+  return h.reply('trello', method, url)
 }
 
 module.exports = Trello

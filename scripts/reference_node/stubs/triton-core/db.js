@@ -1,20 +1,27 @@
 'use strict'
 // triton-core/db stand-in: the media table as an in-memory Map (the rebuilt service's bench
 // uses its in-memory store the same way). Both methods stay async, like the Postgres-backed one.
+//
+// triton-core/db is not vendored, so two behaviours are [inferred], and match the rebuilt
+// service's documented choice (beholder_amd/store/base.py):
+//   * updateStatus of an unknown id changes nothing (an SQL UPDATE that matches zero rows);
+//   * getByID of an unknown id rejects. The error text is the harness's `notFound` template
+//     ("{id}" is replaced by the media id), so the oracle can set one string for both sides.
 class Storage {
   constructor () {
-    this.media = global.__beholderHarness.media
+    const h = global.__beholderHarness
+    this.media = h.media
+    this.notFound = h.notFound || 'media {id} not found'
   }
 
   async updateStatus (mediaId, status) {
     const m = this.media.get(mediaId)
-    if (!m) throw new Error('media ' + mediaId + ' not found')
-    m.status = status
+    if (m) m.status = status
   }
 
   async getByID (mediaId) {
     const m = this.media.get(mediaId)
-    if (!m) throw new Error('media ' + mediaId + ' not found')
+    if (!m) throw new Error(this.notFound.split('{id}').join(mediaId))
     return m
   }
 }

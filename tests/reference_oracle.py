@@ -1,0 +1,329 @@
+"""Reference-executed parity gate: the reference's own ``index.js`` against both handler implementations.
+
+``scripts/reference_node/oracle.js`` runs ``/root/reference/index.js`` (loaded in place, never
+copied) on the image's Node under the stand-ins in ``scripts/reference_node/stubs`` and records,
+per delivered event, acks, the listener's rejection, whether decode threw, every sink request
+(method + full URL) and every log line; at the end it records the counters and the media
+table's statuses. :func:`run_python` replays the same scenario through this repo's handlers
+(``handlers.py`` or the compiled ``ops/csrc/py_handlers.cpp``) and records the same things;
+:func:`diff` compares them field by field.
+
+A scenario (:func:`make_scenario`) is a seeded random config, media table, sink-fault list and
+event stream. The streams are built to reach every branch of index.js:50-155, malformed bodies
+included (truncated fields, wrong wire types, unknown fields and groups, invalid UTF-8, field
+number 0). Modes: ``base``, ``no_trello`` (NO_TRELLO set, index.js:70), ``faults`` (transport
+errors and non-2xx answers from Trello, Telegram and Emby, index.js:92-122) and ``drop``
+(``positional_args: drop``, pino@5's exact message text, quirk Q11).
+
+What the stand-ins assume is listed in their headers. The ones that touch this comparison:
+``triton-core/db`` (not vendored) rejects ``getByID`` of an unknown id with the text in
+``NOT_FOUND`` and ignores ``updateStatus`` of one; ``trello@0.9.1`` resolves on any HTTP status;
+``request-promise`` rejects non-2xx with ``StatusCodeError``.
+
+Run by ``tests/test_reference_oracle.py``; by hand:
+``python tests/reference_oracle.py --seeds 10 --events 600``.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import os
+import random
+import shutil
+import subprocess
+import sys
+import tempfile
+from typing import Dict, List, Optional
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+if HERE not in sys.path:
+    sys.path.insert(0, HERE)
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+from beholder_amd.config import Config  # noqa: E402
+from beholder_amd.models import proto  # noqa: E402
+from beholder_amd.ops import codec_for  # noqa: E402
+from beholder_amd.sinks import RecordingHttpClient  # noqa: E402
+from beholder_amd.store import Media  # noqa: E402
+
+REFERENCE_INDEX = os.environ.get("BEHOLDER_REFERENCE_INDEX", "/root/reference/index.js")
+ORACLE_JS = os.path.join(ROOT, "scripts", "reference_node", "oracle.js")
+STUBS = os.path.join(ROOT, "scripts", "reference_node", "stubs")
+NODE = shutil.which("node")
+NOT_FOUND = "media {id} not found"  # beholder_amd.store.base.MediaNotFound's text
+MODES = ("base", "no_trello", "faults", "drop")
+
+_S = codec_for(proto.load("api.TelemetryStatus"))
+_P = codec_for(proto.load("api.TelemetryProgress"))
+
+
+def available() -> bool:
+    return NODE is not None and os.path.exists(REFERENCE_INDEX)
+
+
+# ---------------------------------------------------------------------------------- scenarios ---
+def _varint(v: int) -> bytes:
+    v &= (1 << 64) - 1
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def _malformed(rng: random.Random, ids: List[str]) -> bytes:
+    """Bodies that reach protobufjs's reader edge cases (ops/csrc/pbjs.hpp lists them)."""
+    mid = rng.choice(ids).encode()
+    st = rng.randrange(-1, 8)
+    valid = _P.encode((mid.decode(), st, rng.randrange(0, 101), "w")) if rng.random() < 0.5 else \
+        _S.encode((mid.decode(), st))
+    kind = rng.randrange(14)
+    if kind == 0:  # random bytes
+        return bytes(rng.randrange(256) for _ in range(rng.randrange(1, 14)))
+    if kind == 1:  # truncated valid message
+        return valid[:rng.randrange(1, max(2, len(valid)))]
+    if kind == 2:  # mediaId with a varint wire type (read as a string anyway)
+        return b"\x08" + _varint(rng.randrange(0, 6)) + mid + b"\x10\x04"
+    if kind == 3:  # status with a length-delimited wire type
+        return b"\x0a" + _varint(len(mid)) + mid + b"\x12\x02\x04\x05"
+    if kind == 4:  # unknown fields of every wire type, then the real fields
+        return (b"\x48\x96\x01" + b"\x51" + bytes(8) + b"\x5a\x02hi" + b"\x65" + bytes(4) + valid)
+    if kind == 5:  # a group (start/end of different field numbers), nested
+        return b"\x6b\x73\x08\x01\x74\x6c" + valid
+    if kind == 6:  # stray end-group / wire types 6 and 7
+        return valid + bytes([rng.choice([0x4c, 0x4e, 0x4f, 0x0e])])
+    if kind == 7:  # invalid UTF-8 in the media id and host
+        bad = bytes([0xFF, 0xC3, 0x28, 0xED, 0xA0, 0x80, 0xF0, 0x9F, 0x98])
+        return b"\x0a" + _varint(len(bad)) + bad + b"\x10\x02\x18\x07\x22\x03\xe2\x82\x28"
+    if kind == 8:  # string length past the end (clamped by protobufjs's BufferReader)
+        return b"\x0a" + _varint(len(mid) + rng.randrange(1, 50)) + mid
+    if kind == 9:  # 10-byte varints (negative int32 status / progress), then more fields
+        return b"\x0a" + _varint(len(mid)) + mid + b"\x10" + _varint(-rng.randrange(1, 3)) + b"\x18" + \
+            _varint(-5) + b"\x22\x01h"
+    if kind == 10:  # field number 0 and a tag with a 5-byte varint
+        return b"\x00\x00" + b"\x80\x80\x80\x80\x00" + valid
+    if kind == 11:  # two messages concatenated: the last value of each field wins
+        return valid + _S.encode(("m1", 4))
+    if kind == 12:  # uint32 overrun: 5 continuation bytes, then fewer than 5 left
+        return b"\x10\xff\xff\xff\xff\xff\x01\x02"
+    return b"\x1d\x01\x02\x03\x04" + valid  # progress field with a fixed32 wire type
+
+
+def make_scenario(seed: int, n_events: int = 520, mode: str = "base") -> dict:
+    """A seeded random config, media table, fault list and event stream."""
+    rng = random.Random(seed * 7919 + MODES.index(mode))
+    names = ["Cowboy Bebop", "Ü & ?", "", "50% *off* [x](y)", "new\nline", "🎬 Trigun"]
+    card_ids = ["card1", "c/2", "", "ü", "a&b=c?d#e", "5f1a0b2c3d4e5f6a7b8c9d0e", "%20 +"]
+    ids = ["m%d" % i for i in range(10)] + ["ü-7", "x y", "%s", ""]
+    media = []
+    for mid in ids:
+        if rng.random() < 0.85:
+            media.append({"id": mid, "name": rng.choice(names), "creator": rng.choice([0, 1, 1, 1, 2]),
+                          "creatorId": rng.choice(card_ids), "metadataId": rng.choice(["1", "42", "", "ä"]),
+                          "status": rng.randrange(0, 7)})
+    statuses = ["queued", "downloading", "converting", "uploading", "deployed", "errored"]
+    flow = {}
+    keys = statuses + ["1", "10", "02"]  # integer-like keys come first in Object.keys
+    rng.shuffle(keys)
+    for k in keys:
+        if rng.random() < 0.6:
+            flow[k] = rng.choice(["L1", "L2", "", 0, 7, "list-ü", "a b"])
+    config: dict = {
+        "keys": {"trello": {"key": "TK", "token": rng.choice(["TT", "t/k=1"])}},
+        "instance": {"flow_ids": flow},
+    }
+    if rng.random() < 0.85:
+        config["keys"]["telegram"] = {"token": rng.choice(["123:TG", "9:a/b"])}
+    if rng.random() < 0.8:
+        config["keys"]["emby"] = {"token": rng.choice(["EMBYKEY", "", "k&y"])}
+    if rng.random() < 0.85:
+        config["instance"]["telegram"] = {"enabled": rng.choice([True, True, False, "yes", 0]),
+                                          "channel": rng.choice(["-1001", 5, "@chan nel"])}
+    if rng.random() < 0.85:
+        config["instance"]["emby"] = {"enabled": rng.choice([True, True, False]),
+                                      "host": rng.choice(["http://emby:8096", "https://e.example/x"])}
+    faults: List[dict] = []
+    if mode == "faults":  # both hooks on, so a Telegram failure visibly skips Emby (Q4)
+        config["keys"]["telegram"] = {"token": "123:TG"}
+        config["keys"]["emby"] = {"token": "EMBYKEY"}
+        config["instance"]["telegram"] = {"enabled": True, "channel": "-1001"}
+        config["instance"]["emby"] = {"enabled": True, "host": rng.choice(["http://emby:8096", "https://e.example/x"])}
+        pool = [("POST", "https://api.trello.com"), ("PUT", "https://api.trello.com"),
+                ("GET", "https://api.telegram.org"), ("GET", "http://emby"), ("GET", "https://e.example"),
+                ("*", "https://api.trello.com/1/cards/card1")]
+        for method, prefix in rng.sample(pool, rng.randrange(1, 4)):
+            f = {"method": method, "prefix": prefix, "status": rng.choice([None, 404, 500, 502, 204]),
+                 "message": rng.choice(["ECONNREFUSED", "socket hang up"]),
+                 "body": rng.choice(['"error"', '{"ok":false,"description":"Bad Request: chat not found é"}'])}
+            faults.append(f)
+    msg_ids = ids + ["missing", "m1", "m1", "m2"]
+    events = []
+    for _ in range(n_events):
+        r = rng.random()
+        mid = rng.choice(msg_ids)
+        st = rng.choice([4, 4, 4, 2]) if rng.random() < 0.3 else rng.choice([-1, 0, 1, 2, 3, 5, 6, 7, 2 ** 31 - 1])
+        if r < 0.12:
+            events.append(["status" if rng.random() < 0.5 else "progress", _malformed(rng, ids).hex()])
+        elif r < 0.5:
+            events.append(["status", _S.encode((mid, st)).hex()])
+        else:
+            prog = rng.choice([0, 5, 45, 100, -5, 150, 2 ** 31 - 1, -2 ** 31])
+            host = rng.choice(["", "", "worker-1", "ünï", "a b&c", "%s %d"])
+            events.append(["progress", _P.encode((mid, st, prog, host)).hex()])
+    return {"seed": seed, "mode": mode, "config": config, "media": media, "events": events, "faults": faults,
+            "positionalArgs": "drop" if mode == "drop" else "append", "notFound": NOT_FOUND, "logLevel": "info",
+            "noTrello": mode == "no_trello"}
+
+
+# ------------------------------------------------------------------------------------- runners ---
+def run_node(sc: dict, timeout: float = 120.0) -> dict:
+    """The reference's own index.js on Node, under the stand-ins (oracle.js)."""
+    env = dict(os.environ, NODE_PATH=STUBS)
+    env.pop("NO_TRELLO", None)
+    if sc.get("noTrello"):
+        env["NO_TRELLO"] = "1"
+    with tempfile.NamedTemporaryFile("w", suffix=".json", delete=False) as f:
+        json.dump(sc, f)
+        path = f.name
+    try:
+        r = subprocess.run([NODE, ORACLE_JS, "--index", REFERENCE_INDEX, "--scenario", path], env=env,
+                           capture_output=True, text=True, timeout=timeout)
+    finally:
+        os.unlink(path)
+    if r.returncode != 0:
+        raise RuntimeError(f"oracle.js failed ({r.returncode}): {r.stderr[-2000:]}")
+    return json.loads(r.stdout)
+
+
+def _counter_hashes(counter, label_names) -> list:
+    """prom-client's hashMap keys ("k:v" joined by ",", keys sorted) -> value; zero entries dropped."""
+    out = []
+    for key, value in counter.values().items():
+        if not value:
+            continue
+        h = ",".join(f"{n}:{v}" for n, v in sorted(zip(label_names, key)))
+        out.append([h, value])
+    return sorted(out)
+
+
+def run_python(sc: dict, impl: str = "python", mutate=None) -> dict:
+    """This repo's handlers (``impl`` = python | native) over the same scenario."""
+    import helpers
+    from beholder_amd.handlers import native_handlers
+    from beholder_amd.models.proto import DecodeError
+
+    config = Config.from_dict(sc["config"], env={})
+    http = RecordingHttpClient()
+    for f in sc["faults"]:
+        http.fail(f["method"], f["prefix"], status=f["status"], message=f["message"],
+                  body=f["body"].encode())
+    rows = [Media(id=m["id"], name=m["name"], creator=m["creator"], creatorId=m["creatorId"],
+                  metadataId=m["metadataId"], status=m["status"]) for m in sc["media"]]
+    rig = helpers.Rig(config=config, medias=rows, no_trello=bool(sc.get("noTrello")), http=http,
+                      positional_args=sc["positionalArgs"])
+    if mutate is not None:
+        mutate(rig.h)
+    target = rig.h if impl == "python" else native_handlers(rig.h)
+    assert target is not None
+    dec = {"status": rig.h.decode_status, "progress": rig.h.decode_progress}
+    events = []
+
+    async def go():
+        for topic, hexbody in sc["events"]:
+            body = bytes.fromhex(hexbody)
+            try:
+                dec[topic](body)
+                decode_error = False
+            except DecodeError:
+                decode_error = True
+            n_http = len(http.calls)
+            n_log = len(rig.stream.lines)
+            d = rig.delivery(1 if topic == "status" else 2, body)
+            threw = None
+            try:
+                await (target.on_status(d) if topic == "status" else target.on_progress(d))
+            except Exception as e:  # noqa: BLE001 - Q1: status errors escape
+                threw = str(e)
+            rig.log.flush()
+            logs = [[x["level"], x["msg"]] for x in map(json.loads, rig.stream.lines[n_log:])]
+            events.append({"acks": 1 if d.state == "acked" else 0, "threw": threw, "decodeError": decode_error,
+                           "requests": [list(c) for c in list(http.calls)[n_http:]], "logs": logs})
+
+    asyncio.run(go())
+    counters = {
+        "beholder_progress_updates_total": _counter_hashes(rig.progress, ["status"]),
+        "beholder_trello_comments": _counter_hashes(rig.comments, []),
+    }
+    snap = rig.h.store.snapshot()
+    return {"events": events, "counters": counters, "media": {k: v.status for k, v in snap.items()}}
+
+
+def diff(ref: dict, got: dict, limit: int = 8) -> List[str]:
+    """Human-readable differences (empty = identical)."""
+    out: List[str] = []
+    if len(ref["events"]) != len(got["events"]):
+        return [f"event count {len(ref['events'])} != {len(got['events'])}"]
+    for i, (a, b) in enumerate(zip(ref["events"], got["events"])):
+        for k in ("acks", "threw", "decodeError", "requests", "logs"):
+            if a[k] != b[k]:
+                out.append(f"event {i} {k}: reference={a[k]!r} ours={b[k]!r}")
+                if len(out) >= limit:
+                    return out
+    ref_counters = {k: [e for e in v if e[1]] for k, v in ref["counters"].items()}
+    if ref_counters != got["counters"]:
+        out.append(f"counters: reference={ref_counters} ours={got['counters']}")
+    if ref["media"] != got["media"]:
+        out.append(f"media: reference={ref['media']} ours={got['media']}")
+    return out
+
+
+def check(seed: int, mode: str, n_events: int = 520, impls=("python", "native")) -> Dict[str, List[str]]:
+    sc = make_scenario(seed, n_events, mode)
+    ref = run_node(sc)
+    return {impl: diff(ref, run_python(sc, impl)) for impl in impls}
+
+
+def coverage(ref: dict) -> dict:
+    """Which reference branches a run reached (from its own trace)."""
+    msgs = [m for e in ref["events"] for _, m in e["logs"]]
+    reqs = [r for e in ref["events"] for r in e["requests"]]
+    return {
+        "threw": sum(1 for e in ref["events"] if e["threw"] is not None),
+        "decode_errors": sum(1 for e in ref["events"] if e["decodeError"]),
+        "unacked": sum(1 for e in ref["events"] if e["acks"] == 0),
+        "card_moves": sum(1 for m, _ in reqs if m == "PUT"),
+        "comments": sum(1 for m, _ in reqs if m == "POST"),
+        "telegram": sum(1 for _, u in reqs if "api.telegram.org" in u),
+        "emby": sum(1 for _, u in reqs if "/emby/library/refresh" in u),
+        "missing_list_warns": sum(1 for m in msgs if m.startswith("unable to find list")),
+        "hook_warns": sum(1 for m in msgs if m.startswith("failed to run deployed hooks")),
+        "progress_warns": sum(1 for m in msgs if m.startswith("failed to update media progress")),
+    }
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    import argparse
+    ap = argparse.ArgumentParser(description="reference-executed parity gate")
+    ap.add_argument("--seeds", type=int, default=5)
+    ap.add_argument("--events", type=int, default=520)
+    ap.add_argument("--modes", default=",".join(MODES))
+    a = ap.parse_args(argv)
+    bad = 0
+    for seed in range(a.seeds):
+        for mode in a.modes.split(","):
+            sc = make_scenario(seed, a.events, mode)
+            ref = run_node(sc)
+            for impl in ("python", "native"):
+                d = diff(ref, run_python(sc, impl))
+                bad += bool(d)
+                print(f"seed {seed} {mode:9s} {impl:6s} {'OK' if not d else 'DIFF'} {coverage(ref) if not d else ''}")
+                for line in d:
+                    print("   ", line)
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

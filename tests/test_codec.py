@@ -190,3 +190,54 @@ def test_varint_edge_cases_agree_with_upb(data):
     except DecodeError:
         got = None
     assert got == want
+
+
+# protobufjs 6.8.8 dialect (ops/csrc/pbjs.hpp): what the reference's reader does with malformed input.
+# Each vector is worked by hand from protobufjs's reader.js / reader_buffer.js; the node oracle
+# (tests/test_reference_oracle.py) checks the same reader against a JS re-implementation.
+PBJS_VECTORS = [
+    (b"\x0a\x03abc\x10\x04\x18\x05", ("abc", 4, 5, "")),
+    (b"\x80", "index out of range: 1 + 10 > 1"),             # uint32 reads past the end, then +5
+    (b"\x0a\x05ab", ("ab", 0, 0, "")),                       # BufferReader.string clamps
+    (b"\x0c", "index out of range: 1 + 10 > 1"),             # known field: no wire-type check
+    (b"\x11ab", "index out of range: 3 + 10 > 3"),           # status read as varint, 'b' is a tag
+    (b"\x1d\x01", ("", 0, 1, "")),                           # progress (int32) despite wire type 5
+    (b"\x0a\x03\xff\xfeA", ("��A", 0, 0, "")),     # no UTF-8 validation
+    (b"\x10\xff\xff\xff\xff\xff\x00\x00\x00\x00\x00", ("", -1, 0, "")),
+    (b"\x10\xff\xff\xff\xff\xff\x00\x00", "index out of range: 8 + 10 > 8"),
+    (b"\x00\x00\x18\x02", ("", 0, 2, "")),                   # field 0 skipped like any unknown field
+    (b"\x2c", "invalid wire type 4 at offset 1"),            # stray end group
+    (b"\x2e", "invalid wire type 6 at offset 1"),
+    (b"\x2b\x33\x08\x01\x34\x3c\x18\x09", ("", 0, 9, "")),  # nested groups end on any end-group tag
+    (b"\x2b\x33\x08\x01\x34", "index out of range: 5 + 10 > 5"),
+    (b"\x29\x01\x02", "index out of range: 1 + 8 > 3"),      # unknown fixed64: skip(8)
+    (b"\x2a\x05ab", "index out of range: 2 + 5 > 4"),        # unknown bytes: skip(n)
+    (b"\x28\x80", "index out of range: 2 + 1 > 2"),          # unknown varint: skip()
+]
+
+
+@pytest.mark.parametrize("data,want", PBJS_VECTORS)
+def test_protobufjs_dialect_vectors(data, want):
+    c = codec_for(PROGRESS, "protobufjs")
+    assert c.dialect == "protobufjs"
+    if isinstance(want, str):
+        with pytest.raises(DecodeError) as ei:
+            c.decode(data)
+        assert str(ei.value) == want
+    else:
+        assert tuple(c.decode(data)) == want
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.text(max_size=40), st.integers(-2**31, 2**31 - 1), st.integers(-2**31, 2**31 - 1), st.text(max_size=20))
+def test_protobufjs_dialect_agrees_with_upb_on_valid_input(mid, status, progress, host):
+    data = codec_for(PROGRESS).encode((mid, status, progress, host))
+    assert tuple(codec_for(PROGRESS, "protobufjs").decode(data)) == tuple(codec_for(PROGRESS).decode(data))
+
+
+def test_handlers_decode_with_the_configured_dialect():
+    import helpers
+    r = helpers.Rig()
+    assert r.h.decode_status.__self__.dialect == "protobufjs"
+    r2 = helpers.Rig(config=helpers.cfg({"service": {"proto": {"dialect": "upb"}}}))
+    assert r2.h.decode_status.__self__.dialect == "upb"

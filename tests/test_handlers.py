@@ -160,9 +160,10 @@ def test_status_not_deployed_no_hooks():
     assert r.calls() == []
 
 
-@pytest.mark.parametrize("body", [b"\x0a\x05ab", b"\xff\xff\xff"])
+@pytest.mark.parametrize("body", [b"\x0a\x02ab\x29", b"\xff\xff\xff"])
 def test_status_decode_error_leaves_unacked(body):
-    """Q1 (index.js:63): no try/catch — a decode failure escapes; message never acked."""
+    """Q1 (index.js:63): no try/catch — a decode failure escapes; message never acked.
+    (protobufjs clamps a string that runs past the end, so ``0a 05 "ab"`` alone would decode.)"""
     r = Rig()
     d, exc = r.status(body)
     assert exc is not None and d.state == "pending"
@@ -243,7 +244,7 @@ def test_progress_counter_increments_before_db_read():
     d = r.progress_(progress_msg("missing", "QUEUED", 1))
     assert d.acked
     assert r.progress.get({"status": "queued"}) == 1
-    assert r.msgs(40) == ["failed to update media progress media 'missing' not found"]
+    assert r.msgs(40) == ["failed to update media progress media missing not found"]
 
 
 def test_progress_unknown_enum_warns_acks_no_count():

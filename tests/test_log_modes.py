@@ -73,7 +73,7 @@ SITES = [
      f"processing progress update on media m1 status {CONV} percent 45"),
     (51, _progress_comment, 30, "creating comment on", "creating comment on CARD1 with text: CONVERTING: Progress **45%** (_w3_)"),
     (150, _progress_fail, 40, "failed to update media progress",
-     "failed to update media progress media 'missing' not found"),
+     "failed to update media progress media missing not found"),
 ]
 
 

@@ -1,0 +1,59 @@
+"""The reference's own business logic (``/root/reference/index.js:50-155``, run on Node) against
+both handler implementations, event by event (``tests/reference_oracle.py`` has the details).
+
+Compared per event: ack count, the status listener's rejection text (Q1), whether decode threw,
+every sink request (method + full URL), every log line (level + message). At the end: counter
+values and the media table's statuses. Modes: plain, ``NO_TRELLO`` (Q2), sink faults (Q4) and
+pino@5's ``positional_args: drop`` (Q11). Skipped without ``node`` or the reference checkout.
+"""
+import pytest
+
+import reference_oracle as ro
+
+pytestmark = pytest.mark.skipif(not ro.available(), reason="needs node and /root/reference/index.js")
+
+SEEDS = range(5)
+EVENTS = 520
+
+
+@pytest.mark.parametrize("mode", ro.MODES)
+def test_reference_parity(mode):
+    failures = {}
+    for seed in SEEDS:
+        sc = ro.make_scenario(seed, EVENTS, mode)
+        ref = ro.run_node(sc)
+        assert len(ref["events"]) == EVENTS
+        for impl in ("python", "native"):
+            d = ro.diff(ref, ro.run_python(sc, impl))
+            if d:
+                failures[(seed, impl)] = d
+    assert not failures, "\n".join(f"{k}: " + "\n  ".join(v) for k, v in failures.items())
+
+
+def test_streams_reach_every_reference_branch():
+    """The gate is only as good as its streams: every branch of index.js:50-155 is reached."""
+    total = {}
+    for mode in ro.MODES:
+        for seed in SEEDS:
+            cov = ro.coverage(ro.run_node(ro.make_scenario(seed, EVENTS, mode)))
+            for k, v in cov.items():
+                total[k] = total.get(k, 0) + v
+    assert all(v > 0 for v in total.values()), total
+
+
+# one-line mutations of the business logic, applied to the handler object both implementations read
+MUTATIONS = {
+    "deployed_enum": lambda h: setattr(h, "deployed", 3),             # index.js:94 compares DEPLOYED
+    "trello_creator": lambda h: setattr(h, "trello_creator", 0),      # index.js:142
+    "flow_lists": lambda h: setattr(h, "lists", dict(h.lists, converting="L-other")),  # index.js:80
+    "no_trello": lambda h: setattr(h, "no_trello", True),             # index.js:70
+}
+
+
+@pytest.mark.parametrize("impl", ["python", "native"])
+@pytest.mark.parametrize("name", sorted(MUTATIONS))
+def test_gate_catches_mutations(name, impl):
+    sc = ro.make_scenario(1, EVENTS, "faults" if name == "deployed_enum" else "base")
+    ref = ro.run_node(sc)
+    assert not ro.diff(ref, ro.run_python(sc, impl))
+    assert ro.diff(ref, ro.run_python(sc, impl, mutate=MUTATIONS[name]))
