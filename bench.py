@@ -25,9 +25,16 @@ region):
 
 * ``all_procs_*``: every CPU of the rank's share busy: ``--procs-per-rank`` consumer processes
   (competing consumers) on independent streams. This moves with the host's load.
+* ``rate_1k_*``: BASELINE config 2, 1k events/s paced for 1 s: sustained ingest, p50/p99
+  receive→ack latency.
 * ``rate_10k_*``: BASELINE config 3, 10k events/s paced for 1 s: p50/p99 receive→ack latency.
-* ``soak_*``: BASELINE config 5, 1M events unpaced: RSS growth and GC pauses.
-* ``overload_*``: BASELINE config 4, unpaced into a 4096-event ring with ``drop_newest``.
+* ``rate_100k_*``: BASELINE config 4, 100k events/s paced for 1 s into a 4096-event ring with
+  ``drop_newest``: offered / accepted / dropped (``offered == accepted + dropped``), p99 latency.
+* ``burst_*``: 200k events written unpaced (pipe speed) into the same ring: drop accounting
+  under overload, beyond config 4.
+* ``soak_*``: BASELINE config 5, 1M events unpaced: the service's RSS growth over the run
+  (workload excluded) and GC pauses. ``bench_proc_maxrss_mb`` is the whole bench process's peak:
+  pre-generated workloads and the torch import included.
 * ``tcp_e2e_*`` / ``http_tcp_h1_*``: the production-shaped path, every dependency over TCP (an
   AMQP replay broker, a Postgres fake and HTTP fakes in their own processes).
 * ``tls_e2e_*``: the same with HTTPS sinks, as Trello and Telegram are in production.
@@ -370,23 +377,39 @@ def inproc_extras(a) -> dict:
     from beholder_amd.bench.generator import Workload
     w = Workload(n_media=10000, seed=a.seed)
     out = {}
+    r = asyncio.run(harness._run_inproc(w.events(1000), 1000, media=w.media))  # config 2: 1 s at 1k/s
+    out.update({"rate_1k_acked": r["acked"], "rate_1k_events_per_sec": _r(r["ingest_rate_eps"], 1),
+                "rate_1k_p50_ingest_latency_us": _r(r["ingest_latency_us"].get("p50")),
+                "rate_1k_p99_ingest_latency_us": _r(r["ingest_latency_us"].get("p99"))})
     r = asyncio.run(harness._run_inproc(w.events(10000), 10000, media=w.media))
     out.update({"rate_10k_acked": r["acked"],
                 "rate_10k_p50_ingest_latency_us": _r(r["ingest_latency_us"].get("p50")),
                 "rate_10k_p99_ingest_latency_us": _r(r["ingest_latency_us"].get("p99"))})
+    # config 4: 1 s paced at 100k/s into the small ring, drop_newest (backpressure + drop accounting)
+    r = asyncio.run(harness._run_inproc(w.events(100_000), 100_000, policy="drop_newest", capacity_events=4096,
+                                        media=w.media))
+    out.update({"rate_100k_offered": r["offered"], "rate_100k_accepted": r["accepted"],
+                "rate_100k_dropped": r["dropped"], "rate_100k_acked": r["acked"],
+                "rate_100k_offered_per_sec": _r(r["offered_rate_eps"], 1),
+                "rate_100k_p50_ingest_latency_us": _r(r["ingest_latency_us"].get("p50")),
+                "rate_100k_p99_ingest_latency_us": _r(r["ingest_latency_us"].get("p99"))})
     r = asyncio.run(harness._run_inproc(w.events(200_000), 0, policy="drop_newest", capacity_events=4096,
                                         media=w.media))
-    out.update({"overload_offered": r["offered"], "overload_accepted": r["accepted"],
-                "overload_dropped": r["dropped"]})
+    out.update({"burst_offered": r["offered"], "burst_accepted": r["accepted"],
+                "burst_dropped": r["dropped"]})
     evs = w.events(a.soak_events)
     probe: list = []
     g = harness.GcPauses()
     r = asyncio.run(harness._run_inproc(evs, 0, media=w.media, rss_probe=probe, gc_probe=g))
     del evs
     gs = g.summary()
+    curve = r.get("rss_curve_mb") or []
     out.update({"soak_events": r["acked"], "soak_events_per_sec": _r(r["ingest_rate_eps"], 1),
+                # the service's RSS growth over the run (from after init, with the 1M-event workload
+                # already in memory): at the end, and at the highest 0.5 s sample
                 "soak_rss_growth_mb": _r(probe[1] - probe[0], 2),
-                "soak_rss_peak_mb": _r(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024, 1),
+                "soak_rss_peak_growth_mb": _r(max(curve + [probe[1]]) - probe[0], 2),
+                "bench_proc_maxrss_mb": _r(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024, 1),
                 "soak_gc_pauses": gs.get("count", 0), "soak_gc_max_pause_us": _r(gs.get("max_us")),
                 "soak_gc_p99_pause_us": _r(gs.get("p99_us"))})
     return out
@@ -468,7 +491,11 @@ def main(argv=None) -> int:
             **extras,
             "notes": "CPU event-consumer workload (the reference has no device compute; see docs/DESIGN.md). "
                      "value = one consumer process per rank; all_procs_* = every CPU of the share busy; "
-                     "rate_10k/overload/soak = BASELINE configs 3-5; tcp_e2e/http_tcp = every dependency over TCP, tls_e2e = same with HTTPS sinks",
+                     "rate_1k/rate_10k/rate_100k/soak = BASELINE configs 2-5 (rate_100k paced into a 4096-event "
+                     "drop_newest ring; burst = the same ring fed unpaced); tcp_e2e/http_tcp = every dependency "
+                     "over TCP, tls_e2e = same with HTTPS sinks; tcp_e2e/tls_e2e latencies are receive->ack at "
+                     "saturation with prefetch 100 in flight (queueing included), warmup_* = the first "
+                     "deliveries while sink/DB connections open",
         }
         print(json.dumps(out), flush=True)
     dist.close()

@@ -11,7 +11,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
             "vs_baseline", "dtype", "data", "config"}
 EXTRAS = {"all_procs_events_per_sec", "rate_10k_p50_ingest_latency_us", "rate_10k_p99_ingest_latency_us",
-          "soak_rss_growth_mb", "soak_gc_max_pause_us", "overload_dropped", "tcp_e2e_events_per_sec",
+          "soak_rss_growth_mb", "soak_gc_max_pause_us", "burst_dropped", "tcp_e2e_events_per_sec",
+          "rate_1k_acked", "rate_1k_p50_ingest_latency_us", "rate_1k_p99_ingest_latency_us",
+          "rate_100k_offered", "rate_100k_accepted", "rate_100k_dropped", "rate_100k_p99_ingest_latency_us",
+          "soak_rss_peak_growth_mb", "bench_proc_maxrss_mb",
           "http_tcp_h1_p999_handle_latency_us", "p50_handle_latency_us", "tls_e2e_events_per_sec",
           "tls_e2e_cpu_us_per_event", "cpu_us_per_event", "involuntary_ctx_switches",
           "tcp_e2e_warmup_p999_handle_latency_us", "tls_e2e_warmup_p999_handle_latency_us"}
@@ -42,7 +45,13 @@ def test_bench_single_rank_contract():
     assert out["all_procs_per_rank"] == 2 and out["all_procs_events_per_sec"] > 0
     assert out["rate_10k_acked"] == 10000 and out["soak_events"] == 20000 and out["tcp_e2e_errors"] == 0
     assert out["tls_e2e_errors"] == 0
-    assert out["overload_accepted"] + out["overload_dropped"] == out["overload_offered"]
+    assert out["burst_accepted"] + out["burst_dropped"] == out["burst_offered"]
+    # BASELINE configs 2 and 4 as specified: 1 s at 1k/s, 1 s paced at 100k/s into the 4096 ring
+    assert out["rate_1k_acked"] == 1000
+    assert out["rate_100k_offered"] == 100_000
+    assert out["rate_100k_accepted"] + out["rate_100k_dropped"] == out["rate_100k_offered"]
+    assert out["rate_100k_acked"] == out["rate_100k_accepted"]
+    assert "soak_rss_peak_mb" not in out and "overload_offered" not in out
 
 
 def test_bench_two_ranks_gloo():
