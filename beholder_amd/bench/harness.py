@@ -391,14 +391,16 @@ def _http_tcp(w: Workload, n: int, servers: int = 3, clients=("h1", "aiohttp")) 
     return out
 
 
-def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = False, preconnect: int = 0) -> dict:
+def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = False, preconnect: int = 0,
+             max_connecting: int = 8) -> dict:
     """Production-shaped: every dependency over real TCP. A replay AMQP broker streams n
     events (prefetch 100, index.js:43). Each handler reads / updates the media row in a
     fake Postgres (pipelined ``pgwire``). Every sink call goes to a fake HTTP endpoint
     (keep-alive ``h1`` client). The fakes are separate processes; the numbers describe
     the consumer process. ``tls`` (config ``tls_e2e``): the sinks are HTTPS, as Trello and
     Telegram are in production (certificate verified against the bench's own CA). ``preconnect``:
-    ``service.http.preconnect`` (sink connections opened at init, before the clock)."""
+    ``service.http.preconnect`` (sink connections opened at init, before the clock).
+    ``max_connecting``: ``service.http.max_connecting`` (connects + handshakes in flight per origin)."""
     from ..config import Config
     from ..service import Service
     from ..sinks import H1Client
@@ -409,7 +411,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
     warm = min(5000, n // 10)
     bport, bprocs = _spawn("beholder_amd.bench.replay_broker", 1, ("--events", str(n)))
     procs = list(bprocs)
-    out: dict = {"events": n, "prefetch": 100, "preconnect": preconnect}
+    out: dict = {"events": n, "prefetch": 100, "preconnect": preconnect, "max_connecting": max_connecting}
     try:
         hport, hp = _spawn("beholder_amd.bench.http_sink_server", http_servers, ("--tls",) if tls else ())
         procs += hp
@@ -428,9 +430,9 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             store = PostgresStore(f"postgres://beholder@127.0.0.1:{pport}/media", pool_size=4)
             if tls:
                 from .http_sink_server import TLS_CERT
-                http = H1Client(timeout_s=30, ssl_cafile=TLS_CERT)
+                http = H1Client(timeout_s=30, ssl_cafile=TLS_CERT, max_connecting=max_connecting)
             else:
-                http = H1Client(timeout_s=30)
+                http = H1Client(timeout_s=30, max_connecting=max_connecting)
             svc = Service(Config.from_dict(cfgd), source=src, store=store, http=http, logger=Logger(stream=sink),
                           serve_metrics=False)
             await svc.init()

@@ -60,8 +60,10 @@ SERVICE_DEFAULTS: dict = {
         "log": {"level": "info", "name": "index.js", "positional_args": "append"},
         # outbound sink HTTP: `h1` = native-parsed keep-alive client (sinks/h1.py), `aiohttp` = library client
         # preconnect: connections opened per sink origin at startup (0 = on demand, as the reference)
+        # max_connecting: connects + TLS handshakes in progress per origin; requests beyond it queue for
+        # the first keep-alive connection that frees up or the next connect slot (h1 client)
         "http": {"timeout_s": 30.0, "client": "h1", "max_per_host": 100, "keepalive_s": 4.0, "preconnect": 0,
-                 "preconnect_wait_s": 5.0},
+                 "preconnect_wait_s": 5.0, "max_connecting": 8},
         # SURVEY §5 race detection: opt-in per-mediaId serialisation (default off = parity, Q9).
         "ordering": "none",
         # Q1: what to do with a status message whose handler threw.
@@ -304,6 +306,9 @@ class Config:
             pc = 0
         if isinstance(pc, bool) or not isinstance(pc, int) or pc < 0:
             raise ConfigError(f"service.http.preconnect must be an integer >= 0, got {pc!r}")
+        mc = svc["http"].get("max_connecting", 8)
+        if isinstance(mc, bool) or not isinstance(mc, int) or mc < 1:
+            raise ConfigError(f"service.http.max_connecting must be an integer >= 1, got {mc!r}")
         pw = svc["http"].get("preconnect_wait_s", 5.0)
         if isinstance(pw, bool) or not isinstance(pw, (int, float)) or pw < 0:
             raise ConfigError(f"service.http.preconnect_wait_s must be a number >= 0, got {pw!r}")

@@ -93,7 +93,8 @@ def make_http_client(http_cfg) -> HttpClient:
     if http_cfg.get("client", "h1") == "aiohttp":
         return AiohttpClient(timeout_s=timeout)
     return H1Client(timeout_s=timeout, max_per_host=int(http_cfg.get("max_per_host", 100)),
-                    keepalive_s=float(http_cfg.get("keepalive_s", 4.0)), ssl_cafile=http_cfg.get("ca_file") or None)
+                    keepalive_s=float(http_cfg.get("keepalive_s", 4.0)), ssl_cafile=http_cfg.get("ca_file") or None,
+                    max_connecting=int(http_cfg.get("max_connecting", 8)))
 
 
 class Service:

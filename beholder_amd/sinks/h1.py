@@ -19,6 +19,12 @@ Additions over the reference:
 
 * keep-alive pooling: at most ``max_per_host`` connections per origin, and
   idle connections expire after ``keepalive_s``;
+* connect admission: at most ``max_connecting`` connects (TCP + TLS handshake) in
+  progress per origin. A request that finds no idle connection and no free connect
+  slot queues, and takes whichever comes first: a keep-alive connection released by
+  another request, or a connect slot. A burst of first requests after start (prefetch
+  100 deliveries at once) therefore shares a few fresh connections instead of running
+  ~100 handshakes at once, which made every one of them slow (the warm-up tail);
 * one transparent retry on a fresh connection when a *reused* idle connection
   dies before any response byte arrives. This applies to idempotent methods only,
   so a POST (a Trello comment) is never sent twice;
@@ -168,7 +174,7 @@ class _Conn(asyncio.Protocol):
 
 
 class _Origin:
-    __slots__ = ("scheme", "host", "port", "tls", "host_header", "auth", "idle", "open", "waiters")
+    __slots__ = ("scheme", "host", "port", "tls", "host_header", "auth", "idle", "open", "waiters", "connecting")
 
     def __init__(self, scheme: str, host: str, port: int, host_header: str, auth: Optional[str]):
         self.scheme = scheme
@@ -179,7 +185,13 @@ class _Origin:
         self.auth = auth
         self.idle: Deque[_Conn] = collections.deque()
         self.open = 0
+        self.connecting = 0  # connects (and TLS handshakes) in progress
         self.waiters: Deque[asyncio.Future] = collections.deque()
+
+
+def _queued(o: _Origin) -> bool:
+    """More requests of ``o`` wait for a connection than connects are in progress for them."""
+    return sum(1 for w in o.waiters if not w.done()) > o.connecting
 
 
 def _split_url(url: str) -> Tuple[str, str]:
@@ -209,10 +221,11 @@ class H1Client(HttpClient):
 
     def __init__(self, timeout_s: float = 30.0, user_agent: str = "beholder/1.0", max_per_host: int = 100,
                  keepalive_s: float = 4.0, ssl_context: Optional[_ssl.SSLContext] = None,
-                 max_redirects: int = 10, ssl_cafile: Optional[str] = None):
+                 max_redirects: int = 10, ssl_cafile: Optional[str] = None, max_connecting: int = 8):
         self.timeout_s = float(timeout_s)
         self.user_agent = user_agent
         self.max_per_host = max(1, int(max_per_host))
+        self.max_connecting = max(1, int(max_connecting))
         self.keepalive_s = float(keepalive_s)
         self.max_redirects = int(max_redirects)
         self._own_ssl = ssl_context is None  # our own context: the native TLS path can mirror it
@@ -226,10 +239,12 @@ class H1Client(HttpClient):
         self._routes: Dict[str, Tuple[_Origin, str, str]] = {}
         self._closed = False
         self._busy: set = set()
+        self._dials: set = set()  # background connects for queued requests (_grow)
         self._sweeper = None
         self._tail = f"User-Agent: {user_agent}\r\n\r\n".encode("latin-1")
         self._tail_cl0 = f"User-Agent: {user_agent}\r\nContent-Length: 0\r\n\r\n".encode("latin-1")
-        self.counts = {"requests": 0, "connections": 0, "reused": 0, "retries": 0, "errors": 0, "timeouts": 0}
+        self.counts = {"requests": 0, "connections": 0, "reused": 0, "retries": 0, "errors": 0, "timeouts": 0,
+                       "connecting_peak": 0, "connect_waits": 0}
 
     # -- pool ----------------------------------------------------------------
     def _origin(self, key: str) -> _Origin:
@@ -281,10 +296,26 @@ class H1Client(HttpClient):
             self._ssl = _ssl.create_default_context()
         return self._ssl
 
+    def _reserve(self, o: _Origin) -> None:
+        """Count a connect about to start against the pool (``open``) and admission (``connecting``)."""
+        o.open += 1
+        o.connecting += 1
+        if o.connecting > self.counts["connecting_peak"]:
+            self.counts["connecting_peak"] = o.connecting
+
     async def _connect(self, o: _Origin, deadline: float, infos=None) -> _Conn:
+        """A connection for the caller itself (preconnect, the retry of a dead reused connection)."""
+        self._reserve(o)
+        try:
+            return await self._dial(o, deadline, infos)
+        except BaseException:
+            self._wake(o)
+            raise
+
+    async def _dial(self, o: _Origin, deadline: float, infos=None) -> _Conn:
+        """Connect (+ TLS) on a slot :meth:`_reserve` counted; frees the slot either way."""
         loop = asyncio.get_running_loop()
         conn = _Conn(o)
-        o.open += 1
         try:
             remaining = deadline - loop.time()
             if remaining <= 0:
@@ -298,10 +329,45 @@ class H1Client(HttpClient):
         except BaseException:
             conn.abort()
             o.open -= 1
-            self._wake(o)
+            o.connecting -= 1
             raise
+        o.connecting -= 1
         self.counts["connections"] += 1
         return conn
+
+    def _grow(self, o: _Origin, deadline: float) -> None:
+        """Start a background connect for the queued requests of ``o`` if a pool slot and a connect
+        slot are free. The new connection goes to whichever request is first in the queue when it is
+        ready (or to the idle pool); a request never waits on one particular handshake."""
+        if self._closed or o.open >= self.max_per_host or o.connecting >= self.max_connecting:
+            return
+        self._reserve(o)
+        t = asyncio.ensure_future(self._dial_for_queue(o, deadline))
+        self._dials.add(t)
+        t.add_done_callback(self._dials.discard)
+
+    async def _dial_for_queue(self, o: _Origin, deadline: float) -> None:
+        try:
+            c = await self._dial(o, deadline)
+        except asyncio.CancelledError:  # client closing
+            self._wake(o)
+            return
+        except asyncio.TimeoutError:  # the queued requests time out on their own deadlines
+            if _queued(o):
+                self._grow(o, asyncio.get_running_loop().time() + self.timeout_s)
+            return
+        except BaseException as e:  # noqa: BLE001 - the first queued request gets the connect error
+            while o.waiters:
+                w = o.waiters.popleft()
+                if not w.done():
+                    w.set_exception(e)
+                    break
+            if _queued(o):
+                self._grow(o, asyncio.get_running_loop().time() + self.timeout_s)
+            return
+        self._release(c, True)
+        if _queued(o):  # a queue longer than the connects under way: the pool grows (max_connecting at a time)
+            self._grow(o, asyncio.get_running_loop().time() + self.timeout_s)
 
     async def _connect_native(self, conn: _Conn, o: _Origin, ntls, deadline: float, loop, infos=None) -> None:
         """TCP connect, and TLS for ``ntls``, in C (``ops netconn_connect``): no asyncio transport
@@ -346,18 +412,31 @@ class H1Client(HttpClient):
         raise OSError("Multiple exceptions: " + ", ".join(str(e) for e in errors))
 
     async def _acquire(self, o: _Origin, deadline: float, fresh: bool = False) -> _Conn:
-        now = time.monotonic()
+        counts = self.counts
         idle = o.idle
-        while idle and not fresh:
-            c = idle.pop()
-            if not c.closed and now - c.last_used < self.keepalive_s:
-                self.counts["reused"] += 1
-                return c
-            self._drop(c)
-        while o.open >= self.max_per_host:
-            w = asyncio.get_running_loop().create_future()
-            o.waiters.append(w)
-            loop = asyncio.get_running_loop()
+        loop = asyncio.get_running_loop()
+        front = False
+        while True:
+            now = time.monotonic()
+            while idle and not fresh:
+                c = idle.pop()
+                if not c.closed and now - c.last_used < self.keepalive_s:
+                    counts["reused"] += 1
+                    return c
+                self._drop(c)
+            if fresh and o.open < self.max_per_host:
+                # the retry of a request whose reused connection died: a connection of its own
+                return await self._connect(o, deadline)
+            # queue: take the first connection released by another request or made by a background
+            # connect (started here when admission allows), whichever is ready first
+            w = loop.create_future()
+            if front:
+                o.waiters.appendleft(w)
+            else:
+                o.waiters.append(w)
+                counts["connect_waits"] += 1
+            if not fresh and _queued(o):
+                self._grow(o, deadline)
             th = loop.call_at(deadline, lambda: w.done() or w.set_exception(asyncio.TimeoutError()))
             try:
                 c = await w
@@ -368,12 +447,15 @@ class H1Client(HttpClient):
                 raise
             finally:
                 th.cancel()
-            if c is not None:
-                if not c.closed and not fresh:
-                    self.counts["reused"] += 1
-                    return c
-                self._drop(c)
-        return await self._connect(o, deadline)
+            if c is None:  # a pool slot was freed: look again, keeping this request's place
+                front = True
+                continue
+            if not c.closed and not (fresh and c.uses):
+                if c.uses:
+                    counts["reused"] += 1
+                return c
+            self._drop(c)  # closed meanwhile, or a used one for a retry that needs a fresh one
+            front = True
 
     async def preconnect(self, url: str, n: int) -> Tuple[int, Optional[BaseException]]:
         """Open up to ``n`` connections to ``url``'s origin at once (never past ``max_per_host``)
@@ -432,7 +514,7 @@ class H1Client(HttpClient):
         while o.waiters:
             w = o.waiters.popleft()
             if not w.done():
-                w.set_result(None)  # a slot is free: the waiter opens its own connection
+                w.set_result(None)  # a slot is free: the waiter opens its own connection (or queues again)
                 return
 
     # -- deadlines -------------------------------------------------------------
@@ -622,6 +704,8 @@ class H1Client(HttpClient):
 
     async def close(self) -> None:
         self._closed = True
+        for t in list(self._dials):
+            t.cancel()
         if self._sweeper is not None:
             self._sweeper.cancel()
             self._sweeper = None

@@ -185,3 +185,13 @@ def test_startup_waits_for_preconnect_at_most_preconnect_wait_s():
     assert any("still connecting after 0.2 s" in m for m in msgs) and "initialized" in msgs
     with pytest.raises(ConfigError, match="preconnect_wait_s"):
         cfg({"service": {"http": {"preconnect_wait_s": -1}}})
+
+
+def test_max_connecting_config_is_validated():
+    assert cfg().data["service"]["http"]["max_connecting"] == 8
+    for bad in (0, -1, "8", True, 1.5):
+        with pytest.raises(ConfigError, match="max_connecting"):
+            cfg({"service": {"http": {"max_connecting": bad}}})
+    from beholder_amd.service import make_http_client
+    assert make_http_client({"max_connecting": 3}).max_connecting == 3
+    assert make_http_client({}).max_connecting == 8

@@ -236,6 +236,7 @@ def test_plain_http_server_and_handshake_timeout():
         c = H1Client(timeout_s=5, ssl_cafile=TLS_CERT)
         with pytest.raises(HttpError, match=r"^ETIMEDOUT: GET https://127\.0\.0\.1:\d+/x$"):
             await c.request("GET", f"https://127.0.0.1:{s.port}/x", timeout=0.3)
+        await asyncio.sleep(0.1)  # the queue's background connect shares the request's deadline
         open_ = sum(o.open for o in c._origins.values())
         await c.close()
         s.server.close()
@@ -401,3 +402,60 @@ def test_garbage_on_an_established_tls_connection():
         return out, st["retries"], st["errors"]
     nat, py = _both(go)
     assert nat == py and nat[0] == [200, 200, "error", 200] and nat[1] == 1 and nat[2] == 1
+
+
+@pytest.mark.parametrize("max_connecting", [1, 8])
+def test_first_burst_admits_at_most_max_connecting_handshakes(max_connecting):
+    """100 concurrent first requests to one HTTPS origin (prefetch 100 deliveries at start):
+    never more than ``max_connecting`` connects + TLS handshakes in flight; queued requests take
+    the first connection that frees up or the next connect slot, and all 100 succeed."""
+    async def go():
+        s = await TlsServer(lambda t: ok()).start()
+        c = H1Client(timeout_s=10, ssl_cafile=TLS_CERT, max_connecting=max_connecting)
+        url = f"https://127.0.0.1:{s.port}/x"
+        inflight = {"now": 0, "peak": 0}
+        real = c._dial
+
+        async def counted(o, deadline, infos=None):
+            inflight["now"] += 1
+            inflight["peak"] = max(inflight["peak"], inflight["now"])
+            try:
+                return await real(o, deadline, infos)
+            finally:
+                inflight["now"] -= 1
+        c._dial = counted
+        rs = await asyncio.gather(*[c.request("GET", url) for _ in range(100)])
+        st = c.stats()
+        await c.close()
+        await s.stop()
+        return rs, st, inflight["peak"], s.connections
+    rs, st, peak, server_conns = run(go())
+    assert all(r.status == 200 for r in rs)
+    assert peak <= max_connecting and st["connecting_peak"] <= max_connecting
+    assert st["connections"] == server_conns < 100 and st["connect_waits"] > 0
+    assert st["reused"] >= 100 - st["connections"]
+
+
+def test_pool_still_grows_past_max_connecting_under_slow_responses():
+    """Admission caps connects in flight, not the pool: with slow responses every request needs
+    its own connection, and the pool grows to serve them (8 at a time)."""
+    async def go():
+        s = await TlsServer(lambda t: ok()).start()
+        real_serve = s._serve
+
+        async def slow_serve(r, w):
+            await asyncio.sleep(0.05)
+            await real_serve(r, w)
+        s.server.close()
+        await s.server.wait_closed()
+        s.server = await asyncio.start_server(slow_serve, "127.0.0.1", s.port, ssl=s.ctx)
+        c = H1Client(timeout_s=10, ssl_cafile=TLS_CERT, max_connecting=4)
+        url = f"https://127.0.0.1:{s.port}/x"
+        rs = await asyncio.gather(*[c.request("GET", url) for _ in range(32)])
+        st = c.stats()
+        await c.close()
+        await s.stop()
+        return rs, st
+    rs, st = run(go())
+    assert all(r.status == 200 for r in rs)
+    assert st["connecting_peak"] <= 4 and st["connections"] > 4
