@@ -43,13 +43,17 @@ def cmd_run(a: argparse.Namespace) -> int:
         if a.metrics_port is not None:
             argv = strip_opt(argv, "--metrics-port")
         try:
-            mcfg = Config.load("events", path=a.config, env=dict(os.environ)).data["service"]["metrics"]
+            scfg = Config.load("events", path=a.config, env=dict(os.environ)).data["service"]
         except ConfigError as e:
             print(f"beholder: config error: {e}", file=sys.stderr)
             return 2
+        mcfg, wcfg = scfg["metrics"], scfg.get("workers") or {}
         port = a.metrics_port if a.metrics_port is not None else (
             int(mcfg.get("port", 3000)) if mcfg.get("enabled", True) else -1)
         return Supervisor(argv, a.workers, metrics_port=port, metrics_host=str(mcfg.get("host", "0.0.0.0")),
+                          max_restarts=int(wcfg.get("max_restarts", 10)),
+                          restart_window_s=float(wcfg.get("restart_window_s", 300.0)),
+                          healthy_s=float(wcfg.get("healthy_s", 60.0)),
                           log=lambda m: print(f"beholder supervisor: {m}", file=sys.stderr)).run()
     env = dict(os.environ)
     try:

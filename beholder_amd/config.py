@@ -64,6 +64,10 @@ SERVICE_DEFAULTS: dict = {
         # the first keep-alive connection that frees up or the next connect slot (h1 client)
         "http": {"timeout_s": 30.0, "client": "h1", "max_per_host": 100, "keepalive_s": 4.0, "preconnect": 0,
                  "preconnect_wait_s": 5.0, "max_connecting": 8},
+        # `run --workers N` supervisor (parallel/workers.py): more than max_restarts crashes of one worker
+        # within restart_window_s is a crash loop (all workers stop, exit 1); a worker that ran healthy_s
+        # starts its backoff over
+        "workers": {"max_restarts": 10, "restart_window_s": 300.0, "healthy_s": 60.0},
         # SURVEY §5 race detection: opt-in per-mediaId serialisation (default off = parity, Q9).
         "ordering": "none",
         # Q1: what to do with a status message whose handler threw.
@@ -306,6 +310,11 @@ class Config:
             pc = 0
         if isinstance(pc, bool) or not isinstance(pc, int) or pc < 0:
             raise ConfigError(f"service.http.preconnect must be an integer >= 0, got {pc!r}")
+        wk = svc.get("workers") or {}
+        for k, lo in (("max_restarts", 0), ("restart_window_s", 1e-9), ("healthy_s", 0)):
+            v = wk.get(k, lo)
+            if isinstance(v, bool) or not isinstance(v, (int, float)) or v < lo:
+                raise ConfigError(f"service.workers.{k} must be a number >= {lo:g}, got {v!r}")
         mc = svc["http"].get("max_connecting", 8)
         if isinstance(mc, bool) or not isinstance(mc, int) or mc < 1:
             raise ConfigError(f"service.http.max_connecting must be an integer >= 1, got {mc!r}")

@@ -116,3 +116,83 @@ def test_workers_merged_metrics_endpoint(tmp_path):
     assert m['beholder_progress_updates_total{status="queued"}'] == 300  # summed over both workers
     assert m['beholder_messages_received{topic="v1.telemetry.progress"}'] == 300
     assert health == 200
+
+
+# A stand-in worker program: worker 0 crashes (exit 3) after CRASH_AFTER_S, every other worker
+# runs until SIGTERM. Each start of worker 0 appends a line to $STARTS.
+FAKE_WORKER = r"""
+import os, signal, sys, time
+wid = os.environ["BEHOLDER_WORKER_ID"]
+with open(os.environ["STARTS"], "a") as f:
+    f.write(f"{wid} {os.getpid()}\n")
+if wid == "0":
+    time.sleep(float(os.environ["CRASH_AFTER_S"]))
+    sys.exit(3)
+signal.signal(signal.SIGTERM, lambda *a: sys.exit(0))
+while True:
+    time.sleep(0.05)
+"""
+
+
+def _supervise(tmp_path, crash_after_s, crashes_wanted, timeout_s, **policy):
+    import threading
+    from beholder_amd.parallel.workers import Supervisor
+    starts = tmp_path / "starts"
+    starts.write_text("")
+    env = dict(os.environ, STARTS=str(starts), CRASH_AFTER_S=str(crash_after_s))
+    logs = []
+    sup = Supervisor([], 2, env=env, log=logs.append, command=[sys.executable, "-c", FAKE_WORKER],
+                     backoff_base_s=0.01, backoff_max_s=0.05, poll_s=0.01, grace_s=5, **policy)
+    t0 = time.monotonic()
+
+    def watch():
+        while time.monotonic() - t0 < timeout_s and not sup._stop:
+            if sup.restarts[0] >= crashes_wanted:
+                break
+            time.sleep(0.01)
+        sup.stop()
+    th = threading.Thread(target=watch, daemon=True)
+    th.start()
+    rc = sup.run()
+    th.join()
+    lines = [x.split() for x in starts.read_text().splitlines()]
+    return rc, sup, lines, logs
+
+
+def test_spaced_crashes_never_stop_the_supervisor(tmp_path):
+    """12 crashes, each after the worker ran longer than the window: no crash loop; the other
+    worker keeps running the whole time (one process, never restarted); stop exits 0."""
+    rc, sup, lines, logs = _supervise(tmp_path, crash_after_s=0.25, crashes_wanted=12, timeout_s=60,
+                                      max_restarts=3, restart_window_s=0.2, healthy_s=10.0)
+    assert sup.restarts[0] >= 12 and sup.restarts[1] == 0
+    assert len({pid for wid, pid in lines if wid == "1"}) == 1
+    assert rc == 0, logs
+    assert not any("crash loop" in m for m in logs)
+
+
+def test_backoff_starts_over_after_a_healthy_run():
+    from beholder_amd.parallel.workers import RestartPolicy
+    p = RestartPolicy(max_restarts=5, restart_window_s=100.0, healthy_s=10.0, backoff_base_s=1.0, backoff_max_s=30.0)
+    assert [p.on_crash(0, started_at=t, now=t + 1) for t in (0, 2, 4)] == [1.0, 2.0, 4.0]
+    assert p.on_crash(0, started_at=10, now=25) == 1.0  # ran 15 s > healthy_s: back to the base delay
+    assert p.recent(0) == 1 and p.total[0] == 4
+
+
+def test_crash_loop_stops_everything_with_exit_1(tmp_path):
+    """A worker that dies at once, over and over: more than max_restarts crashes within the
+    window stops the supervisor, SIGTERMs the healthy worker and exits 1."""
+    rc, sup, lines, logs = _supervise(tmp_path, crash_after_s=0.0, crashes_wanted=100, timeout_s=30,
+                                      max_restarts=3, restart_window_s=30.0, healthy_s=10.0)
+    assert rc == 1
+    assert sup.restarts[0] == 4 and any("crash loop" in m for m in logs)
+    assert sup.procs == {} or all(p.poll() is not None for p in sup.procs.values())
+
+
+def test_workers_config_is_validated():
+    import pytest
+    from beholder_amd.config import ConfigError
+    from helpers import cfg
+    assert cfg().data["service"]["workers"]["max_restarts"] == 10
+    for k, bad in (("max_restarts", -1), ("restart_window_s", 0), ("healthy_s", "x")):
+        with pytest.raises(ConfigError, match=f"service.workers.{k}"):
+            cfg({"service": {"workers": {k: bad}}})
