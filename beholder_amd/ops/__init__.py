@@ -66,7 +66,7 @@ PgReader = native.PgReader
 Driver = native.Driver
 Window = native.Window
 IOFuture = native.IOFuture
-if os.environ.get("BEHOLDER_IOFUTURE", "1") == "0":  # A/B switch: plain asyncio futures for I/O replies
+if os.environ.get("BEHOLDER_NATIVE_IO", "1") == "0":  # all native I/O off: plain asyncio futures for replies
     import asyncio as _asyncio
 
     class IOFuture(_asyncio.Future):  # type: ignore[no-redef]

@@ -1009,8 +1009,8 @@ PyObject *g_done_name, *g_set_result_name, *g_set_exception_name;
 #define s_set_result_name interned(&g_set_result_name, "set_result")
 #define s_set_exception_name interned(&g_set_exception_name, "set_exception")
 
-// The helpers below also accept a foreign future (an asyncio.Future: the BEHOLDER_IOFUTURE=0
-// A/B switch hands those to a NetConn as reply waiters); it goes through its Python methods.
+// The helpers below also accept a foreign future (an asyncio.Future, e.g. a caller's own reply
+// waiter); it goes through its Python methods.
 bool iofuture_done(PyObject* f) {
   if (Py_TYPE(f) == &IOFutureType) return reinterpret_cast<IOFutureObject*>(f)->state != 0;
   PyObject* r = PyObject_CallMethodNoArgs(f, s_done_name);

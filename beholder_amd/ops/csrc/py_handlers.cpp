@@ -48,7 +48,7 @@ PyObject *s_ack, *s_message, *s_content, *s_mediaId, *s_status, *s_progress, *s_
     *s_record, *s_raise_for_status, *s_rows, *s_get_calls, *s_update_calls, *s_limiter, *s_retry,
     *s_hooks_plan, *s_telegram, *s_emby, *s_name, *s_metadataId, *s_GET,
     *s_api_key, *s_send_message, *s_refresh_library, *s_pool, *s_select, *s_update,
-    *s_execute, *s_conns, *s_spread_at, *s_size, *s_h1_fast_name, *kw_params_timeout, *kw_timeout;
+    *s_execute, *s_conns, *s_spread_at, *s_size, *s_native_call, *s_native_pick, *kw_params_timeout, *kw_timeout;
 
 // Reference-visible text: read from beholder_amd/texts.py TEXTS when a NativeHandlers is built
 // (the same table handlers.py and the sink clients read; no such string is spelled here).
@@ -132,9 +132,9 @@ struct HandlersObject {
   PyObject* emby_cls;       // sinks.emby.EmbyClient (exact type: request built here)
   PyObject* memory_cls;     // store.memory.MemoryStore (exact type: row read here)
   PyObject* pg_cls;         // store.postgres.PostgresStore (exact type: queries issued here)
-  PyObject* pool_cls;       // store.pgwire.Pool when its native pick is on (connection picked here), else NULL
-  PyObject* h1_globals;     // sinks/h1.py module dict: `_h1_fast` is read per request (tests switch it)
-  PyObject* h1_fast_fn;     // ops._native.h1_fast: H1Client.request's native path, called directly
+  PyObject* pool_cls;       // store.pgwire.Pool: its `native_pick` capability is used here when set
+  PyObject* h1_fast_fn;     // ops._native.h1_fast: an H1Client's `native_call` capability, called directly
+  PyObject* pick_fn;        // ops._native.pg_pool_execute: a Pool's `native_pick` capability
   PyObject* row_to_media;   // store.postgres.row_to_media (rows that are not all-int / NULL-free)
   PyObject* not_found;      // store.base.MediaNotFound
   PyObject* one;            // TRELLO_CREATOR (index.js:79)
@@ -338,11 +338,14 @@ int pg_execute(CallObject* c, PyObject* store, PyObject* sql_name, PyObject* par
   PyObject* sql = pool ? PyDict_GetItemWithError(sd, sql_name) : nullptr;
   if (PyErr_Occurred()) return -1;
   if (!pool || pool == Py_None || !sql) return 2;  // not connected yet: the store connects first
-  if (hs->pool_cls && reinterpret_cast<PyObject*>(Py_TYPE(pool)) == hs->pool_cls) {
-    // Pool.execute's fast path in C: the least-loaded native connection takes the query
-    PyObject** pdp = _PyObject_GetDictPtr(pool);
-    PyObject* pd = pdp ? *pdp : nullptr;
-    PyObject* conns = pd ? PyDict_GetItemWithError(pd, s_conns) : nullptr;
+  PyObject** pdp = reinterpret_cast<PyObject*>(Py_TYPE(pool)) == hs->pool_cls ? _PyObject_GetDictPtr(pool) : nullptr;
+  PyObject* pd = pdp ? *pdp : nullptr;
+  PyObject* pick = pd ? PyDict_GetItemWithError(pd, s_native_pick) : nullptr;
+  if (PyErr_Occurred()) return -1;
+  if (pick && pick == hs->pick_fn) {
+    // the pool's native_pick capability (Pool.execute's fast path) in C: the least-loaded native
+    // connection takes the query
+    PyObject* conns = PyDict_GetItemWithError(pd, s_conns);
     PyObject* spread = conns ? PyDict_GetItemWithError(pd, s_spread_at) : nullptr;
     PyObject* size = spread ? PyDict_GetItemWithError(pd, s_size) : nullptr;
     if (!size && PyErr_Occurred()) return -1;
@@ -513,11 +516,13 @@ bool record_stats(PyObject* stats, PyObject* status, double seconds) {
   return true;
 }
 
-// http.request(method, url, params=params, timeout=timeout): for a stock H1Client whose native
-// path is on (sinks/h1.py `_h1_fast`), the H1Call is made here without the Python method frame.
+// http.request(method, url, params=params, timeout=timeout): for a stock H1Client whose
+// `native_call` capability is the native request path, the H1Call is made here without the
+// Python method frame.
 PyObject* http_request(HandlersObject* hs, PyObject* http, PyObject* method, PyObject* url, PyObject* params,
                        PyObject* timeout) {
-  PyObject* cur = hs->h1_globals ? PyDict_GetItemWithError(hs->h1_globals, s_h1_fast_name) : nullptr;
+  PyObject** dp = _PyObject_GetDictPtr(http);
+  PyObject* cur = dp && *dp ? PyDict_GetItemWithError(*dp, s_native_call) : nullptr;
   if (cur && cur == hs->h1_fast_fn) {
     PyObject* call = h1_call_new(http, method, url, params ? params : Py_None, timeout);
     if (call != Py_None) return call;  // an H1Call, or NULL with an exception
@@ -1431,7 +1436,7 @@ int hs_traverse(HandlersObject* hs, visitproc visit, void* arg) {
   Py_VISIT(hs->memory_cls);
   Py_VISIT(hs->pg_cls);
   Py_VISIT(hs->pool_cls);
-  Py_VISIT(hs->h1_globals);
+  Py_VISIT(hs->pick_fn);
   Py_VISIT(hs->h1_fast_fn);
   Py_VISIT(hs->row_to_media);
   Py_VISIT(hs->not_found);
@@ -1465,7 +1470,7 @@ int hs_clear(HandlersObject* hs) {
   Py_CLEAR(hs->memory_cls);
   Py_CLEAR(hs->pg_cls);
   Py_CLEAR(hs->pool_cls);
-  Py_CLEAR(hs->h1_globals);
+  Py_CLEAR(hs->pick_fn);
   Py_CLEAR(hs->h1_fast_fn);
   Py_CLEAR(hs->row_to_media);
   Py_CLEAR(hs->not_found);
@@ -1643,31 +1648,12 @@ int hs_init(HandlersObject* hs, PyObject* args, PyObject* kwds) {
   hs->pg_cls = hs->not_found ? import_attr("beholder_amd.store.postgres", "PostgresStore") : nullptr;
   hs->row_to_media = hs->pg_cls ? import_attr("beholder_amd.store.postgres", "row_to_media") : nullptr;
   if (!hs->row_to_media) return -1;
-  {  // Pool.execute's native pick, called directly (unless BEHOLDER_NATIVE_POOL=0 switched it off)
-    PyObject* pick = import_attr("beholder_amd.store.pgwire", "_pg_pool_execute");
-    PyObject* native_pick = pick ? import_attr("beholder_amd.ops._native", "pg_pool_execute") : nullptr;
-    if (!native_pick) {
-      Py_XDECREF(pick);
-      return -1;
-    }
-    if (pick == native_pick && !(hs->pool_cls = import_attr("beholder_amd.store.pgwire", "Pool"))) {
-      Py_DECREF(pick);
-      Py_DECREF(native_pick);
-      return -1;
-    }
-    Py_DECREF(pick);
-    Py_DECREF(native_pick);
-  }
-  {  // H1Client.request's native path, called directly while sinks/h1.py has it switched on
-    PyObject* mod = PyImport_ImportModule("beholder_amd.sinks.h1");
-    if (!mod) return -1;
-    PyObject* d = PyModule_GetDict(mod);
-    Py_XINCREF(d);
-    Py_DECREF(mod);
-    hs->h1_globals = d;
-    hs->h1_fast_fn = d ? import_attr("beholder_amd.ops._native", "h1_fast") : nullptr;
-    if (!hs->h1_fast_fn) return -1;
-  }
+  // the capabilities a Pool (`native_pick`) and an H1Client (`native_call`) hand out are compared
+  // with these when a request is issued: the native paths are called directly
+  hs->pool_cls = import_attr("beholder_amd.store.pgwire", "Pool");
+  hs->pick_fn = hs->pool_cls ? import_attr("beholder_amd.ops._native", "pg_pool_execute") : nullptr;
+  hs->h1_fast_fn = hs->pick_fn ? import_attr("beholder_amd.ops._native", "h1_fast") : nullptr;
+  if (!hs->h1_fast_fn) return -1;
   if (!hs->not_found) return -1;
   static const char* pnames[4] = {"mediaId", "status", "progress", "host"};
   if (!codec_slots(hs->decode_s, pnames, 2, &hs->res_s, hs->ix_s) ||
@@ -1772,7 +1758,7 @@ int init_handler_types(PyObject* m) {
               {&s_conns, "_conns"},
               {&s_spread_at, "spread_at"},
               {&s_size, "size"},
-              {&s_h1_fast_name, "_h1_fast"},
+              {&s_native_call, "native_call"}, {&s_native_pick, "native_pick"},
               {&s_retry, "retry"}};
 
   for (auto& s : strs)

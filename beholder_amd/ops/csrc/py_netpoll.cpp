@@ -10,8 +10,8 @@
 //
 // The poller lives as `loop._beholder_netpoller` while it has sockets and is closed (epoll fd
 // closed, reader removed, attribute dropped) when the last one leaves. Level-triggered: a
-// socket with data left unread is reported again on the next loop iteration. BEHOLDER_NATIVE_POLLER=0
-// keeps every NetConn on its own loop.add_reader registration.
+// socket with data left unread is reported again on the next loop iteration. (NetConns exist only
+// with native I/O on: BEHOLDER_NATIVE_IO=0 keeps every socket on an asyncio transport.)
 #include <sys/epoll.h>
 #include <unistd.h>
 
@@ -177,7 +177,7 @@ PyGetSetDef poller_getset[] = {
 PyObject* mod_netpoll_enabled(PyObject*, PyObject*) { return PyBool_FromLong(g_enabled); }
 
 PyMethodDef poll_functions[] = {
-    {"netpoll_enabled", mod_netpoll_enabled, METH_NOARGS, "NetConns share one epoll set per loop (BEHOLDER_NATIVE_POLLER)"},
+    {"netpoll_enabled", mod_netpoll_enabled, METH_NOARGS, "NetConns share one epoll set per loop (always true)"},
     {nullptr, nullptr, 0, nullptr}};
 
 }  // namespace
@@ -318,8 +318,6 @@ void netpoll_del(PyObject* po, int fd) {
 }
 
 int init_netpoll_types(PyObject* m) {
-  const char* env = getenv("BEHOLDER_NATIVE_POLLER");
-  g_enabled = !(env && strcmp(env, "0") == 0);
   if (!(s_attr = PyUnicode_InternFromString("_beholder_netpoller")) ||
       !(s_add_reader_p = PyUnicode_InternFromString("add_reader")) ||
       !(s_remove_reader_p = PyUnicode_InternFromString("remove_reader")) ||

@@ -31,7 +31,6 @@ from __future__ import annotations
 import array
 import asyncio
 import gc
-import os
 import time
 from typing import Any, Callable, Dict, List, Optional
 
@@ -209,7 +208,7 @@ class Service:
 
         # 8. listeners (index.js:62,127): the compiled handlers unless disabled (same semantics)
         impl = self.handlers
-        if svc.get("native_handlers", True) and os.environ.get("BEHOLDER_NATIVE_HANDLERS", "1") != "0":
+        if svc.get("native_handlers", True):
             impl = native_handlers(self.handlers) or self.handlers
         self.handler_impl = impl
         pc = int(svc["http"].get("preconnect") or 0)
@@ -408,8 +407,7 @@ class Service:
         # native fast path: the per-delivery loop runs in C (ops.dispatch_batch); per-media
         # ordering and debug-line spans keep the Python loop; with Jaeger tracing only the
         # sampled deliveries leave it
-        native = (self.serializer is None and not self.trace
-                  and os.environ.get("BEHOLDER_NATIVE_DISPATCH", "1") != "0")
+        native = self.serializer is None and not self.trace
         tracer = self.tracer
         routes = tuple(routes)
         on_error, on_suspend, on_unroutable = self._on_handler_error, self._inflight, self._unroutable

@@ -39,7 +39,6 @@ import asyncio
 import base64
 import collections
 import ipaddress
-import os
 import socket
 import ssl as _ssl
 import time
@@ -97,7 +96,7 @@ class _Conn(asyncio.Protocol):
         self.deadline = 0.0
         self.what = ("", "")
 
-    # -- protocol callbacks (asyncio transports: BEHOLDER_NATIVE_NET=0, caller-supplied TLS) ------
+    # -- protocol callbacks (asyncio transports: BEHOLDER_NATIVE_IO=0, caller-supplied TLS) ------
     def connection_made(self, transport):
         self.transport = transport
 
@@ -241,6 +240,8 @@ class H1Client(HttpClient):
         self._busy: set = set()
         self._dials: set = set()  # background connects for queued requests (_grow)
         self._sweeper = None
+        # capability for callers in C (the compiled handlers): the native request path when it is on
+        self.native_call = _NATIVE_CALL if netconn.enabled() else None
         self._tail = f"User-Agent: {user_agent}\r\n\r\n".encode("latin-1")
         self._tail_cl0 = f"User-Agent: {user_agent}\r\nContent-Length: 0\r\n\r\n".encode("latin-1")
         self.counts = {"requests": 0, "connections": 0, "reused": 0, "retries": 0, "errors": 0, "timeouts": 0,
@@ -286,7 +287,7 @@ class H1Client(HttpClient):
         t = self._ntls
         if t is None:
             t = False
-            if self._own_ssl and netconn.enabled() and os.environ.get("BEHOLDER_NATIVE_TLS", "1") != "0":
+            if self._own_ssl and netconn.enabled():
                 t = _native.TlsContext(cafile=self.ssl_cafile)
             self._ntls = t
         return t or None
@@ -576,9 +577,11 @@ class H1Client(HttpClient):
         (``ops/csrc/py_h1call.cpp``): like a coroutine it does nothing until awaited; then, on a
         warm pool, it sends the request and completes a plain reply in C, and in every other
         case it delegates to :meth:`_request`."""
-        call = _h1_fast(self, method, url, params, timeout)
-        if call is not None:
-            return call
+        nc = self.native_call
+        if nc is not None:
+            call = nc(self, method, url, params, timeout)
+            if call is not None:
+                return call
         return self._request(method, url, params, timeout)
 
     async def _request(self, method, url, params, timeout) -> HttpResponse:
@@ -754,14 +757,11 @@ def _tls_error(reason: str, message: str, verify: bool) -> _ssl.SSLError:
     return e
 
 
-def _h1_python_only(client, method, url, params, timeout):
-    return None
-
-
-# Native fast path of H1Client.request (ops/csrc/py_h1call.cpp). BEHOLDER_NATIVE_H1=0 keeps every
-# request on the Python path (A/B runs, debugging); so does the plain-asyncio-future A/B switch.
-if os.environ.get("BEHOLDER_NATIVE_H1", "1") != "0" and _IOFuture is _native.IOFuture:
+# Native fast path of H1Client.request (ops/csrc/py_h1call.cpp), handed to each client as its
+# `native_call` capability. With BEHOLDER_NATIVE_IO=0 (replies on plain asyncio futures) every
+# request takes the Python path.
+if _IOFuture is _native.IOFuture:
     _native.h1_setup(H1Client, _Conn, _Origin, HttpResponse)
-    _h1_fast = _native.h1_fast
+    _NATIVE_CALL = _native.h1_fast
 else:
-    _h1_fast = _h1_python_only
+    _NATIVE_CALL = None

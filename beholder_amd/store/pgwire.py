@@ -41,14 +41,6 @@ from ..ops import native as _native
 from ..utils import netconn
 
 
-def _pg_pool_python_only(conns, sql, params, spread_at, size):
-    return None
-
-
-# native pick + execute for a pool of native connections (ops/csrc/py_netconn.cpp); A/B switch
-_pg_pool_execute = (_native.pg_pool_execute if os.environ.get("BEHOLDER_NATIVE_POOL", "1") != "0"
-                    else _pg_pool_python_only)
-
 PROTOCOL_V3 = 196608
 
 
@@ -91,7 +83,7 @@ _NATIVE_TLS: Dict[Tuple[str, Optional[str]], Any] = {}
 def _native_tls_context(mode: str, rootcert: Optional[str]):
     """The native TLS context (ops TlsContext) for an sslmode, as :func:`_ssl_context` sets
     up the ``ssl`` one; None when native connections or native TLS are off."""
-    if not netconn.enabled() or os.environ.get("BEHOLDER_NATIVE_TLS", "1") == "0":
+    if not netconn.enabled():
         return None
     key = (mode, rootcert)
     ctx = _NATIVE_TLS.get(key)
@@ -537,9 +529,6 @@ def _fields(body: bytes) -> Dict[str, str]:
     return out
 
 
-_BACKGROUND_GROW = os.environ.get("BEHOLDER_PG_BACKGROUND_GROW", "1") != "0"
-
-
 class Pool:
     """Up to ``size`` pipelined :class:`PgConnection` s.
 
@@ -567,6 +556,9 @@ class Pool:
         self._closed = False
         self.grows = 0  # connections added by the background grow
         self.grow_errors = 0
+        # capability (also for the compiled handlers): the native least-loaded pick + send over a
+        # pool of native connections (ops/csrc/py_netconn.cpp), None with native I/O off
+        self.native_pick = _native.pg_pool_execute if netconn.enabled() else None
 
     async def open(self) -> "Pool":
         self._conns.append(await PgConnection(self.dsn).connect())  # fail fast on bad DSN/credentials
@@ -574,9 +566,11 @@ class Pool:
 
     def execute(self, sql: str, params: Sequence[Any] = ()):
         """Awaitable ``(rows, command_tag)`` (a future on the fast path)."""
-        f = _pg_pool_execute(self._conns, sql, params, self.spread_at, self.size)  # all connections native
-        if f is not None:
-            return f
+        pick = self.native_pick
+        if pick is not None:
+            f = pick(self._conns, sql, params, self.spread_at, self.size)  # None unless all connections native
+            if f is not None:
+                return f
         best = None
         bp = 0
         live = 0
@@ -589,8 +583,6 @@ class Pool:
         if best is None:
             return self._execute_slow(sql, params)
         if bp >= self.spread_at and live < self.size:
-            if not _BACKGROUND_GROW:  # BEHOLDER_PG_BACKGROUND_GROW=0: the query waits for the new connection
-                return self._execute_slow(sql, params)
             self._grow()
         return best.execute(sql, params)
 
@@ -619,8 +611,7 @@ class Pool:
         self.grows += 1
 
     async def _execute_slow(self, sql: str, params: Sequence[Any]):
-        """No open connection (or the inline grow of ``BEHOLDER_PG_BACKGROUND_GROW=0``): connect
-        under the lock, so a burst makes one connection, then send."""
+        """No open connection: connect under the lock, so a burst makes one connection, then send."""
         async with self._lock:
             self._conns[:] = [c for c in self._conns if not c.closed]
             live = self._conns

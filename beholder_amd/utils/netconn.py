@@ -10,7 +10,9 @@ authenticated with ordinary asyncio transports; a connection that ends up as pla
 adopted: its socket is duplicated, the asyncio transport is aborted (the duplicate keeps the TCP
 connection open) and the duplicate goes to the ``NetConn``. TLS connections stay on asyncio.
 
-``BEHOLDER_NATIVE_NET=0`` keeps every connection on asyncio transports (A/B runs, debugging).
+``BEHOLDER_NATIVE_IO=0`` is the one switch for all native I/O (debugging, A/B runs): every
+connection stays on an asyncio transport (TLS included), the H1 client and the Postgres pool take
+their Python request paths, and replies complete plain ``asyncio.Future``s (read at import).
 """
 from __future__ import annotations
 
@@ -24,7 +26,8 @@ NetConn = native.NetConn
 
 
 def enabled() -> bool:
-    return os.environ.get("BEHOLDER_NATIVE_NET", "1") != "0"
+    """Native I/O on (``BEHOLDER_NATIVE_IO`` is not ``0``)."""
+    return os.environ.get("BEHOLDER_NATIVE_IO", "1") != "0"
 
 
 def adopt(transport) -> Optional[int]:

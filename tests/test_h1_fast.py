@@ -11,8 +11,8 @@ from beholder_amd.ops import native
 from beholder_amd.sinks import H1Client, HttpError
 from beholder_amd.sinks import h1 as h1mod
 
-pytestmark = pytest.mark.skipif(h1mod._h1_fast is h1mod._h1_python_only,
-                                reason="native H1 path switched off (BEHOLDER_NATIVE_H1=0 / BEHOLDER_IOFUTURE=0)")
+pytestmark = pytest.mark.skipif(h1mod._NATIVE_CALL is None or not H1Client().native_call,
+                                reason="native I/O switched off (BEHOLDER_NATIVE_IO=0)")
 
 
 def run(coro):
@@ -76,30 +76,26 @@ def _cases(port, n=150, seed=7):
 
 async def _drive(port, fast: bool):
     """Every case on one client, each after a warm-up request so a keep-alive connection is idle."""
-    saved = h1mod._h1_fast
+    c = H1Client(timeout_s=5)
     if not fast:
-        h1mod._h1_fast = h1mod._h1_python_only
-    try:
-        c = H1Client(timeout_s=5)
-        out, kinds = [], []
-        for m, url, params in _cases(port):
-            try:
-                await c.request("GET", f"http://127.0.0.1:{port}/warm")
-                await c.request("GET", url.split("?")[0].split("#")[0] or url, params=None)
-            except HttpError:
-                pass
-            aw = c.request(m, url, params=params)
-            try:
-                r = await aw
-                out.append((r.status, r.body, r.headers, r.url))
-            except HttpError as e:
-                out.append(("error", str(e)))
-            kinds.append("native" if getattr(aw, "native", False) else "python")
-        counts = dict(c.counts)
-        await c.close()
-        return out, kinds, counts
-    finally:
-        h1mod._h1_fast = saved
+        c.native_call = None
+    out, kinds = [], []
+    for m, url, params in _cases(port):
+        try:
+            await c.request("GET", f"http://127.0.0.1:{port}/warm")
+            await c.request("GET", url.split("?")[0].split("#")[0] or url, params=None)
+        except HttpError:
+            pass
+        aw = c.request(m, url, params=params)
+        try:
+            r = await aw
+            out.append((r.status, r.body, r.headers, r.url))
+        except HttpError as e:
+            out.append(("error", str(e)))
+        kinds.append("native" if getattr(aw, "native", False) else "python")
+    counts = dict(c.counts)
+    await c.close()
+    return out, kinds, counts
 
 
 def test_fast_path_sends_the_same_bytes_and_returns_the_same_responses():
@@ -156,32 +152,28 @@ def test_fast_path_declines_foreign_argument_types():
     import types
 
     async def one(fast):
-        saved = h1mod._h1_fast
+        s = await Raw(lambda t: OK).start()
+        c = H1Client(timeout_s=5)
         if not fast:
-            h1mod._h1_fast = h1mod._h1_python_only
-        try:
-            s = await Raw(lambda t: OK).start()
-            c = H1Client(timeout_s=5)
-            base = f"http://127.0.0.1:{s.port}"
-            seen = []
-            for m, url, params in [("POST", base + "/a", types.MappingProxyType({"k": "v w"})),
-                                   ("POST", base + "/b", [("x", 1)]),
-                                   ("GET", "http://café.invalid/x", None),
-                                   (b"GET", base + "/c", None),
-                                   ("GET", base + "/d", {"ok": 1})]:
-                await c.request("GET", base + "/warm")
-                aw = c.request(m, url, params=params)
-                try:
-                    r = await aw
-                    seen.append((r.status, r.url.replace(base, "")))
-                except Exception as e:  # noqa: BLE001 — the exact outcome is compared
-                    seen.append((type(e).__name__, str(e).replace(base, "")))
-                seen.append(getattr(aw, "native", None) is True)
-            await c.close()
-            await s.stop()
-            return seen, [r.split(b"\r\n")[0] for r in s.raw]
-        finally:
-            h1mod._h1_fast = saved
+            c.native_call = None
+        base = f"http://127.0.0.1:{s.port}"
+        seen = []
+        for m, url, params in [("POST", base + "/a", types.MappingProxyType({"k": "v w"})),
+                               ("POST", base + "/b", [("x", 1)]),
+                               ("GET", "http://café.invalid/x", None),
+                               (b"GET", base + "/c", None),
+                               ("GET", base + "/d", {"ok": 1})]:
+            await c.request("GET", base + "/warm")
+            aw = c.request(m, url, params=params)
+            try:
+                r = await aw
+                seen.append((r.status, r.url.replace(base, "")))
+            except Exception as e:  # noqa: BLE001 — the exact outcome is compared
+                seen.append((type(e).__name__, str(e).replace(base, "")))
+            seen.append(getattr(aw, "native", None) is True)
+        await c.close()
+        await s.stop()
+        return seen, [r.split(b"\r\n")[0] for r in s.raw]
 
     async def go():
         return await one(True), await one(False)
@@ -202,28 +194,24 @@ def test_fast_path_reset_retry_redirect_and_errors_match_python():
         return b"HTTP/1.1 200 OK\r\nContent-Length: 3\r\n\r\nnew"
 
     async def one(fast):
-        saved = h1mod._h1_fast
+        s = await Raw(respond).start()
+        c = H1Client(timeout_s=5)
         if not fast:
-            h1mod._h1_fast = h1mod._h1_python_only
-        try:
-            s = await Raw(respond).start()
-            c = H1Client(timeout_s=5)
-            base = f"http://127.0.0.1:{s.port}"
-            seen = []
-            for m, p in [("GET", "/new"), ("GET", "/old"), ("POST", "/old"), ("GET", "/drop"), ("POST", "/drop"),
-                         ("GET", "/bad"), ("GET", "/new")]:
-                await c.request("GET", base + "/new")  # warm: an idle connection for the fast path
-                try:
-                    r = await c.request(m, base + p)
-                    seen.append((r.status, r.body, r.url.replace(base, "")))
-                except HttpError as e:
-                    seen.append(str(e).replace(base, ""))
-            st = dict(c.counts)
-            await c.close()
-            await s.stop()
-            return seen, st, [r.split(b"\r\n")[0] for r in s.raw]
-        finally:
-            h1mod._h1_fast = saved
+            c.native_call = None
+        base = f"http://127.0.0.1:{s.port}"
+        seen = []
+        for m, p in [("GET", "/new"), ("GET", "/old"), ("POST", "/old"), ("GET", "/drop"), ("POST", "/drop"),
+                     ("GET", "/bad"), ("GET", "/new")]:
+            await c.request("GET", base + "/new")  # warm: an idle connection for the fast path
+            try:
+                r = await c.request(m, base + p)
+                seen.append((r.status, r.body, r.url.replace(base, "")))
+            except HttpError as e:
+                seen.append(str(e).replace(base, ""))
+        st = dict(c.counts)
+        await c.close()
+        await s.stop()
+        return seen, st, [r.split(b"\r\n")[0] for r in s.raw]
 
     async def go():
         return await one(True), await one(False)
@@ -269,23 +257,19 @@ def test_client_close_with_requests_in_flight_matches_python():
     """close() while requests wait for their replies: every waiter ends (no hang), with the
     same outcome on the native path and on the Python one, and nothing stays open."""
     async def one(fast):
-        saved = h1mod._h1_fast
+        s = await Raw(lambda t: "hang" if t.startswith("/slow") else OK).start()
+        c = H1Client(timeout_s=5, max_per_host=4)
         if not fast:
-            h1mod._h1_fast = h1mod._h1_python_only
-        try:
-            s = await Raw(lambda t: "hang" if t.startswith("/slow") else OK).start()
-            c = H1Client(timeout_s=5, max_per_host=4)
-            base = f"http://127.0.0.1:{s.port}"
-            await asyncio.gather(*[c.request("GET", f"{base}/w{i}") for i in range(4)])
-            tasks = [asyncio.ensure_future(c.request("POST", f"{base}/slow{i}", params={"i": i})) for i in range(4)]
-            await asyncio.sleep(0.05)
-            await c.close()
-            done = await asyncio.wait_for(asyncio.gather(*tasks, return_exceptions=True), 5)
-            open_ = sum(o.open for o in c._origins.values())
-            await s.stop()
-            return [type(x).__name__ + ":" + str(x).replace(base, "") for x in done], open_, len(c._busy)
-        finally:
-            h1mod._h1_fast = saved
+            c.native_call = None
+        base = f"http://127.0.0.1:{s.port}"
+        await asyncio.gather(*[c.request("GET", f"{base}/w{i}") for i in range(4)])
+        tasks = [asyncio.ensure_future(c.request("POST", f"{base}/slow{i}", params={"i": i})) for i in range(4)]
+        await asyncio.sleep(0.05)
+        await c.close()
+        done = await asyncio.wait_for(asyncio.gather(*tasks, return_exceptions=True), 5)
+        open_ = sum(o.open for o in c._origins.values())
+        await s.stop()
+        return [type(x).__name__ + ":" + str(x).replace(base, "") for x in done], open_, len(c._busy)
 
     async def go():
         return await one(True), await one(False)
@@ -399,34 +383,30 @@ def test_differential_random_server_behaviour(seed):
                 w.close()
 
     async def one(fast):
-        saved = h1mod._h1_fast
+        s = await Srv().start()
+        c = H1Client(timeout_s=5, max_per_host=4)
         if not fast:
-            h1mod._h1_fast = h1mod._h1_python_only
-        try:
-            s = await Srv().start()
-            c = H1Client(timeout_s=5, max_per_host=4)
-            rnd = random.Random(seed + 100)
-            base = f"http://127.0.0.1:{s.port}"
-            out = []
-            for i in range(80):
-                m = rnd.choice(["GET", "POST", "PUT", "HEAD", "DELETE"])
-                params = rnd.choice([None, {"i": i}, {"text": "a b ü", "k": None}])
-                conc = rnd.choice([1, 1, 1, 3])
-                aws = [c.request(m, f"{base}/p{i}_{j}", params=params) for j in range(conc)]
-                res = await asyncio.gather(*aws, return_exceptions=True)
-                for r in res:
-                    if isinstance(r, HttpError):
-                        out.append(("err", str(r).replace(base, "")))
-                    elif isinstance(r, BaseException):
-                        raise r
-                    else:
-                        out.append((r.status, r.body, r.url.replace(base, ""), sorted(r.headers.items())))
-            st = dict(c.counts)
-            await c.close()
-            await s.stop()
-            return out, st, s.trace
-        finally:
-            h1mod._h1_fast = saved
+            c.native_call = None
+        rnd = random.Random(seed + 100)
+        base = f"http://127.0.0.1:{s.port}"
+        out = []
+        for i in range(80):
+            m = rnd.choice(["GET", "POST", "PUT", "HEAD", "DELETE"])
+            params = rnd.choice([None, {"i": i}, {"text": "a b ü", "k": None}])
+            conc = rnd.choice([1, 1, 1, 3])
+            aws = [c.request(m, f"{base}/p{i}_{j}", params=params) for j in range(conc)]
+            res = await asyncio.gather(*aws, return_exceptions=True)
+            for r in res:
+                if isinstance(r, HttpError):
+                    out.append(("err", str(r).replace(base, "")))
+                elif isinstance(r, BaseException):
+                    raise r
+                else:
+                    out.append((r.status, r.body, r.url.replace(base, ""), sorted(r.headers.items())))
+        st = dict(c.counts)
+        await c.close()
+        await s.stop()
+        return out, st, s.trace
 
     async def go():
         return await one(True), await one(False)
@@ -438,7 +418,7 @@ def test_differential_random_server_behaviour(seed):
 
 def test_compiled_handlers_make_h1_calls_directly(monkeypatch):
     """The compiled handlers make the H1Call themselves (no H1Client.request frame); switching
-    sinks/h1.py's `_h1_fast` off at run time sends them back through the Python method."""
+    a client without the `native_call` capability sends them back through the Python method."""
     from beholder_amd.service import Service
     from beholder_amd.store import MemoryStore
     from beholder_amd.topics import PROGRESS
@@ -458,11 +438,11 @@ def test_compiled_handlers_make_h1_calls_directly(monkeypatch):
     monkeypatch.setattr(H1Client, "request", counting)
 
     async def go(direct):
-        if not direct:
-            monkeypatch.setattr(h1mod, "_h1_fast", h1mod._h1_python_only)
         s = await Raw(lambda t: OK).start()
         b = MemoryBroker()
         http = H1Client(timeout_s=5)
+        if not direct:
+            http.native_call = None  # the client hands out no native capability
         url = f"http://127.0.0.1:{s.port}"
         svc = Service(cfg({"service": {"endpoints": {"trello": url, "telegram": url}}}), source=b.consumer(),
                       store=MemoryStore([M1]), http=http, logger=Logger(stream=MemoryStream()), serve_metrics=False)

@@ -146,7 +146,7 @@ def test_native_matches_python(config, no_trello, rows, evs, fault_list, store_k
     assert run_trace("native", *args) == run_trace("python", *args)
 
 
-def test_native_handlers_selected_by_service_and_switchable(monkeypatch):
+def test_native_handlers_selected_by_service_and_switchable():
     from beholder_amd.bench.generator import Workload, bench_config
     from beholder_amd.config import Config
     from beholder_amd.service import Service
@@ -156,10 +156,11 @@ def test_native_handlers_selected_by_service_and_switchable(monkeypatch):
     w = Workload(n_media=32, seed=5)
     data = w.framed(200)
 
-    def run(env_value):
-        monkeypatch.setenv("BEHOLDER_NATIVE_HANDLERS", env_value)
+    def run(native_on):
+        d = bench_config()
+        d["service"]["native_handlers"] = native_on
         http = RecordingHttpClient()
-        svc = Service(Config.from_dict(bench_config()), source=BytesSource(data), store=MemoryStore(w.media),
+        svc = Service(Config.from_dict(d), source=BytesSource(data), store=MemoryStore(w.media),
                       http=http, serve_metrics=False, logger=helpers.Logger(stream=helpers.MemoryStream()))
 
         async def go():
@@ -170,8 +171,8 @@ def test_native_handlers_selected_by_service_and_switchable(monkeypatch):
         st_ = asyncio.run(go())
         return svc, st_, list(http.calls)
 
-    svc_n, st_n, calls_n = run("1")
-    svc_p, st_p, calls_p = run("0")
+    svc_n, st_n, calls_n = run(True)
+    svc_p, st_p, calls_p = run(False)
     assert isinstance(svc_n.handler_impl, native.NativeHandlers)
     assert svc_p.handler_impl is svc_p.handlers
     assert svc_n.handler_impl.stats()["completed_sync"] == 200

@@ -3,8 +3,8 @@
 The H1 sink client and the Postgres client hand their plain-TCP sockets to a NetConn once
 connected; tests/test_h1.py and tests/test_stores.py therefore exercise the native path. This
 file adds what only the native path has (multi-recv replies, send backpressure, fd ownership),
-and re-runs the network tests of both clients with BEHOLDER_NATIVE_NET=0, so the asyncio
-transport path (TLS connections always take it) stays covered too.
+and re-runs the network tests of both clients with BEHOLDER_NATIVE_IO=0, so the asyncio
+transport path stays covered too.
 """
 import asyncio
 import inspect
@@ -40,7 +40,7 @@ ASYNCIO_PATH = ([f for f in _no_arg_tests(test_h1, "test_")
 
 @pytest.mark.parametrize("fn", ASYNCIO_PATH, ids=[f"{f.__module__}.{f.__name__}" for f in ASYNCIO_PATH])
 def test_asyncio_transport_path(fn, monkeypatch):
-    monkeypatch.setenv("BEHOLDER_NATIVE_NET", "0")
+    monkeypatch.setenv("BEHOLDER_NATIVE_IO", "0")
     fn()
 
 
@@ -166,7 +166,7 @@ def test_bad_arguments():
 
 
 def test_disabled_by_env(monkeypatch):
-    monkeypatch.setenv("BEHOLDER_NATIVE_NET", "0")
+    monkeypatch.setenv("BEHOLDER_NATIVE_IO", "0")
 
     async def go():
         pg = await FakePg(auth="trust").start()
@@ -188,13 +188,11 @@ def test_native_pool_pick_matches_python_pick(monkeypatch):
     from beholder_amd.store import pgwire
 
     async def one(native_pick):
-        if not native_pick:
-            monkeypatch.setattr(pgwire, "_pg_pool_execute", pgwire._pg_pool_python_only)
-        else:
-            monkeypatch.setattr(pgwire, "_pg_pool_execute", pgwire._native.pg_pool_execute)
         pg = await FakePg(auth="md5").start()
         try:
-            pool = await pgwire.Pool(pg.dsn, size=3, spread_at=4).open()
+            pool = pgwire.Pool(pg.dsn, size=3, spread_at=4)
+            pool.native_pick = pgwire._native.pg_pool_execute if native_pick else None
+            await pool.open()
             seq, futs = [], []
             for wave in range(3):
                 for i in range(10):
@@ -281,25 +279,23 @@ def test_native_connect_ipv6_literal():
     assert res == (200, b"v6")
 
 
-@pytest.mark.parametrize("env", ["BEHOLDER_IOFUTURE", "BEHOLDER_NATIVE_H1", "BEHOLDER_NATIVE_TLS", "BEHOLDER_NATIVE_POLLER"])
-def test_switched_off_paths_still_work(env):
-    """Each A/B switch (read at import) leaves a working client: the H1 and TLS suites pass with
-    it set to 0 (a NetConn then also completes plain asyncio futures as reply waiters)."""
+def test_native_io_off_still_works():
+    """BEHOLDER_NATIVE_IO=0 (the one native-I/O switch; replies on plain asyncio futures, read at
+    import) leaves working clients: the H1 and TLS suites pass with it."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-p", "no:cacheprovider", "-x",
                         "tests/test_h1.py", "tests/test_tls.py"], cwd=root, capture_output=True, text=True,
-                       env=dict(os.environ, **{env: "0"}), timeout=600)
+                       env=dict(os.environ, BEHOLDER_NATIVE_IO="0"), timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
 
 
 def test_netconns_share_one_epoll_set_per_loop():
     """ops/csrc/py_netpoll.cpp: every NetConn of a loop sits in one epoll set whose fd is the only
     one registered with the loop; it is closed (and leaves the loop) with its last socket."""
-    from beholder_amd.ops import native
-    if not native.netpoll_enabled():
-        pytest.skip("BEHOLDER_NATIVE_POLLER=0")
+    if not netconn.enabled():
+        pytest.skip("BEHOLDER_NATIVE_IO=0")
 
     async def go():
         loop = asyncio.get_running_loop()

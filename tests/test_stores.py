@@ -1,6 +1,5 @@
 """Media stores (triton-core/db parity, index.js:42,68,76,140): memory, sqlite, postgres (wire protocol)."""
 import asyncio
-import os
 
 import pytest
 
@@ -237,8 +236,7 @@ def test_pool_spreads_load_and_replaces_broken_connections():
                     break
                 await asyncio.sleep(0.005)
             spread = pool.connections
-            from beholder_amd.store import pgwire
-            assert pool.grows == (2 if pgwire._BACKGROUND_GROW else 0) and pool.grow_errors == 0
+            assert pool.grows == 2 and pool.grow_errors == 0
             pool._conns[0].abort()  # a broken connection is dropped and replaced
             await asyncio.sleep(0.01)
             res = await asyncio.gather(*[pool.execute("SELECT $1 + 0", (i,)) for i in range(10)])
@@ -251,8 +249,6 @@ def test_pool_spreads_load_and_replaces_broken_connections():
 
 
 def test_pool_grow_never_delays_a_query_and_backs_off_after_a_failure(monkeypatch):
-    if os.environ.get("BEHOLDER_PG_BACKGROUND_GROW", "1") == "0":
-        pytest.skip("background pool grow switched off")
     from beholder_amd.store import pgwire
     from beholder_amd.store.pgwire import Pool
 
@@ -291,8 +287,6 @@ def test_pool_grow_never_delays_a_query_and_backs_off_after_a_failure(monkeypatc
 
 
 def test_pool_close_cancels_a_grow_in_progress(monkeypatch):
-    if os.environ.get("BEHOLDER_PG_BACKGROUND_GROW", "1") == "0":
-        pytest.skip("background pool grow switched off")
     from beholder_amd.store import pgwire
     from beholder_amd.store.pgwire import Pool
 
@@ -530,18 +524,6 @@ def test_compiled_handlers_pick_the_postgres_connection_in_c(monkeypatch):
     assert stats["source"]["acked"] == 30 and comments == 30
     assert type(impl).__name__ == "NativeHandlers"
     assert calls == []  # every lookup went through the direct native pick
-
-
-def test_inline_pool_grow_switch_still_works():
-    """BEHOLDER_PG_BACKGROUND_GROW=0 (read at import) keeps the earlier inline grow: the store
-    suite passes with it."""
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-p", "no:cacheprovider", "-x", "tests/test_stores.py",
-                        "-k", "not inline_pool_grow_switch"], cwd=root, capture_output=True, text=True,
-                       env=dict(os.environ, BEHOLDER_PG_BACKGROUND_GROW="0"), timeout=600)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
 
 
 def test_pool_metrics_render_postgres_connections_and_grows():

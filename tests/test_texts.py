@@ -37,11 +37,10 @@ ALLOWED_IDENTIFIERS = {
     "row_to_media", "send", "send_message", "state", "stats", "status", "strict", "suspended", "telegram",
     "throw", "timeout", "token", "trello", "trello_creator", "update_calls", "update_status",
     "{s:K,s:K,s:O}", "{s:O}", "{}",
-    # store/pgwire.py Pool internals for the direct native connection pick
-    "Pool", "_conns", "_pg_pool_execute", "beholder_amd.ops._native", "beholder_amd.store.pgwire", "pg_pool_execute",
-    "size", "spread_at",
-    # sinks/h1.py's native request path, called directly
-    "_h1_fast", "beholder_amd.sinks.h1", "h1_fast",
+    # the capabilities a Pool (`native_pick`, over its connections) and an H1Client (`native_call`)
+    # hand out, called directly
+    "Pool", "_conns", "native_pick", "beholder_amd.ops._native", "beholder_amd.store.pgwire", "pg_pool_execute",
+    "size", "spread_at", "native_call", "h1_fast",
 }
 # internal errors and docstrings (Python-level diagnostics, never emitted by the reference)
 ALLOWED_MESSAGES = {

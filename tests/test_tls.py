@@ -3,7 +3,7 @@ NetConn) for the HTTPS sinks (`sinks/h1.py` `_connect`) and for Postgres sslmode
 (`store/pgwire.py` `_negotiate_tls`). Trello and Telegram are HTTPS in production
 (index.js:53,83,99); with H1Client's own SSL context (the default one or ``ssl_cafile``) the
 handshake and the record layer run in C on the socket. Every behaviour is checked against the
-asyncio TLS path (``BEHOLDER_NATIVE_TLS=0``)."""
+asyncio TLS path (``BEHOLDER_NATIVE_IO=0``)."""
 import asyncio
 import os
 import shutil
@@ -63,8 +63,8 @@ class TlsServer:
             w.close()
 
 
-requires_native_tls = pytest.mark.skipif(os.environ.get("BEHOLDER_NATIVE_TLS", "1") == "0",
-                                         reason="inspects native TLS state; BEHOLDER_NATIVE_TLS=0")
+requires_native_tls = pytest.mark.skipif(os.environ.get("BEHOLDER_NATIVE_IO", "1") == "0",
+                                         reason="inspects native TLS state; BEHOLDER_NATIVE_IO=0")
 
 
 def ok(body=b"{}"):
@@ -76,9 +76,8 @@ def native_tls(c):
 
 
 def test_native_tls_requests_take_the_fast_path():
-    from beholder_amd.sinks import h1
-    if h1._h1_fast is h1._h1_python_only or os.environ.get("BEHOLDER_NATIVE_TLS", "1") == "0":
-        pytest.skip("native H1 / TLS path switched off")
+    if not H1Client().native_call:
+        pytest.skip("native I/O switched off (BEHOLDER_NATIVE_IO=0)")
 
     async def go():
         s = await TlsServer(lambda t: ok()).start()
@@ -100,18 +99,19 @@ def test_native_tls_requests_take_the_fast_path():
 
 
 def _both(fn):
-    """fn(native: bool) run with the native TLS path and with asyncio's; returns both results."""
+    """fn(native: bool) run with native I/O (native TLS connections) and with asyncio's TLS
+    (``BEHOLDER_NATIVE_IO=0``, read per connection); returns both results."""
     out = {}
     for native in (True, False):
-        old = os.environ.get("BEHOLDER_NATIVE_TLS")
-        os.environ["BEHOLDER_NATIVE_TLS"] = "1" if native else "0"
+        old = os.environ.get("BEHOLDER_NATIVE_IO")
+        os.environ["BEHOLDER_NATIVE_IO"] = "1" if native else "0"
         try:
             out[native] = run(fn(native))
         finally:
             if old is None:
-                os.environ.pop("BEHOLDER_NATIVE_TLS", None)
+                os.environ.pop("BEHOLDER_NATIVE_IO", None)
             else:
-                os.environ["BEHOLDER_NATIVE_TLS"] = old
+                os.environ["BEHOLDER_NATIVE_IO"] = old
     return out[True], out[False]
 
 

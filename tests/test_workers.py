@@ -84,6 +84,7 @@ def _free_port() -> int:
 
 def test_workers_merged_metrics_endpoint(tmp_path):
     """One scrape target for N workers: the supervisor merges the workers' registries."""
+    import urllib.error
     import urllib.request
     port = _free_port()
     cfg = tmp_path / "events.yaml"
@@ -107,7 +108,13 @@ def test_workers_merged_metrics_endpoint(tmp_path):
             while time.time() < deadline and bt.call(lambda b: b.stats(PROGRESS))["acked"] < 300:
                 time.sleep(0.1)
             text = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
-            health = urllib.request.urlopen(f"http://127.0.0.1:{port}/healthz", timeout=5).status
+            health = None
+            while health != 200 and time.time() < deadline:  # a loaded host can answer late once
+                try:
+                    health = urllib.request.urlopen(f"http://127.0.0.1:{port}/healthz", timeout=5).status
+                except urllib.error.HTTPError as e:
+                    health = e.code
+                    time.sleep(0.2)
         finally:
             p.send_signal(signal.SIGTERM)
             rc = p.wait(60)
