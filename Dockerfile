@@ -1,18 +1,26 @@
 # Reference: FROM tritonmedia/base; yarn; copy source into /stack as uid 999 (Dockerfile:1-6).
-FROM python:3.10-slim
+# Two stages: the native runtime is compiled in `build` (g++, OpenSSL headers); the `runtime`
+# image gets the package with the built extension and no compiler or headers, and never
+# rebuilds on import (BEHOLDER_ALLOW_BUILD=0).
 
+FROM python:3.10-slim AS build
 RUN apt-get update && apt-get install -y --no-install-recommends g++ libssl-dev && rm -rf /var/lib/apt/lists/*
 WORKDIR /stack
+RUN pip install --no-cache-dir --prefix=/install protobuf pyyaml
+COPY . /stack
+# native runtime (ingest ring, codec, deliveries, metrics, text, TLS) built in-tree; the optional
+# gfx950 HIP probe library is skipped (no hipcc in this image)
+RUN python -m beholder_amd._build --force --no-hip \
+    && rm -rf beholder_amd/ops/csrc beholder_amd/ops/*.lock tests profiles scripts \
+    && find /stack -name __pycache__ -prune -exec rm -rf {} +
+
+FROM python:3.10-slim AS runtime
+WORKDIR /stack
 RUN useradd --uid 999 --create-home --home-dir /home/beholder beholder && chown 999:999 /stack
-
-COPY --chown=999:999 pyproject.toml /stack/
-RUN pip install --no-cache-dir protobuf pyyaml
-COPY --chown=999:999 . /stack
-# native runtime (ingest ring, codec, deliveries, metrics, text) built in-tree; the optional gfx950
-# HIP probe library is skipped here (no hipcc in this image)
-RUN python -m beholder_amd.ops.build --force && chown -R 999:999 /stack
-
+COPY --from=build /install /usr/local
+COPY --from=build --chown=999:999 /stack /stack
 USER 999
-ENV CONFIG_PATH=/stack/config
+ENV CONFIG_PATH=/stack/config \
+    BEHOLDER_ALLOW_BUILD=0
 EXPOSE 3000
 ENTRYPOINT ["python", "-m", "beholder_amd", "run"]

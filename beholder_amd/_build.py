@@ -67,38 +67,81 @@ def compile_flags(debug: bool = False, sanitize: str = "") -> list:
     return flags
 
 
+def _stamp_matches(target: str, stamp: str, digest: str) -> bool:
+    if not (os.path.exists(target) and os.path.exists(stamp)):
+        return False
+    with open(stamp) as f:
+        return f.read().strip() == digest
+
+
+def _write_atomic(path: str, text: str) -> None:
+    tmp = f"{path}.{os.getpid()}.tmp"
+    with open(tmp, "w") as f:
+        f.write(text)
+    os.replace(tmp, path)
+
+
+class _BuildLock:
+    """``flock`` on ``<target>.lock``: one compile per tree, however many processes import at
+    once (workers of ``run --workers N`` starting together, parallel test runners). The others
+    wait, then find the stamp current and load what the first one built."""
+
+    def __init__(self, target: str):
+        self.path = target + ".lock"
+        self.fd = -1
+
+    def __enter__(self):
+        import fcntl
+        self.fd = os.open(self.path, os.O_RDWR | os.O_CREAT, 0o644)
+        fcntl.flock(self.fd, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *exc):
+        import fcntl
+        fcntl.flock(self.fd, fcntl.LOCK_UN)
+        os.close(self.fd)
+        self.fd = -1
+
+
 def build(force: bool = False, debug: bool = False, sanitize: str = "", cxx: str = "", verbose: bool = False) -> str:
     cxx = cxx or os.environ.get("CXX") or "g++"
     flags = compile_flags(debug, sanitize)
     # hash path-independent flags so a snapshot copied elsewhere (GPU box) reuses the .so
     digest = source_hash([f for f in flags if not f.startswith("-I")] + LIBS + [cxx, sysconfig.get_config_var("SOABI") or ""])
-    if not force and os.path.exists(TARGET) and os.path.exists(STAMP):
-        with open(STAMP) as f:
-            if f.read().strip() == digest:
-                return TARGET
-    tmp = TARGET + ".tmp"
-    # compile translation units in parallel (one compiler process each), then link
-    import concurrent.futures
-    import tempfile
-    cflags = [f for f in flags if f != "-shared"]
-    jobs = max(1, min(len(sources()), int(os.environ.get("MAX_JOBS", "0") or 0) or (os.cpu_count() or 1), 16))
-    with tempfile.TemporaryDirectory(prefix="beholder-build-") as td:
-        def compile_one(src: str) -> str:
-            obj = os.path.join(td, os.path.basename(src) + ".o")
-            cmd = [cxx, *cflags, "-c", src, "-o", obj]
-            if verbose:
-                print(" ".join(cmd), file=sys.stderr)
-            subprocess.run(cmd, check=True)
-            return obj
-        with concurrent.futures.ThreadPoolExecutor(jobs) as ex:
-            objs = list(ex.map(compile_one, sources()))
-        link = [cxx, *[f for f in flags if not f.startswith("-I") and not f.startswith("-W")], *objs, *LIBS, "-o", tmp]
-        if verbose:
-            print(" ".join(link), file=sys.stderr)
-        subprocess.run(link, check=True)
-    os.replace(tmp, TARGET)
-    with open(STAMP, "w") as f:
-        f.write(digest)
+    if not force and _stamp_matches(TARGET, STAMP, digest):
+        return TARGET
+    with _BuildLock(TARGET):
+        if not force and _stamp_matches(TARGET, STAMP, digest):  # built while this process waited
+            return TARGET
+        print(f"beholder: building the native runtime ({os.path.basename(TARGET)}, pid {os.getpid()})",
+              file=sys.stderr)
+        tmp = f"{TARGET}.{os.getpid()}.tmp"  # per process: nothing else ever writes this file
+        # compile translation units in parallel (one compiler process each), then link
+        import concurrent.futures
+        import tempfile
+        cflags = [f for f in flags if f != "-shared"]
+        jobs = max(1, min(len(sources()), int(os.environ.get("MAX_JOBS", "0") or 0) or (os.cpu_count() or 1), 16))
+        try:
+            with tempfile.TemporaryDirectory(prefix="beholder-build-") as td:
+                def compile_one(src: str) -> str:
+                    obj = os.path.join(td, os.path.basename(src) + ".o")
+                    cmd = [cxx, *cflags, "-c", src, "-o", obj]
+                    if verbose:
+                        print(" ".join(cmd), file=sys.stderr)
+                    subprocess.run(cmd, check=True)
+                    return obj
+                with concurrent.futures.ThreadPoolExecutor(jobs) as ex:
+                    objs = list(ex.map(compile_one, sources()))
+                link = [cxx, *[f for f in flags if not f.startswith("-I") and not f.startswith("-W")], *objs, *LIBS,
+                        "-o", tmp]
+                if verbose:
+                    print(" ".join(link), file=sys.stderr)
+                subprocess.run(link, check=True)
+            os.replace(tmp, TARGET)
+        finally:
+            if os.path.exists(tmp):
+                os.unlink(tmp)
+        _write_atomic(STAMP, digest)
     return TARGET
 
 
@@ -129,18 +172,22 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
             h.update(f.read())
     digest = h.hexdigest()
     stamp = HIP_TARGET + ".srchash"
-    if not force and os.path.exists(HIP_TARGET) and os.path.exists(stamp):
-        with open(stamp) as f:
-            if f.read().strip() == digest:
-                return HIP_TARGET
-    tmp = HIP_TARGET + ".tmp"
-    cmd = [cc, *HIP_FLAGS, *srcs, "-o", tmp]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
-    os.replace(tmp, HIP_TARGET)
-    with open(stamp, "w") as f:
-        f.write(digest)
+    if not force and _stamp_matches(HIP_TARGET, stamp, digest):
+        return HIP_TARGET
+    with _BuildLock(HIP_TARGET):
+        if not force and _stamp_matches(HIP_TARGET, stamp, digest):
+            return HIP_TARGET
+        tmp = f"{HIP_TARGET}.{os.getpid()}.tmp"
+        cmd = [cc, *HIP_FLAGS, *srcs, "-o", tmp]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        try:
+            subprocess.run(cmd, check=True)
+            os.replace(tmp, HIP_TARGET)
+        finally:
+            if os.path.exists(tmp):
+                os.unlink(tmp)
+        _write_atomic(stamp, digest)
     return HIP_TARGET
 
 
