@@ -52,7 +52,11 @@ def server_ssl_context() -> ssl.SSLContext:
 
 async def main(port: int, tls: bool = False) -> int:
     loop = asyncio.get_running_loop()
-    sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    # proto=IPPROTO_TCP: asyncio sets TCP_NODELAY only on sockets whose proto says TCP (accepted
+    # sockets inherit it). With proto 0 a small reply written behind an unacknowledged segment
+    # (TLS 1.3 session tickets, then the first response) waits ~40 ms for the client's delayed
+    # ACK (Nagle) -- a stall no production server (nginx: tcp_nodelay on) has.
+    sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM, socket.IPPROTO_TCP)
     sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
     sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
     sock.bind(("127.0.0.1", port))
