@@ -884,7 +884,13 @@ PyObject* nc_execute(NetConnObject* c, PyObject* const* a, Py_ssize_t n) {
                               : PyObject_CallMethodOneArg(c->loop, s_call_soon, c->flush_cb);
       if (!h) {
         c->pending->pop_back();
-        o.resize(mark);
+        o.resize(mark);  // the Parse of a new statement goes too: forget its name (as above)
+        if (new_sql) {
+          PyObject *et, *ev, *tb;
+          PyErr_Fetch(&et, &ev, &tb);
+          if (PyDict_DelItem(c->stmts, new_sql) < 0) PyErr_Clear();
+          PyErr_Restore(et, ev, tb);
+        }
         Py_DECREF(fut);
         Py_DECREF(fut);
         Py_DECREF(name);

@@ -217,6 +217,10 @@ class Service:
         self.listen(T.STATUS, impl.on_status)
         self.listen(T.PROGRESS, impl.on_progress)
         await self._source.start([t for t in T.TOPIC_IDS if self._routes[T.TOPIC_IDS[t]] is not None])
+        if pc > 0:  # the preconnected connections' keep-alive window starts with consumption
+            touch = getattr(self._http, "touch_idle", None)
+            if touch is not None:
+                touch()
         if self.ordering == "per_media":
             self.serializer = KeyedSerializer(self._dispatch_now, self._media_key)
 

@@ -188,6 +188,14 @@ class _Origin:
         self.waiters: Deque[asyncio.Future] = collections.deque()
 
 
+def _sockaddr_host(sa) -> str:
+    """The address of a getaddrinfo sockaddr; a scoped IPv6 one (link-local, scope id in the 4th
+    field) keeps its scope as ``addr%<id>``, which routes it to asyncio's connect."""
+    if len(sa) == 4 and sa[3]:
+        return f"{sa[0]}%{sa[3]}"
+    return sa[0]
+
+
 def _queued(o: _Origin) -> bool:
     """More requests of ``o`` wait for a connection than connects are in progress for them."""
     return sum(1 for w in o.waiters if not w.done()) > o.connecting
@@ -276,6 +284,8 @@ class H1Client(HttpClient):
             port = int(port_s) if port_s else (443 if scheme == "https" else 80)
         except ValueError:
             raise HttpError(f"Invalid URI \"{redact(key)}\"") from None
+        if not 0 < port < 65536:
+            raise HttpError(f"Invalid URI \"{redact(key)}\"")
         o = _Origin(scheme, host, port, authority, auth)
         self._origins[key] = o
         return o
@@ -384,17 +394,25 @@ class H1Client(HttpClient):
             except ValueError:  # a name: resolved within the request's deadline, like create_connection
                 found = await asyncio.wait_for(loop.getaddrinfo(o.host, o.port, type=socket.SOCK_STREAM),
                                                deadline - loop.time())
-                infos = [ai[4][0] for ai in found]
+                infos = [_sockaddr_host(ai[4]) for ai in found]
         errors = []
         for ip in infos:
             remaining = deadline - loop.time()
             if remaining <= 0:
                 raise asyncio.TimeoutError
+            if "%" in ip:  # a scoped (link-local) IPv6 address: inet_pton cannot take it, asyncio can
+                try:
+                    kw = {"ssl": self._ssl_context(), "server_hostname": o.host} if o.tls else {}
+                    await asyncio.wait_for(loop.create_connection(lambda: conn, ip, o.port, **kw), remaining)
+                    return
+                except OSError as e:
+                    errors.append(e)
+                    continue
             try:
                 net = _netconn_connect(ip, o.port, loop, "h1", conn, conn.parser, tls=ntls, server_hostname=o.host,
                                        port=o.port, tls_error=_tls_error)
-            except OSError as e:
-                errors.append(e)
+            except (OSError, ValueError) as e:  # ValueError: an address the native connect cannot parse
+                errors.append(e if isinstance(e, OSError) else OSError(str(e)))
                 continue
             conn.net = net
             try:
@@ -481,7 +499,7 @@ class H1Client(HttpClient):
                                                    self.timeout_s)
                 except (OSError, asyncio.TimeoutError) as e:
                     return 0, e
-                infos = [ai[4][0] for ai in found]
+                infos = [_sockaddr_host(ai[4]) for ai in found]
         got = await asyncio.gather(*(self._connect(o, deadline, infos) for _ in range(want)), return_exceptions=True)
         opened, err = 0, None
         for c in got:
@@ -491,6 +509,20 @@ class H1Client(HttpClient):
                 self._release(c, True)
                 opened += 1
         return opened, err
+
+    def touch_idle(self) -> int:
+        """Restart the keep-alive clock of every idle connection (the service calls this when it
+        starts consuming, so preconnected connections are not dropped for the time startup took).
+        Connections still unused ``keepalive_s`` after that are dropped at the next acquire, as
+        any idle one is: preconnect pays off when traffic starts within ``keepalive_s``."""
+        now = time.monotonic()
+        n = 0
+        for o in self._origins.values():
+            for c in o.idle:
+                if not c.closed:
+                    c.last_used = now
+                    n += 1
+        return n
 
     def _release(self, c: _Conn, keep: bool) -> None:
         o = c.origin

@@ -68,9 +68,14 @@ class Topology:
         return self.routing_keys.get(topic, [topic])
 
     def publish_target(self, topic: str) -> tuple:
-        """``(exchange, routing_key)`` a publisher uses so ``topic`` reaches this consumer."""
+        """``(exchange, routing_key)`` a publisher uses so ``topic`` reaches this consumer: the
+        first configured binding key that is a plain key (on a topic exchange, one without a
+        ``*`` / ``#`` word), else the topic name (the default binding)."""
         if not self.exchange:
             return "", self.queue(topic)
+        for k in self.routing_keys.get(topic, ()):
+            if self.exchange_type != "topic" or not ({"*", "#"} & set(k.split("."))):
+                return self.exchange, k
         return self.exchange, topic
 
     async def declare(self, ch, topics: Sequence[str]) -> None:

@@ -141,7 +141,15 @@ def test_chaos_every_dependency_drops_connections(tls):
                 assert http._native_tls().stats["handshakes"] >= 1
                 assert all(c._net is not None and c._net.tls for c in store._pool._conns if not c.closed)
             svc.request_stop()
-            stats = await asyncio.wait_for(run, 15)
+            try:
+                stats = await asyncio.wait_for(asyncio.shield(run), 15)
+            except asyncio.TimeoutError:  # diagnostics for a shutdown that does not finish
+                stacks = []
+                for t in asyncio.all_tasks():
+                    fr = t.get_stack(limit=3)
+                    stacks.append(f"{t.get_coro()!r}: " + " <- ".join(f"{f.f_code.co_name}:{f.f_lineno}" for f in fr))
+                raise AssertionError(f"service did not stop: inflight={len(svc._inflight)} "
+                                     f"http={http.stats()} source={src.stats()}\n" + "\n".join(stacks)) from None
             await svc.close()
             return broker.stats(PROGRESS), broker.stats(STATUS), stats, src.reconnects, pg.connections, \
                 sink.requests, hits

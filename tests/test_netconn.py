@@ -321,3 +321,83 @@ def test_netconns_share_one_epoll_set_per_loop():
     sizes, fd, attached, readers = run(go())
     assert sizes == [6, 5, 0] and fd == -1 and not attached
     assert readers == (True, False)  # the loop watches the epoll fd, not the client sockets
+
+
+def test_failed_flush_scheduling_forgets_the_new_statement():
+    """when execute() cannot schedule its flush (loop.call_soon raises), the queued
+    Parse is dropped, and so is the statement name: the next execute of that SQL parses it again
+    instead of binding a name the server never saw."""
+    if not netconn.enabled():
+        pytest.skip("BEHOLDER_NATIVE_IO=0")
+
+    async def go():
+        loop = asyncio.get_running_loop()
+        pg = await FakePg(auth="trust").start()
+        try:
+            p = await PgConnection(pg.dsn).connect()
+            assert p._net is not None
+
+            def refuse(*a, **k):
+                raise RuntimeError("loop refuses callbacks")
+            loop.call_soon = refuse
+            try:
+                with pytest.raises(RuntimeError, match="refuses"):
+                    p.execute("SELECT 5 + $1", (1,))
+            finally:
+                del loop.call_soon
+            r = await p.execute("SELECT 5 + $1", (37,))
+            await p.close()
+            return r
+        finally:
+            await pg.stop()
+    assert run(go()) == ([(42,)], "SELECT 1")
+
+
+def test_scoped_ipv6_address_and_bad_port_are_http_errors_or_work():
+    """getaddrinfo can return a scoped IPv6 address ("fe80::1%eth0") that the native
+    connect (inet_pton) cannot parse: it connects through asyncio instead; an address that fails
+    to connect is an HttpError, never a raw ValueError. A port outside 1-65535 is an invalid URI."""
+    from beholder_amd.sinks import HttpError
+
+    async def go():
+        loop = asyncio.get_running_loop()
+
+        async def serve(r, w):
+            await r.readuntil(b"\r\n\r\n")
+            w.write(b"HTTP/1.1 200 OK\r\nContent-Length: 2\r\n\r\nv6")
+            await w.drain()
+            w.close()
+        try:
+            srv = await asyncio.start_server(serve, "::1", 0)
+        except OSError:
+            return None
+        port = srv.sockets[0].getsockname()[1]
+        real = loop.getaddrinfo
+
+        async def scoped(host, *a, **k):
+            if host == "scoped.test":
+                return [(socket.AF_INET6, socket.SOCK_STREAM, 6, "", ("::1", port, 0, 1))]  # scope id 1
+            if host == "deadscope.test":
+                return [(socket.AF_INET6, socket.SOCK_STREAM, 6, "", ("fe80::dead", port, 0, 1))]
+            return await real(host, *a, **k)
+        loop.getaddrinfo = scoped
+        c = H1Client(timeout_s=2)
+        try:
+            r = await c.request("GET", f"http://scoped.test:{port}/x")
+            out = [(r.status, r.body)]
+            for url in (f"http://deadscope.test:{port}/x", "http://127.0.0.1:70000/x"):
+                try:
+                    await c.request("GET", url)
+                    out.append("no error")
+                except HttpError as e:
+                    out.append(type(e).__name__ + ": " + str(e).split(" ")[0])
+            return out
+        finally:
+            del loop.getaddrinfo
+            await c.close()
+            srv.close()
+    res = run(go())
+    if res is None:
+        pytest.skip("no IPv6 loopback")
+    assert res[0] == (200, b"v6")
+    assert res[1].startswith("HttpError") and res[2] == "HttpError: Invalid"

@@ -195,3 +195,32 @@ def test_max_connecting_config_is_validated():
     from beholder_amd.service import make_http_client
     assert make_http_client({"max_connecting": 3}).max_connecting == 3
     assert make_http_client({}).max_connecting == 8
+
+
+def test_preconnected_connections_keep_alive_from_when_consuming_starts():
+    """a startup that took longer than keepalive_s must not have its preconnected
+    connections dropped at the first delivery: the service restarts their keep-alive clock when
+    it starts consuming (H1Client.touch_idle)."""
+    async def go():
+        s = await Scripted(lambda n, m, t, h: OK).start()
+        http = H1Client(timeout_s=5, keepalive_s=0.3)
+        url = f"http://127.0.0.1:{s.port}"
+        c = cfg({"service": {"http": {"preconnect": 2}, "endpoints": {"trello": url, "telegram": url}},
+                 "instance": {"telegram": {"enabled": False}, "emby": {"enabled": False}}})
+        svc = _service(c, http)
+        real = svc._preconnect
+
+        async def slow_preconnect(n, endpoints):
+            await real(n, endpoints)
+            await asyncio.sleep(0.5)  # startup outlasts keepalive_s after the connects
+        svc._preconnect = slow_preconnect
+        await svc.init()
+        before = s.connections
+        await http.request("GET", url + "/1/cards/x")
+        reused = http.counts["reused"]
+        await svc.close()
+        await http.close()
+        await s.stop()
+        return before, s.connections, reused
+    before, after, reused = run(go())
+    assert before == 2 and after == 2 and reused == 1  # without the touch: dropped, a 3rd connect

@@ -100,6 +100,36 @@ def test_publisher_with_the_same_topology_reaches_the_consumer():
     run(go())
 
 
+def test_publisher_uses_a_custom_binding_key():
+    """with custom routing_keys only (the topic name is not bound), the publisher must
+    route with a configured key, or its messages never reach the queue this consumer declared."""
+    topo = {"exchange": "triton", "exchange_type": "topic",
+            "routing_keys": {T.STATUS: ["beholder.status.*", "beholder.status"], T.PROGRESS: ["v1.#"]}}
+    t = Topology.from_config(topo)
+    assert t.publish_target(T.STATUS) == ("triton", "beholder.status")  # the wildcard key is skipped
+    assert t.publish_target(T.PROGRESS) == ("triton", T.PROGRESS)        # only a pattern: the topic name
+    assert Topology.from_config({"exchange": "x", "exchange_type": "direct",
+                                 "routing_keys": {T.STATUS: ["k1", "k2"]}}).publish_target(T.STATUS) == ("x", "k1")
+
+    async def go():
+        broker = await AmqpBroker().start()
+        try:
+            svc, _ = _service(broker.url, topo, [trello_media("m1")])
+            await svc.init()
+            task = asyncio.ensure_future(svc.run())
+            pub = await AmqpPublisher(broker.url, topology=t).connect()
+            await pub.publish(T.STATUS, status_msg("m1", "CONVERTING"), wait=True)
+            await pub.publish(T.PROGRESS, progress_msg("m1", "CONVERTING", 5), wait=True)
+            await pub.close()
+            await _until(lambda: broker.stats(T.STATUS)["acked"] == 1 and broker.stats(T.PROGRESS)["acked"] == 1)
+            svc.request_stop()
+            await task
+            await svc.close()
+        finally:
+            await broker.stop()
+    run(go())
+
+
 def test_passive_declare_fails_loudly_on_a_missing_queue():
     async def go():
         broker = await AmqpBroker().start()
