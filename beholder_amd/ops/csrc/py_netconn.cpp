@@ -31,6 +31,9 @@
 // the socket fails (the fd is already closed and unregistered), _net_error(exc) for a protocol
 // error or an unsolicited reply, _net_message(type, body) for out-of-band Postgres messages.
 #include <errno.h>
+#include <poll.h>
+#include <pthread.h>
+#include <time.h>
 #include <openssl/err.h>
 #include <openssl/ssl.h>
 #include <arpa/inet.h>
@@ -40,8 +43,13 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <deque>
+#include <mutex>
 #include <string>
+#include <thread>
 
 #include "py_common.hpp"
 
@@ -59,7 +67,8 @@ int netpoll_set_write(PyObject* po, int fd, bool write);
 int netpoll_request_flush(PyObject* po, PyObject* conn);
 void netpoll_del(PyObject* po, int fd);
 SSL* tls_new_ssl(PyObject* ctx_obj, int fd, const char* host, int port);
-void tls_count_handshake(SSL* ssl);
+void tls_count_handshake(SSL* ssl, bool offloaded);
+int netpoll_pause(PyObject* po, int fd);
 void tls_describe_failure(SSL* ssl, std::string& reason, std::string& message, bool& verify);
 
 namespace {
@@ -106,6 +115,7 @@ struct NetConnObject {
   PyObject* hs_fut;          // handshake IOFuture: None when established, rejected on failure
   PyObject* tls_error;       // callable(reason, message, verify) -> exception for a failed handshake
   PyObject* poller;          // the loop's NetPoller (py_netpoll.cpp), or NULL: own loop.add_reader
+  void* hs_job;              // HsJob*: the handshake is running on a handshake thread (tls_state 3)
 };
 
 PyTypeObject NetConnType = {PyVarObject_HEAD_INIT(nullptr, 0)};
@@ -114,6 +124,35 @@ char* read_buf() {
   static char* buf = static_cast<char*>(PyMem_RawMalloc(kReadSize));  // one event-loop thread
   return buf;
 }
+
+// ---- TLS handshakes off the event loop --------------------------------------------------------
+// A TLS handshake costs the client a few hundred microseconds of CPU (key exchange, certificate
+// and signature checks). On the loop thread that time is taken from every delivery in flight: a
+// burst of new sink connections (the first deliveries after start, a pool growing, reconnects
+// after an outage) shows up as the handle-latency tail. With a NetPoller, a NetConn hands its
+// handshake to a small pool of handshake threads instead: the fd leaves the epoll interest set,
+// a thread runs SSL_do_handshake with poll(2) until it completes or fails, and posts the result
+// back with loop.call_soon_threadsafe; the loop thread then resumes the connection exactly as
+// after an on-loop handshake (same stats, same errors). While a thread owns the handshake the
+// loop never touches the SSL: closing the connection marks the job orphaned and shuts the socket
+// down, and whichever side finishes last frees the SSL and closes the fd.
+enum HsState : int { HS_RUNNING = 0, HS_DONE = 1, HS_ORPHANED = 2 };
+enum HsResult : int { HR_OK = 0, HR_SSL = 1, HR_TIMEOUT = 2 };
+constexpr double kHandshakeCapS = 120.0;  // safety net; callers abort on their own deadlines
+
+struct HsJob {
+  NetConnObject* conn;  // reference owned by the job, released on the loop thread
+  SSL* ssl;
+  int fd;
+  double deadline;
+  std::atomic<int> state{HS_RUNNING};
+  int result = HR_OK;
+  std::string reason, message;
+  bool verify = false;
+};
+
+PyObject* g_tls_done = nullptr;  // module function _tls_handshake_done(conn)
+PyObject* s_call_soon_threadsafe = nullptr;
 
 // Stops watching the fd and closes it (idempotent). Errors from the loop are swallowed: this
 // runs on teardown paths.
@@ -140,6 +179,19 @@ void shut(NetConnObject* c) {
   }
   PyErr_Clear();
   PyErr_Restore(et, ev, tb);
+  if (c->hs_job) {
+    auto* j = static_cast<HsJob*>(c->hs_job);
+    if (j->state.exchange(HS_ORPHANED) == HS_RUNNING) {
+      // the handshake thread still uses the SSL and the fd: wake it up; it frees both when done
+      ::shutdown(c->fd, SHUT_RDWR);
+      c->ssl = nullptr;
+      c->fd = -1;
+      c->writing = 0;
+      c->closed = 1;
+      c->out->clear();
+      return;
+    }
+  }
   if (c->ssl) {
     // an established session stays resumable when its connection is dropped without close_notify
     // (idle keep-alive expiry, peer reset): OpenSSL would otherwise mark the cached session
@@ -304,7 +356,7 @@ int tls_handshake(NetConnObject* c) {
   int r = SSL_do_handshake(c->ssl);
   if (r == 1) {
     c->tls_state = 2;
-    tls_count_handshake(c->ssl);
+    tls_count_handshake(c->ssl, false);
     if (unwatch_writes(c) < 0) return -1;
     PyObject* f = c->hs_fut;
     if (f && !iofuture_done(f) && iofuture_resolve(f, Py_None) < 0) return -1;
@@ -326,6 +378,194 @@ int tls_handshake(NetConnObject* c) {
   hs_fail(c, exc);
   Py_DECREF(exc);
   return 0;
+}
+
+double mono_now() {
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return double(t.tv_sec) + double(t.tv_nsec) * 1e-9;
+}
+
+// On a handshake thread: SSL_do_handshake until done, failed or past the deadline.
+void hs_run(HsJob* j) {
+  ERR_clear_error();  // the error queue is per thread
+  for (;;) {
+    int r = SSL_do_handshake(j->ssl);
+    if (r == 1) {
+      j->result = HR_OK;
+      return;
+    }
+    int e = SSL_get_error(j->ssl, r);
+    if ((e == SSL_ERROR_WANT_READ || e == SSL_ERROR_WANT_WRITE) && j->state.load() != HS_ORPHANED) {
+      double left = j->deadline - mono_now();
+      if (left <= 0) {
+        j->result = HR_TIMEOUT;
+        return;
+      }
+      pollfd p;
+      p.fd = j->fd;
+      p.events = short(e == SSL_ERROR_WANT_READ ? POLLIN : POLLOUT);
+      p.revents = 0;
+      int ms = int(std::min(left, 0.25) * 1000.0) + 1;
+      if (::poll(&p, 1, ms) < 0 && errno != EINTR) {
+        j->reason = "SYSCALL";
+        j->message = std::string("[SSL: SYSCALL] poll: ") + strerror(errno);
+        j->result = HR_SSL;
+        return;
+      }
+      continue;
+    }
+    tls_describe_failure(j->ssl, j->reason, j->message, j->verify);
+    ERR_clear_error();
+    j->result = HR_SSL;
+    return;
+  }
+}
+
+// On a handshake thread: hand the finished job back to the loop thread.
+void hs_post(HsJob* j) {
+  if (_Py_IsFinalizing()) return;  // the process is exiting: nothing is waiting any more
+  PyGILState_STATE g = PyGILState_Ensure();
+  PyObject* loop = j->conn->loop;
+  PyObject* r = loop ? PyObject_CallMethodObjArgs(loop, s_call_soon_threadsafe, g_tls_done,
+                                                  reinterpret_cast<PyObject*>(j->conn), nullptr)
+                     : nullptr;
+  if (r) {
+    Py_DECREF(r);
+  } else {  // the loop is closed: the connection is dead; drop the job here
+    PyErr_Clear();
+    NetConnObject* c = j->conn;
+    if (c->hs_job == j) c->hs_job = nullptr;
+    delete j;
+    Py_DECREF(c);
+  }
+  PyGILState_Release(g);
+}
+
+struct HsPool {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<HsJob*> q;
+  unsigned threads = 0;
+};
+HsPool* g_hs = nullptr;  // process-lifetime (its threads never exit); replaced in a forked child
+
+void hs_worker(HsPool* pool) {
+  for (;;) {
+    HsJob* j;
+    {
+      std::unique_lock<std::mutex> lock(pool->mu);
+      pool->cv.wait(lock, [pool] { return !pool->q.empty(); });
+      j = pool->q.front();
+      pool->q.pop_front();
+    }
+    hs_run(j);
+    if (j->state.exchange(HS_DONE) == HS_ORPHANED) {  // closed meanwhile: the SSL and fd are ours
+      SSL_free(j->ssl);
+      ::close(j->fd);
+      j->ssl = nullptr;
+      j->fd = -1;
+    }
+    hs_post(j);
+  }
+}
+
+void hs_after_fork_child() { g_hs = nullptr; }
+
+bool hs_submit(HsJob* j) {
+  static bool atfork = (pthread_atfork(nullptr, nullptr, hs_after_fork_child), true);
+  (void)atfork;
+  try {
+    if (!g_hs) g_hs = new HsPool();
+    HsPool* pool = g_hs;
+    unsigned want = std::max(1u, std::min(4u, std::thread::hardware_concurrency() / 4));
+    {
+      std::lock_guard<std::mutex> lock(pool->mu);
+      pool->q.push_back(j);
+    }
+    while (pool->threads < want) {  // started lazily, on the loop thread
+      std::thread(hs_worker, pool).detach();
+      ++pool->threads;
+    }
+    pool->cv.notify_one();
+    return true;
+  } catch (const std::exception&) {
+    return false;
+  }
+}
+
+// Starts the handshake of `c` (connected, SSL set up) on a handshake thread when it can (a
+// NetPoller to take the fd out of), else on the loop. 0 or -1 with a Python error.
+int tls_start(NetConnObject* c) {
+  c->tls_state = 1;
+  if (!c->poller || !g_tls_done) return tls_handshake(c);
+  auto* j = new (std::nothrow) HsJob();
+  if (!j) return tls_handshake(c);
+  if (netpoll_pause(c->poller, c->fd) < 0) {
+    delete j;
+    return -1;
+  }
+  Py_INCREF(c);
+  j->conn = c;
+  j->ssl = c->ssl;
+  j->fd = c->fd;
+  j->deadline = mono_now() + kHandshakeCapS;
+  c->hs_job = j;
+  c->tls_state = 3;
+  if (!hs_submit(j)) {  // no thread: run it here after all
+    c->hs_job = nullptr;
+    c->tls_state = 1;
+    delete j;
+    Py_DECREF(c);
+    if (netpoll_set_write(c->poller, c->fd, c->writing) < 0) return -1;
+    return tls_handshake(c);
+  }
+  return 0;
+}
+
+// _tls_handshake_done(conn): the loop-thread half (loop.call_soon_threadsafe from hs_post).
+PyObject* mod_tls_done(PyObject*, PyObject* o) {
+  if (Py_TYPE(o) != &NetConnType) {
+    PyErr_SetString(PyExc_TypeError, "_tls_handshake_done(NetConn)");
+    return nullptr;
+  }
+  NetConnObject* c = reinterpret_cast<NetConnObject*>(o);
+  auto* j = static_cast<HsJob*>(c->hs_job);
+  if (!j) Py_RETURN_NONE;
+  c->hs_job = nullptr;
+  int result = j->result;
+  std::string reason = std::move(j->reason), message = std::move(j->message);
+  bool verify = j->verify;
+  delete j;
+  int rc = 0;
+  if (c->fd >= 0 && c->ssl) {  // still open (a close meanwhile has already cleaned up)
+    c->tls_state = 1;
+    if (c->poller && netpoll_set_write(c->poller, c->fd, c->writing) < 0) {
+      rc = -1;
+    } else if (result == HR_OK) {
+      c->tls_state = 2;
+      tls_count_handshake(c->ssl, true);
+      PyObject* f = c->hs_fut;
+      if (f && !iofuture_done(f) && iofuture_resolve(f, Py_None) < 0) rc = -1;
+      if (rc == 0 && c->fd >= 0 && !c->out->empty()) rc = send_out(c);
+    } else if (result == HR_TIMEOUT) {
+      lost(c, ETIMEDOUT);
+    } else {
+      PyObject* exc = c->tls_error ? PyObject_CallFunction(c->tls_error, "ssO", reason.c_str(), message.c_str(),
+                                                           verify ? Py_True : Py_False)
+                                   : PyObject_CallFunction(PyExc_ConnectionError, "s", message.c_str());
+      if (!exc) {
+        rc = -1;
+      } else {
+        shut(c);
+        hs_fail(c, exc);
+        Py_DECREF(exc);
+      }
+    }
+  }
+  Py_DECREF(c);  // the job's reference
+  if (rc < 0) return nullptr;
+  Py_RETURN_NONE;
 }
 
 int append_bytes(NetConnObject* c, PyObject* data) {
@@ -618,8 +858,7 @@ int nc_init(NetConnObject* c, PyObject* args, PyObject* kwds) {
   c->fd = fd;  // owned from here on
   c->closed = 0;
   if (c->ssl && !c->connecting) {
-    c->tls_state = 1;
-    if (tls_handshake(c) < 0) {  // ClientHello goes out now
+    if (tls_start(c) < 0) {  // ClientHello goes out now (here or on a handshake thread)
       shut(c);  // unregistered and closed: the caller only gets the exception
       return -1;
     }
@@ -657,10 +896,7 @@ int connect_done(NetConnObject* c) {
     return 0;
   }
   if (unwatch_writes(c) < 0) return -1;
-  if (c->ssl) {
-    c->tls_state = 1;
-    return tls_handshake(c);
-  }
+  if (c->ssl) return tls_start(c);
   PyObject* f = c->hs_fut;
   if (f && !iofuture_done(f) && iofuture_resolve(f, Py_None) < 0) return -1;
   if (c->fd >= 0 && !c->out->empty()) return send_out(c);
@@ -707,6 +943,7 @@ PyObject* nc_on_readable(NetConnObject* c, PyObject*) {
 // TLS: records are decrypted until OpenSSL wants more bytes; each plaintext chunk goes to the
 // parser as on the plain path (a completed reply resumes its handler right here).
 PyObject* on_readable_tls(NetConnObject* c, char* buf) {
+  if (c->tls_state == 3) Py_RETURN_NONE;  // a handshake thread owns the SSL (an error / hang-up event)
   if (c->tls_state == 1) {
     if (tls_handshake(c) < 0) return nullptr;
     Py_RETURN_NONE;
@@ -771,6 +1008,7 @@ PyObject* nc_on_writable(NetConnObject* c, PyObject*) {
     if (connect_done(c) < 0) return nullptr;
     Py_RETURN_NONE;
   }
+  if (c->ssl && c->tls_state == 3) Py_RETURN_NONE;  // on a handshake thread
   if (c->ssl && c->tls_state == 1) {
     if (tls_handshake(c) < 0) return nullptr;
     Py_RETURN_NONE;
@@ -970,7 +1208,7 @@ PyObject* nc_get_handshake(NetConnObject* c, void*) {
 }
 PyObject* nc_get_tls(NetConnObject* c, void*) {
   if (c->tls_state == 0) Py_RETURN_NONE;
-  if (c->tls_state == 1 || !c->ssl) Py_RETURN_FALSE;
+  if (c->tls_state != 2 || !c->ssl) Py_RETURN_FALSE;
   return PyUnicode_FromString(SSL_get_version(c->ssl));
 }
 PyObject* nc_get_stats(NetConnObject* c, void*) {
@@ -1196,6 +1434,8 @@ PyMethodDef pool_functions[] = {
      "connected (and TLS established)"},
     {"pg_pool_execute", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(mod_pg_pool_execute)),
      METH_FASTCALL, "pg_pool_execute(conns, sql, params, spread_at, size) -> IOFuture or None (store/pgwire.py Pool)"},
+    {"_tls_handshake_done", mod_tls_done, METH_O,
+     "_tls_handshake_done(conn): finish a handshake a handshake thread ran (called via call_soon_threadsafe)"},
     {nullptr, nullptr, 0, nullptr}};
 
 }  // namespace
@@ -1243,9 +1483,12 @@ int init_netconn_types(PyObject* m) {
   if (PyType_Ready(&NetConnType) < 0) return -1;
   Py_INCREF(&NetConnType);
   if (PyModule_AddObject(m, "NetConn", reinterpret_cast<PyObject*>(&NetConnType)) < 0) return -1;
-  if (!(s_closed_name = PyUnicode_InternFromString("closed")) || !(s_net_name = PyUnicode_InternFromString("_net")))
+  if (!(s_closed_name = PyUnicode_InternFromString("closed")) || !(s_net_name = PyUnicode_InternFromString("_net")) ||
+      !(s_call_soon_threadsafe = PyUnicode_InternFromString("call_soon_threadsafe")))
     return -1;
-  return PyModule_AddFunctions(m, pool_functions);
+  if (PyModule_AddFunctions(m, pool_functions) < 0) return -1;
+  g_tls_done = PyObject_GetAttrString(m, "_tls_handshake_done");  // kept for the module's lifetime
+  return g_tls_done ? 0 : -1;
 }
 
 }  // namespace beholder

@@ -281,6 +281,22 @@ int netpoll_set_write(PyObject* po, int fd, bool write) {
   return 0;
 }
 
+// Stop reporting readiness of `fd` (it stays in the set; a hang-up or an error is still
+// reported): a handshake thread owns the socket for now. netpoll_set_write restores it. 0 or -1.
+int netpoll_pause(PyObject* po, int fd) {
+  PollerObject* p = reinterpret_cast<PollerObject*>(po);
+  if (p->epfd < 0) return 0;
+  epoll_event ev;
+  memset(&ev, 0, sizeof ev);
+  ev.events = 0;
+  ev.data.fd = fd;
+  if (epoll_ctl(p->epfd, EPOLL_CTL_MOD, fd, &ev) < 0) {
+    PyErr_SetFromErrno(PyExc_OSError);
+    return -1;
+  }
+  return 0;
+}
+
 // `conn` queued queries (its flush_scheduled flag is set by the caller): flushed at the end of the
 // dispatch in progress, else by one call_soon(_flush) shared by all connections. 0 or -1.
 int netpoll_request_flush(PyObject* po, PyObject* conn) {

@@ -24,6 +24,7 @@
 
 #include <deque>
 #include <map>
+#include <mutex>
 #include <string>
 
 #include "py_common.hpp"
@@ -38,7 +39,10 @@ constexpr const char* kCiphers = "@SECLEVEL=2:ECDH+AESGCM:ECDH+CHACHA20:ECDH+AES
 struct TlsContextObject {
   PyObject_HEAD SSL_CTX* ctx;
   std::map<std::string, std::deque<SSL_SESSION*>>* sessions;  // "host:port" -> newest sessions (one ref each)
-  uint64_t handshakes, resumed;
+  // sessions is shared with the handshake threads (py_netconn.cpp): a TLS 1.2 session is stored by
+  // the new-session callback inside SSL_do_handshake, which may run on one of them
+  std::mutex* mu;
+  uint64_t handshakes, resumed, offloaded;
   bool check_hostname;  // the certificate must name the host (verify-full / HTTPS)
 };
 
@@ -67,6 +71,7 @@ int on_new_session(SSL* ssl, SSL_SESSION* sess) {
   auto* self = static_cast<TlsContextObject*>(SSL_get_ex_data(ssl, g_ex_index));
   auto* key = static_cast<std::string*>(SSL_get_ex_data(ssl, g_key_index));
   if (!self || !key || !self->sessions) return 0;
+  std::lock_guard<std::mutex> lock(*self->mu);
   auto it = self->sessions->find(*key);
   if (it == self->sessions->end()) {
     if (self->sessions->size() >= 1024) free_all(self);  // bounded: rebuilt on demand
@@ -95,7 +100,8 @@ PyObject* tc_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
   s->ctx = nullptr;
   s->check_hostname = verify && check_hostname;
   s->sessions = new (std::nothrow) std::map<std::string, std::deque<SSL_SESSION*>>();
-  if (!s->sessions) {
+  s->mu = new (std::nothrow) std::mutex();
+  if (!s->sessions || !s->mu) {
     Py_DECREF(s);
     return PyErr_NoMemory();
   }
@@ -139,19 +145,25 @@ void tc_dealloc(TlsContextObject* s) {
     free_all(s);
     delete s->sessions;
   }
+  delete s->mu;
   if (s->ctx) SSL_CTX_free(s->ctx);
   Py_TYPE(s)->tp_free(reinterpret_cast<PyObject*>(s));
 }
 
 PyObject* tc_get_stats(TlsContextObject* s, void*) {
   Py_ssize_t n = 0;
-  for (auto& kv : *s->sessions) n += Py_ssize_t(kv.second.size());
-  return Py_BuildValue("{s:K,s:K,s:n}", "handshakes", static_cast<unsigned long long>(s->handshakes), "resumed",
-                       static_cast<unsigned long long>(s->resumed), "cached_sessions", n);
+  {
+    std::lock_guard<std::mutex> lock(*s->mu);
+    for (auto& kv : *s->sessions) n += Py_ssize_t(kv.second.size());
+  }
+  return Py_BuildValue("{s:K,s:K,s:n,s:K}", "handshakes", static_cast<unsigned long long>(s->handshakes), "resumed",
+                       static_cast<unsigned long long>(s->resumed), "cached_sessions", n, "offloaded",
+                       static_cast<unsigned long long>(s->offloaded));
 }
 
 PyGetSetDef tc_getset[] = {
-    {"stats", reinterpret_cast<getter>(tc_get_stats), nullptr, "handshakes, resumed, cached_sessions", nullptr},
+    {"stats", reinterpret_cast<getter>(tc_get_stats), nullptr,
+     "handshakes, resumed, cached_sessions, offloaded (handshakes run on a handshake thread)", nullptr},
     {nullptr, nullptr, nullptr, nullptr, nullptr}};
 
 }  // namespace
@@ -181,26 +193,31 @@ SSL* tls_new_ssl(PyObject* ctx_obj, int fd, const char* host, int port) {
     PyErr_Format(PyExc_RuntimeError, "TLS setup for %s: %s", host, last_error_text().c_str());
     return nullptr;
   }
-  auto it = tc->sessions->find(*key);
-  if (it != tc->sessions->end() && !it->second.empty()) {
-    SSL_SESSION* sess = it->second.back();
-    SSL_set_session(ssl, sess);  // the SSL holds its own reference
-    if (SSL_SESSION_get_protocol_version(sess) == TLS1_3_VERSION) {
-      // TLS 1.3 tickets are single use (RFC 8446 C.4): the resumed connection brings new ones
-      SSL_SESSION_free(sess);
-      it->second.pop_back();
+  {
+    std::lock_guard<std::mutex> lock(*tc->mu);
+    auto it = tc->sessions->find(*key);
+    if (it != tc->sessions->end() && !it->second.empty()) {
+      SSL_SESSION* sess = it->second.back();
+      SSL_set_session(ssl, sess);  // the SSL holds its own reference
+      if (SSL_SESSION_get_protocol_version(sess) == TLS1_3_VERSION) {
+        // TLS 1.3 tickets are single use (RFC 8446 C.4): the resumed connection brings new ones
+        SSL_SESSION_free(sess);
+        it->second.pop_back();
+      }
     }
   }
   SSL_set_connect_state(ssl);
   return ssl;
 }
 
-// Handshake finished on `ssl`: count it (resumed or full).
-void tls_count_handshake(SSL* ssl) {
+// Handshake finished on `ssl`: count it (resumed or full; run on a handshake thread). Called on
+// the loop thread.
+void tls_count_handshake(SSL* ssl, bool offloaded) {
   auto* tc = static_cast<TlsContextObject*>(SSL_get_ex_data(ssl, g_ex_index));
   if (!tc) return;
   ++tc->handshakes;
   if (SSL_session_reused(ssl)) ++tc->resumed;
+  if (offloaded) ++tc->offloaded;
 }
 
 // Description of a failed handshake, Python-ssl style: reason ("CERTIFICATE_VERIFY_FAILED",

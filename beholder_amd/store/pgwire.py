@@ -210,6 +210,7 @@ class PgConnection(asyncio.Protocol):
         self._stmts: Dict[str, bytes] = {}
         self._n_stmts = 0
         self._ssl_answer: Optional[asyncio.Future] = None
+        self._lost_in_startup = False
         self.tls = False
         # plain TCP after startup: the socket belongs to a native NetConn (utils/netconn.py),
         # which takes over execute() and the reply matching
@@ -265,6 +266,7 @@ class PgConnection(asyncio.Protocol):
         if self._net is not None:
             return  # the transport was aborted when the socket was handed to the NetConn
         self.closed = True
+        self._lost_in_startup = self._startup is not None or self._lost_in_startup
         if self._flush_handle is not None:
             self._flush_handle.cancel()
             self._flush_handle = None
@@ -307,6 +309,7 @@ class PgConnection(asyncio.Protocol):
             self.__dict__.pop("execute", None)
         self._reader = PgReader()
         self._startup = asyncio.Queue()
+        self._lost_in_startup = False
         self._stmts.clear()
         mode = p["sslmode"]
         if mode not in SSL_MODES:
@@ -330,6 +333,13 @@ class PgConnection(asyncio.Protocol):
             self._startup = None
             raise
         self._startup = None
+        lost = self._net.closed if self._net is not None else (self._transport is None or self._transport.is_closing()
+                                                               or self._lost_in_startup)
+        if lost:  # the server closed right after ReadyForQuery: connection_lost has already run
+            if self._net is not None:
+                self._net.abort()
+                self._net = None
+            raise PgProtocolError("connection lost during startup")
         self._reader.query_mode = True
         self.closed = False
         if self._net is not None:  # native TLS since the SSLRequest

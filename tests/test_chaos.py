@@ -148,8 +148,14 @@ def test_chaos_every_dependency_drops_connections(tls):
                 for t in asyncio.all_tasks():
                     fr = t.get_stack(limit=3)
                     stacks.append(f"{t.get_coro()!r}: " + " <- ".join(f"{f.f_code.co_name}:{f.f_lineno}" for f in fr))
+                waiters = {k: (len(o.waiters), sum(1 for w in o.waiters if not w.done()), o.open, o.connecting,
+                               len(o.idle)) for k, o in http._origins.items()}
+                pool = store._pool
+                pgc = [(c.closed, getattr(c._net, "pending", None), len(c._pending)) for c in pool._conns] if pool else None
                 raise AssertionError(f"service did not stop: inflight={len(svc._inflight)} "
-                                     f"http={http.stats()} source={src.stats()}\n" + "\n".join(stacks)) from None
+                                     f"http={http.stats()} waiters={waiters} dials={len(http._dials)} "
+                                     f"busy={len(http._busy)} pg={pgc} source={src.stats()}\n"
+                                     + "\n".join(stacks)) from None
             await svc.close()
             return broker.stats(PROGRESS), broker.stats(STATUS), stats, src.reconnects, pg.connections, \
                 sink.requests, hits

@@ -612,3 +612,40 @@ def test_store_pool_knobs_reach_the_pool_and_are_validated():
         finally:
             await pg.stop()
     assert run(go()) == (3, 2)
+
+
+@pytest.mark.parametrize("native_io", ["1", "0"])
+def test_server_closing_right_after_startup_is_a_failed_connect(native_io, monkeypatch):
+    """A server that closes the socket right behind its ReadyForQuery (a restart, a pooler
+    recycling the backend): the connection is lost before connect() returns. connect() must fail
+    (the pool then reconnects) instead of reporting an open connection whose queries are never
+    answered (found by the chaos test: 100 handlers waiting on a dead asyncio-path connection)."""
+    import struct
+
+    monkeypatch.setenv("BEHOLDER_NATIVE_IO", native_io)
+
+    async def serve(reader, writer):
+        n = int.from_bytes(await reader.readexactly(4), "big")
+        await reader.readexactly(n - 4)
+        writer.write(b"R" + struct.pack("!II", 8, 0) + b"Z" + struct.pack("!I", 5) + b"I")
+        await writer.drain()
+        writer.close()
+
+    async def go():
+        srv = await asyncio.start_server(serve, "127.0.0.1", 0)
+        port = srv.sockets[0].getsockname()[1]
+        try:
+            c = PgConnection(f"postgres://u@127.0.0.1:{port}/db?sslmode=disable")
+            try:
+                await c.connect()
+                await asyncio.sleep(0.05)
+                try:  # if connect() won the race, the query must fail fast, never hang
+                    await asyncio.wait_for(c.execute("SELECT 1"), 2)
+                    return "answered"
+                except (PgProtocolError, ConnectionError):
+                    return "query failed"
+            except PgProtocolError:
+                return "connect failed"
+        finally:
+            srv.close()
+    assert run(go()) in ("connect failed", "query failed")

@@ -348,6 +348,10 @@ def test_tls13_tickets_are_single_use_and_a_reconnect_burst_resumes():
             while o.idle:
                 c._drop(o.idle.pop())
         await asyncio.gather(*[c.request("GET", url) for _ in range(cached0)])
+        for _ in range(200):  # a background connect may finish after the burst was served
+            if not c._dials:
+                break
+            await asyncio.sleep(0.005)
         st = t.stats
         await c.close()
         await s.stop()
@@ -425,6 +429,10 @@ def test_first_burst_admits_at_most_max_connecting_handshakes(max_connecting):
                 inflight["now"] -= 1
         c._dial = counted
         rs = await asyncio.gather(*[c.request("GET", url) for _ in range(100)])
+        for _ in range(400):  # background connects may finish after the burst was served
+            if not c._dials:
+                break
+            await asyncio.sleep(0.005)
         st = c.stats()
         await c.close()
         await s.stop()
@@ -459,3 +467,48 @@ def test_pool_still_grows_past_max_connecting_under_slow_responses():
     rs, st = run(go())
     assert all(r.status == 200 for r in rs)
     assert st["connecting_peak"] <= 4 and st["connections"] > 4
+
+
+@requires_native_tls
+def test_handshakes_run_on_handshake_threads_and_abort_cleanly():
+    """The client half of each TLS handshake runs on a handshake thread (py_netconn.cpp), not on
+    the event loop: every handshake of a burst is counted as offloaded. Connections closed while
+    their handshake is still on a thread (a server that never answers) release their socket."""
+    import gc
+
+    import psutil
+
+    def client_sockets(port):  # this process's sockets connected TO `port` (not the server's own)
+        return sum(1 for k in psutil.Process().net_connections(kind="tcp") if k.raddr and k.raddr.port == port)
+
+    async def go():
+        s = await TlsServer(lambda t: ok()).start()
+        silent = await TlsServer(lambda t: ok(), handshake=False).start()
+        c = H1Client(timeout_s=5, ssl_cafile=TLS_CERT)
+        url = f"https://127.0.0.1:{s.port}/x"
+        rs = await asyncio.gather(*[c.request("GET", url) for _ in range(40)])
+        for _ in range(200):
+            if not c._dials:
+                break
+            await asyncio.sleep(0.005)
+        st = dict(c._native_tls().stats)
+        await c.close()
+        for _ in range(3):  # handshakes that never finish, abandoned by the client
+            c2 = H1Client(timeout_s=0.2, ssl_cafile=TLS_CERT)
+            res = await asyncio.gather(*[c2.request("GET", f"https://127.0.0.1:{silent.port}/y") for _ in range(8)],
+                                       return_exceptions=True)
+            assert all(isinstance(x, HttpError) for x in res)
+            await c2.close()
+        for _ in range(100):  # the threads notice the shutdown and close the sockets
+            gc.collect()
+            if client_sockets(silent.port) == 0:
+                break
+            await asyncio.sleep(0.01)
+        left = client_sockets(silent.port)
+        await s.stop()
+        silent.server.close()
+        return rs, st, left
+    rs, st, left = run(go())
+    assert all(r.status == 200 for r in rs)
+    assert st["handshakes"] >= 2 and st["offloaded"] == st["handshakes"]
+    assert left == 0
