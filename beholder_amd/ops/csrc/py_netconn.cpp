@@ -45,12 +45,14 @@
 
 #include <algorithm>
 #include <atomic>
+#include <memory>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
 #include <string>
 #include <thread>
 
+#include "hs_wake.hpp"
 #include "py_common.hpp"
 
 namespace beholder {
@@ -69,6 +71,7 @@ void netpoll_del(PyObject* po, int fd);
 SSL* tls_new_ssl(PyObject* ctx_obj, int fd, const char* host, int port);
 void tls_count_handshake(SSL* ssl, bool offloaded);
 int netpoll_pause(PyObject* po, int fd);
+std::shared_ptr<HsWake> netpoll_wake(PyObject* po);
 void tls_describe_failure(SSL* ssl, std::string& reason, std::string& message, bool& verify);
 
 namespace {
@@ -131,17 +134,19 @@ char* read_buf() {
 // burst of new sink connections (the first deliveries after start, a pool growing, reconnects
 // after an outage) shows up as the handle-latency tail. With a NetPoller, a NetConn hands its
 // handshake to a small pool of handshake threads instead: the fd leaves the epoll interest set,
-// a thread runs SSL_do_handshake with poll(2) until it completes or fails, and posts the result
-// back with loop.call_soon_threadsafe; the loop thread then resumes the connection exactly as
-// after an on-loop handshake (same stats, same errors). While a thread owns the handshake the
-// loop never touches the SSL: closing the connection marks the job orphaned and shuts the socket
-// down, and whichever side finishes last frees the SSL and closes the fd.
+// a thread runs SSL_do_handshake with poll(2) until it completes or fails, and queues the result
+// on the poller's completion channel (hs_wake.hpp: an eventfd in the same epoll set, so the
+// thread never needs the GIL); the poller's `_run` then resumes the connection on the loop
+// thread exactly as after an on-loop handshake (same stats, same errors). While a thread owns
+// the handshake the loop never touches the SSL: closing the connection marks the job orphaned
+// and shuts the socket down, and the thread then frees the SSL, closes the fd and drops the job.
 enum HsState : int { HS_RUNNING = 0, HS_DONE = 1, HS_ORPHANED = 2 };
 enum HsResult : int { HR_OK = 0, HR_SSL = 1, HR_TIMEOUT = 2 };
 constexpr double kHandshakeCapS = 120.0;  // safety net; callers abort on their own deadlines
 
 struct HsJob {
-  NetConnObject* conn;  // reference owned by the job, released on the loop thread
+  NetConnObject* conn;  // no reference: read only on the loop thread, cleared when the conn closes
+  std::shared_ptr<HsWake> wake;  // the loop's completion channel
   SSL* ssl;
   int fd;
   double deadline;
@@ -150,9 +155,6 @@ struct HsJob {
   std::string reason, message;
   bool verify = false;
 };
-
-PyObject* g_tls_done = nullptr;  // module function _tls_handshake_done(conn)
-PyObject* s_call_soon_threadsafe = nullptr;
 
 // Stops watching the fd and closes it (idempotent). Errors from the loop are swallowed: this
 // runs on teardown paths.
@@ -181,8 +183,10 @@ void shut(NetConnObject* c) {
   PyErr_Restore(et, ev, tb);
   if (c->hs_job) {
     auto* j = static_cast<HsJob*>(c->hs_job);
+    c->hs_job = nullptr;
     if (j->state.exchange(HS_ORPHANED) == HS_RUNNING) {
-      // the handshake thread still uses the SSL and the fd: wake it up; it frees both when done
+      // the handshake thread still uses the SSL and the fd: wake it up; it frees both (and the
+      // job) when done
       ::shutdown(c->fd, SHUT_RDWR);
       c->ssl = nullptr;
       c->fd = -1;
@@ -191,6 +195,7 @@ void shut(NetConnObject* c) {
       c->out->clear();
       return;
     }
+    j->conn = nullptr;  // finished and queued for this loop: the drain drops it
   }
   if (c->ssl) {
     // an established session stays resumable when its connection is dropped without close_notify
@@ -422,26 +427,6 @@ void hs_run(HsJob* j) {
   }
 }
 
-// On a handshake thread: hand the finished job back to the loop thread.
-void hs_post(HsJob* j) {
-  if (_Py_IsFinalizing()) return;  // the process is exiting: nothing is waiting any more
-  PyGILState_STATE g = PyGILState_Ensure();
-  PyObject* loop = j->conn->loop;
-  PyObject* r = loop ? PyObject_CallMethodObjArgs(loop, s_call_soon_threadsafe, g_tls_done,
-                                                  reinterpret_cast<PyObject*>(j->conn), nullptr)
-                     : nullptr;
-  if (r) {
-    Py_DECREF(r);
-  } else {  // the loop is closed: the connection is dead; drop the job here
-    PyErr_Clear();
-    NetConnObject* c = j->conn;
-    if (c->hs_job == j) c->hs_job = nullptr;
-    delete j;
-    Py_DECREF(c);
-  }
-  PyGILState_Release(g);
-}
-
 struct HsPool {
   std::mutex mu;
   std::condition_variable cv;
@@ -460,13 +445,14 @@ void hs_worker(HsPool* pool) {
       pool->q.pop_front();
     }
     hs_run(j);
-    if (j->state.exchange(HS_DONE) == HS_ORPHANED) {  // closed meanwhile: the SSL and fd are ours
+    std::shared_ptr<HsWake> wake = j->wake;
+    if (j->state.exchange(HS_DONE) == HS_ORPHANED) {  // closed meanwhile: the SSL, fd and job are ours
       SSL_free(j->ssl);
       ::close(j->fd);
-      j->ssl = nullptr;
-      j->fd = -1;
+      delete j;
+      continue;
     }
-    hs_post(j);
+    wake->post(j);  // the loop thread owns the job from here
   }
 }
 
@@ -498,15 +484,17 @@ bool hs_submit(HsJob* j) {
 // NetPoller to take the fd out of), else on the loop. 0 or -1 with a Python error.
 int tls_start(NetConnObject* c) {
   c->tls_state = 1;
-  if (!c->poller || !g_tls_done) return tls_handshake(c);
+  if (!c->poller) return tls_handshake(c);
+  std::shared_ptr<HsWake> wake = netpoll_wake(c->poller);
+  if (!wake) return tls_handshake(c);
   auto* j = new (std::nothrow) HsJob();
   if (!j) return tls_handshake(c);
   if (netpoll_pause(c->poller, c->fd) < 0) {
     delete j;
     return -1;
   }
-  Py_INCREF(c);
   j->conn = c;
+  j->wake = std::move(wake);
   j->ssl = c->ssl;
   j->fd = c->fd;
   j->deadline = mono_now() + kHandshakeCapS;
@@ -516,56 +504,53 @@ int tls_start(NetConnObject* c) {
     c->hs_job = nullptr;
     c->tls_state = 1;
     delete j;
-    Py_DECREF(c);
     if (netpoll_set_write(c->poller, c->fd, c->writing) < 0) return -1;
     return tls_handshake(c);
   }
   return 0;
 }
 
-// _tls_handshake_done(conn): the loop-thread half (loop.call_soon_threadsafe from hs_post).
-PyObject* mod_tls_done(PyObject*, PyObject* o) {
-  if (Py_TYPE(o) != &NetConnType) {
-    PyErr_SetString(PyExc_TypeError, "_tls_handshake_done(NetConn)");
-    return nullptr;
+// The loop-thread half of an offloaded handshake (the poller drains its completion channel).
+// 0, or -1 with a Python error.
+int tls_done(HsJob* j) {
+  NetConnObject* c = j->conn;
+  if (!c) {  // the connection closed after the thread finished
+    delete j;
+    return 0;
   }
-  NetConnObject* c = reinterpret_cast<NetConnObject*>(o);
-  auto* j = static_cast<HsJob*>(c->hs_job);
-  if (!j) Py_RETURN_NONE;
   c->hs_job = nullptr;
   int result = j->result;
   std::string reason = std::move(j->reason), message = std::move(j->message);
   bool verify = j->verify;
   delete j;
+  if (c->fd < 0 || !c->ssl) return 0;
+  Py_INCREF(c);  // a resumed handler may drop the last other reference
   int rc = 0;
-  if (c->fd >= 0 && c->ssl) {  // still open (a close meanwhile has already cleaned up)
-    c->tls_state = 1;
-    if (c->poller && netpoll_set_write(c->poller, c->fd, c->writing) < 0) {
+  c->tls_state = 1;
+  if (c->poller && netpoll_set_write(c->poller, c->fd, c->writing) < 0) {
+    rc = -1;
+  } else if (result == HR_OK) {
+    c->tls_state = 2;
+    tls_count_handshake(c->ssl, true);
+    PyObject* f = c->hs_fut;
+    if (f && !iofuture_done(f) && iofuture_resolve(f, Py_None) < 0) rc = -1;
+    if (rc == 0 && c->fd >= 0 && !c->out->empty()) rc = send_out(c);
+  } else if (result == HR_TIMEOUT) {
+    lost(c, ETIMEDOUT);
+  } else {
+    PyObject* exc = c->tls_error ? PyObject_CallFunction(c->tls_error, "ssO", reason.c_str(), message.c_str(),
+                                                         verify ? Py_True : Py_False)
+                                 : PyObject_CallFunction(PyExc_ConnectionError, "s", message.c_str());
+    if (!exc) {
       rc = -1;
-    } else if (result == HR_OK) {
-      c->tls_state = 2;
-      tls_count_handshake(c->ssl, true);
-      PyObject* f = c->hs_fut;
-      if (f && !iofuture_done(f) && iofuture_resolve(f, Py_None) < 0) rc = -1;
-      if (rc == 0 && c->fd >= 0 && !c->out->empty()) rc = send_out(c);
-    } else if (result == HR_TIMEOUT) {
-      lost(c, ETIMEDOUT);
     } else {
-      PyObject* exc = c->tls_error ? PyObject_CallFunction(c->tls_error, "ssO", reason.c_str(), message.c_str(),
-                                                           verify ? Py_True : Py_False)
-                                   : PyObject_CallFunction(PyExc_ConnectionError, "s", message.c_str());
-      if (!exc) {
-        rc = -1;
-      } else {
-        shut(c);
-        hs_fail(c, exc);
-        Py_DECREF(exc);
-      }
+      shut(c);
+      hs_fail(c, exc);
+      Py_DECREF(exc);
     }
   }
-  Py_DECREF(c);  // the job's reference
-  if (rc < 0) return nullptr;
-  Py_RETURN_NONE;
+  Py_DECREF(c);
+  return rc;
 }
 
 int append_bytes(NetConnObject* c, PyObject* data) {
@@ -1434,11 +1419,14 @@ PyMethodDef pool_functions[] = {
      "connected (and TLS established)"},
     {"pg_pool_execute", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(mod_pg_pool_execute)),
      METH_FASTCALL, "pg_pool_execute(conns, sql, params, spread_at, size) -> IOFuture or None (store/pgwire.py Pool)"},
-    {"_tls_handshake_done", mod_tls_done, METH_O,
-     "_tls_handshake_done(conn): finish a handshake a handshake thread ran (called via call_soon_threadsafe)"},
     {nullptr, nullptr, 0, nullptr}};
 
 }  // namespace
+
+// The NetPoller's drain of its completion channel: one finished handshake job.
+void netconn_tls_done(void* job) {
+  if (tls_done(static_cast<HsJob*>(job)) < 0) PyErr_WriteUnraisable(Py_None);
+}
 
 // The NetPoller's flush of a connection whose queries it collected.
 void netconn_flush(PyObject* o) {
@@ -1483,12 +1471,9 @@ int init_netconn_types(PyObject* m) {
   if (PyType_Ready(&NetConnType) < 0) return -1;
   Py_INCREF(&NetConnType);
   if (PyModule_AddObject(m, "NetConn", reinterpret_cast<PyObject*>(&NetConnType)) < 0) return -1;
-  if (!(s_closed_name = PyUnicode_InternFromString("closed")) || !(s_net_name = PyUnicode_InternFromString("_net")) ||
-      !(s_call_soon_threadsafe = PyUnicode_InternFromString("call_soon_threadsafe")))
+  if (!(s_closed_name = PyUnicode_InternFromString("closed")) || !(s_net_name = PyUnicode_InternFromString("_net")))
     return -1;
-  if (PyModule_AddFunctions(m, pool_functions) < 0) return -1;
-  g_tls_done = PyObject_GetAttrString(m, "_tls_handshake_done");  // kept for the module's lifetime
-  return g_tls_done ? 0 : -1;
+  return PyModule_AddFunctions(m, pool_functions);
 }
 
 }  // namespace beholder

@@ -17,15 +17,19 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <memory>
 #include <unordered_map>
 #include <vector>
 
+#include "hs_wake.hpp"
 #include "py_common.hpp"
 
 namespace beholder {
 
 PyObject* netconn_dispatch(PyObject* conn, uint32_t events);
 void netconn_flush(PyObject* conn);
+void netconn_tls_done(void* job);
 
 namespace {
 
@@ -37,6 +41,7 @@ struct PollerObject {
   PyObject* flush_cb;                            // bound _flush (call_soon)
   std::unordered_map<int, PyObject*>* conns;     // fd -> NetConn (strong)
   std::vector<PyObject*>* to_flush;              // connections with queued queries (strong)
+  std::shared_ptr<HsWake>* wake;                 // TLS handshake completions (created on first use)
   bool flush_scheduled;
 };
 
@@ -46,10 +51,18 @@ bool g_enabled = true;
 
 // Closes the epoll fd and leaves the loop (reader removed, attribute dropped). Errors are
 // swallowed: this runs when the last socket leaves, possibly while the loop shuts down.
+void drain_wake(PollerObject* p) {
+  if (!p->wake || !*p->wake) return;
+  std::deque<void*> jobs;
+  (*p->wake)->take(jobs);
+  for (void* j : jobs) netconn_tls_done(j);
+}
+
 void poller_close(PollerObject* p) {
   if (p->epfd < 0) return;
   PyObject *et, *ev, *tb;
   PyErr_Fetch(&et, &ev, &tb);
+  drain_wake(p);  // finished handshakes of connections that have left (their jobs are dropped)
   if (p->loop) {
     PyObject* fdo = PyLong_FromLong(p->epfd);
     PyObject* r = fdo ? PyObject_CallMethodOneArg(p->loop, s_remove_reader_p, fdo) : nullptr;
@@ -119,6 +132,7 @@ void poller_dealloc(PollerObject* p) {
   Py_CLEAR(p->loop);
   delete p->conns;
   delete p->to_flush;
+  delete p->wake;
   Py_TYPE(p)->tp_free(reinterpret_cast<PyObject*>(p));
 }
 
@@ -133,7 +147,12 @@ PyObject* poller_run(PollerObject* p, PyObject*) {
   if (n < 0) return PyErr_SetFromErrno(PyExc_OSError);
   Py_INCREF(p);
   ++p->running;
+  const int wfd = p->wake && *p->wake ? (*p->wake)->efd : -1;
   for (int i = 0; i < n && p->conns; ++i) {
+    if (evs[i].data.fd == wfd) {  // handshake threads finished some handshakes
+      drain_wake(p);
+      continue;
+    }
     auto it = p->conns->find(evs[i].data.fd);
     if (it == p->conns->end()) continue;  // left during this batch
     PyObject* c = it->second;
@@ -202,6 +221,7 @@ PyObject* netpoll_for(PyObject* loop) {
   p->run_cb = nullptr;
   p->flush_cb = nullptr;
   p->flush_scheduled = false;
+  p->wake = nullptr;
   p->conns = new (std::nothrow) std::unordered_map<int, PyObject*>();
   p->to_flush = new (std::nothrow) std::vector<PyObject*>();
   PyObject_GC_Track(p);
@@ -279,6 +299,28 @@ int netpoll_set_write(PyObject* po, int fd, bool write) {
     return -1;
   }
   return 0;
+}
+
+// The completion channel of this poller's loop (created and added to the epoll set on first
+// use); empty when the poller is closed or the eventfd cannot be made.
+std::shared_ptr<HsWake> netpoll_wake(PyObject* po) {
+  PollerObject* p = reinterpret_cast<PollerObject*>(po);
+  if (p->epfd < 0) return nullptr;
+  if (p->wake && *p->wake) return *p->wake;
+  try {
+    auto w = std::make_shared<HsWake>();
+    if (w->efd < 0) return nullptr;
+    epoll_event ev;
+    memset(&ev, 0, sizeof ev);
+    ev.events = EPOLLIN;
+    ev.data.fd = w->efd;
+    if (epoll_ctl(p->epfd, EPOLL_CTL_ADD, w->efd, &ev) < 0) return nullptr;
+    if (!p->wake) p->wake = new std::shared_ptr<HsWake>();
+    *p->wake = w;
+    return w;
+  } catch (const std::exception&) {
+    return nullptr;
+  }
 }
 
 // Stop reporting readiness of `fd` (it stays in the set; a hang-up or an error is still
