@@ -51,8 +51,9 @@ SERVICE_DEFAULTS: dict = {
         # index.js:42 `new Storage()` is always Postgres (triton-core/db); dsn default: dyn('postgres')
         # table/columns: triton-core/db's schema is not vendored; defaults are our guess (store/schema.py)
         # spread_at: queries in flight on every open connection before the pool opens another
+        # stall_timeout_s: a connection with queries in flight and no reply for this long is dropped
         "store": {"backend": "postgres", "dsn": None, "pool_size": 4, "spread_at": 8, "create_schema": False,
-                  "table": "media", "columns": {}},
+                  "table": "media", "columns": {}, "stall_timeout_s": 30.0},
         # index.js:28 — Prom.expose(); port/host are [inferred] (triton-core not vendored).
         "metrics": {"enabled": True, "host": "0.0.0.0", "port": 3000, "default_metrics": True},
         # index.js:11-13 — pino logger named after the file basename.
@@ -335,6 +336,9 @@ class Config:
             v = st.get(k, 1)
             if isinstance(v, bool) or not isinstance(v, int) or v < 1:
                 raise ConfigError(f"service.store.{k} must be an integer >= 1, got {v!r}")
+        stv = st.get("stall_timeout_s", 30.0)
+        if stv is not None and (isinstance(stv, bool) or not isinstance(stv, (int, float)) or stv <= 0):
+            raise ConfigError(f"service.store.stall_timeout_s must be a number > 0 or null, got {stv!r}")
         try:
             MediaSchema(st.get("table") or "media", st.get("columns") or {})
         except (TypeError, ValueError) as e:

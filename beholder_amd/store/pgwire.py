@@ -353,12 +353,15 @@ class PgConnection(asyncio.Protocol):
                 self.execute = self._net.execute  # native: Parse/Bind/Execute/Sync + IOFuture
         return self
 
-    def abort(self) -> None:
-        """Drop the connection now; outstanding queries fail with PgProtocolError."""
+    def abort(self, reason: Optional[str] = None) -> None:
+        """Drop the connection now; outstanding queries fail with PgProtocolError (``reason``:
+        its text, default "connection lost")."""
         if self._net is not None:
             self._net.abort()
-            self._net_lost(None)
+            self._net_lost(reason)
         elif self._transport is not None:
+            if reason:
+                self._fail_all(PgProtocolError(reason))
             self._transport.abort()
 
     # -- NetConn callbacks (rare paths) ----------------------------------------
@@ -366,7 +369,8 @@ class PgConnection(asyncio.Protocol):
         self.closed = True
         if self._startup is not None:
             self._startup.put_nowait(_LOST)
-        self._net.fail_all(PgProtocolError(f"connection lost: {exc}" if exc else "connection lost"))
+        text = exc if isinstance(exc, str) else (f"connection lost: {exc}" if exc else "connection lost")
+        self._net.fail_all(PgProtocolError(text))
 
     def _net_error(self, exc) -> None:
         self.closed = True
@@ -555,10 +559,16 @@ class Pool:
 
     GROW_RETRY_S = 1.0
 
-    def __init__(self, dsn: str, size: int = 4, spread_at: int = 8):
+    def __init__(self, dsn: str, size: int = 4, spread_at: int = 8, stall_timeout_s: Optional[float] = 30.0):
         self.dsn = dsn
         self.size = max(1, int(size))
         self.spread_at = spread_at
+        # a connection with queries in flight and no reply for this long is dropped (its queries
+        # fail): a half-open TCP connection (peer gone without a FIN or RST) would otherwise hold
+        # every query sent on it, and their handlers, forever. None = off.
+        self.stall_timeout_s = stall_timeout_s
+        self._watchdog: Optional[asyncio.Task] = None
+        self.stalls = 0
         self._conns: List[PgConnection] = []
         self._lock = asyncio.Lock()
         self._growing: Optional[asyncio.Future] = None
@@ -572,7 +582,32 @@ class Pool:
 
     async def open(self) -> "Pool":
         self._conns.append(await PgConnection(self.dsn).connect())  # fail fast on bad DSN/credentials
+        if self.stall_timeout_s:
+            self._watchdog = asyncio.get_running_loop().create_task(self._watch_stalls())
         return self
+
+    async def _watch_stalls(self) -> None:
+        """Drops a connection whose replies stopped while queries are in flight: progress is the
+        reader's count of answered Sync groups, checked every quarter timeout."""
+        timeout = float(self.stall_timeout_s)
+        seen: Dict[int, Tuple[int, float]] = {}  # id(conn) -> (answered, since)
+        loop = asyncio.get_running_loop()
+        while not self._closed:
+            await asyncio.sleep(min(1.0, timeout / 4))
+            now = loop.time()
+            live = {}
+            for c in list(self._conns):
+                if c.closed or not c.pending:
+                    continue
+                answered = c._reader.results
+                prev = seen.get(id(c))
+                since = prev[1] if prev is not None and prev[0] == answered else now
+                live[id(c)] = (answered, since)
+                if now - since >= timeout:
+                    self.stalls += 1
+                    c.abort(f"no reply from Postgres for {timeout:g} s with {c.pending} queries in flight")
+                    live.pop(id(c))
+            seen = live
 
     def execute(self, sql: str, params: Sequence[Any] = ()):
         """Awaitable ``(rows, command_tag)`` (a future on the fast path)."""
@@ -640,6 +675,9 @@ class Pool:
 
     async def close(self) -> None:
         self._closed = True
+        if self._watchdog is not None:
+            self._watchdog.cancel()
+            self._watchdog = None
         g = self._growing
         if g is not None:
             g.cancel()

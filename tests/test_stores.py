@@ -649,3 +649,49 @@ def test_server_closing_right_after_startup_is_a_failed_connect(native_io, monke
         finally:
             srv.close()
     assert run(go()) in ("connect failed", "query failed")
+
+
+@pytest.mark.parametrize("native_io", ["1", "0"])
+def test_pool_drops_a_connection_whose_replies_stopped(native_io, monkeypatch):
+    """A server that stops answering (a half-open TCP connection: the peer vanished without a
+    FIN or RST) must not hold queries -- and the handlers awaiting them -- forever: after
+    ``stall_timeout_s`` without a reply the pool drops the connection and the queries fail."""
+    import struct
+
+    from beholder_amd.store.pgwire import Pool
+
+    monkeypatch.setenv("BEHOLDER_NATIVE_IO", native_io)
+
+    async def serve(reader, writer):
+        n = int.from_bytes(await reader.readexactly(4), "big")
+        await reader.readexactly(n - 4)
+        writer.write(b"R" + struct.pack("!II", 8, 0) + b"Z" + struct.pack("!I", 5) + b"I")
+        await writer.drain()
+        await reader.read()  # reads the queries, never answers
+
+    async def go():
+        srv = await asyncio.start_server(serve, "127.0.0.1", 0)
+        port = srv.sockets[0].getsockname()[1]
+        try:
+            pool = await Pool(f"postgres://u@127.0.0.1:{port}/db?sslmode=disable", size=1,
+                              stall_timeout_s=0.3).open()
+            t0 = asyncio.get_running_loop().time()
+            with pytest.raises(PgProtocolError, match="no reply from Postgres for 0.3 s"):
+                await asyncio.wait_for(pool.execute("SELECT 1"), 5)
+            took = asyncio.get_running_loop().time() - t0
+            stalls = pool.stalls
+            await pool.close()
+            return took, stalls
+        finally:
+            srv.close()
+    took, stalls = run(go())
+    assert stalls == 1 and 0.3 <= took < 1.5
+
+
+def test_stall_timeout_config():
+    from beholder_amd.config import ConfigError
+    from helpers import cfg
+    assert cfg().data["service"]["store"]["stall_timeout_s"] == 30.0
+    cfg({"service": {"store": {"stall_timeout_s": None}}})  # off
+    with pytest.raises(ConfigError, match="stall_timeout_s"):
+        cfg({"service": {"store": {"stall_timeout_s": 0}}})
