@@ -45,6 +45,7 @@ from .sinks.ratelimit import from_config as sink_policy
 from .store import MediaStore, open_store
 from .transport.base import Source
 from .ops import Driver, Window, dispatch_batch
+from .utils.fdtable import reserve_fd_table
 from .utils.log import Logger
 from .utils.tracing import extract as extract_trace_context, tracer_from_config
 
@@ -152,6 +153,9 @@ class Service:
         cfg = self.config
         svc = cfg.data["service"]
         keys = cfg.root.require("keys.trello")
+        # descriptor table sized now: a grow later blocks the loop thread for an RCU grace period
+        # (140-160 ms on the box) in the socket() of a sink connect (utils/fdtable.py)
+        reserve_fd_table(max(1024, 4 * int(svc["http"].get("max_per_host", 100)) + 256))
         # 2. Trello client (index.js:25)
         if self._http is None:
             self._http = make_http_client(svc["http"])

@@ -1,0 +1,159 @@
+#!/usr/bin/env python3
+"""Where does a ``tcp_e2e`` / ``tls_e2e`` warm-up tail come from? Diagnostic, not a benchmark.
+
+Runs the production-shaped bench (``beholder_amd.bench.harness._tcp_e2e``) several times in one
+process and, for each run, records:
+
+- event-loop stalls: a task sleeping 1 ms at a time notes every overshoot above ``--lag-ms``
+  (ms since service init, stall length). A stall means the loop thread was busy or blocked.
+- GC pauses (``gc.callbacks``) above 1 ms.
+- cgroup CPU throttling (``/sys/fs/cgroup/cpu.stat``: periods throttled, time throttled) over the
+  run: a CFS quota (the GPU box gives 16 CPUs' worth over 256 hardware threads) stops every
+  thread of the group for the rest of a 100 ms period once the group has used its share.
+- loop callbacks that ran longer than ``--lag-ms`` (which callback a stall sits in), and native
+  connect calls (``netconn_connect``) longer than 1 ms.
+- sink connection dials (``H1Client._dial``): count, median / max duration, and the slowest five
+  with their start times.
+
+A tail with no matching loop stall and no slow dial is time spent waiting on a peer.
+
+    python scripts/diag_warmup.py [--tls] [--reps 3] [--events 30000] > out.jsonl
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import gc
+import json
+import os
+import resource
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from beholder_amd.bench import harness  # noqa: E402
+from beholder_amd import service as service_mod  # noqa: E402
+from beholder_amd.sinks import h1  # noqa: E402
+
+
+def _cgroup_dir() -> str:
+    try:
+        with open("/proc/self/cgroup") as f:
+            rel = next((ln.split(":", 2)[2].strip() for ln in f if ln.startswith("0::")), "/")
+    except OSError:
+        rel = "/"
+    d = "/sys/fs/cgroup" + rel
+    return d if os.path.exists(os.path.join(d, "cpu.stat")) else "/sys/fs/cgroup"
+
+
+def _cpu_stat() -> dict:
+    try:
+        with open(os.path.join(_cgroup_dir(), "cpu.stat")) as f:
+            return {k: int(v) for k, v in (ln.split() for ln in f if ln.strip())}
+    except OSError:
+        return {}
+
+
+def _cpu_max() -> str:
+    try:
+        with open(os.path.join(_cgroup_dir(), "cpu.max")) as f:
+            return f.read().strip()
+    except OSError:
+        return ""
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--tls", action="store_true")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--events", type=int, default=30000)
+    ap.add_argument("--lag-ms", type=float, default=3.0)
+    a = ap.parse_args(argv)
+
+    st: dict = {}
+    orig_init, orig_dial = service_mod.Service.init, h1.H1Client._dial
+
+    async def lag_monitor():
+        prev = time.perf_counter()
+        while True:
+            await asyncio.sleep(0.001)
+            now = time.perf_counter()
+            if (now - prev) * 1e3 > a.lag_ms + 1:
+                st["lags"].append((round((prev - st["t0"]) * 1e3, 1), round((now - prev) * 1e3 - 1, 1)))
+            prev = now
+
+    async def init(self):
+        st["t0"] = time.perf_counter()
+        st["mon"] = asyncio.ensure_future(lag_monitor())
+        return await orig_init(self)
+
+    async def dial(self, o, deadline, infos=None):
+        t = time.perf_counter()
+        try:
+            return await orig_dial(self, o, deadline, infos)
+        finally:
+            st["dials"].append((round((t - st["t0"]) * 1e3, 1), round((time.perf_counter() - t) * 1e3, 2)))
+
+    def gc_cb(phase, info):
+        if phase == "start":
+            st["gc_t"] = time.perf_counter()
+        elif "gc_t" in st:
+            ms = (time.perf_counter() - st["gc_t"]) * 1e3
+            if ms > 1:
+                st["gcs"].append((round((st["gc_t"] - st.get("t0", st["gc_t"])) * 1e3, 1), info.get("generation"),
+                                  round(ms, 2)))
+
+    orig_run, orig_connect = asyncio.events.Handle._run, h1._netconn_connect
+
+    def handle_run(self):  # which loop callback a stall sits in
+        t = time.perf_counter()
+        orig_run(self)
+        ms = (time.perf_counter() - t) * 1e3
+        if ms > a.lag_ms and "t0" in st:
+            cb = self._callback
+            st["slow_cbs"].append((round((t - st["t0"]) * 1e3, 1), round(ms, 1),
+                                   getattr(cb, "__qualname__", None) or repr(cb)[:60]))
+
+    def connect(*args, **kw):
+        t = time.perf_counter()
+        try:
+            return orig_connect(*args, **kw)
+        finally:
+            ms = (time.perf_counter() - t) * 1e3
+            if ms > 1:
+                st["slow_connects"].append((round((t - st["t0"]) * 1e3, 1), round(ms, 2)))
+
+    asyncio.events.Handle._run, h1._netconn_connect = handle_run, connect
+    service_mod.Service.init, h1.H1Client._dial = init, dial
+    gc.callbacks.append(gc_cb)
+    for rep in range(a.reps):
+        st.update(lags=[], dials=[], gcs=[], slow_cbs=[], slow_connects=[])
+        c0, ru0 = _cpu_stat(), resource.getrusage(resource.RUSAGE_SELF)
+        r = harness._tcp_e2e(a.events, http_servers=4, tls=a.tls)
+        c1, ru1 = _cpu_stat(), resource.getrusage(resource.RUSAGE_SELF)
+        st["mon"].cancel()
+        durs = sorted(d for _, d in st["dials"])
+        print(json.dumps({
+            "rep": rep, "tls": a.tls,
+            "eps": round(r.get("ingest_rate_eps") or 0),
+            "warm": {k: round(v) for k, v in r["warmup_handle_latency_us"].items()},
+            "steady_p999": round(r["handle_latency_us"].get("p999", 0)),
+            "loop_stalls_ms": sorted(st["lags"], key=lambda x: -x[1])[:8],
+            "gc_over_1ms": st["gcs"][:8],
+            "slow_callbacks": sorted(st["slow_cbs"], key=lambda x: -x[1])[:6],
+            "slow_native_connects": sorted(st["slow_connects"], key=lambda x: -x[1])[:6],
+            "dials": len(durs),
+            "dial_ms_med": durs[len(durs) // 2] if durs else None,
+            "dial_ms_max": durs[-1] if durs else None,
+            "slow_dials": sorted(st["dials"], key=lambda x: -x[1])[:5],
+            "first_dial_at_ms": min((s for s, _ in st["dials"]), default=None),
+            "cgroup_cpu_max": _cpu_max(),
+            "cgroup_throttled": {k: c1[k] - c0.get(k, 0) for k in c1 if "throttl" in k or k == "nr_periods"},
+            "involuntary_switches": ru1.ru_nivcsw - ru0.ru_nivcsw,
+        }), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
