@@ -50,6 +50,34 @@ def server_ssl_context() -> ssl.SSLContext:
     return ctx
 
 
+def warm_up(server_ctx: ssl.SSLContext) -> None:
+    """One full handshake with ``server_ctx`` over memory BIOs, before READY. OpenSSL 3 fetches
+    and caches its algorithm implementations (key exchange, signature, HKDF, AEAD) on first
+    use, so a fresh process's first handshakes cost a few ms more than later ones. The
+    endpoints this fake stands in for (api.trello.com, api.telegram.org) are long-running
+    servers; without this, each run's fresh fake servers would bill their own cold start to
+    the consumer's warm-up latency."""
+    client_ctx = ssl.create_default_context(cafile=TLS_CERT)
+    c_in, c_out, s_in, s_out = ssl.MemoryBIO(), ssl.MemoryBIO(), ssl.MemoryBIO(), ssl.MemoryBIO()
+    cli = client_ctx.wrap_bio(c_in, c_out, server_hostname="127.0.0.1")
+    srv = server_ctx.wrap_bio(s_in, s_out, server_side=True)
+    done = [False, False]
+    for _ in range(10):
+        for i, (end, out, peer_in) in enumerate(((cli, c_out, s_in), (srv, s_out, c_in))):
+            if not done[i]:
+                try:
+                    end.do_handshake()
+                    done[i] = True
+                except ssl.SSLWantReadError:
+                    pass
+            data = out.read()
+            if data:
+                peer_in.write(data)
+        if all(done):
+            return
+    raise RuntimeError("TLS warm-up handshake did not finish")
+
+
 async def main(port: int, tls: bool = False) -> int:
     loop = asyncio.get_running_loop()
     # proto=IPPROTO_TCP: asyncio sets TCP_NODELAY only on sockets whose proto says TCP (accepted
@@ -60,7 +88,10 @@ async def main(port: int, tls: bool = False) -> int:
     sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
     sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
     sock.bind(("127.0.0.1", port))
-    srv = await loop.create_server(_Proto, sock=sock, backlog=1024, ssl=server_ssl_context() if tls else None)
+    ctx = server_ssl_context() if tls else None
+    if ctx is not None:
+        warm_up(ctx)
+    srv = await loop.create_server(_Proto, sock=sock, backlog=1024, ssl=ctx)
     print(f"READY {sock.getsockname()[1]}", flush=True)
     stop = loop.create_future()
     loop.add_signal_handler(signal.SIGTERM, lambda: stop.done() or stop.set_result(None))

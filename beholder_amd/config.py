@@ -52,8 +52,9 @@ SERVICE_DEFAULTS: dict = {
         # table/columns: triton-core/db's schema is not vendored; defaults are our guess (store/schema.py)
         # spread_at: queries in flight on every open connection before the pool opens another
         # stall_timeout_s: a connection with queries in flight and no reply for this long is dropped
+        # min_connections: opened at startup (null = pool_size), so the first burst is spread at once
         "store": {"backend": "postgres", "dsn": None, "pool_size": 4, "spread_at": 8, "create_schema": False,
-                  "table": "media", "columns": {}, "stall_timeout_s": 30.0},
+                  "table": "media", "columns": {}, "stall_timeout_s": 30.0, "min_connections": None},
         # index.js:28 — Prom.expose(); port/host are [inferred] (triton-core not vendored).
         "metrics": {"enabled": True, "host": "0.0.0.0", "port": 3000, "default_metrics": True},
         # index.js:11-13 — pino logger named after the file basename.
@@ -336,6 +337,9 @@ class Config:
             v = st.get(k, 1)
             if isinstance(v, bool) or not isinstance(v, int) or v < 1:
                 raise ConfigError(f"service.store.{k} must be an integer >= 1, got {v!r}")
+        mc = st.get("min_connections")
+        if mc is not None and (isinstance(mc, bool) or not isinstance(mc, int) or mc < 1):
+            raise ConfigError(f"service.store.min_connections must be an integer >= 1 or null, got {mc!r}")
         stv = st.get("stall_timeout_s", 30.0)
         if stv is not None and (isinstance(stv, bool) or not isinstance(stv, (int, float)) or stv <= 0):
             raise ConfigError(f"service.store.stall_timeout_s must be a number > 0 or null, got {stv!r}")

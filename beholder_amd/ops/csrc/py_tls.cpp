@@ -19,6 +19,7 @@
 // own tickets take its place.
 #include <arpa/inet.h>
 #include <openssl/err.h>
+#include <openssl/evp.h>
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
 
@@ -87,6 +88,71 @@ int on_new_session(SSL* ssl, SSL_SESSION* sess) {
 
 void free_key(void*, void* ptr, CRYPTO_EX_DATA*, int, long, void*) { delete static_cast<std::string*>(ptr); }
 
+// One TLS 1.3 handshake between two in-memory endpoints, once per process, when the first
+// TlsContext is made (service startup). OpenSSL 3 looks up and caches each algorithm
+// implementation (key exchange, ECDSA, HKDF, AES-GCM, certificate decoding) the first time a
+// handshake needs it; without this the first burst of sink connects pays those lookups on the
+// handshake threads (~1 ms each on the box). The certificate is a throwaway P-256 one made here;
+// RSA, which the real sinks' chains may use, gets its lookups warmed without a key (making a
+// 2048-bit key would cost more than it saves).
+void warm_up_once() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    for (const char* alg : {"RSA", "RSA-PSS", "EC", "X25519"}) EVP_KEYMGMT_free(EVP_KEYMGMT_fetch(nullptr, alg, nullptr));
+    for (const char* alg : {"RSA", "ECDSA"}) EVP_SIGNATURE_free(EVP_SIGNATURE_fetch(nullptr, alg, nullptr));
+    EVP_PKEY* key = EVP_EC_gen("P-256");
+    X509* cert = key ? X509_new() : nullptr;
+    SSL_CTX* sctx = cert ? SSL_CTX_new(TLS_server_method()) : nullptr;
+    SSL_CTX* cctx = sctx ? SSL_CTX_new(TLS_client_method()) : nullptr;
+    SSL *cli = nullptr, *srv = nullptr;
+    BIO *bc = nullptr, *bs = nullptr;
+    bool ok = cctx != nullptr;
+    if (ok) {
+      X509_set_version(cert, 2);
+      ASN1_INTEGER_set(X509_get_serialNumber(cert), 1);
+      X509_gmtime_adj(X509_getm_notBefore(cert), -60);
+      X509_gmtime_adj(X509_getm_notAfter(cert), 3600);
+      X509_set_pubkey(cert, key);
+      X509_NAME* name = X509_get_subject_name(cert);
+      X509_NAME_add_entry_by_txt(name, "CN", MBSTRING_ASC, reinterpret_cast<const unsigned char*>("warm-up.invalid"),
+                                 -1, -1, 0);
+      X509_set_issuer_name(cert, name);
+      ok = X509_sign(cert, key, EVP_sha256()) > 0 && SSL_CTX_use_certificate(sctx, cert) == 1 &&
+           SSL_CTX_use_PrivateKey(sctx, key) == 1 && X509_STORE_add_cert(SSL_CTX_get_cert_store(cctx), cert) == 1 &&
+           SSL_CTX_set_cipher_list(cctx, kCiphers) == 1 && BIO_new_bio_pair(&bc, 0, &bs, 0) == 1;
+    }
+    if (ok) {
+      SSL_CTX_set_verify(cctx, SSL_VERIFY_PEER, nullptr);
+      cli = SSL_new(cctx);
+      srv = SSL_new(sctx);
+      ok = cli && srv && SSL_set1_host(cli, "warm-up.invalid") == 1;
+    }
+    if (ok) {
+      SSL_set_bio(cli, bc, bc);  // each SSL owns its end of the pair
+      SSL_set_bio(srv, bs, bs);
+      bc = bs = nullptr;
+      SSL_set_connect_state(cli);
+      SSL_set_accept_state(srv);
+      bool cdone = false, sdone = false;
+      for (int i = 0; i < 16 && !(cdone && sdone); ++i) {
+        if (!cdone) cdone = SSL_do_handshake(cli) == 1;
+        if (!sdone) sdone = SSL_do_handshake(srv) == 1;
+      }
+      char b = 'x';
+      if (cdone && sdone && SSL_write(cli, &b, 1) == 1) (void)SSL_read(srv, &b, 1);  // one AEAD record
+    }
+    SSL_free(cli);
+    SSL_free(srv);
+    BIO_free(bc);
+    BIO_free(bs);
+    SSL_CTX_free(cctx);
+    SSL_CTX_free(sctx);
+    X509_free(cert);
+    EVP_PKEY_free(key);
+    ERR_clear_error();  // best effort: a failure here only means a colder first handshake
+  });
+}
+
 PyObject* tc_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
   static const char* kwlist[] = {"cafile", "capath", "verify", "check_hostname", nullptr};
   const char* cafile = nullptr;
@@ -105,6 +171,7 @@ PyObject* tc_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
     Py_DECREF(s);
     return PyErr_NoMemory();
   }
+  warm_up_once();
   ERR_clear_error();
   SSL_CTX* ctx = SSL_CTX_new(TLS_client_method());
   if (!ctx) {

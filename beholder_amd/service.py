@@ -196,7 +196,8 @@ class Service:
             kw = {"table": st.get("table") or "media", "columns": dict(st.get("columns") or {})}
             if backend in ("postgres", "postgresql", "pg"):
                 kw.update(pool_size=int(st.get("pool_size", 4)), create_schema=bool(st.get("create_schema", False)),
-                          spread_at=int(st.get("spread_at", 8)), stall_timeout_s=st.get("stall_timeout_s", 30.0))
+                          spread_at=int(st.get("spread_at", 8)), stall_timeout_s=st.get("stall_timeout_s", 30.0),
+                          min_connections=st.get("min_connections"))
             self._store = open_store(backend, st.get("dsn"), **kw)
         await self._store.connect()
 

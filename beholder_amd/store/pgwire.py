@@ -559,9 +559,13 @@ class Pool:
 
     GROW_RETRY_S = 1.0
 
-    def __init__(self, dsn: str, size: int = 4, spread_at: int = 8, stall_timeout_s: Optional[float] = 30.0):
+    def __init__(self, dsn: str, size: int = 4, spread_at: int = 8, stall_timeout_s: Optional[float] = 30.0,
+                 min_open: int = 1):
         self.dsn = dsn
         self.size = max(1, int(size))
+        # connections opened by open(): the first burst of queries (prefetch 100 deliveries at
+        # startup) is spread at once instead of queueing on one connection while the pool grows
+        self.min_open = max(1, min(self.size, int(min_open)))
         self.spread_at = spread_at
         # a connection with queries in flight and no reply for this long is dropped (its queries
         # fail): a half-open TCP connection (peer gone without a FIN or RST) would otherwise hold
@@ -582,6 +586,16 @@ class Pool:
 
     async def open(self) -> "Pool":
         self._conns.append(await PgConnection(self.dsn).connect())  # fail fast on bad DSN/credentials
+        if self.min_open > 1:  # the rest together; one that fails is left to the background grow
+            more = await asyncio.gather(*(PgConnection(self.dsn).connect() for _ in range(self.min_open - 1)),
+                                        return_exceptions=True)
+            for c in more:
+                if isinstance(c, BaseException):
+                    if not isinstance(c, (OSError, asyncio.TimeoutError, PgError, PgProtocolError)):
+                        raise c
+                    self.grow_errors += 1
+                else:
+                    self._conns.append(c)
         if self.stall_timeout_s:
             self._watchdog = asyncio.get_running_loop().create_task(self._watch_stalls())
         return self

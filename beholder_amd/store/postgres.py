@@ -35,7 +35,7 @@ class PostgresStore(MediaStore):
 
     def __init__(self, dsn: Optional[str] = None, table: str = "media", pool_size: int = 4,
                  create_schema: bool = False, columns: Optional[Mapping[str, str]] = None, spread_at: int = 8,
-                 stall_timeout_s: Optional[float] = 30.0):
+                 stall_timeout_s: Optional[float] = 30.0, min_connections: Optional[int] = None):
         if dsn is None:
             from ..dynamics import dyn
             dsn = dyn("postgres")
@@ -45,6 +45,8 @@ class PostgresStore(MediaStore):
         self.pool_size = pool_size
         self.spread_at = spread_at  # queries in flight on every connection before the pool grows
         self.stall_timeout_s = stall_timeout_s  # Pool: drop a connection whose replies stopped
+        # opened at connect(); None = pool_size (the startup burst spreads over the whole pool)
+        self.min_connections = pool_size if min_connections is None else min_connections
         self.create_schema = create_schema
         self._pool: Optional[Pool] = None
         # the compiled handlers issue these two texts themselves (py_handlers.cpp pg_execute)
@@ -57,7 +59,8 @@ class PostgresStore(MediaStore):
 
     async def connect(self) -> None:
         if self._pool is None:
-            self._pool = await Pool(self.dsn, self.pool_size, self.spread_at, self.stall_timeout_s).open()
+            self._pool = await Pool(self.dsn, self.pool_size, self.spread_at, self.stall_timeout_s,
+                                    min_open=self.min_connections).open()
             if self.create_schema:
                 await self._pool.execute(self.schema.create_table())
 

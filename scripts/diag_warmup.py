@@ -69,6 +69,9 @@ def main(argv=None) -> int:
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--events", type=int, default=30000)
     ap.add_argument("--lag-ms", type=float, default=3.0)
+    ap.add_argument("--timeline-ms", type=float, default=0.0,
+                    help="print a per-ms timeline of the first N ms after init (settled, requests, "
+                         "connections, connect waits, PG connections, PG queries in flight)")
     a = ap.parse_args(argv)
 
     st: dict = {}
@@ -83,10 +86,34 @@ def main(argv=None) -> int:
                 st["lags"].append((round((prev - st["t0"]) * 1e3, 1), round((now - prev) * 1e3 - 1, 1)))
             prev = now
 
+    async def timeline(svc):
+        """Every ~0.25 ms for the first ``--timeline-ms``: deliveries settled, HTTP requests /
+        connections / requests that waited for a connection, Postgres connections and queries
+        in flight. Printed per millisecond."""
+        from beholder_amd.bench.harness import _settled
+        rows, end = [], st["t0"] + a.timeline_ms / 1e3
+        while time.perf_counter() < end:
+            http, pool = svc._http, getattr(svc._store, "_pool", None)
+            c = http.counts
+            rows.append(((time.perf_counter() - st["t0"]) * 1e3, _settled(svc._source.settler), c["requests"],
+                         c["connections"], c["connect_waits"],
+                         pool.connections if pool else 0,
+                         sum(x.pending for x in pool._conns if not x.closed) if pool else 0))
+            await asyncio.sleep(0.00025)
+        per_ms, last = [], -1
+        for r in rows:
+            if int(r[0]) != last:
+                last = int(r[0])
+                per_ms.append([last] + list(r[1:]))
+        st["timeline"] = per_ms
+
     async def init(self):
         st["t0"] = time.perf_counter()
         st["mon"] = asyncio.ensure_future(lag_monitor())
-        return await orig_init(self)
+        out = await orig_init(self)
+        if a.timeline_ms:
+            st["tl"] = asyncio.ensure_future(timeline(self))
+        return out
 
     async def dial(self, o, deadline, infos=None):
         t = time.perf_counter()
@@ -128,7 +155,7 @@ def main(argv=None) -> int:
     service_mod.Service.init, h1.H1Client._dial = init, dial
     gc.callbacks.append(gc_cb)
     for rep in range(a.reps):
-        st.update(lags=[], dials=[], gcs=[], slow_cbs=[], slow_connects=[])
+        st.update(lags=[], dials=[], gcs=[], slow_cbs=[], slow_connects=[], timeline=None)
         c0, ru0 = _cpu_stat(), resource.getrusage(resource.RUSAGE_SELF)
         r = harness._tcp_e2e(a.events, http_servers=4, tls=a.tls)
         c1, ru1 = _cpu_stat(), resource.getrusage(resource.RUSAGE_SELF)
@@ -151,6 +178,8 @@ def main(argv=None) -> int:
             "cgroup_cpu_max": _cpu_max(),
             "cgroup_throttled": {k: c1[k] - c0.get(k, 0) for k in c1 if "throttl" in k or k == "nr_periods"},
             "involuntary_switches": ru1.ru_nivcsw - ru0.ru_nivcsw,
+            **({"timeline_ms_settled_requests_conns_waits_pgconns_pgpending": st["timeline"]}
+               if st["timeline"] is not None else {}),
         }), flush=True)
     return 0
 

@@ -548,7 +548,7 @@ def test_pool_metrics_render_postgres_connections_and_grows():
         finally:
             await pg.stop()
     m = run(go())
-    assert m['beholder_pool{pool="postgres",field="open"}'] == 1
+    assert m['beholder_pool{pool="postgres",field="open"}'] == 2  # min_connections: the whole pool at startup
     assert m['beholder_pool{pool="postgres",field="grows"}'] == 0
     assert m['beholder_pool{pool="postgres",field="grow_errors"}'] == 0
 
@@ -695,3 +695,37 @@ def test_stall_timeout_config():
     cfg({"service": {"store": {"stall_timeout_s": None}}})  # off
     with pytest.raises(ConfigError, match="stall_timeout_s"):
         cfg({"service": {"store": {"stall_timeout_s": 0}}})
+
+
+def test_pool_opens_min_connections_at_startup_and_tolerates_a_failed_extra():
+    """``min_open``: open() makes that many connections together (the startup burst is spread at
+    once). The first must succeed; a failed extra one is counted and left to the background grow."""
+    from beholder_amd.store.pgwire import Pool, PgConnection
+
+    async def go():
+        pg = await FakePg().start()
+        try:
+            pool = await Pool(pg.dsn, size=4, min_open=3).open()
+            assert pool.connections == 3 and pool.grow_errors == 0
+            await pool.close()
+            real, calls = PgConnection.connect, []
+
+            async def flaky(self):
+                calls.append(1)
+                if len(calls) == 2:
+                    raise OSError("refused")
+                return await real(self)
+            PgConnection.connect = flaky
+            try:
+                pool = await Pool(pg.dsn, size=4, min_open=3).open()
+            finally:
+                PgConnection.connect = real
+            assert pool.connections == 2 and pool.grow_errors == 1
+            rows, _ = await pool.execute("SELECT 1")
+            await pool.close()
+            st = PostgresStore(pg.dsn, pool_size=3)
+            assert st.min_connections == 3
+            assert PostgresStore(pg.dsn, pool_size=3, min_connections=1).min_connections == 1
+        finally:
+            await pg.stop()
+    run(go())
