@@ -69,6 +69,7 @@ def main(argv=None) -> int:
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--events", type=int, default=30000)
     ap.add_argument("--lag-ms", type=float, default=3.0)
+    ap.add_argument("--http-servers", type=int, default=4, help="fake HTTP(S) sink processes")
     ap.add_argument("--timeline-ms", type=float, default=0.0,
                     help="print a per-ms timeline of the first N ms after init (settled, requests, "
                          "connections, connect waits, PG connections, PG queries in flight)")
@@ -157,7 +158,7 @@ def main(argv=None) -> int:
     for rep in range(a.reps):
         st.update(lags=[], dials=[], gcs=[], slow_cbs=[], slow_connects=[], timeline=None)
         c0, ru0 = _cpu_stat(), resource.getrusage(resource.RUSAGE_SELF)
-        r = harness._tcp_e2e(a.events, http_servers=4, tls=a.tls)
+        r = harness._tcp_e2e(a.events, http_servers=a.http_servers, tls=a.tls)
         c1, ru1 = _cpu_stat(), resource.getrusage(resource.RUSAGE_SELF)
         st["mon"].cancel()
         durs = sorted(d for _, d in st["dials"])
