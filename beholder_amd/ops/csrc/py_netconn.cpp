@@ -73,6 +73,7 @@ void tls_count_handshake(SSL* ssl, bool offloaded);
 int netpoll_pause(PyObject* po, int fd);
 std::shared_ptr<HsWake> netpoll_wake(PyObject* po);
 void tls_describe_failure(SSL* ssl, std::string& reason, std::string& message, bool& verify);
+bool tls_warm_handshake();
 
 namespace {
 
@@ -436,6 +437,9 @@ struct HsPool {
 HsPool* g_hs = nullptr;  // process-lifetime (its threads never exit); replaced in a forked child
 
 void hs_worker(HsPool* pool) {
+  // OpenSSL 3 keeps per-thread state (random generators, provider caches) that a thread's first
+  // handshake would build inside the first burst of connects: one in-memory handshake first
+  tls_warm_handshake();
   for (;;) {
     HsJob* j;
     {
@@ -458,20 +462,27 @@ void hs_worker(HsPool* pool) {
 
 void hs_after_fork_child() { g_hs = nullptr; }
 
-bool hs_submit(HsJob* j) {
+// The process's handshake pool with its threads started (on the calling thread, which holds the
+// GIL; the threads never take it). Throws std::bad_alloc / std::system_error.
+HsPool* hs_pool() {
   static bool atfork = (pthread_atfork(nullptr, nullptr, hs_after_fork_child), true);
   (void)atfork;
+  if (!g_hs) g_hs = new HsPool();
+  HsPool* pool = g_hs;
+  unsigned want = std::max(1u, std::min(4u, std::thread::hardware_concurrency() / 4));
+  while (pool->threads < want) {
+    std::thread(hs_worker, pool).detach();
+    ++pool->threads;
+  }
+  return pool;
+}
+
+bool hs_submit(HsJob* j) {
   try {
-    if (!g_hs) g_hs = new HsPool();
-    HsPool* pool = g_hs;
-    unsigned want = std::max(1u, std::min(4u, std::thread::hardware_concurrency() / 4));
+    HsPool* pool = hs_pool();
     {
       std::lock_guard<std::mutex> lock(pool->mu);
       pool->q.push_back(j);
-    }
-    while (pool->threads < want) {  // started lazily, on the loop thread
-      std::thread(hs_worker, pool).detach();
-      ++pool->threads;
     }
     pool->cv.notify_one();
     return true;
@@ -1230,6 +1241,15 @@ PyGetSetDef nc_getset[] = {
     {nullptr, nullptr, nullptr, nullptr, nullptr}};
 
 }  // namespace
+
+// Called when a TlsContext is made (service startup): the threads start and warm up before the
+// first connect needs them. Failure is not an error here; hs_submit tries again.
+void hs_prestart() {
+  try {
+    hs_pool();
+  } catch (const std::exception&) {
+  }
+}
 
 bool is_netconn(PyObject* o) { return Py_TYPE(o) == &NetConnType; }
 

@@ -88,18 +88,22 @@ int on_new_session(SSL* ssl, SSL_SESSION* sess) {
 
 void free_key(void*, void* ptr, CRYPTO_EX_DATA*, int, long, void*) { delete static_cast<std::string*>(ptr); }
 
-// One TLS 1.3 handshake between two in-memory endpoints, once per process, when the first
-// TlsContext is made (service startup). OpenSSL 3 looks up and caches each algorithm
-// implementation (key exchange, ECDSA, HKDF, AES-GCM, certificate decoding) the first time a
-// handshake needs it; without this the first burst of sink connects pays those lookups on the
-// handshake threads (~1 ms each on the box). The certificate is a throwaway P-256 one made here;
-// RSA, which the real sinks' chains may use, gets its lookups warmed without a key (making a
-// 2048-bit key would cost more than it saves).
-void warm_up_once() {
-  static std::once_flag once;
-  std::call_once(once, [] {
-    for (const char* alg : {"RSA", "RSA-PSS", "EC", "X25519"}) EVP_KEYMGMT_free(EVP_KEYMGMT_fetch(nullptr, alg, nullptr));
-    for (const char* alg : {"RSA", "ECDSA"}) EVP_SIGNATURE_free(EVP_SIGNATURE_fetch(nullptr, alg, nullptr));
+}  // namespace
+
+void hs_prestart();
+
+// One TLS 1.3 handshake between two in-memory endpoints. OpenSSL 3 looks up and caches each
+// algorithm implementation (key exchange, ECDSA, HKDF, AES-GCM, certificate decoding) the first
+// time a handshake needs it, and builds per-thread state (random generators) on a thread's
+// first use. Run once on the loop thread when the first TlsContext is made (service startup)
+// and once on each handshake thread as it starts (py_netconn.cpp hs_worker); without it the
+// first burst of sink connects paid 0.6-1.35 ms of client CPU per handshake against 0.15-0.4
+// ms later (box). The certificate is a throwaway P-256 one made here. RSA, which the real
+// sinks' chains may use, gets its lookups warmed without a key (making a 2048-bit key would
+// cost more than it saves). Best effort: false only means a colder first handshake.
+bool tls_warm_handshake() {
+  bool finished = false;
+  {
     EVP_PKEY* key = EVP_EC_gen("P-256");
     X509* cert = key ? X509_new() : nullptr;
     SSL_CTX* sctx = cert ? SSL_CTX_new(TLS_server_method()) : nullptr;
@@ -139,7 +143,7 @@ void warm_up_once() {
         if (!sdone) sdone = SSL_do_handshake(srv) == 1;
       }
       char b = 'x';
-      if (cdone && sdone && SSL_write(cli, &b, 1) == 1) (void)SSL_read(srv, &b, 1);  // one AEAD record
+      finished = cdone && sdone && SSL_write(cli, &b, 1) == 1 && SSL_read(srv, &b, 1) == 1;  // one AEAD record
     }
     SSL_free(cli);
     SSL_free(srv);
@@ -149,7 +153,19 @@ void warm_up_once() {
     SSL_CTX_free(sctx);
     X509_free(cert);
     EVP_PKEY_free(key);
-    ERR_clear_error();  // best effort: a failure here only means a colder first handshake
+  }
+  ERR_clear_error();
+  return finished;
+}
+
+namespace {
+
+void warm_up_once() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    for (const char* alg : {"RSA", "RSA-PSS", "EC", "X25519"}) EVP_KEYMGMT_free(EVP_KEYMGMT_fetch(nullptr, alg, nullptr));
+    for (const char* alg : {"RSA", "ECDSA"}) EVP_SIGNATURE_free(EVP_SIGNATURE_fetch(nullptr, alg, nullptr));
+    tls_warm_handshake();
   });
 }
 
@@ -204,6 +220,7 @@ PyObject* tc_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
   }
   SSL_CTX_set_session_cache_mode(ctx, SSL_SESS_CACHE_CLIENT | SSL_SESS_CACHE_NO_INTERNAL_STORE);
   SSL_CTX_sess_set_new_cb(ctx, on_new_session);
+  hs_prestart();  // the handshake threads start (and warm up) now, not in the first burst
   return reinterpret_cast<PyObject*>(s);
 }
 
