@@ -216,6 +216,12 @@ class Service:
         if svc.get("native_handlers", True):
             impl = native_handlers(self.handlers) or self.handlers
         self.handler_impl = impl
+        if any(u.lower().startswith("https:") for u in self._sink_urls(endpoints)):
+            # HTTPS sinks: the native TLS context (one-time OpenSSL warm-up, handshake threads)
+            # is made now, not by the first connect of the first burst
+            prep = getattr(self._http, "prepare_tls", None)
+            if prep is not None:
+                prep()
         pc = int(svc["http"].get("preconnect") or 0)
         if pc > 0:  # opt-in: sink connections made before the first delivery, not inside it
             await self._preconnect(pc, endpoints)
@@ -243,14 +249,10 @@ class Service:
         self.log.info(f"consuming from {self._source.describe()}; store {self._store.describe()}")
         return self
 
-    async def _preconnect(self, n: int, endpoints) -> None:
-        """``service.http.preconnect``: ``n`` connections to each sink origin the handlers will
-        call (Trello; Telegram and Emby when their DEPLOYED hooks are on), all at once, with
-        startup held for at most ``preconnect_wait_s``. A sink that cannot be reached is warned
-        about, never fatal: the reference only meets it on the first event, and the handlers
-        connect on demand as they always do."""
+    def _sink_urls(self, endpoints) -> List[str]:
+        """The sink URLs the handlers will call: Trello; Telegram and Emby when their DEPLOYED
+        hooks are on."""
         from .sinks.emby import _PATH as emby_path
-        from .sinks.http import redact
         urls = [endpoints["trello"]]
         try:
             tg_on, _, _, emby_on, emby_host, _ = self.handlers._hooks_plan()
@@ -260,6 +262,16 @@ class Service:
                 urls.append(emby_path(emby_host))
         except Exception:  # noqa: BLE001 -- a hook config the handler would reject at its own point
             pass
+        return [str(u) for u in urls]
+
+    async def _preconnect(self, n: int, endpoints) -> None:
+        """``service.http.preconnect``: ``n`` connections to each sink origin the handlers will
+        call (Trello; Telegram and Emby when their DEPLOYED hooks are on), all at once, with
+        startup held for at most ``preconnect_wait_s``. A sink that cannot be reached is warned
+        about, never fatal: the reference only meets it on the first event, and the handlers
+        connect on demand as they always do."""
+        from .sinks.http import redact
+        urls = self._sink_urls(endpoints)
         seen, origins = set(), []
         for u in urls:
             o = str(u).split("/", 3)[:3]

@@ -302,6 +302,16 @@ class H1Client(HttpClient):
             self._ntls = t
         return t or None
 
+    def prepare_tls(self) -> bool:
+        """Make the TLS context now (the service calls this at startup when a sink is HTTPS): the
+        native context's one-time OpenSSL warm-up handshake (~6 ms) and the start of its
+        handshake threads then happen before the first delivery, not inside the first connect.
+        True when the native TLS path will be used."""
+        if self._own_ssl and netconn.enabled():
+            return self._native_tls() is not None
+        self._ssl_context()
+        return False
+
     def _ssl_context(self) -> _ssl.SSLContext:
         if self._ssl is None:
             self._ssl = _ssl.create_default_context()

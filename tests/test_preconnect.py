@@ -224,3 +224,27 @@ def test_preconnected_connections_keep_alive_from_when_consuming_starts():
         return before, s.connections, reused
     before, after, reused = run(go())
     assert before == 2 and after == 2 and reused == 1  # without the touch: dropped, a 3rd connect
+
+
+def test_service_makes_the_tls_context_at_startup_only_for_https_sinks():
+    """HTTPS sinks: the native TLS context (one-time OpenSSL warm-up, handshake threads) is made by
+    ``Service.init``, not by the first connect of the first burst. Plain-HTTP sinks never make one.
+    No connection is opened either way (preconnect stays 0)."""
+    from beholder_amd.utils import netconn
+
+    async def go(scheme):
+        c = cfg({"service": {"endpoints": {"trello": f"{scheme}://127.0.0.1:1", "telegram": f"{scheme}://127.0.0.1:1"}}})
+        http = H1Client(timeout_s=2)
+        svc = _service(c, http)
+        await svc.init()
+        made = http._ntls
+        opened = sum(o.open for o in http._origins.values())
+        await svc.close()
+        await http.close()
+        return made, opened
+    made, opened = run(go("https"))
+    assert opened == 0
+    if netconn.enabled():
+        assert made is not None and made is not False and type(made).__name__ == "TlsContext"
+    made, opened = run(go("http"))
+    assert made is None and opened == 0
