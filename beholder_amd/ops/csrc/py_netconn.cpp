@@ -469,6 +469,9 @@ HsPool* hs_pool() {
   (void)atfork;
   if (!g_hs) g_hs = new HsPool();
   HsPool* pool = g_hs;
+  // 4: on the box's 16-CPU share, 8 threads (one per admitted connect) made the first burst
+  // slower, not faster: they compete with the loop and the peers for the same CPUs
+  // (interleaved A/B, profiles/box_r3_warmup/threads/)
   unsigned want = std::max(1u, std::min(4u, std::thread::hardware_concurrency() / 4));
   while (pool->threads < want) {
     std::thread(hs_worker, pool).detach();
