@@ -70,6 +70,8 @@ def main(argv=None) -> int:
     ap.add_argument("--events", type=int, default=30000)
     ap.add_argument("--lag-ms", type=float, default=3.0)
     ap.add_argument("--http-servers", type=int, default=4, help="fake HTTP(S) sink processes")
+    ap.add_argument("--connect-on-start", type=int, default=0,
+                    help="experiment: start N background sink connects (not awaited) when consuming starts")
     ap.add_argument("--timeline-ms", type=float, default=0.0,
                     help="print a per-ms timeline of the first N ms after init (settled, requests, "
                          "connections, connect waits, PG connections, PG queries in flight)")
@@ -112,6 +114,9 @@ def main(argv=None) -> int:
         st["t0"] = time.perf_counter()
         st["mon"] = asyncio.ensure_future(lag_monitor())
         out = await orig_init(self)
+        if a.connect_on_start:
+            url = self.config.data["service"]["endpoints"]["trello"]
+            st["pre"] = asyncio.ensure_future(self._http.preconnect(url, a.connect_on_start))
         if a.timeline_ms:
             st["tl"] = asyncio.ensure_future(timeline(self))
         return out
