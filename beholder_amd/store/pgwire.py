@@ -589,13 +589,19 @@ class Pool:
         if self.min_open > 1:  # the rest together; one that fails is left to the background grow
             more = await asyncio.gather(*(PgConnection(self.dsn).connect() for _ in range(self.min_open - 1)),
                                         return_exceptions=True)
+            fatal = None
             for c in more:
-                if isinstance(c, BaseException):
-                    if not isinstance(c, (OSError, asyncio.TimeoutError, PgError, PgProtocolError)):
-                        raise c
-                    self.grow_errors += 1
-                else:
+                if not isinstance(c, BaseException):
                     self._conns.append(c)
+                elif isinstance(c, (OSError, asyncio.TimeoutError, PgError, PgProtocolError)):
+                    self.grow_errors += 1
+                elif fatal is None:
+                    fatal = c
+            if fatal is not None:  # nothing is handed out: close what opened, then fail
+                for c in self._conns:
+                    await c.close()
+                self._conns = []
+                raise fatal
         if self.stall_timeout_s:
             self._watchdog = asyncio.get_running_loop().create_task(self._watch_stalls())
         return self
