@@ -512,3 +512,26 @@ def test_handshakes_run_on_handshake_threads_and_abort_cleanly():
     assert all(r.status == 200 for r in rs)
     assert st["handshakes"] >= 2 and st["offloaded"] == st["handshakes"]
     assert left == 0
+
+
+def test_first_tls_context_starts_warm_handshake_threads_and_a_warm_up_handshake():
+    """Making the first TlsContext starts the handshake threads (each runs one in-memory warm-up
+    handshake before taking jobs) and runs the process's one-time warm-up handshake, so the
+    first burst of connects pays neither. Fresh process: the pool is process-wide."""
+    import sys
+    code = (
+        "import os, time\n"
+        "from beholder_amd.ops import _native\n"
+        "before = len(os.listdir('/proc/self/task'))\n"
+        f"ctx = _native.TlsContext(cafile={TLS_CERT!r})\n"
+        "time.sleep(0.3)\n"
+        "after = len(os.listdir('/proc/self/task'))\n"
+        f"_native.TlsContext(cafile={TLS_CERT!r})\n"
+        "again = len(os.listdir('/proc/self/task'))\n"
+        "want = max(1, min(4, os.cpu_count() // 4))\n"
+        "print(before, after, again, want)\n")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert out.returncode == 0, out.stderr
+    before, after, again, want = map(int, out.stdout.split())
+    assert after - before == want and again == after  # one pool per process
