@@ -177,6 +177,8 @@ def main(argv=None) -> int:
             "slow_callbacks": sorted(st["slow_cbs"], key=lambda x: -x[1])[:6],
             "slow_native_connects": sorted(st["slow_connects"], key=lambda x: -x[1])[:6],
             "dials": len(durs),
+            "tls_handshakes": (r.get("http") or {}).get("tls_handshakes"),
+            "tls_resumed": (r.get("http") or {}).get("tls_resumed"),
             "dial_ms_med": durs[len(durs) // 2] if durs else None,
             "dial_ms_max": durs[-1] if durs else None,
             "slow_dials": sorted(st["dials"], key=lambda x: -x[1])[:5],
