@@ -76,6 +76,10 @@ void poller_close(PollerObject* p) {
   }
   ::close(p->epfd);
   p->epfd = -1;
+  // the channel's eventfd goes with the epoll set, not when the GC gets to this object (it sits
+  // in a cycle with its bound _run / _flush): every socket has left, so no handshake thread will
+  // post here again (a job whose connection closed meanwhile is orphaned and never posts)
+  if (p->wake) p->wake->reset();
   PyErr_Restore(et, ev, tb);
 }
 

@@ -535,3 +535,54 @@ def test_first_tls_context_starts_warm_handshake_threads_and_a_warm_up_handshake
     assert out.returncode == 0, out.stderr
     before, after, again, want = map(int, out.stdout.split())
     assert after - before == want and again == after  # one pool per process
+
+
+def test_tls_connection_churn_leaks_no_descriptors_or_threads():
+    """Many clients each open a burst of HTTPS connections (handshakes on the handshake threads,
+    completions through the poller's channel), use them and close; servers that drop the
+    connection (``once``, after a reply, when the client asks) add closes on both sides. Afterwards this process holds the same descriptors
+    and threads as after the first round: nothing accumulates per connection."""
+    import psutil
+
+    def fds():  # this process's descriptors, less the test servers' own accepted sockets
+        server_side = sum(1 for k in psutil.Process().net_connections(kind="tcp")
+                          if k.laddr and k.laddr.port in ports and k.raddr)
+        return len(os.listdir("/proc/self/fd")) - server_side
+
+    ports = set()
+
+    def tasks():
+        return len(os.listdir("/proc/self/task"))
+
+    async def go():
+        keep = await TlsServer(lambda t: ok()).start()
+        once = await TlsServer(lambda t: ok(b"{}") if not t.endswith("/bye") else None).start()
+        ports.update((keep.port, once.port))
+
+        async def cycle():
+            c = H1Client(timeout_s=5, ssl_cafile=TLS_CERT)
+            urls = [f"https://127.0.0.1:{keep.port}/a", f"https://127.0.0.1:{once.port}/b"]
+            rs = await asyncio.gather(*[c.request("GET", urls[i % 2]) for i in range(24)])
+            for _ in range(200):
+                if not c._dials:
+                    break
+                await asyncio.sleep(0.005)
+            await c.close()
+            return all(r.status == 200 for r in rs)
+
+        assert await cycle()
+        await asyncio.sleep(0.05)
+        base_fds, base_tasks = fds(), tasks()
+        for _ in range(15):
+            assert await cycle()
+        for _ in range(100):
+            await asyncio.sleep(0.01)
+            if fds() <= base_fds:
+                break
+        out = fds(), tasks(), base_fds, base_tasks
+        await keep.stop()
+        await once.stop()
+        return out
+    now_fds, now_tasks, base_fds, base_tasks = run(go())
+    assert now_fds <= base_fds + 2, (now_fds, base_fds)
+    assert now_tasks == base_tasks, (now_tasks, base_tasks)
