@@ -494,8 +494,8 @@ def main(argv=None) -> int:
                      "rate_1k/rate_10k/rate_100k/soak = BASELINE configs 2-5 (rate_100k paced into a 4096-event "
                      "drop_newest ring; burst = the same ring fed unpaced); tcp_e2e/http_tcp = every dependency "
                      "over TCP, tls_e2e = same with HTTPS sinks; tcp_e2e/tls_e2e latencies are receive->ack at "
-                     "saturation with prefetch 100 in flight (queueing included), warmup_* = the first "
-                     "deliveries while sink/DB connections open",
+                     "saturation with prefetch 100 in flight (queueing included), warmup_* = the first 5,000 "
+                     "deliveries (connection pools filling from zero; http.preconnect 0)",
         }
         print(json.dumps(out), flush=True)
     dist.close()
