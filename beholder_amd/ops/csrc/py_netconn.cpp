@@ -456,7 +456,7 @@ void hs_worker(HsPool* pool) {
       delete j;
       continue;
     }
-    wake->post(j);  // the loop thread owns the job from here
+    if (!wake->post(j)) delete j;  // posted: the loop thread owns the job from here
   }
 }
 

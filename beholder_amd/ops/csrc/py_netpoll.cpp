@@ -62,7 +62,11 @@ void poller_close(PollerObject* p) {
   if (p->epfd < 0) return;
   PyObject *et, *ev, *tb;
   PyErr_Fetch(&et, &ev, &tb);
-  drain_wake(p);  // finished handshakes of connections that have left (their jobs are dropped)
+  if (p->wake && *p->wake) {  // finished handshakes of connections that have left: dropped
+    std::deque<void*> jobs;
+    (*p->wake)->close(jobs);
+    for (void* j : jobs) netconn_tls_done(j);
+  }
   if (p->loop) {
     PyObject* fdo = PyLong_FromLong(p->epfd);
     PyObject* r = fdo ? PyObject_CallMethodOneArg(p->loop, s_remove_reader_p, fdo) : nullptr;
@@ -77,8 +81,8 @@ void poller_close(PollerObject* p) {
   ::close(p->epfd);
   p->epfd = -1;
   // the channel's eventfd goes with the epoll set, not when the GC gets to this object (it sits
-  // in a cycle with its bound _run / _flush): every socket has left, so no handshake thread will
-  // post here again (a job whose connection closed meanwhile is orphaned and never posts)
+  // in a cycle with its bound _run / _flush); a handshake thread still holding it finds it
+  // closed and frees its job itself
   if (p->wake) p->wake->reset();
   PyErr_Restore(et, ev, tb);
 }
@@ -127,6 +131,11 @@ int poller_clear(PollerObject* p) {
 void poller_dealloc(PollerObject* p) {
   PyObject_GC_UnTrack(p);
   drop_all(p);
+  if (p->wake && *p->wake) {  // never closed (collected with its loop): same as poller_close
+    std::deque<void*> jobs;
+    (*p->wake)->close(jobs);
+    for (void* j : jobs) netconn_tls_done(j);
+  }
   if (p->epfd >= 0) {
     ::close(p->epfd);
     p->epfd = -1;
