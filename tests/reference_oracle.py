@@ -178,6 +178,27 @@ def make_scenario(seed: int, n_events: int = 520, mode: str = "base") -> dict:
             "noTrello": mode == "no_trello"}
 
 
+def bench_scenario(n_events: int, seed: int = 0) -> dict:
+    """The bench's own workload (``beholder_amd.bench.generator``: bench config, 10k-media table,
+    90% progress / 10% status stream) as a scenario, so the gate also covers the exact events the
+    throughput numbers are measured on (and the Node A/B, ``scripts/bench_reference_node.py``)."""
+    from beholder_amd.bench.generator import Workload, bench_config
+    w = Workload(n_media=10000, seed=seed)
+    cfg = bench_config()
+    framed = w.framed(n_events)
+    topics = {1: "status", 2: "progress"}
+    events, i = [], 0
+    while i < len(framed):
+        n = int.from_bytes(framed[i:i + 4], "little")
+        events.append([topics[framed[i + 4]], framed[i + 5:i + 4 + n].hex()])
+        i += 4 + n
+    media = [{"id": m.id, "name": m.name, "creator": m.creator, "creatorId": m.creatorId,
+              "metadataId": m.metadataId, "status": m.status} for m in w.media]
+    return {"seed": seed, "mode": "bench", "config": {"keys": cfg["keys"], "instance": cfg["instance"]},
+            "media": media, "events": events, "faults": [], "positionalArgs": "append", "notFound": NOT_FOUND,
+            "logLevel": "info", "noTrello": False}
+
+
 # ------------------------------------------------------------------------------------- runners ---
 def run_node(sc: dict, timeout: float = 120.0) -> dict:
     """The reference's own index.js on Node, under the stand-ins (oracle.js)."""
