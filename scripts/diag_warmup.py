@@ -74,7 +74,8 @@ def main(argv=None) -> int:
                     help="experiment: start N background sink connects (not awaited) when consuming starts")
     ap.add_argument("--timeline-ms", type=float, default=0.0,
                     help="print a per-ms timeline of the first N ms after init (settled, requests, "
-                         "connections, connect waits, PG connections, PG queries in flight)")
+                         "connections, connect waits, PG connections, PG queries in flight, ms of that "
+                         "millisecond the loop spent in callbacks)")
     a = ap.parse_args(argv)
 
     st: dict = {}
@@ -104,16 +105,18 @@ def main(argv=None) -> int:
                          sum(x.pending for x in pool._conns if not x.closed) if pool else 0))
             await asyncio.sleep(0.00025)
         per_ms, last = [], -1
+        busy = st.get("busy", {})
         for r in rows:
             if int(r[0]) != last:
                 last = int(r[0])
-                per_ms.append([last] + list(r[1:]))
+                per_ms.append([last] + list(r[1:]) + [round(busy.get(last, 0.0), 2)])
         st["timeline"] = per_ms
 
     async def init(self):
         st["t0"] = time.perf_counter()
         st["mon"] = asyncio.ensure_future(lag_monitor())
         out = await orig_init(self)
+        st["t_run"] = time.perf_counter()
         if a.connect_on_start:
             url = self.config.data["service"]["endpoints"]["trello"]
             st["pre"] = asyncio.ensure_future(self._http.preconnect(url, a.connect_on_start))
@@ -139,10 +142,27 @@ def main(argv=None) -> int:
 
     orig_run, orig_connect = asyncio.events.Handle._run, h1._netconn_connect
 
-    def handle_run(self):  # which loop callback a stall sits in
+    def handle_run(self):  # which loop callback a stall sits in; loop busy time per ms
         t = time.perf_counter()
         orig_run(self)
-        ms = (time.perf_counter() - t) * 1e3
+        t1 = time.perf_counter()
+        ms = (t1 - t) * 1e3
+        if "t0" in st and a.timeline_ms:
+            b = int((t - st["t0"]) * 1e3)
+            if b < a.timeline_ms:
+                busy = st.setdefault("busy", {})
+                busy[b] = busy.get(b, 0.0) + ms
+                cb = self._callback
+                name = getattr(cb, "__qualname__", None) or type(cb).__name__
+                if name in ("TaskStepMethWrapper", "TaskWakeupMethWrapper", "Task.task_wakeup"):
+                    try:
+                        name = "task:" + cb.__self__.get_coro().__qualname__
+                    except AttributeError:
+                        pass
+                if t < st.get("t_run", float("inf")):  # Service.init itself is not the burst
+                    return
+                by = st.setdefault("busy_by", {})
+                by[name] = by.get(name, 0.0) + ms
         if ms > a.lag_ms and "t0" in st:
             cb = self._callback
             st["slow_cbs"].append((round((t - st["t0"]) * 1e3, 1), round(ms, 1),
@@ -161,7 +181,8 @@ def main(argv=None) -> int:
     service_mod.Service.init, h1.H1Client._dial = init, dial
     gc.callbacks.append(gc_cb)
     for rep in range(a.reps):
-        st.update(lags=[], dials=[], gcs=[], slow_cbs=[], slow_connects=[], timeline=None)
+        st.pop("t_run", None)
+        st.update(lags=[], dials=[], gcs=[], slow_cbs=[], slow_connects=[], timeline=None, busy={}, busy_by={})
         c0, ru0 = _cpu_stat(), resource.getrusage(resource.RUSAGE_SELF)
         r = harness._tcp_e2e(a.events, http_servers=a.http_servers, tls=a.tls)
         c1, ru1 = _cpu_stat(), resource.getrusage(resource.RUSAGE_SELF)
@@ -186,7 +207,9 @@ def main(argv=None) -> int:
             "cgroup_cpu_max": _cpu_max(),
             "cgroup_throttled": {k: c1[k] - c0.get(k, 0) for k in c1 if "throttl" in k or k == "nr_periods"},
             "involuntary_switches": ru1.ru_nivcsw - ru0.ru_nivcsw,
-            **({"timeline_ms_settled_requests_conns_waits_pgconns_pgpending": st["timeline"]}
+            **({"timeline_ms_settled_requests_conns_waits_pgconns_pgpending_loopbusyms": st["timeline"],
+                "timeline_loop_ms_by_callback": sorted(((k, round(v, 2)) for k, v in st["busy_by"].items()),
+                                                       key=lambda kv: -kv[1])[:12]}
                if st["timeline"] is not None else {}),
         }), flush=True)
     return 0
