@@ -99,12 +99,13 @@ struct State {
   Slots conn, origin, resp;
   PyTypeObject* client_type = nullptr;
   PyObject* base_time = nullptr;  // asyncio.BaseEventLoop.time (time.monotonic())
+  PyObject* get_running_loop = nullptr;  // asyncio.get_running_loop
   bool ready = false;
 } g;
 
 PyObject *s_closed_attr, *s_origins, *s_counts, *s_keepalive_s, *s_timeout_s, *s_busy, *s_sweeper, *s_tail,
     *s_tail_cl0, *s_requests, *s_reused, *s_drop, *s_release, *s_arm, *s_resume, *s_time, *s_pop, *s_append,
-    *s_buffered, *s_throw, *s_close, *s_request_py;
+    *s_buffered, *s_throw, *s_close, *s_request_py, *s_cancel, *s_enqueue, *s_after_queue, *s_exception_name;
 
 double mono_s() {
   timespec ts;
@@ -120,6 +121,12 @@ bool is_body_method(const char* m, Py_ssize_t n) {
 bool is_get_or_head(const char* m, Py_ssize_t n) {
   return (n == 3 && memcmp(m, "GET", 3) == 0) || (n == 4 && memcmp(m, "HEAD", 4) == 0);
 }
+
+// owns one reference until destroyed (p = nullptr hands it on)
+struct Own {
+  PyObject* p;
+  ~Own() { Py_XDECREF(p); }
+};
 
 // dict[key] += 1 (int counters of H1Client.counts)
 int bump(PyObject* d, PyObject* key) {
@@ -141,7 +148,9 @@ int bump(PyObject* d, PyObject* key) {
 // ST_INIT: created, nothing done yet (like a coroutine before its first send: the request is
 // prepared and sent when the call is first awaited, so ordering under gather() and an
 // H1Call that is never awaited behave as H1Client._request would)
-enum : uint8_t { ST_WAIT = 0, ST_DELEGATE = 1, ST_DONE = 2, ST_INIT = 3 };
+// ST_QUEUED: no idle connection at the first await; the call waits in the origin's queue
+// (H1Client._enqueue) for one, then sends natively as from the idle pool
+enum : uint8_t { ST_WAIT = 0, ST_DELEGATE = 1, ST_DONE = 2, ST_INIT = 3, ST_QUEUED = 4 };
 
 struct H1CallObject {
   PyObject_HEAD PyObject* client;
@@ -153,9 +162,12 @@ struct H1CallObject {
   PyObject* params;   // ST_INIT: the call's params (or NULL)
   PyObject* timeout;  // ST_INIT: the call's timeout (or NULL)
   PyObject* sub;  // the Python continuation (H1Client._resume / _request) once delegated
+  PyObject* timer;  // ST_QUEUED: the queue deadline's TimerHandle
+  PyObject* req;    // ST_QUEUED: the request bytes, sent once a connection is handed over
   uint8_t state;
   uint8_t reused;  // the connection had served a request before (h1.py `reused`)
   uint8_t path;    // 0 not started, 1 sent natively, 2 delegated to H1Client._request
+  uint8_t head;    // ST_QUEUED: a HEAD request
 };
 
 PyTypeObject H1CallType = {PyVarObject_HEAD_INIT(nullptr, 0)};
@@ -170,6 +182,8 @@ int call_traverse(H1CallObject* s, visitproc visit, void* arg) {
   Py_VISIT(s->params);
   Py_VISIT(s->timeout);
   Py_VISIT(s->sub);
+  Py_VISIT(s->timer);
+  Py_VISIT(s->req);
   return 0;
 }
 
@@ -183,6 +197,8 @@ int call_clear(H1CallObject* s) {
   Py_CLEAR(s->params);
   Py_CLEAR(s->timeout);
   Py_CLEAR(s->sub);
+  Py_CLEAR(s->timer);
+  Py_CLEAR(s->req);
   return 0;
 }
 
@@ -210,8 +226,45 @@ void abandon(H1CallObject* s) {
   PyErr_Restore(et, ev, tb);
 }
 
+// ST_QUEUED, leaving without sending: the deadline timer is cancelled; a connection handed over
+// meanwhile goes back to the pool (h1.py _acquire's CancelledError path); a waiter still in the
+// queue is cancelled, so _release / _wake pass over it. Errors are reported, not raised.
+void leave_queue(H1CallObject* s) {
+  PyObject *et, *ev, *tb;
+  PyErr_Fetch(&et, &ev, &tb);
+  if (s->timer) {
+    PyObject* r = PyObject_CallMethodNoArgs(s->timer, s_cancel);
+    if (!r)
+      PyErr_WriteUnraisable(s->timer);
+    else
+      Py_DECREF(r);
+    Py_CLEAR(s->timer);
+  }
+  if (s->fut) {
+    PyObject* res = nullptr;
+    int st = iofuture_peek(s->fut, &res);
+    if (st == 0) {
+      PyObject* r = PyObject_CallMethodNoArgs(s->fut, s_cancel);
+      if (!r)
+        PyErr_WriteUnraisable(s->fut);
+      else
+        Py_DECREF(r);
+    } else if (st == 1 && res && Py_TYPE(res) == g.conn.type && s->client) {
+      PyObject* r = PyObject_CallMethodObjArgs(s->client, s_release, res, Py_True, nullptr);
+      if (!r)
+        PyErr_WriteUnraisable(s->client);
+      else
+        Py_DECREF(r);
+    }
+  }
+  PyErr_Restore(et, ev, tb);
+}
+
 void call_finalize(H1CallObject* s) {
-  if (s->state == ST_WAIT) {  // never awaited to the end: like a closed coroutine
+  if (s->state == ST_QUEUED) {
+    s->state = ST_DONE;
+    leave_queue(s);
+  } else if (s->state == ST_WAIT) {  // never awaited to the end: like a closed coroutine
     s->state = ST_DONE;
     abandon(s);
   } else if (s->state == ST_DELEGATE && s->sub) {
@@ -338,6 +391,7 @@ int start_delegate(H1CallObject* s, PyObject* thrown) {
 }
 
 int h1_start(H1CallObject* s);
+int queue_resume(H1CallObject* s);
 
 // The fast path declined at the first await: the whole request is H1Client._request's.
 int start_python(H1CallObject* s) {
@@ -379,7 +433,7 @@ PySendResult call_am_send(H1CallObject* s, PyObject* arg, PyObject** out) {
       *out = nullptr;
       return PYGEN_ERROR;
     }
-    s->path = uint8_t(k == 1 ? 1 : 2);
+    s->path = uint8_t(k == 0 ? 2 : 1);
     if (k == 0) {
       if (start_python(s) < 0) {
         *out = nullptr;
@@ -387,7 +441,30 @@ PySendResult call_am_send(H1CallObject* s, PyObject* arg, PyObject** out) {
       }
       return delegate_send(s, Py_None, out);
     }
-    s->state = ST_WAIT;
+  }
+  if (s->state == ST_QUEUED) {
+    PyObject* w = nullptr;
+    if (iofuture_peek(s->fut, &w) == 0) {
+      *out = iofuture_yield(s->fut);
+      return *out ? PYGEN_NEXT : PYGEN_ERROR;
+    }
+    int rc;
+    try {
+      rc = queue_resume(s);
+    } catch (const std::bad_alloc&) {
+      PyErr_NoMemory();
+      rc = -1;
+    }
+    if (rc < 0) {
+      if (s->state == ST_QUEUED) leave_queue(s);
+      s->state = ST_DONE;
+      *out = nullptr;
+      return PYGEN_ERROR;
+    }
+    if (s->state == ST_DELEGATE) {
+      s->path = 2;
+      return delegate_send(s, Py_None, out);
+    }
   }
   PyObject* res = nullptr;
   int st = iofuture_peek(s->fut, &res);
@@ -470,6 +547,33 @@ PyObject* call_throw(H1CallObject* s, PyObject* args) {
     return nullptr;
   }
   if (s->state == ST_INIT) s->state = ST_DONE;  // like throw() into an unstarted coroutine
+  if (s->state == ST_QUEUED) {
+    // a Task throws the waiter's own exception in (its deadline, a failed connect, the client
+    // closing): the request continues as when resumed. Anything else (a cancel, a wrapper's
+    // timeout) leaves the queue and propagates, as from _acquire's await.
+    bool own = false;
+    PyObject* res = nullptr;
+    if (iofuture_peek(s->fut, &res) == 2) {
+      PyObject* e = PyObject_CallMethodNoArgs(s->fut, s_exception_name);
+      if (!e) PyErr_Clear();  // cancelled
+      own = e && e == exc;
+      Py_XDECREF(e);
+    }
+    if (own) {
+      Py_DECREF(exc);
+      int rc = queue_resume(s);
+      if (rc < 0) {
+        if (s->state == ST_QUEUED) leave_queue(s);
+        s->state = ST_DONE;
+        return nullptr;
+      }
+      PyObject* out = nullptr;
+      PySendResult r = PyIter_Send(reinterpret_cast<PyObject*>(s), Py_None, &out);  // ST_DELEGATE or ST_WAIT
+      return call_result(r, out);
+    }
+    s->state = ST_DONE;
+    leave_queue(s);
+  }
   if (s->state == ST_WAIT) {  // the request loop's except clauses see it at the await (h1.py _exchange)
     int rc = start_delegate(s, exc);
     Py_DECREF(exc);
@@ -495,6 +599,9 @@ PyObject* call_close(H1CallObject* s, PyObject*) {
   if (s->state == ST_WAIT) {
     s->state = ST_DONE;
     abandon(s);
+  } else if (s->state == ST_QUEUED) {
+    s->state = ST_DONE;
+    leave_queue(s);
   }
   s->state = ST_DONE;
   Py_RETURN_NONE;
@@ -526,6 +633,12 @@ PyMethodDef call_methods[] = {
     {nullptr, nullptr, 0, nullptr}};
 
 // ---- h1_fast ----------------------------------------------------------------------------------
+PyObject* make_deadline(PyObject* loop, PyObject* timeout, PyObject* timeout_s);
+int send_on(H1CallObject* s, PyObject* conn, const char* req, size_t reqlen, PyObject* method, PyObject* full,
+            PyObject* deadline, bool head, bool from_idle);
+int queue_start(H1CallObject* s, PyObject* client, PyObject* counts, PyObject* o, PyObject* full,
+                const std::string& req, bool head, PyObject* timeout, PyObject* timeout_s);
+
 // At the first await: send the request on an idle pooled connection. 1 = sent (s->conn, fut,
 // method, full, deadline, reused set), 0 = declined before any pool state changed (the Python
 // path runs instead and reproduces any error at its await), -1 = error.
@@ -632,13 +745,27 @@ int h1_start(H1CallObject* s) {
   PyObject* t = is_body_method(m, mn) ? tail_cl0 : tail;
   req.append(PyBytes_AS_STRING(t), size_t(PyBytes_GET_SIZE(t)));
 
+  bool head = mn == 4 && memcmp(m, "HEAD", 4) == 0;
+  PyObject* full;  // the URL with its query (HttpResponse.url, error text)
+  if (q.empty()) {
+    Py_INCREF(url);
+    full = url;
+  } else {
+    std::string f(u, size_t(un));
+    f += '?';
+    f += q;
+    full = PyUnicode_FromStringAndSize(f.data(), Py_ssize_t(f.size()));
+    if (!full) return -1;
+  }
+  Own own_full{full};
+
   // a live idle keep-alive connection on a NetConn (the Python fast path's idle pop)
   double ka = PyFloat_AS_DOUBLE(keepalive);
   PyObject* conn = nullptr;
   for (;;) {
     Py_ssize_t n = PyObject_Size(idle);
     if (n < 0) return -1;
-    if (n == 0) return 0;  // connect or wait for a slot: Python path
+    if (n == 0) return queue_start(s, client, counts, o, full, req, head, timeout, timeout_s);
     PyObject* cand = PyObject_CallMethodNoArgs(idle, s_pop);
     if (!cand) return -1;
     if (Py_TYPE(cand) != g.conn.type) {
@@ -673,74 +800,62 @@ int h1_start(H1CallObject* s) {
     Py_DECREF(r);
   }
 
-  // committed: the request goes out on `conn`
-  struct Own {
-    PyObject* p;
-    ~Own() { Py_XDECREF(p); }
-  } own_conn{conn};
-  if (bump(counts, s_requests) < 0 || bump(counts, s_reused) < 0) return -1;
-  PyObject* uses = g.conn.get(conn, C_USES);
-  bool reused = true;
-  if (uses) {
-    int pos = PyObject_IsTrue(uses);  // reused = c.uses > 0 (an idle connection has served one)
-    if (pos < 0) return -1;
-    reused = pos != 0;
-    PyObject* one = PyLong_FromLong(1);
-    PyObject* nu = one ? PyNumber_Add(uses, one) : nullptr;
-    Py_XDECREF(one);
-    if (!nu) return -1;
-    g.conn.set(conn, C_USES, nu);
+  // committed: the request goes out on `conn` (send_on owns it from here, and hands it back on
+  // a failure); the connection's loop, as asyncio.get_running_loop() would cost a getpid(2)
+  PyObject* deadline = bump(counts, s_requests) < 0 ? nullptr
+                       : make_deadline(netconn_loop(g.conn.get(conn, C_NET)), timeout, timeout_s);
+  if (!deadline) {
+    PyObject *et, *ev, *tb;
+    PyErr_Fetch(&et, &ev, &tb);
+    PyObject* r = PyObject_CallMethodObjArgs(client, s_release, conn, Py_False, nullptr);
+    Py_DECREF(conn);
+    if (!r)
+      PyErr_WriteUnraisable(client);
+    else
+      Py_DECREF(r);
+    PyErr_Restore(et, ev, tb);
+    return -1;
   }
-  // the connection's loop (asyncio.get_running_loop() would cost a getpid(2) per request)
-  PyObject* loop = netconn_loop(g.conn.get(conn, C_NET));
-  Py_INCREF(loop);
-  Own own_loop{loop};
+  Own own_deadline{deadline};
+  return send_on(s, conn, req.data(), req.size(), method, full, deadline, head, true);
+}
+
+// The queue deadline and request deadlines: loop.time() + (timeout or client.timeout_s). New
+// reference, NULL on error.
+PyObject* make_deadline(PyObject* loop, PyObject* timeout, PyObject* timeout_s) {
   double dl;
   if (g.base_time && _PyType_Lookup(Py_TYPE(loop), s_time) == g.base_time) {
     dl = mono_s();  // BaseEventLoop.time() is time.monotonic()
   } else {
     PyObject* now = PyObject_CallMethodNoArgs(loop, s_time);
-    if (!now) return -1;
+    if (!now) return nullptr;
     dl = PyFloat_AsDouble(now);
     Py_DECREF(now);
-    if (dl == -1.0 && PyErr_Occurred()) return -1;
+    if (dl == -1.0 && PyErr_Occurred()) return nullptr;
   }
   PyObject* tmo = timeout;  // `timeout or self.timeout_s`
   if (tmo) {
     int truth = PyObject_IsTrue(tmo);
-    if (truth < 0) return -1;
+    if (truth < 0) return nullptr;
     if (!truth) tmo = nullptr;
   }
   double add = PyFloat_AsDouble(tmo ? tmo : timeout_s);
-  if (add == -1.0 && PyErr_Occurred()) return -1;
-  PyObject* deadline = PyFloat_FromDouble(dl + add);
-  if (!deadline) return -1;
-  Own own_deadline{deadline};
-  PyObject* full;
-  if (q.empty()) {
-    Py_INCREF(url);
-    full = url;
-  } else {
-    std::string f(u, size_t(un));
-    f += '?';
-    f += q;
-    full = PyUnicode_FromStringAndSize(f.data(), Py_ssize_t(f.size()));
-    if (!full) return -1;
-  }
-  Own own_full{full};
-  Py_INCREF(method);
-  PyObject* what = PyTuple_Pack(2, method, full);
-  Py_DECREF(method);
-  if (!what) return -1;
-  Py_INCREF(deadline);
-  g.conn.set(conn, C_DEADLINE, deadline);
-  g.conn.set(conn, C_WHAT, what);
-  PyObject* fut = iofuture_new(loop);
-  if (!fut) return -1;
-  Own own_fut{fut};
-  bool head = mn == 4 && memcmp(m, "HEAD", 4) == 0;
-  if (netconn_h1_request(g.conn.get(conn, C_NET), req, fut, head) < 0) {
-    // the connection left the idle pool: give it back to the pool accounting (dropped), then raise
+  if (add == -1.0 && PyErr_Occurred()) return nullptr;
+  return PyFloat_FromDouble(dl + add);
+}
+
+// Sends `req` on the live NetConn connection `conn` (a new reference, consumed) and moves the
+// call to ST_WAIT: the pool bookkeeping of h1.py _exchange (uses, reused, deadline, what, the
+// busy set, the sweeper). `from_idle`: popped from the idle pool (counted reused, as the Python
+// idle pop does); else handed to a queued request (reused when it served one before, as
+// _acquire counts). 1, or -1 with the connection handed back to the pool accounting.
+int send_on(H1CallObject* s, PyObject* conn, const char* req, size_t reqlen, PyObject* method, PyObject* full,
+            PyObject* deadline, bool head, bool from_idle) {
+  Own own_conn{conn};
+  PyObject* client = s->client;
+  // a failure hands the connection back to the pool accounting (dropped, h1.py _release(c,
+  // False)), or its origin would count it open forever
+  auto fail = [client, conn]() {
     PyObject *et, *ev, *tb;
     PyErr_Fetch(&et, &ev, &tb);
     PyObject* r = PyObject_CallMethodObjArgs(client, s_release, conn, Py_False, nullptr);
@@ -750,29 +865,159 @@ int h1_start(H1CallObject* s) {
       Py_DECREF(r);
     PyErr_Restore(et, ev, tb);
     return -1;
+  };
+  PyObject** dp = _PyObject_GetDictPtr(client);
+  PyObject* d = dp ? *dp : nullptr;
+  PyObject* counts = d ? PyDict_GetItemWithError(d, s_counts) : nullptr;
+  PyObject* busy = counts ? PyDict_GetItemWithError(d, s_busy) : nullptr;
+  if (!busy || !PyDict_CheckExact(counts) || !PySet_CheckExact(busy)) {
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_RuntimeError, "H1Client state changed under a request");
+    return fail();
   }
-  if (PySet_Add(busy, conn) < 0) return -1;
+  PyObject* uses = g.conn.get(conn, C_USES);
+  bool reused = true;
+  if (uses) {
+    int pos = PyObject_IsTrue(uses);  // reused = c.uses > 0
+    if (pos < 0) return fail();
+    reused = pos != 0;
+    PyObject* one = PyLong_FromLong(1);
+    PyObject* nu = one ? PyNumber_Add(uses, one) : nullptr;
+    Py_XDECREF(one);
+    if (!nu) return fail();
+    g.conn.set(conn, C_USES, nu);
+  }
+  if ((from_idle || reused) && bump(counts, s_reused) < 0) return fail();
+  PyObject* loop = netconn_loop(g.conn.get(conn, C_NET));
+  Py_INCREF(loop);
+  Own own_loop{loop};
+  Py_INCREF(method);
+  PyObject* what = PyTuple_Pack(2, method, full);
+  Py_DECREF(method);
+  if (!what) return fail();
+  Py_INCREF(deadline);
+  g.conn.set(conn, C_DEADLINE, deadline);
+  g.conn.set(conn, C_WHAT, what);
+  PyObject* fut = iofuture_new(loop);
+  if (!fut) return fail();
+  Own own_fut{fut};
+  if (netconn_h1_request(g.conn.get(conn, C_NET), std::string(req, reqlen), fut, head) < 0) return fail();
+  if (PySet_Add(busy, conn) < 0) return fail();
   PyObject* sweeper = PyDict_GetItemWithError(d, s_sweeper);
-  if (!sweeper && PyErr_Occurred()) return -1;
+  if (!sweeper && PyErr_Occurred()) {
+    PySet_Discard(busy, conn);
+    return fail();
+  }
   if (!sweeper || sweeper == Py_None) {
     PyObject* r = PyObject_CallMethodOneArg(client, s_arm, loop);
-    if (!r) return -1;
+    if (!r) {
+      PySet_Discard(busy, conn);
+      return fail();
+    }
     Py_DECREF(r);
   }
   own_conn.p = nullptr;
-  s->conn = conn;
+  Py_XSETREF(s->conn, conn);
   own_fut.p = nullptr;
-  s->fut = fut;
+  Py_XSETREF(s->fut, fut);
   Py_INCREF(method);
   Py_SETREF(s->method, method);
-  own_full.p = nullptr;
+  Py_INCREF(full);
   Py_SETREF(s->full, full);
-  own_deadline.p = nullptr;
-  s->deadline = deadline;
+  Py_INCREF(deadline);
+  Py_XSETREF(s->deadline, deadline);
   s->reused = reused;
   Py_CLEAR(s->params);
   Py_CLEAR(s->timeout);
+  Py_CLEAR(s->req);
+  s->state = ST_WAIT;
   return 1;
+}
+
+// No idle connection: the request joins the origin's queue (H1Client._enqueue: the same
+// accounting, background connects and deadline as _acquire) with an IOFuture waiter, and the
+// call waits for a connection in ST_QUEUED. 2 = queued, -1 = error.
+int queue_start(H1CallObject* s, PyObject* client, PyObject* counts, PyObject* o, PyObject* full,
+                const std::string& req, bool head, PyObject* timeout, PyObject* timeout_s) {
+  if (!g.get_running_loop) return 0;
+  PyObject* loop = PyObject_CallNoArgs(g.get_running_loop);
+  if (!loop) return -1;
+  Own own_loop{loop};
+  PyObject* deadline = make_deadline(loop, timeout, timeout_s);
+  if (!deadline) return -1;
+  Own own_deadline{deadline};
+  PyObject* reqb = PyBytes_FromStringAndSize(req.data(), Py_ssize_t(req.size()));
+  if (!reqb) return -1;
+  Own own_req{reqb};
+  PyObject* w = iofuture_new(loop);
+  if (!w) return -1;
+  Own own_w{w};
+  if (bump(counts, s_requests) < 0) return -1;
+  PyObject* args[4] = {client, o, deadline, w};
+  PyObject* timer = PyObject_VectorcallMethod(s_enqueue, args, 4, nullptr);
+  if (!timer) return -1;
+  s->timer = timer;
+  own_w.p = nullptr;
+  Py_XSETREF(s->fut, w);
+  Py_INCREF(full);
+  Py_SETREF(s->full, full);
+  own_deadline.p = nullptr;
+  Py_XSETREF(s->deadline, deadline);
+  own_req.p = nullptr;
+  Py_XSETREF(s->req, reqb);
+  s->head = head;
+  s->state = ST_QUEUED;
+  return 2;
+}
+
+// ST_QUEUED, resumed: the waiter finished. A live native connection: the request is sent on it
+// (ST_WAIT). Anything else (a freed slot, a connection closed meanwhile or not native, the
+// client closing, the deadline, a failed connect): H1Client._after_queue continues the request
+// in Python (ST_DELEGATE). 0, or -1 with an error set.
+int queue_resume(H1CallObject* s) {
+  PyObject* r = PyObject_CallMethodNoArgs(s->timer, s_cancel);
+  if (!r) return -1;
+  Py_DECREF(r);
+  Py_CLEAR(s->timer);
+  PyObject* w = s->fut;
+  PyObject* res = nullptr;
+  int st = iofuture_peek(w, &res);
+  PyObject* got = nullptr;  // new reference: the result, or the exception
+  if (st == 1) {
+    got = res;
+    Py_INCREF(got);
+  } else {
+    got = PyObject_CallMethodNoArgs(w, s_exception_name);  // raises CancelledError when cancelled
+    if (!got) return -1;
+  }
+  Own own_got{got};
+  if (st == 1 && Py_TYPE(got) == g.conn.type) {
+    PyObject* cclosed = client_attr(s->client, s_closed_attr);
+    if (!cclosed) return -1;
+    PyObject* net = g.conn.get(got, C_NET);
+    if (cclosed == Py_False && g.conn.get(got, C_CLOSED) == Py_False && net && is_netconn(net) &&
+        netconn_open(net)) {
+      own_got.p = nullptr;
+      PyObject* req = s->req;
+      Py_INCREF(req);  // send_on clears s->req
+      Own own_req{req};
+      Py_CLEAR(s->fut);
+      return send_on(s, got, PyBytes_AS_STRING(req), size_t(PyBytes_GET_SIZE(req)), s->method, s->full,
+                     s->deadline, s->head != 0, false) < 0 ? -1 : 0;
+    }
+  }
+  Py_CLEAR(s->fut);
+  Py_CLEAR(s->req);
+  PyObject* args[5] = {s->client, s->method, s->full, s->deadline, got};
+  PyObject* sub = PyObject_VectorcallMethod(s_after_queue, args, 5, nullptr);
+  if (!sub) return -1;
+  if (!PyCoro_CheckExact(sub)) {
+    Py_DECREF(sub);
+    PyErr_SetString(PyExc_TypeError, "H1Client._after_queue must be a coroutine function");
+    return -1;
+  }
+  s->sub = sub;
+  s->state = ST_DELEGATE;
+  return 0;
 }
 
 // h1_fast(client, method, url, params=None, timeout=None) -> H1Call or None
@@ -796,7 +1041,8 @@ PyObject* mod_h1_fast(PyObject*, PyObject* const* a, Py_ssize_t n) {
   call->params = params;
   Py_XINCREF(timeout);
   call->timeout = timeout;
-  call->conn = call->fut = call->deadline = call->sub = nullptr;
+  call->conn = call->fut = call->deadline = call->sub = call->timer = call->req = nullptr;
+  call->head = 0;
   call->state = ST_INIT;
   call->reused = 0;
   call->path = 0;
@@ -841,6 +1087,11 @@ PyObject* mod_h1_setup(PyObject*, PyObject* args) {
   Py_XINCREF(bt);
   Py_XSETREF(g.base_time, bt);
   Py_DECREF(cls);
+  PyObject* aio = PyImport_ImportModule("asyncio");
+  PyObject* grl = aio ? PyObject_GetAttrString(aio, "get_running_loop") : nullptr;
+  Py_XDECREF(aio);
+  if (!grl) return nullptr;
+  Py_XSETREF(g.get_running_loop, grl);
   g.ready = true;
   Py_RETURN_NONE;
 }
@@ -872,7 +1123,8 @@ int init_h1call_types(PyObject* m) {
               {&s_release, "_release"},       {&s_arm, "_arm"},           {&s_resume, "_resume"},
               {&s_time, "time"},              {&s_pop, "pop"},            {&s_append, "append"},
               {&s_buffered, "buffered"},      {&s_throw, "throw"},        {&s_close, "close"},
-              {&s_request_py, "_request"}};
+              {&s_request_py, "_request"},    {&s_cancel, "cancel"},      {&s_enqueue, "_enqueue"},
+              {&s_after_queue, "_after_queue"}, {&s_exception_name, "exception"}};
   for (auto& s : strs)
     if (!(*s.slot = PyUnicode_InternFromString(s.text))) return -1;
   H1CallType.tp_name = "beholder_amd.ops._native.H1Call";

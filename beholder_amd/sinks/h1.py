@@ -209,6 +209,12 @@ def _queued(o: _Origin) -> bool:
     return len(w) > o.connecting
 
 
+def _expire(w) -> None:
+    """A queued request's deadline: its waiter fails with TimeoutError unless it was served."""
+    if not w.done():
+        w.set_exception(asyncio.TimeoutError())
+
+
 def _split_url(url: str) -> Tuple[str, str]:
     """``(scheme://authority, target)``; target keeps path + query, drops the fragment."""
     i = url.find("://")
@@ -448,11 +454,13 @@ class H1Client(HttpClient):
             raise errors[0]
         raise OSError("Multiple exceptions: " + ", ".join(str(e) for e in errors))
 
-    async def _acquire(self, o: _Origin, deadline: float, fresh: bool = False) -> _Conn:
+    async def _acquire(self, o: _Origin, deadline: float, fresh: bool = False, front: bool = False) -> _Conn:
+        """A connection for a request of ``o``: a live idle one, else the first released or newly
+        made one (queued; ``front``: at the head of the queue, for a request that had its place
+        already)."""
         counts = self.counts
         idle = o.idle
         loop = asyncio.get_running_loop()
-        front = False
         while True:
             now = time.monotonic()
             while idle and not fresh:
@@ -474,7 +482,7 @@ class H1Client(HttpClient):
                 counts["connect_waits"] += 1
             if not fresh and _queued(o):
                 self._grow(o, deadline)
-            th = loop.call_at(deadline, lambda: w.done() or w.set_exception(asyncio.TimeoutError()))
+            th = loop.call_at(deadline, _expire, w)
             try:
                 c = await w
             except asyncio.CancelledError:
@@ -651,7 +659,45 @@ class H1Client(HttpClient):
         o, target, rest = self._resolve(full)
         return await self._exchange(m, full, o, target, rest, deadline, c, w, reused, thrown)
 
-    async def _exchange(self, m, full, o, target, rest, deadline, c, w, reused, thrown) -> HttpResponse:
+    def _enqueue(self, o: _Origin, deadline: float, w):
+        """The native fast path (``ops h1_fast``) found no idle connection: queue its waiter ``w``
+        as :meth:`_acquire` does (same accounting, background connects, deadline), without the
+        request loop's coroutines. Returns the deadline timer (the caller cancels it)."""
+        o.waiters.append(w)
+        self.counts["connect_waits"] += 1
+        if _queued(o):
+            self._grow(o, deadline)
+        return asyncio.get_running_loop().call_at(deadline, _expire, w)
+
+    async def _after_queue(self, m, full, deadline, got) -> HttpResponse:
+        """A natively queued request (:meth:`_enqueue`) was handed no live connection: a freed pool
+        slot (None), a connection that closed meanwhile, the client closing, or an error (its
+        deadline, a failed background connect). The request loop continues as :meth:`_acquire`
+        and :meth:`_exchange` would have, keeping the request's place in the queue."""
+        o, target, rest = self._resolve(full)
+        counts = self.counts
+        if isinstance(got, BaseException):  # as _exchange maps what its _acquire raised
+            if isinstance(got, asyncio.TimeoutError):
+                counts["timeouts"] += 1
+                counts["errors"] += 1
+                raise HttpError(f"ETIMEDOUT: {m} {redact(full)}") from None
+            if isinstance(got, OSError):
+                counts["errors"] += 1
+                raise HttpError(_connect_error(got, o)) from None
+            raise got
+        if self._closed:
+            if got is not None:
+                self._release(got, False)
+            counts["errors"] += 1
+            raise HttpError("client closed")
+        if got is not None and got.closed:
+            self._drop(got)
+            got = None
+        return await self._exchange(m, full, o, target, rest, deadline, None, None, False, None, front=True,
+                                    conn=got)
+
+    async def _exchange(self, m, full, o, target, rest, deadline, c, w, reused, thrown,
+                        front: bool = False, conn: Optional[_Conn] = None) -> HttpResponse:
         """Send on a pooled connection, await the reply; one transparent retry on a fresh
         connection for an idempotent request whose reused connection died before any response
         byte; redirects for GET/HEAD. ``c``/``w``/``reused``: a request already on the wire;
@@ -665,7 +711,11 @@ class H1Client(HttpClient):
             if w is None:
                 req = f"{m} {target}{rest}".encode("latin-1") + (self._tail_cl0 if m in _BODY_METHODS else self._tail)
                 c = None
-                if not fresh:  # fast path of _acquire: a live idle keep-alive connection, no await
+                if conn is not None:  # handed to a natively queued request (_after_queue)
+                    c, conn = conn, None
+                    if c.uses:
+                        counts["reused"] += 1
+                elif not fresh:  # fast path of _acquire: a live idle keep-alive connection, no await
                     idle = o.idle
                     if idle:
                         now = time.monotonic()
@@ -678,7 +728,8 @@ class H1Client(HttpClient):
                             self._drop(cand)
                 try:
                     if c is None:
-                        c = await self._acquire(o, deadline, fresh)
+                        c = await self._acquire(o, deadline, fresh, front)
+                        front = False
                         if self._closed:  # closed while this request connected or waited for a slot
                             self._release(c, False)
                             counts["errors"] += 1

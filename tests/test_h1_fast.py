@@ -462,3 +462,131 @@ def test_compiled_handlers_make_h1_calls_directly(monkeypatch):
     assert (acked, served, impl) == (20, 20, "NativeHandlers") and calls == []
     acked, served, _ = run(go(False))
     assert (acked, served) == (20, 20) and calls.count("POST") == 20
+
+
+async def _queued_run(fast: bool):
+    """A pool of 3 and 60 concurrent requests: most wait in the origin's queue. Returns what the
+    client did (responses, counts, the exact requests the server saw, connections made)."""
+    s = await Raw(lambda t: OK).start()
+    c = H1Client(timeout_s=5, max_per_host=3)
+    if not fast:
+        c.native_call = None
+    base = f"http://127.0.0.1:{s.port}"
+    await c.request("GET", base + "/warm")
+    shapes = [("POST", "/1/cards/c1/actions/comments", {"text": "DEPLOYED ü", "key": "k"}),
+              ("PUT", "/1/cards/c2", {"idList": "L", "pos": 2}), ("GET", "/bot1:X/sendMessage", {"chat_id": 5}),
+              ("HEAD", "/emby", None), ("GET", "/plain?x=1", None)]
+    aws = [c.request(m, base + p, params=q) for i in range(60) for m, p, q in [shapes[i % len(shapes)]]]
+    rs = await asyncio.gather(*aws)
+    out = [(r.status, r.body, r.url.replace(base, "")) for r in rs]
+    kinds = [getattr(aw, "native", False) for aw in aws]  # the Python path returns coroutines
+    counts = dict(c.counts)
+    open_ = sum(o.open for o in c._origins.values())
+    await c.close()
+    await s.stop()
+    raw = sorted(r.replace(str(s.port).encode(), b"PORT") for r in s.raw)
+    return out, kinds, counts, raw, s.connections, open_
+
+
+def test_queued_requests_take_the_native_path_and_match_python():
+    """No idle connection at the first await: the request waits in the origin's queue
+    (H1Client._enqueue) and is sent natively when a connection is handed over. Responses, the
+    bytes on the wire, every count and the connections made are those of the Python loop."""
+    async def go():
+        return await _queued_run(True), await _queued_run(False)
+    fast, slow = run(go())
+    f_out, f_kinds, f_counts, f_raw, f_conns, f_open = fast
+    p_out, p_kinds, p_counts, p_raw, p_conns, p_open = slow
+    assert f_out == p_out and f_raw == p_raw
+    assert f_counts == p_counts and f_conns == p_conns and f_open == p_open
+    assert f_counts["connect_waits"] > 40
+    # queued ones too (the origin was known, the pool full); a request handed a freed slot
+    # instead of a connection (after a HEAD reply leaves a connection unusable) continues in Python
+    assert f_kinds.count(True) >= 40
+
+
+def test_queued_timeout_cancel_and_close_match_python():
+    """A request waiting in the queue: its deadline (ETIMEDOUT), a cancel (its place is given up,
+    no connection leaks) and the client closing ("client closed") end it as on the Python path,
+    under gather (Tasks) and under the native Driver."""
+    async def one(fast):
+        s = await Raw(lambda t: "hang" if t.startswith("/slow") else OK).start()
+        c = H1Client(timeout_s=5, max_per_host=1)
+        if not fast:
+            c.native_call = None
+        base = f"http://127.0.0.1:{s.port}"
+        await c.request("GET", base + "/warm")
+        hog = asyncio.ensure_future(c.request("GET", base + "/slow"))  # holds the only connection
+        await asyncio.sleep(0.02)
+        res = []
+        try:
+            await c.request("GET", base + "/q", params={"token": "s"}, timeout=0.1)
+        except HttpError as e:
+            res.append(str(e).replace(base, ""))
+        t = asyncio.ensure_future(c.request("GET", base + "/cancelled"))
+        await asyncio.sleep(0.02)
+        t.cancel()
+        res.append(type((await asyncio.gather(t, return_exceptions=True))[0]).__name__)
+        got = []
+
+        async def handler():
+            try:
+                got.append((await c.request("PUT", base + "/d", params={"pos": 2}, timeout=0.1)).status)
+            except HttpError as e:
+                got.append(str(e).replace(base, ""))
+        coro = handler()
+        native.Driver(coro, lambda d, e: None).start(coro.send(None))
+        while not got:
+            await asyncio.sleep(0.01)
+        res.append(got[0])
+        waiting = [asyncio.ensure_future(c.request("GET", base + f"/w{i}")) for i in range(3)]
+        await asyncio.sleep(0.02)
+        await c.close()
+        done = await asyncio.wait_for(asyncio.gather(hog, *waiting, return_exceptions=True), 5)
+        res += [type(x).__name__ + ":" + str(x) for x in done]
+        counts = dict(c.counts)
+        open_ = sum(o.open for o in c._origins.values())
+        await s.stop()
+        return res, counts, open_
+
+    async def go():
+        return await one(True), await one(False)
+    fast, slow = run(go())
+    assert fast == slow
+    res, counts, open_ = fast
+    assert res[0] == "ETIMEDOUT: GET /q" and res[1] == "CancelledError" and res[2] == "ETIMEDOUT: PUT /d"
+    assert res[3:] == ["HttpError:client closed"] * 4 and open_ == 0
+
+
+def test_queued_request_gets_the_connect_error_of_a_failed_background_connect():
+    """The first queued request of an origin whose background connect fails gets the connect
+    error (as from _acquire), mapped to the Node-style message."""
+    import socket as _s
+
+    async def one(fast):
+        srv = await Raw(lambda t: OK).start()
+        c = H1Client(timeout_s=2, max_per_host=1)
+        if not fast:
+            c.native_call = None
+        base = f"http://127.0.0.1:{srv.port}"
+        await c.request("GET", base + "/warm")
+        o = c._origins[base]
+        conn = o.idle.pop()  # the only connection, gone; new connects go to a closed port
+        c._drop(conn)
+        await srv.stop()
+        probe = _s.socket()
+        probe.bind(("127.0.0.1", 0))
+        o.port = probe.getsockname()[1]  # nothing listens here
+        probe.close()
+        try:
+            await c.request("GET", base + "/x")
+            msg = "ok"
+        except HttpError as e:
+            msg = str(e).split(":")[0] + ":" + str(e).split(" ")[1]
+        await c.close()
+        return msg
+
+    async def go():
+        return await one(True), await one(False)
+    fast, slow = run(go())
+    assert fast == slow and fast.startswith("connect ECONNREFUSED")
