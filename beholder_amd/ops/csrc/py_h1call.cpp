@@ -13,9 +13,14 @@
 // the shape the sinks produce on a warm pool: a stock H1Client, an
 // ASCII URL whose origin is already known, a printable path (no fragment), params None or a
 // dict (encodeURIComponent query, the `request` library's qs.stringify), and a live idle
-// keep-alive connection on a native NetConn (utils/netconn.py). Anything else is declined
-// before any state is touched, and the H1Call delegates the whole request to
-// H1Client._request (yield from).
+// keep-alive connection on a native NetConn (utils/netconn.py). With no idle connection the
+// request joins the origin's queue (H1Client._enqueue: _acquire's accounting, background
+// connects and deadline) with an IOFuture waiter and is sent natively on the connection it is
+// handed; a freed slot, a closed or non-native connection, the deadline or a failed connect
+// continue in H1Client._after_queue. (The first burst after start queues ~250 requests while
+// the pools fill, with the loop CPU-bound: the Python request loop cost ~10 us each.)
+// Anything else is declined before any state is touched, and the H1Call delegates the whole
+// request to H1Client._request (yield from).
 //
 // The returned H1Call is an awaitable iterator (send/throw/close). It yields the reply
 // IOFuture; a handler driven by the native Driver is resumed by the NetConn's reply callback.
