@@ -25,6 +25,7 @@
 
 #include <deque>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 
@@ -37,19 +38,38 @@ namespace {
 // Python 3.10's default cipher string for ssl.create_default_context (Lib/ssl.py / _ssl.c)
 constexpr const char* kCiphers = "@SECLEVEL=2:ECDH+AESGCM:ECDH+CHACHA20:ECDH+AES:DHE+AES:!aNULL:!eNULL:!aDSS:!SHA1:!AESCCM";
 
+// The per-origin session cache. Shared with the handshake threads (py_netconn.cpp): a TLS 1.2
+// session is stored by the new-session callback inside SSL_do_handshake, which may run on one
+// of them. Every SSL holds a reference (SslTag), so the cache outlives the TlsContext while a
+// handshake thread still works on an SSL of a connection closed meanwhile.
+struct SessionStore {
+  std::mutex mu;
+  std::map<std::string, std::deque<SSL_SESSION*>> sessions;  // "host:port" -> newest sessions (one ref each)
+
+  void clear() {
+    for (auto& kv : sessions)
+      for (SSL_SESSION* x : kv.second) SSL_SESSION_free(x);
+    sessions.clear();
+  }
+  ~SessionStore() { clear(); }
+};
+
+// SSL ex_data (g_key_index): the session-cache key of the SSL's origin and the cache itself
+struct SslTag {
+  std::string key;
+  std::shared_ptr<SessionStore> store;
+};
+
 struct TlsContextObject {
   PyObject_HEAD SSL_CTX* ctx;
-  std::map<std::string, std::deque<SSL_SESSION*>>* sessions;  // "host:port" -> newest sessions (one ref each)
-  // sessions is shared with the handshake threads (py_netconn.cpp): a TLS 1.2 session is stored by
-  // the new-session callback inside SSL_do_handshake, which may run on one of them
-  std::mutex* mu;
+  std::shared_ptr<SessionStore>* store;
   uint64_t handshakes, resumed, offloaded;
   bool check_hostname;  // the certificate must name the host (verify-full / HTTPS)
 };
 
 PyTypeObject TlsContextType = {PyVarObject_HEAD_INIT(nullptr, 0)};
-int g_ex_index = -1;  // SSL ex_data: the TlsContextObject* of an SSL
-int g_key_index = -1;  // SSL ex_data: std::string* session-cache key
+int g_ex_index = -1;  // SSL ex_data: the TlsContextObject* of an SSL (loop thread only: counts)
+int g_key_index = -1;  // SSL ex_data: SslTag*
 
 std::string last_error_text() {
   unsigned long e = ERR_peek_last_error();
@@ -60,23 +80,17 @@ std::string last_error_text() {
 
 constexpr size_t kTicketsPerOrigin = 16;  // enough for a burst of reconnects to resume
 
-void free_all(TlsContextObject* tc) {
-  for (auto& kv : *tc->sessions)
-    for (SSL_SESSION* x : kv.second) SSL_SESSION_free(x);
-  tc->sessions->clear();
-}
-
 // new-session callback: keep the newest sessions of each origin (TLS 1.3 tickets arrive after
 // the handshake, in the first reads; servers usually send two)
 int on_new_session(SSL* ssl, SSL_SESSION* sess) {
-  auto* self = static_cast<TlsContextObject*>(SSL_get_ex_data(ssl, g_ex_index));
-  auto* key = static_cast<std::string*>(SSL_get_ex_data(ssl, g_key_index));
-  if (!self || !key || !self->sessions) return 0;
-  std::lock_guard<std::mutex> lock(*self->mu);
-  auto it = self->sessions->find(*key);
-  if (it == self->sessions->end()) {
-    if (self->sessions->size() >= 1024) free_all(self);  // bounded: rebuilt on demand
-    it = self->sessions->emplace(*key, std::deque<SSL_SESSION*>()).first;
+  auto* tag = static_cast<SslTag*>(SSL_get_ex_data(ssl, g_key_index));
+  if (!tag || !tag->store) return 0;
+  SessionStore& st = *tag->store;
+  std::lock_guard<std::mutex> lock(st.mu);
+  auto it = st.sessions.find(tag->key);
+  if (it == st.sessions.end()) {
+    if (st.sessions.size() >= 1024) st.clear();  // bounded: rebuilt on demand
+    it = st.sessions.emplace(tag->key, std::deque<SSL_SESSION*>()).first;
   }
   it->second.push_back(sess);
   if (it->second.size() > kTicketsPerOrigin) {
@@ -86,7 +100,8 @@ int on_new_session(SSL* ssl, SSL_SESSION* sess) {
   return 1;  // we hold the reference
 }
 
-void free_key(void*, void* ptr, CRYPTO_EX_DATA*, int, long, void*) { delete static_cast<std::string*>(ptr); }
+// ex_data free callback: SSL_free (on whichever thread) drops the tag and its cache reference
+void free_tag(void*, void* ptr, CRYPTO_EX_DATA*, int, long, void*) { delete static_cast<SslTag*>(ptr); }
 
 }  // namespace
 
@@ -181,9 +196,12 @@ PyObject* tc_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
   if (!s) return nullptr;
   s->ctx = nullptr;
   s->check_hostname = verify && check_hostname;
-  s->sessions = new (std::nothrow) std::map<std::string, std::deque<SSL_SESSION*>>();
-  s->mu = new (std::nothrow) std::mutex();
-  if (!s->sessions || !s->mu) {
+  try {
+    s->store = new std::shared_ptr<SessionStore>(std::make_shared<SessionStore>());
+  } catch (const std::bad_alloc&) {
+    s->store = nullptr;
+  }
+  if (!s->store) {
     Py_DECREF(s);
     return PyErr_NoMemory();
   }
@@ -225,11 +243,7 @@ PyObject* tc_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
 }
 
 void tc_dealloc(TlsContextObject* s) {
-  if (s->sessions) {
-    free_all(s);
-    delete s->sessions;
-  }
-  delete s->mu;
+  delete s->store;  // the cache itself goes with the last SSL that still refers to it
   if (s->ctx) SSL_CTX_free(s->ctx);
   Py_TYPE(s)->tp_free(reinterpret_cast<PyObject*>(s));
 }
@@ -237,8 +251,9 @@ void tc_dealloc(TlsContextObject* s) {
 PyObject* tc_get_stats(TlsContextObject* s, void*) {
   Py_ssize_t n = 0;
   {
-    std::lock_guard<std::mutex> lock(*s->mu);
-    for (auto& kv : *s->sessions) n += Py_ssize_t(kv.second.size());
+    SessionStore& st = **s->store;
+    std::lock_guard<std::mutex> lock(st.mu);
+    for (auto& kv : st.sessions) n += Py_ssize_t(kv.second.size());
   }
   return Py_BuildValue("{s:K,s:K,s:n,s:K}", "handshakes", static_cast<unsigned long long>(s->handshakes), "resumed",
                        static_cast<unsigned long long>(s->resumed), "cached_sessions", n, "offloaded",
@@ -270,17 +285,18 @@ SSL* tls_new_ssl(PyObject* ctx_obj, int fd, const char* host, int port) {
   if (ok && !is_ip) ok = SSL_set_tlsext_host_name(ssl, host) == 1;  // SNI for names only
   if (ok && tc->check_hostname)
     ok = is_ip ? X509_VERIFY_PARAM_set1_ip_asc(SSL_get0_param(ssl), host) == 1 : SSL_set1_host(ssl, host) == 1;
-  std::string* key = ok ? new (std::nothrow) std::string(std::string(host) + ":" + std::to_string(port)) : nullptr;
-  if (!key || SSL_set_ex_data(ssl, g_ex_index, tc) != 1 || SSL_set_ex_data(ssl, g_key_index, key) != 1) {
-    if (key && SSL_get_ex_data(ssl, g_key_index) != key) delete key;
+  SslTag* tag = ok ? new (std::nothrow) SslTag{std::string(host) + ":" + std::to_string(port), *tc->store} : nullptr;
+  if (!tag || SSL_set_ex_data(ssl, g_ex_index, tc) != 1 || SSL_set_ex_data(ssl, g_key_index, tag) != 1) {
+    if (tag && SSL_get_ex_data(ssl, g_key_index) != tag) delete tag;
     SSL_free(ssl);
     PyErr_Format(PyExc_RuntimeError, "TLS setup for %s: %s", host, last_error_text().c_str());
     return nullptr;
   }
   {
-    std::lock_guard<std::mutex> lock(*tc->mu);
-    auto it = tc->sessions->find(*key);
-    if (it != tc->sessions->end() && !it->second.empty()) {
+    SessionStore& st = **tc->store;
+    std::lock_guard<std::mutex> lock(st.mu);
+    auto it = st.sessions.find(tag->key);
+    if (it != st.sessions.end() && !it->second.empty()) {
       SSL_SESSION* sess = it->second.back();
       SSL_set_session(ssl, sess);  // the SSL holds its own reference
       if (SSL_SESSION_get_protocol_version(sess) == TLS1_3_VERSION) {
@@ -325,7 +341,7 @@ void tls_describe_failure(SSL* ssl, std::string& reason, std::string& message, b
 
 int init_tls_types(PyObject* m) {
   g_ex_index = SSL_get_ex_new_index(0, nullptr, nullptr, nullptr, nullptr);
-  g_key_index = SSL_get_ex_new_index(0, nullptr, nullptr, nullptr, free_key);
+  g_key_index = SSL_get_ex_new_index(0, nullptr, nullptr, nullptr, free_tag);
   if (g_ex_index < 0 || g_key_index < 0) {
     PyErr_SetString(PyExc_RuntimeError, "SSL_get_ex_new_index failed");
     return -1;
