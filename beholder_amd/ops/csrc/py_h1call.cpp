@@ -1014,7 +1014,19 @@ int queue_resume(H1CallObject* s) {
   Py_CLEAR(s->req);
   PyObject* args[5] = {s->client, s->method, s->full, s->deadline, got};
   PyObject* sub = PyObject_VectorcallMethod(s_after_queue, args, 5, nullptr);
-  if (!sub) return -1;
+  if (!sub) {
+    if (Py_TYPE(got) == g.conn.type) {  // handed over but not taken: back to the pool accounting
+      PyObject *et, *ev, *tb;
+      PyErr_Fetch(&et, &ev, &tb);
+      PyObject* r = PyObject_CallMethodObjArgs(s->client, s_release, got, Py_False, nullptr);
+      if (!r)
+        PyErr_WriteUnraisable(s->client);
+      else
+        Py_DECREF(r);
+      PyErr_Restore(et, ev, tb);
+    }
+    return -1;
+  }
   if (!PyCoro_CheckExact(sub)) {
     Py_DECREF(sub);
     PyErr_SetString(PyExc_TypeError, "H1Client._after_queue must be a coroutine function");
