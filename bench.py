@@ -352,6 +352,7 @@ def io_extras(a) -> dict:
                 "tcp_e2e_cpu_us_per_event": _r(e2e.get("cpu_us_per_event")),
                 "tcp_e2e_p50_handle_latency_us": _r(hl.get("p50")),
                 "tcp_e2e_p999_handle_latency_us": _r(hl.get("p999")),
+                "tcp_e2e_warmup_p99_handle_latency_us": _r(e2e.get("warmup_handle_latency_us", {}).get("p99")),
                 "tcp_e2e_warmup_p999_handle_latency_us": _r(e2e.get("warmup_handle_latency_us", {}).get("p999")),
                 "tcp_e2e_errors": e2e.get("errors")})
     tls = harness._tcp_e2e(a.io_events, http_servers=4, tls=True)
@@ -359,7 +360,10 @@ def io_extras(a) -> dict:
     out.update({"tls_e2e_events_per_sec": _r(tls.get("ingest_rate_eps"), 1),
                 "tls_e2e_cpu_us_per_event": _r(tls.get("cpu_us_per_event")),
                 "tls_e2e_p999_handle_latency_us": _r(hl.get("p999")),
+                "tls_e2e_warmup_p99_handle_latency_us": _r(tls.get("warmup_handle_latency_us", {}).get("p99")),
                 "tls_e2e_warmup_p999_handle_latency_us": _r(tls.get("warmup_handle_latency_us", {}).get("p999")),
+                "tls_e2e_handshakes": (tls.get("http") or {}).get("tls_handshakes"),
+                "tls_e2e_resumed": (tls.get("http") or {}).get("tls_resumed"),
                 "tls_e2e_errors": tls.get("errors")})
     h = harness._http_tcp(Workload(n_media=10000, seed=a.seed), a.io_events, clients=("h1",))["h1"]
     hl = h["handle_latency_us"]
