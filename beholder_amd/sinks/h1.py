@@ -38,6 +38,7 @@ from __future__ import annotations
 import asyncio
 import base64
 import collections
+import functools
 import ipaddress
 import socket
 import ssl as _ssl
@@ -209,6 +210,9 @@ def _queued(o: _Origin) -> bool:
     return len(w) > o.connecting
 
 
+_DNS_REUSE_S = 1.0  # a successful name lookup serves the connects of the next second too
+
+
 def _expire(w) -> None:
     """A queued request's deadline: its waiter fails with TimeoutError unless it was served."""
     if not w.done():
@@ -256,6 +260,9 @@ class H1Client(HttpClient):
         self.ssl_cafile = ssl_cafile
         self._ntls = None
         self._literal: Dict[str, list] = {}  # hosts that are IP literals: no resolver call
+        # name lookups per (host, port), in flight or finished within _DNS_REUSE_S: the connects of
+        # a burst share one
+        self._resolving: Dict[Tuple[str, int], Tuple[asyncio.Future, float]] = {}
         self._origins: Dict[str, _Origin] = {}
         self._routes: Dict[str, Tuple[_Origin, str, str]] = {}
         self._closed = False
@@ -404,6 +411,37 @@ class H1Client(HttpClient):
         if _queued(o):  # a queue longer than the connects under way: the pool grows (max_connecting at a time)
             self._grow(o, asyncio.get_running_loop().time() + self.timeout_s)
 
+    def _lookup(self, o: _Origin, loop) -> asyncio.Future:
+        """``getaddrinfo`` of ``o``, shared by every connect that needs it while it runs and for
+        ``_DNS_REUSE_S`` after it succeeded: the first burst after start (or after the keep-alive
+        connections expired) opens connections in waves of ``max_connecting``, which would
+        otherwise make one identical lookup each (a resolver query on an executor thread). Each
+        caller still waits only up to its own deadline (the lookup is shielded from a caller's
+        timeout). A failed lookup is not reused."""
+        key = (o.host, o.port)
+        hit = self._resolving.get(key)
+        if hit is not None:
+            f, until = hit
+            if not f.done() or (loop.time() < until and not f.cancelled() and f.exception() is None):
+                return f
+        f = asyncio.ensure_future(loop.getaddrinfo(o.host, o.port, type=socket.SOCK_STREAM))
+        self._resolving[key] = (f, float("inf"))
+        f.add_done_callback(functools.partial(self._lookup_done, key, loop))
+        if len(self._resolving) > 256:  # stale entries of many origins: keep the map small
+            now = loop.time()
+            for k in [k for k, (x, t) in self._resolving.items() if x.done() and t <= now]:
+                del self._resolving[k]
+        return f
+
+    def _lookup_done(self, key, loop, f) -> None:
+        cur = self._resolving.get(key)
+        if cur is None or cur[0] is not f:
+            return
+        if f.cancelled() or f.exception() is not None:  # retrieved: not logged as lost; not reused
+            del self._resolving[key]
+        else:
+            self._resolving[key] = (f, loop.time() + _DNS_REUSE_S)
+
     async def _connect_native(self, conn: _Conn, o: _Origin, ntls, deadline: float, loop, infos=None) -> None:
         """TCP connect, and TLS for ``ntls``, in C (``ops netconn_connect``): no asyncio transport
         is made and dropped. Addresses are tried in order, as ``loop.create_connection`` does
@@ -416,8 +454,7 @@ class H1Client(HttpClient):
                 ipaddress.ip_address(o.host)
                 infos = self._literal[o.host] = [o.host]
             except ValueError:  # a name: resolved within the request's deadline, like create_connection
-                found = await asyncio.wait_for(loop.getaddrinfo(o.host, o.port, type=socket.SOCK_STREAM),
-                                               deadline - loop.time())
+                found = await asyncio.wait_for(asyncio.shield(self._lookup(o, loop)), deadline - loop.time())
                 infos = [_sockaddr_host(ai[4]) for ai in found]
         errors = []
         for ip in infos:
@@ -521,7 +558,7 @@ class H1Client(HttpClient):
                 ipaddress.ip_address(o.host)
             except ValueError:  # a name: one lookup for the whole batch, not one per connection
                 try:
-                    found = await asyncio.wait_for(loop.getaddrinfo(o.host, o.port, type=socket.SOCK_STREAM),
+                    found = await asyncio.wait_for(asyncio.shield(self._lookup(o, loop)),
                                                    self.timeout_s)
                 except (OSError, asyncio.TimeoutError) as e:
                     return 0, e

@@ -2,6 +2,7 @@
 (`sinks/h1.py`) that the service uses by default for Trello / Telegram / Emby
 (index.js:53,83,99,112)."""
 import asyncio
+import socket
 import shutil
 import ssl
 import subprocess
@@ -513,3 +514,43 @@ def test_cached_route_gives_the_uncached_request_target(origin, path, params):
         full, o, target, rest = c._prepare(url, params)
         assert full == with_query(url, params)
         assert (o, target, rest) == want
+
+
+def test_connects_of_a_burst_share_one_name_lookup():
+    """A burst to a host name opens connections in waves (max_connecting at a time); they share
+    one getaddrinfo, in flight or finished within a second, instead of one resolver query each.
+    A later burst resolves again. (Native connects; asyncio's create_connection, with native I/O
+    off, resolves on its own.)"""
+    from beholder_amd.utils import netconn
+    if not netconn.enabled():
+        return
+
+    async def go():
+        s = await Scripted(lambda n, m, t, h: OK).start()
+        loop = asyncio.get_running_loop()
+        real, calls = loop.getaddrinfo, []
+
+        async def slow_lookup(host, port, **kw):
+            calls.append(host)
+            await asyncio.sleep(0.05)
+            return [(socket.AF_INET, socket.SOCK_STREAM, 6, "", ("127.0.0.1", port))]
+        loop.getaddrinfo = slow_lookup
+        try:
+            c = H1Client(timeout_s=5, max_connecting=8)
+            url = f"http://sink.invalid:{s.port}/x"
+            rs = await asyncio.gather(*[c.request("GET", url) for _ in range(12)])
+            first = len(calls)
+            await c.preconnect(url, 20)  # within a second: the same lookup
+            second = len(calls)
+            c._resolving[("sink.invalid", s.port)] = (c._resolving[("sink.invalid", s.port)][0], 0.0)  # expired
+            await c.preconnect(url, 30)  # a later batch resolves again
+            third = len(calls)
+            st = dict(c.counts)
+            await c.close()
+        finally:
+            loop.getaddrinfo = real
+            await s.stop()
+        return [r.status for r in rs], first, second, third, st
+    statuses, first, second, third, st = run(go())
+    assert statuses == [200] * 12 and st["connections"] >= 2
+    assert (first, second, third) == (1, 1, 2)
