@@ -157,10 +157,25 @@ struct HsJob {
   bool verify = false;
 };
 
+// A handshake running on a thread for `c` is given up: true when the thread still runs it (it
+// then frees the SSL, the fd and the job itself); a finished one is marked connection-less so
+// that the drain of the completion channel just frees it. Must run before `c` leaves its
+// poller: leaving can close the poller, which drains the channel, and the drain must not treat
+// a connection that is closing as one whose handshake just succeeded.
+bool detach_job(NetConnObject* c) {
+  if (!c->hs_job) return false;
+  auto* j = static_cast<HsJob*>(c->hs_job);
+  c->hs_job = nullptr;
+  if (j->state.exchange(HS_ORPHANED) == HS_RUNNING) return true;
+  j->conn = nullptr;  // finished and queued for this loop: the drain drops it
+  return false;
+}
+
 // Stops watching the fd and closes it (idempotent). Errors from the loop are swallowed: this
 // runs on teardown paths.
 void shut(NetConnObject* c) {
   if (c->fd < 0) return;
+  bool thread_owns = detach_job(c);
   PyObject *et, *ev, *tb;
   PyErr_Fetch(&et, &ev, &tb);
   if (c->poller) {
@@ -182,21 +197,16 @@ void shut(NetConnObject* c) {
   }
   PyErr_Clear();
   PyErr_Restore(et, ev, tb);
-  if (c->hs_job) {
-    auto* j = static_cast<HsJob*>(c->hs_job);
-    c->hs_job = nullptr;
-    if (j->state.exchange(HS_ORPHANED) == HS_RUNNING) {
-      // the handshake thread still uses the SSL and the fd: wake it up; it frees both (and the
-      // job) when done
-      ::shutdown(c->fd, SHUT_RDWR);
-      c->ssl = nullptr;
-      c->fd = -1;
-      c->writing = 0;
-      c->closed = 1;
-      c->out->clear();
-      return;
-    }
-    j->conn = nullptr;  // finished and queued for this loop: the drain drops it
+  if (thread_owns) {
+    // the handshake thread still uses the SSL and the fd: wake it up; it frees both (and the
+    // job) when done
+    ::shutdown(c->fd, SHUT_RDWR);
+    c->ssl = nullptr;
+    c->fd = -1;
+    c->writing = 0;
+    c->closed = 1;
+    c->out->clear();
+    return;
   }
   if (c->ssl) {
     // an established session stays resumable when its connection is dropped without close_notify
@@ -734,7 +744,14 @@ int nc_clear(NetConnObject* c) {
   Py_CLEAR(c->hs_fut);
   Py_CLEAR(c->tls_error);
   if (c->poller) {  // registered: leave the epoll set first (the poller's reference cycle)
-    if (c->fd >= 0) netpoll_del(c->poller, c->fd);
+    if (c->fd >= 0 && detach_job(c)) {  // the handshake thread frees the SSL and the fd
+      ::shutdown(c->fd, SHUT_RDWR);
+      netpoll_del(c->poller, c->fd);
+      c->ssl = nullptr;
+      c->fd = -1;
+    } else if (c->fd >= 0) {
+      netpoll_del(c->poller, c->fd);
+    }
     Py_CLEAR(c->poller);
   }
   if (c->pending) drop_pending(c);

@@ -586,3 +586,69 @@ def test_tls_connection_churn_leaks_no_descriptors_or_threads():
     now_fds, now_tasks, base_fds, base_tasks = run(go())
     assert now_fds <= base_fds + 2, (now_fds, base_fds)
     assert now_tasks == base_tasks, (now_tasks, base_tasks)
+
+
+def test_https_by_host_name_verifies_the_name_and_shares_the_lookup():
+    """An HTTPS sink addressed by name (as api.trello.com is): the name is resolved once for the
+    burst, sent as SNI and checked against the certificate (the bench certificate names
+    localhost); a name the certificate does not carry fails verification."""
+    async def go():
+        s = await TlsServer(lambda t: ok()).start()
+        loop = asyncio.get_running_loop()
+        real, calls = loop.getaddrinfo, []
+
+        async def lookup(host, port, **kw):
+            calls.append(host)
+            return await real("127.0.0.1", port, **kw)
+        loop.getaddrinfo = lookup
+        try:
+            c = H1Client(timeout_s=5, ssl_cafile=TLS_CERT)
+            rs = await asyncio.gather(*[c.request("GET", f"https://localhost:{s.port}/x") for _ in range(20)])
+            good = ([r.status for r in rs], len(calls), dict(c.counts)["connections"])
+            await c.close()
+            c = H1Client(timeout_s=5, ssl_cafile=TLS_CERT)
+            try:
+                await c.request("GET", f"https://not-the-name.invalid:{s.port}/x")
+                bad = "ok"
+            except HttpError as e:
+                bad = str(e)
+            await c.close()
+        finally:
+            loop.getaddrinfo = real
+            await s.stop()
+        return good, bad
+    (statuses, lookups, conns), bad = run(go())
+    assert statuses == [200] * 20 and conns >= 2
+    from beholder_amd.utils import netconn
+    if netconn.enabled():
+        assert lookups == 1
+    assert "CERTIFICATE_VERIFY_FAILED" in bad or "certificate" in bad.lower()
+
+
+def test_closing_a_connection_whose_handshake_just_finished_reports_nothing():
+    """A connection closed right after its handshake finished on a thread (the completion queued,
+    not yet taken by the loop), while it is the poller's last socket: closing the poller drains
+    the completion channel, and that drain must see the connection as gone (it used to treat it
+    as a fresh success and fail re-arming a socket that had left the epoll set, reported as an
+    unraisable FileNotFoundError). Many bursts whose clients close at once make the window
+    likely; nothing may be reported."""
+    import sys
+    seen = []
+    hook, sys.unraisablehook = sys.unraisablehook, seen.append
+
+    async def go():
+        s = await TlsServer(lambda t: ok()).start()
+        try:
+            for _ in range(60):
+                c = H1Client(timeout_s=5, ssl_cafile=TLS_CERT)
+                rs = await asyncio.gather(*[c.request("GET", f"https://127.0.0.1:{s.port}/x") for _ in range(20)])
+                assert all(r.status == 200 for r in rs)
+                await c.close()  # background connects still finishing their handshakes
+            await asyncio.sleep(0.05)
+        finally:
+            await s.stop()
+    try:
+        run(go())
+    finally:
+        sys.unraisablehook = hook
+    assert [f"{u.exc_type.__name__}: {u.exc_value}" for u in seen] == []
