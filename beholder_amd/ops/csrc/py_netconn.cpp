@@ -31,7 +31,6 @@
 // the socket fails (the fd is already closed and unregistered), _net_error(exc) for a protocol
 // error or an unsolicited reply, _net_message(type, body) for out-of-band Postgres messages.
 #include <errno.h>
-#include <poll.h>
 #include <pthread.h>
 #include <time.h>
 #include <openssl/err.h>
@@ -46,12 +45,12 @@
 #include <algorithm>
 #include <atomic>
 #include <memory>
-#include <condition_variable>
 #include <deque>
 #include <mutex>
 #include <string>
 #include <thread>
 
+#include "hs_reactor.hpp"
 #include "hs_wake.hpp"
 #include "py_common.hpp"
 
@@ -134,24 +133,22 @@ char* read_buf() {
 // and signature checks). On the loop thread that time is taken from every delivery in flight: a
 // burst of new sink connections (the first deliveries after start, a pool growing, reconnects
 // after an outage) shows up as the handle-latency tail. With a NetPoller, a NetConn hands its
-// handshake to a small pool of handshake threads instead: the fd leaves the epoll interest set,
-// a thread runs SSL_do_handshake with poll(2) until it completes or fails, and queues the result
-// on the poller's completion channel (hs_wake.hpp: an eventfd in the same epoll set, so the
-// thread never needs the GIL); the poller's `_run` then resumes the connection on the loop
-// thread exactly as after an on-loop handshake (same stats, same errors). While a thread owns
-// the handshake the loop never touches the SSL: closing the connection marks the job orphaned
-// and shuts the socket down, and the thread then frees the SSL, closes the fd and drops the job.
-enum HsState : int { HS_RUNNING = 0, HS_DONE = 1, HS_ORPHANED = 2 };
+// handshake to the handshake threads instead (hs_reactor.hpp: they share one epoll set and run
+// only the CPU steps, so any number of handshakes wait for their peers at once): the fd leaves
+// the NetPoller's interest set, the threads step SSL_do_handshake until it completes or fails,
+// and the result is queued on the poller's completion channel (hs_wake.hpp: an eventfd in the
+// same epoll set, so no thread ever needs the GIL); the poller's `_run` then resumes the
+// connection on the loop thread exactly as after an on-loop handshake (same stats, same
+// errors). While the threads own the handshake the loop never touches the SSL: closing the
+// connection marks the job orphaned and shuts the socket down, and the thread that takes it next
+// frees the SSL, closes the fd and drops the job.
 enum HsResult : int { HR_OK = 0, HR_SSL = 1, HR_TIMEOUT = 2 };
 constexpr double kHandshakeCapS = 120.0;  // safety net; callers abort on their own deadlines
 
-struct HsJob {
+struct HsJob : ReactorJob {
   NetConnObject* conn;  // no reference: read only on the loop thread, cleared when the conn closes
   std::shared_ptr<HsWake> wake;  // the loop's completion channel
   SSL* ssl;
-  int fd;
-  double deadline;
-  std::atomic<int> state{HS_RUNNING};
   int result = HR_OK;
   std::string reason, message;
   bool verify = false;
@@ -166,6 +163,10 @@ bool detach_job(NetConnObject* c) {
   if (!c->hs_job) return false;
   auto* j = static_cast<HsJob*>(c->hs_job);
   c->hs_job = nullptr;
+  // Wake the job first, while the fd is surely still open: a thread closes it only once it has
+  // seen ORPHANED, and a shutdown(2) after the exchange could hit a closed (or reused) number.
+  // Woken before the exchange, the job just fails and lands on the DONE path below.
+  ::shutdown(c->fd, SHUT_RDWR);
   if (j->state.exchange(HS_ORPHANED) == HS_RUNNING) return true;
   j->conn = nullptr;  // finished and queued for this loop: the drain drops it
   return false;
@@ -198,9 +199,8 @@ void shut(NetConnObject* c) {
   PyErr_Clear();
   PyErr_Restore(et, ev, tb);
   if (thread_owns) {
-    // the handshake thread still uses the SSL and the fd: wake it up; it frees both (and the
-    // job) when done
-    ::shutdown(c->fd, SHUT_RDWR);
+    // the handshake thread still uses the SSL and the fd (woken by detach_job): it frees both
+    // (and the job) when done
     c->ssl = nullptr;
     c->fd = -1;
     c->writing = 0;
@@ -396,109 +396,89 @@ int tls_handshake(NetConnObject* c) {
   return 0;
 }
 
-double mono_now() {
-  timespec t;
-  clock_gettime(CLOCK_MONOTONIC, &t);
-  return double(t.tv_sec) + double(t.tv_nsec) * 1e-9;
+double mono_now() { return reactor_now(); }
+
+// One non-blocking step of an offloaded handshake, on a handshake thread: 0 when finished (the
+// outcome is in the job), else the readiness to wait for.
+int hs_step(ReactorJob* rj) {
+  auto* j = static_cast<HsJob*>(rj);
+  if (j->state.load() == HS_ORPHANED) return 0;  // closed: hs_finish frees it
+  if (j->expired.load()) {
+    j->result = HR_TIMEOUT;
+    return 0;
+  }
+  ERR_clear_error();  // the error queue is per thread; a job's steps may run on different ones
+  int r = SSL_do_handshake(j->ssl);
+  if (r == 1) {
+    j->result = j->expired.load() ? HR_TIMEOUT : HR_OK;  // the scan may have shut it down meanwhile
+    return 0;
+  }
+  int e = SSL_get_error(j->ssl, r);
+  if (e == SSL_ERROR_WANT_READ) return EPOLLIN;
+  if (e == SSL_ERROR_WANT_WRITE) return EPOLLOUT;
+  if (j->expired.load()) {
+    j->result = HR_TIMEOUT;
+  } else {
+    tls_describe_failure(j->ssl, j->reason, j->message, j->verify);
+    j->result = HR_SSL;
+  }
+  ERR_clear_error();
+  return 0;
 }
 
-// On a handshake thread: SSL_do_handshake until done, failed or past the deadline.
-void hs_run(HsJob* j) {
-  ERR_clear_error();  // the error queue is per thread
-  for (;;) {
-    int r = SSL_do_handshake(j->ssl);
-    if (r == 1) {
-      j->result = HR_OK;
-      return;
-    }
-    int e = SSL_get_error(j->ssl, r);
-    if ((e == SSL_ERROR_WANT_READ || e == SSL_ERROR_WANT_WRITE) && j->state.load() != HS_ORPHANED) {
-      double left = j->deadline - mono_now();
-      if (left <= 0) {
-        j->result = HR_TIMEOUT;
-        return;
-      }
-      pollfd p;
-      p.fd = j->fd;
-      p.events = short(e == SSL_ERROR_WANT_READ ? POLLIN : POLLOUT);
-      p.revents = 0;
-      int ms = int(std::min(left, 0.25) * 1000.0) + 1;
-      if (::poll(&p, 1, ms) < 0 && errno != EINTR) {
-        j->reason = "SYSCALL";
-        j->message = std::string("[SSL: SYSCALL] poll: ") + strerror(errno);
-        j->result = HR_SSL;
-        return;
-      }
-      continue;
-    }
-    tls_describe_failure(j->ssl, j->reason, j->message, j->verify);
-    ERR_clear_error();
+// The job has left the reactor: hand it to its loop, or free it if its connection is gone.
+void hs_finish(ReactorJob* rj) {
+  auto* j = static_cast<HsJob*>(rj);
+  if (j->sys_errno && j->result == HR_OK) {
+    j->reason = "SYSCALL";
+    j->message = std::string("[SSL: SYSCALL] epoll_ctl: ") + strerror(j->sys_errno);
     j->result = HR_SSL;
+  }
+  std::shared_ptr<HsWake> wake = j->wake;
+  if (j->state.exchange(HS_DONE) == HS_ORPHANED) {  // closed meanwhile: the SSL, fd and job are ours
+    SSL_free(j->ssl);
+    ::close(j->fd);
+    delete j;
     return;
   }
+  if (!wake->post(j)) delete j;  // posted: the loop thread owns the job from here
 }
 
-struct HsPool {
-  std::mutex mu;
-  std::condition_variable cv;
-  std::deque<HsJob*> q;
-  unsigned threads = 0;
-};
-HsPool* g_hs = nullptr;  // process-lifetime (its threads never exit); replaced in a forked child
-
-void hs_worker(HsPool* pool) {
+void hs_thread(HsReactor* r) {
   // OpenSSL 3 keeps per-thread state (random generators, provider caches) that a thread's first
   // handshake would build inside the first burst of connects: one in-memory handshake first
   tls_warm_handshake();
-  for (;;) {
-    HsJob* j;
-    {
-      std::unique_lock<std::mutex> lock(pool->mu);
-      pool->cv.wait(lock, [pool] { return !pool->q.empty(); });
-      j = pool->q.front();
-      pool->q.pop_front();
-    }
-    hs_run(j);
-    std::shared_ptr<HsWake> wake = j->wake;
-    if (j->state.exchange(HS_DONE) == HS_ORPHANED) {  // closed meanwhile: the SSL, fd and job are ours
-      SSL_free(j->ssl);
-      ::close(j->fd);
-      delete j;
-      continue;
-    }
-    if (!wake->post(j)) delete j;  // posted: the loop thread owns the job from here
-  }
+  r->run();
 }
 
-void hs_after_fork_child() { g_hs = nullptr; }
+HsReactor* g_hs = nullptr;  // process-lifetime (its threads never exit); replaced in a forked child
+unsigned g_hs_threads = 0;
 
-// The process's handshake pool with its threads started (on the calling thread, which holds the
-// GIL; the threads never take it). Throws std::bad_alloc / std::system_error.
-HsPool* hs_pool() {
+void hs_after_fork_child() {
+  if (g_hs) g_hs->abandon_after_fork();  // the object itself is leaked: a parent thread may hold its lock
+  g_hs = nullptr;
+  g_hs_threads = 0;
+}
+
+// The process's handshake reactor with its threads started (on the calling thread, which holds
+// the GIL; the threads never take it). Throws std::bad_alloc / std::system_error.
+HsReactor* hs_pool() {
   static bool atfork = (pthread_atfork(nullptr, nullptr, hs_after_fork_child), true);
   (void)atfork;
-  if (!g_hs) g_hs = new HsPool();
-  HsPool* pool = g_hs;
-  // 4: on the box's 16-CPU share, 8 threads (one per admitted connect) made the first burst
-  // slower, not faster: they compete with the loop and the peers for the same CPUs
-  // (interleaved A/B, profiles/box_r3_warmup/threads/)
+  if (!g_hs) g_hs = new HsReactor(hs_step, hs_finish);
+  // 4: the threads only run CPU steps now, and on the box's 16-CPU share more of them compete
+  // with the loop and the peers for the same CPUs (profiles/box_r3_warmup/threads/)
   unsigned want = std::max(1u, std::min(4u, std::thread::hardware_concurrency() / 4));
-  while (pool->threads < want) {
-    std::thread(hs_worker, pool).detach();
-    ++pool->threads;
+  while (g_hs_threads < want) {
+    std::thread(hs_thread, g_hs).detach();
+    ++g_hs_threads;
   }
-  return pool;
+  return g_hs;
 }
 
 bool hs_submit(HsJob* j) {
   try {
-    HsPool* pool = hs_pool();
-    {
-      std::lock_guard<std::mutex> lock(pool->mu);
-      pool->q.push_back(j);
-    }
-    pool->cv.notify_one();
-    return true;
+    return hs_pool()->submit(j);
   } catch (const std::exception&) {
     return false;
   }
@@ -745,7 +725,6 @@ int nc_clear(NetConnObject* c) {
   Py_CLEAR(c->tls_error);
   if (c->poller) {  // registered: leave the epoll set first (the poller's reference cycle)
     if (c->fd >= 0 && detach_job(c)) {  // the handshake thread frees the SSL and the fd
-      ::shutdown(c->fd, SHUT_RDWR);
       netpoll_del(c->poller, c->fd);
       c->ssl = nullptr;
       c->fd = -1;

@@ -31,11 +31,15 @@ def test_ring_stress_under_sanitizer(target):
 
 
 @pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
-@pytest.mark.parametrize("target", ["hs_wake_stress_tsan", "hs_wake_stress_asan"])
+@pytest.mark.parametrize("target", ["hs_wake_stress_tsan", "hs_wake_stress_asan",
+                                    "hs_reactor_stress_tsan", "hs_reactor_stress_asan"])
 def test_handshake_completion_channel_under_sanitizer(target):
     """The TLS handshake threads' completion channel (ops/csrc/hs_wake.hpp) with the job
     ownership protocol of py_netconn.cpp around it: workers post or free, the loop drains,
-    orphans connections and closes the channel while posts race it; every job is freed once."""
+    orphans connections and closes the channel while posts race it; every job is freed once.
+    hs_reactor_stress: the same protocol on the real reactor (ops/csrc/hs_reactor.hpp) with
+    socketpairs, jobs stepped by whichever thread takes their readiness, orphaned by shutdown(2)
+    or expired by the deadline scan."""
     b = subprocess.run(["make", "-s", target], cwd=HERE, capture_output=True, text=True, timeout=300)
     assert b.returncode == 0, b.stderr
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1", ASAN_OPTIONS="detect_leaks=1")

@@ -652,3 +652,54 @@ def test_closing_a_connection_whose_handshake_just_finished_reports_nothing():
     finally:
         sys.unraisablehook = hook
     assert [f"{u.exc_type.__name__}: {u.exc_value}" for u in seen] == []
+
+
+@requires_native_tls
+def test_handshakes_waiting_for_slow_peers_do_not_hold_the_handshake_threads():
+    """The handshake threads only run the CPU steps (hs_reactor.hpp): a handshake waiting for its
+    peer holds no thread. 16 connects to a peer that answers each ClientHello 0.3 s late all
+    finish in about 0.3 s; with the threads blocked in poll(2) through the wait (the earlier
+    design, 4 threads) they took four rounds, about 1.2 s."""
+    delay, n = 0.3, 16
+
+    async def go():
+        s = await TlsServer(lambda t: ok()).start()
+
+        async def pipe(src, dst, first_delay=0.0):
+            try:
+                while True:
+                    data = await src.read(65536)
+                    if not data:
+                        break
+                    if first_delay:
+                        await asyncio.sleep(first_delay)
+                        first_delay = 0.0
+                    dst.write(data)
+                    await dst.drain()
+            except ConnectionError:
+                pass
+            finally:
+                dst.close()
+
+        async def slow(r, w):  # delays the server's first flight by `delay`, then relays
+            ur, uw = await asyncio.open_connection("127.0.0.1", s.port)
+            await asyncio.gather(pipe(r, uw), pipe(ur, w, delay))
+
+        proxy = await asyncio.start_server(slow, "127.0.0.1", 0)
+        port = proxy.sockets[0].getsockname()[1]
+        c = H1Client(timeout_s=10, ssl_cafile=TLS_CERT, max_per_host=n)
+        url = f"https://127.0.0.1:{port}/x"
+        before = dict(c._native_tls().stats)
+        t0 = asyncio.get_running_loop().time()
+        opened, err = await c.preconnect(url, n)
+        took = asyncio.get_running_loop().time() - t0
+        after = dict(c._native_tls().stats)
+        r = await c.request("GET", url)
+        await c.close()
+        proxy.close()
+        await s.stop()
+        return opened, err, took, after["offloaded"] - before["offloaded"], r.status
+    opened, err, took, offloaded, status = run(go())
+    assert err is None and opened == n and status == 200
+    assert offloaded == n
+    assert delay <= took < 2 * delay + 0.15, took
