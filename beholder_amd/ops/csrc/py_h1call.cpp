@@ -173,6 +173,7 @@ struct H1CallObject {
   uint8_t reused;  // the connection had served a request before (h1.py `reused`)
   uint8_t path;    // 0 not started, 1 sent natively, 2 delegated to H1Client._request
   uint8_t head;    // ST_QUEUED: a HEAD request
+  uint8_t front;   // a continuation of an event's earlier request: waits at the front of the queue
 };
 
 PyTypeObject H1CallType = {PyVarObject_HEAD_INIT(nullptr, 0)};
@@ -957,8 +958,8 @@ int queue_start(H1CallObject* s, PyObject* client, PyObject* counts, PyObject* o
   if (!w) return -1;
   Own own_w{w};
   if (bump(counts, s_requests) < 0) return -1;
-  PyObject* args[4] = {client, o, deadline, w};
-  PyObject* timer = PyObject_VectorcallMethod(s_enqueue, args, 4, nullptr);
+  PyObject* args[5] = {client, o, deadline, w, s->front ? Py_True : Py_False};
+  PyObject* timer = PyObject_VectorcallMethod(s_enqueue, args, 5, nullptr);
   if (!timer) return -1;
   s->timer = timer;
   own_w.p = nullptr;
@@ -1037,13 +1038,15 @@ int queue_resume(H1CallObject* s) {
   return 0;
 }
 
-// h1_fast(client, method, url, params=None, timeout=None) -> H1Call or None
+// h1_fast(client, method, url, params=None, timeout=None, front=False) -> H1Call or None
 PyObject* mod_h1_fast(PyObject*, PyObject* const* a, Py_ssize_t n) {
-  if (n < 3 || n > 5) {
-    PyErr_SetString(PyExc_TypeError, "h1_fast(client, method, url, params=None, timeout=None)");
+  if (n < 3 || n > 6) {
+    PyErr_SetString(PyExc_TypeError, "h1_fast(client, method, url, params=None, timeout=None, front=False)");
     return nullptr;
   }
   if (!g.ready || Py_TYPE(a[0]) != g.client_type) Py_RETURN_NONE;
+  int front = n > 5 ? PyObject_IsTrue(a[5]) : 0;
+  if (front < 0) return nullptr;
   H1CallObject* call = PyObject_GC_New(H1CallObject, &H1CallType);
   if (!call) return nullptr;
   PyObject* params = n > 3 && a[3] != Py_None ? a[3] : nullptr;
@@ -1060,6 +1063,7 @@ PyObject* mod_h1_fast(PyObject*, PyObject* const* a, Py_ssize_t n) {
   call->timeout = timeout;
   call->conn = call->fut = call->deadline = call->sub = call->timer = call->req = nullptr;
   call->head = 0;
+  call->front = uint8_t(front);
   call->state = ST_INIT;
   call->reused = 0;
   call->path = 0;
@@ -1071,9 +1075,10 @@ PyObject* mod_h1_fast(PyObject*, PyObject* const* a, Py_ssize_t n) {
 
 // h1_fast for a caller in C (the compiled handlers): an H1Call, or None when `client` is not a
 // stock H1Client (new reference either way), NULL on error.
-PyObject* h1_call_new(PyObject* client, PyObject* method, PyObject* url, PyObject* params, PyObject* timeout) {
-  PyObject* a[5] = {client, method, url, params, timeout};
-  return mod_h1_fast(nullptr, a, 5);
+PyObject* h1_call_new(PyObject* client, PyObject* method, PyObject* url, PyObject* params, PyObject* timeout,
+                      bool front) {
+  PyObject* a[6] = {client, method, url, params, timeout, front ? Py_True : Py_False};
+  return mod_h1_fast(nullptr, a, 6);
 }
 
 namespace {
@@ -1120,7 +1125,7 @@ PyObject* mod_h1_disable(PyObject*, PyObject*) {
 
 PyMethodDef h1_functions[] = {
     {"h1_fast", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(mod_h1_fast)), METH_FASTCALL,
-     "h1_fast(client, method, url, params=None, timeout=None) -> awaitable H1Call, or None for the Python path "
+     "h1_fast(client, method, url, params=None, timeout=None, front=False) -> awaitable H1Call, or None for the Python path "
      "(sinks/h1.py)"},
     {"h1_setup", mod_h1_setup, METH_VARARGS,
      "h1_setup(H1Client, _Conn, _Origin, HttpResponse): enable h1_fast for these classes"},

@@ -30,7 +30,8 @@ namespace beholder {
 bool text_js_str_append(std::string& out, PyObject* v);
 bool text_query_pair_append(std::string& out, PyObject* k, PyObject* v, bool* first, bool rfc3986);
 PyObject* pg_pool_execute_c(PyObject* conns, PyObject* sql, PyObject* params, PyObject* spread_at, PyObject* size);
-PyObject* h1_call_new(PyObject* client, PyObject* method, PyObject* url, PyObject* params, PyObject* timeout);
+PyObject* h1_call_new(PyObject* client, PyObject* method, PyObject* url, PyObject* params, PyObject* timeout,
+                      bool front);
 bool is_native_logger(PyObject* logger);
 bool logcore_emit(PyObject* logger, bool native, long lvl, PyObject* const* args, Py_ssize_t nargs);
 bool sink_stats_record(PyObject* stats, PyObject* status, double seconds);
@@ -180,6 +181,7 @@ struct CallObject {
   uint8_t started;
   uint8_t done;
   uint8_t did_suspend;
+  uint8_t nreq;  // sink requests this event has issued (a later one is a continuation: front of the queue)
 };
 
 PyTypeObject HandlersType = {PyVarObject_HEAD_INIT(nullptr, 0)};
@@ -518,13 +520,18 @@ bool record_stats(PyObject* stats, PyObject* status, double seconds) {
 
 // http.request(method, url, params=params, timeout=timeout): for a stock H1Client whose
 // `native_call` capability is the native request path, the H1Call is made here without the
-// Python method frame.
-PyObject* http_request(HandlersObject* hs, PyObject* http, PyObject* method, PyObject* url, PyObject* params,
+// Python method frame. The event's second and later sink requests (a status event's move, then
+// its hooks: index.js:83,99,112) are continuations: if they have to wait for a connection they
+// wait at the front of the origin's queue, not behind the first requests of newer deliveries.
+PyObject* http_request(CallObject* c, PyObject* http, PyObject* method, PyObject* url, PyObject* params,
                        PyObject* timeout) {
+  HandlersObject* hs = c->hs;
+  const bool front = c->nreq > 0;
+  if (c->nreq < 255) ++c->nreq;
   PyObject** dp = _PyObject_GetDictPtr(http);
   PyObject* cur = dp && *dp ? PyDict_GetItemWithError(*dp, s_native_call) : nullptr;
   if (cur && cur == hs->h1_fast_fn) {
-    PyObject* call = h1_call_new(http, method, url, params ? params : Py_None, timeout);
+    PyObject* call = h1_call_new(http, method, url, params ? params : Py_None, timeout, front);
     if (call != Py_None) return call;  // an H1Call, or NULL with an exception
     Py_DECREF(call);  // not a stock H1Client
   } else if (PyErr_Occurred()) {
@@ -657,7 +664,7 @@ int trello_request(CallObject* c, PyObject* method, PyObject* method_upper, PyOb
     return -1;
   }
   c->req_t0 = mono_ns();
-  aw = http_request(hs, http, method_upper, url, query, timeout);  // http.request(M, url, params=, timeout=)
+  aw = http_request(c, http, method_upper, url, query, timeout);  // http.request(M, url, params=, timeout=)
   Py_DECREF(url);
   Py_DECREF(query);
   c->req_native = 1;
@@ -721,7 +728,7 @@ int sink_get(CallObject* c, PyObject* cd, std::string& url, PyObject* const* key
   } release{held};
   PyObject* full = unicode_from(url);
   if (!full) return -1;
-  PyObject* aw = http_request(c->hs, http, s_GET, full, nullptr, timeout);  // http.request("GET", full, timeout=)
+  PyObject* aw = http_request(c, http, s_GET, full, nullptr, timeout);  // http.request("GET", full, timeout=)
   Py_DECREF(full);
   c->req_t0 = mono_ns();
   c->req_native = 1;
@@ -1395,6 +1402,7 @@ PyObject* make_call(HandlersObject* hs, PyObject* rmsg, uint8_t kind) {
   c->kind = kind;
   c->state = 0;
   c->started = c->done = c->did_suspend = 0;
+  c->nreq = 0;
   PyObject_GC_Track(c);
   return reinterpret_cast<PyObject*>(c);
 }

@@ -696,11 +696,20 @@ class H1Client(HttpClient):
         o, target, rest = self._resolve(full)
         return await self._exchange(m, full, o, target, rest, deadline, c, w, reused, thrown)
 
-    def _enqueue(self, o: _Origin, deadline: float, w):
+    def _enqueue(self, o: _Origin, deadline: float, w, front: bool = False):
         """The native fast path (``ops h1_fast``) found no idle connection: queue its waiter ``w``
         as :meth:`_acquire` does (same accounting, background connects, deadline), without the
-        request loop's coroutines. Returns the deadline timer (the caller cancels it)."""
-        o.waiters.append(w)
+        request loop's coroutines. Returns the deadline timer (the caller cancels it).
+
+        ``front``: the request continues an event whose earlier sink request has completed (the
+        compiled handlers mark an event's second and later requests). It waits at the head of the
+        queue: in a burst (the first deliveries after start, or a pool at ``max_per_host``) a
+        status event's move / hook requests would otherwise queue behind every newer delivery's
+        first request, once per request, and set the tail of the handle latency."""
+        if front:
+            o.waiters.appendleft(w)
+        else:
+            o.waiters.append(w)
         self.counts["connect_waits"] += 1
         if _queued(o):
             self._grow(o, deadline)

@@ -1,16 +1,18 @@
 #!/bin/bash
-# Does anything before the headline in bench.py (TCP extras, the 15-process phase) move the
-# single-process value? Full default runs interleaved with headline-only runs on one box; each
-# line carries cpu_us_per_event and involuntary_ctx_switches of the timed steps. Output under
-# gpurun_out/$1.
-set -euo pipefail
-cd "$GRAFT_REPO_ROOT"
+# Interleaved headline A/B on one box: an older build checked out under _ab/<name> (built in-tree
+# on the CPU container, not committed) against this tree. Headline phase only: no extras, no
+# all-process phase. Usage: bash scripts/box_headline_ab.sh <out-name> [ab-dir] [runs]
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
 out=gpurun_out/${1:-headline_ab}
+other=${2:-_ab/r2}
+runs=${3:-4}
 mkdir -p "$out"
-for r in 1 2 3; do
-  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 >> $out/full.jsonl 2>> $out/full.err
-  echo "full r$r done"
-  timeout -k 10 120 python bench.py --gpus 1 --steps 20 --warmup 5 --no-extras --all-procs-steps 0 >> $out/headline.jsonl 2>> $out/headline.err
-  echo "headline r$r done"
+for i in $(seq 1 "$runs"); do
+  for side in other head; do
+    if [ "$side" = other ]; then dir=$other; else dir=.; fi
+    (cd "$dir" && timeout -k 10 300 python bench.py --no-extras --all-procs-steps 0 --steps 20 --warmup 5) \
+      >> "$out/$side.jsonl" 2>> "$out/$side.err" || exit $?
+    echo "run $i $side done"
+  done
 done
-echo done

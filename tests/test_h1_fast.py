@@ -590,3 +590,101 @@ def test_queued_request_gets_the_connect_error_of_a_failed_background_connect():
         return await one(True), await one(False)
     fast, slow = run(go())
     assert fast == slow and fast.startswith("connect ECONNREFUSED")
+
+
+class Gated(Raw):
+    """Raw server whose ``/slow`` requests are answered only once ``gate`` is set."""
+
+    def __init__(self):
+        super().__init__(lambda t: OK)
+        self.gate = asyncio.Event()
+
+    async def _serve(self, r, w):
+        self.connections += 1
+        try:
+            while True:
+                try:
+                    head = await r.readuntil(b"\r\n\r\n")
+                except (asyncio.IncompleteReadError, ConnectionError):
+                    return
+                self.raw.append(head)
+                if head.split(b" ", 2)[1].startswith(b"/slow"):
+                    await self.gate.wait()
+                w.write(OK)
+                await w.drain()
+        finally:
+            w.close()
+
+
+def test_queued_continuation_waits_at_the_front():
+    """A request marked as the continuation of an event (h1_fast's ``front``) that finds no idle
+    connection waits at the head of the origin's queue: it is sent on the next freed connection,
+    before requests that were queued earlier by other events."""
+    async def go():
+        s = await Gated().start()
+        c = H1Client(timeout_s=5, max_per_host=1)
+        base = f"http://127.0.0.1:{s.port}"
+        await c.request("GET", base + "/warm")
+        hog = asyncio.ensure_future(c.request("GET", base + "/slow"))  # holds the only connection
+        await asyncio.sleep(0.02)
+        first = [asyncio.ensure_future(c.request("GET", base + f"/n{i}")) for i in range(3)]
+        await asyncio.sleep(0.02)
+        cont = asyncio.ensure_future(c.native_call(c, "GET", base + "/cont", None, None, True))
+        await asyncio.sleep(0.02)
+        queued = len(c._origins[base].waiters)
+        s.gate.set()
+        rs = await asyncio.gather(hog, *first, cont)
+        await c.close()
+        await s.stop()
+        return queued, [r.status for r in rs], [h.split(b" ", 2)[1].decode() for h in s.raw]
+    queued, statuses, order = run(go())
+    assert queued == 4 and statuses == [200] * 5
+    assert order == ["/warm", "/slow", "/cont", "/n0", "/n1", "/n2"]
+
+
+def test_compiled_handlers_queue_an_events_later_requests_at_the_front(monkeypatch):
+    """The compiled handlers mark an event's second and later sink requests (a DEPLOYED status:
+    the Trello move, then the Telegram and Emby hooks, index.js:83,99,112) as continuations; its
+    first request queues behind earlier ones as usual."""
+    from beholder_amd.service import Service
+    from beholder_amd.store import MemoryStore
+    from beholder_amd.topics import STATUS
+    from beholder_amd.transport.memory import MemoryBroker
+    from beholder_amd.utils.log import Logger, MemoryStream
+
+    from helpers import cfg, status_msg, trello_media
+
+    seen = []
+    orig = H1Client._enqueue
+
+    def recording(self, o, deadline, w, front=False):
+        seen.append(front)
+        return orig(self, o, deadline, w, front)
+
+    monkeypatch.setattr(H1Client, "_enqueue", recording)
+
+    async def go():
+        s = await Raw(lambda t: OK).start()
+        b = MemoryBroker()
+        # keepalive 0: no idle connection is ever reused, so every request after the origin's
+        # first goes through the queue
+        http = H1Client(timeout_s=5, keepalive_s=0.0)
+        url = f"http://127.0.0.1:{s.port}"
+        await http.request("GET", url + "/warm")
+        over = {"service": {"endpoints": {"trello": url, "telegram": url}},
+                "instance": {"emby": {"host": url}}}
+        svc = Service(cfg(over), source=b.consumer(), store=MemoryStore([trello_media("m1", card="C1")]), http=http,
+                      logger=Logger(stream=MemoryStream()), serve_metrics=False)
+        await svc.init()
+        run_ = asyncio.ensure_future(svc.run())
+        b.publish(STATUS, status_msg("m1", "DEPLOYED"))
+        b.finish()
+        stats = await run_
+        await svc.close()
+        await http.close()
+        await s.stop()
+        return stats["source"]["acked"], [h.split(b" ", 2)[:2] for h in s.raw], type(svc.handler_impl).__name__
+    acked, reqs, impl = run(go())
+    assert acked == 1 and impl == "NativeHandlers"
+    assert len(reqs) - 1 == len(seen) >= 2, (reqs, seen)
+    assert seen[0] is False and all(seen[1:]), seen
