@@ -518,6 +518,10 @@ bool record_stats(PyObject* stats, PyObject* status, double seconds) {
   return true;
 }
 
+void count_request(CallObject* c) {
+  if (c->nreq < 255) ++c->nreq;
+}
+
 // http.request(method, url, params=params, timeout=timeout): for a stock H1Client whose
 // `native_call` capability is the native request path, the H1Call is made here without the
 // Python method frame. The event's second and later sink requests (a status event's move, then
@@ -527,7 +531,7 @@ PyObject* http_request(CallObject* c, PyObject* http, PyObject* method, PyObject
                        PyObject* timeout) {
   HandlersObject* hs = c->hs;
   const bool front = c->nreq > 0;
-  if (c->nreq < 255) ++c->nreq;
+  count_request(c);
   PyObject** dp = _PyObject_GetDictPtr(http);
   PyObject* cur = dp && *dp ? PyDict_GetItemWithError(*dp, s_native_call) : nullptr;
   if (cur && cur == hs->h1_fast_fn) {
@@ -629,6 +633,7 @@ int trello_request(CallObject* c, PyObject* method, PyObject* method_upper, PyOb
   PyObject* aw;
   if (!td) {
     PyObject* args[4] = {trello, method, path, query};
+    count_request(c);  // a sink request through the client's own method
     aw = PyObject_VectorcallMethod(s_make_request, args, 4, nullptr);
     Py_DECREF(query);
     if (!aw) return -1;
@@ -784,6 +789,7 @@ int hook_telegram(CallObject* c, PyObject** out) {
     }
     PyObject* args[5] = {tg, PyTuple_GET_ITEM(plan, 1), textobj, hs->x[X_PARSE_MODE], tok};
     PyObject* kw = PyTuple_Pack(1, s_token);
+    count_request(c);  // a sink request through the client's own method
     PyObject* aw = kw ? PyObject_VectorcallMethod(s_send_message, args, 4, kw) : nullptr;
     Py_XDECREF(kw);
     Py_DECREF(textobj);
@@ -828,6 +834,7 @@ int hook_emby(CallObject* c, PyObject** out) {
     if (!em) return -1;
     PyObject* args[3] = {em, host, key};
     PyObject* kw = PyTuple_Pack(2, s_host, s_api_key);
+    count_request(c);  // a sink request through the client's own method
     PyObject* aw = kw ? PyObject_VectorcallMethod(s_refresh_library, args, 1, kw) : nullptr;
     Py_XDECREF(kw);
     if (!aw) return -1;
