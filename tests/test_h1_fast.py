@@ -642,10 +642,12 @@ def test_queued_continuation_waits_at_the_front():
     assert order == ["/warm", "/slow", "/cont", "/n0", "/n1", "/n2"]
 
 
-def test_compiled_handlers_queue_an_events_later_requests_at_the_front(monkeypatch):
+@pytest.mark.parametrize("trello_retry", [False, True])
+def test_compiled_handlers_queue_an_events_later_requests_at_the_front(monkeypatch, trello_retry):
     """The compiled handlers mark an event's second and later sink requests (a DEPLOYED status:
     the Trello move, then the Telegram and Emby hooks, index.js:83,99,112) as continuations; its
-    first request queues behind earlier ones as usual."""
+    first request queues behind earlier ones as usual. A Trello client with 429 retries sends
+    through its own Python method (unmarked), and still counts as the event's first request."""
     from beholder_amd.service import Service
     from beholder_amd.store import MemoryStore
     from beholder_amd.topics import STATUS
@@ -673,6 +675,8 @@ def test_compiled_handlers_queue_an_events_later_requests_at_the_front(monkeypat
         await http.request("GET", url + "/warm")
         over = {"service": {"endpoints": {"trello": url, "telegram": url}},
                 "instance": {"emby": {"host": url}}}
+        if trello_retry:
+            over["service"]["sinks"] = {"trello": {"retry_429": 1}}
         svc = Service(cfg(over), source=b.consumer(), store=MemoryStore([trello_media("m1", card="C1")]), http=http,
                       logger=Logger(stream=MemoryStream()), serve_metrics=False)
         await svc.init()
