@@ -86,37 +86,44 @@ class GcPauses:
 
 
 class _Producer(threading.Thread):
-    """Writes pre-framed events into a pipe at ``rate`` events/s (0 = unpaced)."""
+    """Writes pre-framed events into a pipe at ``rate`` events/s (0 = unpaced).
+
+    Paced runs go through :func:`~beholder_amd.ops.paced_write`: the pacing loop is native and
+    holds no GIL (clock_nanosleep to each event's due time, 1 ns timer slack), so the producer
+    neither competes with the consumer's event loop for the GIL nor adds its own wake-up jitter to
+    the receive→ack latency of BASELINE configs 2-4."""
 
     def __init__(self, wfd: int, events, rate: float):
         super().__init__(daemon=True, name="producer")
+        from array import array
+
         from ..ops import frame
         self.wfd = wfd
         self.rate = rate
-        self.chunks = [frame(t, p) for t, p in events]
-        self.offered = len(self.chunks)
+        chunks = [frame(t, p) for t, p in events]
+        self.offered = len(chunks)
+        ends = array("Q")
+        pos = 0
+        for c in chunks:
+            pos += len(c)
+            ends.append(pos)
+        self.data = b"".join(chunks)
+        self.ends = ends.tobytes()
         self.elapsed = 0.0
+        self.writes = 0
 
     def run(self):
         try:
-            t0 = time.perf_counter()
             if self.rate <= 0:
-                data = b"".join(self.chunks)
-                mv = memoryview(data)
+                t0 = time.perf_counter()
+                mv = memoryview(self.data)
                 while mv:
                     n = os.write(self.wfd, mv[:1 << 20])
                     mv = mv[n:]
+                self.elapsed = time.perf_counter() - t0
             else:
-                sent = 0
-                n = len(self.chunks)
-                while sent < n:
-                    due = min(n, int((time.perf_counter() - t0) * self.rate) + 1)
-                    if due > sent:
-                        os.write(self.wfd, b"".join(self.chunks[sent:due]))
-                        sent = due
-                    else:
-                        time.sleep(0.0002)
-            self.elapsed = time.perf_counter() - t0
+                from ..ops import paced_write
+                self.elapsed, self.writes = paced_write(self.wfd, self.data, self.ends, float(self.rate))
         except OSError:
             pass
         finally:
@@ -209,6 +216,10 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
         "offered_rate_eps": prod.offered / prod.elapsed if prod.elapsed else 0.0,
         "ingest_latency_us": {k: v / 1e3 for k, v in stats["ingest_latency_ns"].items() if k.startswith("p")},
         "handle_latency_us": {k: v / 1e3 for k, v in stats["handle_latency_ns"].items() if k.startswith("p")},
+        # the two hops of ingest latency: reader push -> handler start (ring + loop wake), start -> ack
+        "queue_latency_us": {k: v / 1e3 for k, v in stats["queue_latency_ns"].items() if k.startswith("p")},
+        "idle_wakeups": s.get("idle_wakeups"),
+        "producer_writes": prod.writes,
         "producer_blocked_ms": s["blocked_ns"] / 1e6, "ring_high_water": s["high_water_events"],
         "sink_requests": (http.count if hasattr(http, "count") else
                           http.counts["requests"] if hasattr(http, "counts") else None),
@@ -288,6 +299,9 @@ def run_config(name: str, *, duration_s: Optional[float] = None, events: Optiona
     return res
 
 
+SLOW_TRACE_NS = 500_000  # deliveries slower than this (start -> ack) are traced for attribution
+
+
 def _settled(settler) -> int:
     return settler.acked + settler.abandoned + settler.nacked + settler.rejected
 
@@ -348,9 +362,12 @@ def _spawn(module: str, copies: int = 1, args=()) -> "tuple":
     return port, procs
 
 
-def _reap(procs) -> Dict[str, int]:
-    """SIGTERM the endpoint processes; sums their ``DONE key=value`` counters."""
+def _reap(procs, stalls: Optional[list] = None) -> Dict[str, int]:
+    """SIGTERM the endpoint processes; sums their ``DONE key=value`` counters. ``stalls``
+    collects each process's ``STALLS`` report (:mod:`.stallmon`)."""
     import subprocess
+
+    from .stallmon import parse_stall_lines
     total: Dict[str, int] = {}
     for p in procs:
         if p.poll() is None:
@@ -366,7 +383,31 @@ def _reap(procs) -> Dict[str, int]:
                     k, _, v = kv.partition("=")
                     if v.isdigit():
                         total[k] = total.get(k, 0) + int(v)
+        if stalls is not None:
+            stalls.extend(parse_stall_lines(out))
     return total
+
+
+def _slowest(slow, n_measured: int, frac: float = 0.001) -> list:
+    """The slowest ``frac`` of ``n_measured`` deliveries among the traced ``(recv, start, settle)``."""
+    k = max(1, int(round(n_measured * frac)))
+    return sorted(slow, key=lambda x: x[2] - x[1], reverse=True)[:k]
+
+
+def _attribution(slow, consumer, fakes: list) -> dict:
+    """Blames the slow deliveries on the process that stalled under them (:func:`.stallmon.attribute`),
+    and reports each process's own loop lag / GC figures next to it."""
+    from .stallmon import attribute
+    sources: Dict[str, list] = {"consumer": consumer.loop_stalls + consumer.gc_pauses}
+    per_proc = {"consumer": consumer.summary()}
+    for i, f in enumerate(fakes):
+        name = f.get("name", "fake")
+        sources.setdefault(name, []).extend(tuple(x) for x in f.get("stall_intervals", []))
+        per_proc[f"{name}{i}"] = {k: v for k, v in f.items() if k not in ("stall_intervals", "name")}
+    out = attribute(slow, sources)
+    out["slowest_us"] = [round((e - s) / 1e3, 1) for _, s, e in slow[:5]]
+    out["processes"] = per_proc
+    return out
 
 
 def _http_tcp(w: Workload, n: int, servers: int = 3, clients=("h1", "aiohttp")) -> dict:
@@ -406,12 +447,15 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
     from ..sinks import H1Client
     from ..store.postgres import PostgresStore
     from ..transport.amqp import AmqpSource
+    from ..utils.hostinfo import cgroup_cpu_stat, cgroup_delta
     from ..utils.log import Logger
+    from .stallmon import StallMonitor
 
     warm = min(5000, n // 10)
     bport, bprocs = _spawn("beholder_amd.bench.replay_broker", 1, ("--events", str(n)))
     procs = list(bprocs)
     out: dict = {"events": n, "prefetch": 100, "preconnect": preconnect, "max_connecting": max_connecting}
+    diag = None
     try:
         hport, hp = _spawn("beholder_amd.bench.http_sink_server", http_servers, ("--tls",) if tls else ())
         procs += hp
@@ -436,20 +480,31 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             svc = Service(Config.from_dict(cfgd), source=src, store=store, http=http, logger=Logger(stream=sink),
                           serve_metrics=False)
             await svc.init()
+            mon = StallMonitor().start()
+            src.settler.trace_slow(SLOW_TRACE_NS)
+            cg0 = cgroup_cpu_stat()
             task = asyncio.ensure_future(svc.run())
             # warm-up: connection pools fill (up to prefetch sink connections, the PG pool), code
             # paths get hot; then the latency histograms restart and the clock starts
             await _wait_acked(src.settler, warm, task)
             cold = dict(src.settler.handle_latency.summary())
+            warm_slow = _slowest(src.settler.slow_deliveries()[0], _settled(src.settler))
+            warm_mon = (list(mon.loop_stalls), list(mon.gc_pauses))
             src.settler.reset_latency()
+            src.settler.trace_slow(SLOW_TRACE_NS)
             settled0 = _settled(src.settler)
             gc.collect()
+            mon.reset()
             rss0 = _rss_mb()  # pools full, code paths warm: later growth would be a leak
+            cg1 = cgroup_cpu_stat()
             ru0 = resource.getrusage(resource.RUSAGE_SELF)
             t0 = time.perf_counter()
             await _wait_acked(src.settler, n, task)
             elapsed = time.perf_counter() - t0
             ru1 = resource.getrusage(resource.RUSAGE_SELF)
+            cg2 = cgroup_cpu_stat()
+            mon.stop()
+            steady_slow = _slowest(src.settler.slow_deliveries()[0], _settled(src.settler) - settled0)
             gc.collect()
             rss1 = _rss_mb()
             measured = _settled(src.settler) - settled0
@@ -462,9 +517,12 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             await svc.close()
             sink.close()
             cpu = (ru1.ru_utime + ru1.ru_stime) - (ru0.ru_utime + ru0.ru_stime)
-            return elapsed, stats, cpu, ru1.ru_stime - ru0.ru_stime, pg_conns, http_stats, measured, cold, rss1 - rss0
+            diag = {"warm_slow": warm_slow, "steady_slow": steady_slow, "mon": mon, "warm_mon": warm_mon,
+                    "nivcsw": ru1.ru_nivcsw - ru0.ru_nivcsw, "cgroup_warmup": cgroup_delta(cg0, cg1),
+                    "cgroup_steady": cgroup_delta(cg1, cg2)}
+            return elapsed, stats, cpu, ru1.ru_stime - ru0.ru_stime, pg_conns, http_stats, measured, cold, rss1 - rss0, diag
 
-        elapsed, stats, cpu, sys_s, pg_conns, http_stats, m, cold, rss_growth = asyncio.run(go())
+        elapsed, stats, cpu, sys_s, pg_conns, http_stats, m, cold, rss_growth, diag = asyncio.run(go())
         acked = stats["source"]["acked"]
         out.update({
             "acked": acked, "warmup_events": warm, "measured_events": m, "elapsed_s": elapsed,
@@ -475,10 +533,18 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             "warmup_handle_latency_us": {k: v / 1e3 for k, v in cold.items() if k.startswith("p")},
             "errors": sum(stats.get("handler_errors", {}).values()),
             "pg_connections": pg_conns, "http": http_stats, "rss_growth_mb": round(rss_growth, 2),
+            "nivcsw": diag["nivcsw"], "cgroup_warmup": diag["cgroup_warmup"], "cgroup_steady": diag["cgroup_steady"],
         })
     finally:
-        counters = _reap(procs)
+        stalls: list = []
+        counters = _reap(procs, stalls)
         out["server_side"] = counters
+    if diag is not None:
+        mon = diag["mon"]
+        out["attribution_steady"] = _attribution(diag["steady_slow"], mon, stalls)
+        warm_mon = StallMonitor()
+        warm_mon.loop_stalls, warm_mon.gc_pauses = diag["warm_mon"]
+        out["attribution_warmup"] = _attribution(diag["warm_slow"], warm_mon, stalls)
     return out
 
 
@@ -546,12 +612,47 @@ def _amqp(n: int) -> dict:
             "ack_frames": stats["source"].get("ack_frames")}
 
 
-def _plumbing(w: Workload) -> dict:
-    """Config 1: 100 events on the stdin of the real CLI process."""
+def _free_port() -> int:
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _scrape(port: int, path: str = "/metrics", timeout: float = 2.0) -> Optional[str]:
+    import urllib.request
+    try:
+        with urllib.request.urlopen(f"http://127.0.0.1:{port}{path}", timeout=timeout) as r:
+            return r.read().decode()
+    except OSError:
+        return None
+
+
+def _metric_value(text: str, name: str, labels: str = "") -> Optional[float]:
+    """Value of ``name{labels}`` in a Prometheus text exposition (first match)."""
+    want = f"{name}{{{labels}}}" if labels else name
+    for ln in text.splitlines():
+        if ln.startswith("#"):
+            continue
+        key, _, val = ln.rpartition(" ")
+        if key == want:
+            return float(val)
+    return None
+
+
+def _plumbing(w: Workload, *, timeout_s: float = 120.0) -> dict:
+    """Config 1: 100 events on the stdin of the real CLI process (``python -m beholder_amd run
+    --source stdin``, the analogue of ``node index.js``, package.json:5, index.js:160).
+
+    The events go in, then ``/metrics`` is scraped over HTTP while the process still runs (stdin
+    open) until all 100 deliveries show as acked; then stdin closes and the process must exit 0.
+    Reports whether both reference counters (index.js:29-40) are in the scrape."""
     import yaml
 
     from .fakes import FakeHttpServer
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    port = _free_port()
+    scrape = None
     with tempfile.TemporaryDirectory() as td, FakeHttpServer() as fake:
         cfgd = bench_config()
         cfgd["service"]["endpoints"] = {"trello": fake.url, "telegram": fake.url}
@@ -567,19 +668,46 @@ def _plumbing(w: Workload) -> dict:
         data = w.framed(100)
         env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
         t0 = time.perf_counter()
-        p = subprocess.run([sys.executable, "-m", "beholder_amd", "run", "--config", cp, "--media-fixture", mp,
-                            "--stats"], input=data, capture_output=True, timeout=300, env=env, cwd=root)
+        p = subprocess.Popen([sys.executable, "-m", "beholder_amd", "run", "--config", cp, "--media-fixture", mp,
+                              "--source", "stdin", "--metrics-port", str(port), "--stats"],
+                             stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env, cwd=root,
+                             preexec_fn=_die_with_parent())
+        try:
+            p.stdin.write(data)
+            p.stdin.flush()
+            deadline = time.monotonic() + timeout_s
+            while time.monotonic() < deadline and p.poll() is None:
+                text = _scrape(port)
+                if text is not None and (_metric_value(text, "beholder_deliveries", 'state="acked"') or 0) >= 100:
+                    scrape = text
+                    break
+                time.sleep(0.05)
+            # communicate() closes stdin (EOF: the service drains and exits) and collects the output
+            out, err = p.communicate(timeout=max(5.0, deadline - time.monotonic()))
+        except BaseException:
+            p.kill()
+            p.communicate()
+            raise
         elapsed = time.perf_counter() - t0
     if p.returncode != 0:
-        raise RuntimeError(f"plumbing run failed ({p.returncode}): {p.stderr.decode()[-2000:]}")
-    stats = json.loads(p.stderr.decode().strip().splitlines()[-1])
-    lines = [json.loads(x) for x in p.stdout.decode().splitlines() if x.startswith("{")]
+        raise RuntimeError(f"plumbing run failed ({p.returncode}): {err.decode()[-2000:]}")
+    stats = json.loads(err.decode().strip().splitlines()[-1])
+    lines = [json.loads(x) for x in out.decode().splitlines() if x.startswith("{")]
     s = stats["source"]
-    return {"config": "plumbing", "offered": 100, "acked": s["acked"], "abandoned": s["abandoned"],
+    scrape = scrape or ""
+    return {"config": "plumbing", "offered": 100, "rc": p.returncode, "acked": s["acked"], "abandoned": s["abandoned"],
             "errors": sum(stats.get("handler_errors", {}).values()), "process_wall_s": elapsed,
             "http_requests": len(fake.requests),
             "log_lines": len(lines), "warn_lines": sum(1 for x in lines if x["level"] == 40),
-            "received": stats["received"]}
+            "received": stats["received"],
+            "metrics_scraped": bool(scrape),
+            "scrape_acked": _metric_value(scrape, "beholder_deliveries", 'state="acked"'),
+            # the reference's two counters (index.js:29-40): names, the "crreated" typo, no _total on comments
+            "scrape_has_progress_counter": "\n# TYPE beholder_progress_updates_total counter" in scrape
+                                           and "beholder_progress_updates_total{" in scrape,
+            "scrape_has_trello_counter": "\n# TYPE beholder_trello_comments counter" in scrape
+                                         and "\nbeholder_trello_comments " in scrape,
+            "scrape_trello_comments": _metric_value(scrape, "beholder_trello_comments")}
 
 
 def main(argv: Optional[List[str]] = None) -> int:

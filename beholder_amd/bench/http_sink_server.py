@@ -20,6 +20,8 @@ import socket
 import ssl
 import sys
 
+from .stallmon import fake_monitor
+
 _RESP = b"HTTP/1.1 200 OK\r\nContent-Type: application/json; charset=utf-8\r\nContent-Length: 2\r\n\r\n{}"
 
 
@@ -92,12 +94,15 @@ async def main(port: int, tls: bool = False) -> int:
     if ctx is not None:
         warm_up(ctx)
     srv = await loop.create_server(_Proto, sock=sock, backlog=1024, ssl=ctx)
+    mon = fake_monitor()
     print(f"READY {sock.getsockname()[1]}", flush=True)
     stop = loop.create_future()
     loop.add_signal_handler(signal.SIGTERM, lambda: stop.done() or stop.set_result(None))
     await stop
     srv.close()
+    mon.stop()
     print(f"DONE requests={_Proto.count}", flush=True)
+    print(mon.dump_line("https" if tls else "http"), flush=True)
     return 0
 
 

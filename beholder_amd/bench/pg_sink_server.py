@@ -21,6 +21,8 @@ import socket
 import struct
 import sys
 
+from .stallmon import fake_monitor
+
 _U32 = struct.Struct("!I")
 
 
@@ -156,12 +158,15 @@ async def main(port: int, media: int, seed: int) -> int:
     sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
     sock.bind(("127.0.0.1", port))
     srv = await loop.create_server(_Proto, sock=sock, backlog=1024)
+    mon = fake_monitor()
     print(f"READY {sock.getsockname()[1]}", flush=True)
     stop = loop.create_future()
     loop.add_signal_handler(signal.SIGTERM, lambda: stop.done() or stop.set_result(None))
     await stop
     srv.close()
+    mon.stop()
     print(f"DONE queries={_Proto.queries}", flush=True)
+    print(mon.dump_line("pg"), flush=True)
     return 0
 
 

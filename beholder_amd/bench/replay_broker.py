@@ -156,9 +156,14 @@ async def _main(a) -> None:
     w = Workload(n_media=a.media, seed=a.seed)
     events = [(TOPIC_NAMES_BY_ID[t], p) for t, p in w.events(a.events)]
     b = await ReplayBroker(events, a.port).start()
+    del w
+    from .stallmon import fake_monitor
+    mon = fake_monitor()
     print(f"READY {b.port}", flush=True)
     await b.done.wait()
+    mon.stop()
     print(f"DONE sent={b.sent} acked={b.acked} broker_s={b.t_done - b.t_first:.6f}", flush=True)
+    print(mon.dump_line("broker"), flush=True)
     await asyncio.sleep(0.5)
 
 

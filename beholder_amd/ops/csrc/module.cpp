@@ -101,7 +101,42 @@ PyObject* mod_frames_impl(PyObject*, PyObject* it_in) {
   return PyBytes_FromStringAndSize(out.data(), Py_ssize_t(out.size()));
 }
 
+// calib(iters) -> ns: a fixed amount of integer work (xorshift mixing through a
+// 16 KiB, L1-resident table; a dependent chain, so neither vectorised nor
+// removable). Its time moves only with the core's clock and with other load on
+// the core, never with this service's code, so the bench line can tell a slow
+// box from a slow build. Runs without the GIL.
+PyObject* mod_calib(PyObject*, PyObject* args) {
+  unsigned long long iters;
+  if (!PyArg_ParseTuple(args, "K", &iters)) return nullptr;
+  int64_t t0, t1;
+  uint64_t acc;
+  Py_BEGIN_ALLOW_THREADS
+  uint32_t table[4096];
+  uint64_t x = 0x9E3779B97F4A7C15ull;
+  for (uint32_t i = 0; i < 4096; ++i) {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    table[i] = uint32_t(x);
+  }
+  t0 = mono_ns();
+  acc = 0;
+  for (unsigned long long i = 0; i < iters; ++i) {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    uint32_t v = table[(x ^ acc) & 4095];
+    acc = (acc * 31) + v;
+    table[acc & 4095] = v ^ uint32_t(i);
+  }
+  t1 = mono_ns();
+  Py_END_ALLOW_THREADS
+  return Py_BuildValue("(LK)", (long long)(t1 - t0), (unsigned long long)acc);
+}
+
 PyMethodDef module_methods[] = {
+    {"calib", mod_calib, METH_VARARGS, "calib(iters) -> (ns, checksum): fixed-work CPU calibration loop"},
     {"configure", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(mod_configure)),
      METH_VARARGS | METH_KEYWORDS, "configure(decode_error=None, topics=None)"},
     {"mono_ns", mod_mono_ns, METH_NOARGS, "CLOCK_MONOTONIC in ns (same clock as time.monotonic_ns)"},

@@ -49,10 +49,16 @@ extern PyTypeObject CounterType;
 struct SettlerObject {
   PyObject_HEAD HistogramObject* handle_hist;  // start() -> settle, ns
   HistogramObject* ingest_hist;                // recv -> settle, ns
+  HistogramObject* queue_hist;                 // recv -> start(), ns (ring + loop wait)
   uint64_t created, acked, nacked, rejected, abandoned;
   PyObject* on_settle;   // optional callable(delivery, kind:str, requeue:bool)
   PyObject* on_abandon;  // optional callable(tag, topic_id, content)
   PyObject* batcher;     // optional AckBatcher: acks of its channel's deliveries stay in C
+  // slow-delivery trace (bench attribution): (recv, start, settle) ns of every delivery whose
+  // start->settle took >= slow_threshold_ns, up to slow_cap entries; 0 = off
+  int64_t slow_threshold_ns;
+  uint64_t slow_cap, slow_dropped;
+  void* slow;  // std::vector<int64_t>*, owned (3 values per entry)
 };
 
 // AckBatcher hooks (py_acks.cpp): 1 = handled, 0 = other channel, -1 = error

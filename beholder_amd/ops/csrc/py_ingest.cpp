@@ -10,6 +10,8 @@
 //     acked — quirk Q1 (status handler threw). It is counted as `abandoned`
 //     and reported to `on_abandon` so a source can dead-letter / redeliver it.
 #include <poll.h>
+#include <sys/eventfd.h>
+#include <sys/prctl.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -33,7 +35,8 @@ PyObject* settler_new(PyTypeObject* type, PyObject*, PyObject*) {
   if (!self) return nullptr;
   self->handle_hist = reinterpret_cast<HistogramObject*>(PyObject_CallNoArgs(reinterpret_cast<PyObject*>(&HistogramType)));
   self->ingest_hist = reinterpret_cast<HistogramObject*>(PyObject_CallNoArgs(reinterpret_cast<PyObject*>(&HistogramType)));
-  if (!self->handle_hist || !self->ingest_hist) {
+  self->queue_hist = reinterpret_cast<HistogramObject*>(PyObject_CallNoArgs(reinterpret_cast<PyObject*>(&HistogramType)));
+  if (!self->handle_hist || !self->ingest_hist || !self->queue_hist) {
     Py_DECREF(self);
     return nullptr;
   }
@@ -41,6 +44,9 @@ PyObject* settler_new(PyTypeObject* type, PyObject*, PyObject*) {
   self->on_settle = nullptr;
   self->batcher = nullptr;
   self->on_abandon = nullptr;
+  self->slow_threshold_ns = 0;
+  self->slow_cap = self->slow_dropped = 0;
+  self->slow = nullptr;
   return reinterpret_cast<PyObject*>(self);
 }
 
@@ -101,6 +107,8 @@ void settler_dealloc(SettlerObject* self) {
   settler_clear(self);
   Py_XDECREF(self->handle_hist);
   Py_XDECREF(self->ingest_hist);
+  Py_XDECREF(self->queue_hist);
+  delete static_cast<std::vector<int64_t>*>(self->slow);
   Py_TYPE(self)->tp_free(reinterpret_cast<PyObject*>(self));
 }
 
@@ -116,7 +124,49 @@ PyObject* settler_stats(SettlerObject* self, PyObject*) {
 PyObject* settler_reset_latency(SettlerObject* self, PyObject*) {
   self->handle_hist->h->reset();
   self->ingest_hist->h->reset();
+  self->queue_hist->h->reset();
   Py_RETURN_NONE;
+}
+
+// trace_slow(threshold_ns, capacity=65536): start recording (recv, start, settle) of deliveries
+// whose start->settle time is >= threshold_ns (0 stops and clears). slow_deliveries() returns
+// them as a list of tuples and the count that did not fit.
+PyObject* settler_trace_slow(SettlerObject* self, PyObject* args) {
+  long long thr;
+  unsigned long long cap = 65536;
+  if (!PyArg_ParseTuple(args, "L|K", &thr, &cap)) return nullptr;
+  auto* v = static_cast<std::vector<int64_t>*>(self->slow);
+  if (!v) {
+    v = new (std::nothrow) std::vector<int64_t>();
+    if (!v) return PyErr_NoMemory();
+    self->slow = v;
+  }
+  v->clear();
+  try {
+    v->reserve(size_t(cap) * 3);  // settle() appends without allocating (it must not throw)
+  } catch (const std::exception&) {
+    return PyErr_NoMemory();
+  }
+  self->slow_dropped = 0;
+  self->slow_threshold_ns = thr > 0 ? thr : 0;
+  self->slow_cap = cap;
+  Py_RETURN_NONE;
+}
+
+PyObject* settler_slow_deliveries(SettlerObject* self, PyObject*) {
+  auto* v = static_cast<std::vector<int64_t>*>(self->slow);
+  size_t n = v ? v->size() / 3 : 0;
+  PyObject* list = PyList_New(Py_ssize_t(n));
+  if (!list) return nullptr;
+  for (size_t i = 0; i < n; ++i) {
+    PyObject* t = Py_BuildValue("(LLL)", (long long)(*v)[3 * i], (long long)(*v)[3 * i + 1], (long long)(*v)[3 * i + 2]);
+    if (!t) {
+      Py_DECREF(list);
+      return nullptr;
+    }
+    PyList_SET_ITEM(list, Py_ssize_t(i), t);
+  }
+  return Py_BuildValue("(NK)", list, (unsigned long long)self->slow_dropped);
 }
 
 PyObject* settler_get_handle(SettlerObject* self, void*) {
@@ -126,6 +176,10 @@ PyObject* settler_get_handle(SettlerObject* self, void*) {
 PyObject* settler_get_ingest(SettlerObject* self, void*) {
   Py_INCREF(self->ingest_hist);
   return reinterpret_cast<PyObject*>(self->ingest_hist);
+}
+PyObject* settler_get_queue(SettlerObject* self, void*) {
+  Py_INCREF(self->queue_hist);
+  return reinterpret_cast<PyObject*>(self->queue_hist);
 }
 #define SETTLER_U64(fld)                                                     \
   PyObject* settler_get_##fld(SettlerObject* self, void*) {                  \
@@ -143,11 +197,17 @@ PyObject* settler_get_pending(SettlerObject* self, void*) {
 PyMethodDef settler_methods[] = {
     {"stats", reinterpret_cast<PyCFunction>(settler_stats), METH_NOARGS, "settlement counters"},
     {"reset_latency", reinterpret_cast<PyCFunction>(settler_reset_latency), METH_NOARGS, "clear histograms"},
+    {"trace_slow", reinterpret_cast<PyCFunction>(settler_trace_slow), METH_VARARGS,
+     "trace_slow(threshold_ns, capacity=65536): record (recv, start, settle) of slow deliveries (0 = off)"},
+    {"slow_deliveries", reinterpret_cast<PyCFunction>(settler_slow_deliveries), METH_NOARGS,
+     "-> ([(recv_ns, start_ns, settle_ns), ...], dropped)"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyGetSetDef settler_getset[] = {
     {"handle_latency", reinterpret_cast<getter>(settler_get_handle), nullptr, "start()->settle ns", nullptr},
     {"ingest_latency", reinterpret_cast<getter>(settler_get_ingest), nullptr, "receive->settle ns", nullptr},
+    {"queue_latency", reinterpret_cast<getter>(settler_get_queue), nullptr,
+     "receive->start() ns (ring + event-loop wait; ingest = queue + handle)", nullptr},
     {"created", reinterpret_cast<getter>(settler_get_created), nullptr, nullptr, nullptr},
     {"acked", reinterpret_cast<getter>(settler_get_acked), nullptr, nullptr, nullptr},
     {"nacked", reinterpret_cast<getter>(settler_get_nacked), nullptr, nullptr, nullptr},
@@ -278,6 +338,18 @@ PyObject* settle(DeliveryObject* self, uint8_t to, const char* kind, bool requeu
     int64_t now = mono_ns();
     if (self->start_ns > 0) s->handle_hist->h->record(uint64_t(now > self->start_ns ? now - self->start_ns : 0));
     if (self->recv_ns > 0) s->ingest_hist->h->record(uint64_t(now > self->recv_ns ? now - self->recv_ns : 0));
+    if (self->recv_ns > 0 && self->start_ns > 0)
+      s->queue_hist->h->record(uint64_t(self->start_ns > self->recv_ns ? self->start_ns - self->recv_ns : 0));
+    if (s->slow_threshold_ns > 0 && self->start_ns > 0 && now - self->start_ns >= s->slow_threshold_ns) {
+      auto* v = static_cast<std::vector<int64_t>*>(s->slow);
+      if (v->size() / 3 < s->slow_cap) {
+        v->push_back(self->recv_ns);
+        v->push_back(self->start_ns);
+        v->push_back(now);
+      } else {
+        s->slow_dropped++;
+      }
+    }
     if (to == D_ACKED)
       s->acked++;
     else if (to == D_NACKED)
@@ -434,6 +506,7 @@ struct IngestObject {
   uint32_t max_frame;
   int fd;
   int own_fd;
+  int efd;  // eventfd the ring signals when the armed event loop may pop (-1 until notify_fd is read)
 };
 
 void set_error(IngestObject* self, const std::string& e) {
@@ -525,6 +598,7 @@ PyObject* ingest_new(PyTypeObject* type, PyObject*, PyObject*) {
   self->max_frame = 16u << 20;
   self->fd = -1;
   self->own_fd = 0;
+  self->efd = -1;
   return reinterpret_cast<PyObject*>(self);
 }
 
@@ -584,7 +658,8 @@ int ingest_init_impl(IngestObject* self, PyObject* args, PyObject* kwds) {
 
 void ingest_dealloc(IngestObject* self) {
   if (self->ring) ingest_stop_reader(self);
-  delete self->ring;
+  delete self->ring;  // nothing signals the eventfd any more
+  if (self->efd >= 0) close(self->efd);
   delete self->stop;
   delete self->bytes_read;
   delete self->frames_read;
@@ -806,6 +881,41 @@ PyObject* ingest_get_settler(IngestObject* self, void*) {
   Py_INCREF(self->settler);
   return reinterpret_cast<PyObject*>(self->settler);
 }
+// notify_fd: eventfd for loop.add_reader; created on first use and owned by the Ingest.
+PyObject* ingest_get_notify_fd(IngestObject* self, void*) {
+  if (!check_ready(self)) return nullptr;
+  if (self->efd < 0) {
+    int fd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    if (fd < 0) return PyErr_SetFromErrno(PyExc_OSError);
+    self->efd = fd;
+    self->ring->set_notify_fd(fd);
+  }
+  return PyLong_FromLong(self->efd);
+}
+
+// arm() -> bool: True = parked (the next push / EOF / close signals notify_fd);
+// False = something is already poppable, pop again instead of waiting.
+PyObject* ingest_arm(IngestObject* self, PyObject*) {
+  if (!check_ready(self)) return nullptr;
+  if (self->efd < 0) {
+    PyErr_SetString(PyExc_RuntimeError, "arm() before notify_fd was created");
+    return nullptr;
+  }
+  return PyBool_FromLong(self->ring->arm());
+}
+
+// clear_notify(): drains the eventfd counter (readiness callback; never blocks).
+PyObject* ingest_clear_notify(IngestObject* self, PyObject*) {
+  if (self->efd >= 0) {
+    uint64_t v;
+    ssize_t r;
+    do {
+      r = read(self->efd, &v, sizeof v);
+    } while (r < 0 && errno == EINTR);
+  }
+  Py_RETURN_NONE;
+}
+
 PyObject* ingest_get_depth(IngestObject* self, void*) {
   if (!check_ready(self)) return nullptr;
   return PyLong_FromSize_t(self->ring->depth_events());
@@ -824,12 +934,17 @@ PyMethodDef ingest_methods[] = {
     {"pop", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(ingest_pop)), METH_VARARGS | METH_KEYWORDS,
      "pop(max_n=256, timeout=-1.0) -> list[Delivery] | None when drained"},
     {"close", reinterpret_cast<PyCFunction>(ingest_close), METH_NOARGS, "stop the reader and close"},
+    {"arm", reinterpret_cast<PyCFunction>(ingest_arm), METH_NOARGS,
+     "arm() -> True if parked until notify_fd is signalled, False if a pop would succeed now"},
+    {"clear_notify", reinterpret_cast<PyCFunction>(ingest_clear_notify), METH_NOARGS, "drain notify_fd"},
     {"stats", reinterpret_cast<PyCFunction>(ingest_stats), METH_NOARGS, "ring / reader statistics"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyGetSetDef ingest_getset[] = {
     {"settler", reinterpret_cast<getter>(ingest_get_settler), nullptr, "Settler of popped deliveries", nullptr},
     {"depth", reinterpret_cast<getter>(ingest_get_depth), nullptr, "records queued", nullptr},
+    {"notify_fd", reinterpret_cast<getter>(ingest_get_notify_fd), nullptr,
+     "eventfd signalled once per arm() by the next push / EOF / close (for loop.add_reader)", nullptr},
     {"drained", reinterpret_cast<getter>(ingest_get_drained), nullptr, "EOF/closed and empty", nullptr},
     {nullptr, nullptr, nullptr, nullptr, nullptr}};
 
@@ -837,7 +952,104 @@ PyGetSetDef ingest_getset[] = {
 
 PyTypeObject IngestType = {PyVarObject_HEAD_INIT(nullptr, 0)};
 
+// ============================ paced producer ================================
+// paced_write(fd, data, ends, rate) -> (elapsed_s, writes)
+//
+// Writes the frames of `data` (frame i ends at byte ends[i], native-endian
+// u64 array) to `fd` at `rate` frames/s: frame i is written no earlier than
+// t0 + i/rate, every frame already due goes out in one write(2). The whole
+// call runs without the GIL and sleeps with clock_nanosleep(TIMER_ABSTIME) and
+// 1 ns timer slack, so a bench producer neither competes with the consumer's
+// event loop for the GIL nor wakes late by the default 50 us slack
+// (BASELINE configs 2-4: 1k / 10k / 100k events/s). Used by bench/harness.py.
+namespace {
+
+bool write_all(int fd, const uint8_t* p, size_t n) {
+  while (n) {
+    ssize_t w = write(fd, p, n);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      if (errno == EAGAIN) {
+        struct pollfd pfd = {fd, POLLOUT, 0};
+        poll(&pfd, 1, 100);
+        continue;
+      }
+      return false;
+    }
+    p += w;
+    n -= size_t(w);
+  }
+  return true;
+}
+
+PyObject* mod_paced_write(PyObject*, PyObject* args) {
+  int fd;
+  Py_buffer data, ends;
+  double rate;
+  if (!PyArg_ParseTuple(args, "iy*y*d", &fd, &data, &ends, &rate)) return nullptr;
+  size_t n = size_t(ends.len) / sizeof(uint64_t);
+  const uint64_t* endv = static_cast<const uint64_t*>(ends.buf);
+  const uint8_t* base = static_cast<const uint8_t*>(data.buf);
+  bool bad = rate <= 0 || ends.len % sizeof(uint64_t) != 0;
+  for (size_t i = 0; !bad && i < n; ++i)
+    bad = endv[i] > uint64_t(data.len) || (i && endv[i] < endv[i - 1]);
+  if (bad) {
+    PyBuffer_Release(&data);
+    PyBuffer_Release(&ends);
+    PyErr_SetString(PyExc_ValueError, "paced_write: rate must be > 0 and ends a non-decreasing u64 array within data");
+    return nullptr;
+  }
+  int64_t t0 = 0, t1 = 0;
+  uint64_t writes = 0;
+  bool ok = true;
+  int err = 0;
+  Py_BEGIN_ALLOW_THREADS
+  int old_slack = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
+  prctl(PR_SET_TIMERSLACK, 1, 0, 0, 0);
+  const double ns_per = 1e9 / rate;
+  t0 = mono_ns();
+  size_t sent = 0;
+  while (sent < n) {
+    int64_t now = mono_ns();
+    size_t due = size_t(double(now - t0) / ns_per) + 1;
+    if (due > n) due = n;
+    if (due > sent) {
+      uint64_t from = sent ? endv[sent - 1] : 0;
+      if (!write_all(fd, base + from, size_t(endv[due - 1] - from))) {
+        ok = false;
+        err = errno;
+        break;
+      }
+      ++writes;
+      sent = due;
+    } else {
+      int64_t at = t0 + int64_t(double(sent) * ns_per);
+      struct timespec ts = {time_t(at / 1000000000LL), long(at % 1000000000LL)};
+      while (clock_nanosleep(CLOCK_MONOTONIC, TIMER_ABSTIME, &ts, nullptr) == EINTR) {
+      }
+    }
+  }
+  t1 = mono_ns();
+  if (old_slack > 0) prctl(PR_SET_TIMERSLACK, old_slack, 0, 0, 0);
+  Py_END_ALLOW_THREADS
+  PyBuffer_Release(&data);
+  PyBuffer_Release(&ends);
+  if (!ok) {
+    errno = err;
+    return PyErr_SetFromErrno(PyExc_OSError);
+  }
+  return Py_BuildValue("(dK)", double(t1 - t0) / 1e9, (unsigned long long)writes);
+}
+
+PyMethodDef pace_methods[] = {
+    {"paced_write", mod_paced_write, METH_VARARGS,
+     "paced_write(fd, data, ends_u64, rate) -> (elapsed_s, writes): GIL-free paced frame writer"},
+    {nullptr, nullptr, 0, nullptr}};
+
+}  // namespace
+
 int init_ingest_types(PyObject* m) {
+  if (PyModule_AddFunctions(m, pace_methods) < 0) return -1;
   SettlerType.tp_name = "beholder_amd.ops._native.Settler";
   SettlerType.tp_basicsize = sizeof(SettlerObject);
   SettlerType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC;

@@ -20,7 +20,9 @@
 
 #include <pthread.h>
 #include <time.h>
+#include <unistd.h>
 
+#include <cerrno>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -188,6 +190,10 @@ class ByteRing {
     uint64_t depth = wcount_ - rcount_;
     if (depth > stats_.high_water_events) stats_.high_water_events = depth;
     if (consumer_waiting_) cv_data_.notify_one();
+    if (armed_) {  // the event loop found the ring empty and is parked on the notify fd
+      armed_ = false;
+      signal_locked();
+    }
     return 1;
   }
 
@@ -211,6 +217,22 @@ class ByteRing {
       consumer_waiting_ = false;
     }
     return size_t(wpos_ - rpos_);
+  }
+
+  // Event-loop wake-up (one hop, no worker thread): the loop watches `fd`
+  // (an eventfd, loop.add_reader) and calls arm() when a non-blocking pop came
+  // back empty. arm() returns false if a record, EOF or close arrived in the
+  // meantime (pop again); otherwise the next push, set_eof() or close() writes
+  // the fd once. Under load the consumer never arms, so pushes never touch it.
+  void set_notify_fd(int fd) {
+    Lock g(mu_);
+    notify_fd_ = fd;
+  }
+  bool arm() {
+    Lock g(mu_);
+    if (wpos_ != rpos_ || closed_ || eof_) return false;
+    armed_ = true;
+    return true;
   }
 
   // Snapshot of the readable region (call after wait_readable). The consumer
@@ -264,12 +286,16 @@ class ByteRing {
     Lock g(mu_);
     eof_ = true;
     cv_data_.notify_all();
+    armed_ = false;
+    signal_locked();
   }
   void close() {
     Lock g(mu_);
     closed_ = true;
     cv_data_.notify_all();
     cv_space_.notify_all();
+    armed_ = false;
+    signal_locked();
   }
   bool eof() {
     Lock g(mu_);
@@ -297,6 +323,15 @@ class ByteRing {
   }
 
  private:
+  void signal_locked() {
+    if (notify_fd_ < 0) return;
+    uint64_t one = 1;
+    ssize_t r;
+    do {
+      r = ::write(notify_fd_, &one, sizeof one);  // eventfd: never blocks (EFD_NONBLOCK), counts up
+    } while (r < 0 && errno == EINTR);
+  }
+
   void count_drop_locked(uint8_t topic) {
     stats_.dropped[topic < MAX_TOPICS ? topic : 0]++;
     stats_.dropped_total++;
@@ -314,6 +349,8 @@ class ByteRing {
   uint64_t seq_ = 0;
   int producers_waiting_ = 0;
   bool consumer_waiting_ = false;
+  bool armed_ = false;  // the loop is parked on notify_fd_
+  int notify_fd_ = -1;
   bool closed_ = false, eof_ = false;
   RingStats stats_;
 };

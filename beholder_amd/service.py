@@ -670,6 +670,7 @@ class Service:
             if s is not None:
                 out["handle_latency_ns"] = s.handle_latency.summary()
                 out["ingest_latency_ns"] = s.ingest_latency.summary()
+                out["queue_latency_ns"] = s.queue_latency.summary()  # receive -> handler start
         if self.registry is not None and hasattr(self, "handler_errors"):
             out["handler_errors"] = {k[0]: v for k, v in self.handler_errors.values().items()}
             out["trello_comments"] = self.trello_comments_total.get()

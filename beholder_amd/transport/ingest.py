@@ -5,9 +5,12 @@ the fd in large chunks, splits frames and copies them into a bounded byte ring
 without holding the GIL; this source pops whole batches of
 :class:`~beholder_amd.ops.Delivery` objects for the event loop.
 
-Waiting for data never blocks the loop: a non-blocking ``pop`` is tried
-first (the common case under load), and only an empty ring parks in a
-worker thread with a short timeout.
+Waiting for data never blocks the loop and never involves another thread: a
+non-blocking ``pop`` is tried first (the common case under load). When it
+comes back empty the source *arms* the ring and parks on the ring's eventfd
+(``loop.add_reader``); the reader thread's next push writes that fd once, and
+the loop pops on readiness. One cross-thread hop per idle wake-up (reader →
+loop), none under load (the ring is not armed while it has records).
 
 Backpressure (BASELINE config 4): ``policy='block'`` makes the reader stall
 when the ring is full (the kernel pipe then fills and the producer blocks);
@@ -55,8 +58,7 @@ class FdSource(Source):
 
     def __init__(self, fd: Optional[int] = None, path: Optional[str] = None, *,
                  capacity_bytes: int = 64 << 20, capacity_events: int = 0, policy: str = "block",
-                 batch: int = 512, chunk_bytes: int = 1 << 20, dead_letter: Optional[str] = None,
-                 idle_timeout: float = 0.05):
+                 batch: int = 512, chunk_bytes: int = 1 << 20, dead_letter: Optional[str] = None):
         if fd is None and path is None:
             fd = sys.stdin.fileno()
         self._fd = fd
@@ -64,7 +66,7 @@ class FdSource(Source):
         self._own_fd = path is not None
         self.batch = batch
         self.chunk_bytes = chunk_bytes
-        self.idle_timeout = idle_timeout
+        self.idle_wakeups = 0  # times the loop parked on the eventfd and was woken
         self._dl_path = dead_letter
         self._dl_file = None
         self._dl_lock = threading.Lock()
@@ -96,17 +98,34 @@ class FdSource(Source):
         ing = self._ingest
         loop = asyncio.get_running_loop()
         n = self.batch
-        while True:
-            got = ing.pop(n, 0.0)
-            if got is None:
-                return
-            if not got:
-                got = await loop.run_in_executor(None, ing.pop, n, self.idle_timeout)
+        pop, arm, clear = ing.pop, ing.arm, ing.clear_notify
+        efd = ing.notify_fd
+        waiter: list = [None]
+
+        def on_ready():  # the selector saw the eventfd: drain it, wake the parked generator
+            clear()
+            w = waiter[0]
+            if w is not None and not w.done():
+                w.set_result(None)
+
+        loop.add_reader(efd, on_ready)
+        try:
+            while True:
+                got = pop(n, 0.0)
                 if got is None:
                     return
-                if not got:
+                if got:
+                    yield got
                     continue
-            yield got
+                if not arm():  # a record / EOF arrived between the pop and arm(): pop again
+                    continue
+                w = waiter[0] = loop.create_future()
+                await w
+                waiter[0] = None
+                self.idle_wakeups += 1
+        finally:
+            if not loop.is_closed():
+                loop.remove_reader(efd)
 
     async def close(self) -> None:
         if self._closed:
@@ -129,6 +148,7 @@ class FdSource(Source):
         s = self._ingest.stats()
         s.update(self._settler.stats())
         s["abandoned_frames_written"] = self.abandoned_frames
+        s["idle_wakeups"] = self.idle_wakeups
         return s
 
     def ready(self) -> bool:

@@ -130,3 +130,32 @@ def default_procs(local_world: int, gpus: Optional[int] = None) -> int:
     """
     slots = max(1, local_world, gpus_on_node() if gpus is None else gpus)
     return max(1, min(16, available_cpus() // slots - 1))
+
+
+def cgroup_cpu_stat() -> Dict[str, int]:
+    """CFS throttling counters of this process's cgroup: ``nr_periods``, ``nr_throttled`` and
+    ``throttled_usec`` (cgroup v2 ``cpu.stat``; v1 ``cpu/cpu.stat``, whose ``throttled_time`` is
+    in ns). Empty when no CPU controller is visible. A phase whose delta shows throttling ran
+    against the share's quota, not against its own code."""
+    for path, ns in (("/sys/fs/cgroup/cpu.stat", False), ("/sys/fs/cgroup/cpu/cpu.stat", True),
+                     ("/sys/fs/cgroup/cpu,cpuacct/cpu.stat", True)):
+        try:
+            with open(path) as f:
+                raw = dict(ln.split()[:2] for ln in f if len(ln.split()) >= 2)
+        except (OSError, ValueError):
+            continue
+        out: Dict[str, int] = {}
+        for k in ("nr_periods", "nr_throttled"):
+            if k in raw:
+                out[k] = int(raw[k])
+        if "throttled_usec" in raw:
+            out["throttled_usec"] = int(raw["throttled_usec"])
+        elif "throttled_time" in raw:
+            out["throttled_usec"] = int(raw["throttled_time"]) // 1000 if ns else int(raw["throttled_time"])
+        if out:
+            return out
+    return {}
+
+
+def cgroup_delta(before: Mapping[str, int], after: Mapping[str, int]) -> Dict[str, int]:
+    return {k: after[k] - before.get(k, 0) for k in after}

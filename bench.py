@@ -341,11 +341,43 @@ def _r(x, nd=3):
     return None if x is None else round(float(x), nd)
 
 
+def _attr_keys(prefix: str, att: dict) -> dict:
+    """Flat bench-line keys for one phase's slow-delivery attribution (bench/stallmon.py)."""
+    if not att:
+        return {}
+    blamed = att.get("blamed", {})
+    procs = att.get("processes", {})
+    out = {f"{prefix}_slow_n": att.get("deliveries"),
+           f"{prefix}_slow_blamed": blamed,
+           f"{prefix}_slow_time_share": att.get("time_share"),
+           f"{prefix}_slowest_us": att.get("slowest_us")}
+    c = procs.get("consumer", {})
+    out[f"{prefix}_consumer_loop_lag_max_us"] = c.get("loop_lag_max_us")
+    out[f"{prefix}_consumer_loop_stalls"] = c.get("loop_stalls")
+    out[f"{prefix}_consumer_gc_max_pause_us"] = c.get("gc_max_pause_us")
+    fakes = {k: v for k, v in procs.items() if k != "consumer"}
+    out[f"{prefix}_fakes_loop_lag_max_us"] = {k: v.get("loop_lag_max_us") for k, v in fakes.items()}
+    out[f"{prefix}_fakes_gc_max_pause_us"] = max([v.get("gc_max_pause_us") or 0 for v in fakes.values()] or [0])
+    return out
+
+
+def _cg(prefix: str, d: dict) -> dict:
+    return {f"{prefix}_nr_throttled": d.get("nr_throttled"), f"{prefix}_throttled_usec": d.get("throttled_usec")}
+
+
 def io_extras(a) -> dict:
-    """Production-shaped TCP path (starts the fake endpoints as child processes)."""
+    """BASELINE config 1 (the real CLI on stdin) and the production-shaped TCP path. Both start
+    child processes, so they run before this process touches HIP."""
     from beholder_amd.bench import harness
     from beholder_amd.bench.generator import Workload
     out = {}
+    p = harness._plumbing(Workload(n_media=10000, seed=a.seed))
+    out.update({"plumbing_rc": p["rc"], "plumbing_acked": p["acked"], "plumbing_errors": p["errors"],
+                "plumbing_sink_requests": p["http_requests"], "plumbing_metrics_scraped": p["metrics_scraped"],
+                "plumbing_scrape_acked": p["scrape_acked"],
+                "plumbing_has_progress_counter": p["scrape_has_progress_counter"],
+                "plumbing_has_trello_counter": p["scrape_has_trello_counter"],
+                "plumbing_process_wall_s": _r(p["process_wall_s"])})
     e2e = harness._tcp_e2e(a.io_events)
     hl = e2e.get("handle_latency_us", {})
     out.update({"tcp_e2e_events_per_sec": _r(e2e.get("ingest_rate_eps"), 1),
@@ -354,17 +386,24 @@ def io_extras(a) -> dict:
                 "tcp_e2e_p999_handle_latency_us": _r(hl.get("p999")),
                 "tcp_e2e_warmup_p99_handle_latency_us": _r(e2e.get("warmup_handle_latency_us", {}).get("p99")),
                 "tcp_e2e_warmup_p999_handle_latency_us": _r(e2e.get("warmup_handle_latency_us", {}).get("p999")),
-                "tcp_e2e_errors": e2e.get("errors")})
+                "tcp_e2e_errors": e2e.get("errors"), "tcp_e2e_nivcsw": e2e.get("nivcsw"),
+                **_cg("tcp_e2e", e2e.get("cgroup_steady") or {}),
+                **_attr_keys("tcp_e2e", e2e.get("attribution_steady")),
+                **_attr_keys("tcp_e2e_warmup", e2e.get("attribution_warmup"))})
     tls = harness._tcp_e2e(a.io_events, http_servers=4, tls=True)
     hl = tls.get("handle_latency_us", {})
     out.update({"tls_e2e_events_per_sec": _r(tls.get("ingest_rate_eps"), 1),
                 "tls_e2e_cpu_us_per_event": _r(tls.get("cpu_us_per_event")),
+                "tls_e2e_p50_handle_latency_us": _r(hl.get("p50")),
                 "tls_e2e_p999_handle_latency_us": _r(hl.get("p999")),
                 "tls_e2e_warmup_p99_handle_latency_us": _r(tls.get("warmup_handle_latency_us", {}).get("p99")),
                 "tls_e2e_warmup_p999_handle_latency_us": _r(tls.get("warmup_handle_latency_us", {}).get("p999")),
                 "tls_e2e_handshakes": (tls.get("http") or {}).get("tls_handshakes"),
                 "tls_e2e_resumed": (tls.get("http") or {}).get("tls_resumed"),
-                "tls_e2e_errors": tls.get("errors")})
+                "tls_e2e_errors": tls.get("errors"), "tls_e2e_nivcsw": tls.get("nivcsw"),
+                **_cg("tls_e2e", tls.get("cgroup_steady") or {}),
+                **_attr_keys("tls_e2e", tls.get("attribution_steady")),
+                **_attr_keys("tls_e2e_warmup", tls.get("attribution_warmup"))})
     h = harness._http_tcp(Workload(n_media=10000, seed=a.seed), a.io_events, clients=("h1",))["h1"]
     hl = h["handle_latency_us"]
     out.update({"http_tcp_h1_events_per_sec": _r(h["ingest_rate_eps"], 1),
@@ -373,34 +412,56 @@ def io_extras(a) -> dict:
     return out
 
 
-def inproc_extras(a) -> dict:
-    """BASELINE configs 3, 4 and 5 in this process (no child processes)."""
+def _paced(prefix: str, r: dict) -> dict:
+    """Keys of one paced config: receive->ack p50/p99 and its two hops (reader push -> handler
+    start, handler start -> ack)."""
+    il, ql, hl = r["ingest_latency_us"], r.get("queue_latency_us", {}), r["handle_latency_us"]
+    return {f"{prefix}_acked": r["acked"],
+            f"{prefix}_p50_ingest_latency_us": _r(il.get("p50")),
+            f"{prefix}_p99_ingest_latency_us": _r(il.get("p99")),
+            f"{prefix}_p999_ingest_latency_us": _r(il.get("p999")),
+            f"{prefix}_p99_queue_latency_us": _r(ql.get("p99")),
+            f"{prefix}_p99_handle_latency_us": _r(hl.get("p99")),
+            f"{prefix}_idle_wakeups": r.get("idle_wakeups"),
+            f"{prefix}_cpu_us_per_event": _r(r.get("cpu_us_per_event"))}
+
+
+def paced_extras(a) -> dict:
+    """BASELINE configs 2-4 (paced producers) and the unpaced overload, in this process. The
+    producer is native and GIL-free (ops.paced_write); these run before the headline initialises
+    HIP, so nothing but the consumer and its reader thread competes for this process."""
+    from beholder_amd.bench import harness
+    from beholder_amd.bench.generator import Workload
+    from beholder_amd.utils.hostinfo import cgroup_cpu_stat, cgroup_delta
+    w = Workload(n_media=10000, seed=a.seed)
+    out = {}
+    cg0 = cgroup_cpu_stat()
+    r = asyncio.run(harness._run_inproc(w.events(1000), 1000, media=w.media))  # config 2: 1 s at 1k/s
+    out.update({"rate_1k_events_per_sec": _r(r["ingest_rate_eps"], 1), **_paced("rate_1k", r)})
+    r = asyncio.run(harness._run_inproc(w.events(10000), 10000, media=w.media))  # config 3: 1 s at 10k/s
+    out.update(_paced("rate_10k", r))
+    # config 4: 1 s paced at 100k/s into the small ring, drop_newest (backpressure + drop accounting)
+    r = asyncio.run(harness._run_inproc(w.events(100_000), 100_000, policy="drop_newest", capacity_events=4096,
+                                        media=w.media))
+    out.update({"rate_100k_offered": r["offered"], "rate_100k_accepted": r["accepted"],
+                "rate_100k_dropped": r["dropped"],
+                "rate_100k_offered_per_sec": _r(r["offered_rate_eps"], 1), **_paced("rate_100k", r)})
+    out.update(_cg("paced", cgroup_delta(cg0, cgroup_cpu_stat())))
+    r = asyncio.run(harness._run_inproc(w.events(200_000), 0, policy="drop_newest", capacity_events=4096,
+                                        media=w.media))
+    out.update({"burst_offered": r["offered"], "burst_accepted": r["accepted"],
+                "burst_dropped": r["dropped"]})
+    return out
+
+
+def soak_extras(a) -> dict:
+    """BASELINE config 5 in this process (no child processes: HIP may be initialised now)."""
     import resource
 
     from beholder_amd.bench import harness
     from beholder_amd.bench.generator import Workload
     w = Workload(n_media=10000, seed=a.seed)
     out = {}
-    r = asyncio.run(harness._run_inproc(w.events(1000), 1000, media=w.media))  # config 2: 1 s at 1k/s
-    out.update({"rate_1k_acked": r["acked"], "rate_1k_events_per_sec": _r(r["ingest_rate_eps"], 1),
-                "rate_1k_p50_ingest_latency_us": _r(r["ingest_latency_us"].get("p50")),
-                "rate_1k_p99_ingest_latency_us": _r(r["ingest_latency_us"].get("p99"))})
-    r = asyncio.run(harness._run_inproc(w.events(10000), 10000, media=w.media))
-    out.update({"rate_10k_acked": r["acked"],
-                "rate_10k_p50_ingest_latency_us": _r(r["ingest_latency_us"].get("p50")),
-                "rate_10k_p99_ingest_latency_us": _r(r["ingest_latency_us"].get("p99"))})
-    # config 4: 1 s paced at 100k/s into the small ring, drop_newest (backpressure + drop accounting)
-    r = asyncio.run(harness._run_inproc(w.events(100_000), 100_000, policy="drop_newest", capacity_events=4096,
-                                        media=w.media))
-    out.update({"rate_100k_offered": r["offered"], "rate_100k_accepted": r["accepted"],
-                "rate_100k_dropped": r["dropped"], "rate_100k_acked": r["acked"],
-                "rate_100k_offered_per_sec": _r(r["offered_rate_eps"], 1),
-                "rate_100k_p50_ingest_latency_us": _r(r["ingest_latency_us"].get("p50")),
-                "rate_100k_p99_ingest_latency_us": _r(r["ingest_latency_us"].get("p99"))})
-    r = asyncio.run(harness._run_inproc(w.events(200_000), 0, policy="drop_newest", capacity_events=4096,
-                                        media=w.media))
-    out.update({"burst_offered": r["offered"], "burst_accepted": r["accepted"],
-                "burst_dropped": r["dropped"]})
     evs = w.events(a.soak_events)
     probe: list = []
     g = harness.GcPauses()
@@ -409,6 +470,7 @@ def inproc_extras(a) -> dict:
     gs = g.summary()
     curve = r.get("rss_curve_mb") or []
     out.update({"soak_events": r["acked"], "soak_events_per_sec": _r(r["ingest_rate_eps"], 1),
+                "soak_cpu_us_per_event": _r(r.get("cpu_us_per_event")),
                 # the service's RSS growth over the run (from after init, with the 1M-event workload
                 # already in memory): at the end, and at the highest 0.5 s sample
                 "soak_rss_growth_mb": _r(probe[1] - probe[0], 2),
@@ -417,6 +479,20 @@ def inproc_extras(a) -> dict:
                 "soak_gc_pauses": gs.get("count", 0), "soak_gc_max_pause_us": _r(gs.get("max_us")),
                 "soak_gc_p99_pause_us": _r(gs.get("p99_us"))})
     return out
+
+
+# Fixed-work calibration (ops.calib, a pure-C integer loop): ns for CALIB_ITERS iterations, the
+# minimum of CALIB_REPS runs. CALIB_REF_NS is the same figure on the builder's reference box run
+# (profiles/box_r4_calib/); value_calibrated = value * calib_ns / CALIB_REF_NS is the headline a
+# box of the reference box's speed would have given (a slower core clock -> larger calib_ns).
+CALIB_ITERS = 4_000_000
+CALIB_REPS = 5
+CALIB_REF_NS = None
+
+
+def calibrate() -> int:
+    from beholder_amd.ops import calib
+    return min(calib(CALIB_ITERS)[0] for _ in range(CALIB_REPS))
 
 
 def main(argv=None) -> int:
@@ -430,6 +506,8 @@ def main(argv=None) -> int:
     dev = _Device(dist.local_rank)
     extras: dict = {}
 
+    from beholder_amd.utils.hostinfo import cgroup_cpu_stat, cgroup_delta
+
     # 1. phases that start child processes (before any HIP call in this process)
     if a.extras and dist.rank == 0:
         extras.update(io_extras(a))
@@ -440,17 +518,27 @@ def main(argv=None) -> int:
     allp_elapsed = dist.max(allp["elapsed"] if allp else 0.0)
     allp_events = sum(dist.gather(allp["events"] if allp else 0))
 
-    # 2. the headline: one consumer per rank, K timed steps
+    # 2. paced BASELINE configs 2-4 (in process, before HIP is initialised)
+    if a.extras and dist.rank == 0:
+        extras.update(paced_extras(a))
+    dist.barrier()
+
+    # 3. the headline: one consumer per rank, K timed steps, between two calibration runs
+    calib0 = calibrate()
+    cg0 = cgroup_cpu_stat()
     gc.collect()
     res = run_solo(a, dist, dev)
     dist.barrier()
+    cg1 = cgroup_cpu_stat()
+    calib1 = calibrate()
     elapsed = dist.max(res["elapsed"])
     parts = dist.gather({k: res[k] for k in ("handle_hist", "ingest_hist", "http_calls", "errors", "abandoned",
                                              "events", "cpu_s", "nivcsw")})
+    calibs = dist.gather((calib0, calib1))
 
-    # 3. in-process BASELINE configs (no child processes: HIP may be initialised now)
+    # 4. BASELINE config 5 (no child processes: HIP may be initialised now)
     if a.extras and dist.rank == 0:
-        extras.update(inproc_extras(a))
+        extras.update(soak_extras(a))
     dist.barrier()
 
     if dist.rank == 0:
@@ -460,6 +548,11 @@ def main(argv=None) -> int:
             hh.merge_bytes(p["handle_hist"])
         total_events = sum(p["events"] for p in parts)
         value = total_events / elapsed
+        calib_ns = max(max(c) for c in calibs)  # the slowest rank's worse side of the headline
+        cal = {"calib_ns": calib_ns, "calib_ns_before": calib0, "calib_ns_after": calib1,
+               "calib_ref_ns": CALIB_REF_NS,
+               "value_calibrated": round(value * calib_ns / CALIB_REF_NS, 1) if CALIB_REF_NS else None,
+               **_cg("headline", cgroup_delta(cg0, cg1))}
         out = {
             "metric": BASELINE_METRIC,
             "value": round(value, 1),
@@ -485,6 +578,7 @@ def main(argv=None) -> int:
             "p99_handle_latency_us": round(hh.percentile(99) / 1e3, 3),
             "cpu_us_per_event": round(sum(p["cpu_s"] for p in parts) / total_events * 1e6, 3),
             "involuntary_ctx_switches": sum(p["nivcsw"] for p in parts),
+            **cal,
             "http_requests": sum(p["http_calls"] for p in parts),
             "handler_errors": sum(p["errors"] for p in parts),
             "all_procs_per_rank": procs if allp is not None else 0,
@@ -499,7 +593,14 @@ def main(argv=None) -> int:
                      "drop_newest ring; burst = the same ring fed unpaced); tcp_e2e/http_tcp = every dependency "
                      "over TCP, tls_e2e = same with HTTPS sinks; tcp_e2e/tls_e2e latencies are receive->ack at "
                      "saturation with prefetch 100 in flight (queueing included), warmup_* = the first 5,000 "
-                     "deliveries (connection pools filling from zero; http.preconnect 0)",
+                     "deliveries (connection pools filling from zero; http.preconnect 0); *_slow_blamed = the "
+                     "slowest 0.1% of deliveries blamed on the process (consumer / pg / http(s) / broker fake) "
+                     "whose event-loop or GC stall covered most of their time, 'none' = no stall >= 1 ms "
+                     "(bench/stallmon.py); rate_*_p99_queue = reader push -> handler start, "
+                     "rate_*_p99_handle = handler start -> ack; calib_ns = fixed-work C loop (ops.calib) "
+                     "around the headline, value_calibrated = value * calib_ns / calib_ref_ns; "
+                     "plumbing_* = BASELINE config 1 through `python -m beholder_amd run --source stdin`, "
+                     "/metrics scraped before exit",
         }
         print(json.dumps(out), flush=True)
     dist.close()

@@ -17,7 +17,15 @@ EXTRAS = {"all_procs_events_per_sec", "rate_10k_p50_ingest_latency_us", "rate_10
           "soak_rss_peak_growth_mb", "bench_proc_maxrss_mb",
           "http_tcp_h1_p999_handle_latency_us", "p50_handle_latency_us", "tls_e2e_events_per_sec",
           "tls_e2e_cpu_us_per_event", "cpu_us_per_event", "involuntary_ctx_switches",
-          "tcp_e2e_warmup_p999_handle_latency_us", "tls_e2e_warmup_p999_handle_latency_us"}
+          "tcp_e2e_warmup_p999_handle_latency_us", "tls_e2e_warmup_p999_handle_latency_us",
+          # round 4: per-hop paced latency, calibration, config 1, stall attribution, throttling
+          "rate_1k_p99_queue_latency_us", "rate_10k_p99_queue_latency_us", "rate_100k_p99_queue_latency_us",
+          "rate_1k_p99_handle_latency_us", "rate_10k_p99_handle_latency_us", "rate_100k_p99_handle_latency_us",
+          "calib_ns", "calib_ns_before", "calib_ns_after", "value_calibrated", "headline_nr_throttled",
+          "plumbing_rc", "plumbing_acked", "plumbing_sink_requests", "plumbing_has_progress_counter",
+          "plumbing_has_trello_counter", "tcp_e2e_slow_blamed", "tls_e2e_slow_blamed",
+          "tcp_e2e_warmup_slow_blamed", "tls_e2e_warmup_slow_blamed", "tcp_e2e_nr_throttled",
+          "tls_e2e_nr_throttled", "tcp_e2e_nivcsw", "soak_cpu_us_per_event"}
 SMALL = ["--steps", "2", "--warmup", "1", "--events-per-step", "4096", "--media", "500"]
 
 
@@ -52,6 +60,11 @@ def test_bench_single_rank_contract():
     assert out["rate_100k_accepted"] + out["rate_100k_dropped"] == out["rate_100k_offered"]
     assert out["rate_100k_acked"] == out["rate_100k_accepted"]
     assert "soak_rss_peak_mb" not in out and "overload_offered" not in out
+    # BASELINE config 1: the real CLI on stdin, /metrics scraped with both reference counters
+    assert out["plumbing_rc"] == 0 and out["plumbing_acked"] == 100 and out["plumbing_sink_requests"] > 0
+    assert out["plumbing_has_progress_counter"] and out["plumbing_has_trello_counter"]
+    assert out["calib_ns"] >= max(out["calib_ns_before"], out["calib_ns_after"]) > 0
+    assert set(out["tcp_e2e_slow_blamed"]) >= {"consumer", "pg", "http", "none"}
 
 
 def test_bench_two_ranks_gloo():

@@ -140,3 +140,126 @@ def test_ndjson_frames():
                              ' "progress": 5}}', '{"topic": "v1.telemetry.status", "b64": "CgFt"}'])
     fr = list(iter_frames(data))
     assert fr[0][0] == 2 and fr[1] == (1, b"\x0a\x01m")
+
+
+# ---- event-loop wake-up: eventfd, one hop, no executor (transport/ingest.py FdSource.batches) ----
+
+def test_arm_signals_notify_fd_once():
+    ing = Ingest(capacity_bytes=1 << 16)
+    efd = ing.notify_fd
+    assert ing.notify_fd == efd  # created once, owned by the Ingest
+    assert ing.arm() is True  # empty: parked
+    import select
+    assert select.select([efd], [], [], 0)[0] == []
+    ing.push(0, b"a")
+    ing.push(0, b"b")  # second push while disarmed: no extra signal needed
+    assert select.select([efd], [], [], 0)[0] == [efd]
+    ing.clear_notify()
+    assert select.select([efd], [], [], 0)[0] == []
+    assert ing.arm() is False  # records queued: pop instead of parking
+    assert [d.content for d in ing.pop(10, 0.0)] == [b"a", b"b"]
+    assert ing.arm() is True
+    ing.set_eof()  # EOF wakes a parked loop too
+    assert select.select([efd], [], [], 0)[0] == [efd]
+    ing.clear_notify()
+    assert ing.pop(10, 0.0) is None
+    assert ing.arm() is False  # drained: never park again
+    ing.close()
+
+
+def test_idle_fdsource_uses_no_executor_thread():
+    """An idle FdSource parks on the ring's eventfd (loop.add_reader): nothing is submitted to the
+    loop's default executor, and every idle wake-up is one reader->loop hop."""
+    import asyncio
+    import concurrent.futures
+
+    from beholder_amd.transport.ingest import FdSource
+
+    class CountingExecutor(concurrent.futures.ThreadPoolExecutor):
+        submitted = 0
+
+        def submit(self, *a, **kw):
+            CountingExecutor.submitted += 1
+            return super().submit(*a, **kw)
+
+    async def go():
+        loop = asyncio.get_running_loop()
+        ex = CountingExecutor(max_workers=1)
+        loop.set_default_executor(ex)
+        r, w = os.pipe()
+        src = FdSource(fd=r)
+        await src.start()
+        got = []
+
+        async def consume():
+            async for batch in src.batches():
+                for d in batch:
+                    got.append(d.content)
+                    d.ack()
+
+        task = asyncio.ensure_future(consume())
+        for i in range(5):  # idle between events: each one is a separate park + wake-up
+            await asyncio.sleep(0.02)
+            os.write(w, frame(0, b"e%d" % i))
+        await asyncio.sleep(0.05)
+        os.close(w)
+        await asyncio.wait_for(task, 5)
+        st = src.stats()
+        await src.close()
+        os.close(r)
+        ex.shutdown()
+        return got, st
+
+    got, st = asyncio.run(go())
+    assert got == [b"e0", b"e1", b"e2", b"e3", b"e4"]
+    assert CountingExecutor.submitted == 0
+    assert st["idle_wakeups"] >= 5
+    assert st["acked"] == 5
+
+
+def test_paced_write_rate_and_order():
+    from array import array
+
+    from beholder_amd.ops import paced_write
+    chunks = [frame(i % 2, b"x%03d" % i) for i in range(200)]
+    ends = array("Q")
+    pos = 0
+    for c in chunks:
+        pos += len(c)
+        ends.append(pos)
+    r, w = os.pipe()
+    out = bytearray()
+
+    def rd():
+        while True:
+            b = os.read(r, 1 << 16)
+            if not b:
+                return
+            out.extend(b)
+
+    t = threading.Thread(target=rd)
+    t.start()
+    elapsed, writes = paced_write(w, b"".join(chunks), ends.tobytes(), 2000.0)  # 200 frames at 2k/s
+    os.close(w)
+    t.join()
+    os.close(r)
+    assert bytes(out) == b"".join(chunks)
+    assert 0.09 <= elapsed < 1.0  # the last frame is due at 199/2000 s
+    assert 2 <= writes <= 200
+    with pytest.raises(ValueError):
+        paced_write(1, b"ab", array("Q", [3]).tobytes(), 10.0)  # end beyond data
+    with pytest.raises(ValueError):
+        paced_write(1, b"ab", array("Q", [1]).tobytes(), 0.0)
+
+
+def test_queue_latency_is_receive_to_start():
+    from beholder_amd.ops import Delivery, Settler, mono_ns
+    s = Settler()
+    d = Delivery(b"x", 0, 1, s, mono_ns() - 5_000_000)  # received 5 ms ago
+    d.start()
+    d.ack()
+    assert s.queue_latency.count == 1
+    assert s.queue_latency.percentile(50) >= 4_000_000
+    assert s.handle_latency.percentile(50) < 4_000_000
+    s.reset_latency()
+    assert s.queue_latency.count == 0
