@@ -188,7 +188,12 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
             cold.update(src.settler.handle_latency.summary())
             src.settler.reset_latency()
         resetter = asyncio.ensure_future(reset_later())
+    mon = None
+    if rate > 0:  # paced: where a slow receive->ack came from (the loop stalled, or was preempted)
+        from .stallmon import StallMonitor
+        mon = StallMonitor(threshold_us=200).start()
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
+    rt0 = resource.getrusage(resource.RUSAGE_THREAD)
     t0 = time.perf_counter()
     prod.start()
     stats = await svc.run()
@@ -196,6 +201,9 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
         resetter.cancel()
     elapsed = time.perf_counter() - t0
     ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    rt1 = resource.getrusage(resource.RUSAGE_THREAD)
+    if mon is not None:
+        mon.stop()
     cpu_s = (ru1.ru_utime + ru1.ru_stime) - (ru0.ru_utime + ru0.ru_stime)
     prod.join()
     if gc_probe is not None:
@@ -225,6 +233,9 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
                           http.counts["requests"] if hasattr(http, "counts") else None),
         "max_inflight": max_inflight[0],
         "cpu_us_per_event": cpu_s / s["acked"] * 1e6 if s["acked"] else None,
+        # the event loop's thread: preemptions by other work on its CPU, and its stalls >= 200 us
+        "loop_thread_nivcsw": rt1.ru_nivcsw - rt0.ru_nivcsw,
+        **({"loop": mon.summary()} if mon is not None else {}),
         "error_samples": sink.samples,
         **({"rss_curve_mb": rss_curve} if rss_probe is not None else {}),
         **({"warmup_events": reset_latency_after,

@@ -6,9 +6,15 @@ message bodies, copies it to the device, decodes every message in one kernel (on
 message) and returns an ``(n, 8)`` int32 table:
 ``[id_off, id_len, status, progress, host_off, host_len, ok, fields_seen]``.
 
+The kernel reads in either of the CPU codec's dialects (``ops.DIALECTS``). The default is
+``protobufjs``, the reader the service itself runs (``handlers._dialect``, ``csrc/pbjs.hpp``), so
+on malformed input the kernel agrees with production: ``ok == 0`` exactly where
+``codec_for(ptype, "protobufjs").decode`` raises, and the same field values everywhere else.
+
 ``scripts/gpu_offload_probe.py`` prices this path against the CPU decode; docs/DESIGN.md
-("Why there are no HIP kernels") cites the result. :func:`reference_decode` is the plain-Python
-definition of the table, and the GPU tests compare the kernel against it.
+("Why there are no HIP kernels") cites the result. :func:`reference_decode` (upb) and
+:func:`reference_decode_pbjs` are plain-Python definitions of the table; the GPU tests compare
+the kernel against them and against the service's own protobufjs codec.
 
 The extension is built in-tree by ``beholder_amd._build.build_hip`` (hipcc, gfx950) and loaded
 with ctypes after ``import torch``. torch's HIP runtime has the same soname, so the kernel
@@ -25,6 +31,7 @@ import numpy as np
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "hip", "libbeholder_hip.so")
 FIELDS = ("id_off", "id_len", "status", "progress", "host_off", "host_len", "ok", "seen")
+DIALECT_IDS = {"upb": 0, "protobufjs": 1}  # the kernel's DIALECT_* constants
 _lib = None
 
 
@@ -37,7 +44,7 @@ def lib() -> ctypes.CDLL:
         import torch  # noqa: F401  load torch's libamdhip64 first so the kernel shares its runtime
         _lib = ctypes.CDLL(LIB_PATH)
         _lib.bh_decode_telemetry.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
-                                             ctypes.c_void_p]
+                                             ctypes.c_void_p, ctypes.c_int]
         _lib.bh_decode_telemetry.restype = ctypes.c_int
     return _lib
 
@@ -59,11 +66,13 @@ def check_layout(nbytes: int, offs: np.ndarray) -> None:
         raise ValueError("batch too large for int32 offsets")
 
 
-def decode_batch(buf_dev, offs_dev, n: int, out_dev=None):
+def decode_batch(buf_dev, offs_dev, n: int, out_dev=None, dialect: str = "protobufjs"):
     """Decode ``n`` messages already on the device (uint8 ``buf_dev``, int32 ``offs_dev`` of
-    ``n + 1`` host-checked boundaries) on the current torch stream. Returns the ``(n, 8)`` int32
-    table (``out_dev`` if given)."""
+    ``n + 1`` host-checked boundaries) on the current torch stream, in ``dialect``. Returns the
+    ``(n, 8)`` int32 table (``out_dev`` if given)."""
     import torch
+    if dialect not in DIALECT_IDS:
+        raise ValueError(f"unknown dialect {dialect!r} ({'|'.join(DIALECT_IDS)})")
     if buf_dev.dtype != torch.uint8 or offs_dev.dtype != torch.int32 or offs_dev.numel() != n + 1:
         raise ValueError("decode_batch needs uint8 buf, int32 offs of n + 1")
     if not (buf_dev.is_cuda and offs_dev.is_cuda and buf_dev.is_contiguous() and offs_dev.is_contiguous()):
@@ -75,13 +84,14 @@ def decode_batch(buf_dev, offs_dev, n: int, out_dev=None):
     if n == 0:
         return out_dev
     stream = torch.cuda.current_stream(buf_dev.device).cuda_stream
-    err = lib().bh_decode_telemetry(buf_dev.data_ptr(), offs_dev.data_ptr(), n, out_dev.data_ptr(), stream)
+    err = lib().bh_decode_telemetry(buf_dev.data_ptr(), offs_dev.data_ptr(), n, out_dev.data_ptr(), stream,
+                                    DIALECT_IDS[dialect])
     if err:
         raise RuntimeError(f"bh_decode_telemetry launch failed: hipError {err}")
     return out_dev
 
 
-def decode_bodies(bodies: Sequence[bytes], device="cuda"):
+def decode_bodies(bodies: Sequence[bytes], device="cuda", dialect: str = "protobufjs"):
     """Host bodies → host ``(n, 8)`` numpy table through the GPU (tests; the probe times the steps)."""
     import torch
     buf, offs = pack(bodies)
@@ -89,7 +99,7 @@ def decode_bodies(bodies: Sequence[bytes], device="cuda"):
     b = torch.frombuffer(bytearray(buf), dtype=torch.uint8).to(device) if buf else \
         torch.zeros(1, dtype=torch.uint8, device=device)
     o = torch.from_numpy(offs).to(device)
-    out = decode_batch(b, o, len(bodies))
+    out = decode_batch(b, o, len(bodies), dialect=dialect)
     return out.cpu().numpy()
 
 
@@ -163,7 +173,100 @@ def reference_decode(buf: bytes, start: int, end: int) -> List[int]:
     return r
 
 
-def reference_table(bodies: Sequence[bytes]) -> np.ndarray:
+class _PbjsOverrun(Exception):
+    pass
+
+
+class _PbjsReader:
+    """protobufjs 6.8.8 BufferReader over ``buf[start:end]`` (csrc/pbjs.hpp, in Python)."""
+
+    def __init__(self, buf: bytes, start: int, end: int):
+        self.b, self.base, self.len, self.pos = buf, start, end - start, 0
+
+    def at(self, i: int) -> int:
+        return self.b[self.base + i] if i < self.len else -1
+
+    def uint32(self) -> int:
+        v = 0
+        for k in range(4):
+            b = self.at(self.pos)
+            v |= (0 if b < 0 else b & 127) << (7 * k)
+            self.pos += 1
+            if 0 <= b < 128:
+                return v
+        b = self.at(self.pos)
+        v |= (0 if b < 0 else b & 15) << 28
+        self.pos += 1
+        if 0 <= b < 128:
+            return v & 0xFFFFFFFF
+        self.pos += 5
+        if self.pos > self.len:
+            raise _PbjsOverrun
+        return v & 0xFFFFFFFF
+
+    def skip_n(self, n: int) -> None:
+        if self.pos + n > self.len:
+            raise _PbjsOverrun
+        self.pos += n
+
+    def skip_type(self, wt: int) -> None:
+        depth = 0
+        while True:
+            if wt == 0:
+                while True:
+                    if self.pos >= self.len:
+                        raise _PbjsOverrun
+                    b = self.b[self.base + self.pos]
+                    self.pos += 1
+                    if not b & 128:
+                        break
+            elif wt == 1:
+                self.skip_n(8)
+            elif wt == 2:
+                self.skip_n(self.uint32())
+            elif wt == 3:
+                depth += 1
+            elif wt == 5:
+                self.skip_n(4)
+            elif wt == 4 and depth > 0:
+                depth -= 1
+            else:
+                raise _PbjsOverrun
+            if depth == 0:
+                return
+            wt = self.uint32() & 7
+
+    def string(self) -> Tuple[int, int]:
+        n = self.uint32()
+        e = min(self.pos + n, self.len)
+        off, self.pos = self.pos, e
+        return self.base + off, e - off
+
+
+def reference_decode_pbjs(buf: bytes, start: int, end: int) -> List[int]:
+    """Plain-Python definition of one kernel output row in the protobufjs dialect."""
+    r = [0, 0, 0, 0, 0, 0, 1, 0]
+    rd = _PbjsReader(buf, start, end)
+    try:
+        while rd.pos < rd.len:
+            t = rd.uint32()
+            field = t >> 3
+            if field in (1, 4):
+                k = 0 if field == 1 else 4
+                r[k], r[k + 1] = rd.string()
+                r[7] |= 1 if field == 1 else 8
+            elif field in (2, 3):
+                r[field] = _i32(rd.uint32())
+                r[7] |= 2 if field == 2 else 4
+            else:
+                rd.skip_type(t & 7)
+    except _PbjsOverrun:
+        r[6] = 0
+    return r
+
+
+def reference_table(bodies: Sequence[bytes], dialect: str = "upb") -> np.ndarray:
     buf, offs = pack(bodies)
-    return np.array([reference_decode(buf, int(offs[k]), int(offs[k + 1])) for k in range(len(bodies))],
+    row = reference_decode_pbjs if dialect == "protobufjs" else reference_decode
+    return np.array([row(buf, int(offs[k]), int(offs[k + 1])) for k in range(len(bodies))],
                     dtype=np.int32).reshape(len(bodies), 8)

@@ -423,6 +423,10 @@ def _paced(prefix: str, r: dict) -> dict:
             f"{prefix}_p99_queue_latency_us": _r(ql.get("p99")),
             f"{prefix}_p99_handle_latency_us": _r(hl.get("p99")),
             f"{prefix}_idle_wakeups": r.get("idle_wakeups"),
+            f"{prefix}_loop_thread_nivcsw": r.get("loop_thread_nivcsw"),
+            f"{prefix}_loop_stalls": (r.get("loop") or {}).get("loop_stalls"),
+            f"{prefix}_loop_lag_max_us": (r.get("loop") or {}).get("loop_lag_max_us"),
+            f"{prefix}_gc_max_pause_us": (r.get("loop") or {}).get("gc_max_pause_us"),
             f"{prefix}_cpu_us_per_event": _r(r.get("cpu_us_per_event"))}
 
 

@@ -1,0 +1,37 @@
+#!/usr/bin/env python3
+"""Prints the selected keys of one or more bench.py JSON lines side by side (box-run summaries)."""
+import json
+import sys
+
+KEYS = ["value", "cpu_us_per_event", "calib_ns", "calib_ns_before", "calib_ns_after", "value_calibrated",
+        "involuntary_ctx_switches", "headline_nr_throttled",
+        "rate_1k_p50_ingest_latency_us", "rate_1k_p99_ingest_latency_us", "rate_1k_p99_queue_latency_us",
+        "rate_1k_p99_handle_latency_us", "rate_10k_p50_ingest_latency_us", "rate_10k_p99_ingest_latency_us",
+        "rate_10k_p99_queue_latency_us", "rate_10k_p99_handle_latency_us", "rate_100k_p50_ingest_latency_us",
+        "rate_100k_p99_ingest_latency_us", "rate_100k_p99_queue_latency_us", "rate_100k_dropped",
+        "paced_nr_throttled",
+        "tcp_e2e_events_per_sec", "tcp_e2e_p50_handle_latency_us", "tcp_e2e_p999_handle_latency_us",
+        "tcp_e2e_warmup_p999_handle_latency_us", "tcp_e2e_slow_blamed", "tcp_e2e_slow_time_share",
+        "tcp_e2e_warmup_slow_blamed", "tcp_e2e_consumer_loop_lag_max_us", "tcp_e2e_fakes_loop_lag_max_us",
+        "tcp_e2e_nr_throttled", "tcp_e2e_nivcsw",
+        "tls_e2e_events_per_sec", "tls_e2e_p50_handle_latency_us", "tls_e2e_p999_handle_latency_us",
+        "tls_e2e_warmup_p999_handle_latency_us", "tls_e2e_slow_blamed", "tls_e2e_slow_time_share",
+        "tls_e2e_warmup_slow_blamed", "tls_e2e_warmup_slow_time_share", "tls_e2e_consumer_loop_lag_max_us",
+        "tls_e2e_fakes_loop_lag_max_us", "tls_e2e_nr_throttled", "tls_e2e_nivcsw",
+        "plumbing_rc", "plumbing_acked", "plumbing_has_progress_counter", "plumbing_has_trello_counter",
+        "soak_events_per_sec", "soak_gc_max_pause_us"]
+
+
+def main(paths):
+    rows = []
+    for p in paths:
+        with open(p) as f:
+            lines = [x for x in f.read().splitlines() if x.startswith("{")]
+        rows.append(json.loads(lines[-1]) if lines else {})
+    keys = sys.argv[1:] and KEYS
+    for k in keys:
+        print(f"{k:45s} " + " | ".join(json.dumps(r.get(k)) for r in rows))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
