@@ -19,7 +19,10 @@ KEYS = ["value", "cpu_us_per_event", "calib_ns", "calib_ns_before", "calib_ns_af
         "tls_e2e_warmup_slow_blamed", "tls_e2e_warmup_slow_time_share", "tls_e2e_consumer_loop_lag_max_us",
         "tls_e2e_fakes_loop_lag_max_us", "tls_e2e_nr_throttled", "tls_e2e_nivcsw",
         "plumbing_rc", "plumbing_acked", "plumbing_has_progress_counter", "plumbing_has_trello_counter",
-        "soak_events_per_sec", "soak_gc_max_pause_us"]
+        "soak_events_per_sec", "soak_gc_max_pause_us",
+        "rate_1k_loop_stalls", "rate_1k_loop_lag_max_us", "rate_1k_loop_thread_nivcsw", "rate_10k_loop_stalls",
+        "rate_10k_loop_lag_max_us", "rate_10k_loop_thread_nivcsw", "rate_10k_gc_max_pause_us",
+        "rate_100k_loop_stalls", "rate_100k_loop_lag_max_us", "rate_100k_loop_thread_nivcsw"]
 
 
 def main(paths):
@@ -28,8 +31,7 @@ def main(paths):
         with open(p) as f:
             lines = [x for x in f.read().splitlines() if x.startswith("{")]
         rows.append(json.loads(lines[-1]) if lines else {})
-    keys = sys.argv[1:] and KEYS
-    for k in keys:
+    for k in KEYS:
         print(f"{k:45s} " + " | ".join(json.dumps(r.get(k)) for r in rows))
 
 
