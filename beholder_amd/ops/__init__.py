@@ -84,6 +84,7 @@ frames = native.frames
 mono_ns = native.mono_ns
 paced_write = native.paced_write
 calib = native.calib
+calib_mem = native.calib_mem
 format_line = native.format_line
 quick_format = native.quick_format
 js_str = native.js_str
@@ -150,7 +151,7 @@ def codec_for(ptype, dialect: str = "upb") -> Optional[object]:
 
 __all__ = [
     "native", "NativeHandlers", "SinkStats", "AckBatcher", "AmqpDemux", "Driver", "Window", "IOFuture", "H1Parser", "PgReader", "MessageCodec", "Ingest", "Delivery", "Settler", "Counter", "Histogram",
-    "frame", "frames", "mono_ns", "paced_write", "calib", "codec_for", "field_table", "format_line", "quick_format", "js_str",
+    "frame", "frames", "mono_ns", "paced_write", "calib", "calib_mem", "codec_for", "field_table", "format_line", "quick_format", "js_str",
     "js_number", "encode_query", "quote_component",
 ]
 

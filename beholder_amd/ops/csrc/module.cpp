@@ -4,6 +4,7 @@
 // thread), Delivery / Settler (ack semantics + latency), Counter / Histogram
 // (metrics), plus framing helpers. See the per-file headers for the mapping
 // to reference behaviour (/root/reference/index.js).
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -135,7 +136,49 @@ PyObject* mod_calib(PyObject*, PyObject* args) {
   return Py_BuildValue("(LK)", (long long)(t1 - t0), (unsigned long long)acc);
 }
 
+// calib_mem(bytes, steps) -> (ns, checksum): a dependent random walk over `bytes` of cache lines
+// (one random cycle through every line, Sattolo's shuffle). With 16 MiB it lives in the L3 a
+// core shares with its CCD neighbours, so its time moves with other tenants' cache and memory
+// traffic -- which an L1-resident loop (calib) cannot see and a Python consumer, whose objects
+// are scattered over the heap, does. Setup is outside the timed region; runs without the GIL.
+PyObject* mod_calib_mem(PyObject*, PyObject* args) {
+  unsigned long long bytes, steps;
+  if (!PyArg_ParseTuple(args, "KK", &bytes, &steps)) return nullptr;
+  const size_t lines = size_t(bytes / 64);
+  if (lines < 2 || lines > (size_t(1) << 26)) {
+    PyErr_SetString(PyExc_ValueError, "calib_mem: bytes must be in [128, 4 GiB]");
+    return nullptr;
+  }
+  uint64_t* a = static_cast<uint64_t*>(std::aligned_alloc(64, lines * 64));
+  if (!a) return PyErr_NoMemory();
+  int64_t t0, t1;
+  uint64_t idx = 0;
+  Py_BEGIN_ALLOW_THREADS
+  std::vector<uint32_t> perm(lines);
+  for (size_t i = 0; i < lines; ++i) perm[i] = uint32_t(i);
+  uint64_t x = 0x2545F4914F6CDD1Dull;
+  for (size_t i = lines - 1; i > 0; --i) {  // Sattolo: a single cycle through every line
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    size_t j = size_t(x % i);
+    uint32_t t = perm[i];
+    perm[i] = perm[j];
+    perm[j] = t;
+  }
+  for (size_t i = 0; i < lines; ++i) a[size_t(i) * 8] = perm[i];
+  for (size_t i = 0; i < lines; ++i) idx = a[idx * 8];  // one warm lap
+  t0 = mono_ns();
+  for (unsigned long long s = 0; s < steps; ++s) idx = a[idx * 8];
+  t1 = mono_ns();
+  Py_END_ALLOW_THREADS
+  std::free(a);
+  return Py_BuildValue("(LK)", (long long)(t1 - t0), (unsigned long long)idx);
+}
+
 PyMethodDef module_methods[] = {
+    {"calib_mem", mod_calib_mem, METH_VARARGS,
+     "calib_mem(bytes, steps) -> (ns, checksum): fixed-work dependent random walk over `bytes`"},
     {"calib", mod_calib, METH_VARARGS, "calib(iters) -> (ns, checksum): fixed-work CPU calibration loop"},
     {"configure", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(mod_configure)),
      METH_VARARGS | METH_KEYWORDS, "configure(decode_error=None, topics=None)"},

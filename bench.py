@@ -485,18 +485,33 @@ def soak_extras(a) -> dict:
     return out
 
 
-# Fixed-work calibration (ops.calib, a pure-C integer loop): ns for CALIB_ITERS iterations, the
-# minimum of CALIB_REPS runs. CALIB_REF_NS is the same figure on the builder's reference box run
-# (profiles/box_r4_calib/); value_calibrated = value * calib_ns / CALIB_REF_NS is the headline a
-# box of the reference box's speed would have given (a slower core clock -> larger calib_ns).
+# Fixed-work calibrations around the headline, each the minimum of CALIB_REPS runs (ns):
+#   calib_ns      ops.calib: an L1-resident integer loop (core clock, time-sharing of the core);
+#   calib_mem_ns  ops.calib_mem: a dependent random walk over 8 MiB (L3 / memory latency, which
+#                 other tenants' traffic moves);
+#   calib_py_ns   a fixed pure-Python loop (the interpreter: dict, str and int churn, as the
+#                 consumer's Python glue does).
+# CALIB_REF_* are the same figures on the builder's reference box runs (profiles/box_r4_calib/).
 CALIB_ITERS = 4_000_000
+CALIB_MEM_BYTES, CALIB_MEM_STEPS = 8 << 20, 500_000
 CALIB_REPS = 5
-CALIB_REF_NS = None
+CALIB_REF = {"calib_ns": None, "calib_mem_ns": None, "calib_py_ns": None}
 
 
-def calibrate() -> int:
-    from beholder_amd.ops import calib
-    return min(calib(CALIB_ITERS)[0] for _ in range(CALIB_REPS))
+def _calib_py_once() -> int:
+    t0 = time.perf_counter_ns()
+    d: dict = {}
+    for i in range(20_000):
+        k = f"m{i % 997}"
+        d[k] = d.get(k, 0) + len(str(i * 7))
+    return time.perf_counter_ns() - t0
+
+
+def calibrate() -> dict:
+    from beholder_amd.ops import calib, calib_mem
+    return {"calib_ns": min(calib(CALIB_ITERS)[0] for _ in range(CALIB_REPS)),
+            "calib_mem_ns": min(calib_mem(CALIB_MEM_BYTES, CALIB_MEM_STEPS)[0] for _ in range(CALIB_REPS)),
+            "calib_py_ns": min(_calib_py_once() for _ in range(CALIB_REPS))}
 
 
 def main(argv=None) -> int:
@@ -552,11 +567,16 @@ def main(argv=None) -> int:
             hh.merge_bytes(p["handle_hist"])
         total_events = sum(p["events"] for p in parts)
         value = total_events / elapsed
-        calib_ns = max(max(c) for c in calibs)  # the slowest rank's worse side of the headline
-        cal = {"calib_ns": calib_ns, "calib_ns_before": calib0, "calib_ns_after": calib1,
-               "calib_ref_ns": CALIB_REF_NS,
-               "value_calibrated": round(value * calib_ns / CALIB_REF_NS, 1) if CALIB_REF_NS else None,
-               **_cg("headline", cgroup_delta(cg0, cg1))}
+        cal = {}
+        for k in CALIB_REF:  # the slowest rank's worse side of the headline
+            cal[k] = max(max(c0[k], c1[k]) for c0, c1 in calibs)
+            cal[k + "_before"] = calib0[k]
+            cal[k + "_after"] = calib1[k]
+        ref = CALIB_REF["calib_py_ns"]
+        cal.update({"calib_ref": CALIB_REF,
+                    # what a box as fast as the reference box (by the interpreter calibration) would give
+                    "value_calibrated": round(value * cal["calib_py_ns"] / ref, 1) if ref else None,
+                    **_cg("headline", cgroup_delta(cg0, cg1))})
         out = {
             "metric": BASELINE_METRIC,
             "value": round(value, 1),
