@@ -19,6 +19,7 @@
 //             comment (Q8) } catch -> warn -> ack (Q7)
 // The rare branches (missing-list warning, DEPLOYED hooks) call the Python helpers that the
 // Python method calls too, so their text and ordering come from one place.
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -527,10 +528,20 @@ void count_request(CallObject* c) {
 // Python method frame. The event's second and later sink requests (a status event's move, then
 // its hooks: index.js:83,99,112) are continuations: if they have to wait for a connection they
 // wait at the front of the origin's queue, not behind the first requests of newer deliveries.
+// A/B switch for the round-4 native-I/O budget: BEHOLDER_AB_FRONT=0 queues an
+// event's later sink requests at the back like any other.
+bool front_enabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("BEHOLDER_AB_FRONT");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 PyObject* http_request(CallObject* c, PyObject* http, PyObject* method, PyObject* url, PyObject* params,
                        PyObject* timeout) {
   HandlersObject* hs = c->hs;
-  const bool front = c->nreq > 0;
+  const bool front = c->nreq > 0 && front_enabled();
   count_request(c);
   PyObject** dp = _PyObject_GetDictPtr(http);
   PyObject* cur = dp && *dp ? PyDict_GetItemWithError(*dp, s_native_call) : nullptr;
