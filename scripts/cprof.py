@@ -1,0 +1,145 @@
+#!/usr/bin/env python3
+"""Native-level flat CPU profile of the headline consumer (no `perf` on these hosts).
+
+Samples instruction pointers with the extension's SIGPROF sampler (``ops/csrc/py_prof.cpp``)
+while one consumer runs the bench's timed steps (``bench.run_consumer``), then resolves every
+sample to ``object:function`` through ``/proc/self/maps``, the objects' ELF load segments and
+their symbol tables (``nm``: our extension's full table, the interpreter's exported symbols).
+Prints the top functions by self samples, and the split by object.
+
+    python scripts/cprof.py [--steps 20] [--hz 2000] [--top 60] [--tid main|all]
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import bisect
+import collections
+import os
+import subprocess
+import sys
+import threading
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def maps():
+    out = []
+    with open("/proc/self/maps") as f:
+        for ln in f:
+            parts = ln.split()
+            if len(parts) < 6 or "x" not in parts[1]:
+                continue
+            a, b = (int(x, 16) for x in parts[0].split("-"))
+            out.append((a, b, int(parts[2], 16), parts[5]))
+    out.sort()
+    return out
+
+
+_segs_cache: dict = {}
+_syms_cache: dict = {}
+
+
+def load_segments(path):
+    """[(p_offset, p_vaddr, p_filesz)] of the LOAD segments."""
+    if path in _segs_cache:
+        return _segs_cache[path]
+    segs = []
+    try:
+        txt = subprocess.run(["readelf", "-lW", path], capture_output=True, text=True, timeout=30).stdout
+        for ln in txt.splitlines():
+            p = ln.split()
+            if p and p[0] == "LOAD":
+                segs.append((int(p[1], 16), int(p[2], 16), int(p[4], 16)))
+    except (OSError, subprocess.SubprocessError):
+        pass
+    _segs_cache[path] = segs
+    return segs
+
+
+def symbols(path):
+    """Sorted (vaddr, name) of the function symbols (static table, else dynamic)."""
+    if path in _syms_cache:
+        return _syms_cache[path]
+    syms = []
+    for args in (["nm", "-n", "--defined-only", "-C", path], ["nm", "-D", "-n", "--defined-only", "-C", path]):
+        try:
+            txt = subprocess.run(args, capture_output=True, text=True, timeout=60).stdout
+        except (OSError, subprocess.SubprocessError):
+            continue
+        for ln in txt.splitlines():
+            p = ln.split(" ", 2)
+            if len(p) == 3 and p[1] in "tTwWiI":
+                syms.append((int(p[0], 16), p[2]))
+        if syms:
+            break
+    syms.sort()
+    _syms_cache[path] = (syms, [a for a, _ in syms])
+    return _syms_cache[path]
+
+
+def resolve(ip, mp, starts):
+    i = bisect.bisect_right(starts, ip) - 1
+    if i < 0 or ip >= mp[i][1]:
+        return ("?", "?")
+    a, _, off, path = mp[i]
+    foff = ip - a + off
+    vaddr = foff
+    for so, sv, sz in load_segments(path):
+        if so <= foff < so + sz:
+            vaddr = foff - so + sv
+            break
+    syms, addrs = symbols(path)
+    j = bisect.bisect_right(addrs, vaddr) - 1
+    name = syms[j][1] if j >= 0 else f"+{vaddr:#x}"
+    return (os.path.basename(path), name)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--hz", type=int, default=2000)
+    ap.add_argument("--top", type=int, default=60)
+    ap.add_argument("--tid", default="main", choices=["main", "all"])
+    a = ap.parse_args(argv)
+    import bench
+    from beholder_amd.ops import native
+
+    ba = bench.parse(["--steps", str(a.steps), "--warmup", str(a.warmup), "--no-extras"])
+    main_tid = threading.get_native_id()
+
+    def go():
+        native.prof_start(a.hz)
+
+    def stop():
+        res["samples"], res["lost"] = native.prof_stop()
+
+    res: dict = {}
+    r = asyncio.run(bench.run_consumer(ba, 0, go, stop))
+    mp = maps()
+    starts = [m[0] for m in mp]
+    samples = res["samples"]
+    if a.tid == "main":
+        samples = [s for s in samples if s[1] == main_tid]
+    fn = collections.Counter()
+    obj = collections.Counter()
+    for ip, _tid in samples:
+        o, f = resolve(ip, mp, starts)
+        fn[(o, f)] += 1
+        obj[o] += 1
+    n = max(1, len(samples))
+    print(f"events/s {r['events'] / r['elapsed']:.0f}  cpu us/event {r['cpu_s'] / r['events'] * 1e6:.3f}  "
+          f"samples {len(samples)} ({a.tid} thread), lost {res['lost']}")
+    print("\n-- by object --")
+    for o, c in obj.most_common():
+        print(f"{100 * c / n:6.2f}%  {o}")
+    print("\n-- by function (self) --")
+    for (o, f), c in fn.most_common(a.top):
+        print(f"{100 * c / n:6.2f}%  {o:28s} {f}")
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
