@@ -77,6 +77,7 @@ if os.environ.get("BEHOLDER_NATIVE_IO", "1") == "0":  # all native I/O off: plai
         reject = _asyncio.Future.set_exception
 AckBatcher = native.AckBatcher
 SinkStats = native.SinkStats
+Recorder = native.Recorder
 NativeHandlers = native.NativeHandlers
 dispatch_batch = native.dispatch_batch
 frame = native.frame
@@ -150,7 +151,7 @@ def codec_for(ptype, dialect: str = "upb") -> Optional[object]:
 
 
 __all__ = [
-    "native", "NativeHandlers", "SinkStats", "AckBatcher", "AmqpDemux", "Driver", "Window", "IOFuture", "H1Parser", "PgReader", "MessageCodec", "Ingest", "Delivery", "Settler", "Counter", "Histogram",
+    "native", "NativeHandlers", "SinkStats", "Recorder", "AckBatcher", "AmqpDemux", "Driver", "Window", "IOFuture", "H1Parser", "PgReader", "MessageCodec", "Ingest", "Delivery", "Settler", "Counter", "Histogram",
     "frame", "frames", "mono_ns", "paced_write", "calib", "calib_mem", "codec_for", "field_table", "format_line", "quick_format", "js_str",
     "js_number", "encode_query", "quote_component",
 ]

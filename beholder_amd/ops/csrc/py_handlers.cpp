@@ -46,7 +46,7 @@ PyObject *s_ack, *s_message, *s_content, *s_mediaId, *s_status, *s_progress, *s_
     *s_put, *s_deployed_hooks, *s_warn_missing_list, *s_child_for, *s_inc, *s_lower,
     *s_throw, *s_close, *s_lists, *s_no_trello, *s_deployed, *s_trello_creator, *s_log, *s_decode_status,
     *s_decode_progress, *s_status_names_s, *s_status_names_p, *s_progress_counter, *s_comment_inc, *s_key,
-    *s_token, *s_base_url, *s_http, *s_timeout, *s_strict, *s_stats, *s_request, *s_params, *s_POST, *s_PUT,
+    *s_token, *s_native_record, *s_base_url, *s_http, *s_timeout, *s_strict, *s_stats, *s_request, *s_params, *s_POST, *s_PUT,
     *s_record, *s_raise_for_status, *s_rows, *s_get_calls, *s_update_calls, *s_limiter, *s_retry,
     *s_hooks_plan, *s_telegram, *s_emby, *s_name, *s_metadataId, *s_GET,
     *s_api_key, *s_send_message, *s_refresh_library, *s_pool, *s_select, *s_update,
@@ -544,6 +544,12 @@ PyObject* http_request(CallObject* c, PyObject* http, PyObject* method, PyObject
   const bool front = c->nreq > 0 && front_enabled();
   count_request(c);
   PyObject** dp = _PyObject_GetDictPtr(http);
+  PyObject* rec = dp && *dp ? PyDict_GetItemWithError(*dp, s_native_record) : nullptr;
+  if (rec && is_recorder(rec)) {  // the in-process stub (sinks/http.py RecordingHttpClient)
+    PyObject* m = method;
+    return recorder_request(rec, m, url, params ? params : Py_None);
+  }
+  if (PyErr_Occurred()) return nullptr;
   PyObject* cur = dp && *dp ? PyDict_GetItemWithError(*dp, s_native_call) : nullptr;
   if (cur && cur == hs->h1_fast_fn) {
     PyObject* call = h1_call_new(http, method, url, params ? params : Py_None, timeout, front);
@@ -1759,6 +1765,7 @@ int init_handler_types(PyObject* m) {
               {&s_strict, "strict"},
               {&s_stats, "stats"},
               {&s_request, "request"},
+              {&s_native_record, "native_record"},
               {&s_params, "params"},
               {&s_POST, "POST"},
               {&s_PUT, "PUT"},

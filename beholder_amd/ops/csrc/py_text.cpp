@@ -915,6 +915,44 @@ PyMethodDef text_methods[] = {
 
 }  // namespace
 
+// The recorded request URL: `url` + "?" + encode_query(params) for a non-empty dict (what
+// restler builds for the trello client, index.js:53,83: "?" even when the path already has one,
+// and even when every value is None), `url` alone for None or {}. For the native bench
+// recorder (py_recorder.cpp). NULL with a Python error.
+PyObject* url_with_query(PyObject* url, PyObject* params) {
+  if (params == nullptr || params == Py_None) return Py_NewRef(url);
+  if (!PyDict_Check(params)) {
+    PyErr_SetString(PyExc_TypeError, "params must be a dict or None");
+    return nullptr;
+  }
+  if (PyDict_GET_SIZE(params) == 0) return Py_NewRef(url);
+  try {
+    std::string q;
+    Py_ssize_t pos = 0;
+    PyObject *k, *v;
+    bool first = true;
+    while (PyDict_Next(params, &pos, &k, &v)) {
+      if (v == Py_None) continue;
+      if (!first) q += '&';
+      first = false;
+      if (!quote_js_str_append(q, k, false)) return nullptr;
+      q += '=';
+      if (!qs_value_append(q, v, false)) return nullptr;
+    }
+    Py_ssize_t ulen;
+    const char* u = PyUnicode_AsUTF8AndSize(url, &ulen);
+    if (!u) return nullptr;
+    std::string out;
+    out.reserve(size_t(ulen) + 1 + q.size());
+    out.append(u, size_t(ulen));
+    out += '?';
+    out += q;
+    return PyUnicode_DecodeUTF8(out.data(), Py_ssize_t(out.size()), "strict");
+  } catch (const std::bad_alloc&) {
+    return PyErr_NoMemory();
+  }
+}
+
 // ---- used by the native handlers (py_handlers.cpp) ---------------------------
 bool text_js_str_append(std::string& out, PyObject* v) { return js_str_append(out, v); }
 

@@ -220,16 +220,30 @@ class RecordingHttpClient(HttpClient):
     matching rule the answer is ``200 {}``. ``keep`` bounds the call log (the
     total count is always exact), so benches can use it as a null sink.
     ``delay_s`` simulates network latency (forces a real suspension).
+
+    Counting, URL building and the call log are native (``ops Recorder``). While the client has
+    no rules and no delay it also exposes that core as ``native_record``: the compiled handlers
+    then record and get their ``200 {}`` without entering this class's coroutine, the way they
+    use the H1 client's native request path in production (``H1Client.native_call``).
     """
 
     def __init__(self, keep: Optional[int] = None, delay_s: float = 0.0):
         self.calls: Deque[Tuple[str, str]] = collections.deque(maxlen=keep)
-        self.count = 0
         self.rules: List[Rule] = []
         self.delay_s = delay_s
+        self._ok = HttpResponse(200, b"{}", None, "")
+        self._rec = _native_ops.Recorder(self.calls, self._ok)
+        # a subclass that overrides request() (jitter, counting) keeps every call on its own path
+        plain = type(self).request is RecordingHttpClient.request
+        self.native_record = self._rec if plain and not delay_s else None
+
+    @property
+    def count(self) -> int:
+        return self._rec.count
 
     def add_rule(self, method: str, url_prefix: str, fn) -> None:
         self.rules.append((method.upper(), url_prefix, fn))
+        self.native_record = None  # answers now depend on the rules: the Python path decides
 
     def fail(self, method: str, url_prefix: str, status: Optional[int] = None, message: str = "ECONNREFUSED",
              body: bytes = b'"error"'):
@@ -242,9 +256,10 @@ class RecordingHttpClient(HttpClient):
 
     async def request(self, method, url, *, params=None, timeout=None) -> HttpResponse:
         m = method.upper()
-        full = url + "?" + _native_encode_query(params) if type(params) is dict and params else with_query(url, params)
-        self.count += 1
-        self.calls.append((m, full))
+        if type(params) is dict or params is None:  # dict: url + "?" + query, as restler builds it
+            full = self._rec.record(m, url, params)
+        else:
+            full = self._rec.record(m, with_query(url, params), None)
         if self.delay_s:
             await asyncio.sleep(self.delay_s)
         if not self.rules:
