@@ -19,8 +19,15 @@ for name, kw in (("tcp", {}), ("tls", {"http_servers": 4, "tls": True})):
                "blamed": (x.get("attribution_steady") or {}).get("blamed"),
                "warm_blamed": (x.get("attribution_warmup") or {}).get("blamed")}
 print(json.dumps(r))'
+arms=${ARMS:-AB}  # A = current; B = no handshake threads, no continuation-first; C = no continuation-first only
 for i in $(seq 1 "$runs"); do
-  timeout -k 10 120 python3 -c "$probe" > "$out/A_$i.json" 2> "$out/A_$i.err" || exit $?
-  BEHOLDER_AB_HS_THREADS=0 BEHOLDER_AB_FRONT=0 timeout -k 10 120 python3 -c "$probe" > "$out/B_$i.json" 2> "$out/B_$i.err" || exit $?
-  echo "pair $i: A $(cut -c1-150 "$out/A_$i.json") B $(cut -c1-150 "$out/B_$i.json")"
+  for arm in $(echo "$arms" | fold -w1); do
+    case $arm in
+      A) env=() ;;
+      B) env=(BEHOLDER_AB_HS_THREADS=0 BEHOLDER_AB_FRONT=0) ;;
+      C) env=(BEHOLDER_AB_FRONT=0) ;;
+    esac
+    env "${env[@]}" timeout -k 10 120 python3 -c "$probe" > "$out/${arm}_$i.json" 2> "$out/${arm}_$i.err" || exit $?
+    echo "run $i arm $arm: $(cut -c1-150 "$out/${arm}_$i.json")"
+  done
 done
