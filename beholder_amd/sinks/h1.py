@@ -540,7 +540,12 @@ class H1Client(HttpClient):
                 if c.uses:
                     counts["reused"] += 1
                 return c
-            self._drop(c)  # closed meanwhile, or a used one for a retry that needs a fresh one
+            if not c.closed and any(not x.done() for x in o.waiters):
+                # a healthy keep-alive connection, but this retry needs a fresh one: another queued
+                # request takes it (no connect + handshake thrown away); this one keeps its place
+                self._release(c, True)
+            else:
+                self._drop(c)  # closed meanwhile, or nobody else to take it: make room for a fresh one
             front = True
 
     async def preconnect(self, url: str, n: int) -> Tuple[int, Optional[BaseException]]:

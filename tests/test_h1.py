@@ -554,3 +554,53 @@ def test_connects_of_a_burst_share_one_name_lookup():
     statuses, first, second, third, st = run(go())
     assert statuses == [200] * 12 and st["connections"] >= 2
     assert (first, second, third) == (1, 1, 2)
+
+
+def test_fresh_retry_hands_a_healthy_used_connection_to_the_next_waiter():
+    """a retry that needs a fresh connection, queued at max_per_host and handed a
+    healthy keep-alive connection, passes it to the next queued request instead of aborting it
+    (a connect plus, for HTTPS, a handshake saved); with nobody else queued it still makes room."""
+    from beholder_amd.sinks.h1 import _Conn
+
+    class Tracked(_Conn):
+        __slots__ = ("aborted",)
+
+        def __init__(self, o):
+            super().__init__(o)
+            self.aborted = False
+
+        def abort(self):
+            self.aborted = True
+            self.closed = True
+
+    async def go():
+        c = H1Client(timeout_s=5, max_per_host=1)
+        o = c._origin("http://127.0.0.1:9")
+        o.open = 1  # the pool is full with one busy connection
+        used = Tracked(o)
+        used.uses = 3
+        loop = asyncio.get_running_loop()
+        deadline = loop.time() + 5
+        retry = asyncio.ensure_future(c._acquire(o, deadline, fresh=True))
+        await asyncio.sleep(0)
+        other = asyncio.ensure_future(c._acquire(o, deadline))
+        await asyncio.sleep(0)
+        c._release(used, True)  # the first waiter is the fresh retry
+        got = await asyncio.wait_for(other, 1)
+        pending = not retry.done()
+        retry.cancel()
+        # alone in the queue, the retry drops the used connection to make room for its own
+        o2 = c._origin("http://127.0.0.1:10")
+        o2.open = 1
+        used2 = Tracked(o2)
+        used2.uses = 1
+        retry2 = asyncio.ensure_future(c._acquire(o2, deadline, fresh=True))
+        await asyncio.sleep(0)
+        c._connect = lambda o, d, infos=None: asyncio.sleep(0, "fresh")  # the retry's own connect
+        c._release(used2, True)
+        got2 = await asyncio.wait_for(retry2, 1)
+        await c.close()
+        return got, used, pending, o.open, got2, used2
+    got, used, pending, open_, got2, used2 = run(go())
+    assert got is used and not used.aborted and pending and open_ == 1
+    assert got2 == "fresh" and used2.aborted
