@@ -528,20 +528,10 @@ void count_request(CallObject* c) {
 // Python method frame. The event's second and later sink requests (a status event's move, then
 // its hooks: index.js:83,99,112) are continuations: if they have to wait for a connection they
 // wait at the front of the origin's queue, not behind the first requests of newer deliveries.
-// A/B switch for the round-4 native-I/O budget: BEHOLDER_AB_FRONT=0 queues an
-// event's later sink requests at the back like any other.
-bool front_enabled() {
-  static const bool on = [] {
-    const char* v = std::getenv("BEHOLDER_AB_FRONT");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
-
 PyObject* http_request(CallObject* c, PyObject* http, PyObject* method, PyObject* url, PyObject* params,
                        PyObject* timeout) {
   HandlersObject* hs = c->hs;
-  const bool front = c->nreq > 0 && front_enabled();
+  const bool front = c->nreq > 0;
   count_request(c);
   PyObject** dp = _PyObject_GetDictPtr(http);
   PyObject* rec = dp && *dp ? PyDict_GetItemWithError(*dp, s_native_record) : nullptr;

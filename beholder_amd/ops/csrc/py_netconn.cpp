@@ -430,6 +430,11 @@ int hs_step(ReactorJob* rj) {
 // The job has left the reactor: hand it to its loop, or free it if its connection is gone.
 void hs_finish(ReactorJob* rj) {
   auto* j = static_cast<HsJob*>(rj);
+  // The deadline scan walks the registry until the unlink that precedes this call, so it can shut
+  // the socket of a job whose last step had already succeeded: that connection is unusable, and
+  // the honest outcome is the timeout the scan enforced, not a success whose first request fails
+  // as a connection error. Past the unlink the flag can no longer change.
+  if (j->result == HR_OK && j->expired.load()) j->result = HR_TIMEOUT;
   if (j->sys_errno && j->result == HR_OK) {
     j->reason = "SYSCALL";
     j->message = std::string("[SSL: SYSCALL] epoll_ctl: ") + strerror(j->sys_errno);
@@ -487,19 +492,9 @@ bool hs_submit(HsJob* j) {
 
 // Starts the handshake of `c` (connected, SSL set up) on a handshake thread when it can (a
 // NetPoller to take the fd out of), else on the loop. 0 or -1 with a Python error.
-// A/B switch for the round-4 native-I/O budget: BEHOLDER_AB_HS_THREADS=0
-// keeps every handshake on the loop thread (no handshake threads are started).
-bool hs_threads_enabled() {
-  static const bool on = [] {
-    const char* v = std::getenv("BEHOLDER_AB_HS_THREADS");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
-
 int tls_start(NetConnObject* c) {
   c->tls_state = 1;
-  if (!c->poller || !hs_threads_enabled()) return tls_handshake(c);
+  if (!c->poller) return tls_handshake(c);
   std::shared_ptr<HsWake> wake = netpoll_wake(c->poller);
   if (!wake) return tls_handshake(c);
   auto* j = new (std::nothrow) HsJob();
@@ -1255,7 +1250,6 @@ PyGetSetDef nc_getset[] = {
 // Called when a TlsContext is made (service startup): the threads start and warm up before the
 // first connect needs them. Failure is not an error here; hs_submit tries again.
 void hs_prestart() {
-  if (!hs_threads_enabled()) return;
   try {
     hs_pool();
   } catch (const std::exception&) {

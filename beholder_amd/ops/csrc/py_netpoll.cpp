@@ -336,14 +336,17 @@ std::shared_ptr<HsWake> netpoll_wake(PyObject* po) {
   }
 }
 
-// Stop reporting readiness of `fd` (it stays in the set; a hang-up or an error is still
-// reported): a handshake thread owns the socket for now. netpoll_set_write restores it. 0 or -1.
+// Stop reporting readiness of `fd` while a handshake thread owns the socket; netpoll_set_write
+// restores it. The fd stays in the set (its entry in `conns` too), but epoll reports EPOLLERR and
+// EPOLLHUP whatever the mask says, and the set is level-triggered: a peer reset during the
+// offload would wake this loop on every iteration until the handshake thread posts the job.
+// EPOLLONESHOT disarms the fd after the first such report. 0 or -1.
 int netpoll_pause(PyObject* po, int fd) {
   PollerObject* p = reinterpret_cast<PollerObject*>(po);
   if (p->epfd < 0) return 0;
   epoll_event ev;
   memset(&ev, 0, sizeof ev);
-  ev.events = 0;
+  ev.events = EPOLLONESHOT;
   ev.data.fd = fd;
   if (epoll_ctl(p->epfd, EPOLL_CTL_MOD, fd, &ev) < 0) {
     PyErr_SetFromErrno(PyExc_OSError);

@@ -40,7 +40,6 @@ import base64
 import collections
 import functools
 import ipaddress
-import os
 import socket
 import ssl as _ssl
 import time
@@ -58,9 +57,6 @@ from .http import HttpClient, HttpError, HttpResponse, encode_query, redact, wit
 
 _IDEMPOTENT = frozenset(("GET", "HEAD", "PUT", "DELETE", "OPTIONS"))
 _BODY_METHODS = frozenset(("POST", "PUT", "PATCH", "DELETE"))
-# A/B switch for the round-4 native-I/O budget: BEHOLDER_AB_FRONT=0 queues an
-# event's later sink requests at the back (the compiled handlers read the same variable)
-_FRONT = os.environ.get("BEHOLDER_AB_FRONT", "1") != "0"
 _REDIRECTS = frozenset((301, 302, 303, 307, 308))
 _TICK = 0.05  # deadline sweep period (s): timeouts fire at most this late
 _PATH_SAFE = "".join(chr(c) for c in range(0x21, 0x7F) if chr(c) not in '"<>\\^`{|}')
@@ -715,7 +711,7 @@ class H1Client(HttpClient):
         queue: in a burst (the first deliveries after start, or a pool at ``max_per_host``) a
         status event's move / hook requests would otherwise queue behind every newer delivery's
         first request, once per request, and set the tail of the handle latency."""
-        if front and _FRONT:
+        if front:
             o.waiters.appendleft(w)
         else:
             o.waiters.append(w)

@@ -40,7 +40,7 @@ ALLOWED_IDENTIFIERS = {
     # the capabilities a Pool (`native_pick`, over its connections) and an H1Client (`native_call`)
     # hand out, called directly
     "Pool", "_conns", "native_pick", "beholder_amd.ops._native", "beholder_amd.store.pgwire", "pg_pool_execute",
-    "size", "spread_at", "native_call", "native_record", "BEHOLDER_AB_FRONT", "h1_fast",
+    "size", "spread_at", "native_call", "native_record", "h1_fast",
 }
 # internal errors and docstrings (Python-level diagnostics, never emitted by the reference)
 ALLOWED_MESSAGES = {

@@ -703,3 +703,37 @@ def test_handshakes_waiting_for_slow_peers_do_not_hold_the_handshake_threads():
     assert err is None and opened == n and status == 200
     assert offloaded == n
     assert delay <= took < 2 * delay + 0.15, took
+
+
+def test_peer_reset_during_offloaded_handshakes_fails_them_promptly():
+    """A peer that resets the connection right after the ClientHello, while the handshake runs on
+    a handshake thread (the loop's poller has the socket paused with EPOLLONESHOT, so the reset's
+    EPOLLHUP wakes the loop at most once): every request fails with a connection error,
+    quickly, and no socket is left behind."""
+    import socket
+    import struct
+
+    import psutil
+
+    async def go():
+        async def rst(r, w):
+            await r.read(1)  # the ClientHello has arrived
+            so = w.get_extra_info("socket")
+            so.setsockopt(socket.SOL_SOCKET, socket.SO_LINGER, struct.pack("ii", 1, 0))
+            w.transport.abort()  # RST
+
+        srv = await asyncio.start_server(rst, "127.0.0.1", 0)
+        port = srv.sockets[0].getsockname()[1]
+        c = H1Client(timeout_s=5, ssl_cafile=TLS_CERT, max_per_host=16, max_connecting=16)
+        t0 = asyncio.get_running_loop().time()
+        res = await asyncio.gather(*[c.request("GET", f"https://127.0.0.1:{port}/x") for _ in range(16)],
+                                   return_exceptions=True)
+        took = asyncio.get_running_loop().time() - t0
+        await c.close()
+        srv.close()
+        await asyncio.sleep(0.05)
+        left = sum(1 for k in psutil.Process().net_connections(kind="tcp") if k.raddr and k.raddr.port == port)
+        return res, took, left
+    res, took, left = run(go())
+    assert all(isinstance(x, HttpError) for x in res), res
+    assert took < 2.0 and left == 0
