@@ -11,7 +11,10 @@ protobuf-encoded, framed) pushed through the **whole** service path of the consu
       -> native protobuf decode -> handler logic (index.js:62-155)
       -> media store (in-memory, 10k rows) -> Prometheus counters
       -> Trello/Telegram/Emby request construction (URL + query encoding)
-         into an in-process HTTP recorder (no network)
+         into an in-process HTTP recorder (no network; its counting, URL building
+         and call log are native, ops/csrc/py_recorder.cpp, and the compiled
+         handlers call it directly, as they call the H1 client's native path
+         in production)
       -> pino JSON log line per reference log call (info level, to /dev/null)
       -> ack (latency recorded natively)
 
@@ -39,9 +42,17 @@ region):
   AMQP replay broker, a Postgres fake and HTTP fakes in their own processes).
 * ``tls_e2e_*``: the same with HTTPS sinks, as Trello and Telegram are in production.
 
-Order of the phases: everything that starts child processes (the TCP fakes, the all-process
-consumers) runs before the headline phase, whose ``torch.cuda.synchronize()`` is the first HIP
-call of this process (a process that initialised the GPU must not start programs).
+Order of the phases: (1) everything that starts child processes (config 1's CLI process, the TCP
+fakes, the all-process consumers); (2) the paced configs 2-4, in process, before HIP is touched;
+(3) the headline between two calibration runs, whose ``torch.cuda.synchronize()`` is the first
+HIP call of this process (a process that initialised the GPU must not start programs); (4) the
+soak (config 5).
+
+* ``plumbing_*``: BASELINE config 1, 100 events on the stdin of ``python -m beholder_amd run``
+  with ``/metrics`` scraped before it exits.
+* ``calib_*``: fixed-work calibrations before and after the headline (see CALIB_REF below).
+* ``*_slow_*``: the slowest 0.1% of ``tcp_e2e`` / ``tls_e2e`` deliveries blamed on the process
+  that stalled under them (bench/stallmon.py).
 
 Prints ONE JSON line on rank 0.
 """
@@ -491,11 +502,14 @@ def soak_extras(a) -> dict:
 #                 other tenants' traffic moves);
 #   calib_py_ns   a fixed pure-Python loop (the interpreter: dict, str and int churn, as the
 #                 consumer's Python glue does).
-# CALIB_REF_* are the same figures on the builder's reference box runs (profiles/box_r4_calib/).
+# CALIB_REF holds the medians of the same figures over the builder's reference box runs
+# (profiles/box_r4_calib1/, 8 runs on one box). value_calibrated = value * calib_ns / CALIB_REF:
+# the headline a box with the reference box's core speed would have given. README "Reading the
+# headline" explains what the calibrations do and do not account for.
 CALIB_ITERS = 4_000_000
 CALIB_MEM_BYTES, CALIB_MEM_STEPS = 8 << 20, 500_000
 CALIB_REPS = 5
-CALIB_REF = {"calib_ns": None, "calib_mem_ns": None, "calib_py_ns": None}
+CALIB_REF = {"calib_ns": 6_439_000, "calib_mem_ns": 5_627_000, "calib_py_ns": 2_766_000}
 
 
 def _calib_py_once() -> int:
@@ -572,10 +586,10 @@ def main(argv=None) -> int:
             cal[k] = max(max(c0[k], c1[k]) for c0, c1 in calibs)
             cal[k + "_before"] = calib0[k]
             cal[k + "_after"] = calib1[k]
-        ref = CALIB_REF["calib_py_ns"]
+        ref = CALIB_REF["calib_ns"]
         cal.update({"calib_ref": CALIB_REF,
-                    # what a box as fast as the reference box (by the interpreter calibration) would give
-                    "value_calibrated": round(value * cal["calib_py_ns"] / ref, 1) if ref else None,
+                    # what a box with the reference box's core speed (the C loop) would give
+                    "value_calibrated": round(value * cal["calib_ns"] / ref, 1) if ref else None,
                     **_cg("headline", cgroup_delta(cg0, cg1))})
         out = {
             "metric": BASELINE_METRIC,
@@ -590,7 +604,8 @@ def main(argv=None) -> int:
             "vs_baseline": None,
             "dtype": "protobuf-events (no tensor compute)",
             "data": "synthetic telemetry (90% progress / 10% status), 10k-media in-memory store, "
-                    "Trello/Telegram/Emby stubbed in-process, info logs to /dev/null",
+                    "Trello/Telegram/Emby stubbed in-process (native recorder: URL + query built and logged "
+                    "per request), info logs to /dev/null",
             "config": {
                 "model": "beholder telemetry consumer (status+progress handlers, index.js:62-155)",
                 "global_batch": a.events_per_step * n,
