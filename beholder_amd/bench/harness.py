@@ -191,9 +191,9 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
     mon = None
     if rate > 0:  # paced: where a slow receive->ack came from (the loop stalled, or was preempted)
         from .stallmon import StallMonitor
-        # default 1 ms threshold: an idle loop's timer wakes up to 1 ms late by construction
-        # (epoll_wait takes whole milliseconds; asyncio rounds the timeout up)
-        mon = StallMonitor().start()
+        # 2 ms threshold: an idle loop's timer wakes up to ~1 ms late by construction (epoll_wait
+        # takes whole milliseconds and asyncio rounds the timeout up), which is not a stall
+        mon = StallMonitor(threshold_us=2000).start()
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
     rt0 = resource.getrusage(resource.RUSAGE_THREAD)
     t0 = time.perf_counter()
@@ -235,7 +235,7 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
                           http.counts["requests"] if hasattr(http, "counts") else None),
         "max_inflight": max_inflight[0],
         "cpu_us_per_event": cpu_s / s["acked"] * 1e6 if s["acked"] else None,
-        # the event loop's thread: preemptions by other work on its CPU, and its stalls >= 1 ms
+        # the event loop's thread: preemptions by other work on its CPU, and its stalls >= 2 ms
         "loop_thread_nivcsw": rt1.ru_nivcsw - rt0.ru_nivcsw,
         **({"loop": mon.summary()} if mon is not None else {}),
         "error_samples": sink.samples,
