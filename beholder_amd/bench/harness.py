@@ -446,7 +446,7 @@ def _http_tcp(w: Workload, n: int, servers: int = 3, clients=("h1", "aiohttp")) 
 
 
 def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = False, preconnect: int = 0,
-             max_connecting: int = 8) -> dict:
+             max_connecting: int = 8, hooks: Optional[tuple] = None) -> dict:
     """Production-shaped: every dependency over real TCP. A replay AMQP broker streams n
     events (prefetch 100, index.js:43). Each handler reads / updates the media row in a
     fake Postgres (pipelined ``pgwire``). Every sink call goes to a fake HTTP endpoint
@@ -454,7 +454,8 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
     the consumer process. ``tls`` (config ``tls_e2e``): the sinks are HTTPS, as Trello and
     Telegram are in production (certificate verified against the bench's own CA). ``preconnect``:
     ``service.http.preconnect`` (sink connections opened at init, before the clock).
-    ``max_connecting``: ``service.http.max_connecting`` (connects + handshakes in flight per origin)."""
+    ``max_connecting``: ``service.http.max_connecting`` (connects + handshakes in flight per origin).
+    ``hooks``: ``(start, stop)`` callables run around the measured phase (scripts/cprof.py)."""
     from ..config import Config
     from ..service import Service
     from ..sinks import H1Client
@@ -511,9 +512,13 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             rss0 = _rss_mb()  # pools full, code paths warm: later growth would be a leak
             cg1 = cgroup_cpu_stat()
             ru0 = resource.getrusage(resource.RUSAGE_SELF)
+            if hooks:
+                hooks[0]()
             t0 = time.perf_counter()
             await _wait_acked(src.settler, n, task)
             elapsed = time.perf_counter() - t0
+            if hooks:
+                hooks[1]()
             ru1 = resource.getrusage(resource.RUSAGE_SELF)
             cg2 = cgroup_cpu_stat()
             mon.stop()

@@ -8,6 +8,7 @@ their symbol tables (``nm``: our extension's full table, the interpreter's expor
 Prints the top functions by self samples, and the split by object.
 
     python scripts/cprof.py [--steps 20] [--hz 2000] [--top 60] [--tid main|all]
+    python scripts/cprof.py --workload tcp_e2e|tls_e2e [--events 200000]   # the production-shaped path
 """
 from __future__ import annotations
 
@@ -103,6 +104,8 @@ def main(argv=None) -> int:
     ap.add_argument("--hz", type=int, default=2000)
     ap.add_argument("--top", type=int, default=60)
     ap.add_argument("--tid", default="main", choices=["main", "all"])
+    ap.add_argument("--workload", default="headline", choices=["headline", "tcp_e2e", "tls_e2e"])
+    ap.add_argument("--events", type=int, default=200_000, help="tcp_e2e / tls_e2e events")
     a = ap.parse_args(argv)
     import bench
     from beholder_amd.ops import native
@@ -117,7 +120,14 @@ def main(argv=None) -> int:
         res["samples"], res["lost"] = native.prof_stop()
 
     res: dict = {}
-    r = asyncio.run(bench.run_consumer(ba, 0, go, stop))
+    if a.workload == "headline":
+        r = asyncio.run(bench.run_consumer(ba, 0, go, stop))
+    else:
+        from beholder_amd.bench import harness
+        tls = a.workload == "tls_e2e"
+        x = harness._tcp_e2e(a.events, http_servers=4 if tls else 2, tls=tls, hooks=(go, stop))
+        r = {"events": x["measured_events"], "elapsed": x["elapsed_s"],
+             "cpu_s": x["cpu_us_per_event"] * x["measured_events"] / 1e6}
     mp = maps()
     starts = [m[0] for m in mp]
     samples = res["samples"]
