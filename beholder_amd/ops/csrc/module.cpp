@@ -151,10 +151,16 @@ PyObject* mod_calib_mem(PyObject*, PyObject* args) {
   }
   uint64_t* a = static_cast<uint64_t*>(std::aligned_alloc(64, lines * 64));
   if (!a) return PyErr_NoMemory();
+  std::vector<uint32_t> perm;
+  try {
+    perm.resize(lines);
+  } catch (const std::bad_alloc&) {
+    std::free(a);
+    return PyErr_NoMemory();
+  }
   int64_t t0, t1;
   uint64_t idx = 0;
   Py_BEGIN_ALLOW_THREADS
-  std::vector<uint32_t> perm(lines);
   for (size_t i = 0; i < lines; ++i) perm[i] = uint32_t(i);
   uint64_t x = 0x2545F4914F6CDD1Dull;
   for (size_t i = lines - 1; i > 0; --i) {  // Sattolo: a single cycle through every line

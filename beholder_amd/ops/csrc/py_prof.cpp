@@ -29,10 +29,15 @@ uint64_t* g_ip = nullptr;
 uint32_t* g_tid = nullptr;
 std::atomic<size_t> g_n{0};
 std::atomic<uint64_t> g_lost{0};
+std::atomic<bool> g_active{false};
 bool g_armed = false;
-struct sigaction g_old;
+bool g_installed = false;
 
+// Installed once and never removed: a SIGPROF generated just before the timer is disarmed can
+// still be pending for another thread, and under the default disposition it would end the
+// process. While no profile is being taken the handler returns at once.
 void on_sigprof(int, siginfo_t*, void* uc_v) {
+  if (!g_active.load(std::memory_order_relaxed)) return;
   size_t i = g_n.fetch_add(1, std::memory_order_relaxed);
   if (i >= kMaxSamples) {
     g_lost.fetch_add(1, std::memory_order_relaxed);
@@ -67,17 +72,21 @@ PyObject* prof_start(PyObject*, PyObject* args) {
   }
   g_n.store(0);
   g_lost.store(0);
-  struct sigaction sa = {};
-  sa.sa_sigaction = on_sigprof;
-  sa.sa_flags = SA_SIGINFO | SA_RESTART;
-  sigemptyset(&sa.sa_mask);
-  if (sigaction(SIGPROF, &sa, &g_old) < 0) return PyErr_SetFromErrno(PyExc_OSError);
+  if (!g_installed) {
+    struct sigaction sa = {};
+    sa.sa_sigaction = on_sigprof;
+    sa.sa_flags = SA_SIGINFO | SA_RESTART;
+    sigemptyset(&sa.sa_mask);
+    if (sigaction(SIGPROF, &sa, nullptr) < 0) return PyErr_SetFromErrno(PyExc_OSError);
+    g_installed = true;
+  }
+  g_active.store(true);
   struct itimerval it = {};
   it.it_interval.tv_sec = 0;
   it.it_interval.tv_usec = 1000000 / hz;
   it.it_value = it.it_interval;
   if (setitimer(ITIMER_PROF, &it, nullptr) < 0) {
-    sigaction(SIGPROF, &g_old, nullptr);
+    g_active.store(false);
     return PyErr_SetFromErrno(PyExc_OSError);
   }
   g_armed = true;
@@ -89,11 +98,9 @@ PyObject* prof_stop(PyObject*, PyObject*) {
     PyErr_SetString(PyExc_RuntimeError, "profiler not running");
     return nullptr;
   }
+  g_active.store(false);
   struct itimerval off = {};
   setitimer(ITIMER_PROF, &off, nullptr);
-  // a SIGPROF already queued is handled by our handler before the old one is restored below;
-  // samples past this point are dropped by the bounds check
-  sigaction(SIGPROF, &g_old, nullptr);
   g_armed = false;
   size_t n = g_n.load();
   if (n > kMaxSamples) n = kMaxSamples;
