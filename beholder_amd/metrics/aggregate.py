@@ -125,9 +125,40 @@ class ClusterMetricsServer:
         self._alive = alive
         self._httpd: Optional[ThreadingHTTPServer] = None
         self._thread: Optional[threading.Thread] = None
+        # last good exposition per worker: a worker that misses one scrape (a loaded host, a long
+        # GC pause) is served from it, so the merged counters never step back (Prometheus would
+        # read a drop in a summed counter as a reset); beholder_cluster_worker_up says it was stale
+        self._last: Dict[int, str] = {}
+        self._failures: Dict[int, int] = {}
+        self._lock = threading.Lock()
 
     def _gather(self, path: str) -> List[Tuple[int, Optional[str]]]:
         return [(i, fetch(f"http://127.0.0.1:{p}{path}")) for i, p in self._worker_ports()]
+
+    def merged_metrics(self) -> str:
+        """The workers' expositions summed, a worker whose scrape failed taken from its last good
+        one, plus ``beholder_cluster_worker_up{worker}`` and
+        ``beholder_cluster_scrape_failures_total{worker}``."""
+        got = self._gather("/metrics")
+        texts, up = [], []
+        with self._lock:
+            for i, t in got:
+                up.append((i, bool(t)))
+                if t:
+                    self._last[i] = t
+                else:
+                    self._failures[i] = self._failures.get(i, 0) + 1
+                    t = self._last.get(i)
+                if t:
+                    texts.append(t)
+            fails = dict(self._failures)
+        extra = ["# HELP beholder_cluster_worker_up 1 when the worker answered this scrape (0: its last good "
+                 "exposition was used)", "# TYPE beholder_cluster_worker_up gauge"]
+        extra += [f'beholder_cluster_worker_up{{worker="{i}"}} {1 if ok else 0}' for i, ok in up]
+        extra += ["# HELP beholder_cluster_scrape_failures_total Worker scrapes that failed since the supervisor "
+                  "started", "# TYPE beholder_cluster_scrape_failures_total counter"]
+        extra += [f'beholder_cluster_scrape_failures_total{{worker="{i}"}} {fails.get(i, 0)}' for i, _ in up]
+        return aggregate(texts) + "\n".join(extra) + "\n"
 
     def start(self) -> "ClusterMetricsServer":
         outer = self
@@ -146,8 +177,7 @@ class ClusterMetricsServer:
             def do_GET(self):  # noqa: N802
                 path = self.path.split("?", 1)[0]
                 if path == "/metrics":
-                    texts = [t for _, t in outer._gather("/metrics") if t]
-                    self._send(200, aggregate(texts).encode(), "text/plain; version=0.0.4; charset=utf-8")
+                    self._send(200, outer.merged_metrics().encode(), "text/plain; version=0.0.4; charset=utf-8")
                 elif path == "/healthz":
                     ok = outer._alive() and all(t is not None and t.strip() == "ok"
                                                 for _, t in outer._gather("/healthz"))

@@ -114,3 +114,24 @@ def test_native_buckets_match_bisect_reference():
     check()
     with pytest.raises(ValueError):
         native.Buckets([1, 1])
+
+
+def test_cluster_metrics_serve_a_missed_worker_from_its_last_exposition(monkeypatch):
+    """A worker that misses a scrape is summed from its last good exposition, so the merged
+    counters never step back, and beholder_cluster_worker_up / _scrape_failures_total say so."""
+    from beholder_amd.metrics import aggregate as agg
+    answers = {1: ["c_total 5\n", None, "c_total 7\n"], 2: ["c_total 1\n", "c_total 2\n", "c_total 3\n"]}
+
+    def fake_fetch(url, timeout=2.0):
+        port = int(url.split(":")[2].split("/")[0])
+        return answers[port].pop(0)
+    monkeypatch.setattr(agg, "fetch", fake_fetch)
+    srv = agg.ClusterMetricsServer("127.0.0.1", 0, lambda: [(0, 1), (1, 2)], lambda: True)
+    first, second, third = srv.merged_metrics(), srv.merged_metrics(), srv.merged_metrics()
+
+    def val(text, key):
+        return float([ln for ln in text.splitlines() if ln.startswith(key + " ")][0].split()[-1])
+    assert val(first, "c_total") == 6 and val(second, "c_total") == 7 and val(third, "c_total") == 10
+    assert val(second, 'beholder_cluster_worker_up{worker="0"}') == 0
+    assert val(second, 'beholder_cluster_worker_up{worker="1"}') == 1
+    assert val(third, 'beholder_cluster_scrape_failures_total{worker="0"}') == 1
