@@ -172,6 +172,20 @@ inline bool word_needs_escape(uint64_t w) {
   return (ctl | quote | bslash) != 0;
 }
 
+bool needs_escape(const char* s, size_t n) {
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    memcpy(&w, s + i, 8);
+    if (word_needs_escape(w)) return true;
+  }
+  for (; i < n; ++i) {
+    unsigned char c = static_cast<unsigned char>(s[i]);
+    if (c < 0x20 || c == '"' || c == '\\') return true;
+  }
+  return false;
+}
+
 void json_escape_append(std::string& out, const char* s, size_t n) {
   static const char* hex = "0123456789abcdef";
   size_t i = 0;
@@ -350,11 +364,17 @@ bool append_line(std::string& out, long lvl, long long t, const char* prefix, Py
     out.append(ex, size_t(el));
   }
   if (nargs) {
-    static thread_local std::string msg;  // scratch: no allocation per line
-    msg.clear();
-    if (!quick_format_append(msg, argv, nargs, drop_extra)) return false;
     out += ",\"msg\":\"";
-    json_escape_append(out, msg.data(), msg.size());
+    // format straight into the line; escape afterwards only if the text needs it (rare: the
+    // handlers' messages are plain text), which saves a copy of every message
+    const size_t at = out.size();
+    if (!quick_format_append(out, argv, nargs, drop_extra)) return false;
+    if (needs_escape(out.data() + at, out.size() - at)) {
+      static thread_local std::string msg;  // scratch: no allocation per line
+      msg.assign(out, at, std::string::npos);
+      out.resize(at);
+      json_escape_append(out, msg.data(), msg.size());
+    }
     out += '"';
   }
   out += ",\"v\":1}\n";
