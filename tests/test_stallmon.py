@@ -1,0 +1,47 @@
+"""bench/stallmon.py: stall intervals and the attribution of slow deliveries to processes."""
+import asyncio
+import time
+
+from beholder_amd.bench.stallmon import StallMonitor, _overlap, attribute, parse_stall_lines
+
+
+def test_overlap_merges_overlapping_intervals():
+    ivs = sorted([(0, 10), (5, 20), (30, 40), (100, 200)])
+    starts = [a for a, _ in ivs]
+    assert _overlap(0, 50, ivs, starts) == 30  # [0,20) + [30,40)
+    assert _overlap(15, 35, ivs, starts) == 10  # [15,20) + [30,35)
+    assert _overlap(50, 90, ivs, starts) == 0
+    assert _overlap(150, 400, ivs, starts) == 50
+
+
+def test_attribute_blames_the_process_that_stalled_under_each_delivery():
+    slow = [(0, 100, 1100),      # 1 ms; pg stalled 100..900
+            (0, 2000, 3000),     # 1 ms; consumer stalled 2000..2900, pg a little
+            (0, 5000, 6000)]     # 1 ms; nothing stalled: queueing
+    sources = {"consumer": [(2000, 2900)], "pg": [(100, 900), (2950, 3000)], "http": []}
+    r = attribute(slow, sources)
+    assert r["deliveries"] == 3
+    assert r["blamed"] == {"consumer": 1, "pg": 1, "http": 0, "none": 1}
+    assert r["time_share"]["pg"] == round((800 + 50) / 3000, 3)
+    # under min_share: a 10% overlap is not enough to blame
+    assert attribute([(0, 0, 1000)], {"pg": [(0, 100)]})["blamed"] == {"pg": 0, "none": 1}
+
+
+def test_monitor_records_a_blocked_loop_as_a_stall_and_round_trips_its_report():
+    async def go():
+        mon = StallMonitor(period_s=0.001, threshold_us=5000).start()
+        await asyncio.sleep(0.02)
+        t0 = time.monotonic_ns()
+        time.sleep(0.03)  # the loop is blocked for 30 ms
+        t1 = time.monotonic_ns()
+        await asyncio.sleep(0.02)
+        mon.stop()
+        return mon, t0, t1
+    mon, t0, t1 = asyncio.run(go())
+    s = mon.summary()
+    assert s["loop_stalls"] >= 1 and s["loop_lag_max_us"] >= 20_000
+    a, b = max(mon.loop_stalls, key=lambda iv: iv[1] - iv[0])
+    assert a >= t0 - 2_000_000 and b >= t1 - 1_000_000  # the stall interval covers the block
+    rep = parse_stall_lines("noise\n" + mon.dump_line("pg") + "\nDONE queries=1\n")
+    assert rep[0]["name"] == "pg" and [tuple(x) for x in rep[0]["stall_intervals"]] == \
+        [tuple(x) for x in mon.loop_stalls + mon.gc_pauses]
