@@ -5,7 +5,13 @@
 //     with intact payloads (wrap-around exercised by a tiny ring);
 //   * DROP_NEWEST accounting: accepted + dropped == offered;
 //   * the Framer reassembles a stream split at random chunk boundaries;
-//   * close() wakes a blocked producer and a waiting consumer.
+//   * close() wakes a blocked producer and a waiting consumer;
+//   * the event-loop consumer (pop without waiting, arm(), sleep on the eventfd) never misses a
+//     wake-up: every record is consumed while producers push at random intervals.
+#include <poll.h>
+#include <sys/eventfd.h>
+#include <unistd.h>
+
 #include <atomic>
 #include <cassert>
 #include <cstdio>
@@ -151,12 +157,61 @@ static void close_wakes_everyone() {
   std::printf("close ok\n");
 }
 
+// The FdSource pattern (transport/ingest.py): non-blocking pop; when empty, arm() and poll the
+// eventfd (with a long timeout that must never be what wakes us up).
+static void eventfd_consumer(int producers, int per) {
+  ByteRing ring(1 << 16, 0, POLICY_BLOCK);
+  int efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+  CHECK(efd >= 0);
+  ring.set_notify_fd(efd);
+  std::atomic<int> live{producers};
+  std::vector<std::thread> ts;
+  for (int p = 0; p < producers; ++p) {
+    ts.emplace_back([&, p] {
+      std::mt19937 rng(uint32_t(p) + 7);
+      uint8_t buf[24] = {0};
+      for (int i = 0; i < per; ++i) {
+        if (rng() % 8 == 0) std::this_thread::sleep_for(std::chrono::microseconds(rng() % 200));
+        CHECK(ring.push(1, 0, buf, sizeof buf, 0) == 1);
+      }
+      if (--live == 0) ring.set_eof();
+    });
+  }
+  long got = 0, parks = 0, timeouts = 0;
+  const long want = long(producers) * per;
+  for (;;) {
+    size_t avail = ring.wait_readable(0);
+    if (avail) {
+      uint64_t pos = ring.read_begin(), end = ring.read_end();
+      uint64_t n = 0;
+      while (ring.next_record(pos, end)) ++n;
+      ring.consume(pos, n);
+      got += long(n);
+      continue;
+    }
+    if (ring.drained()) break;
+    if (!ring.arm()) continue;  // something arrived between the pop and arm()
+    ++parks;
+    pollfd pfd = {efd, POLLIN, 0};
+    int r = poll(&pfd, 1, 5000);
+    if (r == 0) ++timeouts;  // a lost wake-up: only the timeout got us out
+    uint64_t v;
+    ssize_t rd = read(efd, &v, sizeof v);
+    (void)rd;
+  }
+  for (auto& t : ts) t.join();
+  close(efd);
+  CHECK(got == want && timeouts == 0);
+  std::printf("eventfd_consumer ok: %ld records, %ld parks, no lost wake-up\n", got, parks);
+}
+
 int main() {
   mpsc_block(4, 20000, 8192);
   mpsc_block(1, 50000, 4096);
   drop_newest(200000);
   framer_random_chunks();
   close_wakes_everyone();
+  eventfd_consumer(3, 20000);
   std::printf("ALL OK\n");
   return 0;
 }
