@@ -272,6 +272,9 @@ async def run_consumer(a, seed: int, go, stop=None, *, steps: int = None, warmup
         # is other load on the box, not the consumer
         "cpu_s": (ru1.ru_utime + ru1.ru_stime) - (ru0.ru_utime + ru0.ru_stime) if ru0 else 0.0,
         "nivcsw": ru1.ru_nivcsw - ru0.ru_nivcsw if ru0 else 0,
+        # page faults in the timed steps: a box still compacting memory shows here, not in calib_*
+        "minflt": ru1.ru_minflt - ru0.ru_minflt if ru0 else 0,
+        "majflt": ru1.ru_majflt - ru0.ru_majflt if ru0 else 0,
     }
 
 
@@ -525,6 +528,16 @@ def _calib_py_once() -> int:
     return time.perf_counter_ns() - t0
 
 
+def _thp_mode():
+    """The host's transparent-huge-page mode (the bracketed word of the sysfs setting)."""
+    try:
+        with open("/sys/kernel/mm/transparent_hugepage/enabled") as f:
+            t = f.read()
+        return t[t.index("[") + 1:t.index("]")]
+    except (OSError, ValueError):
+        return None
+
+
 def calibrate() -> dict:
     from beholder_amd.ops import calib, calib_mem
     return {"calib_ns": min(calib(CALIB_ITERS)[0] for _ in range(CALIB_REPS)),
@@ -570,7 +583,7 @@ def main(argv=None) -> int:
     calib1 = calibrate()
     elapsed = dist.max(res["elapsed"])
     parts = dist.gather({k: res[k] for k in ("handle_hist", "ingest_hist", "http_calls", "errors", "abandoned",
-                                             "events", "cpu_s", "nivcsw")})
+                                             "events", "cpu_s", "nivcsw", "minflt", "majflt")})
     calibs = dist.gather((calib0, calib1))
 
     # 4. BASELINE config 5 (no child processes: HIP may be initialised now)
@@ -621,6 +634,9 @@ def main(argv=None) -> int:
             "p99_handle_latency_us": round(hh.percentile(99) / 1e3, 3),
             "cpu_us_per_event": round(sum(p["cpu_s"] for p in parts) / total_events * 1e6, 3),
             "involuntary_ctx_switches": sum(p["nivcsw"] for p in parts),
+            "headline_minflt": sum(p["minflt"] for p in parts),
+            "headline_majflt": sum(p["majflt"] for p in parts),
+            "thp": _thp_mode(),
             **cal,
             "http_requests": sum(p["http_calls"] for p in parts),
             "handler_errors": sum(p["errors"] for p in parts),
