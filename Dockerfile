@@ -20,11 +20,7 @@ RUN useradd --uid 999 --create-home --home-dir /home/beholder beholder && chown 
 COPY --from=build /install /usr/local
 COPY --from=build --chown=999:999 /stack /stack
 USER 999
-# the interpreter's heap on transparent huge pages (beholder_amd/utils/heap.py: hosts in THP
-# "madvise" mode back it only when malloc asks; profiles/box_r4_alloc_ab/)
 ENV CONFIG_PATH=/stack/config \
-    BEHOLDER_ALLOW_BUILD=0 \
-    PYTHONMALLOC=malloc \
-    GLIBC_TUNABLES=glibc.malloc.hugetlb=1
+    BEHOLDER_ALLOW_BUILD=0
 EXPOSE 3000
 ENTRYPOINT ["python", "-m", "beholder_amd", "run"]

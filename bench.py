@@ -75,7 +75,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-from beholder_amd.utils.heap import heap_tuned, thp_mode  # noqa: E402
 from beholder_amd.utils.hostinfo import available_cpus, cpu_share, default_procs, gpus_on_node  # noqa: E402
 
 BASELINE_METRIC = "metric_events_ingested_per_sec"
@@ -529,6 +528,16 @@ def _calib_py_once() -> int:
     return time.perf_counter_ns() - t0
 
 
+def _thp_mode():
+    """The host's transparent-huge-page mode (the bracketed word of the sysfs setting)."""
+    try:
+        with open("/sys/kernel/mm/transparent_hugepage/enabled") as f:
+            t = f.read()
+        return t[t.index("[") + 1:t.index("]")]
+    except (OSError, ValueError):
+        return None
+
+
 def calibrate() -> dict:
     from beholder_amd.ops import calib, calib_mem
     return {"calib_ns": min(calib(CALIB_ITERS)[0] for _ in range(CALIB_REPS)),
@@ -627,8 +636,7 @@ def main(argv=None) -> int:
             "involuntary_ctx_switches": sum(p["nivcsw"] for p in parts),
             "headline_minflt": sum(p["minflt"] for p in parts),
             "headline_majflt": sum(p["majflt"] for p in parts),
-            "thp": thp_mode(),
-            "heap_hugepages": heap_tuned(),
+            "thp": _thp_mode(),
             **cal,
             "http_requests": sum(p["http_calls"] for p in parts),
             "handler_errors": sum(p["errors"] for p in parts),
@@ -659,8 +667,4 @@ def main(argv=None) -> int:
 
 
 if __name__ == "__main__":
-    # the interpreter's heap on transparent huge pages (utils/heap.py): a process-start setting,
-    # so the bench re-executes itself with it, before anything here has touched the GPU
-    from beholder_amd.utils.heap import reexec_with_hugepage_heap
-    reexec_with_hugepage_heap(sys.argv)
     raise SystemExit(main())

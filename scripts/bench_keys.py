@@ -3,7 +3,7 @@
 import json
 import sys
 
-KEYS = ["value", "cpu_us_per_event", "heap_hugepages", "thp", "headline_minflt", "calib_ns", "calib_ns_before", "calib_ns_after", "value_calibrated",
+KEYS = ["value", "cpu_us_per_event", "thp", "headline_minflt", "calib_ns", "calib_ns_before", "calib_ns_after", "value_calibrated",
         "involuntary_ctx_switches", "headline_nr_throttled",
         "rate_1k_p50_ingest_latency_us", "rate_1k_p99_ingest_latency_us", "rate_1k_p99_queue_latency_us",
         "rate_1k_p99_handle_latency_us", "rate_10k_p50_ingest_latency_us", "rate_10k_p99_ingest_latency_us",
