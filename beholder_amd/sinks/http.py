@@ -230,12 +230,24 @@ class RecordingHttpClient(HttpClient):
     def __init__(self, keep: Optional[int] = None, delay_s: float = 0.0):
         self.calls: Deque[Tuple[str, str]] = collections.deque(maxlen=keep)
         self.rules: List[Rule] = []
-        self.delay_s = delay_s
         self._ok = HttpResponse(200, b"{}", None, "")
         self._rec = _native_ops.Recorder(self.calls, self._ok)
-        # a subclass that overrides request() (jitter, counting) keeps every call on its own path
+        self.delay_s = delay_s  # (sets native_record)
+
+    @property
+    def delay_s(self) -> float:
+        return self._delay_s
+
+    @delay_s.setter
+    def delay_s(self, v: float) -> None:
+        self._delay_s = v
+        self._sync_fast_path()
+
+    def _sync_fast_path(self) -> None:
+        """Expose the native core to the compiled handlers only while every answer is the plain
+        ``200 {}`` with no delay, and no subclass overrides request() (jitter, counting)."""
         plain = type(self).request is RecordingHttpClient.request
-        self.native_record = self._rec if plain and not delay_s else None
+        self.native_record = self._rec if plain and not self._delay_s and not self.rules else None
 
     @property
     def count(self) -> int:
@@ -243,7 +255,7 @@ class RecordingHttpClient(HttpClient):
 
     def add_rule(self, method: str, url_prefix: str, fn) -> None:
         self.rules.append((method.upper(), url_prefix, fn))
-        self.native_record = None  # answers now depend on the rules: the Python path decides
+        self._sync_fast_path()  # answers now depend on the rules: the Python path decides
 
     def fail(self, method: str, url_prefix: str, status: Optional[int] = None, message: str = "ECONNREFUSED",
              body: bytes = b'"error"'):

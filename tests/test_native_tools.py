@@ -74,3 +74,13 @@ def test_recording_client_fast_path_only_without_rules_delay_or_override():
         asyncio.run(go())  # the rule added above fails POSTs to https://api
     assert plain.count == 1 and plain.urls() == ["https://api/x?a=1"]
 
+
+
+def test_recording_client_fast_path_follows_a_later_delay():
+    from beholder_amd.sinks import RecordingHttpClient
+    c = RecordingHttpClient()
+    assert c.native_record is not None
+    c.delay_s = 0.01
+    assert c.native_record is None
+    c.delay_s = 0.0
+    assert c.native_record is not None
