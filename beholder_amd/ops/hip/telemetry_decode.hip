@@ -84,18 +84,38 @@ __device__ __forceinline__ void decode_upb(const uint8_t* __restrict__ buf, int 
 }
 
 // ---- protobufjs 6.8.8 -------------------------------------------------------------------------
-// Positions are int64 relative to the message start: Reader.uint32() may step past the end
-// (reading `undefined`) before it reports the overrun, exactly as pbjs.hpp does.
+// Positions are relative to the message start and may step past its end: Reader.uint32() reads
+// `undefined` bytes before it reports the overrun, exactly as pbjs.hpp does. 32-bit arithmetic
+// (messages are < 2^31 bytes, checked on the host) and an unchecked fast path while at least 5
+// bytes remain keep the per-byte work at the upb kernel's level; only the last bytes of a
+// message take the bounds-checked path.
 
 struct PbjsReader {
   const uint8_t* __restrict__ p;  // message start
-  int64_t len;
-  int64_t pos;
+  int len;
+  int pos;
 
-  __device__ __forceinline__ int at(int64_t i) const { return i < len ? int(p[i]) : -1; }
+  __device__ __forceinline__ int at(int i) const { return i < len ? int(p[i]) : -1; }
 
   // Reader.prototype.uint32
   __device__ __forceinline__ bool uint32(uint32_t& out) {
+    if (pos + 5 <= len) {  // every byte it may read is inside the message
+      uint32_t b = p[pos++];
+      uint32_t v = b & 127u;
+      if (b < 128u) { out = v; return true; }
+      b = p[pos++]; v |= (b & 127u) << 7;
+      if (b < 128u) { out = v; return true; }
+      b = p[pos++]; v |= (b & 127u) << 14;
+      if (b < 128u) { out = v; return true; }
+      b = p[pos++]; v |= (b & 127u) << 21;
+      if (b < 128u) { out = v; return true; }
+      b = p[pos++]; v |= (b & 15u) << 28;
+      if (b < 128u) { out = v; return true; }
+      pos += 5;  // the 64-bit tail, unchecked byte by byte
+      if (pos > len) { pos = len; return false; }
+      out = v;
+      return true;
+    }
     uint32_t v = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -108,15 +128,15 @@ struct PbjsReader {
     v |= uint32_t(b < 0 ? 0 : (b & 15)) << 28;
     ++pos;
     if (b >= 0 && b < 128) { out = v; return true; }
-    pos += 5;  // the 64-bit tail, unchecked byte by byte
+    pos += 5;
     if (pos > len) { pos = len; return false; }
     out = v;
     return true;
   }
 
-  __device__ __forceinline__ bool skip_n(int64_t n) {
-    if (pos + n > len) return false;
-    pos += n;
+  __device__ __forceinline__ bool skip_n(uint32_t n) {
+    if (n > uint32_t(len - pos)) return false;  // pos <= len here
+    pos += int(n);
     return true;
   }
 
@@ -128,8 +148,8 @@ struct PbjsReader {
   }
 
   // Reader.prototype.skipType(wireType), groups counted instead of recursed into
-  __device__ bool skip_type(uint32_t wt) {
-    uint64_t depth = 0;
+  __device__ __forceinline__ bool skip_type(uint32_t wt) {
+    uint32_t depth = 0;
     for (;;) {
       switch (wt) {
         case 0: if (!skip_varint()) return false; break;
@@ -154,10 +174,10 @@ struct PbjsReader {
   }
 
   // BufferReader.prototype.string: the byte range clamped to the end
-  __device__ __forceinline__ bool string(int64_t& off, int64_t& n) {
+  __device__ __forceinline__ bool string(int& off, int& n) {
     uint32_t L;
     if (!uint32(L)) return false;
-    const int64_t e = pos + int64_t(L) < len ? pos + int64_t(L) : len;
+    const int e = L < uint32_t(len - pos) ? pos + int(L) : len;  // pos <= len here
     off = pos;
     n = e - pos;
     pos = e;
@@ -166,23 +186,21 @@ struct PbjsReader {
 };
 
 __device__ __forceinline__ void decode_pbjs(const uint8_t* __restrict__ buf, const int start, const int end, int* r) {
-  PbjsReader rd{buf + start, int64_t(end - start), 0};
+  PbjsReader rd{buf + start, end - start, 0};
   while (rd.pos < rd.len) {
     uint32_t t;
     if (!rd.uint32(t)) { r[6] = 0; return; }
     const uint32_t field = t >> 3;
     if (field == 1 || field == 4) {  // string mediaId / host
-      int64_t off, n;
+      int off, n;
       if (!rd.string(off, n)) { r[6] = 0; return; }
-      const int k = field == 1 ? 0 : 4;
-      r[k] = start + int(off);
-      r[k + 1] = int(n);
-      r[7] |= field == 1 ? 1 : 8;
+      if (field == 1) { r[0] = start + off; r[1] = n; r[7] |= 1; }
+      else { r[4] = start + off; r[5] = n; r[7] |= 8; }
     } else if (field == 2 || field == 3) {  // enum status / int32 progress: uint32() | 0
       uint32_t v;
       if (!rd.uint32(v)) { r[6] = 0; return; }
-      r[field] = static_cast<int32_t>(v);
-      r[7] |= field == 2 ? 2 : 4;
+      if (field == 2) { r[2] = static_cast<int32_t>(v); r[7] |= 2; }
+      else { r[3] = static_cast<int32_t>(v); r[7] |= 4; }
     } else if (!rd.skip_type(t & 7)) {
       r[6] = 0;
       return;
