@@ -275,6 +275,11 @@ class H1Client(HttpClient):
         self._tail_cl0 = f"User-Agent: {user_agent}\r\nContent-Length: 0\r\n\r\n".encode("latin-1")
         self.counts = {"requests": 0, "connections": 0, "reused": 0, "retries": 0, "errors": 0, "timeouts": 0,
                        "connecting_peak": 0, "connect_waits": 0}
+        # where a cold pool's time goes (the warm-up tail): each successful connect (+ TLS
+        # handshake), and each wait of a queued request until a connection was handed to it
+        self.dial_ns = _native.Histogram()
+        self.queue_wait_ns = _native.Histogram()
+        self._queued_at: Dict[object, int] = {}
 
     # -- pool ----------------------------------------------------------------
     def _origin(self, key: str) -> _Origin:
@@ -358,6 +363,7 @@ class H1Client(HttpClient):
         """Connect (+ TLS) on a slot :meth:`_reserve` counted; frees the slot either way."""
         loop = asyncio.get_running_loop()
         conn = _Conn(o)
+        t0 = time.monotonic_ns()
         try:
             remaining = deadline - loop.time()
             if remaining <= 0:
@@ -375,6 +381,7 @@ class H1Client(HttpClient):
             raise
         o.connecting -= 1
         self.counts["connections"] += 1
+        self.dial_ns.record(time.monotonic_ns() - t0)
         return conn
 
     def _grow(self, o: _Origin, deadline: float) -> None:
@@ -517,15 +524,20 @@ class H1Client(HttpClient):
             else:
                 o.waiters.append(w)
                 counts["connect_waits"] += 1
+            self._queued_at[w] = time.monotonic_ns()
             if not fresh and _queued(o):
                 self._grow(o, deadline)
             th = loop.call_at(deadline, _expire, w)
             try:
                 c = await w
             except asyncio.CancelledError:
+                self._queued_at.pop(w, None)
                 # a connection handed over just before the cancel must go back to the pool
                 if w.done() and not w.cancelled() and w.exception() is None and w.result() is not None:
                     self._release(w.result(), True)
+                raise
+            except BaseException:  # its deadline, a failed background connect
+                self._queued_at.pop(w, None)
                 raise
             finally:
                 th.cancel()
@@ -600,7 +612,10 @@ class H1Client(HttpClient):
         c.last_used = time.monotonic()
         while o.waiters:
             w = o.waiters.popleft()
+            t0 = self._queued_at.pop(w, None)
             if not w.done():
+                if t0 is not None:
+                    self.queue_wait_ns.record(time.monotonic_ns() - t0)
                 w.set_result(c)
                 return
         o.idle.append(c)
@@ -614,6 +629,7 @@ class H1Client(HttpClient):
     def _wake(self, o: _Origin) -> None:
         while o.waiters:
             w = o.waiters.popleft()
+            self._queued_at.pop(w, None)  # it queues again (keeping its place) or connects itself
             if not w.done():
                 w.set_result(None)  # a slot is free: the waiter opens its own connection (or queues again)
                 return
@@ -715,6 +731,7 @@ class H1Client(HttpClient):
             o.waiters.appendleft(w)
         else:
             o.waiters.append(w)
+        self._queued_at.setdefault(w, time.monotonic_ns())
         self.counts["connect_waits"] += 1
         if _queued(o):
             self._grow(o, deadline)
@@ -851,6 +868,10 @@ class H1Client(HttpClient):
         out = dict(self.counts)
         out["open"] = sum(o.open for o in self._origins.values())
         out["idle"] = sum(len(o.idle) for o in self._origins.values())
+        for name, h in (("dial", self.dial_ns), ("queue_wait", self.queue_wait_ns)):
+            if h.count:
+                out[f"{name}_p99_us"] = round(h.percentile(99) / 1e3, 1)
+                out[f"{name}_max_us"] = round(h.percentile(100) / 1e3, 1)
         if self._ntls:  # native TLS: full and resumed handshakes (beholder_pool{pool="http"})
             t = self._ntls.stats
             out["tls_handshakes"] = t["handshakes"]

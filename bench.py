@@ -375,6 +375,16 @@ def _attr_keys(prefix: str, att: dict) -> dict:
     return out
 
 
+def _pool_keys(prefix: str, http: dict) -> dict:
+    """Where a cold sink pool's time went (sinks/h1.py): the slowest connect (+ TLS handshake),
+    and how long queued requests waited for a connection (p99 / max over the run; in steady state
+    nothing queues, so these describe the warm-up)."""
+    http = http or {}
+    return {f"{prefix}_dial_max_us": http.get("dial_max_us"),
+            f"{prefix}_queue_wait_p99_us": http.get("queue_wait_p99_us"),
+            f"{prefix}_queue_wait_max_us": http.get("queue_wait_max_us")}
+
+
 def _cg(prefix: str, d: dict) -> dict:
     return {f"{prefix}_nr_throttled": d.get("nr_throttled"), f"{prefix}_throttled_usec": d.get("throttled_usec")}
 
@@ -403,7 +413,8 @@ def io_extras(a) -> dict:
                 "tcp_e2e_errors": e2e.get("errors"), "tcp_e2e_nivcsw": e2e.get("nivcsw"),
                 **_cg("tcp_e2e", e2e.get("cgroup_steady") or {}),
                 **_attr_keys("tcp_e2e", e2e.get("attribution_steady")),
-                **_attr_keys("tcp_e2e_warmup", e2e.get("attribution_warmup"))})
+                **_attr_keys("tcp_e2e_warmup", e2e.get("attribution_warmup")),
+                **_pool_keys("tcp_e2e", e2e.get("http"))})
     tls = harness._tcp_e2e(a.io_events, http_servers=4, tls=True)
     hl = tls.get("handle_latency_us", {})
     out.update({"tls_e2e_events_per_sec": _r(tls.get("ingest_rate_eps"), 1),
@@ -417,7 +428,8 @@ def io_extras(a) -> dict:
                 "tls_e2e_errors": tls.get("errors"), "tls_e2e_nivcsw": tls.get("nivcsw"),
                 **_cg("tls_e2e", tls.get("cgroup_steady") or {}),
                 **_attr_keys("tls_e2e", tls.get("attribution_steady")),
-                **_attr_keys("tls_e2e_warmup", tls.get("attribution_warmup"))})
+                **_attr_keys("tls_e2e_warmup", tls.get("attribution_warmup")),
+                **_pool_keys("tls_e2e", tls.get("http"))})
     h = harness._http_tcp(Workload(n_media=10000, seed=a.seed), a.io_events, clients=("h1",))["h1"]
     hl = h["handle_latency_us"]
     out.update({"http_tcp_h1_events_per_sec": _r(h["ingest_rate_eps"], 1),
@@ -656,7 +668,9 @@ def main(argv=None) -> int:
                      "slowest 0.1% of deliveries blamed on the process (consumer / pg / http(s) / broker fake) "
                      "whose event-loop or GC stall covered most of their time, 'none' = no stall >= 1 ms "
                      "(bench/stallmon.py); rate_*_p99_queue = reader push -> handler start, "
-                     "rate_*_p99_handle = handler start -> ack; calib_ns = fixed-work C loop (ops.calib) "
+                     "rate_*_p99_handle = handler start -> ack; *_dial_max / *_queue_wait_* = the slowest sink "
+                     "connect (+TLS handshake) and the wait of requests queued for a connection (the warm-up); "
+                     "calib_ns = fixed-work C loop (ops.calib) "
                      "around the headline, value_calibrated = value * calib_ns / calib_ref_ns; "
                      "plumbing_* = BASELINE config 1 through `python -m beholder_amd run --source stdin`, "
                      "/metrics scraped before exit",

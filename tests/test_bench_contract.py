@@ -25,7 +25,8 @@ EXTRAS = {"all_procs_events_per_sec", "rate_10k_p50_ingest_latency_us", "rate_10
           "plumbing_rc", "plumbing_acked", "plumbing_sink_requests", "plumbing_has_progress_counter",
           "plumbing_has_trello_counter", "tcp_e2e_slow_blamed", "tls_e2e_slow_blamed",
           "tcp_e2e_warmup_slow_blamed", "tls_e2e_warmup_slow_blamed", "tcp_e2e_nr_throttled",
-          "tls_e2e_nr_throttled", "tcp_e2e_nivcsw", "soak_cpu_us_per_event"}
+          "tls_e2e_nr_throttled", "tcp_e2e_nivcsw", "soak_cpu_us_per_event", "tls_e2e_dial_max_us",
+          "tls_e2e_queue_wait_max_us", "headline_minflt", "thp"}
 SMALL = ["--steps", "2", "--warmup", "1", "--events-per-step", "4096", "--media", "500"]
 
 
