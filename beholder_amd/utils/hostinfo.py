@@ -159,3 +159,27 @@ def cgroup_cpu_stat() -> Dict[str, int]:
 
 def cgroup_delta(before: Mapping[str, int], after: Mapping[str, int]) -> Dict[str, int]:
     return {k: after[k] - before.get(k, 0) for k in after}
+
+
+def host_cpu_times() -> Optional[tuple]:
+    """(busy, total) jiffies of the whole host from /proc/stat's ``cpu`` line (all CPUs, all
+    tenants: /proc/stat is not namespaced), or None."""
+    try:
+        with open("/proc/stat") as f:
+            parts = f.readline().split()
+    except OSError:
+        return None
+    if not parts or parts[0] != "cpu":
+        return None
+    v = [int(x) for x in parts[1:]]
+    idle = v[3] + (v[4] if len(v) > 4 else 0)  # idle + iowait
+    total = sum(v[:8])  # user nice system idle iowait irq softirq steal (guest is inside user)
+    return total - idle, total
+
+
+def host_busy_pct(before: Optional[tuple], after: Optional[tuple]) -> Optional[float]:
+    """Share of the host's CPU time that was busy between two :func:`host_cpu_times` readings:
+    how loaded the machine was around a phase, whoever loaded it."""
+    if not before or not after or after[1] <= before[1]:
+        return None
+    return round(100.0 * (after[0] - before[0]) / (after[1] - before[1]), 1)

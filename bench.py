@@ -402,7 +402,10 @@ def io_extras(a) -> dict:
                 "plumbing_has_progress_counter": p["scrape_has_progress_counter"],
                 "plumbing_has_trello_counter": p["scrape_has_trello_counter"],
                 "plumbing_process_wall_s": _r(p["process_wall_s"])})
+    from beholder_amd.utils.hostinfo import host_busy_pct, host_cpu_times
+    h0 = host_cpu_times()
     e2e = harness._tcp_e2e(a.io_events)
+    h1 = host_cpu_times()
     hl = e2e.get("handle_latency_us", {})
     out.update({"tcp_e2e_events_per_sec": _r(e2e.get("ingest_rate_eps"), 1),
                 "tcp_e2e_cpu_us_per_event": _r(e2e.get("cpu_us_per_event")),
@@ -411,11 +414,14 @@ def io_extras(a) -> dict:
                 "tcp_e2e_warmup_p99_handle_latency_us": _r(e2e.get("warmup_handle_latency_us", {}).get("p99")),
                 "tcp_e2e_warmup_p999_handle_latency_us": _r(e2e.get("warmup_handle_latency_us", {}).get("p999")),
                 "tcp_e2e_errors": e2e.get("errors"), "tcp_e2e_nivcsw": e2e.get("nivcsw"),
+                "tcp_e2e_host_cpu_busy_pct": host_busy_pct(h0, h1),
                 **_cg("tcp_e2e", e2e.get("cgroup_steady") or {}),
                 **_attr_keys("tcp_e2e", e2e.get("attribution_steady")),
                 **_attr_keys("tcp_e2e_warmup", e2e.get("attribution_warmup")),
                 **_pool_keys("tcp_e2e", e2e.get("http"))})
+    h0 = host_cpu_times()
     tls = harness._tcp_e2e(a.io_events, http_servers=4, tls=True)
+    h1 = host_cpu_times()
     hl = tls.get("handle_latency_us", {})
     out.update({"tls_e2e_events_per_sec": _r(tls.get("ingest_rate_eps"), 1),
                 "tls_e2e_cpu_us_per_event": _r(tls.get("cpu_us_per_event")),
@@ -426,6 +432,7 @@ def io_extras(a) -> dict:
                 "tls_e2e_handshakes": (tls.get("http") or {}).get("tls_handshakes"),
                 "tls_e2e_resumed": (tls.get("http") or {}).get("tls_resumed"),
                 "tls_e2e_errors": tls.get("errors"), "tls_e2e_nivcsw": tls.get("nivcsw"),
+                "tls_e2e_host_cpu_busy_pct": host_busy_pct(h0, h1),
                 **_cg("tls_e2e", tls.get("cgroup_steady") or {}),
                 **_attr_keys("tls_e2e", tls.get("attribution_steady")),
                 **_attr_keys("tls_e2e_warmup", tls.get("attribution_warmup")),
@@ -462,7 +469,7 @@ def paced_extras(a) -> dict:
     HIP, so nothing but the consumer and its reader thread competes for this process."""
     from beholder_amd.bench import harness
     from beholder_amd.bench.generator import Workload
-    from beholder_amd.utils.hostinfo import cgroup_cpu_stat, cgroup_delta
+    from beholder_amd.utils.hostinfo import cgroup_cpu_stat, cgroup_delta, host_busy_pct, host_cpu_times
     w = Workload(n_media=10000, seed=a.seed)
     out = {}
     # unmeasured: 0.3 s at 10k/s through a fresh service first, so the paced configs do not also
@@ -470,6 +477,7 @@ def paced_extras(a) -> dict:
     # the exited all-process consumers' memory being reclaimed)
     asyncio.run(harness._run_inproc(w.events(3000), 10000, media=w.media))
     cg0 = cgroup_cpu_stat()
+    h0 = host_cpu_times()
     r = asyncio.run(harness._run_inproc(w.events(1000), 1000, media=w.media))  # config 2: 1 s at 1k/s
     out.update({"rate_1k_events_per_sec": _r(r["ingest_rate_eps"], 1), **_paced("rate_1k", r)})
     r = asyncio.run(harness._run_inproc(w.events(10000), 10000, media=w.media))  # config 3: 1 s at 10k/s
@@ -481,6 +489,7 @@ def paced_extras(a) -> dict:
                 "rate_100k_dropped": r["dropped"],
                 "rate_100k_offered_per_sec": _r(r["offered_rate_eps"], 1), **_paced("rate_100k", r)})
     out.update(_cg("paced", cgroup_delta(cg0, cgroup_cpu_stat())))
+    out["paced_host_cpu_busy_pct"] = host_busy_pct(h0, host_cpu_times())
     r = asyncio.run(harness._run_inproc(w.events(200_000), 0, policy="drop_newest", capacity_events=4096,
                                         media=w.media))
     out.update({"burst_offered": r["offered"], "burst_accepted": r["accepted"],
@@ -568,7 +577,7 @@ def main(argv=None) -> int:
     dev = _Device(dist.local_rank)
     extras: dict = {}
 
-    from beholder_amd.utils.hostinfo import cgroup_cpu_stat, cgroup_delta
+    from beholder_amd.utils.hostinfo import cgroup_cpu_stat, cgroup_delta, host_busy_pct, host_cpu_times
 
     # 1. phases that start child processes (before any HIP call in this process)
     if a.extras and dist.rank == 0:
@@ -588,10 +597,12 @@ def main(argv=None) -> int:
     # 3. the headline: one consumer per rank, K timed steps, between two calibration runs
     calib0 = calibrate()
     cg0 = cgroup_cpu_stat()
+    h0 = host_cpu_times()
     gc.collect()
     res = run_solo(a, dist, dev)
     dist.barrier()
     cg1 = cgroup_cpu_stat()
+    h1 = host_cpu_times()
     calib1 = calibrate()
     elapsed = dist.max(res["elapsed"])
     parts = dist.gather({k: res[k] for k in ("handle_hist", "ingest_hist", "http_calls", "errors", "abandoned",
@@ -619,6 +630,7 @@ def main(argv=None) -> int:
         cal.update({"calib_ref": CALIB_REF,
                     # what a box with the reference box's core speed (the C loop) would give
                     "value_calibrated": round(value * cal["calib_ns"] / ref, 1) if ref else None,
+                    "headline_host_cpu_busy_pct": host_busy_pct(h0, h1),
                     **_cg("headline", cgroup_delta(cg0, cg1))})
         out = {
             "metric": BASELINE_METRIC,

@@ -4,7 +4,8 @@ import json
 import sys
 
 KEYS = ["value", "cpu_us_per_event", "thp", "headline_minflt", "calib_ns", "calib_ns_before", "calib_ns_after", "value_calibrated",
-        "involuntary_ctx_switches", "headline_nr_throttled",
+        "involuntary_ctx_switches", "headline_nr_throttled", "headline_host_cpu_busy_pct", "paced_host_cpu_busy_pct",
+        "tcp_e2e_host_cpu_busy_pct", "tls_e2e_host_cpu_busy_pct",
         "rate_1k_p50_ingest_latency_us", "rate_1k_p99_ingest_latency_us", "rate_1k_p99_queue_latency_us",
         "rate_1k_p99_handle_latency_us", "rate_10k_p50_ingest_latency_us", "rate_10k_p99_ingest_latency_us",
         "rate_10k_p99_queue_latency_us", "rate_10k_p99_handle_latency_us", "rate_100k_p50_ingest_latency_us",
