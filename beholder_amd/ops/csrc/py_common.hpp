@@ -84,6 +84,9 @@ struct DeliveryObject {
 };
 extern PyTypeObject DeliveryType;
 
+// rmsg.ack() of a native Delivery, called directly (py_handlers.cpp). New reference or NULL.
+PyObject* delivery_ack_c(PyObject* d);
+
 // Creates a pending delivery; steals nothing (increfs content/settler).
 PyObject* delivery_new(PyObject* content, uint8_t topic, uint64_t tag, int64_t recv_ns,
                        SettlerObject* settler, bool redelivered);

@@ -314,7 +314,8 @@ bool catch_and_warn(HandlersObject* hs, PyObject* text) {
 
 PySendResult finish_ack(CallObject* c, PyObject** result) {
   c->done = 1;
-  PyObject* r = PyObject_CallMethodNoArgs(c->rmsg, s_ack);
+  PyObject* r = Py_TYPE(c->rmsg) == &DeliveryType ? delivery_ack_c(c->rmsg)  // rmsg.ack(), index.js:124,151,154
+                                                   : PyObject_CallMethodNoArgs(c->rmsg, s_ack);
   if (!r) return PYGEN_ERROR;
   *result = r;
   return PYGEN_RETURN;

@@ -490,6 +490,9 @@ PyGetSetDef delivery_getset[] = {
 
 PyTypeObject DeliveryType = {PyVarObject_HEAD_INIT(nullptr, 0)};
 
+// rmsg.ack() for a native Delivery without the method lookup (the compiled handlers' last step).
+PyObject* delivery_ack_c(PyObject* d) { return settle(reinterpret_cast<DeliveryObject*>(d), D_ACKED, "ack", false); }
+
 // ================================= Ingest ===================================
 namespace {
 
