@@ -73,3 +73,16 @@ def test_default_procs_without_torch():
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert int(r.stdout.strip()) >= 1
+
+
+def test_host_busy_share_and_cgroup_stat_readers():
+    from beholder_amd.utils import hostinfo as hi
+    assert hi.host_busy_pct((10, 100), (60, 200)) == 50.0
+    assert hi.host_busy_pct(None, (1, 2)) is None and hi.host_busy_pct((5, 10), (5, 10)) is None
+    t = hi.host_cpu_times()
+    assert t is None or (0 <= t[0] <= t[1])
+    st = hi.cgroup_cpu_stat()  # whatever this host exposes: known keys, integer values
+    assert set(st) <= {"nr_periods", "nr_throttled", "throttled_usec"}
+    assert all(isinstance(v, int) for v in st.values())
+    assert hi.cgroup_delta({"nr_throttled": 2}, {"nr_throttled": 5, "throttled_usec": 7}) == \
+        {"nr_throttled": 3, "throttled_usec": 7}
