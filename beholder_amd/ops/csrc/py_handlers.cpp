@@ -370,6 +370,20 @@ int pg_execute(CallObject* c, PyObject* store, PyObject* sql_name, PyObject* par
   return await_start(c, aw, out);
 }
 
+// A Media row (a NamedTuple: a tuple subclass without __dict__) whose fields are all atoms (str,
+// int, None: nothing the collector tracks) can never be part of a reference cycle, so it leaves
+// the collector's lists at birth. CPython does this lazily for exact tuples only, so a row type
+// is otherwise tracked for life: every fresh row from Postgres (one per event) and every row the
+// in-memory store replaces filled the young generation, and each full collection walked them.
+void untrack_row(PyObject* t) {
+  if (!PyObject_GC_IsTracked(t) || Py_TYPE(t)->tp_dictoffset != 0) return;
+  for (Py_ssize_t i = 0, n = PyTuple_GET_SIZE(t); i < n; ++i) {
+    PyObject* v = PyTuple_GET_ITEM(t, i);
+    if (PyObject_IS_GC(v) && PyObject_GC_IsTracked(v)) return;
+  }
+  PyObject_GC_UnTrack(t);
+}
+
 // (rows, tag) of the media SELECT -> Media (store/postgres.py get_by_id + row_to_media).
 // Takes and returns a reference; NULL = raised.
 PyObject* pg_media(CallObject* c, PyObject* res) {
@@ -399,6 +413,7 @@ PyObject* pg_media(CallObject* c, PyObject* res) {
     PyObject* args = PyTuple_Pack(1, r);
     m = args ? PyTuple_Type.tp_new(reinterpret_cast<PyTypeObject*>(hs->media_cls), args, nullptr) : nullptr;
     Py_XDECREF(args);
+    if (m) untrack_row(m);
   } else {
     m = PyObject_CallOneArg(hs->row_to_media, r);
   }
@@ -504,6 +519,7 @@ int update_inline(CallObject* c) {
   PyObject* nm = PyTuple_Type.tp_new(reinterpret_cast<PyTypeObject*>(hs->media_cls), args, nullptr);
   Py_DECREF(args);
   if (!nm) return -1;
+  untrack_row(nm);
   rc = PyDict_SetItem(rows, c->media_id, nm);
   Py_DECREF(nm);
   return rc < 0 ? -1 : 1;

@@ -374,3 +374,27 @@ def test_native_matches_python_over_postgres(concurrent):
     assert got == want
     assert stats["suspended"] > 0  # the native path really waited on the wire
     assert any(e and "MediaNotFound" in e for _, e in got["deliveries"])
+
+
+def test_rows_the_compiled_handlers_make_leave_the_collector():
+    """A Media row made by the compiled handlers (the in-memory store's replaced row) holds only
+    atoms, so it is untracked at birth: rows no longer fill the young generation (soak GC pauses)."""
+    import gc
+
+    from beholder_amd.handlers import native_handlers
+    from beholder_amd.ops import Delivery, Settler, dispatch_batch
+    from beholder_amd.bench.generator import Workload
+    from helpers import Rig
+    import array
+
+    w = Workload(n_media=50, seed=3, progress_fraction=0.0)
+    r = Rig(medias=w.media)
+    impl = native_handlers(r.h)
+    s = Settler()
+    ds = [Delivery(b, t, i, s) for i, (t, b) in enumerate(w.events(200))]
+    dispatch_batch(ds, 0, (None, impl.on_status, impl.on_progress), array.array("Q", [0, 0, 0]), None, None, None)
+    rows = list(r.store._rows.values())
+    changed = [m for m in rows if m not in w.media]
+    assert changed, "the status events replaced some rows"
+    assert not any(gc.is_tracked(m) for m in changed)
+    assert all(type(m).__name__ == "Media" for m in changed)
