@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import abc
 from typing import Iterable, NamedTuple, Optional
+from ..ops import native as _native
 
 
 class MediaNotFound(LookupError):
@@ -28,6 +29,12 @@ class MediaNotFound(LookupError):
 
 class StoreError(RuntimeError):
     pass
+
+
+# untrack_row(row) -> row: a row of atoms leaves the cyclic collector at once. NamedTuple rows are
+# otherwise tracked for life, and a store that replaces or reads many of them keeps the young
+# generation full of them (the compiled handlers do the same for the rows they make).
+untrack_row = _native.untrack_row
 
 
 class Media(NamedTuple):

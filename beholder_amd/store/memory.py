@@ -3,7 +3,7 @@ from __future__ import annotations
 
 from typing import Dict, Iterable, Optional
 
-from .base import Media, MediaNotFound, MediaStore
+from .base import Media, MediaNotFound, MediaStore, untrack_row
 
 
 class MemoryStore(MediaStore):
@@ -32,7 +32,7 @@ class MemoryStore(MediaStore):
         self.update_calls += 1
         m = self._rows.get(media_id)
         if m is not None:
-            self._rows[media_id] = m._replace(status=int(status))
+            self._rows[media_id] = untrack_row(m._replace(status=int(status)))
 
     def get_by_id_nowait(self, media_id: str) -> Media:
         self.get_calls += 1

@@ -15,7 +15,7 @@ from __future__ import annotations
 
 from typing import Iterable, Mapping, Optional
 
-from .base import Media, MediaNotFound, MediaStore
+from .base import untrack_row, Media, MediaNotFound, MediaStore
 from .pgwire import Pool
 from .schema import MediaSchema, pg_ph
 
@@ -25,9 +25,9 @@ def row_to_media(r) -> Media:
     int). The compiled handlers (ops/csrc/py_handlers.cpp) take the all-int, no-NULL case
     themselves."""
     if None not in r and type(r[2]) is type(r[4]) is type(r[5]) is type(r[7]) is type(r[9]) is int:
-        return Media._make(r)  # int columns arrived as int4/int8: no per-field conversion
-    return Media(*(("" if v is None else v) if i in (0, 1, 3, 6, 8) else (0 if v is None else int(v))
-                   for i, v in enumerate(r)))
+        return untrack_row(Media._make(r))  # int columns arrived as int4/int8: no per-field conversion
+    return untrack_row(Media(*(("" if v is None else v) if i in (0, 1, 3, 6, 8) else (0 if v is None else int(v))
+                               for i, v in enumerate(r))))
 
 
 class PostgresStore(MediaStore):
