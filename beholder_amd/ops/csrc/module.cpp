@@ -182,7 +182,19 @@ PyObject* mod_calib_mem(PyObject*, PyObject* args) {
   return Py_BuildValue("(LK)", (long long)(t1 - t0), (unsigned long long)idx);
 }
 
+// untrack_row(row) -> row (store/base.py): a NamedTuple row of atoms leaves the cyclic collector.
+PyObject* mod_untrack_row(PyObject*, PyObject* t) {
+  if (!PyTuple_Check(t)) {
+    PyErr_SetString(PyExc_TypeError, "untrack_row expects a tuple (a Media row)");
+    return nullptr;
+  }
+  untrack_atomic_row(t);
+  return Py_NewRef(t);
+}
+
 PyMethodDef module_methods[] = {
+    {"untrack_row", mod_untrack_row, METH_O,
+     "untrack_row(row) -> row: a tuple row holding only atoms leaves the cyclic collector"},
     {"calib_mem", mod_calib_mem, METH_VARARGS,
      "calib_mem(bytes, steps) -> (ns, checksum): fixed-work dependent random walk over `bytes`"},
     {"calib", mod_calib, METH_VARARGS, "calib(iters) -> (ns, checksum): fixed-work CPU calibration loop"},

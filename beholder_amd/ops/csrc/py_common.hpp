@@ -84,6 +84,9 @@ struct DeliveryObject {
 };
 extern PyTypeObject DeliveryType;
 
+// A tuple row holding only atoms leaves the cyclic collector (py_handlers.cpp).
+void untrack_atomic_row(PyObject* t);
+
 // rmsg.ack() of a native Delivery, called directly (py_handlers.cpp). New reference or NULL.
 PyObject* delivery_ack_c(PyObject* d);
 

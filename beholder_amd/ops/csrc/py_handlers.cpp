@@ -421,14 +421,11 @@ PyObject* pg_media(CallObject* c, PyObject* res) {
   return m;
 }
 
-PyObject* mod_untrack_row(PyObject*, PyObject* t) {
-  if (!PyTuple_Check(t)) {
-    PyErr_SetString(PyExc_TypeError, "untrack_row expects a tuple (a Media row)");
-    return nullptr;
-  }
-  untrack_row(t);
-  return Py_NewRef(t);
-}
+}  // namespace
+
+void untrack_atomic_row(PyObject* t) { untrack_row(t); }
+
+namespace {
 
 // media = await db.getByID(mediaId). The in-memory store's row read (store/memory.py
 // get_by_id_nowait) runs inline; other stores go through their nowait accessor or the coroutine.
@@ -1731,15 +1728,9 @@ PyMethodDef hs_methods[] = {
 
 PyObject* intern(const char* s) { return PyUnicode_InternFromString(s); }
 
-PyMethodDef row_functions[] = {
-    {"untrack_row", mod_untrack_row, METH_O,
-     "untrack_row(row) -> row: a tuple row holding only atoms leaves the cyclic collector"},
-    {nullptr, nullptr, 0, nullptr}};
-
 }  // namespace
 
 int init_handler_types(PyObject* m) {
-  if (PyModule_AddFunctions(m, row_functions) < 0) return -1;
   struct {
     PyObject** slot;
     const char* text;
