@@ -174,7 +174,8 @@ class _Conn(asyncio.Protocol):
 
 
 class _Origin:
-    __slots__ = ("scheme", "host", "port", "tls", "host_header", "auth", "idle", "open", "waiters", "connecting")
+    __slots__ = ("scheme", "host", "port", "tls", "host_header", "auth", "idle", "open", "waiters", "connecting",
+                 "queued_at")
 
     def __init__(self, scheme: str, host: str, port: int, host_header: str, auth: Optional[str]):
         self.scheme = scheme
@@ -187,6 +188,9 @@ class _Origin:
         self.open = 0
         self.connecting = 0  # connects (and TLS handshakes) in progress
         self.waiters: Deque[asyncio.Future] = collections.deque()
+        # monotonic ns at which each waiter queued (the queue-wait histogram); an entry leaves with
+        # its waiter, whichever path pops it from ``waiters``
+        self.queued_at: Dict[object, int] = {}
 
 
 def _sockaddr_host(sa) -> str:
@@ -206,7 +210,7 @@ def _queued(o: _Origin) -> bool:
     ``max_connecting``."""
     w = o.waiters
     while w and w[0].done():
-        w.popleft()
+        o.queued_at.pop(w.popleft(), None)
     return len(w) > o.connecting
 
 
@@ -279,7 +283,6 @@ class H1Client(HttpClient):
         # handshake), and each wait of a queued request until a connection was handed to it
         self.dial_ns = _native.Histogram()
         self.queue_wait_ns = _native.Histogram()
-        self._queued_at: Dict[object, int] = {}
 
     # -- pool ----------------------------------------------------------------
     def _origin(self, key: str) -> _Origin:
@@ -408,6 +411,7 @@ class H1Client(HttpClient):
         except BaseException as e:  # noqa: BLE001 - the first queued request gets the connect error
             while o.waiters:
                 w = o.waiters.popleft()
+                o.queued_at.pop(w, None)
                 if not w.done():
                     w.set_exception(e)
                     break
@@ -524,20 +528,20 @@ class H1Client(HttpClient):
             else:
                 o.waiters.append(w)
                 counts["connect_waits"] += 1
-            self._queued_at[w] = time.monotonic_ns()
+            o.queued_at[w] = time.monotonic_ns()
             if not fresh and _queued(o):
                 self._grow(o, deadline)
             th = loop.call_at(deadline, _expire, w)
             try:
                 c = await w
             except asyncio.CancelledError:
-                self._queued_at.pop(w, None)
+                o.queued_at.pop(w, None)
                 # a connection handed over just before the cancel must go back to the pool
                 if w.done() and not w.cancelled() and w.exception() is None and w.result() is not None:
                     self._release(w.result(), True)
                 raise
             except BaseException:  # its deadline, a failed background connect
-                self._queued_at.pop(w, None)
+                o.queued_at.pop(w, None)
                 raise
             finally:
                 th.cancel()
@@ -612,7 +616,7 @@ class H1Client(HttpClient):
         c.last_used = time.monotonic()
         while o.waiters:
             w = o.waiters.popleft()
-            t0 = self._queued_at.pop(w, None)
+            t0 = o.queued_at.pop(w, None)
             if not w.done():
                 if t0 is not None:
                     self.queue_wait_ns.record(time.monotonic_ns() - t0)
@@ -629,7 +633,7 @@ class H1Client(HttpClient):
     def _wake(self, o: _Origin) -> None:
         while o.waiters:
             w = o.waiters.popleft()
-            self._queued_at.pop(w, None)  # it queues again (keeping its place) or connects itself
+            o.queued_at.pop(w, None)  # it queues again (keeping its place) or connects itself
             if not w.done():
                 w.set_result(None)  # a slot is free: the waiter opens its own connection (or queues again)
                 return
@@ -731,7 +735,7 @@ class H1Client(HttpClient):
             o.waiters.appendleft(w)
         else:
             o.waiters.append(w)
-        self._queued_at.setdefault(w, time.monotonic_ns())
+        o.queued_at.setdefault(w, time.monotonic_ns())
         self.counts["connect_waits"] += 1
         if _queued(o):
             self._grow(o, deadline)
@@ -894,6 +898,7 @@ class H1Client(HttpClient):
         for o in self._origins.values():
             while o.idle:
                 self._drop(o.idle.pop())
+            o.queued_at.clear()
             while o.waiters:
                 w = o.waiters.popleft()
                 if not w.done():

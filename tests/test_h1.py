@@ -396,6 +396,38 @@ def test_max_per_host_bounds_connections():
     assert all(r.status == 200 for r in rs) and s.connections <= 3 and len(s.requests) == 40
 
 
+def test_queue_wait_timestamps_leave_with_their_waiters():
+    """Requests that time out in the connection queue keep no enqueue timestamp once their waiter
+    is dropped from the queue; the ones handed a connection are in the queue-wait histogram."""
+    async def go():
+        s = Scripted(lambda n, m, t, h: OK)
+        orig = s._serve
+
+        async def serve(r, w):
+            await asyncio.sleep(0.15)
+            await orig(r, w)
+        s._serve = serve
+        await s.start()
+        c = H1Client(timeout_s=5, max_per_host=1)
+        url = f"http://127.0.0.1:{s.port}/"
+        first = asyncio.ensure_future(c.request("GET", url + "0"))
+        await asyncio.sleep(0.02)
+        short = [asyncio.ensure_future(c.request("GET", url + str(i), timeout=0.05)) for i in range(1, 7)]
+        await asyncio.sleep(0.08)  # they have timed out, their waiters still queued
+        late = asyncio.ensure_future(c.request("GET", url + "late"))  # queues behind them: drops them
+        rs = await asyncio.gather(first, *short, late, return_exceptions=True)
+        o = next(iter(c._origins.values()))
+        left = (len(o.queued_at), len(o.waiters))
+        await c.close()
+        await s.stop()
+        return rs, left, c.queue_wait_ns.count
+    rs, (stamps, waiters), waited = run(go())
+    assert rs[0].status == 200 and rs[-1].status == 200
+    assert all(isinstance(r, HttpError) for r in rs[1:-1])
+    assert stamps == 0 and waiters == 0
+    assert waited >= 1  # the late request was handed the connection
+
+
 def test_connection_refused_and_bad_urls():
     async def go():
         c = H1Client(timeout_s=2)
