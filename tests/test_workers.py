@@ -107,7 +107,14 @@ def test_workers_merged_metrics_endpoint(tmp_path):
             bt.call(lambda b: [b.publish(PROGRESS, x) for x in bodies])
             while time.time() < deadline and bt.call(lambda b: b.stats(PROGRESS))["acked"] < 300:
                 time.sleep(0.1)
-            text = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
+            # a worker whose scrape times out on a loaded host is left out of that one merge (and
+            # reported by beholder_cluster_worker_up): scrape until both are in
+            while True:
+                text = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
+                m = parse_exposition(text)
+                if m.get('beholder_progress_updates_total{status="queued"}') == 300 or time.time() > deadline:
+                    break
+                time.sleep(0.2)
             health = None
             while health != 200 and time.time() < deadline:  # a loaded host can answer late once
                 try:
