@@ -500,7 +500,9 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
                 http = H1Client(timeout_s=30, max_connecting=max_connecting)
             svc = Service(Config.from_dict(cfgd), source=src, store=store, http=http, logger=Logger(stream=sink),
                           serve_metrics=False)
-            await svc.init()
+            t_init = time.perf_counter()
+            await svc.init()  # connects to the broker and PG; preconnect opens the sink connections
+            out["init_ms"] = round((time.perf_counter() - t_init) * 1e3, 2)
             mon = StallMonitor().start()
             src.settler.trace_slow(SLOW_TRACE_NS)
             cg0 = cgroup_cpu_stat()

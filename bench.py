@@ -41,6 +41,8 @@ region):
 * ``tcp_e2e_*`` / ``http_tcp_h1_*``: the production-shaped path, every dependency over TCP (an
   AMQP replay broker, a Postgres fake and HTTP fakes in their own processes).
 * ``tls_e2e_*``: the same with HTTPS sinks, as Trello and Telegram are in production.
+  ``tls_e2e_preconnect_*``: the same again with ``service.http.preconnect`` = 100 (sink
+  connections and their handshakes made in init, ``_init_ms``; the default is 0, on demand).
 
 Order of the phases: (1) everything that starts child processes (config 1's CLI process, the TCP
 fakes, the all-process consumers); (2) the paced configs 2-4, in process, before HIP is touched;
@@ -437,6 +439,16 @@ def io_extras(a) -> dict:
                 **_attr_keys("tls_e2e", tls.get("attribution_steady")),
                 **_attr_keys("tls_e2e_warmup", tls.get("attribution_warmup")),
                 **_pool_keys("tls_e2e", tls.get("http"))})
+    # the same with service.http.preconnect = prefetch: the first wave of TLS handshakes happens
+    # in init (`_init_ms`), not inside the first deliveries' handle latency
+    pre = harness._tcp_e2e(a.io_events, http_servers=4, tls=True, preconnect=100)
+    out.update({"tls_e2e_preconnect_events_per_sec": _r(pre.get("ingest_rate_eps"), 1),
+                "tls_e2e_preconnect_p999_handle_latency_us": _r(pre.get("handle_latency_us", {}).get("p999")),
+                "tls_e2e_preconnect_warmup_p999_handle_latency_us":
+                    _r(pre.get("warmup_handle_latency_us", {}).get("p999")),
+                "tls_e2e_preconnect_init_ms": pre.get("init_ms"), "tls_e2e_init_ms": tls.get("init_ms"),
+                "tls_e2e_preconnect_handshakes": (pre.get("http") or {}).get("tls_handshakes"),
+                "tls_e2e_preconnect_errors": pre.get("errors")})
     h = harness._http_tcp(Workload(n_media=10000, seed=a.seed), a.io_events, clients=("h1",))["h1"]
     hl = h["handle_latency_us"]
     out.update({"http_tcp_h1_events_per_sec": _r(h["ingest_rate_eps"], 1),

@@ -18,6 +18,8 @@ KEYS = ["value", "cpu_us_per_event", "thp", "headline_minflt", "calib_ns", "cali
         "tls_e2e_events_per_sec", "tls_e2e_p50_handle_latency_us", "tls_e2e_p999_handle_latency_us",
         "tls_e2e_warmup_p999_handle_latency_us", "tls_e2e_slow_blamed", "tls_e2e_slow_time_share",
         "tls_e2e_warmup_slow_blamed", "tls_e2e_warmup_slow_time_share", "tls_e2e_dial_max_us",
+        "tls_e2e_init_ms", "tls_e2e_preconnect_events_per_sec", "tls_e2e_preconnect_p999_handle_latency_us",
+        "tls_e2e_preconnect_warmup_p999_handle_latency_us", "tls_e2e_preconnect_init_ms",
         "tls_e2e_queue_wait_p99_us", "tls_e2e_queue_wait_max_us", "tls_e2e_consumer_loop_lag_max_us",
         "tls_e2e_fakes_loop_lag_max_us", "tls_e2e_nr_throttled", "tls_e2e_nivcsw",
         "plumbing_rc", "plumbing_acked", "plumbing_has_progress_counter", "plumbing_has_trello_counter",

@@ -26,7 +26,8 @@ EXTRAS = {"all_procs_events_per_sec", "rate_10k_p50_ingest_latency_us", "rate_10
           "plumbing_has_trello_counter", "tcp_e2e_slow_blamed", "tls_e2e_slow_blamed",
           "tcp_e2e_warmup_slow_blamed", "tls_e2e_warmup_slow_blamed", "tcp_e2e_nr_throttled",
           "tls_e2e_nr_throttled", "tcp_e2e_nivcsw", "soak_cpu_us_per_event", "tls_e2e_dial_max_us",
-          "tls_e2e_queue_wait_max_us", "headline_minflt", "thp"}
+          "tls_e2e_queue_wait_max_us", "headline_minflt", "thp", "tls_e2e_preconnect_warmup_p999_handle_latency_us",
+          "tls_e2e_preconnect_init_ms", "tls_e2e_init_ms"}
 SMALL = ["--steps", "2", "--warmup", "1", "--events-per-step", "4096", "--media", "500"]
 
 
@@ -53,7 +54,8 @@ def test_bench_single_rank_contract():
     assert out["value"] == pytest.approx(4096 * 2 / (out["ms_per_step"] * 2 / 1000), rel=0.01)
     assert out["all_procs_per_rank"] == 2 and out["all_procs_events_per_sec"] > 0
     assert out["rate_10k_acked"] == 10000 and out["soak_events"] == 20000 and out["tcp_e2e_errors"] == 0
-    assert out["tls_e2e_errors"] == 0
+    assert out["tls_e2e_errors"] == 0 and out["tls_e2e_preconnect_errors"] == 0
+    assert out["tls_e2e_preconnect_handshakes"] >= 1
     assert out["burst_accepted"] + out["burst_dropped"] == out["burst_offered"]
     # BASELINE configs 2 and 4 as specified: 1 s at 1k/s, 1 s paced at 100k/s into the 4096 ring
     assert out["rate_1k_acked"] == 1000
