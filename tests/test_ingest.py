@@ -250,6 +250,15 @@ def test_paced_write_rate_and_order():
         paced_write(1, b"ab", array("Q", [3]).tobytes(), 10.0)  # end beyond data
     with pytest.raises(ValueError):
         paced_write(1, b"ab", array("Q", [1]).tobytes(), 0.0)
+    with pytest.raises(ValueError):
+        paced_write(1, b"abc", array("Q", [2, 1]).tobytes(), 10.0)  # ends must not decrease
+    r, w = os.pipe()
+    os.close(r)  # the consumer went away: EPIPE, not a signal
+    try:
+        with pytest.raises(OSError):
+            paced_write(w, b"abcd", array("Q", [2, 4]).tobytes(), 1000.0)
+    finally:
+        os.close(w)
 
 
 def test_queue_latency_is_receive_to_start():
