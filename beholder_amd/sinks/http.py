@@ -229,7 +229,7 @@ class RecordingHttpClient(HttpClient):
 
     def __init__(self, keep: Optional[int] = None, delay_s: float = 0.0):
         self.calls: Deque[Tuple[str, str]] = collections.deque(maxlen=keep)
-        self.rules: List[Rule] = []
+        self._rules: Tuple[Rule, ...] = ()
         self._ok = HttpResponse(200, b"{}", None, "")
         self._rec = _native_ops.Recorder(self.calls, self._ok)
         self.delay_s = delay_s  # (sets native_record)
@@ -247,15 +247,25 @@ class RecordingHttpClient(HttpClient):
         """Expose the native core to the compiled handlers only while every answer is the plain
         ``200 {}`` with no delay, and no subclass overrides request() (jitter, counting)."""
         plain = type(self).request is RecordingHttpClient.request
-        self.native_record = self._rec if plain and not self._delay_s and not self.rules else None
+        self.native_record = self._rec if plain and not self._delay_s and not self._rules else None
 
     @property
     def count(self) -> int:
         return self._rec.count
 
+    @property
+    def rules(self) -> Tuple[Rule, ...]:
+        """The rules, read-only: change them with :meth:`add_rule` / :meth:`clear_rules`, which
+        keep ``native_record`` in step (a list mutated in place would leave it stale)."""
+        return self._rules
+
     def add_rule(self, method: str, url_prefix: str, fn) -> None:
-        self.rules.append((method.upper(), url_prefix, fn))
+        self._rules = self._rules + ((method.upper(), url_prefix, fn),)
         self._sync_fast_path()  # answers now depend on the rules: the Python path decides
+
+    def clear_rules(self) -> None:
+        self._rules = ()
+        self._sync_fast_path()
 
     def fail(self, method: str, url_prefix: str, status: Optional[int] = None, message: str = "ECONNREFUSED",
              body: bytes = b'"error"'):
@@ -274,9 +284,9 @@ class RecordingHttpClient(HttpClient):
             full = self._rec.record(m, with_query(url, params), None)
         if self.delay_s:
             await asyncio.sleep(self.delay_s)
-        if not self.rules:
+        if not self._rules:
             return HttpResponse(200, b"{}", None, full)
-        for rm, pref, fn in self.rules:
+        for rm, pref, fn in self._rules:
             if (rm == "*" or rm == m) and full.startswith(pref):
                 r = fn(m, full)
                 if isinstance(r, int):

@@ -73,7 +73,10 @@ def test_recording_client_fast_path_only_without_rules_delay_or_override():
     with pytest.raises(Exception):
         asyncio.run(go())  # the rule added above fails POSTs to https://api
     assert plain.count == 1 and plain.urls() == ["https://api/x?a=1"]
-
+    with pytest.raises(AttributeError):
+        plain.rules.append(("*", "", None))  # read-only: a stale native_record cannot happen
+    plain.clear_rules()
+    assert plain.rules == () and plain.native_record is not None
 
 
 def test_recording_client_fast_path_follows_a_later_delay():
