@@ -111,6 +111,7 @@ class _Producer(threading.Thread):
         self.ends = ends.tobytes()
         self.elapsed = 0.0
         self.writes = 0
+        self.t0_ns = 0  # paced: CLOCK_MONOTONIC time frame 0 was due (frame i: + i * 1e9 / rate)
 
     def run(self):
         try:
@@ -130,7 +131,8 @@ class _Producer(threading.Thread):
                 self.elapsed = time.perf_counter() - t0
             else:
                 from ..ops import paced_write
-                self.elapsed, self.writes = paced_write(self.wfd, self.data, self.ends, float(self.rate))
+                self.elapsed, self.writes, self.t0_ns = paced_write(self.wfd, self.data, self.ends,
+                                                                    float(self.rate))
         except OSError:
             pass
         finally:
@@ -201,6 +203,8 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
         # 2 ms threshold: an idle loop's timer wakes up to ~1 ms late by construction (epoll_wait
         # takes whole milliseconds and asyncio rounds the timeout up), which is not a stall
         mon = StallMonitor(threshold_us=2000).start()
+    if rate > 0:  # every delivery's (receive, start, ack) times, for the due -> ack latency below
+        src.settler.trace_slow(1, prod.offered + 16)
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
     rt0 = resource.getrusage(resource.RUSAGE_THREAD)
     t0 = time.perf_counter()
@@ -223,9 +227,11 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
         rss_probe.append(_rss_mb())  # after 1M events, before teardown
     if sink_delay_s:
         watcher.cancel()
+    due = _due_latencies(src.settler, prod, stats["source"]) if rate > 0 else {}
     await svc.close()
     s = stats["source"]
     return {
+        **due,
         "offered": prod.offered, "accepted": s["pushed"], "dropped": s["dropped_total"],
         "acked": s["acked"], "abandoned": s["abandoned"], "errors": sum(stats.get("handler_errors", {}).values()),
         "elapsed_s": elapsed, "producer_s": prod.elapsed,
@@ -251,6 +257,32 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
             "warmup_handle_latency_us": {k: v / 1e3 for k, v in cold.items() if k.startswith("p")}}
            if reset_latency_after else {}),
     }
+
+
+def _due_latencies(settler, prod: "_Producer", source_stats: dict) -> dict:
+    """For a paced run: each event's latency from its *due time* (when the producer was to write
+    it: ``t0 + i / rate``), not from when the reader thread received it. ``due_to_ack`` therefore
+    also holds the producer's own lateness, the pipe and the reader thread's wake-up, which the
+    receive -> ack histograms cannot see; ``due_to_recv`` is that part alone. Computed only when
+    every offered event was delivered and traced (no drops), so event i is the i-th started."""
+    recs, lost = settler.slow_deliveries()
+    if lost or source_stats.get("dropped_total") or len(recs) != prod.offered or not prod.t0_ns:
+        return {}
+    recs.sort(key=lambda r: r[1])  # dispatch order = arrival order = frame order
+    ns_per = 1e9 / prod.rate
+    to_ack = []
+    to_recv = []
+    for i, (recv, _start, settle) in enumerate(recs):
+        d = prod.t0_ns + int(i * ns_per)
+        to_ack.append(max(0, settle - d))
+        to_recv.append(max(0, recv - d))
+
+    def pct(xs):
+        xs.sort()
+        n = len(xs)
+        return {"p50": xs[n // 2] / 1e3, "p99": xs[min(n - 1, int(n * 0.99))] / 1e3,
+                "p999": xs[min(n - 1, int(n * 0.999))] / 1e3, "max": xs[-1] / 1e3}
+    return {"due_to_ack_us": pct(to_ack), "due_to_recv_us": pct(to_recv)}
 
 
 def run_config(name: str, *, duration_s: Optional[float] = None, events: Optional[int] = None,

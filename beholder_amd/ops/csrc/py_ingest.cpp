@@ -956,7 +956,7 @@ PyGetSetDef ingest_getset[] = {
 PyTypeObject IngestType = {PyVarObject_HEAD_INIT(nullptr, 0)};
 
 // ============================ paced producer ================================
-// paced_write(fd, data, ends, rate) -> (elapsed_s, writes)
+// paced_write(fd, data, ends, rate) -> (elapsed_s, writes, t0_ns)
 //
 // Writes the frames of `data` (frame i ends at byte ends[i], native-endian
 // u64 array) to `fd` at `rate` frames/s: frame i is written no earlier than
@@ -965,6 +965,8 @@ PyTypeObject IngestType = {PyVarObject_HEAD_INIT(nullptr, 0)};
 // 1 ns timer slack, so a bench producer neither competes with the consumer's
 // event loop for the GIL nor wakes late by the default 50 us slack
 // (BASELINE configs 2-4: 1k / 10k / 100k events/s). Used by bench/harness.py.
+// t0_ns (CLOCK_MONOTONIC, the clock of every Delivery timestamp) is when frame 0
+// was due, so the caller can measure each event from its due time to its ack.
 namespace {
 
 bool write_all(int fd, const uint8_t* p, size_t n) {
@@ -1041,12 +1043,13 @@ PyObject* mod_paced_write(PyObject*, PyObject* args) {
     errno = err;
     return PyErr_SetFromErrno(PyExc_OSError);
   }
-  return Py_BuildValue("(dK)", double(t1 - t0) / 1e9, (unsigned long long)writes);
+  return Py_BuildValue("(dKL)", double(t1 - t0) / 1e9, (unsigned long long)writes, (long long)t0);
 }
 
 PyMethodDef pace_methods[] = {
     {"paced_write", mod_paced_write, METH_VARARGS,
-     "paced_write(fd, data, ends_u64, rate) -> (elapsed_s, writes): GIL-free paced frame writer"},
+     "paced_write(fd, data, ends_u64, rate) -> (elapsed_s, writes, t0_ns): GIL-free paced frame writer; "
+     "frame i is due at t0_ns + i * 1e9 / rate"},
     {nullptr, nullptr, 0, nullptr}};
 
 }  // namespace

@@ -459,9 +459,16 @@ def io_extras(a) -> dict:
 
 def _paced(prefix: str, r: dict) -> dict:
     """Keys of one paced config: receive->ack p50/p99 and its two hops (reader push -> handler
-    start, handler start -> ack)."""
+    start, handler start -> ack), and the same from each event's due time (``due_to_ack``:
+    also the producer's lateness, the pipe and the reader thread's wake-up; ``due_to_recv``:
+    that part alone). The due-time keys are null when events were dropped."""
     il, ql, hl = r["ingest_latency_us"], r.get("queue_latency_us", {}), r["handle_latency_us"]
+    da, dr = r.get("due_to_ack_us") or {}, r.get("due_to_recv_us") or {}
     return {f"{prefix}_acked": r["acked"],
+            f"{prefix}_p50_due_to_ack_us": _r(da.get("p50")),
+            f"{prefix}_p99_due_to_ack_us": _r(da.get("p99")),
+            f"{prefix}_p999_due_to_ack_us": _r(da.get("p999")),
+            f"{prefix}_p99_due_to_recv_us": _r(dr.get("p99")),
             f"{prefix}_p50_ingest_latency_us": _r(il.get("p50")),
             f"{prefix}_p99_ingest_latency_us": _r(il.get("p99")),
             f"{prefix}_p999_ingest_latency_us": _r(il.get("p999")),

@@ -7,9 +7,9 @@ KEYS = ["value", "cpu_us_per_event", "thp", "headline_minflt", "calib_ns", "cali
         "involuntary_ctx_switches", "headline_nr_throttled", "headline_host_cpu_busy_pct", "paced_host_cpu_busy_pct",
         "tcp_e2e_host_cpu_busy_pct", "tls_e2e_host_cpu_busy_pct",
         "rate_1k_p50_ingest_latency_us", "rate_1k_p99_ingest_latency_us", "rate_1k_p99_queue_latency_us",
-        "rate_1k_p99_handle_latency_us", "rate_10k_p50_ingest_latency_us", "rate_10k_p99_ingest_latency_us",
-        "rate_10k_p99_queue_latency_us", "rate_10k_p99_handle_latency_us", "rate_100k_p50_ingest_latency_us",
-        "rate_100k_p99_ingest_latency_us", "rate_100k_p99_queue_latency_us", "rate_100k_dropped",
+        "rate_1k_p99_handle_latency_us", "rate_1k_p99_due_to_ack_us", "rate_1k_p99_due_to_recv_us", "rate_10k_p50_ingest_latency_us", "rate_10k_p99_ingest_latency_us",
+        "rate_10k_p99_queue_latency_us", "rate_10k_p99_handle_latency_us", "rate_10k_p99_due_to_ack_us", "rate_10k_p99_due_to_recv_us", "rate_100k_p50_ingest_latency_us",
+        "rate_100k_p99_ingest_latency_us", "rate_100k_p99_queue_latency_us", "rate_100k_p99_due_to_ack_us", "rate_100k_p99_due_to_recv_us", "rate_100k_dropped",
         "paced_nr_throttled",
         "tcp_e2e_events_per_sec", "tcp_e2e_p50_handle_latency_us", "tcp_e2e_p999_handle_latency_us",
         "tcp_e2e_warmup_p999_handle_latency_us", "tcp_e2e_slow_blamed", "tcp_e2e_slow_time_share",

@@ -27,7 +27,8 @@ EXTRAS = {"all_procs_events_per_sec", "rate_10k_p50_ingest_latency_us", "rate_10
           "tcp_e2e_warmup_slow_blamed", "tls_e2e_warmup_slow_blamed", "tcp_e2e_nr_throttled",
           "tls_e2e_nr_throttled", "tcp_e2e_nivcsw", "soak_cpu_us_per_event", "tls_e2e_dial_max_us",
           "tls_e2e_queue_wait_max_us", "headline_minflt", "thp", "tls_e2e_preconnect_warmup_p999_handle_latency_us",
-          "tls_e2e_preconnect_init_ms", "tls_e2e_init_ms"}
+          "tls_e2e_preconnect_init_ms", "tls_e2e_init_ms", "rate_1k_p99_due_to_ack_us",
+          "rate_10k_p99_due_to_ack_us", "rate_100k_p99_due_to_ack_us", "rate_10k_p99_due_to_recv_us"}
 SMALL = ["--steps", "2", "--warmup", "1", "--events-per-step", "4096", "--media", "500"]
 
 
@@ -59,6 +60,9 @@ def test_bench_single_rank_contract():
     assert out["burst_accepted"] + out["burst_dropped"] == out["burst_offered"]
     # BASELINE configs 2 and 4 as specified: 1 s at 1k/s, 1 s paced at 100k/s into the 4096 ring
     assert out["rate_1k_acked"] == 1000
+    # due -> ack holds receive -> ack (the event cannot be received before it is due... almost:
+    # the producer writes every frame already due in one write, so allow the pacing grain)
+    assert out["rate_10k_p99_due_to_ack_us"] + 200 >= out["rate_10k_p99_ingest_latency_us"]
     assert out["rate_100k_offered"] == 100_000
     assert out["rate_100k_accepted"] + out["rate_100k_dropped"] == out["rate_100k_offered"]
     assert out["rate_100k_acked"] == out["rate_100k_accepted"]

@@ -239,7 +239,10 @@ def test_paced_write_rate_and_order():
 
     t = threading.Thread(target=rd)
     t.start()
-    elapsed, writes = paced_write(w, b"".join(chunks), ends.tobytes(), 2000.0)  # 200 frames at 2k/s
+    from beholder_amd.ops import mono_ns
+    before = mono_ns()
+    elapsed, writes, t0 = paced_write(w, b"".join(chunks), ends.tobytes(), 2000.0)  # 200 frames at 2k/s
+    assert before <= t0 <= mono_ns()  # frame 0's due time, on the Delivery clock
     os.close(w)
     t.join()
     os.close(r)
