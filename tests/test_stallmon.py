@@ -45,3 +45,25 @@ def test_monitor_records_a_blocked_loop_as_a_stall_and_round_trips_its_report():
     rep = parse_stall_lines("noise\n" + mon.dump_line("pg") + "\nDONE queries=1\n")
     assert rep[0]["name"] == "pg" and [tuple(x) for x in rep[0]["stall_intervals"]] == \
         [tuple(x) for x in mon.loop_stalls + mon.gc_pauses]
+
+
+def test_due_latencies_from_the_producer_schedule():
+    """Paced runs measure each event from its due time (t0 + i / rate): event i is the i-th to
+    start, whatever order the trace holds; nothing is reported when events were dropped."""
+    from types import SimpleNamespace
+
+    from beholder_amd.bench.harness import _due_latencies
+
+    t0, rate = 1_000_000_000, 1000.0  # one event per ms
+    recs = [(t0 + i * 1_000_000 + 5_000, t0 + i * 1_000_000 + 7_000, t0 + i * 1_000_000 + 9_000 + i)
+            for i in range(100)]
+
+    class S:
+        def slow_deliveries(self):
+            return list(reversed(recs)), 0  # settle order need not be start order
+    prod = SimpleNamespace(offered=100, rate=rate, t0_ns=t0)
+    d = _due_latencies(S(), prod, {"dropped_total": 0})
+    assert d["due_to_recv_us"]["p50"] == 5.0 and d["due_to_recv_us"]["max"] == 5.0
+    assert d["due_to_ack_us"]["p50"] == (9_000 + 50) / 1e3 and d["due_to_ack_us"]["max"] == (9_000 + 99) / 1e3
+    assert _due_latencies(S(), prod, {"dropped_total": 3}) == {}
+    assert _due_latencies(S(), SimpleNamespace(offered=101, rate=rate, t0_ns=t0), {"dropped_total": 0}) == {}
