@@ -135,13 +135,19 @@ PyObject* settler_trace_slow(SettlerObject* self, PyObject* args) {
   long long thr;
   unsigned long long cap = 65536;
   if (!PyArg_ParseTuple(args, "L|K", &thr, &cap)) return nullptr;
+  if (cap > (1ULL << 28)) {  // 3 x 8 bytes each: at most 6 GiB, and cap * 3 cannot wrap
+    PyErr_SetString(PyExc_ValueError, "trace_slow: capacity must be <= 2**28");
+    return nullptr;
+  }
   auto* v = static_cast<std::vector<int64_t>*>(self->slow);
   if (!v) {
     v = new (std::nothrow) std::vector<int64_t>();
     if (!v) return PyErr_NoMemory();
     self->slow = v;
   }
-  v->clear();
+  self->slow_threshold_ns = 0;  // off while the buffer changes
+  if (thr <= 0) cap = 0;         // stop: give the buffer back
+  std::vector<int64_t>().swap(*v);
   try {
     v->reserve(size_t(cap) * 3);  // settle() appends without allocating (it must not throw)
   } catch (const std::exception&) {

@@ -275,3 +275,26 @@ def test_queue_latency_is_receive_to_start():
     assert s.handle_latency.percentile(50) < 4_000_000
     s.reset_latency()
     assert s.queue_latency.count == 0
+
+
+def test_settler_slow_trace_threshold_capacity_and_stop():
+    from beholder_amd.ops import Delivery, Settler, mono_ns
+    s = Settler()
+    s.trace_slow(1_000_000, 2)  # >= 1 ms from start to settle, room for two
+
+    def settle(start_ago_ns):
+        d = Delivery(b"x", 0, 1, s, mono_ns() - start_ago_ns - 10)
+        d.start()
+        if start_ago_ns:  # pretend the handler started earlier
+            time.sleep(start_ago_ns / 1e9)
+        d.ack()
+    settle(0)          # fast: not traced
+    for _ in range(3):
+        settle(2_000_000)  # slow: two fit, one is counted as dropped
+    recs, dropped = s.slow_deliveries()
+    assert len(recs) == 2 and dropped == 1
+    assert all(recv <= start <= settle_ and settle_ - start >= 1_000_000 for recv, start, settle_ in recs)
+    s.trace_slow(0)
+    assert s.slow_deliveries() == ([], 0)
+    with pytest.raises(ValueError):
+        s.trace_slow(1, 1 << 40)
