@@ -280,7 +280,7 @@ def test_queue_latency_is_receive_to_start():
 def test_settler_slow_trace_threshold_capacity_and_stop():
     from beholder_amd.ops import Delivery, Settler, mono_ns
     s = Settler()
-    s.trace_slow(1_000_000, 2)  # >= 1 ms from start to settle, room for two
+    s.trace_slow(50_000_000, 2)  # >= 50 ms from start to settle, room for two
 
     def settle(start_ago_ns):
         d = Delivery(b"x", 0, 1, s, mono_ns() - start_ago_ns - 10)
@@ -290,10 +290,10 @@ def test_settler_slow_trace_threshold_capacity_and_stop():
         d.ack()
     settle(0)          # fast: not traced
     for _ in range(3):
-        settle(2_000_000)  # slow: two fit, one is counted as dropped
+        settle(60_000_000)  # slow: two fit, one is counted as dropped
     recs, dropped = s.slow_deliveries()
     assert len(recs) == 2 and dropped == 1
-    assert all(recv <= start <= settle_ and settle_ - start >= 1_000_000 for recv, start, settle_ in recs)
+    assert all(recv <= start <= settle_ and settle_ - start >= 50_000_000 for recv, start, settle_ in recs)
     s.trace_slow(0)
     assert s.slow_deliveries() == ([], 0)
     with pytest.raises(ValueError):
