@@ -75,18 +75,35 @@ def test_aggregate_merge_rules():
     assert text.count("# TYPE beholder_trello_comments counter") == 1
 
 
-def _free_port() -> int:
+def _free_port(span: int = 1) -> int:
+    """A port P with P .. P+span-1 all free. The supervisor puts worker i on P+1+i, so the whole
+    span must be free; it is taken below the kernel's ephemeral range, where the outgoing
+    connections of tests running in parallel never land."""
+    import random
     import socket
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    rnd = random.Random(os.getpid() ^ time.monotonic_ns())
+    for _ in range(200):
+        base = rnd.randrange(20000, 32000 - span)
+        socks = []
+        try:
+            for k in range(span):
+                s = socket.socket()
+                socks.append(s)
+                s.bind(("127.0.0.1", base + k))
+            return base
+        except OSError:
+            continue
+        finally:
+            for s in socks:
+                s.close()
+    raise RuntimeError("no free port span")
 
 
 def test_workers_merged_metrics_endpoint(tmp_path):
     """One scrape target for N workers: the supervisor merges the workers' registries."""
     import urllib.error
     import urllib.request
-    port = _free_port()
+    port = _free_port(3)  # the merged endpoint and the two workers' own
     cfg = tmp_path / "events.yaml"
     cfg.write_text("keys: {trello: {key: k, token: t}}\ninstance: {flow_ids: {}}\n"
                    f"service: {{store: {{backend: memory}}, metrics: {{enabled: true, host: 127.0.0.1, "
