@@ -3,6 +3,8 @@
 # interleaved, current tree (A) against the tree with handshakes on the loop thread and no
 # continuation-first queueing (B: BEHOLDER_AB_HS_THREADS=0 BEHOLDER_AB_FRONT=0; max_connecting
 # stays 8). RUNS pairs; one JSON line per run under gpurun_out/$OUT/.
+# Historical: the BEHOLDER_AB_* switches were removed after this A/B (profiles/box_r4_native_budget/),
+# so arms B and C now run the same code as A.
 set -o pipefail
 out=gpurun_out/${OUT:-box_r4_native_budget}
 mkdir -p "$out"
