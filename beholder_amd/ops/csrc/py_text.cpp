@@ -351,11 +351,25 @@ bool quick_format_append(std::string& out, PyObject* const* args, Py_ssize_t nar
 // Appends one pino line for `args` to `out`. Returns false with a Python error set.
 bool append_line(std::string& out, long lvl, long long t, const char* prefix, Py_ssize_t plen, PyObject* extra,
                  PyObject* const* argv, Py_ssize_t nargs, bool drop_extra) {
-  out += "{\"level\":";
-  append_i64(out, lvl);
-  out += ",\"time\":";
-  append_i64(out, t);
-  out += ',';
+  // `{"level":L,"time":T,` is the same for every line of one level within one millisecond
+  // (~1,800 lines at the headline rate): format it once per (level, ms) and copy it
+  struct Head {
+    long lvl = -1;
+    long long t = -1;
+    std::string s;
+  };
+  static thread_local Head head;
+  if (head.lvl != lvl || head.t != t) {
+    head.s.assign("{\"level\":");
+    append_i64(head.s, lvl);
+    head.s += ",\"time\":";
+    append_i64(head.s, t);
+    head.s += ',';
+    head.lvl = lvl;
+    head.t = t;
+  }
+  out.reserve(out.size() + head.s.size() + size_t(plen) + 160);
+  out.append(head.s);
   out.append(prefix, size_t(plen));
   if (extra && extra != Py_None) {
     Py_ssize_t el;
