@@ -304,8 +304,10 @@ bool quick_format_append(std::string& out, PyObject* const* args, Py_ssize_t nar
   }
   size_t last = 0;
   for (Py_ssize_t i = 0; i + 1 < flen;) {
-    if (fs[i] != '%') {
-      ++i;
+    if (fs[i] != '%') {  // jump to the next '%' (most messages have none)
+      const void* p = memchr(fs + i, '%', size_t(flen - i));
+      if (!p) break;
+      i = static_cast<const char*>(p) - fs;
       continue;
     }
     char c = fs[i + 1];
