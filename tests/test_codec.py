@@ -241,3 +241,28 @@ def test_handlers_decode_with_the_configured_dialect():
     assert r.h.decode_status.__self__.dialect == "protobufjs"
     r2 = helpers.Rig(config=helpers.cfg({"service": {"proto": {"dialect": "upb"}}}))
     assert r2.h.decode_status.__self__.dialect == "upb"
+
+
+def test_decoded_messages_release_their_type_and_fields():
+    """Decoded messages are made without CPython's per-object struct-sequence size lookups
+    (py_codec.cpp new_result / result_dealloc): every one still holds and releases one
+    reference to its type and its fields, and behaves as the struct sequence it is."""
+    import gc
+    import sys
+    for dialect in ("upb", "protobufjs"):
+        c = codec_for(PROGRESS, dialect)
+        body = proto.encode(PROGRESS, {"mediaId": "m-1", "status": 2, "progress": 7, "host": "worker-1"})
+        tp = type(c.decode(body))
+        r0 = sys.getrefcount(tp)
+        ms = [c.decode(body) for _ in range(500)]
+        assert sys.getrefcount(tp) == r0 + 500
+        host = ms[0].host
+        hr = sys.getrefcount(host)
+        del ms
+        assert sys.getrefcount(tp) == r0
+        assert sys.getrefcount(host) == hr - 1  # the last message holding it is gone
+        m = c.decode(body)
+        assert not gc.is_tracked(m)  # as PyStructSequence_New leaves it (atoms only)
+        assert m == ("m-1", 2, 7, "worker-1") and tuple(m) == ("m-1", 2, 7, "worker-1") and len(m) == 4
+        assert (m.mediaId, m[1], m.progress, m[-1]) == ("m-1", 2, 7, "worker-1")
+        assert repr(m) == "api.TelemetryProgress(mediaId='m-1', status=2, progress=7, host='worker-1')"
