@@ -398,3 +398,47 @@ def test_rows_the_compiled_handlers_make_leave_the_collector():
     assert changed, "the status events replaced some rows"
     assert not any(gc.is_tracked(m) for m in changed)
     assert all(type(m).__name__ == "Media" for m in changed)
+
+
+def test_client_attribute_changes_are_seen_by_the_next_request():
+    """The compiled handlers remember the Trello client's and the HTTP client's attributes until
+    the instance dict changes (its version tag): a key, a rate limiter or a recorder switched off
+    between two events takes effect on the very next request."""
+    r = Rig(medias=[helpers.trello_media("m1")])
+    nh = native_handlers(r.h)
+
+    def progress():
+        d = r.delivery(2, progress_msg("m1", "QUEUED", 5))
+        asyncio.run(_drive(nh.on_progress(d)))
+        assert d.acked
+        return r.http.urls()[-1]
+
+    first = progress()
+    assert "key=" in first and r.http.native_record is not None
+    r.h.trello.key = "rotated-key"
+    assert "key=rotated-key" in progress()
+    calls = []
+    orig = r.h.trello.make_request
+
+    async def counting(*a, **kw):
+        calls.append(a)
+        return await orig(*a, **kw)
+    r.h.trello.limiter = object()  # a rate limit: the client's own make_request from now on
+    r.h.trello.make_request = counting
+    try:
+        progress()
+    except Exception:  # noqa: BLE001 - the dummy limiter is not a real one; only the route matters
+        pass
+    assert calls
+    r.h.trello.limiter = None
+    del r.h.trello.make_request
+    n = len(calls)
+    progress()
+    assert len(calls) == n  # back on the native path
+    r.http.delay_s = 0.001  # the recorder's fast path off: the Python request coroutine
+    assert r.http.native_record is None
+    assert "key=rotated-key" in progress()
+
+
+async def _drive(aw):
+    return await aw
