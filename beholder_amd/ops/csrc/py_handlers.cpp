@@ -596,8 +596,10 @@ PyObject* http_request(CallObject* c, PyObject* http, PyObject* method, PyObject
     cur = hs->http_view.v[HD_CALL];
   }
   if (rec && is_recorder(rec)) {  // the in-process stub (sinks/http.py RecordingHttpClient)
-    PyObject* m = method;
-    return recorder_request(rec, m, url, params ? params : Py_None);
+    Py_INCREF(rec);  // borrowed from the client's dict; held while it records
+    PyObject* r = recorder_request(rec, method, url, params ? params : Py_None);
+    Py_DECREF(rec);
+    return r;
   }
   if (cur && cur == hs->h1_fast_fn) {
     PyObject* call = h1_call_new(http, method, url, params ? params : Py_None, timeout, front);
@@ -669,8 +671,8 @@ int trello_request(CallObject* c, PyObject* method, PyObject* method_upper, PyOb
   PyObject** dp = fast ? _PyObject_GetDictPtr(trello) : nullptr;
   PyObject* td = dp && *dp && PyDict_CheckExact(*dp) ? *dp : nullptr;
   PyObject* const* tv = nullptr;  // the client's attributes, by TD_* (borrowed, NULL = absent)
+  PyObject* const names[TD_N] = {s_limiter, s_retry, s_key, s_token, s_base_url, s_http, s_timeout, s_strict, s_stats};
   if (td) {
-    PyObject* const names[TD_N] = {s_limiter, s_retry, s_key, s_token, s_base_url, s_http, s_timeout, s_strict, s_stats};
     if (!hs->trello_view.load(td, names)) return -1;
     tv = hs->trello_view.v;
     // a rate limit or 429 retries (sinks/ratelimit.py): the client's own make_request
@@ -705,6 +707,12 @@ int trello_request(CallObject* c, PyObject* method, PyObject* method_upper, PyOb
     Py_DECREF(query);
     if (!aw) return -1;
     return await_start(c, aw, out);
+  }
+  // the allocations above may have run a collection, and a finalizer Python code: look again
+  // (free while the client's dict is unchanged)
+  if (!hs->trello_view.load(td, names)) {
+    Py_DECREF(query);
+    return -1;
   }
   PyObject* base = tv[TD_BASE];
   PyObject* http = base ? tv[TD_HTTP] : nullptr;
