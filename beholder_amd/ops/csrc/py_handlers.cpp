@@ -104,34 +104,6 @@ struct Templates {
   std::vector<std::string> t[T_N];
 };
 
-// N keys looked up in one dict, remembered until the dict changes. CPython 3.10 gives every dict a
-// version tag (PEP 509) that changes on any mutation and is unique across dicts, so an unchanged
-// (dict, tag) pair means the borrowed values are the dict's current ones. Zeroed memory is the
-// empty state (the owner is allocated by tp_alloc).
-template <int N>
-struct DictView {
-  PyObject* dict;
-  uint64_t tag;
-  PyObject* v[N];  // borrowed; NULL = key absent
-
-  // false with a Python error set
-  bool load(PyObject* d, PyObject* const* keys) {
-    const uint64_t t = reinterpret_cast<PyDictObject*>(d)->ma_version_tag;
-    if (d == dict && t == tag) return true;
-    dict = nullptr;
-    for (int i = 0; i < N; ++i) {
-      v[i] = PyDict_GetItemWithError(d, keys[i]);
-      if (!v[i] && PyErr_Occurred()) return false;
-    }
-    dict = d;
-    tag = t;
-    return true;
-  }
-};
-
-enum { TD_LIMITER, TD_RETRY, TD_KEY, TD_TOKEN, TD_BASE, TD_HTTP, TD_TIMEOUT, TD_STRICT, TD_STATS, TD_N };
-enum { HD_RECORD, HD_CALL, HD_N };
-
 struct HandlersObject {
   PyObject_HEAD PyObject* h;  // the TelemetryHandlers
   PyObject* hdict;            // h.__dict__ (store / sinks are read per call: swappable)
@@ -172,8 +144,6 @@ struct HandlersObject {
   uint64_t suspended;
   uint8_t no_trello;
   uint8_t native_log;
-  DictView<TD_N> trello_view;  // the stock TrelloClient's instance dict (trello_request)
-  DictView<HD_N> http_view;    // the last sink HTTP client's instance dict (http_request)
 };
 
 // out += template `t` with its holes filled by String(vals[i]) (as the reference's template literals)
@@ -587,24 +557,21 @@ PyObject* http_request(CallObject* c, PyObject* http, PyObject* method, PyObject
   const bool front = c->nreq > 0;
   count_request(c);
   PyObject** dp = _PyObject_GetDictPtr(http);
-  PyObject* rec = nullptr;
-  PyObject* cur = nullptr;
-  if (dp && *dp && PyDict_CheckExact(*dp)) {
-    PyObject* const names[HD_N] = {s_native_record, s_native_call};
-    if (!hs->http_view.load(*dp, names)) return nullptr;
-    rec = hs->http_view.v[HD_RECORD];
-    cur = hs->http_view.v[HD_CALL];
-  }
+  PyObject* rec = dp && *dp ? PyDict_GetItemWithError(*dp, s_native_record) : nullptr;
   if (rec && is_recorder(rec)) {  // the in-process stub (sinks/http.py RecordingHttpClient)
     Py_INCREF(rec);  // borrowed from the client's dict; held while it records
     PyObject* r = recorder_request(rec, method, url, params ? params : Py_None);
     Py_DECREF(rec);
     return r;
   }
+  if (PyErr_Occurred()) return nullptr;
+  PyObject* cur = dp && *dp ? PyDict_GetItemWithError(*dp, s_native_call) : nullptr;
   if (cur && cur == hs->h1_fast_fn) {
     PyObject* call = h1_call_new(http, method, url, params ? params : Py_None, timeout, front);
     if (call != Py_None) return call;  // an H1Call, or NULL with an exception
     Py_DECREF(call);  // not a stock H1Client
+  } else if (PyErr_Occurred()) {
+    return nullptr;
   }
   if (params) {
     PyObject* args[5] = {http, method, url, params, timeout};
@@ -669,22 +636,18 @@ int trello_request(CallObject* c, PyObject* method, PyObject* method_upper, PyOb
   if (!trello) return -1;
   bool fast = reinterpret_cast<PyObject*>(Py_TYPE(trello)) == hs->trello_cls;
   PyObject** dp = fast ? _PyObject_GetDictPtr(trello) : nullptr;
-  PyObject* td = dp && *dp && PyDict_CheckExact(*dp) ? *dp : nullptr;
-  PyObject* const* tv = nullptr;  // the client's attributes, by TD_* (borrowed, NULL = absent)
-  PyObject* const names[TD_N] = {s_limiter, s_retry, s_key, s_token, s_base_url, s_http, s_timeout, s_strict, s_stats};
-  if (td) {
-    if (!hs->trello_view.load(td, names)) return -1;
-    tv = hs->trello_view.v;
-    // a rate limit or 429 retries (sinks/ratelimit.py): the client's own make_request
-    PyObject* lim = tv[TD_LIMITER];
-    PyObject* rty = tv[TD_RETRY];
+  PyObject* td = dp ? *dp : nullptr;
+  if (td) {  // a rate limit or 429 retries (sinks/ratelimit.py): the client's own make_request
+    PyObject* lim = PyDict_GetItemWithError(td, s_limiter);
+    PyObject* rty = !PyErr_Occurred() ? PyDict_GetItemWithError(td, s_retry) : nullptr;
+    if (PyErr_Occurred()) return -1;
     if ((lim && lim != Py_None) || (rty && rty != Py_None)) td = nullptr;
   }
   PyObject* query = PyDict_New();
   if (!query) return -1;
   if (td) {  // {"key": self.key, "token": self.token, **options}
-    PyObject* key = tv[TD_KEY];
-    PyObject* token = key ? tv[TD_TOKEN] : nullptr;
+    PyObject* key = PyDict_GetItemWithError(td, s_key);
+    PyObject* token = key ? PyDict_GetItemWithError(td, s_token) : nullptr;
     if (!token || PyDict_SetItem(query, hs->x[X_Q_KEY], key) < 0 || PyDict_SetItem(query, hs->x[X_Q_TOKEN], token) < 0) {
       Py_DECREF(query);
       if (PyErr_Occurred()) return -1;
@@ -708,17 +671,11 @@ int trello_request(CallObject* c, PyObject* method, PyObject* method_upper, PyOb
     if (!aw) return -1;
     return await_start(c, aw, out);
   }
-  // the allocations above may have run a collection, and a finalizer Python code: look again
-  // (free while the client's dict is unchanged)
-  if (!hs->trello_view.load(td, names)) {
-    Py_DECREF(query);
-    return -1;
-  }
-  PyObject* base = tv[TD_BASE];
-  PyObject* http = base ? tv[TD_HTTP] : nullptr;
-  PyObject* timeout = http ? tv[TD_TIMEOUT] : nullptr;
-  PyObject* strict = timeout ? tv[TD_STRICT] : nullptr;
-  PyObject* stats = strict ? tv[TD_STATS] : nullptr;
+  PyObject* base = PyDict_GetItemWithError(td, s_base_url);
+  PyObject* http = base ? PyDict_GetItemWithError(td, s_http) : nullptr;
+  PyObject* timeout = http ? PyDict_GetItemWithError(td, s_timeout) : nullptr;
+  PyObject* strict = timeout ? PyDict_GetItemWithError(td, s_strict) : nullptr;
+  PyObject* stats = strict ? PyDict_GetItemWithError(td, s_stats) : nullptr;
   if (!stats) {
     Py_DECREF(query);
     if (!PyErr_Occurred()) PyErr_SetString(PyExc_AttributeError, "TrelloClient attributes missing");
