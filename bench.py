@@ -31,6 +31,8 @@ region):
 * ``rate_1k_*``: BASELINE config 2, 1k events/s paced for 1 s: sustained ingest, p50/p99
   receive→ack latency.
 * ``rate_10k_*``: BASELINE config 3, 10k events/s paced for 1 s: p50/p99 receive→ack latency.
+  Every paced config also reports ``_due_to_ack`` (from the time the producer was to write the
+  event: its lateness, the pipe and the reader thread's wake-up included) and ``_due_to_recv``.
 * ``rate_100k_*``: BASELINE config 4, 100k events/s paced for 1 s into a 4096-event ring with
   ``drop_newest``: offered / accepted / dropped (``offered == accepted + dropped``), p99 latency.
 * ``burst_*``: 200k events written unpaced (pipe speed) into the same ring: drop accounting
