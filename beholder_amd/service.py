@@ -398,6 +398,10 @@ class Service:
         reg.register(NativeHistogramView("beholder_ingest_latency_seconds",
                                          "Receive to ack latency (includes queueing)",
                                          lambda: settler().ingest_latency if settler() is not None else None))
+        reg.register(NativeHistogramView("beholder_queue_latency_seconds",
+                                         "Receive to handler start: time a delivery waited for the consumer "
+                                         "(backlog, prefetch window, event-loop wake-up)",
+                                         lambda: settler().queue_latency if settler() is not None else None))
 
     # ------------------------------------------------------------------ run ---
     def healthy(self) -> bool:

@@ -50,6 +50,7 @@ def test_memory_broker_end_to_end_and_metrics():
     assert m['beholder_deliveries{state="acked"}'] == 3
     assert "# TYPE beholder_handle_latency_seconds histogram" in text
     assert m['beholder_handle_latency_seconds_bucket{le="+Inf"}'] == 3
+    assert m['beholder_queue_latency_seconds_count'] == 3  # receive -> handler start, per delivery
     # the init log line (index.js:157)
     assert "initialized" in [r["msg"] for r in svc.log.stream.records()]
 
