@@ -44,7 +44,7 @@ from .sinks import AiohttpClient, EmbyClient, H1Client, HttpClient, SinkObserver
 from .sinks.ratelimit import from_config as sink_policy
 from .store import MediaStore, open_store
 from .transport.base import Source
-from .ops import Driver, Window, dispatch_batch
+from .ops import Driver, Histogram, Window, dispatch_batch
 from .utils.fdtable import reserve_fd_table
 from .utils.log import Logger
 from .utils.tracing import extract as extract_trace_context, tracer_from_config
@@ -97,6 +97,21 @@ def make_http_client(http_cfg) -> HttpClient:
                     max_connecting=int(http_cfg.get("max_connecting", 8)))
 
 
+def _gc_pause_recorder(hist):
+    """A ``gc.callbacks`` entry recording each collection's duration (ns) into ``hist``. It holds
+    only the histogram, so a service that is never closed does not stay alive through it."""
+    t0 = [0]
+    mono = time.monotonic_ns
+
+    def cb(phase, _info):
+        if phase == "start":
+            t0[0] = mono()
+        elif t0[0]:
+            hist.record(mono() - t0[0])
+            t0[0] = 0
+    return cb
+
+
 class Service:
     """The beholder service. Inject ``source``/``store``/``http`` for tests and benches."""
 
@@ -136,6 +151,11 @@ class Service:
         self.received = array.array("Q", [0] * len(T.TOPIC_NAMES_BY_ID))
         self.source_error: Optional[str] = None
         self._preconnecting: set = set()  # preconnect tasks still running after startup
+        # event-loop lag (how late the 100 ms log flusher wakes) and GC pauses, in ns: the two
+        # process-side causes of a slow delivery (bench/stallmon.py attributes them in the bench)
+        self.loop_lag = Histogram()
+        self.gc_pause = Histogram()
+        self._gc_cb = None
 
     # ------------------------------------------------------------ properties --
     @property
@@ -243,6 +263,8 @@ class Service:
             # move them out of the collected generations so young-gen passes stay cheap.
             gc.collect()
             gc.freeze()
+        self._gc_cb = _gc_pause_recorder(self.gc_pause)
+        gc.callbacks.append(self._gc_cb)
         self.log.info("initialized")
         # the unpinned parts (triton-core's queue layout and media table are not vendored), stated
         # once so a mismatch with the real deployment is visible in the log
@@ -398,6 +420,11 @@ class Service:
         reg.register(NativeHistogramView("beholder_ingest_latency_seconds",
                                          "Receive to ack latency (includes queueing)",
                                          lambda: settler().ingest_latency if settler() is not None else None))
+        reg.register(NativeHistogramView("beholder_event_loop_lag_seconds",
+                                         "How late the event loop ran a 100 ms timer (a long callback, "
+                                         "a GC pause, the process descheduled)", lambda: self.loop_lag))
+        reg.register(NativeHistogramView("beholder_gc_pause_seconds",
+                                         "Cyclic garbage collector pauses", lambda: self.gc_pause))
         reg.register(NativeHistogramView("beholder_queue_latency_seconds",
                                          "Receive to handler start: time a delivery waited for the consumer "
                                          "(backlog, prefetch window, event-loop wake-up)",
@@ -499,10 +526,18 @@ class Service:
             i = j + 1
 
     async def _flush_logs_periodically(self, every_s: float = 0.1) -> None:
-        """Lines logged outside the batch loop (reconnects, idle periods) reach the stream within 100 ms."""
+        """Lines logged outside the batch loop (reconnects, idle periods) reach the stream within
+        100 ms. How late each of these wake-ups comes is the event loop's lag
+        (``beholder_event_loop_lag_seconds``): no extra timer for it."""
+        mono = time.monotonic_ns
+        period_ns = int(every_s * 1e9)
+        lag = self.loop_lag
         try:
             while True:
+                due = mono() + period_ns
                 await asyncio.sleep(every_s)
+                late = mono() - due
+                lag.record(late if late > 0 else 0)
                 self.log.flush()
                 if self.tracer is not None:
                     self.tracer.flush()
@@ -647,6 +682,12 @@ class Service:
 
     async def close(self) -> None:
         """Release transport, store, HTTP client and the metrics server."""
+        if self._gc_cb is not None:
+            try:
+                gc.callbacks.remove(self._gc_cb)
+            except ValueError:
+                pass
+            self._gc_cb = None
         for t in self._preconnecting:
             t.cancel()
         if self._preconnecting:

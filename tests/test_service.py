@@ -51,6 +51,8 @@ def test_memory_broker_end_to_end_and_metrics():
     assert "# TYPE beholder_handle_latency_seconds histogram" in text
     assert m['beholder_handle_latency_seconds_bucket{le="+Inf"}'] == 3
     assert m['beholder_queue_latency_seconds_count'] == 3  # receive -> handler start, per delivery
+    assert "# TYPE beholder_event_loop_lag_seconds histogram" in text
+    assert "# TYPE beholder_gc_pause_seconds histogram" in text
     # the init log line (index.js:157)
     assert "initialized" in [r["msg"] for r in svc.log.stream.records()]
 
@@ -337,3 +339,28 @@ def test_on_status_error_policy_applies_to_status_only(policy):
     st, pr = _FakeDelivery(T.STATUS_ID), _FakeDelivery(T.PROGRESS_ID)
     run(go())
     assert st.nacks == [policy == "nack_requeue"] and pr.nacks == [] and not pr.settled
+
+
+def test_loop_lag_and_gc_pause_histograms():
+    """The 100 ms log flusher's lateness is the loop lag; gc.callbacks time every collection; a
+    closed service leaves no callback behind."""
+    import gc
+    import time as _time
+
+    async def go():
+        b = MemoryBroker()
+        svc = make_service(b.consumer(prefetch=100))
+        await svc.init()
+        n_cb = len(gc.callbacks)
+        task = asyncio.ensure_future(svc._flush_logs_periodically(0.01))
+        await asyncio.sleep(0.03)
+        _time.sleep(0.05)  # block the loop: the next wake-up is >= 40 ms late
+        await asyncio.sleep(0.03)
+        task.cancel()
+        gc.collect()
+        await svc.close()
+        return svc, n_cb, len(gc.callbacks)
+    svc, n_cb, after = asyncio.run(go())
+    assert svc.loop_lag.count >= 3 and svc.loop_lag.max >= 30_000_000
+    assert svc.gc_pause.count >= 1
+    assert after == n_cb - 1
