@@ -68,6 +68,7 @@ import contextlib
 import ctypes
 import gc
 import json
+import math
 import multiprocessing as mp
 import os
 import resource
@@ -587,6 +588,18 @@ def calibrate() -> dict:
             "calib_py_ns": min(_calib_py_once() for _ in range(CALIB_REPS))}
 
 
+def _finite(x):
+    """The line must be strict JSON for the driver: a NaN or infinity anywhere (an extra key
+    computed from an empty phase) becomes null instead of an unparseable token."""
+    if isinstance(x, float):
+        return x if math.isfinite(x) else None
+    if isinstance(x, dict):
+        return {k: _finite(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_finite(v) for v in x]
+    return x
+
+
 def main(argv=None) -> int:
     a = parse(argv)
     dist = _Dist()
@@ -708,7 +721,7 @@ def main(argv=None) -> int:
                      "plumbing_* = BASELINE config 1 through `python -m beholder_amd run --source stdin`, "
                      "/metrics scraped before exit",
         }
-        print(json.dumps(out), flush=True)
+        print(json.dumps(_finite(out), allow_nan=False), flush=True)
     dist.close()
     return 0
 

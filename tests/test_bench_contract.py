@@ -152,3 +152,11 @@ def test_no_hip_before_child_processes(monkeypatch, capsys):
     assert "spawn" in order and "procs" in order and "sync" in order
     first = order.index("sync")
     assert all(x == "sync" for x in order[first:]), order
+
+
+def test_line_is_strict_json():
+    """A NaN or infinity in any extra key would make the driver's JSON parse fail: they print as
+    null."""
+    import bench
+    out = bench._finite({"value": 1.5, "x": float("nan"), "y": [float("inf"), 2], "z": {"w": float("-inf")}})
+    assert json.loads(json.dumps(out, allow_nan=False)) == {"value": 1.5, "x": None, "y": [None, 2], "z": {"w": None}}
