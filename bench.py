@@ -588,6 +588,18 @@ def calibrate() -> dict:
             "calib_py_ns": min(_calib_py_once() for _ in range(CALIB_REPS))}
 
 
+def _phase(name: str, fn, a) -> dict:
+    """One extra phase. A failure there (a fake that would not start on some host) must not cost
+    the driver its line: the headline still runs and prints, with ``<phase>_error`` saying what
+    went wrong (the contract tests check the extra keys themselves)."""
+    try:
+        return fn(a)
+    except Exception as e:  # noqa: BLE001 - reported on the line, and on stderr in full
+        import traceback
+        traceback.print_exc(file=sys.stderr)
+        return {f"{name}_error": f"{type(e).__name__}: {e}"[:300]}
+
+
 def _finite(x):
     """The line must be strict JSON for the driver: a NaN or infinity anywhere (an extra key
     computed from an empty phase) becomes null instead of an unparseable token."""
@@ -615,7 +627,7 @@ def main(argv=None) -> int:
 
     # 1. phases that start child processes (before any HIP call in this process)
     if a.extras and dist.rank == 0:
-        extras.update(io_extras(a))
+        extras.update(_phase("io_extras", io_extras, a))
     dist.barrier()
     allp = None
     if a.all_procs_steps > 0 and procs > 1:
@@ -625,7 +637,7 @@ def main(argv=None) -> int:
 
     # 2. paced BASELINE configs 2-4 (in process, before HIP is initialised)
     if a.extras and dist.rank == 0:
-        extras.update(paced_extras(a))
+        extras.update(_phase("paced_extras", paced_extras, a))
     dist.barrier()
 
     # 3. the headline: one consumer per rank, K timed steps, between two calibration runs
@@ -645,7 +657,7 @@ def main(argv=None) -> int:
 
     # 4. BASELINE config 5 (no child processes: HIP may be initialised now)
     if a.extras and dist.rank == 0:
-        extras.update(soak_extras(a))
+        extras.update(_phase("soak_extras", soak_extras, a))
     dist.barrier()
 
     if dist.rank == 0:

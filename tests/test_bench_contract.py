@@ -160,3 +160,13 @@ def test_line_is_strict_json():
     import bench
     out = bench._finite({"value": 1.5, "x": float("nan"), "y": [float("inf"), 2], "z": {"w": float("-inf")}})
     assert json.loads(json.dumps(out, allow_nan=False)) == {"value": 1.5, "x": None, "y": [None, 2], "z": {"w": None}}
+
+
+def test_a_failing_extra_phase_still_leaves_the_line(capsys):
+    import bench
+
+    def boom(a):
+        raise RuntimeError("fake would not start")
+    assert bench._phase("io_extras", boom, None) == {"io_extras_error": "RuntimeError: fake would not start"}
+    assert "fake would not start" in capsys.readouterr().err
+    assert bench._phase("paced_extras", lambda a: {"k": 1}, None) == {"k": 1}
