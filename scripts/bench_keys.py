@@ -30,12 +30,22 @@ KEYS = ["value", "cpu_us_per_event", "thp", "headline_minflt", "calib_ns", "cali
 
 
 def main(paths):
+    """Bench lines side by side; ``--range`` prints min / median / max of the numeric keys instead
+    (the spread over several lines, as the docs quote it)."""
+    spread = "--range" in paths
+    paths = [p for p in paths if p != "--range"]
     rows = []
     for p in paths:
         with open(p) as f:
             lines = [x for x in f.read().splitlines() if x.startswith("{")]
         rows.append(json.loads(lines[-1]) if lines else {})
     for k in KEYS:
+        if spread:
+            v = sorted(r[k] for r in rows if isinstance(r.get(k), (int, float)) and not isinstance(r.get(k), bool))
+            if v:
+                med = v[len(v) // 2] if len(v) % 2 else (v[len(v) // 2 - 1] + v[len(v) // 2]) / 2
+                print(f"{k:45s} min {v[0]:.6g}  median {med:.6g}  max {v[-1]:.6g}  (n={len(v)})")
+            continue
         print(f"{k:45s} " + " | ".join(json.dumps(r.get(k)) for r in rows))
 
 
