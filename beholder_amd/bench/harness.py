@@ -500,7 +500,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
     from ..sinks import H1Client
     from ..store.postgres import PostgresStore
     from ..transport.amqp import AmqpSource
-    from ..utils.hostinfo import cgroup_cpu_stat, cgroup_delta
+    from ..utils.hostinfo import cgroup_cpu_stat, cgroup_delta, proc_cpu_s
     from ..utils.log import Logger
     from .stallmon import StallMonitor
 
@@ -516,6 +516,11 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
         procs += pp
         url = f"{'https' if tls else 'http'}://127.0.0.1:{hport}"
         out["tls"] = tls
+        kinds = [("broker", p) for p in bprocs] + [("http", p) for p in hp] + [("pg", p) for p in pp]
+        # the box's core speed right before the phase (the same fixed-work loop as bench.py's
+        # calib_ns): a slow phase on a slow core says so on the line
+        from ..ops import calib
+        out["calib_ns"] = min(calib(4_000_000)[0] for _ in range(3))
 
         async def go():
             cfgd = bench_config()
@@ -552,6 +557,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             mon.reset()
             rss0 = _rss_mb()  # pools full, code paths warm: later growth would be a leak
             cg1 = cgroup_cpu_stat()
+            fcpu0 = [proc_cpu_s(p.pid) for _, p in kinds]
             ru0 = resource.getrusage(resource.RUSAGE_SELF)
             if hooks:
                 hooks[0]()
@@ -561,6 +567,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             if hooks:
                 hooks[1]()
             ru1 = resource.getrusage(resource.RUSAGE_SELF)
+            fcpu1 = [proc_cpu_s(p.pid) for _, p in kinds]
             cg2 = cgroup_cpu_stat()
             mon.stop()
             steady_slow = _slowest(src.settler.slow_deliveries()[0], _settled(src.settler) - settled0)
@@ -576,9 +583,14 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             await svc.close()
             sink.close()
             cpu = (ru1.ru_utime + ru1.ru_stime) - (ru0.ru_utime + ru0.ru_stime)
+            fakes_cpu: Dict[str, float] = {}
+            for (kind, _), a0, a1 in zip(kinds, fcpu0, fcpu1):
+                if a0 is not None and a1 is not None:
+                    fakes_cpu[kind] = fakes_cpu.get(kind, 0.0) + (a1 - a0)
             diag = {"warm_slow": warm_slow, "steady_slow": steady_slow, "mon": mon, "warm_mon": warm_mon,
                     "nivcsw": ru1.ru_nivcsw - ru0.ru_nivcsw, "cgroup_warmup": cgroup_delta(cg0, cg1),
-                    "cgroup_steady": cgroup_delta(cg1, cg2)}
+                    "cgroup_steady": cgroup_delta(cg1, cg2), "fakes_cpu_s": fakes_cpu,
+                    "minflt": ru1.ru_minflt - ru0.ru_minflt, "majflt": ru1.ru_majflt - ru0.ru_majflt}
             return elapsed, stats, cpu, ru1.ru_stime - ru0.ru_stime, pg_conns, http_stats, measured, cold, rss1 - rss0, diag
 
         elapsed, stats, cpu, sys_s, pg_conns, http_stats, m, cold, rss_growth, diag = asyncio.run(go())
@@ -593,6 +605,10 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             "errors": sum(stats.get("handler_errors", {}).values()),
             "pg_connections": pg_conns, "http": http_stats, "rss_growth_mb": round(rss_growth, 2),
             "nivcsw": diag["nivcsw"], "cgroup_warmup": diag["cgroup_warmup"], "cgroup_steady": diag["cgroup_steady"],
+            "minflt": diag["minflt"], "majflt": diag["majflt"],
+            # each fake's CPU over the measured window, per consumed event (broker / pg / http(s)):
+            # the share of the phase's CPU the consumer does not own
+            "fakes_cpu_us_per_event": {k: round(v / m * 1e6, 3) for k, v in diag["fakes_cpu_s"].items()} if m else {},
         })
     finally:
         stalls: list = []

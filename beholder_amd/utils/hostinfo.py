@@ -183,3 +183,21 @@ def host_busy_pct(before: Optional[tuple], after: Optional[tuple]) -> Optional[f
     if not before or not after or after[1] <= before[1]:
         return None
     return round(100.0 * (after[0] - before[0]) / (after[1] - before[1]), 1)
+
+
+def proc_cpu_s(pid: int) -> Optional[float]:
+    """User + system CPU seconds a process has used so far (``/proc/<pid>/stat`` fields 14-15),
+    or None when it is gone. The e2e bench phases read it for each fake around the measured window,
+    so a slow phase can be put on the consumer or on the processes it talks to."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            raw = f.read()
+    except OSError:
+        return None
+    # the command name (field 2) may hold spaces and parentheses: split after its last ')'
+    fields = raw[raw.rfind(")") + 2:].split()
+    try:
+        ticks = int(fields[11]) + int(fields[12])  # utime, stime (fields 14 and 15 of the line)
+    except (IndexError, ValueError):
+        return None
+    return ticks / os.sysconf("SC_CLK_TCK")

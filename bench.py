@@ -97,11 +97,16 @@ def parse(argv=None):
                     help="timed steps of the all-process phase (0 = skip it)")
     ap.add_argument("--no-extras", dest="extras", action="store_false",
                     help="skip the rate_10k / soak / overload / TCP measurements")
-    ap.add_argument("--io-events", type=int, default=50000, help="events of each TCP measurement")
+    ap.add_argument("--io-events", type=int, default=50000,
+                    help="events of the preconnect and http_tcp measurements")
+    ap.add_argument("--e2e-events", type=int, default=250000,
+                    help="events of each tcp_e2e / tls_e2e measurement (the first 5,000 are the warm-up)")
     ap.add_argument("--soak-events", type=int, default=1_000_000)
     ap.add_argument("--media", type=int, default=10000)
     ap.add_argument("--log-level", default="info")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--full-out", default=os.environ.get("BENCH_FULL_OUT", os.path.join(ROOT, "gpurun_out", "bench_full.json")),
+                    help="where the full record (every key of the run) is written; '' = nowhere")
     ap.add_argument("--ordering", default="none", choices=["none", "per_media"])
     ap.add_argument("--pin", action="store_true",
                     help="pin each all-process consumer to its own CPU of the rank's affinity mask")
@@ -394,6 +399,42 @@ def _cg(prefix: str, d: dict) -> dict:
     return {f"{prefix}_nr_throttled": d.get("nr_throttled"), f"{prefix}_throttled_usec": d.get("throttled_usec")}
 
 
+def _e2e_keys(prefix: str, run, n: int, **kw) -> dict:
+    """One production-shaped phase (harness._tcp_e2e): rate, CPU per event (user+sys and sys alone),
+    latency, and what else could have moved them: the box's core speed right before the phase,
+    page faults and involuntary switches of the measured window, each fake's CPU per event, the
+    host's busy share, throttling, and the slow-delivery attribution."""
+    from beholder_amd.utils.hostinfo import host_busy_pct, host_cpu_times
+    h0 = host_cpu_times()
+    e = run(n, **kw)
+    h1 = host_cpu_times()
+    hl = e.get("handle_latency_us", {})
+    wl = e.get("warmup_handle_latency_us", {})
+    out = {f"{prefix}_events_per_sec": _r(e.get("ingest_rate_eps"), 1),
+           f"{prefix}_measured_events": e.get("measured_events"),
+           f"{prefix}_cpu_us_per_event": _r(e.get("cpu_us_per_event")),
+           f"{prefix}_sys_cpu_us_per_event": _r(e.get("sys_cpu_us_per_event")),
+           f"{prefix}_p50_handle_latency_us": _r(hl.get("p50")),
+           f"{prefix}_p99_handle_latency_us": _r(hl.get("p99")),
+           f"{prefix}_p999_handle_latency_us": _r(hl.get("p999")),
+           f"{prefix}_warmup_p99_handle_latency_us": _r(wl.get("p99")),
+           f"{prefix}_warmup_p999_handle_latency_us": _r(wl.get("p999")),
+           f"{prefix}_errors": e.get("errors"), f"{prefix}_nivcsw": e.get("nivcsw"),
+           f"{prefix}_minflt": e.get("minflt"), f"{prefix}_majflt": e.get("majflt"),
+           f"{prefix}_calib_ns": e.get("calib_ns"),
+           f"{prefix}_fakes_cpu_us_per_event": e.get("fakes_cpu_us_per_event"),
+           f"{prefix}_host_cpu_busy_pct": host_busy_pct(h0, h1),
+           **_cg(prefix, e.get("cgroup_steady") or {}),
+           **_attr_keys(prefix, e.get("attribution_steady")),
+           **_attr_keys(f"{prefix}_warmup", e.get("attribution_warmup")),
+           **_pool_keys(prefix, e.get("http"))}
+    if kw.get("tls"):
+        http = e.get("http") or {}
+        out.update({f"{prefix}_handshakes": http.get("tls_handshakes"), f"{prefix}_resumed": http.get("tls_resumed"),
+                    f"{prefix}_init_ms": e.get("init_ms")})
+    return out
+
+
 def io_extras(a) -> dict:
     """BASELINE config 1 (the real CLI on stdin) and the production-shaped TCP path. Both start
     child processes, so they run before this process touches HIP."""
@@ -407,41 +448,12 @@ def io_extras(a) -> dict:
                 "plumbing_has_progress_counter": p["scrape_has_progress_counter"],
                 "plumbing_has_trello_counter": p["scrape_has_trello_counter"],
                 "plumbing_process_wall_s": _r(p["process_wall_s"])})
-    from beholder_amd.utils.hostinfo import host_busy_pct, host_cpu_times
-    h0 = host_cpu_times()
-    e2e = harness._tcp_e2e(a.io_events)
-    h1 = host_cpu_times()
-    hl = e2e.get("handle_latency_us", {})
-    out.update({"tcp_e2e_events_per_sec": _r(e2e.get("ingest_rate_eps"), 1),
-                "tcp_e2e_cpu_us_per_event": _r(e2e.get("cpu_us_per_event")),
-                "tcp_e2e_p50_handle_latency_us": _r(hl.get("p50")),
-                "tcp_e2e_p999_handle_latency_us": _r(hl.get("p999")),
-                "tcp_e2e_warmup_p99_handle_latency_us": _r(e2e.get("warmup_handle_latency_us", {}).get("p99")),
-                "tcp_e2e_warmup_p999_handle_latency_us": _r(e2e.get("warmup_handle_latency_us", {}).get("p999")),
-                "tcp_e2e_errors": e2e.get("errors"), "tcp_e2e_nivcsw": e2e.get("nivcsw"),
-                "tcp_e2e_host_cpu_busy_pct": host_busy_pct(h0, h1),
-                **_cg("tcp_e2e", e2e.get("cgroup_steady") or {}),
-                **_attr_keys("tcp_e2e", e2e.get("attribution_steady")),
-                **_attr_keys("tcp_e2e_warmup", e2e.get("attribution_warmup")),
-                **_pool_keys("tcp_e2e", e2e.get("http"))})
-    h0 = host_cpu_times()
-    tls = harness._tcp_e2e(a.io_events, http_servers=4, tls=True)
-    h1 = host_cpu_times()
-    hl = tls.get("handle_latency_us", {})
-    out.update({"tls_e2e_events_per_sec": _r(tls.get("ingest_rate_eps"), 1),
-                "tls_e2e_cpu_us_per_event": _r(tls.get("cpu_us_per_event")),
-                "tls_e2e_p50_handle_latency_us": _r(hl.get("p50")),
-                "tls_e2e_p999_handle_latency_us": _r(hl.get("p999")),
-                "tls_e2e_warmup_p99_handle_latency_us": _r(tls.get("warmup_handle_latency_us", {}).get("p99")),
-                "tls_e2e_warmup_p999_handle_latency_us": _r(tls.get("warmup_handle_latency_us", {}).get("p999")),
-                "tls_e2e_handshakes": (tls.get("http") or {}).get("tls_handshakes"),
-                "tls_e2e_resumed": (tls.get("http") or {}).get("tls_resumed"),
-                "tls_e2e_errors": tls.get("errors"), "tls_e2e_nivcsw": tls.get("nivcsw"),
-                "tls_e2e_host_cpu_busy_pct": host_busy_pct(h0, h1),
-                **_cg("tls_e2e", tls.get("cgroup_steady") or {}),
-                **_attr_keys("tls_e2e", tls.get("attribution_steady")),
-                **_attr_keys("tls_e2e_warmup", tls.get("attribution_warmup")),
-                **_pool_keys("tls_e2e", tls.get("http"))})
+    # unmeasured: one short pass of the whole TCP path first, so the first measured e2e phase is
+    # not also this process's first (first-touch page faults, the pools' and fakes' first
+    # connections, lazily imported modules), as the paced configs get one
+    harness._tcp_e2e(min(20000, a.e2e_events))
+    out.update(_e2e_keys("tcp_e2e", harness._tcp_e2e, a.e2e_events))
+    out.update(_e2e_keys("tls_e2e", harness._tcp_e2e, a.e2e_events, http_servers=4, tls=True))
     # the same with service.http.preconnect = prefetch: the first wave of TLS handshakes happens
     # in init (`_init_ms`), not inside the first deliveries' handle latency
     pre = harness._tcp_e2e(a.io_events, http_servers=4, tls=True, preconnect=100)
@@ -449,7 +461,7 @@ def io_extras(a) -> dict:
                 "tls_e2e_preconnect_p999_handle_latency_us": _r(pre.get("handle_latency_us", {}).get("p999")),
                 "tls_e2e_preconnect_warmup_p999_handle_latency_us":
                     _r(pre.get("warmup_handle_latency_us", {}).get("p999")),
-                "tls_e2e_preconnect_init_ms": pre.get("init_ms"), "tls_e2e_init_ms": tls.get("init_ms"),
+                "tls_e2e_preconnect_init_ms": pre.get("init_ms"),
                 "tls_e2e_preconnect_handshakes": (pre.get("http") or {}).get("tls_handshakes"),
                 "tls_e2e_preconnect_errors": pre.get("errors")})
     h = harness._http_tcp(Workload(n_media=10000, seed=a.seed), a.io_events, clients=("h1",))["h1"]
@@ -612,6 +624,115 @@ def _finite(x):
     return x
 
 
+DATA = ("synthetic telemetry (90% progress / 10% status), 10k-media in-memory store, "
+        "Trello/Telegram/Emby stubbed in-process (native recorder: URL + query built and logged "
+        "per request), info logs to /dev/null")
+
+NOTES = ("CPU event-consumer workload (the reference has no device compute; see docs/DESIGN.md). "
+         "value = one consumer process per rank; all_procs_* = every CPU of the share busy; "
+         "rate_1k/rate_10k/rate_100k/soak = BASELINE configs 2-5 (rate_100k paced into a 4096-event "
+         "drop_newest ring; burst = the same ring fed unpaced); tcp_e2e/http_tcp = every dependency "
+         "over TCP, tls_e2e = same with HTTPS sinks; tcp_e2e/tls_e2e latencies are receive->ack at "
+         "saturation with prefetch 100 in flight (queueing included), warmup_* = the first 5,000 "
+         "deliveries (connection pools filling from zero; http.preconnect 0); *_slow_blamed = the "
+         "slowest 0.1% of deliveries blamed on the process (consumer / pg / http(s) / broker fake) "
+         "whose event-loop or GC stall covered most of their time, 'none' = no stall >= 1 ms "
+         "(bench/stallmon.py); rate_*_p99_queue = reader push -> handler start, "
+         "rate_*_p99_handle = handler start -> ack; *_dial_max / *_queue_wait_* = the slowest sink "
+         "connect (+TLS handshake) and the wait of requests queued for a connection (the warm-up); "
+         "*_fakes_cpu_us_per_event = each fake's CPU over the measured window per event; "
+         "*_e2e_calib_ns = the calib loop right before that phase; "
+         "calib_ns = fixed-work C loop (ops.calib) "
+         "around the headline, value_calibrated = value * calib_ns / calib_ref_ns; "
+         "plumbing_* = BASELINE config 1 through `python -m beholder_amd run --source stdin`, "
+         "/metrics scraped before exit")
+
+# The driver keeps the tail of stdout (its `tail` field: the last ~2,000 characters; its
+# `stdout_tail`: the last ~8,000), so the one JSON line is built for that:
+# the contract keys first, then diagnostics while the line stays within LINE_BUDGET characters,
+# then the decision keys, with the headline's own figures last of all. Every key of the run goes
+# to the full record (``--full-out``). tests/test_bench_contract.py pins the layout.
+LINE_BUDGET = 6000
+TAIL_BUDGET = 2000
+HEAD_KEYS = ("metric", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+             "vs_baseline", "dtype", "data", "config")
+# decision keys, in line order: the last one printed is `value`
+TAIL_KEYS = (
+    "soak_gc_max_pause_us", "soak_rss_growth_mb", "soak_events_per_sec",
+    "burst_dropped", "rate_100k_dropped",
+    "rate_1k_p99_ingest_latency_us", "rate_10k_p50_ingest_latency_us", "rate_10k_p99_ingest_latency_us",
+    "rate_100k_p99_ingest_latency_us",
+    "all_procs_events_per_sec",
+    "shared_queue_events_per_sec", "shared_queue_exactly_once",
+    "http_tcp_h1_events_per_sec",
+    "tls_e2e_preconnect_warmup_p999_handle_latency_us",
+    "tls_e2e_warmup_p999_handle_latency_us", "tls_e2e_p999_handle_latency_us", "tls_e2e_cpu_us_per_event",
+    "tls_e2e_events_per_sec",
+    "tcp_e2e_warmup_p999_handle_latency_us", "tcp_e2e_p999_handle_latency_us", "tcp_e2e_p99_handle_latency_us",
+    "tcp_e2e_sys_cpu_us_per_event", "tcp_e2e_cpu_us_per_event", "tcp_e2e_events_per_sec",
+    "calib_ns", "value_calibrated", "handler_errors",
+    "cpu_us_per_event", "p99_handle_latency_us", "p50_handle_latency_us", "value",
+)
+# diagnostics that go on the line first, while it has room (the rest follow in run order)
+DIAG_FIRST = (
+    "tcp_e2e_calib_ns", "tcp_e2e_minflt", "tcp_e2e_majflt", "tcp_e2e_nivcsw", "tcp_e2e_fakes_cpu_us_per_event",
+    "tcp_e2e_host_cpu_busy_pct", "tcp_e2e_nr_throttled", "tcp_e2e_measured_events", "tcp_e2e_slow_blamed",
+    "tls_e2e_calib_ns", "tls_e2e_sys_cpu_us_per_event", "tls_e2e_minflt", "tls_e2e_nivcsw",
+    "tls_e2e_fakes_cpu_us_per_event", "tls_e2e_host_cpu_busy_pct", "tls_e2e_slow_blamed",
+    "headline_minflt", "involuntary_ctx_switches", "headline_host_cpu_busy_pct", "calib_mem_ns", "calib_py_ns",
+    "shared_queue_broker_cpu_us_per_event", "shared_queue_acked", "shared_queue_published",
+    "plumbing_rc", "plumbing_acked", "plumbing_sink_requests", "rate_1k_acked", "rate_10k_acked",
+    "rate_100k_offered", "rate_100k_accepted", "burst_offered", "burst_accepted",
+    "tcp_e2e_errors", "tls_e2e_errors", "soak_events",
+)
+
+
+def _write_full(path: str, full: dict):
+    """Every key of the run as one JSON document (the line carries a subset). Returns the path
+    written, or None when it could not be written (the line is still printed)."""
+    if not path:
+        return None
+    try:
+        d = os.path.dirname(os.path.abspath(path))
+        os.makedirs(d, exist_ok=True)
+        tmp = f"{path}.{os.getpid()}.tmp"
+        with open(tmp, "w") as f:
+            json.dump(full, f, indent=1, allow_nan=False)
+        os.replace(tmp, path)
+        return path
+    except OSError as e:
+        print(f"bench.py: could not write the full record to {path}: {e}", file=sys.stderr)
+        return None
+
+
+def _enc(k, v) -> int:
+    return len(json.dumps({k: v}, allow_nan=False))  # '"k": v, ' as it sits inside the line
+
+
+def compact_line(full: dict, full_path=None) -> dict:
+    """The printed line: HEAD_KEYS, a pointer to the full record, diagnostics while they fit in
+    LINE_BUDGET, then TAIL_KEYS (which fit in TAIL_BUDGET: the driver's `tail`)."""
+    head = {k: full[k] for k in HEAD_KEYS if k in full}
+    head["full_record"] = {"path": full_path, "keys": len(full)}
+    tail = {k: full[k] for k in TAIL_KEYS if k in full}
+    used = len(json.dumps(head)) + len(json.dumps(tail))
+    diag: dict = {}
+    order = [k for k in DIAG_FIRST if k in full] + [k for k in full if k not in DIAG_FIRST]
+    for k in order:
+        if k in head or k in tail or k in diag or k == "notes":
+            continue
+        c = _enc(k, full[k])
+        if used + c > LINE_BUDGET:
+            continue  # too big for what is left: a smaller later key may still fit
+        diag[k] = full[k]
+        used += c
+    out = {**head, **diag, **tail}
+    while diag and len(json.dumps(out, allow_nan=False)) > LINE_BUDGET:  # never reached; a guard
+        diag.popitem()
+        out = {**head, **diag, **tail}
+    return out
+
+
 def main(argv=None) -> int:
     a = parse(argv)
     dist = _Dist()
@@ -678,7 +799,7 @@ def main(argv=None) -> int:
                     "value_calibrated": round(value * cal["calib_ns"] / ref, 1) if ref else None,
                     "headline_host_cpu_busy_pct": host_busy_pct(h0, h1),
                     **_cg("headline", cgroup_delta(cg0, cg1))})
-        out = {
+        full = {
             "metric": BASELINE_METRIC,
             "value": round(value, 1),
             "unit": "events/s",
@@ -690,9 +811,7 @@ def main(argv=None) -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "protobuf-events (no tensor compute)",
-            "data": "synthetic telemetry (90% progress / 10% status), 10k-media in-memory store, "
-                    "Trello/Telegram/Emby stubbed in-process (native recorder: URL + query built and logged "
-                    "per request), info logs to /dev/null",
+            "data": DATA,
             "config": {
                 "model": "beholder telemetry consumer (status+progress handlers, index.js:62-155)",
                 "global_batch": a.events_per_step * n,
@@ -716,24 +835,12 @@ def main(argv=None) -> int:
             "cpu_share": cpu_share(),
             "gpus_on_node": gpus_on_node(),
             **extras,
-            "notes": "CPU event-consumer workload (the reference has no device compute; see docs/DESIGN.md). "
-                     "value = one consumer process per rank; all_procs_* = every CPU of the share busy; "
-                     "rate_1k/rate_10k/rate_100k/soak = BASELINE configs 2-5 (rate_100k paced into a 4096-event "
-                     "drop_newest ring; burst = the same ring fed unpaced); tcp_e2e/http_tcp = every dependency "
-                     "over TCP, tls_e2e = same with HTTPS sinks; tcp_e2e/tls_e2e latencies are receive->ack at "
-                     "saturation with prefetch 100 in flight (queueing included), warmup_* = the first 5,000 "
-                     "deliveries (connection pools filling from zero; http.preconnect 0); *_slow_blamed = the "
-                     "slowest 0.1% of deliveries blamed on the process (consumer / pg / http(s) / broker fake) "
-                     "whose event-loop or GC stall covered most of their time, 'none' = no stall >= 1 ms "
-                     "(bench/stallmon.py); rate_*_p99_queue = reader push -> handler start, "
-                     "rate_*_p99_handle = handler start -> ack; *_dial_max / *_queue_wait_* = the slowest sink "
-                     "connect (+TLS handshake) and the wait of requests queued for a connection (the warm-up); "
-                     "calib_ns = fixed-work C loop (ops.calib) "
-                     "around the headline, value_calibrated = value * calib_ns / calib_ref_ns; "
-                     "plumbing_* = BASELINE config 1 through `python -m beholder_amd run --source stdin`, "
-                     "/metrics scraped before exit",
+            "notes": NOTES,
         }
-        print(json.dumps(_finite(out), allow_nan=False), flush=True)
+        full = _finite(full)
+        full_path = _write_full(a.full_out, full)
+        out = compact_line(full, full_path)
+        print(json.dumps(out, allow_nan=False), flush=True)
     dist.close()
     return 0
 

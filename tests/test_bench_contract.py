@@ -29,7 +29,13 @@ EXTRAS = {"all_procs_events_per_sec", "rate_10k_p50_ingest_latency_us", "rate_10
           "tls_e2e_queue_wait_max_us", "headline_minflt", "thp", "tls_e2e_preconnect_warmup_p999_handle_latency_us",
           "tls_e2e_preconnect_init_ms", "tls_e2e_init_ms", "rate_1k_p99_due_to_ack_us",
           "rate_10k_p99_due_to_ack_us", "rate_100k_p99_due_to_ack_us", "rate_10k_p99_due_to_recv_us"}
-SMALL = ["--steps", "2", "--warmup", "1", "--events-per-step", "4096", "--media", "500"]
+SMALL = ["--steps", "2", "--warmup", "1", "--events-per-step", "4096", "--media", "500", "--full-out", ""]
+# the keys the driver's `tail` (the last ~2,000 characters of stdout) must show
+DECISION = ("value", "p50_handle_latency_us", "p99_handle_latency_us", "cpu_us_per_event", "calib_ns",
+            "value_calibrated", "tcp_e2e_events_per_sec", "tcp_e2e_cpu_us_per_event", "tcp_e2e_sys_cpu_us_per_event",
+            "tcp_e2e_p999_handle_latency_us", "tls_e2e_events_per_sec", "tls_e2e_p999_handle_latency_us",
+            "rate_1k_p99_ingest_latency_us", "rate_10k_p99_ingest_latency_us", "rate_100k_p99_ingest_latency_us",
+            "soak_events_per_sec", "soak_gc_max_pause_us", "all_procs_events_per_sec")
 
 
 def _last_json(stdout: str) -> dict:
@@ -40,12 +46,29 @@ def _last_json(stdout: str) -> dict:
     return json.loads(lines[0])
 
 
-def test_bench_single_rank_contract():
+def test_bench_single_rank_contract(tmp_path):
+    full_path = str(tmp_path / "full.json")
     r = subprocess.run([sys.executable, "bench.py", *SMALL, "--procs-per-rank", "2", "--all-procs-steps", "1",
-                        "--io-events", "2000", "--soak-events", "20000"],
+                        "--io-events", "2000", "--e2e-events", "4000", "--soak-events", "20000",
+                        "--full-out", full_path],
                        cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
-    out = _last_json(r.stdout)
+    line = [x for x in r.stdout.splitlines() if x.strip()][-1]
+    printed = _last_json(r.stdout)
+    # the line the driver keeps: short, and every decision key inside its last 2,000 characters
+    import bench
+    assert len(line) <= bench.LINE_BUDGET <= 8000, len(line)
+    tail = line[-2000:]
+    for k in DECISION:
+        assert f'"{k}": ' in tail, (k, tail)
+    assert REQUIRED <= set(printed)
+    assert printed["full_record"] == {"path": full_path, "keys": printed["full_record"]["keys"]}
+    with open(full_path) as f:
+        out = json.load(f)  # every key of the run
+    assert printed["full_record"]["keys"] == len(out)
+    for k, v in printed.items():
+        if k != "full_record":
+            assert out[k] == v, k
     assert REQUIRED <= set(out) and out["n_gpus"] == 1 and out["steps"] == 2 and out["warmup"] == 1
     assert {"model", "global_batch", "seq_len", "parallelism"} <= set(out["config"])
     assert EXTRAS <= set(out), EXTRAS - set(out)
@@ -72,6 +95,10 @@ def test_bench_single_rank_contract():
     assert out["plumbing_has_progress_counter"] and out["plumbing_has_trello_counter"]
     assert out["calib_ns"] >= max(out["calib_ns_before"], out["calib_ns_after"]) > 0
     assert set(out["tcp_e2e_slow_blamed"]) >= {"consumer", "pg", "http", "none"}
+    # the e2e phases say what else could have moved them
+    assert 4000 - 400 - 100 <= out["tcp_e2e_measured_events"] <= 4000 - 400 and out["tcp_e2e_calib_ns"] > 0
+    assert set(out["tcp_e2e_fakes_cpu_us_per_event"]) == {"broker", "pg", "http"}
+    assert out["tcp_e2e_sys_cpu_us_per_event"] >= 0 and out["tcp_e2e_minflt"] >= 0
 
 
 def test_bench_two_ranks_gloo():
@@ -146,7 +173,7 @@ def test_no_hip_before_child_processes(monkeypatch, capsys):
     monkeypatch.setattr(harness, "_spawn", spy_spawn)
     monkeypatch.setattr(bench, "run_procs", spy_procs)
     assert bench.main([*SMALL, "--procs-per-rank", "2", "--all-procs-steps", "1", "--io-events", "1000",
-                       "--soak-events", "5000"]) == 0
+                       "--e2e-events", "1000", "--soak-events", "5000"]) == 0
     out = _last_json(capsys.readouterr().out)
     assert out["value"] > 0
     assert "spawn" in order and "procs" in order and "sync" in order
@@ -170,3 +197,24 @@ def test_a_failing_extra_phase_still_leaves_the_line(capsys):
     assert bench._phase("io_extras", boom, None) == {"io_extras_error": "RuntimeError: fake would not start"}
     assert "fake would not start" in capsys.readouterr().err
     assert bench._phase("paced_extras", lambda a: {"k": 1}, None) == {"k": 1}
+
+
+def test_compact_line_keeps_decision_keys_last_and_fits():
+    """However many diagnostic keys a run produces, the printed line stays within LINE_BUDGET and
+    the decision keys are its last TAIL_BUDGET characters; oversized diagnostics are left to the
+    full record."""
+    import bench
+    full = {k: 1 for k in bench.HEAD_KEYS}
+    full.update({"data": "x" * 300, "config": {"model": "m", "global_batch": 1, "seq_len": None, "parallelism": "dp1"}})
+    full.update({f"diag_{i}": {"a": 123456.7, "b": [1, 2, 3]} for i in range(400)})
+    full["huge"] = "y" * 9000
+    full.update({k: 123456.789 for k in bench.TAIL_KEYS if k not in ("shared_queue_events_per_sec",)})
+    full["shared_queue_events_per_sec"] = {"1": 123456.7, "2": 234567.8, "4": 345678.9, "8": 456789.1}
+    line = json.dumps(bench.compact_line(full, "/x/full.json"))
+    assert len(line) <= bench.LINE_BUDGET
+    assert "huge" not in line and '"diag_0"' in line
+    tail_keys = [k for k in json.loads(line)][-len(bench.TAIL_KEYS):]
+    assert tail_keys == list(bench.TAIL_KEYS)
+    assert tail_keys[-1] == "value"
+    start = line.index(f'"{bench.TAIL_KEYS[0]}"')
+    assert len(line) - start <= bench.TAIL_BUDGET, len(line) - start
