@@ -9,9 +9,10 @@ WORKDIR /stack
 RUN pip install --no-cache-dir --prefix=/install protobuf pyyaml
 COPY . /stack
 # native runtime (ingest ring, codec, deliveries, metrics, text, TLS) built in-tree; the optional
-# gfx950 HIP probe library is skipped (no hipcc in this image)
-RUN python -m beholder_amd._build --force --no-hip \
-    && rm -rf beholder_amd/ops/csrc beholder_amd/ops/*.lock tests profiles scripts \
+# gfx950 HIP probe library and the bench/test natives (_native_bench: sink stub, paced producer,
+# calibrations, profiler) are not built: the image ships only the service
+RUN python -m beholder_amd._build --force --no-hip --no-bench \
+    && rm -rf beholder_amd/ops/csrc beholder_amd/ops/csrc_bench beholder_amd/ops/*.lock tests profiles scripts \
     && find /stack -name __pycache__ -prune -exec rm -rf {} +
 
 FROM python:3.10-slim AS runtime

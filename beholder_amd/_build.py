@@ -1,5 +1,6 @@
-"""Build the native runtime in-tree (``beholder_amd/ops/_native*.so``) and the HIP offload
-probe (``beholder_amd/ops/hip/libbeholder_hip.so``, gfx950).
+"""Build the native runtime in-tree (``beholder_amd/ops/_native*.so``), the bench/test natives
+(``beholder_amd/ops/_native_bench*.so``, not part of the service) and the HIP offload probe
+(``beholder_amd/ops/hip/libbeholder_hip.so``, gfx950).
 
 Beholder's runtime around the Python handlers (ingest reader thread, ring,
 codec, deliveries, histograms) is C++ — see ``csrc/``. The service has no
@@ -12,7 +13,7 @@ The HIP library is optional for the service: ``main`` builds it only when ``hipc
 (``--hip`` makes it required, ``--no-hip`` skips it), so the deployment image and CI, which have
 no ROCm, build the runtime alone.
 
-Usage: ``python -m beholder_amd.ops.build [--debug] [--sanitize=address,undefined] [--hip|--no-hip]``
+Usage: ``python -m beholder_amd.ops.build [--debug] [--sanitize=address,undefined] [--hip|--no-hip] [--no-bench]``
 (thin CLI over this module)
 """
 from __future__ import annotations
@@ -37,16 +38,24 @@ STAMP = TARGET + ".srchash"
 LIBS = ["-lssl", "-lcrypto"]
 
 
-def sources() -> list:
-    return sorted(glob.glob(os.path.join(CSRC, "*.cpp")))
+# bench / test / diagnostic natives (the sink stub, the paced producer, calibration loops, the
+# sampling profiler): a module of their own, `_native_bench`, never linked into the service's
+# extension; the runtime image does not build it (`--no-bench`, Dockerfile)
+CSRC_BENCH = os.path.join(HERE, "csrc_bench")
+BENCH_TARGET = os.path.join(HERE, "_native_bench" + EXT_SUFFIX)
 
 
-def source_hash(flags: list) -> str:
+def sources(src_dir: str = CSRC) -> list:
+    return sorted(glob.glob(os.path.join(src_dir, "*.cpp")))
+
+
+def source_hash(flags: list, dirs=(CSRC,)) -> str:
     h = hashlib.sha256()
-    for p in sorted(glob.glob(os.path.join(CSRC, "*"))):
-        with open(p, "rb") as f:
-            h.update(os.path.basename(p).encode())
-            h.update(f.read())
+    for d in dirs:
+        for p in sorted(glob.glob(os.path.join(d, "*"))):
+            with open(p, "rb") as f:
+                h.update(os.path.basename(p).encode())
+                h.update(f.read())
     h.update(" ".join(flags).encode())
     return h.hexdigest()
 
@@ -55,7 +64,7 @@ def compile_flags(debug: bool = False, sanitize: str = "") -> list:
     inc = sysconfig.get_paths()["include"]
     flags = ["-std=c++17", "-fPIC", "-shared", "-pthread", "-fvisibility=hidden",
              "-Wall", "-Wextra", "-Wno-missing-field-initializers", "-Wno-cast-function-type",
-             f"-I{inc}", f"-I{CSRC}"]
+             f"-I{inc}", f"-I{CSRC}", f"-I{CSRC_BENCH}"]
     if debug:
         flags += ["-O0", "-g"]
     else:
@@ -104,23 +113,39 @@ class _BuildLock:
 
 
 def build(force: bool = False, debug: bool = False, sanitize: str = "", cxx: str = "", verbose: bool = False) -> str:
+    """The service's extension ``_native`` from ``csrc/``."""
+    return _build_module(TARGET, sources(CSRC), (CSRC,), LIBS, force, debug, sanitize, cxx, verbose)
+
+
+def build_bench(force: bool = False, debug: bool = False, sanitize: str = "", cxx: str = "",
+                verbose: bool = False) -> str:
+    """The bench/test extension ``_native_bench`` from ``csrc_bench/`` (headers from ``csrc/``:
+    it calls the service's code through ``_native._C_API``, never links it)."""
+    return _build_module(BENCH_TARGET, sources(CSRC_BENCH), (CSRC_BENCH, CSRC), [], force, debug, sanitize, cxx,
+                         verbose)
+
+
+def _build_module(target: str, srcs: list, dirs: tuple, libs: list, force: bool, debug: bool, sanitize: str,
+                  cxx: str, verbose: bool) -> str:
     cxx = cxx or os.environ.get("CXX") or "g++"
     flags = compile_flags(debug, sanitize)
+    stamp = target + ".srchash"
     # hash path-independent flags so a snapshot copied elsewhere (GPU box) reuses the .so
-    digest = source_hash([f for f in flags if not f.startswith("-I")] + LIBS + [cxx, sysconfig.get_config_var("SOABI") or ""])
-    if not force and _stamp_matches(TARGET, STAMP, digest):
-        return TARGET
-    with _BuildLock(TARGET):
-        if not force and _stamp_matches(TARGET, STAMP, digest):  # built while this process waited
-            return TARGET
-        print(f"beholder: building the native runtime ({os.path.basename(TARGET)}, pid {os.getpid()})",
+    digest = source_hash([f for f in flags if not f.startswith("-I")] + libs + [cxx, sysconfig.get_config_var("SOABI") or ""],
+                         dirs)
+    if not force and _stamp_matches(target, stamp, digest):
+        return target
+    with _BuildLock(target):
+        if not force and _stamp_matches(target, stamp, digest):  # built while this process waited
+            return target
+        print(f"beholder: building the native runtime ({os.path.basename(target)}, pid {os.getpid()})",
               file=sys.stderr)
-        tmp = f"{TARGET}.{os.getpid()}.tmp"  # per process: nothing else ever writes this file
+        tmp = f"{target}.{os.getpid()}.tmp"  # per process: nothing else ever writes this file
         # compile translation units in parallel (one compiler process each), then link
         import concurrent.futures
         import tempfile
         cflags = [f for f in flags if f != "-shared"]
-        jobs = max(1, min(len(sources()), int(os.environ.get("MAX_JOBS", "0") or 0) or (os.cpu_count() or 1), 16))
+        jobs = max(1, min(len(srcs), int(os.environ.get("MAX_JOBS", "0") or 0) or (os.cpu_count() or 1), 16))
         try:
             with tempfile.TemporaryDirectory(prefix="beholder-build-") as td:
                 def compile_one(src: str) -> str:
@@ -131,18 +156,18 @@ def build(force: bool = False, debug: bool = False, sanitize: str = "", cxx: str
                     subprocess.run(cmd, check=True)
                     return obj
                 with concurrent.futures.ThreadPoolExecutor(jobs) as ex:
-                    objs = list(ex.map(compile_one, sources()))
-                link = [cxx, *[f for f in flags if not f.startswith("-I") and not f.startswith("-W")], *objs, *LIBS,
+                    objs = list(ex.map(compile_one, srcs))
+                link = [cxx, *[f for f in flags if not f.startswith("-I") and not f.startswith("-W")], *objs, *libs,
                         "-o", tmp]
                 if verbose:
                     print(" ".join(link), file=sys.stderr)
                 subprocess.run(link, check=True)
-            os.replace(tmp, TARGET)
+            os.replace(tmp, target)
         finally:
             if os.path.exists(tmp):
                 os.unlink(tmp)
-        _write_atomic(STAMP, digest)
-    return TARGET
+        _write_atomic(stamp, digest)
+    return target
 
 
 HIP_DIR = os.path.join(HERE, "hip")
@@ -200,8 +225,12 @@ def main(argv=None) -> int:
     g = ap.add_mutually_exclusive_group()
     g.add_argument("--hip", action="store_true", help="require the gfx950 HIP extension (fail without hipcc)")
     g.add_argument("--no-hip", action="store_true", help="skip the gfx950 HIP extension")
+    ap.add_argument("--no-bench", action="store_true",
+                    help="skip the bench/test extension _native_bench (the runtime image ships only the service)")
     a = ap.parse_args(argv)
     print(build(force=a.force, debug=a.debug, sanitize=a.sanitize, cxx=a.cxx, verbose=True))
+    if not a.no_bench:
+        print(build_bench(force=a.force, debug=a.debug, sanitize=a.sanitize, cxx=a.cxx, verbose=True))
     if a.no_hip or a.sanitize:
         return 0
     if not a.hip and not hipcc():

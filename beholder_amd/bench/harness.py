@@ -88,7 +88,7 @@ class GcPauses:
 class _Producer(threading.Thread):
     """Writes pre-framed events into a pipe at ``rate`` events/s (0 = unpaced).
 
-    Paced runs go through :func:`~beholder_amd.ops.paced_write`: the pacing loop is native and
+    Paced runs go through :func:`~beholder_amd.ops.bench_native.paced_write`: the pacing loop is native and
     holds no GIL (clock_nanosleep to each event's due time, 1 ns timer slack), so the producer
     neither competes with the consumer's event loop for the GIL nor adds its own wake-up jitter to
     the receive→ack latency of BASELINE configs 2-4."""
@@ -130,7 +130,7 @@ class _Producer(threading.Thread):
                     mv = mv[n:]
                 self.elapsed = time.perf_counter() - t0
             else:
-                from ..ops import paced_write
+                from ..ops.bench_native import paced_write
                 self.elapsed, self.writes, self.t0_ns = paced_write(self.wfd, self.data, self.ends,
                                                                     float(self.rate))
         except OSError:
@@ -519,7 +519,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
         kinds = [("broker", p) for p in bprocs] + [("http", p) for p in hp] + [("pg", p) for p in pp]
         # the box's core speed right before the phase (the same fixed-work loop as bench.py's
         # calib_ns): a slow phase on a slow core says so on the line
-        from ..ops import calib
+        from ..ops.bench_native import calib
         out["calib_ns"] = min(calib(4_000_000)[0] for _ in range(3))
 
         async def go():

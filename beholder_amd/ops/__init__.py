@@ -8,7 +8,8 @@ fallback (set ``BEHOLDER_ALLOW_BUILD=0`` to forbid the on-import build).
 
 Exports: ``MessageCodec``, ``Ingest``, ``Delivery``, ``Settler``, ``Counter``,
 ``Histogram``, ``frame``, ``frames``, ``mono_ns`` and :func:`codec_for`, which
-derives a native codec from a runtime protobuf descriptor.
+derives a native codec from a runtime protobuf descriptor. Bench and diagnostic
+natives are a separate module (:mod:`beholder_amd.ops.bench_native`).
 """
 from __future__ import annotations
 
@@ -77,15 +78,11 @@ if os.environ.get("BEHOLDER_NATIVE_IO", "1") == "0":  # all native I/O off: plai
         reject = _asyncio.Future.set_exception
 AckBatcher = native.AckBatcher
 SinkStats = native.SinkStats
-Recorder = native.Recorder
 NativeHandlers = native.NativeHandlers
 dispatch_batch = native.dispatch_batch
 frame = native.frame
 frames = native.frames
 mono_ns = native.mono_ns
-paced_write = native.paced_write
-calib = native.calib
-calib_mem = native.calib_mem
 format_line = native.format_line
 quick_format = native.quick_format
 js_str = native.js_str
@@ -151,8 +148,8 @@ def codec_for(ptype, dialect: str = "upb") -> Optional[object]:
 
 
 __all__ = [
-    "native", "NativeHandlers", "SinkStats", "Recorder", "AckBatcher", "AmqpDemux", "Driver", "Window", "IOFuture", "H1Parser", "PgReader", "MessageCodec", "Ingest", "Delivery", "Settler", "Counter", "Histogram",
-    "frame", "frames", "mono_ns", "paced_write", "calib", "calib_mem", "codec_for", "field_table", "format_line", "quick_format", "js_str",
+    "native", "NativeHandlers", "SinkStats", "AckBatcher", "AmqpDemux", "Driver", "Window", "IOFuture", "H1Parser", "PgReader", "MessageCodec", "Ingest", "Delivery", "Settler", "Counter", "Histogram",
+    "frame", "frames", "mono_ns", "codec_for", "field_table", "format_line", "quick_format", "js_str",
     "js_number", "encode_query", "quote_component",
 ]
 

@@ -2,18 +2,30 @@
 //
 // Contents: MessageCodec (protobuf decode/encode), Ingest (byte ring + reader
 // thread), Delivery / Settler (ack semantics + latency), Counter / Histogram
-// (metrics), plus framing helpers. See the per-file headers for the mapping
+// (metrics), plus framing helpers. Bench and diagnostic code (the sink stub, the
+// paced producer, calibration loops, the sampling profiler) is not linked here: it
+// is `_native_bench` (csrc_bench/), which reaches this module through `_C_API`. See the per-file headers for the mapping
 // to reference behaviour (/root/reference/index.js).
 #include <cstdlib>
 #include <string>
 #include <vector>
 
+#include "native_api.hpp"
 #include "py_common.hpp"
 #include "ring.hpp"
 
 namespace beholder {
 
 ModuleState g_state = {nullptr, nullptr};
+
+PyObject* url_with_query(PyObject* url, PyObject* params);  // py_text.cpp
+int api_h1_request_text(PyObject* method, PyObject* url, PyObject* params, PyObject* host, PyObject* auth,
+                        PyObject* tail, PyObject* tail_cl0, std::string* req, PyObject** full,
+                        Py_ssize_t* key_len);  // py_h1call.cpp
+PyObject* api_h1_response(PyObject* parsed, PyObject* full);  // py_h1call.cpp
+int api_h1_origin_key(PyObject* method, PyObject* url, PyObject* params, Py_ssize_t* key_len);  // py_h1call.cpp
+
+const NativeApi g_api = {kNativeApiAbi, api_h1_origin_key, api_h1_request_text, api_h1_response, url_with_query};
 
 namespace {
 
@@ -102,86 +114,6 @@ PyObject* mod_frames_impl(PyObject*, PyObject* it_in) {
   return PyBytes_FromStringAndSize(out.data(), Py_ssize_t(out.size()));
 }
 
-// calib(iters) -> ns: a fixed amount of integer work (xorshift mixing through a
-// 16 KiB, L1-resident table; a dependent chain, so neither vectorised nor
-// removable). Its time moves only with the core's clock and with other load on
-// the core, never with this service's code, so the bench line can tell a slow
-// box from a slow build. Runs without the GIL.
-PyObject* mod_calib(PyObject*, PyObject* args) {
-  unsigned long long iters;
-  if (!PyArg_ParseTuple(args, "K", &iters)) return nullptr;
-  int64_t t0, t1;
-  uint64_t acc;
-  Py_BEGIN_ALLOW_THREADS
-  uint32_t table[4096];
-  uint64_t x = 0x9E3779B97F4A7C15ull;
-  for (uint32_t i = 0; i < 4096; ++i) {
-    x ^= x << 13;
-    x ^= x >> 7;
-    x ^= x << 17;
-    table[i] = uint32_t(x);
-  }
-  t0 = mono_ns();
-  acc = 0;
-  for (unsigned long long i = 0; i < iters; ++i) {
-    x ^= x << 13;
-    x ^= x >> 7;
-    x ^= x << 17;
-    uint32_t v = table[(x ^ acc) & 4095];
-    acc = (acc * 31) + v;
-    table[acc & 4095] = v ^ uint32_t(i);
-  }
-  t1 = mono_ns();
-  Py_END_ALLOW_THREADS
-  return Py_BuildValue("(LK)", (long long)(t1 - t0), (unsigned long long)acc);
-}
-
-// calib_mem(bytes, steps) -> (ns, checksum): a dependent random walk over `bytes` of cache lines
-// (one random cycle through every line, Sattolo's shuffle). With 16 MiB it lives in the L3 a
-// core shares with its CCD neighbours, so its time moves with other tenants' cache and memory
-// traffic -- which an L1-resident loop (calib) cannot see and a Python consumer, whose objects
-// are scattered over the heap, does. Setup is outside the timed region; runs without the GIL.
-PyObject* mod_calib_mem(PyObject*, PyObject* args) {
-  unsigned long long bytes, steps;
-  if (!PyArg_ParseTuple(args, "KK", &bytes, &steps)) return nullptr;
-  const size_t lines = size_t(bytes / 64);
-  if (lines < 2 || lines > (size_t(1) << 26)) {
-    PyErr_SetString(PyExc_ValueError, "calib_mem: bytes must be in [128, 4 GiB]");
-    return nullptr;
-  }
-  uint64_t* a = static_cast<uint64_t*>(std::aligned_alloc(64, lines * 64));
-  if (!a) return PyErr_NoMemory();
-  std::vector<uint32_t> perm;
-  try {
-    perm.resize(lines);
-  } catch (const std::bad_alloc&) {
-    std::free(a);
-    return PyErr_NoMemory();
-  }
-  int64_t t0, t1;
-  uint64_t idx = 0;
-  Py_BEGIN_ALLOW_THREADS
-  for (size_t i = 0; i < lines; ++i) perm[i] = uint32_t(i);
-  uint64_t x = 0x2545F4914F6CDD1Dull;
-  for (size_t i = lines - 1; i > 0; --i) {  // Sattolo: a single cycle through every line
-    x ^= x << 13;
-    x ^= x >> 7;
-    x ^= x << 17;
-    size_t j = size_t(x % i);
-    uint32_t t = perm[i];
-    perm[i] = perm[j];
-    perm[j] = t;
-  }
-  for (size_t i = 0; i < lines; ++i) a[size_t(i) * 8] = perm[i];
-  for (size_t i = 0; i < lines; ++i) idx = a[idx * 8];  // one warm lap
-  t0 = mono_ns();
-  for (unsigned long long s = 0; s < steps; ++s) idx = a[idx * 8];
-  t1 = mono_ns();
-  Py_END_ALLOW_THREADS
-  std::free(a);
-  return Py_BuildValue("(LK)", (long long)(t1 - t0), (unsigned long long)idx);
-}
-
 // untrack_row(row) -> row (store/base.py): a NamedTuple row of atoms leaves the cyclic collector.
 PyObject* mod_untrack_row(PyObject*, PyObject* t) {
   if (!PyTuple_Check(t)) {
@@ -195,9 +127,6 @@ PyObject* mod_untrack_row(PyObject*, PyObject* t) {
 PyMethodDef module_methods[] = {
     {"untrack_row", mod_untrack_row, METH_O,
      "untrack_row(row) -> row: a tuple row holding only atoms leaves the cyclic collector"},
-    {"calib_mem", mod_calib_mem, METH_VARARGS,
-     "calib_mem(bytes, steps) -> (ns, checksum): fixed-work dependent random walk over `bytes`"},
-    {"calib", mod_calib, METH_VARARGS, "calib(iters) -> (ns, checksum): fixed-work CPU calibration loop"},
     {"configure", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(mod_configure)),
      METH_VARARGS | METH_KEYWORDS, "configure(decode_error=None, topics=None)"},
     {"mono_ns", mod_mono_ns, METH_NOARGS, "CLOCK_MONOTONIC in ns (same clock as time.monotonic_ns)"},
@@ -220,8 +149,14 @@ PyMODINIT_FUNC PyInit__native(void) {
       init_dispatch_functions(m) < 0 || init_http_types(m) < 0 ||
       init_pg_types(m) < 0 || init_driver_types(m) < 0 ||
       init_ack_types(m) < 0 || init_handler_types(m) < 0 || init_netconn_types(m) < 0 || init_h1call_types(m) < 0 ||
-      init_tls_types(m) < 0 || init_netpoll_types(m) < 0 || init_prof_functions(m) < 0 ||
-      init_recorder_types(m) < 0) {
+      init_tls_types(m) < 0 || init_netpoll_types(m) < 0) {
+    Py_DECREF(m);
+    return nullptr;
+  }
+  // the C interface for the package's other extension modules (native_api.hpp)
+  PyObject* api = PyCapsule_New(const_cast<NativeApi*>(&g_api), kNativeApiName, nullptr);
+  if (!api || PyModule_AddObject(m, "_C_API", api) < 0) {
+    Py_XDECREF(api);
     Py_DECREF(m);
     return nullptr;
   }

@@ -115,12 +115,6 @@ int init_netconn_types(PyObject* m);
 int init_h1call_types(PyObject* m);
 int init_tls_types(PyObject* m);
 int init_netpoll_types(PyObject* m);
-int init_prof_functions(PyObject* m);
-int init_recorder_types(PyObject* m);
-
-// ---- Recorder (py_recorder.cpp): the in-process sink stub's native core ----
-bool is_recorder(PyObject* o);
-PyObject* recorder_request(PyObject* rec, PyObject* method, PyObject* url, PyObject* params);
 
 // ---- Window (py_driver.cpp): the in-flight set dispatch_batch hands suspended handlers to ----
 bool is_window(PyObject* o);

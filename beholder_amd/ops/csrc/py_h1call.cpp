@@ -37,6 +37,7 @@
 #include <string>
 
 #include "py_common.hpp"
+#include "native_api.hpp"
 
 #include <structmember.h>
 
@@ -293,6 +294,24 @@ void call_dealloc(H1CallObject* s) {
   Py_TYPE(s)->tp_free(reinterpret_cast<PyObject*>(s));
 }
 
+// HttpResponse(status, body, None, full, raw) without its __init__ (slots set directly). New
+// reference, NULL on error.
+PyObject* make_response(PyObject* status, PyObject* body, PyObject* raw, PyObject* full) {
+  PyTypeObject* rt = g.resp.type;
+  if (!rt) {
+    PyErr_SetString(PyExc_RuntimeError, "h1_setup has not run (import beholder_amd.sinks.h1)");
+    return nullptr;
+  }
+  PyObject* resp = rt->tp_alloc(rt, 0);
+  if (!resp) return nullptr;
+  PyObject* vals[R_N] = {status, body, Py_None, raw, full};
+  for (int i = 0; i < R_N; ++i) {
+    Py_INCREF(vals[i]);
+    g.resp.set(resp, i, vals[i]);
+  }
+  return resp;
+}
+
 // The reply `res` arrived. 1 = finished here (*out = HttpResponse), 0 = the Python loop must
 // continue (a redirect to follow), -1 = error.
 int finish_fast(H1CallObject* s, PyObject* res, PyObject** out) {
@@ -348,15 +367,8 @@ int finish_fast(H1CallObject* s, PyObject* res, PyObject** out) {
     if (!r) return -1;
     Py_DECREF(r);
   }
-  // HttpResponse(status, body, None, full, raw)
-  PyTypeObject* rt = g.resp.type;
-  PyObject* resp = rt->tp_alloc(rt, 0);
+  PyObject* resp = make_response(status, PyTuple_GET_ITEM(res, 3), PyTuple_GET_ITEM(res, 2), s->full);
   if (!resp) return -1;
-  PyObject* vals[R_N] = {status, PyTuple_GET_ITEM(res, 3), Py_None, PyTuple_GET_ITEM(res, 2), s->full};
-  for (int i = 0; i < R_N; ++i) {
-    Py_INCREF(vals[i]);
-    g.resp.set(resp, i, vals[i]);
-  }
   *out = resp;
   return 1;
 }
@@ -645,6 +657,92 @@ int send_on(H1CallObject* s, PyObject* conn, const char* req, size_t reqlen, PyO
 int queue_start(H1CallObject* s, PyObject* client, PyObject* counts, PyObject* o, PyObject* full,
                 const std::string& req, bool head, PyObject* timeout, PyObject* timeout_s);
 
+// The shapes the native path sends (sinks/h1.py _split_url, no quoting needed): a str method
+// that is an upper-case ASCII token, an ASCII URL scheme://authority[/path][?query] with a
+// printable target and no fragment, params absent or a dict (not combined with a query already
+// in the URL). *k = length of "scheme://authority". true = send natively.
+bool split_shape(PyObject* method, PyObject* url, PyObject* params, Py_ssize_t* k_out) {
+  if (!PyUnicode_CheckExact(method) || !PyUnicode_IS_ASCII(method) || !PyUnicode_CheckExact(url) ||
+      !PyUnicode_IS_ASCII(url) || (params && !PyDict_CheckExact(params)))
+    return false;
+  Py_ssize_t mn = PyUnicode_GET_LENGTH(method);
+  const char* m = reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(method));
+  if (mn == 0) return false;
+  for (Py_ssize_t i = 0; i < mn; ++i)
+    if (m[i] < 'A' || m[i] > 'Z') return false;
+  Py_ssize_t un = PyUnicode_GET_LENGTH(url);
+  const char* u = reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(url));
+  Py_ssize_t i = 0;
+  while (i + 2 < un && !(u[i] == ':' && u[i + 1] == '/' && u[i + 2] == '/')) ++i;
+  if (i == 0 || i + 2 >= un) return false;
+  Py_ssize_t k = i + 3;
+  while (k < un && u[k] != '/' && u[k] != '?' && u[k] != '#') ++k;
+  bool has_q = false;
+  for (Py_ssize_t j = k; j < un; ++j) {
+    unsigned char ch = static_cast<unsigned char>(u[j]);
+    if (ch < 0x21 || ch > 0x7E || ch == '#') return false;  // _resolve would quote it
+    if (ch == '?') has_q = true;
+  }
+  if (params && has_q && PyDict_GET_SIZE(params)) return false;  // with_query appends with '&'
+  *k_out = k;
+  return true;
+}
+
+// The request text for a URL that passed split_shape, on an origin whose Host header is `host`
+// and Authorization `auth` (str or None): "M target HTTP/1.1\r\nHost: h\r\n[Authorization:
+// a\r\n]" + the User-Agent tail (`tail_cl0` for methods with a body). `q` = the encoded query.
+// false = not the native shape (a non-ASCII host, a query value the encoder refuses).
+bool request_text(PyObject* method, PyObject* url, Py_ssize_t k, PyObject* params, PyObject* host, PyObject* auth,
+                  PyObject* tail, PyObject* tail_cl0, std::string& req, std::string& q) {
+  if (!PyUnicode_CheckExact(host) || !PyUnicode_IS_ASCII(host) ||
+      (auth != Py_None && (!PyUnicode_CheckExact(auth) || !PyUnicode_IS_ASCII(auth))))
+    return false;
+  Py_ssize_t mn = PyUnicode_GET_LENGTH(method);
+  const char* m = reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(method));
+  Py_ssize_t un = PyUnicode_GET_LENGTH(url);
+  const char* u = reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(url));
+  req.reserve(size_t(un) + 256);
+  req.append(m, size_t(mn));
+  req += ' ';
+  if (k == un || u[k] != '/') req += '/';
+  req.append(u + k, size_t(un - k));
+  if (params && PyDict_GET_SIZE(params)) {
+    Py_ssize_t pos = 0;
+    PyObject *pk, *pv;
+    bool first = true;
+    while (PyDict_Next(params, &pos, &pk, &pv)) {
+      if (!text_query_pair_append(q, pk, pv, &first, false)) {
+        PyErr_Clear();  // the Python path raises it at the await
+        return false;
+      }
+    }
+    if (!q.empty()) {
+      req += '?';
+      req += q;
+    }
+  }
+  req += " HTTP/1.1\r\nHost: ";
+  req.append(reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(host)), size_t(PyUnicode_GET_LENGTH(host)));
+  req += "\r\n";
+  if (auth != Py_None) {
+    req += "Authorization: ";
+    req.append(reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(auth)), size_t(PyUnicode_GET_LENGTH(auth)));
+    req += "\r\n";
+  }
+  PyObject* t = is_body_method(m, mn) ? tail_cl0 : tail;
+  req.append(PyBytes_AS_STRING(t), size_t(PyBytes_GET_SIZE(t)));
+  return true;
+}
+
+// `url` with its query `q` appended (new reference).
+PyObject* full_url(PyObject* url, const std::string& q) {
+  if (q.empty()) return Py_NewRef(url);
+  std::string f(reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(url)), size_t(PyUnicode_GET_LENGTH(url)));
+  f += '?';
+  f += q;
+  return PyUnicode_FromStringAndSize(f.data(), Py_ssize_t(f.size()));
+}
+
 // At the first await: send the request on an idle pooled connection. 1 = sent (s->conn, fut,
 // method, full, deadline, reused set), 0 = declined before any pool state changed (the Python
 // path runs instead and reproduces any error at its await), -1 = error.
@@ -654,12 +752,8 @@ int h1_start(H1CallObject* s) {
   PyObject* url = s->full;
   PyObject* params = s->params;
   PyObject* timeout = s->timeout;
-  // the shapes the sinks produce: str method and URL (ASCII: one byte per character, as read
-  // below), params a dict or absent; anything else takes the Python path, which raises or
-  // handles it (a Mapping that is not a dict, a non-ASCII host, a bytes method, ...)
-  if (!PyUnicode_CheckExact(method) || !PyUnicode_IS_ASCII(method) || !PyUnicode_CheckExact(url) ||
-      !PyUnicode_IS_ASCII(url) || (params && !PyDict_CheckExact(params)))
-    return 0;
+  // the shapes the sinks produce (split_shape): anything else takes the Python path, which
+  // raises or handles it (a Mapping that is not a dict, a non-ASCII host, a bytes method, ...)
   PyObject** dp = _PyObject_GetDictPtr(client);
   PyObject* d = dp ? *dp : nullptr;
   if (!d) return 0;
@@ -679,29 +773,9 @@ int h1_start(H1CallObject* s) {
       !PyBytes_CheckExact(tail) || !PyBytes_CheckExact(tail_cl0) || !PyFloat_CheckExact(keepalive))
     return 0;
 
-  // method: upper-case token
-  Py_ssize_t mn = PyUnicode_GET_LENGTH(method);
-  const char* m = reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(method));
-  if (mn == 0) return 0;
-  for (Py_ssize_t i = 0; i < mn; ++i)
-    if (m[i] < 'A' || m[i] > 'Z') return 0;
-
-  // url: scheme://authority[/path][?query], no fragment (h1.py _split_url)
-  Py_ssize_t un = PyUnicode_GET_LENGTH(url);
-  const char* u = reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(url));
-  Py_ssize_t i = 0;
-  while (i + 2 < un && !(u[i] == ':' && u[i + 1] == '/' && u[i + 2] == '/')) ++i;
-  if (i == 0 || i + 2 >= un) return 0;
-  Py_ssize_t k = i + 3;
-  while (k < un && u[k] != '/' && u[k] != '?' && u[k] != '#') ++k;
-  bool has_q = false;
-  for (Py_ssize_t j = k; j < un; ++j) {
-    unsigned char ch = static_cast<unsigned char>(u[j]);
-    if (ch < 0x21 || ch > 0x7E || ch == '#') return 0;  // _resolve would quote it
-    if (ch == '?') has_q = true;
-  }
-  if (params && has_q && PyDict_GET_SIZE(params)) return 0;  // with_query appends with '&'
-  PyObject* key = PyUnicode_FromStringAndSize(u, k);
+  Py_ssize_t k;
+  if (!split_shape(method, url, params, &k)) return 0;
+  PyObject* key = PyUnicode_FromStringAndSize(reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(url)), k);
   if (!key) return -1;
   PyObject* o = PyDict_GetItemWithError(origins, key);
   Py_DECREF(key);
@@ -713,56 +787,13 @@ int h1_start(H1CallObject* s) {
   PyObject* host = g.origin.get(o, O_HOST_HEADER);
   PyObject* auth = g.origin.get(o, O_AUTH);
   PyObject* idle = g.origin.get(o, O_IDLE);
-  if (!host || !auth || !idle || !PyUnicode_CheckExact(host) || !PyUnicode_IS_ASCII(host) ||
-      (auth != Py_None && (!PyUnicode_CheckExact(auth) || !PyUnicode_IS_ASCII(auth))))
-    return 0;
-
-  // request text: "M target HTTP/1.1\r\nHost: h\r\n[Authorization: a\r\n]" + User-Agent tail
-  std::string req;
-  req.reserve(size_t(un) + 256);
-  req.append(m, size_t(mn));
-  req += ' ';
-  if (k == un || u[k] != '/') req += '/';
-  req.append(u + k, size_t(un - k));
-  std::string q;
-  if (params && PyDict_GET_SIZE(params)) {
-    Py_ssize_t pos = 0;
-    PyObject *pk, *pv;
-    bool first = true;
-    while (PyDict_Next(params, &pos, &pk, &pv)) {
-      if (!text_query_pair_append(q, pk, pv, &first, false)) {
-        PyErr_Clear();  // the Python path raises it at the await
-        return 0;
-      }
-    }
-    if (!q.empty()) {
-      req += '?';
-      req += q;
-    }
-  }
-  req += " HTTP/1.1\r\nHost: ";
-  req.append(reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(host)), size_t(PyUnicode_GET_LENGTH(host)));
-  req += "\r\n";
-  if (auth != Py_None) {
-    req += "Authorization: ";
-    req.append(reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(auth)), size_t(PyUnicode_GET_LENGTH(auth)));
-    req += "\r\n";
-  }
-  PyObject* t = is_body_method(m, mn) ? tail_cl0 : tail;
-  req.append(PyBytes_AS_STRING(t), size_t(PyBytes_GET_SIZE(t)));
-
-  bool head = mn == 4 && memcmp(m, "HEAD", 4) == 0;
-  PyObject* full;  // the URL with its query (HttpResponse.url, error text)
-  if (q.empty()) {
-    Py_INCREF(url);
-    full = url;
-  } else {
-    std::string f(u, size_t(un));
-    f += '?';
-    f += q;
-    full = PyUnicode_FromStringAndSize(f.data(), Py_ssize_t(f.size()));
-    if (!full) return -1;
-  }
+  if (!host || !auth || !idle) return 0;
+  std::string req, q;
+  if (!request_text(method, url, k, params, host, auth, tail, tail_cl0, req, q)) return 0;
+  const char* m = reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(method));
+  bool head = PyUnicode_GET_LENGTH(method) == 4 && memcmp(m, "HEAD", 4) == 0;
+  PyObject* full = full_url(url, q);  // the URL with its query (HttpResponse.url, error text)
+  if (!full) return -1;
   Own own_full{full};
 
   // a live idle keep-alive connection on a NetConn (the Python fast path's idle pop)
@@ -1079,6 +1110,40 @@ PyObject* h1_call_new(PyObject* client, PyObject* method, PyObject* url, PyObjec
                       bool front) {
   PyObject* a[6] = {client, method, url, params, timeout, front ? Py_True : Py_False};
   return mod_h1_fast(nullptr, a, 6);
+}
+
+// ---- NativeApi entries (native_api.hpp) -------------------------------------------------------
+int api_h1_request_text(PyObject* method, PyObject* url, PyObject* params, PyObject* host, PyObject* auth,
+                        PyObject* tail, PyObject* tail_cl0, std::string* req, PyObject** full, Py_ssize_t* key_len) {
+  BEHOLDER_TRY {
+    if (params == Py_None) params = nullptr;
+    if (!PyBytes_Check(tail) || !PyBytes_Check(tail_cl0)) {
+      PyErr_SetString(PyExc_TypeError, "h1_request_text: tail and tail_cl0 must be bytes");
+      return -1;
+    }
+    Py_ssize_t k;
+    if (!split_shape(method, url, params, &k)) return 0;
+    std::string q;
+    req->clear();
+    if (!request_text(method, url, k, params, host, auth, tail, tail_cl0, *req, q)) return 0;
+    *full = full_url(url, q);
+    if (!*full) return -1;
+    *key_len = k;
+    return 1;
+  }
+  BEHOLDER_CATCH(-1)
+}
+
+int api_h1_origin_key(PyObject* method, PyObject* url, PyObject* params, Py_ssize_t* key_len) {
+  return split_shape(method, url, params == Py_None ? nullptr : params, key_len) ? 1 : 0;
+}
+
+PyObject* api_h1_response(PyObject* parsed, PyObject* full) {
+  if (!PyTuple_CheckExact(parsed) || PyTuple_GET_SIZE(parsed) != 5) {
+    PyErr_SetString(PyExc_TypeError, "h1_response: expected an H1Parser result tuple");
+    return nullptr;
+  }
+  return make_response(PyTuple_GET_ITEM(parsed, 0), PyTuple_GET_ITEM(parsed, 3), PyTuple_GET_ITEM(parsed, 2), full);
 }
 
 namespace {

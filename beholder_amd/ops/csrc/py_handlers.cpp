@@ -23,6 +23,7 @@
 #include <string>
 #include <vector>
 
+#include "native_api.hpp"
 #include "py_common.hpp"
 #include "ring.hpp"
 
@@ -558,9 +559,17 @@ PyObject* http_request(CallObject* c, PyObject* http, PyObject* method, PyObject
   count_request(c);
   PyObject** dp = _PyObject_GetDictPtr(http);
   PyObject* rec = dp && *dp ? PyDict_GetItemWithError(*dp, s_native_record) : nullptr;
-  if (rec && is_recorder(rec)) {  // the in-process stub (sinks/http.py RecordingHttpClient)
-    Py_INCREF(rec);  // borrowed from the client's dict; held while it records
-    PyObject* r = recorder_request(rec, method, url, params ? params : Py_None);
+  if (rec && PyCapsule_CheckExact(rec) && PyCapsule_IsValid(rec, kSinkHookName)) {
+    // a client with a native sink hook (native_api.hpp; the in-process stub of the benches and
+    // tests, sinks/http.py RecordingHttpClient): its request, without its coroutine
+    const SinkHook* hook = static_cast<const SinkHook*>(PyCapsule_GetPointer(rec, kSinkHookName));
+    PyObject* self = static_cast<PyObject*>(PyCapsule_GetContext(rec));
+    if (!hook || !self || hook->abi != kSinkHookAbi) {
+      if (!PyErr_Occurred()) PyErr_SetString(PyExc_RuntimeError, "native_record: incompatible sink hook");
+      return nullptr;
+    }
+    Py_INCREF(rec);  // borrowed from the client's dict; held (with its context) while it runs
+    PyObject* r = hook->request(self, method, url, params ? params : Py_None);
     Py_DECREF(rec);
     return r;
   }

@@ -1,5 +1,6 @@
 // In-process sampling CPU profiler (native-level), for the per-event cost work on hosts without
-// `perf` (neither this build container nor the MI355X boxes have it).
+// `perf` (neither this build container nor the MI355X boxes have it). Part of `_native_bench`:
+// diagnostic code, not linked into the service's extension.
 //
 // prof_start(hz): ITIMER_PROF fires every 1/hz s of process CPU time; the kernel delivers SIGPROF
 // to a thread that is running, whose handler stores the interrupted instruction pointer (and the
@@ -19,7 +20,7 @@
 #include <cstdint>
 #include <cstdlib>
 
-#include "py_common.hpp"
+#include "bench_common.hpp"
 
 namespace beholder {
 namespace {
@@ -124,6 +125,6 @@ PyMethodDef prof_methods[] = {
 
 }  // namespace
 
-int init_prof_functions(PyObject* m) { return PyModule_AddFunctions(m, prof_methods); }
+int init_bench_prof(PyObject* m) { return PyModule_AddFunctions(m, prof_methods); }
 
 }  // namespace beholder

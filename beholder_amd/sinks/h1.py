@@ -938,8 +938,11 @@ def _tls_error(reason: str, message: str, verify: bool) -> _ssl.SSLError:
 # Native fast path of H1Client.request (ops/csrc/py_h1call.cpp), handed to each client as its
 # `native_call` capability. With BEHOLDER_NATIVE_IO=0 (replies on plain asyncio futures) every
 # request takes the Python path.
+# (The classes are registered either way: the in-process sink stub builds its responses with the
+# same native code, ops/csrc_bench/recorder.cpp.)
+_native.h1_setup(H1Client, _Conn, _Origin, HttpResponse)
 if _IOFuture is _native.IOFuture:
-    _native.h1_setup(H1Client, _Conn, _Origin, HttpResponse)
     _NATIVE_CALL = _native.h1_fast
 else:
+    _native.h1_disable()
     _NATIVE_CALL = None

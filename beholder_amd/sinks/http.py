@@ -212,6 +212,11 @@ class AiohttpClient(HttpClient):
 Rule = Tuple[str, str, Callable[[str, str], Any]]
 
 
+# The canned answer of the in-process stub: what the bench's HTTP fake sends
+# (bench/http_sink_server.py), parsed per request like a real reply.
+STUB_RESPONSE = b"HTTP/1.1 200 OK\r\nContent-Type: application/json; charset=utf-8\r\nContent-Length: 2\r\n\r\n{}"
+
+
 class RecordingHttpClient(HttpClient):
     """In-process fake: records every request and answers from rules.
 
@@ -221,17 +226,31 @@ class RecordingHttpClient(HttpClient):
     total count is always exact), so benches can use it as a null sink.
     ``delay_s`` simulates network latency (forces a real suspension).
 
-    Counting, URL building and the call log are native (``ops Recorder``). While the client has
-    no rules and no delay it also exposes that core as ``native_record``: the compiled handlers
-    then record and get their ``200 {}`` without entering this class's coroutine, the way they
-    use the H1 client's native request path in production (``H1Client.native_call``).
+    Its core is native and lives in the bench/test extension (``ops.bench_native.Recorder``,
+    ops/csrc_bench/recorder.cpp), not in the service's: per request it builds the request bytes
+    with the H1 client's own builder, parses the canned ``200 {}`` with an ``H1Parser`` and
+    answers with the H1 client's ``HttpResponse`` (the production client's per-request work,
+    minus the socket). While the client has no rules and no delay it exposes that core as
+    ``native_record`` (a sink-hook capsule, ops/csrc/native_api.hpp): the compiled handlers then
+    call it without entering this class's coroutine, the way they use the H1 client's native
+    request path in production (``H1Client.native_call``). ``stub="url"`` is the round-4 stub
+    (URL + log only), kept for the A/B of the two (profiles/box_r5_stub_ab/).
     """
 
-    def __init__(self, keep: Optional[int] = None, delay_s: float = 0.0):
+    def __init__(self, keep: Optional[int] = None, delay_s: float = 0.0, stub: str = "h1"):
+        from ..ops.bench_native import Recorder
+        from .h1 import H1Client
         self.calls: Deque[Tuple[str, str]] = collections.deque(maxlen=keep)
         self._rules: Tuple[Rule, ...] = ()
         self._ok = HttpResponse(200, b"{}", None, "")
-        self._rec = _native_ops.Recorder(self.calls, self._ok)
+        shape = H1Client()  # never connects: its origins give Host / Authorization, its tails the User-Agent
+
+        def origin(key: str):
+            o = shape._origin(key)
+            return o.host_header, o.auth
+        self._rec = Recorder(self.calls, self._ok, _native_ops.H1Parser(), STUB_RESPONSE, origin, shape._tail,
+                             shape._tail_cl0, mode=stub)
+        self._hook = self._rec.hook
         self.delay_s = delay_s  # (sets native_record)
 
     @property
@@ -247,7 +266,7 @@ class RecordingHttpClient(HttpClient):
         """Expose the native core to the compiled handlers only while every answer is the plain
         ``200 {}`` with no delay, and no subclass overrides request() (jitter, counting)."""
         plain = type(self).request is RecordingHttpClient.request
-        self.native_record = self._rec if plain and not self._delay_s and not self._rules else None
+        self.native_record = self._hook if plain and not self._delay_s and not self._rules else None
 
     @property
     def count(self) -> int:

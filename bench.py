@@ -11,10 +11,12 @@ protobuf-encoded, framed) pushed through the **whole** service path of the consu
       -> native protobuf decode -> handler logic (index.js:62-155)
       -> media store (in-memory, 10k rows) -> Prometheus counters
       -> Trello/Telegram/Emby request construction (URL + query encoding)
-         into an in-process HTTP recorder (no network; its counting, URL building
-         and call log are native, ops/csrc/py_recorder.cpp, and the compiled
-         handlers call it directly, as they call the H1 client's native path
-         in production)
+         into an in-process HTTP stub that does the production client's
+         per-request work minus the socket: the request bytes from the H1
+         client's own builder, a canned `200 {}` through an H1Parser, the H1
+         client's HttpResponse (ops/csrc_bench/recorder.cpp, in the bench
+         extension; the compiled handlers call it through its sink hook, as they
+         call the H1 client's native path in production)
       -> pino JSON log line per reference log call (info level, to /dev/null)
       -> ack (latency recorded natively)
 
@@ -83,6 +85,10 @@ if ROOT not in sys.path:
 from beholder_amd.utils.hostinfo import available_cpus, cpu_share, default_procs, gpus_on_node  # noqa: E402
 
 BASELINE_METRIC = "metric_events_ingested_per_sec"
+# the headline's sink stub (sinks/http.py RecordingHttpClient): "h1" builds every request's bytes
+# with the H1 client's builder and parses a canned `200 {}` per request (production's per-request
+# work minus the socket); "url" is round 4's URL-only stub, for the A/B of the two
+STUB = os.environ.get("BEHOLDER_BENCH_STUB", "h1")
 
 
 def parse(argv=None):
@@ -224,7 +230,7 @@ async def run_consumer(a, seed: int, go, stop=None, *, steps: int = None, warmup
     cfg_d["service"]["ordering"] = a.ordering
     cfg = Config.from_dict(cfg_d)
     log_sink = open(os.devnull, "w", buffering=1 << 16)
-    http = RecordingHttpClient(keep=16)
+    http = RecordingHttpClient(keep=16, stub=STUB)
     svc = Service(cfg, source=FdSource(fd=rfd, batch=512), store=MemoryStore(w.media), http=http,
                   logger=Logger(stream=log_sink, level=a.log_level), serve_metrics=False)
     await svc.init()
@@ -499,7 +505,7 @@ def _paced(prefix: str, r: dict) -> dict:
 
 def paced_extras(a) -> dict:
     """BASELINE configs 2-4 (paced producers) and the unpaced overload, in this process. The
-    producer is native and GIL-free (ops.paced_write); these run before the headline initialises
+    producer is native and GIL-free (ops.bench_native.paced_write); these run before the headline initialises
     HIP, so nothing but the consumer and its reader thread competes for this process."""
     from beholder_amd.bench import harness
     from beholder_amd.bench.generator import Workload
@@ -594,7 +600,7 @@ def _thp_mode():
 
 
 def calibrate() -> dict:
-    from beholder_amd.ops import calib, calib_mem
+    from beholder_amd.ops.bench_native import calib, calib_mem
     return {"calib_ns": min(calib(CALIB_ITERS)[0] for _ in range(CALIB_REPS)),
             "calib_mem_ns": min(calib_mem(CALIB_MEM_BYTES, CALIB_MEM_STEPS)[0] for _ in range(CALIB_REPS)),
             "calib_py_ns": min(_calib_py_once() for _ in range(CALIB_REPS))}
@@ -625,8 +631,10 @@ def _finite(x):
 
 
 DATA = ("synthetic telemetry (90% progress / 10% status), 10k-media in-memory store, "
-        "Trello/Telegram/Emby stubbed in-process (native recorder: URL + query built and logged "
-        "per request), info logs to /dev/null")
+        "Trello/Telegram/Emby stubbed in-process (" + ("h1 stub: each request's bytes built by the H1 client's "
+                                                      "builder, a canned 200 parsed by H1Parser into its HttpResponse"
+                                                      if STUB == "h1" else "url stub: URL + query built and logged")
+        + "; no socket), info logs to /dev/null")
 
 NOTES = ("CPU event-consumer workload (the reference has no device compute; see docs/DESIGN.md). "
          "value = one consumer process per rank; all_procs_* = every CPU of the share busy; "

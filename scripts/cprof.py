@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Native-level flat CPU profile of the headline consumer (no `perf` on these hosts).
 
-Samples instruction pointers with the extension's SIGPROF sampler (``ops/csrc/py_prof.cpp``)
+Samples instruction pointers with the bench extension's SIGPROF sampler (``ops/csrc_bench/prof.cpp``)
 while one consumer runs the bench's timed steps (``bench.run_consumer``), then resolves every
 sample to ``object:function`` through ``/proc/self/maps``, the objects' ELF load segments and
 their symbol tables (``nm``: our extension's full table, the interpreter's exported symbols).
@@ -108,7 +108,7 @@ def main(argv=None) -> int:
     ap.add_argument("--events", type=int, default=200_000, help="tcp_e2e / tls_e2e events")
     a = ap.parse_args(argv)
     import bench
-    from beholder_amd.ops import native
+    from beholder_amd.ops import bench_native as native
 
     ba = bench.parse(["--steps", str(a.steps), "--warmup", str(a.warmup), "--no-extras"])
     main_tid = threading.get_native_id()

@@ -220,7 +220,7 @@ def test_idle_fdsource_uses_no_executor_thread():
 def test_paced_write_rate_and_order():
     from array import array
 
-    from beholder_amd.ops import paced_write
+    from beholder_amd.ops.bench_native import paced_write
     chunks = [frame(i % 2, b"x%03d" % i) for i in range(200)]
     ends = array("Q")
     pos = 0

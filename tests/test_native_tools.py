@@ -1,5 +1,6 @@
-"""Round-4 native tools: the SIGPROF sampler (scripts/cprof.py), the fixed-work calibrations
-(bench.py calib_*), and the recorder core behind the in-process sink stub."""
+"""Bench and diagnostic natives (``_native_bench``, ops/csrc_bench/): the SIGPROF sampler
+(scripts/cprof.py), the fixed-work calibrations (bench.py calib_*), and the recorder core behind
+the in-process sink stub. None of it is in the service's extension."""
 import asyncio
 import collections
 import threading
@@ -7,7 +8,29 @@ import threading
 import pytest
 
 from beholder_amd import ops
-from beholder_amd.ops import native
+from beholder_amd.ops import bench_native
+from beholder_amd.ops import bench_native as native
+
+
+def test_service_extension_has_no_bench_or_profiler_code():
+    for name in ("Recorder", "Ready", "prof_start", "prof_stop", "calib", "calib_mem", "paced_write"):
+        assert not hasattr(ops.native, name), name
+        assert not hasattr(ops, name), name
+        if name != "Ready":
+            assert hasattr(bench_native, name), name
+    assert "_native_bench" not in ops.native.__file__ and ops.native._C_API is not None
+
+
+def _recorder(calls, mode="h1"):
+    from beholder_amd.sinks.h1 import H1Client
+    from beholder_amd.sinks.http import STUB_RESPONSE, HttpResponse
+    shape = H1Client()
+
+    def origin(key):
+        o = shape._origin(key)
+        return o.host_header, o.auth
+    return bench_native.Recorder(calls, HttpResponse(200, b"{}", None, ""), ops.H1Parser(), STUB_RESPONSE, origin,
+                                 shape._tail, shape._tail_cl0, mode=mode)
 
 
 def test_sampler_collects_main_thread_samples_and_stops_cleanly():
@@ -31,20 +54,19 @@ def test_sampler_collects_main_thread_samples_and_stops_cleanly():
 
 
 def test_calibrations_are_fixed_work():
-    ns1, c1 = ops.calib(200_000)
-    ns2, c2 = ops.calib(200_000)
+    ns1, c1 = bench_native.calib(200_000)
+    ns2, c2 = bench_native.calib(200_000)
     assert c1 == c2 and ns1 > 0 and ns2 > 0  # same work, same checksum
-    m1, k1 = ops.calib_mem(1 << 20, 50_000)
-    m2, k2 = ops.calib_mem(1 << 20, 50_000)
+    m1, k1 = bench_native.calib_mem(1 << 20, 50_000)
+    m2, k2 = bench_native.calib_mem(1 << 20, 50_000)
     assert k1 == k2 and m1 > 0
     with pytest.raises(ValueError):
-        ops.calib_mem(64, 10)
+        bench_native.calib_mem(64, 10)
 
 
 def test_recorder_core_builds_urls_like_restler_and_counts():
     calls = collections.deque(maxlen=2)
-    ok = object()
-    rec = ops.Recorder(calls, ok)
+    rec = _recorder(calls)
     assert rec.record("POST", "https://t/1/cards/a?b/actions", {"key": "k", "token": None, "text": "a b"}) == \
         "https://t/1/cards/a?b/actions?key=k&text=a%20b"  # "?" even after a "?", None dropped
     assert rec.record("GET", "https://x/y?q=1", None) == "https://x/y?q=1"
@@ -87,3 +109,47 @@ def test_recording_client_fast_path_follows_a_later_delay():
     assert c.native_record is None
     c.delay_s = 0.0
     assert c.native_record is not None
+
+
+def test_stub_request_bytes_are_the_h1_clients():
+    """The stub builds each request with the H1 client's own builder: the bytes its native path
+    writes to the socket (request line with the encodeURIComponent query, Host, Authorization
+    from the URL's userinfo, User-Agent, Content-Length: 0 for a PUT/POST)."""
+    rec = _recorder(collections.deque())
+    rec.record("PUT", "https://api.trello.com/1/cards/c1/idList", {"key": "k", "token": "t", "value": "l 2"})
+    assert rec.last_request == (b"PUT /1/cards/c1/idList?key=k&token=t&value=l%202 HTTP/1.1\r\n"
+                                b"Host: api.trello.com\r\nUser-Agent: beholder/1.0\r\nContent-Length: 0\r\n\r\n")
+    rec.record("GET", "http://u:p%40ss@emby:8096/Library/Refresh?api_key=x", None)
+    assert rec.last_request == (b"GET /Library/Refresh?api_key=x HTTP/1.1\r\nHost: emby:8096\r\n"
+                                b"Authorization: Basic dTpwQHNz\r\nUser-Agent: beholder/1.0\r\n\r\n")
+    assert rec.built == 2 and rec.count == 2 and rec.bytes_out > 200
+
+
+def test_stub_answers_with_a_parsed_response_carrying_the_url():
+    """Each answer is the canned bytes through an H1Parser and the H1 client's HttpResponse, with
+    the request's own URL (round 4's fast path shared one response whose url was "")."""
+    from beholder_amd.sinks.http import HttpResponse
+    rec = _recorder(collections.deque())
+
+    async def go():
+        a = await rec.request("POST", "https://api.trello.com/1/cards/c/actions/comments", {"key": "k", "text": "hi"})
+        b = await rec.request("GET", "https://api.telegram.org/botT/sendMessage?chat_id=1", None)
+        return a, b
+    a, b = asyncio.run(go())
+    assert type(a) is HttpResponse and a is not b
+    assert a.status == 200 and a.body == b"{}" and a.headers["content-length"] == "2"
+    assert a.url == "https://api.trello.com/1/cards/c/actions/comments?key=k&text=hi"
+    assert b.url == "https://api.telegram.org/botT/sendMessage?chat_id=1"
+    old = _recorder(collections.deque(), mode="url")  # the round-4 arm of the A/B
+
+    async def go_old():
+        return await old.request("GET", "https://x/y", {"a": 1})
+    assert asyncio.run(go_old()).url == "" and old.built == 0 and old.count == 1
+
+
+def test_recording_client_exposes_a_sink_hook_capsule():
+    from beholder_amd.sinks import RecordingHttpClient
+    c = RecordingHttpClient()
+    assert type(c.native_record).__name__ == "PyCapsule" and "beholder_amd.sink_hook" in repr(c.native_record)
+    with pytest.raises(ValueError):
+        RecordingHttpClient(stub="nope")

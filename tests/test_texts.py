@@ -44,7 +44,7 @@ ALLOWED_IDENTIFIERS = {
 }
 # internal errors and docstrings (Python-level diagnostics, never emitted by the reference)
 ALLOWED_MESSAGES = {
-    "HandlerCall: bad state",
+    "HandlerCall: bad state", "native_api.hpp", "native_record: incompatible sink hook",
     "NativeHandlers(handlers): the status / progress handlers compiled to native state machines",
     "TelegramClient.base_url missing", "TrelloClient attributes missing", "_hooks_plan() must return a 6-tuple",
     "calls finished without / after suspending", "can't send non-None value to a just-started handler call",
