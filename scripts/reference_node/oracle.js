@@ -16,7 +16,8 @@
 //
 // scenario.json: {config, media: [{id,name,creator,creatorId,metadataId,status}],
 //   events: [["status"|"progress", hexBody]], faults: [{method, prefix, status|null, message, body}],
-//   positionalArgs: "append"|"drop", notFound: "media {id} not found", logLevel: "info"}
+//   positionalArgs: "append"|"drop", notFound: "media {id} not found", logLevel: "info",
+//   races: {mediaId: status} (the status another writer leaves in the row after each updateStatus)}
 // NO_TRELLO comes from the environment, as in the reference (index.js:70).
 // Events are delivered one at a time and each listener's promise is awaited before the next
 // (the Python side does the same), so traces are deterministic.
@@ -49,6 +50,7 @@ const h = global.__beholderHarness = {
   logLevel: sc.logLevel || 'info',
   positionalArgs: sc.positionalArgs || 'append',
   notFound: sc.notFound,
+  races: sc.races || {},
   logSink: {
     write (s) {
       for (const line of s.split('\n')) {

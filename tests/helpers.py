@@ -64,10 +64,10 @@ class Rig:
     """Handlers wired to an in-memory store, a recording HTTP client and a captured log."""
 
     def __init__(self, config: Optional[Config] = None, medias=(), no_trello: Optional[bool] = None,
-                 http: Optional[RecordingHttpClient] = None, positional_args: str = "append"):
+                 http: Optional[RecordingHttpClient] = None, positional_args: str = "append", store=None):
         self.config = config or cfg()
         self.http = http or RecordingHttpClient()
-        self.store = MemoryStore(list(medias))
+        self.store = store if store is not None else MemoryStore(list(medias))
         self.stream = MemoryStream()
         self.log = Logger(stream=self.stream, positional_args=positional_args)
         self.registry = Registry()

@@ -12,8 +12,12 @@ A scenario (:func:`make_scenario`) is a seeded random config, media table, sink-
 event stream. The streams are built to reach every branch of index.js:50-155, malformed bodies
 included (truncated fields, wrong wire types, unknown fields and groups, invalid UTF-8, field
 number 0). Modes: ``base``, ``no_trello`` (NO_TRELLO set, index.js:70), ``faults`` (transport
-errors and non-2xx answers from Trello, Telegram and Emby, index.js:92-122) and ``drop``
-(``positional_args: drop``, pino@5's exact message text, quirk Q11).
+errors and non-2xx answers from Trello, Telegram and Emby, index.js:92-122), ``drop``
+(``positional_args: drop``, pino@5's exact message text, quirk Q11) and ``reread`` (another writer
+updates chosen rows between the listener's ``updateStatus`` and its ``getByID``, index.js:68,76:
+the re-read status differs from the message's, so a handler that keys the hooks off the message's
+status instead of the row's, quirk Q3 at index.js:94, or the list off the row's instead of the
+message's, index.js:74-80, diverges from the reference).
 
 What the stand-ins assume is listed in their headers. The ones that touch this comparison:
 ``triton-core/db`` (not vendored) rejects ``getByID`` of an unknown id with the text in
@@ -46,14 +50,14 @@ from beholder_amd.config import Config  # noqa: E402
 from beholder_amd.models import proto  # noqa: E402
 from beholder_amd.ops import codec_for  # noqa: E402
 from beholder_amd.sinks import RecordingHttpClient  # noqa: E402
-from beholder_amd.store import Media  # noqa: E402
+from beholder_amd.store import Media, MemoryStore  # noqa: E402
 
 REFERENCE_INDEX = os.environ.get("BEHOLDER_REFERENCE_INDEX", "/root/reference/index.js")
 ORACLE_JS = os.path.join(ROOT, "scripts", "reference_node", "oracle.js")
 STUBS = os.path.join(ROOT, "scripts", "reference_node", "stubs")
 NODE = shutil.which("node")
 NOT_FOUND = "media {id} not found"  # beholder_amd.store.base.MediaNotFound's text
-MODES = ("base", "no_trello", "faults", "drop")
+MODES = ("base", "no_trello", "faults", "drop", "reread")
 
 _S = codec_for(proto.load("api.TelemetryStatus"))
 _P = codec_for(proto.load("api.TelemetryProgress"))
@@ -159,6 +163,17 @@ def make_scenario(seed: int, n_events: int = 520, mode: str = "base") -> dict:
                  "message": rng.choice(["ECONNREFUSED", "socket hang up"]),
                  "body": rng.choice(['"error"', '{"ok":false,"description":"Bad Request: chat not found é"}'])}
             faults.append(f)
+    races: Dict[str, int] = {}
+    if mode == "reread":
+        # both hooks on; half the rows end DEPLOYED whatever the message said, the other half end
+        # in another status even after a DEPLOYED message
+        config["keys"]["telegram"] = {"token": "123:TG"}
+        config["keys"]["emby"] = {"token": "EMBYKEY"}
+        config["instance"]["telegram"] = {"enabled": True, "channel": "-1001"}
+        config["instance"]["emby"] = {"enabled": True, "host": "http://emby:8096"}
+        for m in media:
+            if rng.random() < 0.7:
+                races[m["id"]] = 4 if rng.random() < 0.5 else rng.choice([0, 1, 2, 3, 5])
     msg_ids = ids + ["missing", "m1", "m1", "m2"]
     events = []
     for _ in range(n_events):
@@ -175,7 +190,7 @@ def make_scenario(seed: int, n_events: int = 520, mode: str = "base") -> dict:
             events.append(["progress", _P.encode((mid, st, prog, host)).hex()])
     return {"seed": seed, "mode": mode, "config": config, "media": media, "events": events, "faults": faults,
             "positionalArgs": "drop" if mode == "drop" else "append", "notFound": NOT_FOUND, "logLevel": "info",
-            "noTrello": mode == "no_trello"}
+            "noTrello": mode == "no_trello", "races": races}
 
 
 def bench_scenario(n_events: int, seed: int = 0) -> dict:
@@ -230,6 +245,22 @@ def _counter_hashes(counter, label_names) -> list:
     return sorted(out)
 
 
+class RacingStore(MemoryStore):
+    """The ``reread`` scenarios' media table: after each ``update_status`` of a row in ``races``,
+    another writer's UPDATE leaves ``races[id]`` in it before the handler's ``get_by_id``
+    (the Node stand-in, stubs/triton-core/db.js, does the same)."""
+
+    def __init__(self, medias, races: Dict[str, int]):
+        super().__init__(medias)
+        self.races = dict(races)
+
+    def update_status_nowait(self, media_id: str, status: int) -> None:
+        super().update_status_nowait(media_id, status)
+        row = self._rows.get(media_id)
+        if row is not None and media_id in self.races:
+            self._rows[media_id] = row._replace(status=self.races[media_id])
+
+
 def run_python(sc: dict, impl: str = "python", mutate=None) -> dict:
     """This repo's handlers (``impl`` = python | native) over the same scenario."""
     import helpers
@@ -243,8 +274,9 @@ def run_python(sc: dict, impl: str = "python", mutate=None) -> dict:
                   body=f["body"].encode())
     rows = [Media(id=m["id"], name=m["name"], creator=m["creator"], creatorId=m["creatorId"],
                   metadataId=m["metadataId"], status=m["status"]) for m in sc["media"]]
+    store = RacingStore(rows, sc["races"]) if sc.get("races") else None
     rig = helpers.Rig(config=config, medias=rows, no_trello=bool(sc.get("noTrello")), http=http,
-                      positional_args=sc["positionalArgs"])
+                      positional_args=sc["positionalArgs"], store=store)
     if mutate is not None:
         mutate(rig.h)
     target = rig.h if impl == "python" else native_handlers(rig.h)
@@ -325,19 +357,44 @@ def coverage(ref: dict) -> dict:
     }
 
 
+def reread_coverage(sc: dict, ref: dict) -> dict:
+    """For a ``reread`` scenario: status events whose re-read row status differs from the message's
+    in the direction that decides the hooks (index.js:94), as the reference ran them."""
+    races = sc.get("races") or {}
+    known = {m["id"] for m in sc["media"]}
+    hooks_without_deployed_msg = hooks_skipped_on_deployed_msg = 0
+    for (topic, hexbody), ev in zip(sc["events"], ref["events"]):
+        if topic != "status" or ev["decodeError"]:
+            continue
+        try:
+            mid, st = _S.decode(bytes.fromhex(hexbody))[:2]
+        except Exception:  # noqa: BLE001
+            continue
+        if mid not in known or mid not in races:
+            continue
+        hooked = any("api.telegram.org" in u for _, u in ev["requests"])
+        if races[mid] == 4 and st != 4 and hooked:
+            hooks_without_deployed_msg += 1
+        if races[mid] != 4 and st == 4 and not hooked:
+            hooks_skipped_on_deployed_msg += 1
+    return {"hooks_without_deployed_msg": hooks_without_deployed_msg,
+            "hooks_skipped_on_deployed_msg": hooks_skipped_on_deployed_msg}
+
+
 def main(argv: Optional[List[str]] = None) -> int:
     import argparse
     ap = argparse.ArgumentParser(description="reference-executed parity gate")
     ap.add_argument("--seeds", type=int, default=5)
     ap.add_argument("--events", type=int, default=520)
     ap.add_argument("--modes", default=",".join(MODES))
+    ap.add_argument("--impls", default="python,native")
     a = ap.parse_args(argv)
     bad = 0
     for seed in range(a.seeds):
         for mode in a.modes.split(","):
             sc = make_scenario(seed, a.events, mode)
             ref = run_node(sc)
-            for impl in ("python", "native"):
+            for impl in a.impls.split(","):
                 d = diff(ref, run_python(sc, impl))
                 bad += bool(d)
                 print(f"seed {seed} {mode:9s} {impl:6s} {'OK' if not d else 'DIFF'} {coverage(ref) if not d else ''}")
