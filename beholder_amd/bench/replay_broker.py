@@ -13,12 +13,14 @@ at most ``prefetch × consumers`` un-acked deliveries in flight (RabbitMQ's
 per-consumer ``basic.qos`` summed over the channel's consumers).
 
 Run as a process: ``python -m beholder_amd.bench.replay_broker --events N --port P``
-(prints ``READY <port>`` then serves one consumer connection).
+(prints ``READY <port>`` then serves one consumer connection). ``--shared --consumers N``: any
+number of connections share the queues (:class:`SharedQueueBroker`, competing consumers).
 """
 from __future__ import annotations
 
 import argparse
 import asyncio
+import collections
 import struct
 import sys
 import time
@@ -150,11 +152,250 @@ class ReplayBroker:
             w.close()
 
 
+class SharedQueueBroker:
+    """Competing consumers on one set of queues (the reference's only scaling mode: N replicas,
+    each ``prefetch`` 100, on the same RabbitMQ queues; index.js:43,62,127).
+
+    Every connection that consumes all the queues takes deliveries from one shared queue head;
+    delivery starts once ``consumers`` connections have subscribed, so every N starts together.
+    Each connection gets the next events while its window (prefetch x its consumers) has room,
+    which is how RabbitMQ spreads a saturated queue over consumers. Delivery tags are per
+    channel; acks (single, or ``multiple`` up to a tag) are mapped back to the events they
+    settle, and every event's acks are counted: ``acked`` (events acked at least once),
+    ``dup_acks`` (acks of an event already acked), ``unknown_acks`` (tags never delivered or
+    already settled on that channel) and, at the end, ``lost`` (events never acked). A
+    connection that closes with deliveries unacked has them requeued (``redelivered``), as
+    RabbitMQ does. ``cpu_s``: this process's CPU from the first delivery to the last ack.
+    """
+
+    def __init__(self, events: List[Tuple[str, bytes]], port: int = 0, consumers: int = 1):
+        self.events = events
+        self.bodies = [body for _, body in events]
+        self._content: Dict[int, List[bytes]] = {}  # channel -> pre-encoded header + body frames
+        self.port = port
+        self.expected = max(1, consumers)
+        self.total = len(events)
+        self.cursor = 0
+        self.requeue: collections.deque = collections.deque()
+        self.ack_counts = bytearray(self.total)
+        self.acked = 0
+        self.dup_acks = 0
+        self.unknown_acks = 0
+        self.redelivered = 0
+        self.sent = 0
+        self.per_conn: List[int] = []
+        self.subscribed = 0
+        self.go = asyncio.Event()
+        self.more = asyncio.Event()  # requeued events for a waiting pump
+        self.done = asyncio.Event()
+        self.t_first: Optional[float] = None
+        self.t_done: Optional[float] = None
+        self.cpu_first = 0.0
+        self.cpu_s = 0.0
+
+    def content(self, channel: int) -> List[bytes]:
+        c = self._content.get(channel)
+        if c is None:
+            c = self._content[channel] = [wire.encode_content(channel, 60, b, None, 131072) for b in self.bodies]
+        return c
+
+    async def start(self) -> "SharedQueueBroker":
+        self.content(1)  # the consumers' first channel: encoded before READY
+        self._server = await asyncio.start_server(self._serve, "127.0.0.1", self.port)
+        self.port = self._server.sockets[0].getsockname()[1]
+        return self
+
+    def _settle(self, idx: int) -> None:
+        n = self.ack_counts[idx]
+        if n:
+            self.dup_acks += 1
+        else:
+            self.acked += 1
+            if self.acked == self.total:
+                self.t_done = time.perf_counter()
+                self.cpu_s = _cpu_now() - self.cpu_first
+                self.done.set()
+        if n < 255:
+            self.ack_counts[idx] = n + 1
+
+    def _take(self, n: int) -> List[Tuple[int, bool]]:
+        """Up to n events off the shared head: requeued ones first (redelivered)."""
+        out: List[Tuple[int, bool]] = []
+        while self.requeue and len(out) < n:
+            out.append((self.requeue.popleft(), True))
+        k = min(n - len(out), self.total - self.cursor)
+        if k > 0:
+            out.extend((i, False) for i in range(self.cursor, self.cursor + k))
+            self.cursor += k
+        return out
+
+    async def _serve(self, r: asyncio.StreamReader, w: asyncio.StreamWriter) -> None:
+        await r.readexactly(8)
+        w.write(wire.encode_method(0, "connection.start", version_major=0, version_minor=9,
+                                   server_properties={"product": "replay-shared"}, mechanisms=b"PLAIN",
+                                   locales=b"en_US"))
+        parser = wire.FrameParser(0)
+        conn = len(self.per_conn)
+        self.per_conn.append(0)
+        prefetch = 0
+        consumers: Dict[str, str] = {}
+        channel = 0
+        mhead: Dict[str, bytes] = {}
+        tags: List[int] = []      # tag - 1 -> event index
+        settled = bytearray()     # tag - 1 -> settled on this channel
+        state = {"low": 0, "open": 0}  # lowest unsettled tag - 1; deliveries not yet settled
+        room_ev = asyncio.Event()
+
+        def settle_tag(t: int) -> None:  # t: tag - 1
+            if t < 0 or t >= len(tags) or settled[t]:
+                self.unknown_acks += 1
+                return
+            settled[t] = 1
+            state["open"] -= 1
+            self._settle(tags[t])
+
+        async def pump():
+            await self.go.wait()
+            content = self.content(channel)
+            while not self.done.is_set():
+                window = prefetch * max(1, len(consumers)) if prefetch else 512
+                room = window - state["open"]
+                if room <= 0:
+                    room_ev.clear()
+                    await room_ev.wait()
+                    continue
+                batch = self._take(min(room, 512))
+                if not batch:  # the head is empty: wait for requeued events or the end
+                    self.more.clear()
+                    waiter = asyncio.ensure_future(self.more.wait())
+                    await asyncio.wait([waiter, asyncio.ensure_future(self.done.wait())],
+                                       return_when=asyncio.FIRST_COMPLETED)
+                    waiter.cancel()
+                    continue
+                if self.t_first is None:
+                    self.t_first = time.perf_counter()
+                    self.cpu_first = _cpu_now()
+                parts = []
+                for idx, redelivered in batch:
+                    q = self.events[idx][0]
+                    tags.append(idx)
+                    settled.append(0)
+                    rk = q.encode()
+                    meth = mhead[q] + struct.pack(">Q", len(tags)) + (b"\x01" if redelivered else b"\x00") + \
+                        b"\x00" + bytes([len(rk)]) + rk
+                    parts.append(struct.pack(">BHI", 1, channel, len(meth)) + meth + b"\xce")
+                    parts.append(content[idx])
+                state["open"] += len(batch)
+                self.per_conn[conn] += len(batch)
+                self.sent += len(batch)
+                self.redelivered += sum(1 for _, rd in batch if rd)
+                w.write(b"".join(parts))
+                await w.drain()
+
+        pump_task = None
+        try:
+            while True:
+                data = await r.read(1 << 17)
+                if not data:
+                    return
+                for ftype, ch, payload in parser.feed(data):
+                    if ftype != wire.FRAME_METHOD:
+                        continue
+                    cid, mid = struct.unpack_from(">HH", payload)
+                    if (cid, mid) == _ACK:
+                        tag, flags = struct.unpack_from(">QB", payload, 4)
+                        if flags & 1:  # multiple: every unsettled tag up to `tag`
+                            if tag > len(tags):
+                                self.unknown_acks += 1
+                                tag = len(tags)
+                            low = state["low"]
+                            for t in range(low, tag):
+                                if not settled[t]:
+                                    settle_tag(t)
+                        else:
+                            settle_tag(tag - 1)
+                        low = state["low"]
+                        while low < len(settled) and settled[low]:
+                            low += 1
+                        state["low"] = low
+                        room_ev.set()
+                        continue
+                    m = wire.decode_method(payload)
+                    n = m.name
+                    if n == "connection.start_ok":
+                        w.write(wire.encode_method(0, "connection.tune", channel_max=2047, frame_max=131072,
+                                                   heartbeat=0))
+                    elif n == "connection.open":
+                        w.write(wire.encode_method(0, "connection.open_ok", known_hosts=""))
+                    elif n == "channel.open":
+                        channel = ch
+                        w.write(wire.encode_method(ch, "channel.open_ok", channel_id=b""))
+                    elif n == "basic.qos":
+                        prefetch = m.prefetch_count
+                        w.write(wire.encode_method(ch, "basic.qos_ok"))
+                    elif n == "queue.declare":
+                        w.write(wire.encode_method(ch, "queue.declare_ok", queue=m.queue, message_count=0,
+                                                   consumer_count=0))
+                    elif n == "basic.consume":
+                        consumers[m.queue] = m.consumer_tag
+                        w.write(wire.encode_method(ch, "basic.consume_ok", consumer_tag=m.consumer_tag))
+                        if {q for q, _ in self.events} <= set(consumers) and pump_task is None:
+                            for q, tag in consumers.items():
+                                ct = tag.encode()
+                                mhead[q] = struct.pack(">HH", 60, 60) + bytes([len(ct)]) + ct
+                            pump_task = asyncio.ensure_future(pump())
+                            self.subscribed += 1
+                            if self.subscribed >= self.expected:
+                                self.go.set()
+                    elif n == "basic.cancel":
+                        w.write(wire.encode_method(ch, "basic.cancel_ok", consumer_tag=m.consumer_tag))
+                    elif n == "channel.close":
+                        w.write(wire.encode_method(ch, "channel.close_ok"))
+                    elif n == "connection.close":
+                        w.write(wire.encode_method(0, "connection.close_ok"))
+                        await w.drain()
+                        return
+        except (ConnectionError, asyncio.IncompleteReadError):
+            return
+        finally:
+            if pump_task is not None:
+                pump_task.cancel()
+            # unacked deliveries go back to the queue head, redelivered (RabbitMQ's requeue on close)
+            back = [tags[t] for t in range(state["low"], len(tags)) if not settled[t] and not self.ack_counts[tags[t]]]
+            if back:
+                self.requeue.extend(back)
+                self.more.set()
+            w.close()
+
+    def done_line(self) -> str:
+        lost = sum(1 for c in self.ack_counts if c == 0)
+        span = (self.t_done - self.t_first) if self.t_done and self.t_first else 0.0
+        return (f"DONE sent={self.sent} acked={self.acked} published={self.total} dup_acks={self.dup_acks} "
+                f"unknown_acks={self.unknown_acks} lost={lost} redelivered={self.redelivered} "
+                f"connections={len(self.per_conn)} per_conn={','.join(map(str, self.per_conn))} "
+                f"broker_s={span:.6f} cpu_s={self.cpu_s:.6f}")
+
+
+def _cpu_now() -> float:
+    import resource
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    return ru.ru_utime + ru.ru_stime
+
+
 async def _main(a) -> None:
     from ..topics import TOPIC_NAMES_BY_ID
     from .generator import Workload
     w = Workload(n_media=a.media, seed=a.seed)
     events = [(TOPIC_NAMES_BY_ID[t], p) for t, p in w.events(a.events)]
+    if a.shared:
+        sb = await SharedQueueBroker(events, a.port, consumers=a.consumers).start()
+        del w
+        print(f"READY {sb.port}", flush=True)
+        await sb.done.wait()
+        print(sb.done_line(), flush=True)
+        await asyncio.sleep(0.2)  # the consumers' last acks of duplicates, if any, are counted
+        print(sb.done_line().replace("DONE ", "FINAL ", 1), flush=True)
+        return
     b = await ReplayBroker(events, a.port).start()
     del w
     from .stallmon import fake_monitor
@@ -173,6 +414,10 @@ def main(argv=None) -> int:
     ap.add_argument("--media", type=int, default=10000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--port", type=int, default=0)
+    ap.add_argument("--shared", action="store_true",
+                    help="competing consumers: any number of connections share the queues (SharedQueueBroker)")
+    ap.add_argument("--consumers", type=int, default=1,
+                    help="--shared: start delivering once this many connections have subscribed")
     asyncio.run(_main(ap.parse_args(argv)))
     return 0
 

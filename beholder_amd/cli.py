@@ -33,6 +33,18 @@ def _load_fixture(path: str):
     return [Media(**r) for r in rows]
 
 
+def worker_command() -> List[str]:
+    """How ``run --workers N`` starts each worker: the interpreter and entry module this process
+    was started with (``python -m beholder_amd`` -> the same; a wrapper entry module such as the
+    bench's ``beholder_amd.bench.shared_worker`` -> that module again), then the run arguments."""
+    main = sys.modules.get("__main__")
+    spec = getattr(main, "__spec__", None)
+    name = getattr(spec, "name", None) or "beholder_amd"
+    if name.endswith(".__main__"):
+        name = name[: -len(".__main__")]
+    return [sys.executable, "-m", name]
+
+
 def cmd_run(a: argparse.Namespace) -> int:
     if a.workers and a.workers > 1:
         if a.source in ("stdin", "file"):
@@ -51,6 +63,7 @@ def cmd_run(a: argparse.Namespace) -> int:
         port = a.metrics_port if a.metrics_port is not None else (
             int(mcfg.get("port", 3000)) if mcfg.get("enabled", True) else -1)
         return Supervisor(argv, a.workers, metrics_port=port, metrics_host=str(mcfg.get("host", "0.0.0.0")),
+                          command=worker_command(),
                           max_restarts=int(wcfg.get("max_restarts", 10)),
                           restart_window_s=float(wcfg.get("restart_window_s", 300.0)),
                           healthy_s=float(wcfg.get("healthy_s", 60.0)),

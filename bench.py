@@ -108,6 +108,8 @@ def parse(argv=None):
     ap.add_argument("--e2e-events", type=int, default=250000,
                     help="events of each tcp_e2e / tls_e2e measurement (the first 5,000 are the warm-up)")
     ap.add_argument("--soak-events", type=int, default=1_000_000)
+    ap.add_argument("--shared-queue-events", type=int, default=50_000,
+                    help="events per worker of each shared-queue run (run --workers N on one queue; 0 = skip)")
     ap.add_argument("--media", type=int, default=10000)
     ap.add_argument("--log-level", default="info")
     ap.add_argument("--seed", type=int, default=0)
@@ -441,6 +443,36 @@ def _e2e_keys(prefix: str, run, n: int, **kw) -> dict:
     return out
 
 
+def shared_queue_workers(cpus: int, cap: int = 8) -> list:
+    """N of the shared-queue sweep: 1, 2, 4, 8 while N workers + the broker + this process + one
+    spare CPU fit in the share."""
+    return [n for n in (1, 2, 4, 8) if n <= cap and n + 3 <= max(4, cpus)]
+
+
+def shared_queue_keys(a) -> dict:
+    """The reference's own scaling mode (competing consumers on one queue, index.js:43,62,127):
+    ``run --workers N`` against one shared-queue broker, the same load per worker for each N
+    (bench/shared_queue.py). Keyed by N: events/s, the broker's CPU per event, and whether every
+    published event was acked exactly once."""
+    from beholder_amd.bench.shared_queue import run_shared
+    ns = shared_queue_workers(available_cpus())
+    if a.shared_queue_events <= 0 or not ns:
+        return {}
+    eps, bcpu, once, acked, published, per_conn = {}, {}, {}, {}, {}, {}
+    for n in ns:
+        r = run_shared(n, a.shared_queue_events * n, seed=a.seed)
+        key = str(n)
+        eps[key] = _r(r["events_per_sec"], 1)
+        bcpu[key] = _r(r["broker_cpu_us_per_event"])
+        once[key] = bool(r["exactly_once"] and r.get("supervisor_rc") == 0)
+        acked[key], published[key] = r["acked"], r["published"]
+        per_conn[key] = r["per_connection_delivered"]
+    return {"shared_queue_events_per_sec": eps, "shared_queue_exactly_once": all(once.values()),
+            "shared_queue_broker_cpu_us_per_event": bcpu, "shared_queue_acked": acked,
+            "shared_queue_published": published, "shared_queue_exactly_once_by_n": once,
+            "shared_queue_per_worker_delivered": per_conn}
+
+
 def io_extras(a) -> dict:
     """BASELINE config 1 (the real CLI on stdin) and the production-shaped TCP path. Both start
     child processes, so they run before this process touches HIP."""
@@ -470,6 +502,7 @@ def io_extras(a) -> dict:
                 "tls_e2e_preconnect_init_ms": pre.get("init_ms"),
                 "tls_e2e_preconnect_handshakes": (pre.get("http") or {}).get("tls_handshakes"),
                 "tls_e2e_preconnect_errors": pre.get("errors")})
+    out.update(shared_queue_keys(a))
     h = harness._http_tcp(Workload(n_media=10000, seed=a.seed), a.io_events, clients=("h1",))["h1"]
     hl = h["handle_latency_us"]
     out.update({"http_tcp_h1_events_per_sec": _r(h["ingest_rate_eps"], 1),

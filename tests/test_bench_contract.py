@@ -50,7 +50,7 @@ def test_bench_single_rank_contract(tmp_path):
     full_path = str(tmp_path / "full.json")
     r = subprocess.run([sys.executable, "bench.py", *SMALL, "--procs-per-rank", "2", "--all-procs-steps", "1",
                         "--io-events", "2000", "--e2e-events", "4000", "--soak-events", "20000",
-                        "--full-out", full_path],
+                        "--shared-queue-events", "3000", "--full-out", full_path],
                        cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.strip()][-1]
@@ -99,6 +99,10 @@ def test_bench_single_rank_contract(tmp_path):
     assert 4000 - 400 - 100 <= out["tcp_e2e_measured_events"] <= 4000 - 400 and out["tcp_e2e_calib_ns"] > 0
     assert set(out["tcp_e2e_fakes_cpu_us_per_event"]) == {"broker", "pg", "http"}
     assert out["tcp_e2e_sys_cpu_us_per_event"] >= 0 and out["tcp_e2e_minflt"] >= 0
+    # competing consumers on one queue (run --workers N), every event acked exactly once
+    ns = bench.shared_queue_workers(out["cpus_available"])
+    assert list(out["shared_queue_events_per_sec"]) == [str(n) for n in ns] and out["shared_queue_exactly_once"]
+    assert all(out["shared_queue_acked"][str(n)] == out["shared_queue_published"][str(n)] == 3000 * n for n in ns)
 
 
 def test_bench_two_ranks_gloo():
@@ -173,7 +177,7 @@ def test_no_hip_before_child_processes(monkeypatch, capsys):
     monkeypatch.setattr(harness, "_spawn", spy_spawn)
     monkeypatch.setattr(bench, "run_procs", spy_procs)
     assert bench.main([*SMALL, "--procs-per-rank", "2", "--all-procs-steps", "1", "--io-events", "1000",
-                       "--e2e-events", "1000", "--soak-events", "5000"]) == 0
+                       "--e2e-events", "1000", "--soak-events", "5000", "--shared-queue-events", "0"]) == 0
     out = _last_json(capsys.readouterr().out)
     assert out["value"] > 0
     assert "spawn" in order and "procs" in order and "sync" in order

@@ -227,3 +227,33 @@ def test_workers_config_is_validated():
     for k, bad in (("max_restarts", -1), ("restart_window_s", 0), ("healthy_s", "x")):
         with pytest.raises(ConfigError, match=f"service.workers.{k}"):
             cfg({"service": {"workers": {k: bad}}})
+
+
+def test_shared_queue_two_workers_ack_every_event_exactly_once():
+    """The bench's shared-queue phase (VERDICT r4 item 5): `run --workers 2` on one broker queue;
+    the broker counts every ack per event: all published events acked, none twice, none lost,
+    no ack of an unknown tag, and both workers got deliveries."""
+    from beholder_amd.bench.shared_queue import run_shared
+    r = run_shared(2, 6000)
+    assert r["supervisor_rc"] == 0, r.get("supervisor_stderr")
+    assert r["published"] == r["acked"] == 6000
+    assert r["dup_acks"] == 0 and r["lost"] == 0 and r["unknown_acks"] == 0 and r["exactly_once"]
+    assert r["connections"] == 2 and len(r["per_connection_delivered"]) == 2
+    assert all(n > 0 for n in r["per_connection_delivered"]) and sum(r["per_connection_delivered"]) == 6000
+    assert r["events_per_sec"] > 0 and r["broker_cpu_us_per_event"] > 0
+
+
+def test_worker_command_reruns_the_entry_module(monkeypatch):
+    """Workers re-run the module the supervisor was started with, so a wrapper entry (the bench's
+    shared_worker) stays in force in every worker."""
+    import types
+
+    from beholder_amd import cli
+    fake = types.ModuleType("__main__")
+    fake.__spec__ = types.SimpleNamespace(name="beholder_amd.bench.shared_worker")
+    monkeypatch.setitem(sys.modules, "__main__", fake)
+    assert cli.worker_command() == [sys.executable, "-m", "beholder_amd.bench.shared_worker"]
+    fake.__spec__ = types.SimpleNamespace(name="beholder_amd.__main__")
+    assert cli.worker_command() == [sys.executable, "-m", "beholder_amd"]
+    fake.__spec__ = None
+    assert cli.worker_command() == [sys.executable, "-m", "beholder_amd"]
