@@ -737,10 +737,16 @@ bool request_text(PyObject* method, PyObject* url, Py_ssize_t k, PyObject* param
 // `url` with its query `q` appended (new reference).
 PyObject* full_url(PyObject* url, const std::string& q) {
   if (q.empty()) return Py_NewRef(url);
-  std::string f(reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(url)), size_t(PyUnicode_GET_LENGTH(url)));
-  f += '?';
-  f += q;
-  return PyUnicode_FromStringAndSize(f.data(), Py_ssize_t(f.size()));
+  // url (ASCII: split_shape) + "?" + q (percent-encoded: ASCII): one compact ASCII str, filled in
+  // place, without a UTF-8 decode of the joined text
+  Py_ssize_t un = PyUnicode_GET_LENGTH(url);
+  PyObject* f = PyUnicode_New(un + 1 + Py_ssize_t(q.size()), 127);
+  if (!f) return nullptr;
+  Py_UCS1* d = PyUnicode_1BYTE_DATA(f);
+  memcpy(d, PyUnicode_1BYTE_DATA(url), size_t(un));
+  d[un] = '?';
+  memcpy(d + un + 1, q.data(), q.size());
+  return f;
 }
 
 // At the first await: send the request on an idle pooled connection. 1 = sent (s->conn, fut,
@@ -1133,6 +1139,10 @@ int api_h1_request_text(PyObject* method, PyObject* url, PyObject* params, PyObj
   }
   BEHOLDER_CATCH(-1)
 }
+
+PyTypeObject* h1_response_type() { return g.resp.type; }
+
+PyObject* h1_response_status(PyObject* resp) { return g.resp.get(resp, R_STATUS); }
 
 int api_h1_origin_key(PyObject* method, PyObject* url, PyObject* params, Py_ssize_t* key_len) {
   return split_shape(method, url, params == Py_None ? nullptr : params, key_len) ? 1 : 0;

@@ -25,6 +25,11 @@
 
 #include "native_api.hpp"
 #include "py_common.hpp"
+
+namespace beholder {
+PyTypeObject* h1_response_type();       // py_h1call.cpp: sinks/http.py HttpResponse, once registered
+PyObject* h1_response_status(PyObject* resp);  // its `status` slot (borrowed; NULL when unset)
+}  // namespace beholder
 #include "ring.hpp"
 
 namespace beholder {
@@ -614,6 +619,17 @@ PyObject* request_finish(CallObject* c, PyObject* value) {
     }
     return nullptr;
   }
+  // the stock HttpResponse (sinks/http.py): its status read from the slot, and a 2xx needs no
+  // raise_for_status() call (it only raises for a non-2xx status)
+  PyObject* rt = reinterpret_cast<PyObject*>(h1_response_type());
+  long code = -1;
+  if (rt && reinterpret_cast<PyObject*>(Py_TYPE(value)) == rt) {
+    PyObject* st = h1_response_status(value);
+    if (st && PyLong_CheckExact(st)) {
+      code = PyLong_AsLong(st);
+      if (code == -1 && PyErr_Occurred()) PyErr_Clear();
+    }
+  }
   if (stats) {
     PyObject* st = PyObject_GetAttr(value, s_status);
     bool ok = st && record_stats(stats, st, dt);
@@ -624,7 +640,7 @@ PyObject* request_finish(CallObject* c, PyObject* value) {
       return nullptr;
     }
   }
-  if (c->req_strict) {
+  if (c->req_strict && !(code >= 200 && code < 300)) {
     PyObject* r = PyObject_CallMethodNoArgs(value, s_raise_for_status);
     if (!r) {
       Py_DECREF(value);

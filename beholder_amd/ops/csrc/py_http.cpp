@@ -42,6 +42,9 @@ struct H1ParserObject {
   bool keep_alive;
   bool http11;
   uint64_t responses;
+  PyObject* last_reason;   // the last reply's reason / raw headers / body objects (reuse_or_make)
+  PyObject* last_headers;
+  PyObject* last_body;
 };
 
 PyTypeObject H1ParserType = {PyVarObject_HEAD_INIT(nullptr, 0)};
@@ -328,19 +331,58 @@ bool run(H1ParserObject* s) {
   }
 }
 
-PyObject* make_result(H1ParserObject* s) {
-  PyObject* r = Py_BuildValue("(is#y#y#O)", s->status, s->reason->data(), Py_ssize_t(s->reason->size()),
-                              s->headers->data(), Py_ssize_t(s->headers->size()), s->body->data(),
-                              Py_ssize_t(s->body->size()), s->keep_alive ? Py_True : Py_False);
-  if (!r) {
-    // reason phrases are opaque octets; fall back to latin-1
-    PyErr_Clear();
-    r = Py_BuildValue("(iNy#y#O)", s->status,
-                      PyUnicode_DecodeLatin1(s->reason->data(), Py_ssize_t(s->reason->size()), nullptr),
-                      s->headers->data(), Py_ssize_t(s->headers->size()), s->body->data(),
-                      Py_ssize_t(s->body->size()), s->keep_alive ? Py_True : Py_False);
+// An immutable object equal to the last one made from the same field, or a new one (then kept).
+// A keep-alive connection's replies mostly repeat the reason phrase and often the headers and
+// body, so most replies reuse the objects (they are immutable: sharing is invisible).
+PyObject* reuse_or_make(PyObject** cache, const std::string& v, bool text) {
+  PyObject* c = *cache;
+  if (c) {
+    const char* d;
+    Py_ssize_t n;
+    if (text) {
+      d = reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(c));
+      n = PyUnicode_GET_LENGTH(c);
+    } else {
+      d = PyBytes_AS_STRING(c);
+      n = PyBytes_GET_SIZE(c);
+    }
+    if (size_t(n) == v.size() && memcmp(d, v.data(), v.size()) == 0) return Py_NewRef(c);
   }
-  if (!r) return nullptr;
+  PyObject* o;
+  if (text) {
+    // reason phrases are opaque octets: UTF-8 when they are, else latin-1
+    o = PyUnicode_DecodeUTF8(v.data(), Py_ssize_t(v.size()), nullptr);
+    if (!o) {
+      PyErr_Clear();
+      o = PyUnicode_DecodeLatin1(v.data(), Py_ssize_t(v.size()), nullptr);
+    }
+    if (o && !PyUnicode_IS_ASCII(o)) return o;  // only ASCII ones are cached (compared bytewise above)
+  } else {
+    o = PyBytes_FromStringAndSize(v.data(), Py_ssize_t(v.size()));
+  }
+  if (!o) return nullptr;
+  if (v.size() <= 4096) Py_XSETREF(*cache, Py_NewRef(o));
+  return o;
+}
+
+PyObject* make_result(H1ParserObject* s) {
+  PyObject* st = PyLong_FromLong(s->status);
+  PyObject* reason = st ? reuse_or_make(&s->last_reason, *s->reason, true) : nullptr;
+  PyObject* hdr = reason ? reuse_or_make(&s->last_headers, *s->headers, false) : nullptr;
+  PyObject* body = hdr ? reuse_or_make(&s->last_body, *s->body, false) : nullptr;
+  PyObject* r = body ? PyTuple_New(5) : nullptr;
+  if (!r) {
+    Py_XDECREF(st);
+    Py_XDECREF(reason);
+    Py_XDECREF(hdr);
+    Py_XDECREF(body);
+    return nullptr;
+  }
+  PyTuple_SET_ITEM(r, 0, st);
+  PyTuple_SET_ITEM(r, 1, reason);
+  PyTuple_SET_ITEM(r, 2, hdr);
+  PyTuple_SET_ITEM(r, 3, body);
+  PyTuple_SET_ITEM(r, 4, Py_NewRef(s->keep_alive ? Py_True : Py_False));
   ++s->responses;
   s->st = St::IDLE;
   s->body->clear();
@@ -396,6 +438,9 @@ int h1_init(H1ParserObject* s, PyObject* args, PyObject* kwds) {
 }
 
 void h1_dealloc(H1ParserObject* s) {
+  Py_XDECREF(s->last_reason);
+  Py_XDECREF(s->last_headers);
+  Py_XDECREF(s->last_body);
   delete s->buf;
   delete s->body;
   delete s->reason;
@@ -403,27 +448,43 @@ void h1_dealloc(H1ParserObject* s) {
   Py_TYPE(s)->tp_free(reinterpret_cast<PyObject*>(s));
 }
 
-PyObject* h1_start(H1ParserObject* s, PyObject* args, PyObject* kwds) {
-  static const char* kwlist[] = {"head", nullptr};
-  int head = 0;
-  if (!PyArg_ParseTupleAndKeywords(args, kwds, "|p", const_cast<char**>(kwlist), &head)) return nullptr;
+int start_core(H1ParserObject* s, bool head) {
   if (s->st != St::IDLE) {
     PyErr_SetString(PyExc_RuntimeError, "H1Parser.start() while a response is in progress");
-    return nullptr;
+    return -1;
   }
   reset_response(s);
-  s->head_req = head != 0;
+  s->head_req = head;
   s->scan = 0;
   s->st = St::HEAD;
+  return 0;
+}
+
+// start(head=False): vectorcall, one optional argument (positional or `head=`)
+PyObject* h1_start(H1ParserObject* s, PyObject* const* args, Py_ssize_t nargs, PyObject* kwnames) {
+  Py_ssize_t nkw = kwnames ? PyTuple_GET_SIZE(kwnames) : 0;
+  PyObject* v = nullptr;
+  if (nargs > 1 || nargs + nkw > 1) {
+    PyErr_SetString(PyExc_TypeError, "start(head=False) takes one optional argument");
+    return nullptr;
+  }
+  if (nargs == 1) {
+    v = args[0];
+  } else if (nkw == 1) {
+    if (PyUnicode_CompareWithASCIIString(PyTuple_GET_ITEM(kwnames, 0), "head") != 0) {
+      PyErr_Format(PyExc_TypeError, "start() got an unexpected keyword argument '%U'", PyTuple_GET_ITEM(kwnames, 0));
+      return nullptr;
+    }
+    v = args[0];
+  }
+  int head = v ? PyObject_IsTrue(v) : 0;
+  if (head < 0 || start_core(s, head != 0) < 0) return nullptr;
   Py_RETURN_NONE;
 }
 
-PyObject* h1_feed(H1ParserObject* s, PyObject* arg) {
+PyObject* feed_core(H1ParserObject* s, const char* data, size_t n) {
   BEHOLDER_TRY {
-    Py_buffer view;
-    if (PyObject_GetBuffer(arg, &view, PyBUF_SIMPLE) < 0) return nullptr;
-    s->buf->append(static_cast<const char*>(view.buf), size_t(view.len));
-    PyBuffer_Release(&view);
+    s->buf->append(data, n);
     bool done;
     try {
       done = run(s);
@@ -439,6 +500,14 @@ PyObject* h1_feed(H1ParserObject* s, PyObject* arg) {
     Py_RETURN_NONE;
   }
   BEHOLDER_CATCH(nullptr)
+}
+
+PyObject* h1_feed(H1ParserObject* s, PyObject* arg) {
+  Py_buffer view;
+  if (PyObject_GetBuffer(arg, &view, PyBUF_SIMPLE) < 0) return nullptr;
+  PyObject* r = feed_core(s, static_cast<const char*>(view.buf), size_t(view.len));
+  PyBuffer_Release(&view);
+  return r;
 }
 
 PyObject* h1_eof(H1ParserObject* s, PyObject*) {
@@ -470,7 +539,7 @@ PyObject* h1_get_started(H1ParserObject* s, void*) {
 }
 
 PyMethodDef h1_methods[] = {
-    {"start", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(h1_start)), METH_VARARGS | METH_KEYWORDS,
+    {"start", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(h1_start)), METH_FASTCALL | METH_KEYWORDS,
      "start(head=False): expect the response to a new request"},
     {"feed", reinterpret_cast<PyCFunction>(h1_feed), METH_O,
      "feed(data) -> None | (status, reason, raw_headers, body, keep_alive)"},
@@ -486,6 +555,16 @@ PyGetSetDef h1_getset[] = {
     {nullptr, nullptr, nullptr, nullptr, nullptr}};
 
 }  // namespace
+
+// H1Parser.start / feed for a caller in C (py_netconn.cpp): no argument parsing, no memoryview.
+// Exact H1Parser only (is_h1_parser); the same semantics as the methods.
+bool is_h1_parser(PyObject* o) { return Py_TYPE(o) == &H1ParserType; }
+
+int h1_parser_start_c(PyObject* o, bool head) { return start_core(reinterpret_cast<H1ParserObject*>(o), head); }
+
+PyObject* h1_parser_feed_c(PyObject* o, const char* data, size_t n) {
+  return feed_core(reinterpret_cast<H1ParserObject*>(o), data, n);
+}
 
 int init_http_types(PyObject* m) {
   H1ParserType.tp_name = "beholder_amd.ops._native.H1Parser";

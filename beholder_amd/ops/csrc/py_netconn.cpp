@@ -75,6 +75,12 @@ std::shared_ptr<HsWake> netpoll_wake(PyObject* po);
 void tls_describe_failure(SSL* ssl, std::string& reason, std::string& message, bool& verify);
 bool tls_warm_handshake();
 
+bool is_h1_parser(PyObject* o);  // py_http.cpp
+int h1_parser_start_c(PyObject* o, bool head);
+PyObject* h1_parser_feed_c(PyObject* o, const char* data, size_t n);
+bool is_pg_reader(PyObject* o);  // py_pg.cpp
+PyObject* pg_reader_feed_c(PyObject* o, const char* data, size_t n);
+
 namespace {
 
 PyObject *s_add_reader, *s_remove_reader, *s_add_writer, *s_remove_writer, *s_call_soon, *s_feed, *s_start,
@@ -577,8 +583,32 @@ PyObject* closed_error(NetConnObject* c) {
 }
 
 // ---- reply dispatch -----------------------------------------------------------------------
-void on_h1_data(NetConnObject* c, PyObject* mv) {
+// parser.feed(bytes received): the stock parsers directly in C, any other through its method
+PyObject* feed_parser(NetConnObject* c, const char* data, size_t n) {
+  if (c->kind == K_H1 ? is_h1_parser(c->parser) : is_pg_reader(c->parser))
+    return c->kind == K_H1 ? h1_parser_feed_c(c->parser, data, n) : pg_reader_feed_c(c->parser, data, n);
+  PyObject* mv = PyMemoryView_FromMemory(const_cast<char*>(data), Py_ssize_t(n), PyBUF_READ);
+  if (!mv) return nullptr;
   PyObject* r = PyObject_CallOneArg(c->feed, mv);
+  Py_DECREF(mv);
+  return r;
+}
+
+// parser.start(head=head) before a request: the stock H1Parser directly in C
+int start_parser(NetConnObject* c, bool head) {
+  if (is_h1_parser(c->parser)) return h1_parser_start_c(c->parser, head);
+  PyObject* kw = PyTuple_Pack(1, s_head);
+  if (!kw) return -1;
+  PyObject* args[1] = {head ? Py_True : Py_False};
+  PyObject* r = PyObject_Vectorcall(c->start, args, 0, kw);
+  Py_DECREF(kw);
+  if (!r) return -1;
+  Py_DECREF(r);
+  return 0;
+}
+
+void on_h1_data(NetConnObject* c, const char* data, size_t n) {
+  PyObject* r = feed_parser(c, data, n);
   if (!r) {  // malformed response: the owner fails the request and drops the connection
     PyObject *et, *ev, *tb;
     PyErr_Fetch(&et, &ev, &tb);
@@ -606,8 +636,8 @@ void on_h1_data(NetConnObject* c, PyObject* mv) {
   Py_DECREF(r);
 }
 
-void on_pg_data(NetConnObject* c, PyObject* mv) {
-  PyObject* items = PyObject_CallOneArg(c->feed, mv);
+void on_pg_data(NetConnObject* c, const char* data, size_t len) {
+  PyObject* items = feed_parser(c, data, len);
   if (!items) {
     PyObject *et, *ev, *tb;
     PyErr_Fetch(&et, &ev, &tb);
@@ -928,15 +958,12 @@ PyObject* nc_on_readable(NetConnObject* c, PyObject*) {
   }
   c->bytes_in += uint64_t(n);
   ++c->recvs;
-  PyObject* mv = PyMemoryView_FromMemory(buf, Py_ssize_t(n), PyBUF_READ);
-  if (!mv) return nullptr;
   Py_INCREF(c);  // a resumed handler may drop the last other reference
   if (c->kind == K_H1) {
-    on_h1_data(c, mv);
+    on_h1_data(c, buf, size_t(n));
   } else {
-    on_pg_data(c, mv);
+    on_pg_data(c, buf, size_t(n));
   }
-  Py_DECREF(mv);
   Py_DECREF(c);
   Py_RETURN_NONE;
 }
@@ -963,17 +990,11 @@ PyObject* on_readable_tls(NetConnObject* c, char* buf) {
     if (n > 0) {
       c->bytes_in += uint64_t(n);
       ++c->recvs;
-      PyObject* mv = PyMemoryView_FromMemory(buf, Py_ssize_t(n), PyBUF_READ);
-      if (!mv) {
-        Py_DECREF(c);
-        return nullptr;
-      }
       if (c->kind == K_H1) {
-        on_h1_data(c, mv);
+        on_h1_data(c, buf, size_t(n));
       } else {
-        on_pg_data(c, mv);
+        on_pg_data(c, buf, size_t(n));
       }
-      Py_DECREF(mv);
       // nothing buffered in OpenSSL: stop without the recv(2) that would only say EAGAIN (the
       // loop's level-triggered poll comes back if the kernel holds more)
       if (c->ssl && !SSL_has_pending(c->ssl)) break;
@@ -1038,13 +1059,8 @@ PyObject* nc_request(NetConnObject* c, PyObject* const* a, Py_ssize_t n) {
       return nullptr;
     }
     if (c->fd < 0) return closed_error(c);
-    PyObject* kw = PyTuple_Pack(1, s_head);
-    if (!kw) return nullptr;
-    PyObject* args[1] = {a[2]};
-    PyObject* r = PyObject_Vectorcall(c->start, args, 0, kw);  // parser.start(head=head)
-    Py_DECREF(kw);
-    if (!r) return nullptr;
-    Py_DECREF(r);
+    int head = PyObject_IsTrue(a[2]);
+    if (head < 0 || start_parser(c, head != 0) < 0) return nullptr;  // parser.start(head=head)
     Py_INCREF(a[1]);
     Py_XSETREF(c->waiter, a[1]);
     if (append_bytes(c, a[0]) < 0) return nullptr;
@@ -1294,13 +1310,7 @@ int netconn_h1_request(PyObject* o, const std::string& data, PyObject* waiter, b
     closed_error(c);
     return -1;
   }
-  PyObject* kw = PyTuple_Pack(1, s_head);
-  if (!kw) return -1;
-  PyObject* args[1] = {head ? Py_True : Py_False};
-  PyObject* r = PyObject_Vectorcall(c->start, args, 0, kw);  // parser.start(head=head)
-  Py_DECREF(kw);
-  if (!r) return -1;
-  Py_DECREF(r);
+  if (start_parser(c, head) < 0) return -1;  // parser.start(head=head)
   Py_INCREF(waiter);
   Py_XSETREF(c->waiter, waiter);
   c->out->append(data);

@@ -60,6 +60,19 @@ PyObject* decode_text(uint32_t oid, const char* s, size_t n) {
     case 16:
       return PyBool_FromLong(n == 1 && s[0] == 't');
     case 20: case 21: case 23: case 26: {
+      // the common case (a status, a creator, an id that fits in 18 digits): no string copy and
+      // no PyLong_FromString parse; anything else (a sign, spaces, longer) takes the general path
+      if (n && n <= 18) {
+        size_t i = s[0] == '-' ? 1 : 0;
+        long long v = 0;
+        bool ok = i < n;
+        for (; ok && i < n; ++i) {
+          unsigned d = unsigned(s[i]) - '0';
+          if (d > 9) ok = false;
+          else v = v * 10 + d;
+        }
+        if (ok) return PyLong_FromLongLong(s[0] == '-' ? -v : v);
+      }
       std::string tmp(s, n);
       return PyLong_FromString(tmp.c_str(), nullptr, 10);
     }
@@ -296,25 +309,20 @@ void pg_dealloc(PgReaderObject* r) {
   Py_TYPE(r)->tp_free(reinterpret_cast<PyObject*>(r));
 }
 
-PyObject* pg_feed_impl(PgReaderObject* r, PyObject* arg) {
-  Py_buffer view;
-  if (PyObject_GetBuffer(arg, &view, PyBUF_SIMPLE) < 0) return nullptr;
+PyObject* pg_feed_bytes(PgReaderObject* r, const char* in, size_t in_len) {
   const uint8_t* data;
   size_t len;
   std::string& carry = *r->carry;
   if (carry.empty()) {
-    data = static_cast<const uint8_t*>(view.buf);
-    len = size_t(view.len);
+    data = reinterpret_cast<const uint8_t*>(in);
+    len = in_len;
   } else {
-    carry.append(static_cast<const char*>(view.buf), size_t(view.len));
+    carry.append(in, in_len);
     data = reinterpret_cast<const uint8_t*>(carry.data());
     len = carry.size();
   }
   PyObject* out = PyList_New(0);
-  if (!out) {
-    PyBuffer_Release(&view);
-    return nullptr;
-  }
+  if (!out) return nullptr;
   size_t i = 0;
   try {
     while (len - i >= 5) {
@@ -328,7 +336,6 @@ PyObject* pg_feed_impl(PgReaderObject* r, PyObject* arg) {
       int rc = r->query_mode ? on_message(r, out, typ, body, bn) : emit_raw(out, typ, body, bn);
       if (rc < 0) {
         Py_DECREF(out);
-        PyBuffer_Release(&view);
         carry.clear();
         clear_query(r);
         return nullptr;
@@ -337,7 +344,6 @@ PyObject* pg_feed_impl(PgReaderObject* r, PyObject* arg) {
     }
   } catch (const std::invalid_argument& e) {
     Py_DECREF(out);
-    PyBuffer_Release(&view);
     carry.clear();
     clear_query(r);
     PyErr_SetString(PyExc_ValueError, e.what());
@@ -347,6 +353,19 @@ PyObject* pg_feed_impl(PgReaderObject* r, PyObject* arg) {
     if (i < len) carry.assign(reinterpret_cast<const char*>(data + i), len - i);
   } else {
     carry.erase(0, i);
+  }
+  return out;
+}
+
+PyObject* pg_feed_impl(PgReaderObject* r, PyObject* arg) {
+  Py_buffer view;
+  if (PyObject_GetBuffer(arg, &view, PyBUF_SIMPLE) < 0) return nullptr;
+  PyObject* out;
+  try {
+    out = pg_feed_bytes(r, static_cast<const char*>(view.buf), size_t(view.len));
+  } catch (...) {
+    PyBuffer_Release(&view);
+    throw;
   }
   PyBuffer_Release(&view);
   return out;
@@ -437,6 +456,15 @@ int put_param(std::string& o, PyObject* v) {
 }
 
 }  // namespace
+
+// PgReader.feed for a caller in C (py_netconn.cpp): the received bytes without a memoryview and
+// a method call. The same result as feed(); exact PgReader only (is_pg_reader).
+bool is_pg_reader(PyObject* o) { return Py_TYPE(o) == &PgReaderType; }
+
+PyObject* pg_reader_feed_c(PyObject* o, const char* data, size_t n) {
+  BEHOLDER_TRY { return pg_feed_bytes(reinterpret_cast<PgReaderObject*>(o), data, n); }
+  BEHOLDER_CATCH(nullptr)
+}
 
 // Appends Bind + Describe(portal) + Execute + Sync for statement `name` to `o`. -1 on error.
 int pg_bind_append(std::string& o, const char* name, size_t nlen, PyObject* params) {

@@ -10,6 +10,14 @@
 //
 // The handler is async-signal-safe: one atomic increment and two stores into memory allocated
 // before the timer is armed. No allocation, no locks, no Python.
+//
+// prof_start(hz, depth): with depth > 0 each sample also keeps up to `depth` return addresses of
+// the interrupted thread (glibc backtrace(), unwinding through the signal frame with the
+// objects' .eh_frame tables), so cprof.py can charge a sample to every function on the stack
+// (inclusive cost) and name a leaf's callers. backtrace() is called once before the timer is
+// armed (it loads the unwinder on first use); it is not formally async-signal-safe, which is
+// acceptable for this diagnostic: the samples of one profiling run, never the service.
+#include <execinfo.h>
 #include <signal.h>
 #include <sys/syscall.h>
 #include <sys/time.h>
@@ -26,8 +34,12 @@ namespace beholder {
 namespace {
 
 constexpr size_t kMaxSamples = 1 << 20;
+constexpr int kMaxDepth = 32;
 uint64_t* g_ip = nullptr;
 uint32_t* g_tid = nullptr;
+void** g_stk = nullptr;     // kMaxSamples x g_depth return addresses (depth > 0)
+uint8_t* g_stk_n = nullptr;  // frames kept per sample
+int g_depth = 0;
 std::atomic<size_t> g_n{0};
 std::atomic<uint64_t> g_lost{0};
 std::atomic<bool> g_active{false};
@@ -47,11 +59,24 @@ void on_sigprof(int, siginfo_t*, void* uc_v) {
   const ucontext_t* uc = static_cast<const ucontext_t*>(uc_v);
   g_ip[i] = uint64_t(uc->uc_mcontext.gregs[REG_RIP]);
   g_tid[i] = uint32_t(syscall(SYS_gettid));
+  if (g_depth) {
+    // frames 0-1: this handler and the signal trampoline; then the interrupted function and its callers
+    void* buf[kMaxDepth + 2];
+    int n = backtrace(buf, g_depth + 2);
+    int k = n > 2 ? n - 2 : 0;
+    void** dst = g_stk + i * size_t(g_depth);
+    for (int j = 0; j < k; ++j) dst[j] = buf[j + 2];
+    g_stk_n[i] = uint8_t(k);
+  }
 }
 
 PyObject* prof_start(PyObject*, PyObject* args) {
-  int hz = 997;
-  if (!PyArg_ParseTuple(args, "|i", &hz)) return nullptr;
+  int hz = 997, depth = 0;
+  if (!PyArg_ParseTuple(args, "|ii", &hz, &depth)) return nullptr;
+  if (depth < 0 || depth > kMaxDepth) {
+    PyErr_Format(PyExc_ValueError, "depth must be in [0, %d]", kMaxDepth);
+    return nullptr;
+  }
   if (g_armed) {
     PyErr_SetString(PyExc_RuntimeError, "profiler already running");
     return nullptr;
@@ -70,6 +95,27 @@ PyObject* prof_start(PyObject*, PyObject* args) {
       g_tid = nullptr;
       return PyErr_NoMemory();
     }
+  }
+  if (depth != g_depth || (depth && !g_stk)) {
+    std::free(g_stk);
+    std::free(g_stk_n);
+    g_stk = nullptr;
+    g_stk_n = nullptr;
+    g_depth = 0;
+    if (depth) {
+      g_stk = static_cast<void**>(std::calloc(kMaxSamples * size_t(depth), sizeof(void*)));
+      g_stk_n = static_cast<uint8_t*>(std::calloc(kMaxSamples, 1));
+      if (!g_stk || !g_stk_n) {
+        std::free(g_stk);
+        std::free(g_stk_n);
+        g_stk = nullptr;
+        g_stk_n = nullptr;
+        return PyErr_NoMemory();
+      }
+      void* warm[4];
+      backtrace(warm, 4);  // loads the unwinder outside the signal handler
+    }
+    g_depth = depth;
   }
   g_n.store(0);
   g_lost.store(0);
@@ -108,7 +154,27 @@ PyObject* prof_stop(PyObject*, PyObject*) {
   PyObject* ips = PyList_New(Py_ssize_t(n));
   if (!ips) return nullptr;
   for (size_t i = 0; i < n; ++i) {
-    PyObject* t = Py_BuildValue("(KI)", (unsigned long long)g_ip[i], (unsigned int)g_tid[i]);
+    PyObject* t;
+    if (g_depth) {
+      PyObject* fr = PyTuple_New(g_stk_n[i]);
+      if (!fr) {
+        Py_DECREF(ips);
+        return nullptr;
+      }
+      void** src = g_stk + i * size_t(g_depth);
+      for (int j = 0; j < g_stk_n[i]; ++j) {
+        PyObject* a = PyLong_FromUnsignedLongLong((unsigned long long)(uintptr_t)src[j]);
+        if (!a) {
+          Py_DECREF(fr);
+          Py_DECREF(ips);
+          return nullptr;
+        }
+        PyTuple_SET_ITEM(fr, j, a);
+      }
+      t = Py_BuildValue("(KIN)", (unsigned long long)g_ip[i], (unsigned int)g_tid[i], fr);
+    } else {
+      t = Py_BuildValue("(KI)", (unsigned long long)g_ip[i], (unsigned int)g_tid[i]);
+    }
     if (!t) {
       Py_DECREF(ips);
       return nullptr;
@@ -119,8 +185,9 @@ PyObject* prof_stop(PyObject*, PyObject*) {
 }
 
 PyMethodDef prof_methods[] = {
-    {"prof_start", prof_start, METH_VARARGS, "prof_start(hz=997): sample instruction pointers on SIGPROF"},
-    {"prof_stop", prof_stop, METH_NOARGS, "prof_stop() -> ([(ip, tid), ...], lost)"},
+    {"prof_start", prof_start, METH_VARARGS,
+     "prof_start(hz=997, depth=0): sample instruction pointers (and `depth` return addresses) on SIGPROF"},
+    {"prof_stop", prof_stop, METH_NOARGS, "prof_stop() -> ([(ip, tid[, frames]), ...], lost)"},
     {nullptr, nullptr, 0, nullptr}};
 
 }  // namespace

@@ -509,6 +509,7 @@ class H1Client(HttpClient):
         counts = self.counts
         idle = o.idle
         loop = asyncio.get_running_loop()
+        passed_on = False  # a fresh retry passes a healthy connection on to another request only once
         while True:
             now = time.monotonic()
             while idle and not fresh:
@@ -552,12 +553,20 @@ class H1Client(HttpClient):
                 if c.uses:
                     counts["reused"] += 1
                 return c
-            if not c.closed and any(not x.done() for x in o.waiters):
+            if not fresh:
+                self._drop(c)  # closed meanwhile: its slot goes to the next waiter; this one queues again
+            elif not c.closed and not passed_on and any(not x.done() for x in o.waiters):
                 # a healthy keep-alive connection, but this retry needs a fresh one: another queued
-                # request takes it (no connect + handshake thrown away); this one keeps its place
+                # request takes it (no connect + handshake thrown away); this one keeps its place.
+                # Once only: at max_per_host nothing else ever frees a slot while requests queue, so
+                # passing every connection on would starve the retry until its deadline
                 self._release(c, True)
+                passed_on = True
             else:
-                self._drop(c)  # closed meanwhile, or nobody else to take it: make room for a fresh one
+                # closed meanwhile, nobody else to take it, or one passed on already: the slot is this
+                # retry's, for its own connect at the top of the loop (no other waiter is woken for it)
+                c.abort()
+                o.open -= 1
             front = True
 
     async def preconnect(self, url: str, n: int) -> Tuple[int, Optional[BaseException]]:

@@ -9,6 +9,7 @@ Prints the top functions by self samples, and the split by object.
 
     python scripts/cprof.py [--steps 20] [--hz 2000] [--top 60] [--tid main|all]
     python scripts/cprof.py --workload tcp_e2e|tls_e2e [--events 200000]   # the production-shaped path
+    python scripts/cprof.py ... --depth 24 [--focus send,recv]   # + inclusive cost and callers
 """
 from __future__ import annotations
 
@@ -106,6 +107,12 @@ def main(argv=None) -> int:
     ap.add_argument("--tid", default="main", choices=["main", "all"])
     ap.add_argument("--workload", default="headline", choices=["headline", "tcp_e2e", "tls_e2e"])
     ap.add_argument("--events", type=int, default=200_000, help="tcp_e2e / tls_e2e events")
+    ap.add_argument("--depth", type=int, default=0,
+                    help="also unwind this many frames per sample: inclusive cost per function and each "
+                         "top leaf's callers")
+    ap.add_argument("--focus", default="",
+                    help="with --depth: comma-separated substrings of leaf functions whose callers are listed "
+                         "(default: the top 8 leaves)")
     a = ap.parse_args(argv)
     import bench
     from beholder_amd.ops import bench_native as native
@@ -114,7 +121,7 @@ def main(argv=None) -> int:
     main_tid = threading.get_native_id()
 
     def go():
-        native.prof_start(a.hz)
+        native.prof_start(a.hz, a.depth)
 
     def stop():
         res["samples"], res["lost"] = native.prof_stop()
@@ -135,10 +142,20 @@ def main(argv=None) -> int:
         samples = [s for s in samples if s[1] == main_tid]
     fn = collections.Counter()
     obj = collections.Counter()
-    for ip, _tid in samples:
+    incl = collections.Counter()
+    callers = collections.defaultdict(collections.Counter)
+    for smp in samples:
+        ip = smp[0]
         o, f = resolve(ip, mp, starts)
         fn[(o, f)] += 1
         obj[o] += 1
+        if len(smp) > 2:
+            # return addresses: the call instruction is just before each one
+            frames = [(o, f)] + [resolve(r - 1, mp, starts) for r in smp[2][1:]]
+            for x in set(frames):
+                incl[x] += 1
+            chain = " <- ".join(g for _, g in frames[1:4])
+            callers[(o, f)][chain] += 1
     n = max(1, len(samples))
     print(f"events/s {r['events'] / r['elapsed']:.0f}  cpu us/event {r['cpu_s'] / r['events'] * 1e6:.3f}  "
           f"samples {len(samples)} ({a.tid} thread), lost {res['lost']}")
@@ -148,6 +165,17 @@ def main(argv=None) -> int:
     print("\n-- by function (self) --")
     for (o, f), c in fn.most_common(a.top):
         print(f"{100 * c / n:6.2f}%  {o:28s} {f}")
+    if incl:
+        print("\n-- by function (inclusive: on the stack) --")
+        for (o, f), c in incl.most_common(a.top):
+            print(f"{100 * c / n:6.2f}%  {o:28s} {f}")
+        focus = [x for x in a.focus.split(",") if x]
+        leaves = [k for k, _ in fn.most_common(8)] if not focus else \
+            [k for k in fn if any(x in k[1] for x in focus)]
+        for k in leaves:
+            print(f"\n-- callers of {k[1]} ({100 * fn[k] / n:.2f}% self) --")
+            for chain, c in callers[k].most_common(8):
+                print(f"{100 * c / n:6.2f}%  {chain}")
     return 0
 
 

@@ -636,3 +636,60 @@ def test_fresh_retry_hands_a_healthy_used_connection_to_the_next_waiter():
     got, used, pending, open_, got2, used2 = run(go())
     assert got is used and not used.aborted and pending and open_ == 1
     assert got2 == "fresh" and used2.aborted
+
+
+def test_fresh_retry_in_a_saturated_pool_is_not_starved():
+    """at max_per_host with several requests queued, a fresh retry passes a healthy
+    used connection on at most once; the next one it is handed makes room for its own connect,
+    so it finishes well before its deadline instead of waiting behind every release."""
+    from beholder_amd.sinks.h1 import _Conn
+
+    class Tracked(_Conn):
+        __slots__ = ("aborted",)
+
+        def __init__(self, o):
+            super().__init__(o)
+            self.aborted = False
+
+        def abort(self):
+            self.aborted = True
+            self.closed = True
+
+    async def go():
+        c = H1Client(timeout_s=5, max_per_host=2)
+        o = c._origin("http://127.0.0.1:9")
+        o.open = 2  # full: two busy connections
+        loop = asyncio.get_running_loop()
+        deadline = loop.time() + 5
+        retry = asyncio.ensure_future(c._acquire(o, deadline, fresh=True))
+        await asyncio.sleep(0)
+        others = [asyncio.ensure_future(c._acquire(o, deadline)) for _ in range(4)]
+        await asyncio.sleep(0)
+        connects = []
+
+        async def connect(o_, d, infos=None):
+            o_.open += 1
+            connects.append(1)
+            return "fresh"
+        c._connect = connect
+        conns = []
+        t0 = loop.time()
+        for _ in range(2):  # the two busy connections finish; each is released healthy
+            used = Tracked(o)
+            used.uses = 5
+            conns.append(used)
+            c._release(used, True)
+            await asyncio.sleep(0)
+            await asyncio.sleep(0)
+        got = await asyncio.wait_for(retry, 1)
+        took = loop.time() - t0
+        served = [x for x in others if x.done()]
+        for x in others:
+            x.cancel()
+        await c.close()
+        return got, took, conns, served, connects, o.open
+    got, took, conns, served, connects, open_ = run(go())
+    assert got == "fresh" and took < 0.5 and len(connects) == 1
+    assert not conns[0].aborted and conns[1].aborted  # passed on once, then its slot was taken
+    assert len(served) == 1 and served[0].result() is conns[0]
+    assert open_ == 2  # one kept by the other request, one the retry's own
