@@ -142,11 +142,15 @@ def parse_stall_lines(text: str) -> List[dict]:
     return out
 
 
-def _overlap(a0: int, a1: int, ivs: Sequence[Interval], starts: Sequence[int]) -> int:
-    """Total overlap of [a0, a1) with the sorted, possibly overlapping intervals ``ivs``."""
+def _overlap(a0: int, a1: int, ivs: Sequence[Interval], starts: Sequence[int], longest: Optional[int] = None) -> int:
+    """Total overlap of [a0, a1) with the sorted, possibly overlapping intervals ``ivs``, whose
+    longest is ``longest`` ns: no interval that starts earlier than ``a0 - longest`` can still
+    run at ``a0``, so the scan starts there (a stall that began long before the delivery and is
+    still going is the one the attribution most needs to see: ADVICE r4)."""
     import bisect
-    # intervals are short (ms); look back a bounded distance from a0
-    i = bisect.bisect_left(starts, a0 - 200_000_000)
+    if longest is None:
+        longest = max((e - s for s, e in ivs), default=0)
+    i = bisect.bisect_left(starts, a0 - max(longest, 0))
     covered = 0
     cur0 = cur1 = None
     for s, e in ivs[i:]:
@@ -176,7 +180,7 @@ def attribute(slow: Iterable[Tuple[int, int, int]], sources: Dict[str, Iterable[
     prepared = {}
     for name, ivs in sources.items():
         iv = sorted((int(a), int(b)) for a, b in ivs)
-        prepared[name] = (iv, [a for a, _ in iv])
+        prepared[name] = (iv, [a for a, _ in iv], max((b - a for a, b in iv), default=0))
     counts: Dict[str, int] = {name: 0 for name in prepared}
     counts["none"] = 0
     covered_ns: Dict[str, int] = {name: 0 for name in prepared}
@@ -187,8 +191,8 @@ def attribute(slow: Iterable[Tuple[int, int, int]], sources: Dict[str, Iterable[
         dur = max(1, settle - start)
         total_ns += dur
         best, best_ns = "none", 0
-        for name, (iv, starts) in prepared.items():
-            c = _overlap(start, settle, iv, starts)
+        for name, (iv, starts, longest) in prepared.items():
+            c = _overlap(start, settle, iv, starts, longest)
             covered_ns[name] += c
             if c > best_ns:
                 best, best_ns = name, c

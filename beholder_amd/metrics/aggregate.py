@@ -23,6 +23,7 @@ from __future__ import annotations
 import json
 import math
 import threading
+import time
 import urllib.request
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -118,7 +119,7 @@ class ClusterMetricsServer:
     ``/stats`` (per-worker JSON)."""
 
     def __init__(self, host: str, port: int, worker_ports: Callable[[], List[Tuple[int, int]]],
-                 alive: Callable[[], bool]):
+                 alive: Callable[[], bool], stale_after: int = 5, stale_s: float = 60.0):
         self.host = host
         self.port = port
         self._worker_ports = worker_ports  # [(worker id, port)]
@@ -128,8 +129,14 @@ class ClusterMetricsServer:
         # last good exposition per worker: a worker that misses one scrape (a loaded host, a long
         # GC pause) is served from it, so the merged counters never step back (Prometheus would
         # read a drop in a summed counter as a reset); beholder_cluster_worker_up says it was stale
-        self._last: Dict[int, str] = {}
+        self._last: Dict[int, Tuple[str, float]] = {}  # worker -> (exposition, monotonic time it was scraped)
         self._failures: Dict[int, int] = {}
+        self._streak: Dict[int, int] = {}  # consecutive failed scrapes per worker
+        # a worker that keeps failing (dead, wedged) stops being served from its last exposition after
+        # `stale_after` consecutive failures or `stale_s` seconds, whichever comes first: its frozen
+        # counters must not stay in the merged totals for good
+        self.stale_after = stale_after
+        self.stale_s = stale_s
         self._lock = threading.Lock()
 
     def _gather(self, path: str) -> List[Tuple[int, Optional[str]]]:
@@ -141,14 +148,24 @@ class ClusterMetricsServer:
         ``beholder_cluster_scrape_failures_total{worker}``."""
         got = self._gather("/metrics")
         texts, up = [], []
+        now = time.monotonic()
         with self._lock:
+            for i in [i for i in self._last if i not in {w for w, _ in got}]:
+                del self._last[i]  # no longer a worker of this supervisor
+                self._streak.pop(i, None)
             for i, t in got:
                 up.append((i, bool(t)))
                 if t:
-                    self._last[i] = t
+                    self._last[i] = (t, now)
+                    self._streak[i] = 0
                 else:
                     self._failures[i] = self._failures.get(i, 0) + 1
-                    t = self._last.get(i)
+                    self._streak[i] = self._streak.get(i, 0) + 1
+                    last = self._last.get(i)
+                    if last is not None and (self._streak[i] > self.stale_after or now - last[1] > self.stale_s):
+                        del self._last[i]
+                        last = None
+                    t = last[0] if last is not None else None
                 if t:
                     texts.append(t)
             fails = dict(self._failures)

@@ -25,7 +25,12 @@ int api_h1_request_text(PyObject* method, PyObject* url, PyObject* params, PyObj
 PyObject* api_h1_response(PyObject* parsed, PyObject* full);  // py_h1call.cpp
 int api_h1_origin_key(PyObject* method, PyObject* url, PyObject* params, Py_ssize_t* key_len);  // py_h1call.cpp
 
-const NativeApi g_api = {kNativeApiAbi, api_h1_origin_key, api_h1_request_text, api_h1_response, url_with_query};
+bool is_h1_parser(PyObject* o);  // py_http.cpp
+int h1_parser_start_c(PyObject* o, bool head);
+PyObject* h1_parser_feed_c(PyObject* o, const char* data, size_t n);
+
+const NativeApi g_api = {kNativeApiAbi,  api_h1_origin_key, api_h1_request_text, api_h1_response,
+                         url_with_query, is_h1_parser,      h1_parser_start_c,   h1_parser_feed_c};
 
 namespace {
 

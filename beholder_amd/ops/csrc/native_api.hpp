@@ -18,7 +18,7 @@
 namespace beholder {
 
 constexpr const char* kNativeApiName = "beholder_amd.ops._native._C_API";
-constexpr uint32_t kNativeApiAbi = 1;
+constexpr uint32_t kNativeApiAbi = 2;
 
 struct NativeApi {
   uint32_t abi;  // kNativeApiAbi
@@ -40,6 +40,11 @@ struct NativeApi {
   PyObject* (*h1_response)(PyObject* parsed, PyObject* full);
   // url + "?" + encode_query(params) for a non-empty dict (restler's URL), else url. New reference.
   PyObject* (*url_with_query)(PyObject* url, PyObject* params);
+  // H1Parser.start(head=...) / .feed(data) as the NetConn calls them (py_http.cpp): exact
+  // H1Parser only (is_h1_parser). start: 0 or -1; feed: the parse result (None: incomplete).
+  bool (*is_h1_parser)(PyObject* o);
+  int (*h1_parser_start)(PyObject* parser, bool head);
+  PyObject* (*h1_parser_feed)(PyObject* parser, const char* data, size_t n);
 };
 
 constexpr const char* kSinkHookName = "beholder_amd.sink_hook";

@@ -8,8 +8,8 @@
 //     h1_request_text, py_h1call.cpp): request line with the encodeURIComponent query, Host,
 //     Authorization, User-Agent (+ Content-Length: 0 for PUT/POST), copied into the stub's
 //     send buffer as the NetConn copies them into its output buffer;
-//   * the canned answer (`200 {}` as the bench's HTTP fake sends it) goes through an H1Parser
-//     (parser.start(head=...), parser.feed(bytes)), as the NetConn's reply dispatch does;
+//   * the canned answer (`200 {}` as the bench's HTTP fake sends it) goes through an H1Parser,
+//     started and fed through the same C entry points the NetConn's reply dispatch uses;
 //   * the HttpResponse is built by the H1 client's own code (h1_response) with the request's
 //     URL, and the request is counted and logged as (METHOD, url) in the client's bounded deque.
 //
@@ -75,6 +75,7 @@ struct RecorderObject {
   PyObject_HEAD PyObject* append;  // calls.append (bound method of the client's deque)
   PyObject* ok;                    // MODE_URL: the shared `200 {}` response
   PyObject* ready;                 // MODE_URL: Ready(ok), shared by every answer
+  PyObject* parser;                // the H1Parser
   PyObject* start;                 // parser.start
   PyObject* feed;                  // parser.feed
   PyObject* response;              // bytes: the canned answer
@@ -140,6 +141,7 @@ int recorder_init(RecorderObject* self, PyObject* args, PyObject* kwds) {
   Py_XSETREF(self->append, app);
   Py_XSETREF(self->ok, Py_NewRef(ok));
   Py_XSETREF(self->ready, ready);
+  Py_XSETREF(self->parser, Py_NewRef(parser));
   Py_XSETREF(self->start, st);
   Py_XSETREF(self->feed, fd);
   Py_XSETREF(self->response, Py_NewRef(response));
@@ -155,6 +157,7 @@ int recorder_traverse(RecorderObject* self, visitproc visit, void* arg) {
   Py_VISIT(self->append);
   Py_VISIT(self->ok);
   Py_VISIT(self->ready);
+  Py_VISIT(self->parser);
   Py_VISIT(self->start);
   Py_VISIT(self->feed);
   Py_VISIT(self->origin_fn);
@@ -166,6 +169,7 @@ int recorder_clear(RecorderObject* self) {
   Py_CLEAR(self->append);
   Py_CLEAR(self->ok);
   Py_CLEAR(self->ready);
+  Py_CLEAR(self->parser);
   Py_CLEAR(self->start);
   Py_CLEAR(self->feed);
   Py_CLEAR(self->response);
@@ -262,11 +266,18 @@ PyObject* record_core(RecorderObject* self, PyObject* method, PyObject* url, PyO
 PyObject* answer(RecorderObject* self, PyObject* method, PyObject* full) {
   int head = PyObject_RichCompareBool(method, s_HEAD, Py_EQ);
   if (head < 0) return nullptr;
-  PyObject* args[1] = {head ? Py_True : Py_False};
-  PyObject* r = PyObject_Vectorcall(self->start, args, 0, kw_head);  // parser.start(head=head)
-  if (!r) return nullptr;
-  Py_DECREF(r);
-  PyObject* parsed = PyObject_CallOneArg(self->feed, self->response);
+  PyObject* parsed;
+  if (self->parser && g_api->is_h1_parser(self->parser)) {  // as the NetConn drives its parser
+    if (g_api->h1_parser_start(self->parser, head != 0) < 0) return nullptr;
+    parsed = g_api->h1_parser_feed(self->parser, PyBytes_AS_STRING(self->response),
+                                   size_t(PyBytes_GET_SIZE(self->response)));
+  } else {
+    PyObject* args[1] = {head ? Py_True : Py_False};
+    PyObject* r = PyObject_Vectorcall(self->start, args, 0, kw_head);  // parser.start(head=head)
+    if (!r) return nullptr;
+    Py_DECREF(r);
+    parsed = PyObject_CallOneArg(self->feed, self->response);
+  }
   if (!parsed) return nullptr;
   if (parsed == Py_None) {
     Py_DECREF(parsed);

@@ -135,3 +135,34 @@ def test_cluster_metrics_serve_a_missed_worker_from_its_last_exposition(monkeypa
     assert val(second, 'beholder_cluster_worker_up{worker="0"}') == 0
     assert val(second, 'beholder_cluster_worker_up{worker="1"}') == 1
     assert val(third, 'beholder_cluster_scrape_failures_total{worker="0"}') == 1
+
+
+def test_cluster_metrics_stop_serving_a_worker_that_keeps_failing(monkeypatch):
+    """a dead or wedged worker's last exposition is served for at most `stale_after`
+    consecutive failed scrapes (or `stale_s` seconds); a worker no longer in the supervisor's
+    list is forgotten at once."""
+    from beholder_amd.metrics import aggregate as agg
+    answers = {1: ["c_total 5\n"] + [None] * 4, 2: ["c_total 1\n"] * 5}
+    workers = [(0, 1), (1, 2)]
+
+    def fake_fetch(url, timeout=2.0):
+        port = int(url.split(":")[2].split("/")[0])
+        return answers[port].pop(0)
+    monkeypatch.setattr(agg, "fetch", fake_fetch)
+    srv = agg.ClusterMetricsServer("127.0.0.1", 0, lambda: list(workers), lambda: True, stale_after=2)
+
+    def val(text):
+        return float([ln for ln in text.splitlines() if ln.startswith("c_total ")][0].split()[-1])
+    got = [val(srv.merged_metrics()) for _ in range(4)]
+    assert got == [6, 6, 6, 1]  # scrape ok, 2 failures served stale, the 3rd drops it
+    srv2 = agg.ClusterMetricsServer("127.0.0.1", 0, lambda: list(workers), lambda: True, stale_s=0.0)
+    answers[1] = ["c_total 5\n", None]
+    answers[2] = ["c_total 1\n"] * 2
+    assert val(srv2.merged_metrics()) == 6
+    import time as _t
+    _t.sleep(0.01)
+    assert val(srv2.merged_metrics()) == 1  # older than stale_s: not served
+    answers[2] = ["c_total 1\n"]
+    workers[:] = [(1, 2)]
+    srv2.merged_metrics()
+    assert 0 not in srv2._last

@@ -67,3 +67,16 @@ def test_due_latencies_from_the_producer_schedule():
     assert d["due_to_ack_us"]["p50"] == (9_000 + 50) / 1e3 and d["due_to_ack_us"]["max"] == (9_000 + 99) / 1e3
     assert _due_latencies(S(), prod, {"dropped_total": 3}) == {}
     assert _due_latencies(S(), SimpleNamespace(offered=101, rate=rate, t0_ns=t0), {"dropped_total": 0}) == {}
+
+
+def test_a_long_stall_that_began_well_before_the_delivery_is_still_seen():
+    """ADVICE r4: a 2 s stall that started 1.5 s before the delivery started covers all of it;
+    the lookback is the longest stall, not a fixed 200 ms."""
+    from beholder_amd.bench.stallmon import attribute
+    s0 = 10_000_000_000
+    stall = (s0, s0 + 2_000_000_000)
+    start = s0 + 1_500_000_000
+    slow = [(start - 10, start, start + 5_000_000)]
+    out = attribute(slow, {"pg": [stall], "http": [(start + 4_000_000, start + 4_100_000)]})
+    assert out["blamed"]["pg"] == 1 and out["blamed"]["none"] == 0
+    assert out["time_share"]["pg"] == 1.0
