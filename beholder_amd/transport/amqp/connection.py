@@ -286,6 +286,55 @@ class Channel:
             cb(self, err)
 
 
+class _Protocol(asyncio.Protocol):
+    """The socket side of a :class:`Connection`: bytes go to ``Connection._on_data`` as they
+    arrive (no StreamReader buffer, no read-loop coroutine resumed per read: one callback per
+    socket read, the way the loop delivers them), writes go to the transport directly, and
+    ``pause_writing`` / ``resume_writing`` give the publisher its back-pressure."""
+
+    def __init__(self, conn: "Connection"):
+        self.conn = conn
+        self.transport: Optional[asyncio.Transport] = None
+        self.paused = False
+        self._drain: List[asyncio.Future] = []
+        self.closed: Optional[asyncio.Future] = None
+
+    def connection_made(self, transport) -> None:
+        self.transport = transport
+        self.closed = asyncio.get_running_loop().create_future()
+
+    def data_received(self, data: bytes) -> None:
+        self.conn._on_data(data)
+
+    def eof_received(self):
+        return False  # close the transport: connection_lost follows
+
+    def connection_lost(self, exc) -> None:
+        if self.closed is not None and not self.closed.done():
+            self.closed.set_result(None)
+        self._wake_drain()
+        self.conn._on_transport_lost(exc)
+
+    def pause_writing(self) -> None:
+        self.paused = True
+
+    def resume_writing(self) -> None:
+        self.paused = False
+        self._wake_drain()
+
+    def _wake_drain(self) -> None:
+        for f in self._drain:
+            if not f.done():
+                f.set_result(None)
+        self._drain.clear()
+
+    async def drain(self) -> None:
+        if self.paused and self.transport is not None and not self.transport.is_closing():
+            f = asyncio.get_running_loop().create_future()
+            self._drain.append(f)
+            await f
+
+
 class Connection:
     def __init__(self, url: str, *, heartbeat: Optional[int] = None, connect_timeout: float = 10.0,
                  logger=None, on_lost: Optional[Callable[[Optional[BaseException]], None]] = None,
@@ -308,14 +357,14 @@ class Connection:
         self.server_properties: Dict[str, Any] = {}
         self.is_open = False
         self.blocked = False
-        self._reader: Optional[asyncio.StreamReader] = None
-        self._writer: Optional[asyncio.StreamWriter] = None
+        self._proto: Optional[_Protocol] = None
+        self._transport: Optional[asyncio.Transport] = None
+        self._aborting = False  # the transport is being closed on purpose: its loss is not reported
         self._parser = wire.FrameParser(0)
         self._channels: Dict[int, Channel] = {}
         self._ids = itertools.count(1)
         self._ctags = itertools.count(1)
         self._ctag_prefix = f"{os.getpid()}-{id(self):x}"
-        self._rx_task: Optional[asyncio.Task] = None
         self._hb_task: Optional[asyncio.Task] = None
         self._wbuf = bytearray()
         self._flush_scheduled = False
@@ -348,13 +397,13 @@ class Connection:
                 ssl_ctx.check_hostname = False
                 ssl_ctx.verify_mode = ssl.CERT_NONE
             server_hostname = p.get("server_name") or p["host"]
-        self._reader, self._writer = await asyncio.wait_for(
-            asyncio.open_connection(p["host"], p["port"], ssl=ssl_ctx, server_hostname=server_hostname),
-            self.connect_timeout)
         self._handshake = loop.create_future()
-        self._writer.write(wire.PROTOCOL_HEADER)
+        self._transport, self._proto = await asyncio.wait_for(
+            loop.create_connection(lambda: _Protocol(self), p["host"], p["port"], ssl=ssl_ctx,
+                                   server_hostname=server_hostname),
+            self.connect_timeout)
+        self._transport.write(wire.PROTOCOL_HEADER)
         self._last_rx = self._last_tx = time.monotonic()
-        self._rx_task = loop.create_task(self._read_loop())
         try:
             await asyncio.wait_for(asyncio.shield(self._handshake), self.connect_timeout)
         except BaseException:
@@ -400,17 +449,32 @@ class Connection:
     def _write_now(self, data: bytes) -> None:
         """Append and send at once (with anything already queued, in order): the ack flush runs
         once per loop iteration already, so it need not wait for another one."""
+        t = self._transport
+        if not self._wbuf and t is not None and not t.is_closing():  # nothing queued: no copy
+            try:
+                t.write(data)
+            except (ConnectionError, RuntimeError) as e:
+                self._lost(e)
+                return
+            self.bytes_out += len(data)
+            self._last_tx = time.monotonic()
+            return
         self._wbuf += data
         self._flush()
 
     def _flush(self) -> None:
         self._flush_scheduled = False
-        if not self._wbuf or self._writer is None:
+        t = self._transport
+        if not self._wbuf or t is None:
+            return
+        if t.is_closing():
+            self._wbuf.clear()
+            self._lost(ConnectionError("connection is closed"))
             return
         data = bytes(self._wbuf)
         self._wbuf.clear()
         try:
-            self._writer.write(data)
+            t.write(data)
         except (ConnectionError, RuntimeError) as e:
             self._lost(e)
             return
@@ -418,47 +482,47 @@ class Connection:
         self._last_tx = time.monotonic()
 
     async def _maybe_drain(self) -> None:
-        w = self._writer
-        if w is not None and w.transport.get_write_buffer_size() > (4 << 20):
+        t = self._transport
+        if t is not None and t.get_write_buffer_size() > (4 << 20):
             self._flush()
-            await w.drain()
+            await self._proto.drain()
 
     # ------------------------------------------------------------- reads ---
-    async def _read_loop(self) -> None:
-        err: Optional[BaseException] = None
-        try:
-            while True:
-                data = await self._reader.read(1 << 17)
-                if not data:
-                    err = ConnectionError("connection closed by peer")
-                    break
-                self.bytes_in += len(data)
-                self._last_rx = time.monotonic()
-                demux = self._demux
-                if demux is not None:
-                    before = demux.passthrough
-                    try:
-                        items = demux.feed(data)
-                    except ValueError as e:
-                        raise wire.FrameError(str(e), wire.FRAME_ERROR) from None
-                    if demux.passthrough == before:
-                        if items:
-                            self.on_deliveries(items)  # only deliveries: hand over the whole list
-                    else:
-                        on_deliveries = self.on_deliveries
-                        for it in items:  # control frames interleaved: keep stream order
-                            if type(it) is tuple:
-                                self._dispatch(*it)
-                            else:
-                                on_deliveries([it])
-                else:
-                    for ftype, ch, payload in self._parser.feed(data):
-                        self._dispatch(ftype, ch, payload)
-        except asyncio.CancelledError:
+    def _on_data(self, data: bytes) -> None:
+        """One socket read (``_Protocol.data_received``): frames to the native delivery demux or
+        the Python parser. A protocol error ends the connection as a loss."""
+        if self._aborting:
             return
+        self.bytes_in += len(data)
+        self._last_rx = time.monotonic()
+        try:
+            demux = self._demux
+            if demux is not None:
+                before = demux.passthrough
+                try:
+                    items = demux.feed(data)
+                except ValueError as e:
+                    raise wire.FrameError(str(e), wire.FRAME_ERROR) from None
+                if demux.passthrough == before:
+                    if items:
+                        self.on_deliveries(items)  # only deliveries: hand over the whole list
+                else:
+                    on_deliveries = self.on_deliveries
+                    for it in items:  # control frames interleaved: keep stream order
+                        if type(it) is tuple:
+                            self._dispatch(*it)
+                        else:
+                            on_deliveries([it])
+            else:
+                for ftype, ch, payload in self._parser.feed(data):
+                    self._dispatch(ftype, ch, payload)
         except (ConnectionError, OSError, AmqpError) as e:
-            err = e
-        self._lost(err)
+            self._lost(e)
+
+    def _on_transport_lost(self, exc: Optional[BaseException]) -> None:
+        if self._aborting:
+            return
+        self._lost(exc if exc is not None else ConnectionError("connection closed by peer"))
 
     def _dispatch(self, ftype: int, ch: int, payload: bytes) -> None:
         if ftype == wire.FRAME_HEARTBEAT:
@@ -553,9 +617,9 @@ class Connection:
             ch._closed(err if isinstance(err, AmqpError) else AmqpError(str(err or "connection lost")))
         if self._close_waiter and not self._close_waiter.done():
             self._close_waiter.set_result(True)
-        if self._writer is not None:
+        if self._transport is not None:
             try:
-                self._writer.close()
+                self._transport.close()
             except Exception:  # noqa: BLE001
                 pass
         if self._hb_task is not None:
@@ -569,20 +633,20 @@ class Connection:
         self.is_open = False
         if self._hb_task is not None:
             self._hb_task.cancel()
-        if self._rx_task is not None and self._rx_task is not asyncio.current_task():
-            self._rx_task.cancel()
-            try:
-                await self._rx_task
-            except (asyncio.CancelledError, Exception):  # noqa: BLE001
-                pass
-        if self._writer is not None:
+        t, proto = self._transport, self._proto
+        if t is not None:
             try:
                 self._flush()
-                self._writer.close()
-                await asyncio.wait_for(self._writer.wait_closed(), 2)
             except Exception:  # noqa: BLE001
                 pass
-            self._writer = None
+            self._aborting = True  # from here on, reads and the transport's loss are ours
+            try:
+                t.close()
+                if proto is not None and proto.closed is not None:
+                    await asyncio.wait_for(asyncio.shield(proto.closed), 2)
+            except Exception:  # noqa: BLE001
+                pass
+            self._transport = None
 
 
 async def connect(url: str, **kw) -> Connection:
