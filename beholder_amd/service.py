@@ -40,6 +40,7 @@ from .handlers import TelemetryHandlers, err_message, native_handlers
 from .metrics import MetricsServer, NativeHistogramView, Registry, default_metrics
 from .metrics.registry import Gauge
 from .parallel.ordering import KeyedSerializer
+from .utils.waits import Signal
 from .sinks import AiohttpClient, EmbyClient, H1Client, HttpClient, SinkObserver, TelegramClient, TrelloClient
 from .sinks.ratelimit import from_config as sink_policy
 from .store import MediaStore, open_store
@@ -139,7 +140,7 @@ class Service:
         self._routes: List[Optional[Handler]] = [None] * len(T.TOPIC_NAMES_BY_ID)
         # handlers suspended on I/O, at most `prefetch` (index.js:43); drivers report back in C
         self._inflight = Window(self.prefetch, self._on_handler_error, self._on_wake)
-        self._slot_free: Optional[asyncio.Event] = None
+        self._slot_free: Optional[Signal] = None
         self._idle: Optional[asyncio.Event] = None  # set when the last suspended handler finishes
         self._stop = False
         self._running = False
@@ -446,7 +447,7 @@ class Service:
         if not self._initialized:
             await self.init()
         self._running = True
-        self._slot_free = asyncio.Event()
+        self._slot_free = Signal()
         flusher = asyncio.ensure_future(self._flush_logs_periodically())
         log = self.log
         routes = self._routes
@@ -463,8 +464,13 @@ class Service:
         tracer = self.tracer
         routes = tuple(routes)
         on_error, on_suspend, on_unroutable = self._on_handler_error, self._inflight, self._unroutable
+        # a source that counts its waits (`idle_wakeups`): a batch that came after a wait was
+        # preceded by a trip through the loop already, so it needs no extra yield (below)
+        src = self.source
+        counts_waits = isinstance(getattr(src, "idle_wakeups", None), int)
+        last_wakeups = -1
         try:
-            async for batch in self.source.batches():
+            async for batch in src.batches():
                 if native and tracer is not None:
                     await self._dispatch_sampled(batch, routes, on_error, on_suspend, on_unroutable)
                 elif native:
@@ -482,6 +488,11 @@ class Service:
                 log.flush()
                 if self._stop:
                     break
+                if counts_waits:
+                    w = src.idle_wakeups
+                    if w != last_wakeups:  # this batch followed a wait: the loop ran just before it
+                        last_wakeups = w
+                        continue
                 await sleep(0)  # keep timers / the metrics endpoint responsive under sustained load
         finally:
             self._running = False

@@ -28,6 +28,7 @@ from typing import Dict, List, Optional, Sequence
 
 from ...ops import AckBatcher, Delivery, Settler
 from ...topics import TOPIC_IDS, topic_id
+from ...utils.waits import Signal
 from ..base import Source
 from .connection import Channel, Connection
 from .topology import Topology
@@ -66,7 +67,8 @@ class AmqpSource(Source):
         self._conn: Optional[Connection] = None
         self._ch: Optional[Channel] = None
         self._pending: List = []
-        self._event: Optional[asyncio.Event] = None
+        self._event: Optional[Signal] = None
+        self.idle_wakeups = 0  # batches that came after the consumer waited for deliveries
         self._loop: Optional[asyncio.AbstractEventLoop] = None  # set at start(): one lookup, not one per flush
         self._closing = False
         self._stopping = False
@@ -90,7 +92,7 @@ class AmqpSource(Source):
         for t in topics:
             topic_id(t)
         self._topics = list(topics)
-        self._event = asyncio.Event()
+        self._event = Signal()
         self._loop = asyncio.get_running_loop()
         delay = self.backoff_initial
         for attempt in range(self.retries + 1):
@@ -185,6 +187,7 @@ class AmqpSource(Source):
                 return
             self._event.clear()
             await self._event.wait()
+            self.idle_wakeups += 1  # this batch came after a wait: the consumer yielded to the loop
 
     async def stop_consuming(self) -> None:
         """``basic.cancel`` every consumer; the channel stays open so acks of in-flight

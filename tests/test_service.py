@@ -364,3 +364,64 @@ def test_loop_lag_and_gc_pause_histograms():
     assert svc.loop_lag.count >= 3 and svc.loop_lag.max >= 30_000_000
     assert svc.gc_pause.count >= 1
     assert after == n_cb - 1
+
+
+def test_the_loop_stays_responsive_under_sustained_load():
+    """The dispatch loop yields to the event loop at least every other batch: a batch that came
+    after the source waited needs no extra yield, one that did not gets `sleep(0)` (a timer keeps
+    ticking while a 200k-event stream that never runs dry goes through)."""
+    from beholder_amd.bench.generator import Workload, bench_config
+    from beholder_amd.transport.ingest import BytesSource
+    w = Workload(n_media=200, seed=5)
+    data = w.framed(200_000)
+    ticks = []
+
+    async def go():
+        svc = Service(Config.from_dict(bench_config()), source=BytesSource(data, batch=256), store=MemoryStore(w.media),
+                      http=RecordingHttpClient(keep=0), logger=Logger(stream=MemoryStream()), serve_metrics=False)
+        await svc.init()
+
+        async def ticker():
+            while True:
+                await asyncio.sleep(0.002)
+                ticks.append(1)
+        t = asyncio.ensure_future(ticker())
+        loop = asyncio.get_running_loop()
+        t0 = loop.time()
+        st = await svc.run()
+        took = loop.time() - t0
+        t.cancel()
+        await svc.close()
+        return st, took
+    st, took = asyncio.run(go())
+    assert st["source"]["acked"] == 200_000
+    assert len(ticks) >= max(3, int(took / 0.002 * 0.1)), (len(ticks), took)  # starved: ~0
+
+
+def test_signal_has_event_semantics():
+    from beholder_amd.utils.waits import Signal
+
+    async def go():
+        s = Signal()
+        assert not s.is_set()
+        got = []
+
+        async def waiter(i):
+            await s.wait()
+            got.append(i)
+        ts = [asyncio.ensure_future(waiter(i)) for i in range(3)]
+        await asyncio.sleep(0)
+        assert got == []
+        s.set()
+        await asyncio.sleep(0)
+        assert sorted(got) == [0, 1, 2] and s.is_set()
+        await s.wait()  # set: returns at once
+        s.clear()
+        t = asyncio.ensure_future(s.wait())
+        await asyncio.sleep(0)
+        assert not t.done()
+        s.set()
+        await t
+        for x in ts:
+            await x
+    asyncio.run(go())
