@@ -210,13 +210,16 @@ class SharedQueueBroker:
         if n:
             self.dup_acks += 1
         else:
-            self.acked += 1
-            if self.acked == self.total:
-                self.t_done = time.perf_counter()
-                self.cpu_s = _cpu_now() - self.cpu_first
-                self.done.set()
+            self._add_acked(1)
         if n < 255:
             self.ack_counts[idx] = n + 1
+
+    def _add_acked(self, k: int) -> None:
+        self.acked += k
+        if self.acked == self.total:
+            self.t_done = time.perf_counter()
+            self.cpu_s = _cpu_now() - self.cpu_first
+            self.done.set()
 
     def _take(self, n: int) -> List[Tuple[int, bool]]:
         """Up to n events off the shared head: requeued ones first (redelivered)."""
@@ -257,6 +260,19 @@ class SharedQueueBroker:
         async def pump():
             await self.go.wait()
             content = self.content(channel)
+            events = self.events
+            # per queue: the frame header + basic.deliver up to the delivery tag, and the rest of
+            # it (redelivered flag, exchange "", routing key, frame end) for both flag values:
+            # a delivery is then four appends (the tag packed in place)
+            pre: Dict[str, bytes] = {}
+            post: Dict[Tuple[str, bool], bytes] = {}
+            for q in mhead:
+                rk = q.encode()
+                size = len(mhead[q]) + 8 + 1 + 1 + 1 + len(rk)
+                pre[q] = struct.pack(">BHI", 1, channel, size) + mhead[q]
+                for rd in (False, True):
+                    post[(q, rd)] = (b"\x01" if rd else b"\x00") + b"\x00" + bytes([len(rk)]) + rk + b"\xce"
+            pack_tag = struct.Struct(">Q").pack
             while not self.done.is_set():
                 window = prefetch * max(1, len(consumers)) if prefetch else 512
                 room = window - state["open"]
@@ -275,21 +291,24 @@ class SharedQueueBroker:
                 if self.t_first is None:
                     self.t_first = time.perf_counter()
                     self.cpu_first = _cpu_now()
-                parts = []
+                buf = bytearray()
+                tag = len(tags)
+                nred = 0
                 for idx, redelivered in batch:
-                    q = self.events[idx][0]
+                    q = events[idx][0]
+                    tag += 1
                     tags.append(idx)
-                    settled.append(0)
-                    rk = q.encode()
-                    meth = mhead[q] + struct.pack(">Q", len(tags)) + (b"\x01" if redelivered else b"\x00") + \
-                        b"\x00" + bytes([len(rk)]) + rk
-                    parts.append(struct.pack(">BHI", 1, channel, len(meth)) + meth + b"\xce")
-                    parts.append(content[idx])
+                    buf += pre[q]
+                    buf += pack_tag(tag)
+                    buf += post[(q, redelivered)]
+                    buf += content[idx]
+                    nred += redelivered
+                settled.extend(bytes(len(batch)))
                 state["open"] += len(batch)
                 self.per_conn[conn] += len(batch)
                 self.sent += len(batch)
-                self.redelivered += sum(1 for _, rd in batch if rd)
-                w.write(b"".join(parts))
+                self.redelivered += nred
+                w.write(buf)
                 await w.drain()
 
         pump_task = None
@@ -309,9 +328,23 @@ class SharedQueueBroker:
                                 self.unknown_acks += 1
                                 tag = len(tags)
                             low = state["low"]
-                            for t in range(low, tag):
-                                if not settled[t]:
-                                    settle_tag(t)
+                            counts = self.ack_counts
+                            n_new = 0
+                            for t in range(low, tag):  # settle_tag, inlined: one loop per ack frame
+                                if settled[t]:
+                                    continue
+                                settled[t] = 1
+                                idx = tags[t]
+                                c = counts[idx]
+                                if c:
+                                    self.dup_acks += 1
+                                else:
+                                    n_new += 1
+                                if c < 255:
+                                    counts[idx] = c + 1
+                                state["open"] -= 1
+                            if n_new:
+                                self._add_acked(n_new)
                         else:
                             settle_tag(tag - 1)
                         low = state["low"]
