@@ -598,8 +598,8 @@ def soak_extras(a) -> dict:
 
 
 # Fixed-work calibrations around the headline, each the minimum of CALIB_REPS runs (ns):
-#   calib_ns      ops.calib: an L1-resident integer loop (core clock, time-sharing of the core);
-#   calib_mem_ns  ops.calib_mem: a dependent random walk over 8 MiB (L3 / memory latency, which
+#   calib_ns      bench_native.calib: an L1-resident integer loop (core clock, time-sharing of the core);
+#   calib_mem_ns  bench_native.calib_mem: a dependent random walk over 8 MiB (L3 / memory latency, which
 #                 other tenants' traffic moves);
 #   calib_py_ns   a fixed pure-Python loop (the interpreter: dict, str and int churn, as the
 #                 consumer's Python glue does).
@@ -683,7 +683,7 @@ NOTES = ("CPU event-consumer workload (the reference has no device compute; see 
          "connect (+TLS handshake) and the wait of requests queued for a connection (the warm-up); "
          "*_fakes_cpu_us_per_event = each fake's CPU over the measured window per event; "
          "*_e2e_calib_ns = the calib loop right before that phase; "
-         "calib_ns = fixed-work C loop (ops.calib) "
+         "calib_ns = fixed-work C loop (bench_native.calib) "
          "around the headline, value_calibrated = value * calib_ns / calib_ref_ns; "
          "plumbing_* = BASELINE config 1 through `python -m beholder_amd run --source stdin`, "
          "/metrics scraped before exit")
