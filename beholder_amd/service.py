@@ -141,6 +141,7 @@ class Service:
         # handlers suspended on I/O, at most `prefetch` (index.js:43); drivers report back in C
         self._inflight = Window(self.prefetch, self._on_handler_error, self._on_wake)
         self._slot_free: Optional[Signal] = None
+        self._slot_waits = 0  # times the dispatch loop waited for a prefetch slot
         self._idle: Optional[asyncio.Event] = None  # set when the last suspended handler finishes
         self._stop = False
         self._running = False
@@ -471,6 +472,7 @@ class Service:
         last_wakeups = -1
         try:
             async for batch in src.batches():
+                waited = self._slot_waits
                 if native and tracer is not None:
                     await self._dispatch_sampled(batch, routes, on_error, on_suspend, on_unroutable)
                 elif native:
@@ -493,6 +495,8 @@ class Service:
                     if w != last_wakeups:  # this batch followed a wait: the loop ran just before it
                         last_wakeups = w
                         continue
+                if self._slot_waits != waited:  # it waited for a prefetch slot: the loop ran meanwhile
+                    continue
                 await sleep(0)  # keep timers / the metrics endpoint responsive under sustained load
         finally:
             self._running = False
@@ -648,6 +652,7 @@ class Service:
     async def _wait_slots(self) -> None:
         while len(self._inflight) >= self.prefetch:
             self._slot_free.clear()
+            self._slot_waits += 1
             await self._slot_free.wait()
 
     def _on_handler_error(self, d, exc: BaseException) -> None:
