@@ -50,7 +50,7 @@ def test_bench_single_rank_contract(tmp_path):
     full_path = str(tmp_path / "full.json")
     r = subprocess.run([sys.executable, "bench.py", *SMALL, "--procs-per-rank", "2", "--all-procs-steps", "1",
                         "--io-events", "2000", "--e2e-events", "4000", "--soak-events", "20000",
-                        "--shared-queue-events", "3000", "--full-out", full_path],
+                        "--shared-queue-events", "3000", "--e2e-repeats", "2", "--full-out", full_path],
                        cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.strip()][-1]
@@ -98,6 +98,8 @@ def test_bench_single_rank_contract(tmp_path):
     # the e2e phases say what else could have moved them
     assert 4000 - 400 - 100 <= out["tcp_e2e_measured_events"] <= 4000 - 400 and out["tcp_e2e_calib_ns"] > 0
     assert set(out["tcp_e2e_fakes_cpu_us_per_event"]) == {"broker", "pg", "http"}
+    assert len(out["tcp_e2e_runs"]["events_per_sec"]) == 2 and out["tcp_e2e_events_per_sec"] in \
+        out["tcp_e2e_runs"]["events_per_sec"]
     assert out["tcp_e2e_sys_cpu_us_per_event"] >= 0 and out["tcp_e2e_minflt"] >= 0
     # competing consumers on one queue (run --workers N), every event acked exactly once
     ns = bench.shared_queue_workers(out["cpus_available"])
