@@ -168,7 +168,9 @@ class SharedQueueBroker:
     RabbitMQ does. ``cpu_s``: this process's CPU from the first delivery to the last ack.
     """
 
-    def __init__(self, events: List[Tuple[str, bytes]], port: int = 0, consumers: int = 1):
+    def __init__(self, events: List[Tuple[str, bytes]], port: int = 0, consumers: int = 1, progress_every: int = 0):
+        self.progress_every = progress_every  # print "PROGRESS acked=N" each time N more events are acked
+        self._next_progress = progress_every or 0
         self.events = events
         self.bodies = [body for _, body in events]
         self._content: Dict[int, List[bytes]] = {}  # channel -> pre-encoded header + body frames
@@ -216,6 +218,9 @@ class SharedQueueBroker:
 
     def _add_acked(self, k: int) -> None:
         self.acked += k
+        if self.progress_every and self.acked >= self._next_progress:
+            self._next_progress = (self.acked // self.progress_every + 1) * self.progress_every
+            print(f"PROGRESS acked={self.acked} connections={len(self.per_conn)}", flush=True)
         if self.acked == self.total:
             self.t_done = time.perf_counter()
             self.cpu_s = _cpu_now() - self.cpu_first
@@ -421,7 +426,7 @@ async def _main(a) -> None:
     w = Workload(n_media=a.media, seed=a.seed)
     events = [(TOPIC_NAMES_BY_ID[t], p) for t, p in w.events(a.events)]
     if a.shared:
-        sb = await SharedQueueBroker(events, a.port, consumers=a.consumers).start()
+        sb = await SharedQueueBroker(events, a.port, consumers=a.consumers, progress_every=a.progress_every).start()
         del w
         print(f"READY {sb.port}", flush=True)
         await sb.done.wait()
@@ -451,6 +456,8 @@ def main(argv=None) -> int:
                     help="competing consumers: any number of connections share the queues (SharedQueueBroker)")
     ap.add_argument("--consumers", type=int, default=1,
                     help="--shared: start delivering once this many connections have subscribed")
+    ap.add_argument("--progress-every", type=int, default=0,
+                    help="--shared: print a PROGRESS line each time this many more events are acked")
     asyncio.run(_main(ap.parse_args(argv)))
     return 0
 

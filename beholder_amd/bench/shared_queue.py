@@ -49,8 +49,13 @@ def _parse_kv(line: str) -> Dict[str, object]:
 
 
 def run_shared(workers: int, events: int, *, media: int = 10000, seed: int = 0, timeout_s: float = 120.0,
-               log_level: str = "info") -> dict:
-    """One shared-queue run with ``workers`` competing consumers; see the module docstring."""
+               log_level: str = "info", kill_one_after: int = 0) -> dict:
+    """One shared-queue run with ``workers`` competing consumers; see the module docstring.
+
+    ``kill_one_after``: once the broker reports that many events acked, one worker process gets
+    SIGKILL (a crash in the middle of the stream): the supervisor restarts it, the broker requeues
+    what the dead connection had un-acked (``redelivered``), and every event must still be acked
+    exactly once at the broker (tests/test_workers.py)."""
     import yaml
 
     from .generator import Workload, bench_config
@@ -58,14 +63,17 @@ def run_shared(workers: int, events: int, *, media: int = 10000, seed: int = 0, 
 
     port, bprocs = _spawn("beholder_amd.bench.replay_broker", 1,
                           ("--events", str(events), "--media", str(media), "--seed", str(seed), "--shared",
-                           "--consumers", str(workers)))
+                           "--consumers", str(workers), "--progress-every", str(kill_one_after)))
     broker = bprocs[0]
     lines: List[str] = []
     got_done = threading.Event()
+    progress = threading.Event()
 
     def read_broker():
         for ln in broker.stdout:
             lines.append(ln.strip())
+            if ln.startswith("PROGRESS "):
+                progress.set()
             if ln.startswith("FINAL "):
                 got_done.set()
         got_done.set()
@@ -93,6 +101,16 @@ def run_shared(workers: int, events: int, *, media: int = 10000, seed: int = 0, 
                                    preexec_fn=_die_with_parent())
             err: List[bytes] = []
             threading.Thread(target=lambda: err.append(sup.stderr.read()), daemon=True).start()
+            if kill_one_after:
+                def kill_one():
+                    import psutil
+                    if not progress.wait(timeout_s):
+                        return
+                    kids = psutil.Process(sup.pid).children()
+                    if kids:
+                        out["killed_worker_pid"] = kids[0].pid
+                        kids[0].kill()
+                threading.Thread(target=kill_one, daemon=True).start()
             if not got_done.wait(timeout_s):
                 raise RuntimeError(f"shared queue run with {workers} workers did not finish in {timeout_s:.0f} s")
             sup.send_signal(signal.SIGTERM)

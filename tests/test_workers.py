@@ -257,3 +257,17 @@ def test_worker_command_reruns_the_entry_module(monkeypatch):
     assert cli.worker_command() == [sys.executable, "-m", "beholder_amd"]
     fake.__spec__ = None
     assert cli.worker_command() == [sys.executable, "-m", "beholder_amd"]
+
+
+def test_shared_queue_worker_crash_requeues_and_still_acks_every_event_once():
+    """A worker SIGKILLed mid-stream: the supervisor restarts it, the broker requeues the dead
+    connection's un-acked deliveries (redelivered, as RabbitMQ does), and at the broker every
+    published event ends up acked exactly once (the reference's at-least-once consumption with
+    no loss: index.js acks after the handler, so nothing un-acked is lost)."""
+    from beholder_amd.bench.shared_queue import run_shared
+    r = run_shared(2, 60000, kill_one_after=4000)
+    assert r.get("killed_worker_pid"), r
+    assert r["supervisor_rc"] == 0, r.get("supervisor_stderr")
+    assert r["published"] == r["acked"] == 60000 and r["lost"] == 0 and r["unknown_acks"] == 0
+    assert r["dup_acks"] == 0 and r["exactly_once"]
+    assert r["redelivered"] > 0  # the dead connection's un-acked deliveries went to the other worker
