@@ -166,3 +166,15 @@ def test_http_tcp_both_clients_error_free():
     res = harness.run_config("http_tcp", events=20_000)
     for kind in ("h1", "aiohttp"):
         assert res[kind]["acked"] == 20_000 and res[kind]["errors"] == 0, (kind, res[kind]["error_samples"])
+
+
+def test_shared_queue_competing_consumers_on_the_box():
+    """The reference's scaling mode at full scale on the target machine: `run --workers 4` on one
+    shared queue, 50k events per worker, every event acked exactly once at the broker, the work
+    spread over all four workers."""
+    from beholder_amd.bench.shared_queue import run_shared
+    r = run_shared(4, 200_000)
+    assert r["supervisor_rc"] == 0, r.get("supervisor_stderr")
+    assert r["exactly_once"] and r["acked"] == r["published"] == 200_000
+    assert len(r["per_connection_delivered"]) == 4 and min(r["per_connection_delivered"]) > 20_000
+    assert r["events_per_sec"] > 100_000, r
