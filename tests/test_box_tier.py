@@ -82,7 +82,9 @@ def test_compiled_handlers_match_python_on_the_box():
 
 
 def test_bench_single_rank_full_path():
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "1"],
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "1",
+                          "--e2e-repeats", "1", "--e2e-events", "50000", "--shared-queue-events", "20000",
+                          "--full-out", ""],
                          capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-2000:]
     line = [x for x in out.stdout.splitlines() if x.startswith("{")][-1]
