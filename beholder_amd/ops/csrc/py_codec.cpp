@@ -318,64 +318,10 @@ bool decode_pbjs_into(CodecObject* self, pbjs::Reader& r, SlotVal* vals, bool* s
   return true;
 }
 
-// ---- recent short strings -----------------------------------------------------------------
-// The string fields of telemetry repeat: the media ids of the media in flight, a handful of
-// worker host names. A short ASCII field is looked up in a direct-mapped table of recently
-// decoded str objects (keyed by its bytes) and shared when the bytes match: no allocation, no
-// UTF-8 decode, and the str's cached hash serves the store's lookup by id. Any other field (long,
-// non-ASCII, empty) is decoded as before. str is immutable, so sharing one is invisible; the GIL
-// serialises the table.
-constexpr size_t kStrCacheSlots = 1 << 14;
-constexpr size_t kStrCacheMaxLen = 64;
-PyObject* g_str_cache[kStrCacheSlots];
-
-inline uint64_t mix64(uint64_t x) {
-  x ^= x >> 32;
-  x *= 0xd6e8feb86659fd93ull;
-  x ^= x >> 32;
-  return x;
-}
-
-// NULL: not cacheable (the caller decodes); else a new reference.
-PyObject* cached_ascii(const uint8_t* p, size_t n) {
-  if (n == 0 || n > kStrCacheMaxLen) return nullptr;
-  uint64_t h = 0x9E3779B97F4A7C15ull ^ n, hi = 0;
-  size_t i = 0;
-  for (; i + 8 <= n; i += 8) {
-    uint64_t w;
-    memcpy(&w, p + i, 8);
-    hi |= w;
-    h = mix64(h ^ w) + 0x632BE59BD9B4E019ull;
-  }
-  if (i < n) {
-    uint64_t w = 0;
-    memcpy(&w, p + i, n - i);
-    hi |= w;
-    h = mix64(h ^ w);
-  }
-  if (hi & 0x8080808080808080ull) return nullptr;  // not ASCII: the UTF-8 decoder's job
-  PyObject*& slot = g_str_cache[mix64(h) & (kStrCacheSlots - 1)];
-  PyObject* s = slot;
-  if (s && size_t(PyUnicode_GET_LENGTH(s)) == n && memcmp(PyUnicode_1BYTE_DATA(s), p, n) == 0)
-    return Py_NewRef(s);
-  PyObject* ns = PyUnicode_New(Py_ssize_t(n), 127);
-  if (!ns) return nullptr;
-  memcpy(PyUnicode_1BYTE_DATA(ns), p, n);
-  Py_XSETREF(slot, Py_NewRef(ns));
-  return ns;
-}
-
-// A decoded string field: the shared recent str, else PyUnicode_DecodeUTF8(errors).
-PyObject* string_value(const uint8_t* p, size_t n, const char* errors) {
-  PyObject* s = cached_ascii(p, n);
-  if (s || PyErr_Occurred()) return s;
-  return PyUnicode_DecodeUTF8(reinterpret_cast<const char*>(p), Py_ssize_t(n), errors);
-}
-
 PyObject* value_for(int kind, const SlotVal& v) {
   switch (kind) {
     case wire::K_STRING:
-      return string_value(v.s.p, v.s.n, "strict");
+      return PyUnicode_DecodeUTF8(reinterpret_cast<const char*>(v.s.p), Py_ssize_t(v.s.n), "strict");
     case wire::K_BYTES:
       return PyBytes_FromStringAndSize(reinterpret_cast<const char*>(v.s.p), Py_ssize_t(v.s.n));
     case wire::K_INT32:
@@ -442,7 +388,8 @@ PyObject* codec_decode_raw(PyObject* self_obj, const uint8_t* data, size_t len) 
     PyObject* v;
     if (seen[i]) {
       const int kind = (*self->fields)[i].kind;
-      v = pbjs_dialect && (kind == wire::K_STRING) ? string_value(vals[i].s.p, vals[i].s.n, "replace")
+      v = pbjs_dialect && (kind == wire::K_STRING) ? PyUnicode_DecodeUTF8(reinterpret_cast<const char*>(vals[i].s.p),
+                                                                          Py_ssize_t(vals[i].s.n), "replace")
                                                    : value_for(kind, vals[i]);
       if (!v) {
         Py_DECREF(out);
