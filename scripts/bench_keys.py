@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Prints the selected keys of one or more bench.py JSON lines side by side (box-run summaries)."""
+"""Prints the selected keys of bench.py JSON lines or full records (``--full-out``) side by side
+(box-run summaries)."""
 import json
 import sys
 
@@ -11,7 +12,10 @@ KEYS = ["value", "cpu_us_per_event", "thp", "headline_minflt", "calib_ns", "cali
         "rate_10k_p99_queue_latency_us", "rate_10k_p99_handle_latency_us", "rate_10k_p99_due_to_ack_us", "rate_10k_p99_due_to_recv_us", "rate_100k_p50_ingest_latency_us",
         "rate_100k_p99_ingest_latency_us", "rate_100k_p99_queue_latency_us", "rate_100k_p99_due_to_ack_us", "rate_100k_p99_due_to_recv_us", "rate_100k_dropped",
         "paced_nr_throttled",
-        "tcp_e2e_events_per_sec", "tcp_e2e_p50_handle_latency_us", "tcp_e2e_p999_handle_latency_us",
+        "tcp_e2e_events_per_sec", "tcp_e2e_cpu_us_per_event", "tcp_e2e_sys_cpu_us_per_event", "tcp_e2e_calib_ns",
+        "tcp_e2e_fakes_cpu_us_per_event", "tcp_e2e_runs", "shared_queue_events_per_sec",
+        "shared_queue_broker_cpu_us_per_event", "shared_queue_exactly_once",
+        "tcp_e2e_p50_handle_latency_us", "tcp_e2e_p999_handle_latency_us",
         "tcp_e2e_warmup_p999_handle_latency_us", "tcp_e2e_slow_blamed", "tcp_e2e_slow_time_share",
         "tcp_e2e_warmup_slow_blamed", "tcp_e2e_consumer_loop_lag_max_us", "tcp_e2e_fakes_loop_lag_max_us",
         "tcp_e2e_nr_throttled", "tcp_e2e_nivcsw",
@@ -37,7 +41,14 @@ def main(paths):
     rows = []
     for p in paths:
         with open(p) as f:
-            lines = [x for x in f.read().splitlines() if x.startswith("{")]
+            text = f.read()
+        try:  # a full record (bench.py --full-out): one JSON document with every key
+            doc = json.loads(text)
+            rows.append(doc if isinstance(doc, dict) else {})
+            continue
+        except ValueError:
+            pass
+        lines = [x for x in text.splitlines() if x.startswith("{")]  # a bench line (the last one)
         rows.append(json.loads(lines[-1]) if lines else {})
     for k in KEYS:
         if spread:
