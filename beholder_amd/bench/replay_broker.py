@@ -420,11 +420,54 @@ def _cpu_now() -> float:
     return ru.ru_utime + ru.ru_stime
 
 
+def _serve_native(events: List[Tuple[str, bytes]], a) -> None:
+    """``--shared`` on the native SharedBroker (ops/csrc_bench/shared_broker.cpp): the same protocol
+    subset, queue semantics and accounting as :class:`SharedQueueBroker`, on an epoll loop of its
+    own, so the shared-queue curve is not capped by this process. Prints the same READY /
+    PROGRESS / DONE / FINAL lines."""
+    import array
+    import threading
+
+    from ..ops.bench_native import SharedBroker
+    names = sorted({q for q, _ in events})
+    qi = {q: i for i, q in enumerate(names)}
+    pieces = [wire.encode_content(1, 60, body, None, 131072) for _, body in events]
+    offs = array.array("Q", [0])
+    for p in pieces:
+        offs.append(offs[-1] + len(p))
+    b = SharedBroker(b"".join(pieces), offs.tobytes(), bytes(qi[q] for q, _ in events), tuple(names), a.consumers)
+    del pieces
+    port = b.listen()
+    print(f"READY {port}", flush=True)
+    t = threading.Thread(target=b.run, args=(0.2,), name="shared-broker", daemon=True)
+    t.start()
+    every = a.progress_every
+    nxt = every
+    while t.is_alive():
+        t.join(0.005)
+        if every:
+            st = b.stats()
+            if st["acked"] >= nxt:
+                nxt = (st["acked"] // every + 1) * every
+                print(f"PROGRESS acked={st['acked']} connections={st['connections']}", flush=True)
+    st = b.stats()
+    line = (f"sent={st['sent']} acked={st['acked']} published={st['published']} dup_acks={st['dup_acks']} "
+            f"unknown_acks={st['unknown_acks']} lost={st['lost']} redelivered={st['redelivered']} "
+            f"connections={st['connections']} per_conn={','.join(map(str, st['per_conn']))} "
+            f"broker_s={st['broker_s']:.6f} cpu_s={st['cpu_s']:.6f}")
+    print("DONE " + line, flush=True)
+    print("FINAL " + line, flush=True)
+
+
 async def _main(a) -> None:
     from ..topics import TOPIC_NAMES_BY_ID
     from .generator import Workload
     w = Workload(n_media=a.media, seed=a.seed)
     events = [(TOPIC_NAMES_BY_ID[t], p) for t, p in w.events(a.events)]
+    if a.shared and not a.python:
+        del w
+        _serve_native(events, a)
+        return
     if a.shared:
         sb = await SharedQueueBroker(events, a.port, consumers=a.consumers, progress_every=a.progress_every).start()
         del w
@@ -458,6 +501,8 @@ def main(argv=None) -> int:
                     help="--shared: start delivering once this many connections have subscribed")
     ap.add_argument("--progress-every", type=int, default=0,
                     help="--shared: print a PROGRESS line each time this many more events are acked")
+    ap.add_argument("--python", action="store_true",
+                    help="--shared: the asyncio SharedQueueBroker instead of the native SharedBroker")
     asyncio.run(_main(ap.parse_args(argv)))
     return 0
 

@@ -5,9 +5,11 @@ service on the same RabbitMQ queues, each with prefetch 100; index.js:43,62,127,
 
 One measurement (:func:`run_shared`):
 
-* a :class:`~beholder_amd.bench.replay_broker.SharedQueueBroker` process holds ``events``
-  pre-encoded telemetry messages (the bench workload) and starts delivering once all N
-  connections have subscribed;
+* a broker process holds ``events`` pre-encoded telemetry messages (the bench workload) and
+  starts delivering once all N connections have subscribed: the native ``SharedBroker``
+  (ops/csrc_bench/shared_broker.cpp, the default) or the asyncio
+  :class:`~beholder_amd.bench.replay_broker.SharedQueueBroker` (``broker="python"``, whose own
+  CPU capped the curve at about 2.2M events/s);
 * ``python -m beholder_amd.bench.shared_worker run --workers N --source amqp ...`` is the
   service's ``run`` command with its supervisor; each worker has the 10k-media table in memory
   (``--media-fixture``) and the headline's in-process sink stub (no Trello/Telegram/Emby);
@@ -16,8 +18,8 @@ One measurement (:func:`run_shared`):
   and reports its own CPU over that span; then the supervisor gets SIGTERM and must drain and
   exit 0.
 
-``events_per_sec`` is events / broker span. The broker is one Python process: its
-``broker_cpu_us_per_event`` next to the rate says when the broker, not the workers, is the limit.
+``events_per_sec`` is events / broker span. ``broker_cpu_us_per_event`` (the broker loop's CPU
+over the span) next to the rate says when the broker, not the workers, is the limit.
 """
 from __future__ import annotations
 
@@ -49,7 +51,7 @@ def _parse_kv(line: str) -> Dict[str, object]:
 
 
 def run_shared(workers: int, events: int, *, media: int = 10000, seed: int = 0, timeout_s: float = 120.0,
-               log_level: str = "info", kill_one_after: int = 0) -> dict:
+               log_level: str = "info", kill_one_after: int = 0, broker: str = "native") -> dict:
     """One shared-queue run with ``workers`` competing consumers; see the module docstring.
 
     ``kill_one_after``: once the broker reports that many events acked, one worker process gets
@@ -61,16 +63,19 @@ def run_shared(workers: int, events: int, *, media: int = 10000, seed: int = 0, 
     from .generator import Workload, bench_config
     from .harness import _die_with_parent, _spawn
 
+    if broker not in ("native", "python"):
+        raise ValueError("broker must be 'native' or 'python'")
     port, bprocs = _spawn("beholder_amd.bench.replay_broker", 1,
                           ("--events", str(events), "--media", str(media), "--seed", str(seed), "--shared",
-                           "--consumers", str(workers), "--progress-every", str(kill_one_after)))
-    broker = bprocs[0]
+                           "--consumers", str(workers), "--progress-every", str(kill_one_after),
+                           *(("--python",) if broker == "python" else ())))
+    broker_proc = bprocs[0]
     lines: List[str] = []
     got_done = threading.Event()
     progress = threading.Event()
 
     def read_broker():
-        for ln in broker.stdout:
+        for ln in broker_proc.stdout:
             lines.append(ln.strip())
             if ln.startswith("PROGRESS "):
                 progress.set()
@@ -79,7 +84,7 @@ def run_shared(workers: int, events: int, *, media: int = 10000, seed: int = 0, 
         got_done.set()
     threading.Thread(target=read_broker, daemon=True).start()
     sup = None
-    out: dict = {"workers": workers, "events": events}
+    out: dict = {"workers": workers, "events": events, "broker": broker}
     try:
         with tempfile.TemporaryDirectory(prefix="beholder-shared-") as td:
             w = Workload(n_media=media, seed=seed)
@@ -126,12 +131,12 @@ def run_shared(workers: int, events: int, *, media: int = 10000, seed: int = 0, 
     finally:
         if sup is not None and sup.poll() is None:
             sup.kill()
-        if broker.poll() is None:
-            broker.terminate()
+        if broker_proc.poll() is None:
+            broker_proc.terminate()
         try:
-            broker.wait(10)
+            broker_proc.wait(10)
         except subprocess.TimeoutExpired:
-            broker.kill()
+            broker_proc.kill()
     done = next((ln for ln in lines if ln.startswith("FINAL ")), None) or \
         next((ln for ln in lines if ln.startswith("DONE ")), None)
     if done is None:

@@ -27,6 +27,7 @@ extern const NativeApi* g_api;  // set by PyInit__native_bench
 int init_calib(PyObject* m);
 int init_paced(PyObject* m);
 int init_recorder(PyObject* m);
+int init_shared_broker(PyObject* m);
 
 }  // namespace bench
 

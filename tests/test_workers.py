@@ -229,13 +229,17 @@ def test_workers_config_is_validated():
             cfg({"service": {"workers": {k: bad}}})
 
 
-def test_shared_queue_two_workers_ack_every_event_exactly_once():
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("broker", ["native", "python"])
+def test_shared_queue_two_workers_ack_every_event_exactly_once(broker):
     """The bench's shared-queue phase (VERDICT r4 item 5): `run --workers 2` on one broker queue;
     the broker counts every ack per event: all published events acked, none twice, none lost,
     no ack of an unknown tag, and both workers got deliveries."""
     from beholder_amd.bench.shared_queue import run_shared
-    r = run_shared(2, 6000)
-    assert r["supervisor_rc"] == 0, r.get("supervisor_stderr")
+    r = run_shared(2, 6000, broker=broker)
+    assert r["supervisor_rc"] == 0 and r["broker"] == broker, r.get("supervisor_stderr")
     assert r["published"] == r["acked"] == 6000
     assert r["dup_acks"] == 0 and r["lost"] == 0 and r["unknown_acks"] == 0 and r["exactly_once"]
     assert r["connections"] == 2 and len(r["per_connection_delivered"]) == 2
@@ -259,15 +263,83 @@ def test_worker_command_reruns_the_entry_module(monkeypatch):
     assert cli.worker_command() == [sys.executable, "-m", "beholder_amd"]
 
 
-def test_shared_queue_worker_crash_requeues_and_still_acks_every_event_once():
+@pytest.mark.parametrize("broker", ["native", "python"])
+def test_shared_queue_worker_crash_requeues_and_still_acks_every_event_once(broker):
     """A worker SIGKILLed mid-stream: the supervisor restarts it, the broker requeues the dead
     connection's un-acked deliveries (redelivered, as RabbitMQ does), and at the broker every
     published event ends up acked exactly once (the reference's at-least-once consumption with
     no loss: index.js acks after the handler, so nothing un-acked is lost)."""
     from beholder_amd.bench.shared_queue import run_shared
-    r = run_shared(2, 60000, kill_one_after=4000)
+    r = run_shared(2, 60000, kill_one_after=4000, broker=broker)
     assert r.get("killed_worker_pid"), r
     assert r["supervisor_rc"] == 0, r.get("supervisor_stderr")
     assert r["published"] == r["acked"] == 60000 and r["lost"] == 0 and r["unknown_acks"] == 0
     assert r["dup_acks"] == 0 and r["exactly_once"]
     assert r["redelivered"] > 0  # the dead connection's un-acked deliveries went to the other worker
+
+
+def test_native_shared_broker_ack_accounting_and_requeue():
+    """SharedBroker (ops/csrc_bench/shared_broker.cpp) spoken to by the service's own AMQP client:
+    the window is prefetch x consumers, single and multiple acks settle what they name, an ack of
+    an unknown or already settled tag is counted, and deliveries a closed connection left un-acked
+    go to the next consumer marked redelivered."""
+    import array
+    import asyncio
+    import threading
+
+    from beholder_amd.ops.bench_native import SharedBroker
+    from beholder_amd.transport.amqp import wire
+    from beholder_amd.transport.amqp.connection import Connection
+
+    names = ("q.a", "q.b")
+    events = [(names[i % 2], b"body-%d" % i) for i in range(40)]
+    pieces = [wire.encode_content(1, 60, b, None, 131072) for _, b in events]
+    offs = array.array("Q", [0])
+    for p in pieces:
+        offs.append(offs[-1] + len(p))
+    b = SharedBroker(b"".join(pieces), offs.tobytes(), bytes(names.index(q) for q, _ in events), names, 1)
+    port = b.listen()
+    t = threading.Thread(target=b.run, args=(0.05,), daemon=True)
+    t.start()
+
+    async def consume(prefetch, take, ack):
+        conn = await Connection(f"amqp://guest:guest@127.0.0.1:{port}/").open()
+        ch = await conn.channel()
+        await ch.basic_qos(prefetch)
+        got = []
+        for q in names:
+            await ch.queue_declare(q)
+            await ch.basic_consume(q, lambda c, m, props, body: got.append((m.delivery_tag, m.redelivered, body)))
+        for _ in range(200):
+            if len(got) >= take:
+                break
+            await asyncio.sleep(0.01)
+        await asyncio.sleep(0.05)
+        n = len(got)
+        ack(ch, got)
+        await asyncio.sleep(0.05)
+        await conn.close()
+        return n, got
+
+    async def go():
+        # first consumer: window 2 x 3 = 6; acks tag 1, tags <= 3 (multiple), tag 2 again, tag 99; the
+        # rest stays un-acked until it closes
+        def ack1(ch, got):
+            ch.basic_ack(1)
+            ch.basic_ack(3, multiple=True)
+            ch.basic_ack(2)
+            ch.basic_ack(99)
+        n1, got1 = await consume(3, 6, ack1)
+        # second consumer: gets the 3 requeued ones first (redelivered), then the rest; acks all
+        n2, got2 = await consume(100, 37, lambda ch, got: ch.basic_ack(len(got), multiple=True))
+        return n1, got1, n2, got2
+    n1, got1, n2, got2 = asyncio.run(go())
+    t.join(10)
+    st = b.stats()
+    assert n1 == 6  # prefetch 3 per consumer x 2 consumers on the channel
+    k = len(got1) - 3  # un-acked at close (the acks freed room for more deliveries before it)
+    assert k >= 3 and all(r for _, r, _ in got2[:k]) and not any(r for _, r, _ in got2[k:])
+    assert {x for _, _, x in got2[:k]} == {x for _, _, x in got1[3:]}
+    assert n2 == 37 and st["published"] == st["acked"] == 40 and st["finished"]
+    assert st["unknown_acks"] == 2 and st["dup_acks"] == 0 and st["lost"] == 0 and st["redelivered"] == k
+    assert st["per_conn"] == [len(got1), 37] and st["broker_s"] > 0
