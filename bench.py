@@ -110,7 +110,7 @@ def parse(argv=None):
     ap.add_argument("--e2e-repeats", type=int, default=3,
                     help="tcp_e2e / tls_e2e runs each; the line has the median run (by rate) and every run's figures")
     ap.add_argument("--soak-events", type=int, default=1_000_000)
-    ap.add_argument("--shared-queue-events", type=int, default=50_000,
+    ap.add_argument("--shared-queue-events", type=int, default=100_000,
                     help="events per worker of each shared-queue run (run --workers N on one queue; 0 = skip)")
     ap.add_argument("--media", type=int, default=10000)
     ap.add_argument("--log-level", default="info")
