@@ -706,7 +706,7 @@ def _scrape(port: int, path: str = "/metrics", timeout: float = 2.0) -> Optional
 def _metric_value(text: str, name: str, labels: str = "") -> Optional[float]:
     """Value of ``name{labels}`` in a Prometheus text exposition (first match)."""
     want = f"{name}{{{labels}}}" if labels else name
-    for ln in text.splitlines():
+    for ln in text.split("\n"):
         if ln.startswith("#"):
             continue
         key, _, val = ln.rpartition(" ")
@@ -767,7 +767,7 @@ def _plumbing(w: Workload, *, timeout_s: float = 120.0) -> dict:
     if p.returncode != 0:
         raise RuntimeError(f"plumbing run failed ({p.returncode}): {err.decode()[-2000:]}")
     stats = json.loads(err.decode().strip().splitlines()[-1])
-    lines = [json.loads(x) for x in out.decode().splitlines() if x.startswith("{")]
+    lines = [json.loads(x) for x in out.decode().split("\n") if x.startswith("{")]
     s = stats["source"]
     scrape = scrape or ""
     return {"config": "plumbing", "offered": 100, "rc": p.returncode, "acked": s["acked"], "abandoned": s["abandoned"],

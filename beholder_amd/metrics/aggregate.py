@@ -54,7 +54,7 @@ def aggregate(texts: Sequence[str]) -> str:
     sample_order: Dict[str, List[str]] = {}
     for text in texts:
         family = None
-        for line in text.splitlines():
+        for line in text.split("\n"):  # exposition lines end in \n; a label value may hold U+0085
             if not line:
                 continue
             if line.startswith("#"):

@@ -334,7 +334,7 @@ class Registry:
 def parse_exposition(text: str) -> Dict[str, float]:
     """Parse sample lines of a text exposition into ``{'name{labels}': value}`` (tests/tools)."""
     out: Dict[str, float] = {}
-    for line in text.splitlines():
+    for line in text.split("\n"):
         if not line or line.startswith("#"):
             continue
         key, _, val = line.rpartition(" ")

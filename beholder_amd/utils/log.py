@@ -345,7 +345,7 @@ class ErrorSampleStream:
     def write(self, s: str) -> int:
         self.bytes += len(s)
         if len(self.samples) < self.keep and ('"level":50' in s or '"level":60' in s):
-            for line in s.splitlines():
+            for line in s.split("\n"):  # not splitlines(): U+0085 / U+2028 are text in a JSON string
                 if ('"level":50' in line or '"level":60' in line) and len(self.samples) < self.keep:
                     self.samples.append(line[:400])
         return len(s)
@@ -361,7 +361,7 @@ class MemoryStream:
         self.lines = []
 
     def write(self, s: str) -> int:
-        self.lines.extend(x for x in s.splitlines() if x)
+        self.lines.extend(x for x in s.split("\n") if x)  # lines end in \n only (see ErrorSampleStream)
         return len(s)
 
     def flush(self) -> None:

@@ -3,6 +3,7 @@ import pytest
 
 from beholder_amd.metrics import Registry, parse_exposition
 from beholder_amd.metrics.registry import Histogram
+from beholder_amd.utils.log import Logger
 
 
 def reference_registry():
@@ -166,3 +167,20 @@ def test_cluster_metrics_stop_serving_a_worker_that_keeps_failing(monkeypatch):
     workers[:] = [(1, 2)]
     srv2.merged_metrics()
     assert 0 not in srv2._last
+
+
+def test_line_splitting_keeps_unicode_line_separators_in_values():
+    """Exposition and log lines end in "\\n" only: a label value or log message holding U+0085,
+    U+2028 or U+001E (all line breaks to str.splitlines) stays inside its line."""
+    from beholder_amd.metrics.aggregate import aggregate
+    from beholder_amd.utils.log import MemoryStream
+    odd = "a\x85b c\x1ed"
+    r = Registry()
+    c = r.counter("odd_total", "x", ["status"])
+    c.labels(status=odd).inc(2)
+    text = r.render()
+    merged = parse_exposition(aggregate([text, text]))
+    assert merged == {f'odd_total{{status="{odd}"}}': 4.0}
+    s = MemoryStream()
+    Logger(stream=s).info("media " + odd)
+    assert [rec["msg"] for rec in s.records()] == ["media " + odd]
