@@ -484,6 +484,16 @@ def _http_tcp(w: Workload, n: int, servers: int = 3, clients=("h1", "aiohttp")) 
     return out
 
 
+def _io_counts(src) -> Dict[str, int]:
+    """Socket call counts of this process so far: NetConn sends / receives by kind, NetPoller
+    callbacks (ops io_counts) and the AMQP connection's reads / writes."""
+    from ..ops import native
+    c = dict(native.io_counts())
+    st = src.stats()
+    c["amqp_reads"], c["amqp_writes"] = st.get("reads", 0), st.get("writes", 0)
+    return c
+
+
 def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = False, preconnect: int = 0,
              max_connecting: int = 8, hooks: Optional[tuple] = None) -> dict:
     """Production-shaped: every dependency over real TCP. A replay AMQP broker streams n
@@ -558,6 +568,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             rss0 = _rss_mb()  # pools full, code paths warm: later growth would be a leak
             cg1 = cgroup_cpu_stat()
             fcpu0 = [proc_cpu_s(p.pid) for _, p in kinds]
+            io0 = _io_counts(src)
             ru0 = resource.getrusage(resource.RUSAGE_SELF)
             if hooks:
                 hooks[0]()
@@ -567,6 +578,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             if hooks:
                 hooks[1]()
             ru1 = resource.getrusage(resource.RUSAGE_SELF)
+            io1 = _io_counts(src)
             fcpu1 = [proc_cpu_s(p.pid) for _, p in kinds]
             cg2 = cgroup_cpu_stat()
             mon.stop()
@@ -590,7 +602,8 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             diag = {"warm_slow": warm_slow, "steady_slow": steady_slow, "mon": mon, "warm_mon": warm_mon,
                     "nivcsw": ru1.ru_nivcsw - ru0.ru_nivcsw, "cgroup_warmup": cgroup_delta(cg0, cg1),
                     "cgroup_steady": cgroup_delta(cg1, cg2), "fakes_cpu_s": fakes_cpu,
-                    "minflt": ru1.ru_minflt - ru0.ru_minflt, "majflt": ru1.ru_majflt - ru0.ru_majflt}
+                    "minflt": ru1.ru_minflt - ru0.ru_minflt, "majflt": ru1.ru_majflt - ru0.ru_majflt,
+                    "io": {k: io1[k] - io0[k] for k in io0}}
             return elapsed, stats, cpu, ru1.ru_stime - ru0.ru_stime, pg_conns, http_stats, measured, cold, rss1 - rss0, diag
 
         elapsed, stats, cpu, sys_s, pg_conns, http_stats, m, cold, rss_growth, diag = asyncio.run(go())
@@ -609,6 +622,10 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             # each fake's CPU over the measured window, per consumed event (broker / pg / http(s)):
             # the share of the phase's CPU the consumer does not own
             "fakes_cpu_us_per_event": {k: round(v / m * 1e6, 3) for k, v in diag["fakes_cpu_s"].items()} if m else {},
+            # the consumer's socket calls per event over the window, by connection (VERDICT r4
+            # item 4: which writes could share a wake-up): AMQP reads / writes (acks), sink and
+            # Postgres sends / receives, NetPoller callbacks and the sockets each found ready
+            "io_per_event": {k: round(v / m, 4) for k, v in diag["io"].items()} if m else {},
         })
     finally:
         stalls: list = []

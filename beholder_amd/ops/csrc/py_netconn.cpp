@@ -80,6 +80,11 @@ int h1_parser_start_c(PyObject* o, bool head);
 PyObject* h1_parser_feed_c(PyObject* o, const char* data, size_t n);
 bool is_pg_reader(PyObject* o);  // py_pg.cpp
 PyObject* pg_reader_feed_c(PyObject* o, const char* data, size_t n);
+extern uint64_t g_netpoll_runs, g_netpoll_ready;  // py_netpoll.cpp
+
+// Process-wide socket call counts by connection kind ([kind][0] sends, [kind][1] receives), read
+// by io_counts(): the bench's syscalls-per-event keys (one loop thread: plain increments).
+uint64_t g_io_calls[2][2];
 
 namespace {
 
@@ -310,6 +315,7 @@ int send_out(NetConnObject* c) {
       off += size_t(n);
       c->bytes_out += uint64_t(n);
       ++c->sends;
+      ++g_io_calls[c->kind][0];
       continue;
     }
     if (n < 0 && errno == EINTR) continue;
@@ -354,6 +360,7 @@ int send_out_tls(NetConnObject* c) {
       off += size_t(n);
       c->bytes_out += uint64_t(n);
       ++c->sends;
+      ++g_io_calls[c->kind][0];
       continue;
     }
     int e = SSL_get_error(c->ssl, n);
@@ -958,6 +965,7 @@ PyObject* nc_on_readable(NetConnObject* c, PyObject*) {
   }
   c->bytes_in += uint64_t(n);
   ++c->recvs;
+  ++g_io_calls[c->kind][1];
   Py_INCREF(c);  // a resumed handler may drop the last other reference
   if (c->kind == K_H1) {
     on_h1_data(c, buf, size_t(n));
@@ -990,6 +998,7 @@ PyObject* on_readable_tls(NetConnObject* c, char* buf) {
     if (n > 0) {
       c->bytes_in += uint64_t(n);
       ++c->recvs;
+      ++g_io_calls[c->kind][1];
       if (c->kind == K_H1) {
         on_h1_data(c, buf, size_t(n));
       } else {
@@ -1447,7 +1456,17 @@ PyObject* mod_pg_pool_execute(PyObject*, PyObject* const* a, Py_ssize_t n) {
   return nc_execute(best, args, 2);
 }
 
+// io_counts() -> {"h1_sends", "h1_recvs", "pg_sends", "pg_recvs", "poll_runs", "poll_ready"}:
+// socket calls made by every NetConn of the process (a TLS record write / read counts as one),
+// NetPoller callbacks and the sockets they found ready. Monotonic; callers take differences.
+PyObject* mod_io_counts(PyObject*, PyObject*) {
+  return Py_BuildValue("{s:K,s:K,s:K,s:K,s:K,s:K}", "h1_sends", g_io_calls[K_H1][0], "h1_recvs", g_io_calls[K_H1][1],
+                       "pg_sends", g_io_calls[K_PG][0], "pg_recvs", g_io_calls[K_PG][1], "poll_runs", g_netpoll_runs,
+                       "poll_ready", g_netpoll_ready);
+}
+
 PyMethodDef pool_functions[] = {
+    {"io_counts", mod_io_counts, METH_NOARGS, "io_counts() -> dict of process-wide NetConn / NetPoller call counts"},
     {"netconn_connect", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(mod_netconn_connect)),
      METH_VARARGS | METH_KEYWORDS,
      "netconn_connect(ip, port, loop, kind, owner, parser, **NetConn keywords) -> NetConn; `handshake` resolves once "

@@ -31,6 +31,8 @@ PyObject* netconn_dispatch(PyObject* conn, uint32_t events);
 void netconn_flush(PyObject* conn);
 void netconn_tls_done(void* job);
 
+uint64_t g_netpoll_runs, g_netpoll_ready;  // _run callbacks and the ready sockets they took (io_counts)
+
 namespace {
 
 struct PollerObject {
@@ -158,6 +160,8 @@ PyObject* poller_run(PollerObject* p, PyObject*) {
     n = epoll_wait(p->epfd, evs, 256, 0);
   } while (n < 0 && errno == EINTR);
   if (n < 0) return PyErr_SetFromErrno(PyExc_OSError);
+  ++g_netpoll_runs;
+  g_netpoll_ready += uint64_t(n);
   Py_INCREF(p);
   ++p->running;
   const int wfd = p->wake && *p->wake ? (*p->wake)->efd : -1;

@@ -375,6 +375,8 @@ class Connection:
         self._lost_reported = False
         self.bytes_in = 0
         self.bytes_out = 0
+        self.reads = 0  # data_received calls (one socket read each)
+        self.writes = 0  # transport.write calls
         self.on_deliveries = on_deliveries
         self._demux = None
         if native_settler is not None and on_deliveries is not None:
@@ -457,6 +459,7 @@ class Connection:
                 self._lost(e)
                 return
             self.bytes_out += len(data)
+            self.writes += 1
             self._last_tx = time.monotonic()
             return
         self._wbuf += data
@@ -479,6 +482,7 @@ class Connection:
             self._lost(e)
             return
         self.bytes_out += len(data)
+        self.writes += 1
         self._last_tx = time.monotonic()
 
     async def _maybe_drain(self) -> None:
@@ -494,6 +498,7 @@ class Connection:
         if self._aborting:
             return
         self.bytes_in += len(data)
+        self.reads += 1
         self._last_rx = time.monotonic()
         try:
             demux = self._demux

@@ -244,6 +244,7 @@ class AmqpSource(Source):
         s.update({"connected": self.ready(), "reconnects": self.reconnects, "delivered": self.delivered,
                   "stale_settles": self.stale_settles, "last_error": self.last_error,
                   "bytes_in": c.bytes_in if c else 0, "bytes_out": c.bytes_out if c else 0,
+                  "reads": c.reads if c else 0, "writes": c.writes if c else 0,
                   "buffered": len(self._pending),
                   "ack_frames": self._batcher.frames if self._batcher is not None else None,
                   "ack_multiples": self._batcher.multiples if self._batcher is not None else None,

@@ -439,6 +439,7 @@ def _e2e_keys(prefix: str, run, n: int, repeats: int = 1, **kw) -> dict:
            f"{prefix}_minflt": e.get("minflt"), f"{prefix}_majflt": e.get("majflt"),
            f"{prefix}_calib_ns": e.get("calib_ns"),
            f"{prefix}_fakes_cpu_us_per_event": e.get("fakes_cpu_us_per_event"),
+           f"{prefix}_io_per_event": e.get("io_per_event"),
            f"{prefix}_host_cpu_busy_pct": busy,
            **_cg(prefix, e.get("cgroup_steady") or {}),
            **_attr_keys(prefix, e.get("attribution_steady")),

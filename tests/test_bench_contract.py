@@ -101,6 +101,12 @@ def test_bench_single_rank_contract(tmp_path):
     assert len(out["tcp_e2e_runs"]["events_per_sec"]) == 2 and out["tcp_e2e_events_per_sec"] in \
         out["tcp_e2e_runs"]["events_per_sec"]
     assert out["tcp_e2e_sys_cpu_us_per_event"] >= 0 and out["tcp_e2e_minflt"] >= 0
+    # the consumer's socket calls per event: a send per sink request, queries
+    # and acks batched, every kind of connection seen
+    io = out["tcp_e2e_io_per_event"]
+    assert set(io) == {"h1_sends", "h1_recvs", "pg_sends", "pg_recvs", "poll_runs", "poll_ready", "amqp_reads",
+                       "amqp_writes"}
+    assert 0.2 < io["h1_sends"] < 1.0 and all(io[k] > 0 for k in io), io
     # competing consumers on one queue (run --workers N), every event acked exactly once
     ns = bench.shared_queue_workers(out["cpus_available"])
     assert list(out["shared_queue_events_per_sec"]) == [str(n) for n in ns] and out["shared_queue_exactly_once"]

@@ -26,7 +26,7 @@ def test_native_runtime_is_in_tree_and_loaded():
     # every hot-path entry point is native
     for name in ("MessageCodec", "Ingest", "Delivery", "Settler", "Histogram", "format_line", "encode_query",
                  "AmqpDemux", "H1Parser", "PgReader", "Driver", "IOFuture", "AckBatcher", "Buckets",
-                 "dispatch_batch", "pg_bind", "NativeHandlers", "HandlerCall", "SinkStats", "_C_API"):
+                 "dispatch_batch", "pg_bind", "NativeHandlers", "HandlerCall", "SinkStats", "_C_API", "io_counts"):
         assert hasattr(ops.native, name), name
     # bench / diagnostic code is a module of its own, also in-tree
     for name in ("Recorder", "prof_start", "prof_stop", "calib", "calib_mem", "paced_write"):

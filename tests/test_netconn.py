@@ -65,6 +65,38 @@ def test_both_clients_adopt_plain_tcp_connections():
     assert run(go()) == ("NetConn", None, "NetConn", None, [(2,)], "SELECT 1")
 
 
+def test_process_io_counts_follow_the_connections():
+    """ops.io_counts(): the process-wide socket call counts (the bench's ``*_io_per_event``) move
+    with each NetConn's own sends / receives, by kind."""
+    from beholder_amd.ops import native
+
+    async def go():
+        s = await test_h1.Scripted(lambda n, m, t, h: test_h1.OK).start()
+        pg = await FakePg(auth="md5").start()
+        try:
+            c0 = dict(native.io_counts())
+            h = H1Client(timeout_s=5)
+            for _ in range(3):
+                await h.request("GET", f"http://127.0.0.1:{s.port}/x")
+            p = await PgConnection(pg.dsn).connect()
+            for i in range(2):
+                await p.execute("SELECT $1 + 1", (i,))
+            c1 = dict(native.io_counts())
+            hs = next(iter(h._origins.values())).idle[0].net.stats
+            ps = p._net.stats
+            await h.close()
+            await p.close()
+            return c0, c1, hs, ps
+        finally:
+            await s.stop()
+            await pg.stop()
+    c0, c1, hs, ps = run(go())
+    d = {k: c1[k] - c0[k] for k in c0}
+    assert d["h1_sends"] == hs["sends"] >= 3 and d["h1_recvs"] == hs["recvs"] >= 3
+    assert d["pg_sends"] >= 2 and d["pg_recvs"] >= 2 and ps["sends"] <= d["pg_sends"]
+    assert d["poll_runs"] >= 5 and d["poll_ready"] >= d["poll_runs"]
+
+
 def test_large_response_spans_many_recvs():
     body = os.urandom(3 << 20).hex().encode()  # 6 MiB: 24+ reads of 256 KiB
 
