@@ -15,7 +15,8 @@ from typing import Optional
 class Signal:
     """``set()`` / ``clear()`` / ``is_set()`` / ``await wait()`` with asyncio.Event's meaning:
     ``wait()`` returns at once while set, else when ``set()`` is next called. Every waiter of
-    one wait shares its future."""
+    one wait shares its future, so a waiter cancelled mid-wait cancels the others too: this is
+    for one waiting task at a time (the dispatch loop), not a general asyncio.Event."""
 
     __slots__ = ("_flag", "_fut")
 
