@@ -420,3 +420,47 @@ def test_amqps_tls_with_ca_verification(tmp_path):
         finally:
             await b.stop()
     run(go())
+
+
+def test_protocol_write_backpressure_and_loss_wake_the_publisher():
+    """connection._Protocol: a publisher waits in drain() while the transport is paused, resumes
+    on resume_writing(), and is woken (not left hanging) when the connection is lost meanwhile."""
+    from beholder_amd.transport.amqp.connection import _Protocol
+
+    class Conn:
+        lost = None
+        data = []
+
+        def _on_data(self, b):
+            self.data.append(b)
+
+        def _on_transport_lost(self, exc):
+            self.lost = exc
+
+    class Transport:
+        closing = False
+
+        def is_closing(self):
+            return self.closing
+
+    async def go():
+        c = Conn()
+        p = _Protocol(c)
+        p.connection_made(Transport())
+        await p.drain()  # not paused: returns at once
+        p.pause_writing()
+        t = asyncio.ensure_future(p.drain())
+        await asyncio.sleep(0.01)
+        blocked = not t.done()
+        p.resume_writing()
+        await asyncio.wait_for(t, 1)
+        p.pause_writing()
+        t2 = asyncio.ensure_future(p.drain())
+        await asyncio.sleep(0.01)
+        err = ConnectionResetError("gone")
+        p.connection_lost(err)
+        await asyncio.wait_for(t2, 1)
+        p.data_received(b"x")
+        return blocked, c.lost is err, p.closed.done(), c.data
+    blocked, lost, closed, data = asyncio.run(go())
+    assert blocked and lost and closed and data == [b"x"]

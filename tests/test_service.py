@@ -425,3 +425,25 @@ def test_signal_has_event_semantics():
         for x in ts:
             await x
     asyncio.run(go())
+
+
+def test_signal_wait_after_a_cancelled_waiter():
+    """The one-waiter contract (utils/waits.py): a waiter cancelled mid-wait leaves the Signal
+    usable; the next wait gets a fresh future and is woken by the next set()."""
+    from beholder_amd.utils.waits import Signal
+
+    async def go():
+        s = Signal()
+        t = asyncio.ensure_future(s.wait())
+        await asyncio.sleep(0)
+        t.cancel()
+        try:
+            await t
+        except asyncio.CancelledError:
+            pass
+        t2 = asyncio.ensure_future(s.wait())
+        await asyncio.sleep(0)
+        pending = not t2.done()
+        s.set()
+        return pending, await asyncio.wait_for(t2, 1)
+    assert asyncio.run(go()) == (True, True)
