@@ -409,6 +409,12 @@ def _cg(prefix: str, d: dict) -> dict:
     return {f"{prefix}_nr_throttled": d.get("nr_throttled"), f"{prefix}_throttled_usec": d.get("throttled_usec")}
 
 
+def _events_per_poll(e: dict):
+    """Events per NetPoller callback over one e2e run (None without the socket-call counts)."""
+    p = (e.get("io_per_event") or {}).get("poll_runs")
+    return _r(1 / p, 1) if p else None
+
+
 def _e2e_keys(prefix: str, run, n: int, repeats: int = 1, **kw) -> dict:
     """One production-shaped phase (harness._tcp_e2e), run ``repeats`` times: the keys are those
     of the run with the median rate (``*_runs``: every run's rate, CPU per event and p999). Each
@@ -453,7 +459,12 @@ def _e2e_keys(prefix: str, run, n: int, repeats: int = 1, **kw) -> dict:
         out[f"{prefix}_runs"] = {
             "events_per_sec": [_r(r.get("ingest_rate_eps"), 1) for r, _ in runs],
             "cpu_us_per_event": [_r(r.get("cpu_us_per_event")) for r, _ in runs],
-            "p999_handle_latency_us": [_r((r.get("handle_latency_us") or {}).get("p999")) for r, _ in runs]}
+            "p999_handle_latency_us": [_r((r.get("handle_latency_us") or {}).get("p999")) for r, _ in runs],
+            # what moves CPU per event between runs of one line: system time, how many events
+            # each NetPoller callback found ready (bigger batches, fewer calls), the core speed
+            "sys_cpu_us_per_event": [_r(r.get("sys_cpu_us_per_event")) for r, _ in runs],
+            "events_per_poll_run": [_events_per_poll(r) for r, _ in runs],
+            "calib_ns": [r.get("calib_ns") for r, _ in runs]}
     return out
 
 

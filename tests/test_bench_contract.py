@@ -101,6 +101,9 @@ def test_bench_single_rank_contract(tmp_path):
     assert len(out["tcp_e2e_runs"]["events_per_sec"]) == 2 and out["tcp_e2e_events_per_sec"] in \
         out["tcp_e2e_runs"]["events_per_sec"]
     assert out["tcp_e2e_sys_cpu_us_per_event"] >= 0 and out["tcp_e2e_minflt"] >= 0
+    runs = out["tcp_e2e_runs"]
+    assert all(len(runs[k]) == 2 for k in ("sys_cpu_us_per_event", "events_per_poll_run", "calib_ns"))
+    assert all(x > 0 for x in runs["events_per_poll_run"]), runs
     # the consumer's socket calls per event: a send per sink request, queries
     # and acks batched, every kind of connection seen
     io = out["tcp_e2e_io_per_event"]
