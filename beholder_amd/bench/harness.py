@@ -149,6 +149,7 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
     from ..sinks import RecordingHttpClient
     from ..store import MemoryStore
     from ..transport.ingest import FdSource
+    from ..utils.hostinfo import thread_run_delay_ns
     from ..utils.log import Logger
 
     rfd, wfd = os.pipe()
@@ -207,6 +208,7 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
         src.settler.trace_slow(1, prod.offered + 16)
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
     rt0 = resource.getrusage(resource.RUSAGE_THREAD)
+    rd0 = thread_run_delay_ns()
     t0 = time.perf_counter()
     prod.start()
     stats = await svc.run()
@@ -215,6 +217,7 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
     elapsed = time.perf_counter() - t0
     ru1 = resource.getrusage(resource.RUSAGE_SELF)
     rt1 = resource.getrusage(resource.RUSAGE_THREAD)
+    rd1 = thread_run_delay_ns()
     if mon is not None:
         mon.stop()
     cpu_s = (ru1.ru_utime + ru1.ru_stime) - (ru0.ru_utime + ru0.ru_stime)
@@ -250,6 +253,8 @@ async def _run_inproc(events, rate: float, *, policy: str = "block", capacity_ev
         "cpu_us_per_event": cpu_s / s["acked"] * 1e6 if s["acked"] else None,
         # the event loop's thread: preemptions by other work on its CPU, and its stalls >= 2 ms
         "loop_thread_nivcsw": rt1.ru_nivcsw - rt0.ru_nivcsw,
+        # ... and its time runnable but without a CPU (a wake-up the host delayed)
+        "loop_run_delay_us": (rd1 - rd0) / 1e3 if rd0 is not None and rd1 is not None else None,
         **({"loop": mon.summary()} if mon is not None else {}),
         "error_samples": sink.samples,
         **({"rss_curve_mb": rss_curve} if rss_probe is not None else {}),
@@ -510,7 +515,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
     from ..sinks import H1Client
     from ..store.postgres import PostgresStore
     from ..transport.amqp import AmqpSource
-    from ..utils.hostinfo import cgroup_cpu_stat, cgroup_delta, proc_cpu_s
+    from ..utils.hostinfo import cgroup_cpu_stat, cgroup_delta, proc_cpu_s, proc_run_delay_ns
     from ..utils.log import Logger
     from .stallmon import StallMonitor
 
@@ -569,6 +574,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             cg1 = cgroup_cpu_stat()
             fcpu0 = [proc_cpu_s(p.pid) for _, p in kinds]
             io0 = _io_counts(src)
+            rq0 = proc_run_delay_ns()
             ru0 = resource.getrusage(resource.RUSAGE_SELF)
             if hooks:
                 hooks[0]()
@@ -578,6 +584,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             if hooks:
                 hooks[1]()
             ru1 = resource.getrusage(resource.RUSAGE_SELF)
+            rq1 = proc_run_delay_ns()
             io1 = _io_counts(src)
             fcpu1 = [proc_cpu_s(p.pid) for _, p in kinds]
             cg2 = cgroup_cpu_stat()
@@ -603,7 +610,8 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
                     "nivcsw": ru1.ru_nivcsw - ru0.ru_nivcsw, "cgroup_warmup": cgroup_delta(cg0, cg1),
                     "cgroup_steady": cgroup_delta(cg1, cg2), "fakes_cpu_s": fakes_cpu,
                     "minflt": ru1.ru_minflt - ru0.ru_minflt, "majflt": ru1.ru_majflt - ru0.ru_majflt,
-                    "io": {k: io1[k] - io0[k] for k in io0}}
+                    "io": {k: io1[k] - io0[k] for k in io0},
+                    "run_delay_ms": (rq1 - rq0) / 1e6 if rq0 is not None and rq1 is not None else None}
             return elapsed, stats, cpu, ru1.ru_stime - ru0.ru_stime, pg_conns, http_stats, measured, cold, rss1 - rss0, diag
 
         elapsed, stats, cpu, sys_s, pg_conns, http_stats, m, cold, rss_growth, diag = asyncio.run(go())
@@ -626,6 +634,8 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 2, tls: bool = Fal
             # item 4: which writes could share a wake-up): AMQP reads / writes (acks), sink and
             # Postgres sends / receives, NetPoller callbacks and the sockets each found ready
             "io_per_event": {k: round(v / m, 4) for k, v in diag["io"].items()} if m else {},
+            # the consumer's threads' time runnable but waiting for a CPU over the window
+            "run_delay_ms": diag["run_delay_ms"],
         })
     finally:
         stalls: list = []

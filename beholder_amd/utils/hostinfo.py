@@ -185,6 +185,35 @@ def host_busy_pct(before: Optional[tuple], after: Optional[tuple]) -> Optional[f
     return round(100.0 * (after[0] - before[0]) / (after[1] - before[1]), 1)
 
 
+def thread_run_delay_ns() -> Optional[int]:
+    """Nanoseconds the calling thread has spent runnable but waiting for a CPU
+    (``/proc/thread-self/schedstat`` field 2), or None where the kernel has no schedstat. A loop
+    stall with this moving is the host's (no CPU to wake on), not the loop's own work."""
+    try:
+        with open("/proc/thread-self/schedstat") as f:
+            return int(f.read().split()[1])
+    except (OSError, IndexError, ValueError):
+        return None
+
+
+def proc_run_delay_ns(pid="self") -> Optional[int]:
+    """Run-queue wait of every thread of a process so far (the sum of ``schedstat`` field 2 over
+    ``/proc/<pid>/task/*``), or None. Threads that exited meanwhile drop out of the sum, so take
+    differences over a window in which the process keeps its threads."""
+    try:
+        tids = os.listdir(f"/proc/{pid}/task")
+    except OSError:
+        return None
+    total = 0
+    for t in tids:
+        try:
+            with open(f"/proc/{pid}/task/{t}/schedstat") as f:
+                total += int(f.read().split()[1])
+        except (OSError, IndexError, ValueError):
+            continue
+    return total
+
+
 def proc_cpu_s(pid: int) -> Optional[float]:
     """User + system CPU seconds a process has used so far (``/proc/<pid>/stat`` fields 14-15),
     or None when it is gone. The e2e bench phases read it for each fake around the measured window,

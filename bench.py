@@ -446,6 +446,7 @@ def _e2e_keys(prefix: str, run, n: int, repeats: int = 1, **kw) -> dict:
            f"{prefix}_calib_ns": e.get("calib_ns"),
            f"{prefix}_fakes_cpu_us_per_event": e.get("fakes_cpu_us_per_event"),
            f"{prefix}_io_per_event": e.get("io_per_event"),
+           f"{prefix}_run_delay_ms": _r(e.get("run_delay_ms"), 2),
            f"{prefix}_host_cpu_busy_pct": busy,
            **_cg(prefix, e.get("cgroup_steady") or {}),
            **_attr_keys(prefix, e.get("attribution_steady")),
@@ -464,7 +465,8 @@ def _e2e_keys(prefix: str, run, n: int, repeats: int = 1, **kw) -> dict:
             # each NetPoller callback found ready (bigger batches, fewer calls), the core speed
             "sys_cpu_us_per_event": [_r(r.get("sys_cpu_us_per_event")) for r, _ in runs],
             "events_per_poll_run": [_events_per_poll(r) for r, _ in runs],
-            "calib_ns": [r.get("calib_ns") for r, _ in runs]}
+            "calib_ns": [r.get("calib_ns") for r, _ in runs],
+            "run_delay_ms": [_r(r.get("run_delay_ms"), 2) for r, _ in runs]}
     return out
 
 
@@ -555,6 +557,7 @@ def _paced(prefix: str, r: dict) -> dict:
             f"{prefix}_p99_handle_latency_us": _r(hl.get("p99")),
             f"{prefix}_idle_wakeups": r.get("idle_wakeups"),
             f"{prefix}_loop_thread_nivcsw": r.get("loop_thread_nivcsw"),
+            f"{prefix}_loop_run_delay_us": _r(r.get("loop_run_delay_us"), 1),
             f"{prefix}_loop_stalls": (r.get("loop") or {}).get("loop_stalls"),
             f"{prefix}_loop_lag_max_us": (r.get("loop") or {}).get("loop_lag_max_us"),
             f"{prefix}_gc_max_pause_us": (r.get("loop") or {}).get("gc_max_pause_us"),

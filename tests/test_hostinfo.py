@@ -86,3 +86,16 @@ def test_host_busy_share_and_cgroup_stat_readers():
     assert all(isinstance(v, int) for v in st.values())
     assert hi.cgroup_delta({"nr_throttled": 2}, {"nr_throttled": 5, "throttled_usec": 7}) == \
         {"nr_throttled": 3, "throttled_usec": 7}
+
+
+def test_run_queue_delay_readers():
+    """schedstat readers: this thread's and this process's time runnable but without a CPU
+    (None where the kernel has no schedstat); the process total covers the thread's."""
+    from beholder_amd.utils import hostinfo as hi
+    t = hi.thread_run_delay_ns()
+    p = hi.proc_run_delay_ns()
+    if t is None:
+        return
+    assert isinstance(t, int) and t >= 0 and p is not None and p >= 0
+    assert hi.proc_run_delay_ns(os.getpid()) >= t
+    assert hi.proc_run_delay_ns(2 ** 22 + 12345) is None  # no such process
