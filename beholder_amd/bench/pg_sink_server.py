@@ -7,10 +7,14 @@ extended protocol (including pipelined Sync groups) and an in-memory table. The
 table is the synthetic media population of :class:`~.generator.Workload`
 (``--media N --seed S``), so a replayed event stream finds its rows. Several
 copies can share one port (``SO_REUSEPORT``). It prints ``READY <port>`` once it
-is listening. On SIGTERM it prints ``DONE queries=<n>``.
+is listening. On SIGTERM it prints ``DONE queries=<n>`` and its ``STALLS`` line.
 
 It stands in for the database so the bench measures the consumer. It is not a
-database.
+database. By default the protocol is served by the native ``PgFake``
+(ops/csrc_bench/pg_fake.cpp) on its own thread: this asyncio server costs ~5 us of CPU
+per query, and with the consumer's pool spread unevenly over two copies by
+SO_REUSEPORT one copy saturated and capped the run (profiles/box_r5_util/).
+``--python`` serves it from the asyncio protocol below instead.
 """
 from __future__ import annotations
 
@@ -170,10 +174,41 @@ async def main(port: int, media: int, seed: int) -> int:
     return 0
 
 
+def main_native(port: int, media: int, seed: int) -> int:
+    """The same endpoint on the native PgFake: its loop runs on a thread without the GIL; this
+    thread waits for SIGTERM (blocked, so it reaches no other thread), then stops it and reports
+    the queries and the loop's busy spells in the asyncio server's DONE / STALLS format."""
+    import json
+    import threading
+
+    from ..ops.bench_native import PgFake
+    from .generator import make_media
+    signal.pthread_sigmask(signal.SIG_BLOCK, {signal.SIGTERM})  # before the loop thread starts
+    f = PgFake([list(m) for m in make_media(media, seed)])
+    bound = f.listen(port)
+    t = threading.Thread(target=f.run, name="pg-fake", daemon=True)
+    t.start()
+    print(f"READY {bound}", flush=True)
+    signal.sigwait({signal.SIGTERM})
+    f.stop()
+    t.join(5)
+    st = f.stats()
+    print(f"DONE queries={st['queries']}", flush=True)
+    ivs = st["stall_intervals"]
+    print("STALLS " + json.dumps({
+        "name": "pg", "loop_lag_max_us": round(st["max_busy_us"], 1), "loop_stalls": len(ivs),
+        "loop_stalled_ms": round(sum(b - a for a, b in ivs) / 1e6, 2), "gc_pauses": 0,
+        "gc_max_pause_us": None, "gc_stalls": 0, "stall_intervals": ivs}, separators=(",", ":")), flush=True)
+    return 0
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--port", type=int, default=0)
     ap.add_argument("--media", type=int, default=10000)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--python", action="store_true", help="serve from the asyncio protocol, not the native PgFake")
     a = ap.parse_args()
-    sys.exit(asyncio.run(main(a.port, a.media, a.seed)))
+    if a.python:
+        sys.exit(asyncio.run(main(a.port, a.media, a.seed)))
+    sys.exit(main_native(a.port, a.media, a.seed))

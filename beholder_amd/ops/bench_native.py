@@ -5,8 +5,9 @@ extension. The runtime image does not build or ship it (Dock
 Exports ``Recorder`` (the in-process sink stub's core, sinks/http.py RecordingHttpClient),
 ``paced_write`` (the paced producer of BASELINE configs 2-4), ``calib`` / ``calib_mem`` (the bench
 line's fixed-work calibrations) and ``prof_start`` / ``prof_stop`` (the SIGPROF sampler of
-scripts/cprof.py) and ``SharedBroker`` (the shared-queue bench's broker fake). Like :mod:`beholder_amd.ops`, a missing or stale module is built on import when
-a compiler is there (``BEHOLDER_ALLOW_BUILD=0`` forbids it), and the import fails loudly otherwise.
+scripts/cprof.py), ``SharedBroker`` (the shared-queue bench's broker fake) and ``PgFake`` (the e2e
+bench's Postgres fake). Like :mod:`beholder_amd.ops`, a missing or stale module is built on import
+when a compiler is there (``BEHOLDER_ALLOW_BUILD=0`` forbids it), and the import fails loudly otherwise.
 """
 from __future__ import annotations
 
@@ -40,5 +41,7 @@ calib_mem = native_bench.calib_mem
 prof_start = native_bench.prof_start
 prof_stop = native_bench.prof_stop
 SharedBroker = native_bench.SharedBroker
+PgFake = native_bench.PgFake
 
-__all__ = ["native_bench", "Recorder", "paced_write", "calib", "calib_mem", "prof_start", "prof_stop", "SharedBroker"]
+__all__ = ["native_bench", "Recorder", "paced_write", "calib", "calib_mem", "prof_start", "prof_stop", "SharedBroker",
+           "PgFake"]

@@ -28,6 +28,7 @@ int init_calib(PyObject* m);
 int init_paced(PyObject* m);
 int init_recorder(PyObject* m);
 int init_shared_broker(PyObject* m);
+int init_pg_fake(PyObject* m);
 
 }  // namespace bench
 

@@ -1,7 +1,7 @@
 // `beholder_amd.ops._native_bench`: bench, test and diagnostic machinery kept out of the
 // service's extension: the in-process sink stub (recorder.cpp), the paced
 // producer (paced.cpp), the calibration loops (calib.cpp), the sampling profiler (prof.cpp) and
-// the shared-queue broker fake (shared_broker.cpp).
+// the shared-queue broker fake (shared_broker.cpp) and the e2e bench's Postgres fake (pg_fake.cpp).
 #include "bench_common.hpp"
 
 namespace beholder {
@@ -33,6 +33,7 @@ PyMODINIT_FUNC PyInit__native_bench(void) {
   PyObject* m = PyModule_Create(&bench::module_def);
   if (!m) return nullptr;
   if (bench::init_calib(m) < 0 || bench::init_paced(m) < 0 || bench::init_recorder(m) < 0 || bench::init_shared_broker(m) < 0 ||
+      bench::init_pg_fake(m) < 0 ||
       init_bench_prof(m) < 0) {
     Py_DECREF(m);
     return nullptr;

@@ -96,7 +96,8 @@ def test_bench_single_rank_contract(tmp_path):
     assert out["calib_ns"] >= max(out["calib_ns_before"], out["calib_ns_after"]) > 0
     assert set(out["tcp_e2e_slow_blamed"]) >= {"consumer", "pg", "http", "none"}
     # the e2e phases say what else could have moved them
-    assert 4000 - 400 - 100 <= out["tcp_e2e_measured_events"] <= 4000 - 400 and out["tcp_e2e_calib_ns"] > 0
+    # the window starts at the settled count read after the warm-up (a few in-flight deliveries past it)
+    assert 4000 - 400 - 300 <= out["tcp_e2e_measured_events"] <= 4000 - 400 and out["tcp_e2e_calib_ns"] > 0
     assert set(out["tcp_e2e_fakes_cpu_us_per_event"]) == {"broker", "pg", "http"}
     assert len(out["tcp_e2e_runs"]["events_per_sec"]) == 2 and out["tcp_e2e_events_per_sec"] in \
         out["tcp_e2e_runs"]["events_per_sec"]
