@@ -409,6 +409,12 @@ def _cg(prefix: str, d: dict) -> dict:
     return {f"{prefix}_nr_throttled": d.get("nr_throttled"), f"{prefix}_throttled_usec": d.get("throttled_usec")}
 
 
+def _busiest(e: dict):
+    """The busiest fake process's CPU share of one e2e run's window (None without the data)."""
+    us = [u for v in (e.get("fakes_util") or {}).values() for u in v if u is not None]
+    return max(us) if us else None
+
+
 def _events_per_poll(e: dict):
     """Events per NetPoller callback over one e2e run (None without the socket-call counts)."""
     p = (e.get("io_per_event") or {}).get("poll_runs")
@@ -445,6 +451,7 @@ def _e2e_keys(prefix: str, run, n: int, repeats: int = 1, **kw) -> dict:
            f"{prefix}_minflt": e.get("minflt"), f"{prefix}_majflt": e.get("majflt"),
            f"{prefix}_calib_ns": e.get("calib_ns"),
            f"{prefix}_fakes_cpu_us_per_event": e.get("fakes_cpu_us_per_event"),
+           f"{prefix}_fakes_util": e.get("fakes_util"),
            f"{prefix}_io_per_event": e.get("io_per_event"),
            f"{prefix}_run_delay_ms": _r(e.get("run_delay_ms"), 2),
            f"{prefix}_host_cpu_busy_pct": busy,
@@ -466,7 +473,8 @@ def _e2e_keys(prefix: str, run, n: int, repeats: int = 1, **kw) -> dict:
             "sys_cpu_us_per_event": [_r(r.get("sys_cpu_us_per_event")) for r, _ in runs],
             "events_per_poll_run": [_events_per_poll(r) for r, _ in runs],
             "calib_ns": [r.get("calib_ns") for r, _ in runs],
-            "run_delay_ms": [_r(r.get("run_delay_ms"), 2) for r, _ in runs]}
+            "run_delay_ms": [_r(r.get("run_delay_ms"), 2) for r, _ in runs],
+            "busiest_fake_util": [_busiest(r) for r, _ in runs]}
     return out
 
 
