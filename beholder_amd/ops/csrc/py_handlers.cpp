@@ -36,7 +36,7 @@ namespace beholder {
 
 bool text_js_str_append(std::string& out, PyObject* v);
 bool text_query_pair_append(std::string& out, PyObject* k, PyObject* v, bool* first, bool rfc3986);
-PyObject* pg_pool_execute_c(PyObject* conns, PyObject* sql, PyObject* params, PyObject* spread_at, PyObject* size);
+PyObject* pg_pool_execute_c(PyObject* nets, PyObject* sql, PyObject* params, PyObject* spread_at, PyObject* size);
 PyObject* h1_call_new(PyObject* client, PyObject* method, PyObject* url, PyObject* params, PyObject* timeout,
                       bool front);
 bool is_native_logger(PyObject* logger);
@@ -354,7 +354,7 @@ int pg_execute(CallObject* c, PyObject* store, PyObject* sql_name, PyObject* par
   if (PyErr_Occurred()) return -1;
   if (pick && pick == hs->pick_fn) {
     // the pool's native_pick capability (Pool.execute's fast path) in C: the least-loaded native
-    // connection takes the query
+    // connection takes the query (Pool._nets: None while a connection is on the asyncio path)
     PyObject* conns = PyDict_GetItemWithError(pd, s_conns);
     PyObject* spread = conns ? PyDict_GetItemWithError(pd, s_spread_at) : nullptr;
     PyObject* size = spread ? PyDict_GetItemWithError(pd, s_size) : nullptr;
@@ -1828,7 +1828,7 @@ int init_handler_types(PyObject* m) {
               {&s_select, "_select"},
               {&s_update, "_update"},
               {&s_execute, "execute"},
-              {&s_conns, "_conns"},
+              {&s_conns, "_nets"},
               {&s_spread_at, "spread_at"},
               {&s_size, "size"},
               {&s_native_call, "native_call"}, {&s_native_pick, "native_pick"},

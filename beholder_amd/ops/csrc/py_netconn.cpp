@@ -1413,36 +1413,35 @@ PyObject* mod_netconn_connect(PyObject*, PyObject* args, PyObject* kwds) {
   return reinterpret_cast<PyObject*>(c);
 }
 
-// pg_pool_execute(conns, sql, params, spread_at, size) -> IOFuture, or None for the Python path.
-// store/pgwire.py Pool.execute for a pool whose open connections are all native: the open
-// connection with the fewest queries in flight (the first on ties) gets the query, unless every
-// one has `spread_at` or more in flight and the pool may still grow (fewer than `size` open).
+// pg_pool_execute(nets, sql, params, spread_at, size) -> IOFuture, or None for the Python path.
+// store/pgwire.py Pool.execute for a pool whose connections are all native: `nets` is the pool's
+// list of their NetConns (Pool._nets, None while any connection is on the asyncio path). The open
+// one with the fewest queries in flight (the first on ties) gets the query, unless every one has
+// `spread_at` or more in flight and the pool may still grow (fewer than `size` open). A NetConn's
+// own closed flag is its connection's: PgConnection.closed is set in the same call that closes it.
 PyObject* mod_pg_pool_execute(PyObject*, PyObject* const* a, Py_ssize_t n) {
-  if (n != 5 || !PyList_CheckExact(a[0])) {
-    PyErr_SetString(PyExc_TypeError, "pg_pool_execute(conns: list, sql, params, spread_at, size)");
+  if (n != 5) {
+    PyErr_SetString(PyExc_TypeError, "pg_pool_execute(nets: list | None, sql, params, spread_at, size)");
+    return nullptr;
+  }
+  if (a[0] == Py_None) Py_RETURN_NONE;
+  if (!PyList_CheckExact(a[0])) {
+    PyErr_SetString(PyExc_TypeError, "pg_pool_execute: nets must be a list of NetConn or None");
     return nullptr;
   }
   Py_ssize_t spread = PyLong_AsSsize_t(a[3]);
   Py_ssize_t size = spread == -1 && PyErr_Occurred() ? -1 : PyLong_AsSsize_t(a[4]);
   if (size == -1 && PyErr_Occurred()) return nullptr;
-  PyObject* conns = a[0];
-  Py_ssize_t nc = PyList_GET_SIZE(conns);
+  PyObject* nets = a[0];
+  Py_ssize_t nc = PyList_GET_SIZE(nets);
   NetConnObject* best = nullptr;
   size_t bp = 0;
   Py_ssize_t live = 0;  // open connections: a closed one left in the list does not fill the pool
   for (Py_ssize_t i = 0; i < nc; ++i) {
-    PyObject* c = PyList_GET_ITEM(conns, i);
-    PyObject** dp = _PyObject_GetDictPtr(c);
-    PyObject* d = dp ? *dp : nullptr;
-    PyObject* closed = d ? PyDict_GetItemWithError(d, s_closed_name) : nullptr;
-    PyObject* net = closed ? PyDict_GetItemWithError(d, s_net_name) : nullptr;
-    if (!net) {
-      if (PyErr_Occurred()) return nullptr;
-      Py_RETURN_NONE;
-    }
-    if (closed == Py_True) continue;
-    if (closed != Py_False || Py_TYPE(net) != &NetConnType) Py_RETURN_NONE;  // asyncio transport: Python path
+    PyObject* net = PyList_GET_ITEM(nets, i);
+    if (Py_TYPE(net) != &NetConnType) Py_RETURN_NONE;
     NetConnObject* nc_ = reinterpret_cast<NetConnObject*>(net);
+    if (nc_->closed) continue;
     if (nc_->kind != K_PG) Py_RETURN_NONE;
     ++live;
     size_t p = nc_->pending->size();
@@ -1472,7 +1471,7 @@ PyMethodDef pool_functions[] = {
      "netconn_connect(ip, port, loop, kind, owner, parser, **NetConn keywords) -> NetConn; `handshake` resolves once "
      "connected (and TLS established)"},
     {"pg_pool_execute", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(mod_pg_pool_execute)),
-     METH_FASTCALL, "pg_pool_execute(conns, sql, params, spread_at, size) -> IOFuture or None (store/pgwire.py Pool)"},
+     METH_FASTCALL, "pg_pool_execute(nets, sql, params, spread_at, size) -> IOFuture or None (store/pgwire.py Pool)"},
     {nullptr, nullptr, 0, nullptr}};
 
 }  // namespace
@@ -1493,8 +1492,8 @@ void netconn_flush(PyObject* o) {
 
 // pg_pool_execute for a caller in C (the compiled handlers' Postgres queries): the same pick,
 // IOFuture or None (Python path), NULL on error.
-PyObject* pg_pool_execute_c(PyObject* conns, PyObject* sql, PyObject* params, PyObject* spread_at, PyObject* size) {
-  PyObject* a[5] = {conns, sql, params, spread_at, size};
+PyObject* pg_pool_execute_c(PyObject* nets, PyObject* sql, PyObject* params, PyObject* spread_at, PyObject* size) {
+  PyObject* a[5] = {nets, sql, params, spread_at, size};
   return mod_pg_pool_execute(nullptr, a, 5);
 }
 

@@ -574,6 +574,10 @@ class Pool:
         self._watchdog: Optional[asyncio.Task] = None
         self.stalls = 0
         self._conns: List[PgConnection] = []
+        # the native pick's view of `_conns` (_sync_nets): their NetConns, whose own closed flags
+        # it reads (a PgConnection and its NetConn close together), or None while any connection
+        # is on the asyncio path
+        self._nets: Optional[List[Any]] = []
         self._lock = asyncio.Lock()
         self._growing: Optional[asyncio.Future] = None
         self._grow_after = 0.0
@@ -601,7 +605,9 @@ class Pool:
                 for c in self._conns:
                     await c.close()
                 self._conns = []
+                self._sync_nets()
                 raise fatal
+        self._sync_nets()
         if self.stall_timeout_s:
             self._watchdog = asyncio.get_running_loop().create_task(self._watch_stalls())
         return self
@@ -633,7 +639,7 @@ class Pool:
         """Awaitable ``(rows, command_tag)`` (a future on the fast path)."""
         pick = self.native_pick
         if pick is not None:
-            f = pick(self._conns, sql, params, self.spread_at, self.size)  # None unless all connections native
+            f = pick(self._nets, sql, params, self.spread_at, self.size)  # None unless all connections native
             if f is not None:
                 return f
         best = None
@@ -673,12 +679,14 @@ class Pool:
             return
         self._conns[:] = [x for x in self._conns if not x.closed]
         self._conns.append(c)  # in place: a connect in _execute_slow appends to the same list
+        self._sync_nets()
         self.grows += 1
 
     async def _execute_slow(self, sql: str, params: Sequence[Any]):
         """No open connection: connect under the lock, so a burst makes one connection, then send."""
         async with self._lock:
             self._conns[:] = [c for c in self._conns if not c.closed]
+            self._sync_nets()
             live = self._conns
             if len(live) < self.size and (not live or min(c.pending for c in live) >= self.spread_at):
                 try:
@@ -686,6 +694,7 @@ class Pool:
                 except (OSError, asyncio.TimeoutError, PgError, PgProtocolError):
                     if not live:
                         raise
+                self._sync_nets()
             c = min(live, key=lambda c: c.pending)
         return await c.execute(sql, params)
 
@@ -708,3 +717,10 @@ class Pool:
         for c in list(self._conns):
             await c.close()
         self._conns = []
+        self._sync_nets()
+
+    def _sync_nets(self) -> None:
+        """Rebuilds ``_nets`` after ``_conns`` changed (closing needs no rebuild: the pick skips a
+        closed NetConn, as Pool.execute skips a closed connection)."""
+        nets = [c._net for c in self._conns]
+        self._nets = nets if all(n is not None for n in nets) else None

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Interleaved A/B of tcp_e2e in fresh processes: this tree ("new") against ab_old/ (an older tree
+# built in place, as scripts/box_r5_e2e_ab.sh describes). Each measurement: scripts/e2e_runs.py
+# (the bench's unmeasured warm-up pass, then one 250k-event run). One JSON line per measurement
+# in gpurun_out/$OUT/ab.jsonl.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+out=gpurun_out/${OUT:-e2e_pair_ab}
+mkdir -p "$out"
+root=$PWD
+for i in $(seq 1 "${RUNS:-8}"); do
+  for arm in new old; do
+    if [ "$arm" = old ]; then dir=$root/ab_old; else dir=$root; fi
+    (cd "$dir" && PYTHONPATH=$dir timeout -k 10 120 python scripts/e2e_runs.py --repeats "${REPEATS:-2}" ${TLS:+--tls}) > "$out/tmp.jsonl" 2>> "$out/ab.err" || exit 1
+    python - "$arm" "$i" "$out/tmp.jsonl" >> "$out/ab.jsonl" <<'PY'
+import json, sys
+for ln in open(sys.argv[3]):
+    k, r = next(iter(json.loads(ln).items()))
+    r.update(arm=sys.argv[1], pair=int(sys.argv[2]), cfg=k)
+    print(json.dumps(r))
+PY
+  done
+  tail -n 4 "$out/ab.jsonl" | cut -c1-200
+done

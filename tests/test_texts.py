@@ -39,7 +39,7 @@ ALLOWED_IDENTIFIERS = {
     "{s:K,s:K,s:O}", "{s:O}", "{}",
     # the capabilities a Pool (`native_pick`, over its connections) and an H1Client (`native_call`)
     # hand out, called directly
-    "Pool", "_conns", "native_pick", "beholder_amd.ops._native", "beholder_amd.store.pgwire", "pg_pool_execute",
+    "Pool", "_conns", "_nets", "native_pick", "beholder_amd.ops._native", "beholder_amd.store.pgwire", "pg_pool_execute",
     "size", "spread_at", "native_call", "native_record", "h1_fast",
 }
 # internal errors and docstrings (Python-level diagnostics, never emitted by the reference)
