@@ -26,6 +26,32 @@ namespace beholder {
     return errval;                                             \
   }
 
+// Values of a fixed set of keys in one dict, looked up again only after that dict changed. Every
+// modification of a dict gives it a new process-wide version (CPython 3.10 `ma_version_tag`, a
+// global counter), so the same dict object at the same version still holds the same values: the
+// hot paths read a client's or a store's configuration attributes from its instance dict per
+// request, and those never change after setup. Zero-initialised (tp_alloc / static) is empty.
+// Values are borrowed, exactly as PyDict_GetItemWithError's are (valid until the dict changes).
+template <int N>
+struct DictView {
+  PyObject* dict;
+  uint64_t version;
+  PyObject* v[N];
+  // `keys`: addresses of the interned key objects. false = a lookup raised (v not valid).
+  bool refresh(PyObject* d, PyObject* const* const* keys) {
+    const uint64_t ver = reinterpret_cast<PyDictObject*>(d)->ma_version_tag;
+    if (d == dict && ver == version) return true;
+    dict = nullptr;
+    for (int i = 0; i < N; ++i) {
+      v[i] = PyDict_GetItemWithError(d, *keys[i]);
+      if (!v[i] && PyErr_Occurred()) return false;
+    }
+    dict = d;
+    version = ver;
+    return true;
+  }
+};
+
 // Module-level state (single-phase init; one interpreter).
 struct ModuleState {
   PyObject* decode_error;  // exception raised by MessageCodec.decode

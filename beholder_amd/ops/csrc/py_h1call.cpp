@@ -209,6 +209,23 @@ int call_clear(H1CallObject* s) {
   return 0;
 }
 
+// The stock H1Client's attributes the native path reads per request (h1_start, send_on), from its
+// instance dict: looked up again only when that dict changed (DictView; `_sweeper` is rebound each
+// sweep tick, nothing else after setup).
+enum { CV_CLOSED, CV_ORIGINS, CV_COUNTS, CV_KEEPALIVE, CV_TIMEOUT, CV_BUSY, CV_TAIL, CV_TAIL_CL0, CV_SWEEPER, CV_N };
+PyObject* const* const kClientKeys[CV_N] = {&s_closed_attr, &s_origins, &s_counts, &s_keepalive_s, &s_timeout_s,
+                                            &s_busy,        &s_tail,    &s_tail_cl0, &s_sweeper};
+DictView<CV_N> g_client_view;
+
+// The client's instance dict with g_client_view current for it; NULL (no error) without one,
+// NULL with an error if a lookup raised.
+PyObject* client_view(PyObject* client) {
+  PyObject** dp = _PyObject_GetDictPtr(client);
+  PyObject* d = dp ? *dp : nullptr;
+  if (!d || !PyDict_CheckExact(d)) return nullptr;
+  return g_client_view.refresh(d, kClientKeys) ? d : nullptr;
+}
+
 PyObject* client_attr(PyObject* client, PyObject* name) {  // borrowed, from the instance dict
   PyObject** dp = _PyObject_GetDictPtr(client);
   PyObject* v = dp && *dp ? PyDict_GetItemWithError(*dp, name) : nullptr;
@@ -760,21 +777,12 @@ int h1_start(H1CallObject* s) {
   PyObject* timeout = s->timeout;
   // the shapes the sinks produce (split_shape): anything else takes the Python path, which
   // raises or handles it (a Mapping that is not a dict, a non-ASCII host, a bytes method, ...)
-  PyObject** dp = _PyObject_GetDictPtr(client);
-  PyObject* d = dp ? *dp : nullptr;
-  if (!d) return 0;
-  PyObject* cclosed = PyDict_GetItemWithError(d, s_closed_attr);
-  PyObject* origins = cclosed ? PyDict_GetItemWithError(d, s_origins) : nullptr;
-  PyObject* counts = origins ? PyDict_GetItemWithError(d, s_counts) : nullptr;
-  PyObject* keepalive = counts ? PyDict_GetItemWithError(d, s_keepalive_s) : nullptr;
-  PyObject* timeout_s = keepalive ? PyDict_GetItemWithError(d, s_timeout_s) : nullptr;
-  PyObject* busy = timeout_s ? PyDict_GetItemWithError(d, s_busy) : nullptr;
-  PyObject* tail = busy ? PyDict_GetItemWithError(d, s_tail) : nullptr;
-  PyObject* tail_cl0 = tail ? PyDict_GetItemWithError(d, s_tail_cl0) : nullptr;
-  if (!tail_cl0) {
-    if (PyErr_Occurred()) return -1;
-    return 0;
-  }
+  if (!client_view(client)) return PyErr_Occurred() ? -1 : 0;
+  PyObject* const* v = g_client_view.v;
+  PyObject *cclosed = v[CV_CLOSED], *origins = v[CV_ORIGINS], *counts = v[CV_COUNTS],
+           *keepalive = v[CV_KEEPALIVE], *timeout_s = v[CV_TIMEOUT], *busy = v[CV_BUSY], *tail = v[CV_TAIL],
+           *tail_cl0 = v[CV_TAIL_CL0];
+  if (!cclosed || !origins || !counts || !keepalive || !timeout_s || !busy || !tail || !tail_cl0) return 0;
   if (cclosed != Py_False || !PyDict_CheckExact(origins) || !PyDict_CheckExact(counts) || !PySet_CheckExact(busy) ||
       !PyBytes_CheckExact(tail) || !PyBytes_CheckExact(tail_cl0) || !PyFloat_CheckExact(keepalive))
     return 0;
@@ -909,11 +917,10 @@ int send_on(H1CallObject* s, PyObject* conn, const char* req, size_t reqlen, PyO
     PyErr_Restore(et, ev, tb);
     return -1;
   };
-  PyObject** dp = _PyObject_GetDictPtr(client);
-  PyObject* d = dp ? *dp : nullptr;
-  PyObject* counts = d ? PyDict_GetItemWithError(d, s_counts) : nullptr;
-  PyObject* busy = counts ? PyDict_GetItemWithError(d, s_busy) : nullptr;
-  if (!busy || !PyDict_CheckExact(counts) || !PySet_CheckExact(busy)) {
+  PyObject* d = client_view(client);
+  PyObject* counts = d ? g_client_view.v[CV_COUNTS] : nullptr;
+  PyObject* busy = d ? g_client_view.v[CV_BUSY] : nullptr;
+  if (!counts || !busy || !PyDict_CheckExact(counts) || !PySet_CheckExact(busy)) {
     if (!PyErr_Occurred()) PyErr_SetString(PyExc_RuntimeError, "H1Client state changed under a request");
     return fail();
   }

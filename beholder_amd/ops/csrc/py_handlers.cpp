@@ -150,6 +150,11 @@ struct HandlersObject {
   uint64_t suspended;
   uint8_t no_trello;
   uint8_t native_log;
+  // per-request attribute reads of the stock clients / store, cached per dict version (DictView)
+  DictView<9> trello_view;  // the Trello client's instance dict (TV_*)
+  DictView<2> http_view;    // the sink HTTP client's native_record / native_call
+  DictView<3> store_view;   // PostgresStore: _pool, _select, _update
+  DictView<4> pool_view;    // Pool: native_pick, _nets, spread_at, size
 };
 
 // out += template `t` with its holes filled by String(vals[i]) (as the reference's template literals)
@@ -339,27 +344,34 @@ bool raise_to_lower_case(HandlersObject* hs) {
 
 // The stock Postgres store with an open pool: `pool.execute(sql, params)` issued here (the
 // store's own coroutine is skipped). 2 = not applicable (use the store's API), else as await_start.
+PyObject* const* const kStoreKeys[3] = {&s_pool, &s_select, &s_update};
+PyObject* const* const kPoolKeys[4] = {&s_native_pick, &s_conns, &s_spread_at, &s_size};
+
 int pg_execute(CallObject* c, PyObject* store, PyObject* sql_name, PyObject* params, PyObject** out) {
   HandlersObject* hs = c->hs;
   if (reinterpret_cast<PyObject*>(Py_TYPE(store)) != hs->pg_cls) return 2;
   PyObject** dp = _PyObject_GetDictPtr(store);
   PyObject* sd = dp ? *dp : nullptr;
-  PyObject* pool = sd ? PyDict_GetItemWithError(sd, s_pool) : nullptr;
-  PyObject* sql = pool ? PyDict_GetItemWithError(sd, sql_name) : nullptr;
-  if (PyErr_Occurred()) return -1;
+  if (!sd || !PyDict_CheckExact(sd)) return 2;
+  if (!hs->store_view.refresh(sd, kStoreKeys)) return -1;
+  PyObject* pool = hs->store_view.v[0];
+  PyObject* sql = sql_name == s_select ? hs->store_view.v[1] : sql_name == s_update ? hs->store_view.v[2] : nullptr;
+  if (!sql && pool && sql_name != s_select && sql_name != s_update) {
+    sql = PyDict_GetItemWithError(sd, sql_name);
+    if (!sql && PyErr_Occurred()) return -1;
+  }
   if (!pool || pool == Py_None || !sql) return 2;  // not connected yet: the store connects first
   PyObject** pdp = reinterpret_cast<PyObject*>(Py_TYPE(pool)) == hs->pool_cls ? _PyObject_GetDictPtr(pool) : nullptr;
   PyObject* pd = pdp ? *pdp : nullptr;
-  PyObject* pick = pd ? PyDict_GetItemWithError(pd, s_native_pick) : nullptr;
-  if (PyErr_Occurred()) return -1;
+  if (pd && PyDict_CheckExact(pd) && !hs->pool_view.refresh(pd, kPoolKeys)) return -1;
+  PyObject* pick = pd && PyDict_CheckExact(pd) ? hs->pool_view.v[0] : nullptr;
   if (pick && pick == hs->pick_fn) {
     // the pool's native_pick capability (Pool.execute's fast path) in C: the least-loaded native
     // connection takes the query (Pool._nets: None while a connection is on the asyncio path)
-    PyObject* conns = PyDict_GetItemWithError(pd, s_conns);
-    PyObject* spread = conns ? PyDict_GetItemWithError(pd, s_spread_at) : nullptr;
-    PyObject* size = spread ? PyDict_GetItemWithError(pd, s_size) : nullptr;
-    if (!size && PyErr_Occurred()) return -1;
-    if (size && PyList_CheckExact(conns)) {
+    PyObject* conns = hs->pool_view.v[1];
+    PyObject* spread = hs->pool_view.v[2];
+    PyObject* size = hs->pool_view.v[3];
+    if (conns && spread && size && PyList_CheckExact(conns)) {
       Py_INCREF(conns);
       PyObject* f = pg_pool_execute_c(conns, sql, params, spread, size);
       Py_DECREF(conns);
@@ -557,13 +569,17 @@ void count_request(CallObject* c) {
 // Python method frame. The event's second and later sink requests (a status event's move, then
 // its hooks: index.js:83,99,112) are continuations: if they have to wait for a connection they
 // wait at the front of the origin's queue, not behind the first requests of newer deliveries.
+PyObject* const* const kHttpKeys[2] = {&s_native_record, &s_native_call};
+
 PyObject* http_request(CallObject* c, PyObject* http, PyObject* method, PyObject* url, PyObject* params,
                        PyObject* timeout) {
   HandlersObject* hs = c->hs;
   const bool front = c->nreq > 0;
   count_request(c);
   PyObject** dp = _PyObject_GetDictPtr(http);
-  PyObject* rec = dp && *dp ? PyDict_GetItemWithError(*dp, s_native_record) : nullptr;
+  PyObject* hd = dp && *dp && PyDict_CheckExact(*dp) ? *dp : nullptr;
+  if (hd && !hs->http_view.refresh(hd, kHttpKeys)) return nullptr;
+  PyObject* rec = hd ? hs->http_view.v[0] : nullptr;
   if (rec && PyCapsule_CheckExact(rec) && PyCapsule_IsValid(rec, kSinkHookName)) {
     // a client with a native sink hook (native_api.hpp; the in-process stub of the benches and
     // tests, sinks/http.py RecordingHttpClient): its request, without its coroutine
@@ -578,8 +594,7 @@ PyObject* http_request(CallObject* c, PyObject* http, PyObject* method, PyObject
     Py_DECREF(rec);
     return r;
   }
-  if (PyErr_Occurred()) return nullptr;
-  PyObject* cur = dp && *dp ? PyDict_GetItemWithError(*dp, s_native_call) : nullptr;
+  PyObject* cur = hd ? hs->http_view.v[1] : nullptr;
   if (cur && cur == hs->h1_fast_fn) {
     PyObject* call = h1_call_new(http, method, url, params ? params : Py_None, timeout, front);
     if (call != Py_None) return call;  // an H1Call, or NULL with an exception
@@ -654,6 +669,10 @@ PyObject* request_finish(CallObject* c, PyObject* value) {
 // await trello.makeRequest(method, path, {keys[i]: vals[i]}). For the stock TrelloClient the
 // request is built here: query {key, token, ...options} handed to http.request, as
 // sinks/trello.py does, with stats recorded by request_finish().
+enum { TV_LIMITER, TV_RETRY, TV_KEY, TV_TOKEN, TV_BASE_URL, TV_HTTP, TV_TIMEOUT, TV_STRICT, TV_STATS, TV_N };
+PyObject* const* const kTrelloKeys[TV_N] = {&s_limiter, &s_retry,   &s_key,    &s_token, &s_base_url,
+                                            &s_http,    &s_timeout, &s_strict, &s_stats};
+
 int trello_request(CallObject* c, PyObject* method, PyObject* method_upper, PyObject* path, PyObject* const* keys,
                    PyObject* const* vals, int nopt, PyObject** out) {
   HandlersObject* hs = c->hs;
@@ -661,18 +680,19 @@ int trello_request(CallObject* c, PyObject* method, PyObject* method_upper, PyOb
   if (!trello) return -1;
   bool fast = reinterpret_cast<PyObject*>(Py_TYPE(trello)) == hs->trello_cls;
   PyObject** dp = fast ? _PyObject_GetDictPtr(trello) : nullptr;
-  PyObject* td = dp ? *dp : nullptr;
+  PyObject* td = dp && *dp && PyDict_CheckExact(*dp) ? *dp : nullptr;
+  PyObject* const* tv = hs->trello_view.v;
   if (td) {  // a rate limit or 429 retries (sinks/ratelimit.py): the client's own make_request
-    PyObject* lim = PyDict_GetItemWithError(td, s_limiter);
-    PyObject* rty = !PyErr_Occurred() ? PyDict_GetItemWithError(td, s_retry) : nullptr;
-    if (PyErr_Occurred()) return -1;
+    if (!hs->trello_view.refresh(td, kTrelloKeys)) return -1;
+    PyObject* lim = tv[TV_LIMITER];
+    PyObject* rty = tv[TV_RETRY];
     if ((lim && lim != Py_None) || (rty && rty != Py_None)) td = nullptr;
   }
   PyObject* query = PyDict_New();
   if (!query) return -1;
   if (td) {  // {"key": self.key, "token": self.token, **options}
-    PyObject* key = PyDict_GetItemWithError(td, s_key);
-    PyObject* token = key ? PyDict_GetItemWithError(td, s_token) : nullptr;
+    PyObject* key = tv[TV_KEY];
+    PyObject* token = key ? tv[TV_TOKEN] : nullptr;
     if (!token || PyDict_SetItem(query, hs->x[X_Q_KEY], key) < 0 || PyDict_SetItem(query, hs->x[X_Q_TOKEN], token) < 0) {
       Py_DECREF(query);
       if (PyErr_Occurred()) return -1;
@@ -696,11 +716,12 @@ int trello_request(CallObject* c, PyObject* method, PyObject* method_upper, PyOb
     if (!aw) return -1;
     return await_start(c, aw, out);
   }
-  PyObject* base = PyDict_GetItemWithError(td, s_base_url);
-  PyObject* http = base ? PyDict_GetItemWithError(td, s_http) : nullptr;
-  PyObject* timeout = http ? PyDict_GetItemWithError(td, s_timeout) : nullptr;
-  PyObject* strict = timeout ? PyDict_GetItemWithError(td, s_strict) : nullptr;
-  PyObject* stats = strict ? PyDict_GetItemWithError(td, s_stats) : nullptr;
+  // the view is current for td: nothing ran since its refresh but dict stores on `query`
+  PyObject* base = tv[TV_BASE_URL];
+  PyObject* http = base ? tv[TV_HTTP] : nullptr;
+  PyObject* timeout = http ? tv[TV_TIMEOUT] : nullptr;
+  PyObject* strict = timeout ? tv[TV_STRICT] : nullptr;
+  PyObject* stats = strict ? tv[TV_STATS] : nullptr;
   if (!stats) {
     Py_DECREF(query);
     if (!PyErr_Occurred()) PyErr_SetString(PyExc_AttributeError, "TrelloClient attributes missing");
