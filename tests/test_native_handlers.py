@@ -442,3 +442,59 @@ def test_client_attribute_changes_are_seen_by_the_next_request():
 
 async def _drive(aw):
     return await aw
+
+
+def test_store_and_pool_changes_are_seen_by_the_next_query():
+    """The compiled handlers remember the Postgres store's `_pool` / statements and the pool's
+    pick state until their instance dicts change: a store reconnected onto a new pool (a new
+    Pool object, new NetConns) and a pool whose native pick is switched off are both used by the
+    very next event, and every event still reads its row."""
+    from pg_fake import FakePg
+    from beholder_amd.store import pgwire
+    from beholder_amd.store.postgres import PostgresStore
+    from helpers import trello_media
+
+    async def go():
+        pg = await FakePg(auth="trust").start()
+        try:
+            st = PostgresStore(pg.dsn, create_schema=True, pool_size=1)
+            await st.connect()
+            await st.upsert(trello_media("m1", "UPLOADING", card="C1"))
+            helpers.HANDLER_IMPL = "native"
+            try:
+                r = Rig(medias=[])
+            finally:
+                helpers.HANDLER_IMPL = "python"
+            r.h.store = st
+            nh = native_handlers(r.h)
+            calls = []
+            orig = pgwire.Pool.execute
+
+            def counting(self, sql, params=()):
+                if sql.startswith("SELECT"):  # the handlers' row reads (not the store's own DDL)
+                    calls.append(sql)
+                return orig(self, sql, params)
+            pgwire.Pool.execute = counting
+            try:
+                async def progress(i):
+                    d = r.delivery(2, progress_msg("m1", "QUEUED", i))
+                    await nh.on_progress(d)
+                    return d.acked
+                ok = [await progress(1)]
+                first_pool = st._pool
+                await st.close()  # a new pool on the next connect: new Pool, new NetConns
+                await st.connect()
+                ok.append(await progress(2))
+                ok.append(st._pool is not first_pool)
+                direct = len(calls)
+                st._pool.native_pick = None  # the pick off: Pool.execute in Python from now on
+                ok.append(await progress(3))
+                return ok, direct, len(calls), len(r.http.calls), list(calls)
+            finally:
+                pgwire.Pool.execute = orig
+                await st.close()
+        finally:
+            await pg.stop()
+    ok, direct, total, comments, calls_seen = asyncio.run(go())
+    assert ok == [True, True, True, True] and comments == 3
+    assert direct == 0 and total == 1, calls_seen  # native pick on both pools, then the Python path once
