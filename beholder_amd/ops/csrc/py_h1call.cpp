@@ -668,7 +668,7 @@ PyMethodDef call_methods[] = {
     {nullptr, nullptr, 0, nullptr}};
 
 // ---- h1_fast ----------------------------------------------------------------------------------
-PyObject* make_deadline(PyObject* loop, PyObject* timeout, PyObject* timeout_s, double now = -1.0);
+PyObject* make_deadline(PyObject* loop, PyObject* timeout, PyObject* timeout_s);
 int send_on(H1CallObject* s, PyObject* conn, const char* req, size_t reqlen, PyObject* method, PyObject* full,
             PyObject* deadline, bool head, bool from_idle);
 int queue_start(H1CallObject* s, PyObject* client, PyObject* counts, PyObject* o, PyObject* full,
@@ -703,43 +703,6 @@ bool split_shape(PyObject* method, PyObject* url, PyObject* params, Py_ssize_t* 
   if (params && has_q && PyDict_GET_SIZE(params)) return false;  // with_query appends with '&'
   *k_out = k;
   return true;
-}
-
-// The `_origins` entry of "scheme://authority" (u[0..k)), borrowed, or NULL (error set if a lookup
-// raised): a few recently used ones are remembered with the dict's version tag (see DictView), so a
-// request to a known origin skips making and hashing the key string.
-struct OriginCache {
-  PyObject* dict;
-  uint64_t version;
-  unsigned next;
-  struct Entry {
-    std::string key;
-    PyObject* origin;  // borrowed from `dict` (valid while its version is unchanged)
-  } e[4];
-};
-OriginCache* g_origin_cache;
-
-PyObject* origin_for(PyObject* origins, const char* u, Py_ssize_t k) {
-  if (!g_origin_cache) g_origin_cache = new OriginCache{};
-  OriginCache& oc = *g_origin_cache;
-  const uint64_t ver = reinterpret_cast<PyDictObject*>(origins)->ma_version_tag;
-  if (oc.dict != origins || oc.version != ver) {
-    for (auto& en : oc.e) en.origin = nullptr;
-    oc.dict = origins;
-    oc.version = ver;
-  }
-  for (auto& en : oc.e)
-    if (en.origin && en.key.size() == size_t(k) && memcmp(en.key.data(), u, size_t(k)) == 0) return en.origin;
-  PyObject* key = PyUnicode_FromStringAndSize(u, k);
-  if (!key) return nullptr;
-  PyObject* o = PyDict_GetItemWithError(origins, key);
-  Py_DECREF(key);
-  if (o) {
-    auto& en = oc.e[oc.next++ % 4];
-    en.key.assign(u, size_t(k));
-    en.origin = o;
-  }
-  return o;
 }
 
 // The request text for a URL that passed split_shape, on an origin whose Host header is `host`
@@ -826,7 +789,10 @@ int h1_start(H1CallObject* s) {
 
   Py_ssize_t k;
   if (!split_shape(method, url, params, &k)) return 0;
-  PyObject* o = origin_for(origins, reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(url)), k);
+  PyObject* key = PyUnicode_FromStringAndSize(reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(url)), k);
+  if (!key) return -1;
+  PyObject* o = PyDict_GetItemWithError(origins, key);
+  Py_DECREF(key);
   if (!o) {
     if (PyErr_Occurred()) return -1;
     return 0;  // first request to this origin: the Python path creates it
@@ -846,7 +812,6 @@ int h1_start(H1CallObject* s) {
 
   // a live idle keep-alive connection on a NetConn (the Python fast path's idle pop)
   double ka = PyFloat_AS_DOUBLE(keepalive);
-  const double now = mono_s();  // the idle check's and the request deadline's clock reading
   PyObject* conn = nullptr;
   for (;;) {
     Py_ssize_t n = PyObject_Size(idle);
@@ -868,7 +833,7 @@ int h1_start(H1CallObject* s) {
       Py_DECREF(cand);
       return -1;
     }
-    if (closed == Py_False && now - lu < ka) {
+    if (closed == Py_False && mono_s() - lu < ka) {
       PyObject* net = g.conn.get(cand, C_NET);
       if (!net || !is_netconn(net) || !netconn_open(net)) {  // asyncio transport: Python path
         PyObject* r = PyObject_CallMethodOneArg(idle, s_append, cand);
@@ -889,7 +854,7 @@ int h1_start(H1CallObject* s) {
   // committed: the request goes out on `conn` (send_on owns it from here, and hands it back on
   // a failure); the connection's loop, as asyncio.get_running_loop() would cost a getpid(2)
   PyObject* deadline = bump(counts, s_requests) < 0 ? nullptr
-                       : make_deadline(netconn_loop(g.conn.get(conn, C_NET)), timeout, timeout_s, now);
+                       : make_deadline(netconn_loop(g.conn.get(conn, C_NET)), timeout, timeout_s);
   if (!deadline) {
     PyObject *et, *ev, *tb;
     PyErr_Fetch(&et, &ev, &tb);
@@ -907,12 +872,11 @@ int h1_start(H1CallObject* s) {
 }
 
 // The queue deadline and request deadlines: loop.time() + (timeout or client.timeout_s). New
-// reference, NULL on error. `now`: a time.monotonic() reading the caller took just before (>= 0),
-// used when loop.time() is BaseEventLoop's.
-PyObject* make_deadline(PyObject* loop, PyObject* timeout, PyObject* timeout_s, double now) {
+// reference, NULL on error.
+PyObject* make_deadline(PyObject* loop, PyObject* timeout, PyObject* timeout_s) {
   double dl;
   if (g.base_time && _PyType_Lookup(Py_TYPE(loop), s_time) == g.base_time) {
-    dl = now >= 0 ? now : mono_s();  // BaseEventLoop.time() is time.monotonic()
+    dl = mono_s();  // BaseEventLoop.time() is time.monotonic()
   } else {
     PyObject* now = PyObject_CallMethodNoArgs(loop, s_time);
     if (!now) return nullptr;
