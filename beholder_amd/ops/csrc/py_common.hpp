@@ -27,7 +27,7 @@ namespace beholder {
   }
 
 // Values of a fixed set of keys in one dict, looked up again only after that dict changed. Every
-// modification of a dict gives it a new process-wide version (CPython 3.10 `ma_version_tag`, a
+// modification of a dict gives it a new process-wide version (CPython 3.10/3.11 `ma_version_tag`, a
 // global counter), so the same dict object at the same version still holds the same values: the
 // hot paths read a client's or a store's configuration attributes from its instance dict per
 // request, and those never change after setup. Zero-initialised (tp_alloc / static) is empty.
@@ -39,8 +39,12 @@ struct DictView {
   PyObject* v[N];
   // `keys`: addresses of the interned key objects. false = a lookup raised (v not valid).
   bool refresh(PyObject* d, PyObject* const* const* keys) {
+#if PY_VERSION_HEX < 0x030C0000
     const uint64_t ver = reinterpret_cast<PyDictObject*>(d)->ma_version_tag;
     if (d == dict && ver == version) return true;
+#else  // the version tag is deprecated from 3.12 (PEP 699): look the keys up every time
+    const uint64_t ver = 0;
+#endif
     dict = nullptr;
     for (int i = 0; i < N; ++i) {
       v[i] = PyDict_GetItemWithError(d, *keys[i]);
