@@ -524,11 +524,11 @@ def io_extras(a) -> dict:
     # unmeasured: one short pass of the whole TCP path first, so the first measured e2e phase is
     # not also this process's first (first-touch page faults, the pools' and fakes' first
     # connections, lazily imported modules), as the paced configs get one
-    harness._tcp_e2e(min(20000, a.e2e_events))
+    harness._tcp_e2e(min(100000, a.e2e_events))
     out.update(_e2e_keys("tcp_e2e", harness._tcp_e2e, a.e2e_events, a.e2e_repeats))
     # and of the TLS path: its first run in a process paid ~1 µs/event more system time (OpenSSL's
     # connection buffers first touched; profiles/box_r5_runs/, box_r5_pgn/)
-    harness._tcp_e2e(min(20000, a.e2e_events), http_servers=4, tls=True)
+    harness._tcp_e2e(min(100000, a.e2e_events), http_servers=4, tls=True)
     out.update(_e2e_keys("tls_e2e", harness._tcp_e2e, a.e2e_events, a.e2e_repeats, http_servers=4, tls=True))
     # the same with service.http.preconnect = prefetch: the first wave of TLS handshakes happens
     # in init (`_init_ms`), not inside the first deliveries' handle latency
