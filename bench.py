@@ -760,7 +760,8 @@ DIAG_FIRST = (
     "tcp_e2e_runs", "tls_e2e_runs",
     "tls_e2e_calib_ns", "tls_e2e_sys_cpu_us_per_event", "tls_e2e_minflt", "tls_e2e_nivcsw",
     "tls_e2e_fakes_cpu_us_per_event", "tls_e2e_host_cpu_busy_pct", "tls_e2e_slow_blamed",
-    "headline_minflt", "involuntary_ctx_switches", "headline_host_cpu_busy_pct", "calib_mem_ns", "calib_py_ns",
+    "headline_minflt", "headline_run_delay_ms", "involuntary_ctx_switches", "headline_host_cpu_busy_pct",
+    "calib_mem_ns", "calib_py_ns",
     "shared_queue_broker_cpu_us_per_event", "shared_queue_acked", "shared_queue_published",
     "plumbing_rc", "plumbing_acked", "plumbing_sink_requests", "rate_1k_acked", "rate_10k_acked",
     "rate_100k_offered", "rate_100k_accepted", "burst_offered", "burst_accepted",
@@ -825,7 +826,8 @@ def main(argv=None) -> int:
     dev = _Device(dist.local_rank)
     extras: dict = {}
 
-    from beholder_amd.utils.hostinfo import cgroup_cpu_stat, cgroup_delta, host_busy_pct, host_cpu_times
+    from beholder_amd.utils.hostinfo import (cgroup_cpu_stat, cgroup_delta, host_busy_pct, host_cpu_times,
+                                             proc_run_delay_ns)
 
     # 1. phases that start child processes (before any HIP call in this process)
     if a.extras and dist.rank == 0:
@@ -847,7 +849,9 @@ def main(argv=None) -> int:
     cg0 = cgroup_cpu_stat()
     h0 = host_cpu_times()
     gc.collect()
+    rq0 = proc_run_delay_ns()
     res = run_solo(a, dist, dev)
+    rq1 = proc_run_delay_ns()
     dist.barrier()
     cg1 = cgroup_cpu_stat()
     h1 = host_cpu_times()
@@ -856,6 +860,8 @@ def main(argv=None) -> int:
     parts = dist.gather({k: res[k] for k in ("handle_hist", "ingest_hist", "http_calls", "errors", "abandoned",
                                              "events", "cpu_s", "nivcsw", "minflt", "majflt")})
     calibs = dist.gather((calib0, calib1))
+    # this rank's threads' time runnable without a CPU over the headline (warm-up steps included)
+    run_delays = dist.gather((rq1 - rq0) / 1e6 if rq0 is not None and rq1 is not None else None)
 
     # 4. BASELINE config 5 (no child processes: HIP may be initialised now)
     if a.extras and dist.rank == 0:
@@ -905,6 +911,8 @@ def main(argv=None) -> int:
             "cpu_us_per_event": round(sum(p["cpu_s"] for p in parts) / total_events * 1e6, 3),
             "involuntary_ctx_switches": sum(p["nivcsw"] for p in parts),
             "headline_minflt": sum(p["minflt"] for p in parts),
+            "headline_run_delay_ms": (round(max(run_delays), 2) if all(x is not None for x in run_delays)
+                                      else None),
             "headline_majflt": sum(p["majflt"] for p in parts),
             "thp": _thp_mode(),
             **cal,

@@ -107,6 +107,7 @@ def test_bench_single_rank_contract(tmp_path):
     assert all(x > 0 for x in runs["events_per_poll_run"]), runs
     assert out["tcp_e2e_run_delay_ms"] is None or out["tcp_e2e_run_delay_ms"] >= 0
     assert out["rate_10k_loop_run_delay_us"] is None or out["rate_10k_loop_run_delay_us"] >= 0
+    assert out["headline_run_delay_ms"] is None or out["headline_run_delay_ms"] >= 0
     # the consumer's socket calls per event: a send per sink request, queries
     # and acks batched, every kind of connection seen
     io = out["tcp_e2e_io_per_event"]
