@@ -516,7 +516,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = Fal
     from ..sinks import H1Client
     from ..store.postgres import PostgresStore
     from ..transport.amqp import AmqpSource
-    from ..utils.hostinfo import cgroup_cpu_stat, cgroup_delta, proc_cpu_s, proc_run_delay_ns
+    from ..utils.hostinfo import cgroup_cpu_stat, cgroup_delta, proc_cpu_s, thread_run_delay_ns
     from ..utils.log import Logger
     from .stallmon import StallMonitor
 
@@ -575,7 +575,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = Fal
             cg1 = cgroup_cpu_stat()
             fcpu0 = [proc_cpu_s(p.pid) for _, p in kinds]
             io0 = _io_counts(src)
-            rq0 = proc_run_delay_ns()
+            rq0 = thread_run_delay_ns()  # this (the event loop's) thread
             ru0 = resource.getrusage(resource.RUSAGE_SELF)
             if hooks:
                 hooks[0]()
@@ -585,7 +585,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = Fal
             if hooks:
                 hooks[1]()
             ru1 = resource.getrusage(resource.RUSAGE_SELF)
-            rq1 = proc_run_delay_ns()
+            rq1 = thread_run_delay_ns()
             io1 = _io_counts(src)
             fcpu1 = [proc_cpu_s(p.pid) for _, p in kinds]
             cg2 = cgroup_cpu_stat()
@@ -640,7 +640,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = Fal
             # item 4: which writes could share a wake-up): AMQP reads / writes (acks), sink and
             # Postgres sends / receives, NetPoller callbacks and the sockets each found ready
             "io_per_event": {k: round(v / m, 4) for k, v in diag["io"].items()} if m else {},
-            # the consumer's threads' time runnable but waiting for a CPU over the window
+            # the consumer's loop thread's time runnable but waiting for a CPU over the window
             "run_delay_ms": diag["run_delay_ms"],
         })
     finally:

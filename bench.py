@@ -827,7 +827,7 @@ def main(argv=None) -> int:
     extras: dict = {}
 
     from beholder_amd.utils.hostinfo import (cgroup_cpu_stat, cgroup_delta, host_busy_pct, host_cpu_times,
-                                             proc_run_delay_ns)
+                                             thread_run_delay_ns)
 
     # 1. phases that start child processes (before any HIP call in this process)
     if a.extras and dist.rank == 0:
@@ -849,9 +849,9 @@ def main(argv=None) -> int:
     cg0 = cgroup_cpu_stat()
     h0 = host_cpu_times()
     gc.collect()
-    rq0 = proc_run_delay_ns()
+    rq0 = thread_run_delay_ns()  # the thread that runs the consumer's event loop
     res = run_solo(a, dist, dev)
-    rq1 = proc_run_delay_ns()
+    rq1 = thread_run_delay_ns()
     dist.barrier()
     cg1 = cgroup_cpu_stat()
     h1 = host_cpu_times()
@@ -860,7 +860,8 @@ def main(argv=None) -> int:
     parts = dist.gather({k: res[k] for k in ("handle_hist", "ingest_hist", "http_calls", "errors", "abandoned",
                                              "events", "cpu_s", "nivcsw", "minflt", "majflt")})
     calibs = dist.gather((calib0, calib1))
-    # this rank's threads' time runnable without a CPU over the headline (warm-up steps included)
+    # the loop thread's time runnable without a CPU over the headline (warm-up steps included); the
+    # process total would also hold the reader thread's many short wake-up waits
     run_delays = dist.gather((rq1 - rq0) / 1e6 if rq0 is not None and rq1 is not None else None)
 
     # 4. BASELINE config 5 (no child processes: HIP may be initialised now)
