@@ -580,6 +580,10 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = Fal
             if hooks:
                 hooks[0]()
             t0 = time.perf_counter()
+            # half-way: the RSS there against the end is the leak check (the first half still
+            # grows the sink pool towards its steady size: tens of connections with their buffers)
+            await _wait_acked(src.settler, warm + (n - warm) // 2, task)
+            rss_mid = _rss_mb()
             await _wait_acked(src.settler, n, task)
             elapsed = time.perf_counter() - t0
             if hooks:
@@ -612,8 +616,8 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = Fal
             diag = {"warm_slow": warm_slow, "steady_slow": steady_slow, "mon": mon, "warm_mon": warm_mon,
                     "nivcsw": ru1.ru_nivcsw - ru0.ru_nivcsw, "cgroup_warmup": cgroup_delta(cg0, cg1),
                     "cgroup_steady": cgroup_delta(cg1, cg2), "fakes_cpu_s": fakes_cpu, "fakes_util": fakes_util,
-                    "minflt": ru1.ru_minflt - ru0.ru_minflt, "majflt": ru1.ru_majflt - ru0.ru_majflt,
-                    "io": {k: io1[k] - io0[k] for k in io0},
+                    "minflt": ru1.ru_minflt - ru0.ru_minflt, "majflt": ru1.ru_majflt - ru0.ru_majflt, "rss0": rss0,
+                    "io": {k: io1[k] - io0[k] for k in io0}, "rss_mid": rss_mid,
                     "run_delay_ms": (rq1 - rq0) / 1e6 if rq0 is not None and rq1 is not None else None}
             return elapsed, stats, cpu, ru1.ru_stime - ru0.ru_stime, pg_conns, http_stats, measured, cold, rss1 - rss0, diag
 
@@ -628,6 +632,8 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = Fal
             "warmup_handle_latency_us": {k: v / 1e3 for k, v in cold.items() if k.startswith("p")},
             "errors": sum(stats.get("handler_errors", {}).values()),
             "pg_connections": pg_conns, "http": http_stats, "rss_growth_mb": round(rss_growth, 2),
+            # second half of the window only (see rss_mid): growth there would be per event
+            "rss_growth_second_half_mb": round(rss_growth - (diag["rss_mid"] - diag["rss0"]), 2),
             "nivcsw": diag["nivcsw"], "cgroup_warmup": diag["cgroup_warmup"], "cgroup_steady": diag["cgroup_steady"],
             "minflt": diag["minflt"], "majflt": diag["majflt"],
             # each fake's CPU over the measured window, per consumed event (broker / pg / http(s)):
