@@ -594,9 +594,11 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = Fal
             fcpu1 = [proc_cpu_s(p.pid) for _, p in kinds]
             cg2 = cgroup_cpu_stat()
             mon.stop()
-            steady_slow = _slowest(src.settler.slow_deliveries()[0], _settled(src.settler) - settled0)
             gc.collect()
+            # before the slow-delivery list is made: up to 65,536 traced (recv, start, settle)
+            # tuples are ~10 MB of Python objects whose pymalloc arenas stay mapped afterwards
             rss1 = _rss_mb()
+            steady_slow = _slowest(src.settler.slow_deliveries()[0], _settled(src.settler) - settled0)
             measured = _settled(src.settler) - settled0
             await asyncio.sleep(0.05)  # let the last acks flush
             svc.request_stop()
