@@ -365,17 +365,26 @@ def _settled(settler) -> int:
 
 async def _wait_acked(settler, n: int, task, stall_s: float = 15.0) -> None:
     """Until n deliveries are settled one way or another (acked, or abandoned under Q1), the
-    service stops, or nothing moves for ``stall_s`` (a broken run must not hang the bench)."""
+    service stops, or nothing moves for ``stall_s`` (a broken run must not hang the bench).
+
+    The poll runs on the measured event loop, so it sleeps about a quarter of the remaining time
+    at the rate seen so far (at most 50 ms, at least 1 ms near the end): a fixed 1 ms poll made
+    ~1,000 bench wake-ups per second of the consumer's CPU."""
     last, t_last = -1, time.monotonic()
+    rate = 0.0
     while not task.done():
         done = _settled(settler)
         if done >= n:
             return
+        now = time.monotonic()
         if done != last:
-            last, t_last = done, time.monotonic()
-        elif time.monotonic() - t_last > stall_s:
+            if last >= 0 and now > t_last:
+                rate = (done - last) / (now - t_last)
+            last, t_last = done, now
+        elif now - t_last > stall_s:
             return
-        await asyncio.sleep(0.001)
+        wait = (n - done) / rate / 4 if rate > 0 else 0.001
+        await asyncio.sleep(min(0.05, max(0.001, wait)))
 
 
 def _die_with_parent():
