@@ -453,6 +453,8 @@ def _e2e_keys(prefix: str, run, n: int, repeats: int = 1, **kw) -> dict:
            f"{prefix}_fakes_cpu_us_per_event": e.get("fakes_cpu_us_per_event"),
            f"{prefix}_fakes_util": e.get("fakes_util"),
            f"{prefix}_io_per_event": e.get("io_per_event"),
+           f"{prefix}_rss_growth_mb": e.get("rss_growth_mb"),
+           f"{prefix}_rss_growth_second_half_mb": e.get("rss_growth_second_half_mb"),
            f"{prefix}_run_delay_ms": _r(e.get("run_delay_ms"), 2),
            f"{prefix}_host_cpu_busy_pct": busy,
            **_cg(prefix, e.get("cgroup_steady") or {}),
