@@ -21,6 +21,7 @@ from __future__ import annotations
 import argparse
 import asyncio
 import collections
+import signal
 import struct
 import sys
 import time
@@ -438,25 +439,36 @@ def _serve_native(events: List[Tuple[str, bytes]], a) -> None:
     b = SharedBroker(b"".join(pieces), offs.tobytes(), bytes(qi[q] for q, _ in events), tuple(names), a.consumers)
     del pieces
     port = b.listen()
+    if a.hold:  # SIGTERM reaches this thread only (sigwait below), never the loop's
+        signal.pthread_sigmask(signal.SIG_BLOCK, {signal.SIGTERM})
     print(f"READY {port}", flush=True)
-    t = threading.Thread(target=b.run, args=(0.2,), name="shared-broker", daemon=True)
+    t = threading.Thread(target=b.run, args=(-1.0 if a.hold else 0.2,), name="shared-broker", daemon=True)
     t.start()
     every = a.progress_every
     nxt = every
     while t.is_alive():
         t.join(0.005)
-        if every:
-            st = b.stats()
-            if st["acked"] >= nxt:
-                nxt = (st["acked"] // every + 1) * every
-                print(f"PROGRESS acked={st['acked']} connections={st['connections']}", flush=True)
-    st = b.stats()
-    line = (f"sent={st['sent']} acked={st['acked']} published={st['published']} dup_acks={st['dup_acks']} "
-            f"unknown_acks={st['unknown_acks']} lost={st['lost']} redelivered={st['redelivered']} "
-            f"connections={st['connections']} per_conn={','.join(map(str, st['per_conn']))} "
-            f"broker_s={st['broker_s']:.6f} cpu_s={st['cpu_s']:.6f}")
-    print("DONE " + line, flush=True)
-    print("FINAL " + line, flush=True)
+        st = b.stats()
+        if every and st["acked"] >= nxt:
+            nxt = (st["acked"] // every + 1) * every
+            print(f"PROGRESS acked={st['acked']} connections={st['connections']}", flush=True)
+        if a.hold and st["done"]:
+            time.sleep(0.2)  # late duplicate acks, if any, are counted
+            break
+
+    def line() -> str:
+        st = b.stats()
+        return (f"sent={st['sent']} acked={st['acked']} published={st['published']} dup_acks={st['dup_acks']} "
+                f"unknown_acks={st['unknown_acks']} lost={st['lost']} redelivered={st['redelivered']} "
+                f"connections={st['connections']} per_conn={','.join(map(str, st['per_conn']))} "
+                f"broker_s={st['broker_s']:.6f} cpu_s={st['cpu_s']:.6f}")
+    done = line()
+    print("DONE " + done, flush=True)
+    print("FINAL " + done, flush=True)
+    if a.hold:  # still serving (a worker restarted after the last ack gets its session) until SIGTERM
+        signal.sigwait({signal.SIGTERM})
+        b.stop()
+        t.join(5)
 
 
 async def _main(a) -> None:
@@ -476,6 +488,10 @@ async def _main(a) -> None:
         print(sb.done_line(), flush=True)
         await asyncio.sleep(0.2)  # the consumers' last acks of duplicates, if any, are counted
         print(sb.done_line().replace("DONE ", "FINAL ", 1), flush=True)
+        if a.hold:  # still serving (a worker restarted after the last ack gets its session) until SIGTERM
+            stop = asyncio.get_running_loop().create_future()
+            asyncio.get_running_loop().add_signal_handler(signal.SIGTERM, lambda: stop.done() or stop.set_result(None))
+            await stop
         return
     b = await ReplayBroker(events, a.port).start()
     del w
@@ -501,6 +517,9 @@ def main(argv=None) -> int:
                     help="--shared: start delivering once this many connections have subscribed")
     ap.add_argument("--progress-every", type=int, default=0,
                     help="--shared: print a PROGRESS line each time this many more events are acked")
+    ap.add_argument("--hold", action="store_true",
+                    help="--shared: keep serving after FINAL until SIGTERM (a consumer restarted after the "
+                         "last ack still gets its session)")
     ap.add_argument("--python", action="store_true",
                     help="--shared: the asyncio SharedQueueBroker instead of the native SharedBroker")
     asyncio.run(_main(ap.parse_args(argv)))

@@ -67,7 +67,7 @@ def run_shared(workers: int, events: int, *, media: int = 10000, seed: int = 0, 
         raise ValueError("broker must be 'native' or 'python'")
     port, bprocs = _spawn("beholder_amd.bench.replay_broker", 1,
                           ("--events", str(events), "--media", str(media), "--seed", str(seed), "--shared",
-                           "--consumers", str(workers), "--progress-every", str(kill_one_after),
+                           "--consumers", str(workers), "--progress-every", str(kill_one_after), "--hold",
                            *(("--python",) if broker == "python" else ())))
     broker_proc = bprocs[0]
     lines: List[str] = []

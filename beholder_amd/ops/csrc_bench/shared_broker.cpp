@@ -123,7 +123,12 @@ struct SharedBrokerObject {
   int64_t t_first, t_done;
   double cpu_first, cpu_s;
   std::vector<uint64_t>* per_conn;  // deliveries per connection (in connection order)
+  // the same, readable while the loop runs (stats() of a broker serving until stop()); the first
+  // kLiveSlots connections only
+  std::atomic<uint64_t>* per_conn_live;
 };
+
+constexpr size_t kLiveSlots = 4096;
 
 PyTypeObject SharedBrokerType = {PyVarObject_HEAD_INIT(nullptr, 0)};
 
@@ -401,6 +406,7 @@ struct Loop {
     for (size_t t = c.low; t < c.tags.size(); ++t)
       if (!c.settled[t] && !(*b->ack_counts)[c.tags[t]]) b->requeue->push_back(c.tags[t]);
     (*b->per_conn)[slot_of[fd]] = c.delivered;
+    if (slot_of[fd] < kLiveSlots) b->per_conn_live[slot_of[fd]].store(c.delivered, std::memory_order_relaxed);
     epoll_ctl(b->efd, EPOLL_CTL_DEL, fd, nullptr);
     ::close(fd);
     conns.erase(it);
@@ -425,12 +431,12 @@ struct Loop {
     }
   }
 
-  void run(double linger_s) {
+  void run(double linger_s) {  // linger_s < 0: serve until stop() (done or not)
     std::vector<epoll_event> evs(256);
     std::vector<char> buf(1 << 17);
     int64_t linger_until = 0;
     while (!b->stop.load()) {
-      if (b->done.load()) {
+      if (b->done.load() && linger_s >= 0) {
         if (!linger_until) linger_until = mono_ns() + int64_t(linger_s * 1e9);
         if (mono_ns() >= linger_until) break;
       }
@@ -473,6 +479,8 @@ struct Loop {
       for (auto& kv : conns) {
         Conn& c = *kv.second;
         pump(c);
+        size_t slot = slot_of[kv.first];
+        if (slot < kLiveSlots) b->per_conn_live[slot].store(c.delivered, std::memory_order_relaxed);
         if (c.writable && c.out.size() > c.out_off && !flush(c)) dead.push_back(kv.first);
       }
       for (int fd : dead) drop(fd);
@@ -502,7 +510,9 @@ PyObject* sb_new(PyTypeObject* type, PyObject*, PyObject*) {
   s->ack_counts = new (std::nothrow) std::vector<uint8_t>();
   s->requeue = new (std::nothrow) std::deque<uint32_t>();
   s->per_conn = new (std::nothrow) std::vector<uint64_t>();
-  if (!s->content || !s->coff || !s->qidx || !s->qnames || !s->ack_counts || !s->requeue || !s->per_conn) {
+  s->per_conn_live = new (std::nothrow) std::atomic<uint64_t>[kLiveSlots]();
+  if (!s->content || !s->coff || !s->qidx || !s->qnames || !s->ack_counts || !s->requeue || !s->per_conn ||
+      !s->per_conn_live) {
     Py_DECREF(s);
     return PyErr_NoMemory();
   }
@@ -519,6 +529,7 @@ void sb_dealloc(SharedBrokerObject* s) {
   delete s->ack_counts;
   delete s->requeue;
   delete s->per_conn;
+  delete[] s->per_conn_live;
   Py_TYPE(s)->tp_free(reinterpret_cast<PyObject*>(s));
 }
 
@@ -610,7 +621,8 @@ PyObject* sb_listen(SharedBrokerObject* s, PyObject*) {
 }
 
 // run(linger_s=0.2): serves until every event is acked (then `linger_s` more, so late duplicate
-// acks are counted) or stop(). Blocks without the GIL.
+// acks are counted) or stop(); linger_s < 0: until stop() only (a consumer that connects after the
+// last ack still gets its session). Blocks without the GIL.
 PyObject* sb_run(SharedBrokerObject* s, PyObject* args) {
   double linger = 0.2;
   if (!PyArg_ParseTuple(args, "|d", &linger)) return nullptr;
@@ -643,24 +655,30 @@ PyObject* sb_stop(SharedBrokerObject* s, PyObject*) {
   Py_RETURN_NONE;
 }
 
-// stats() -> dict; safe while run() is going (per-connection counts once it has returned)
+// stats() -> dict; safe while run() is going (per-connection counts then from the live slots,
+// `lost` = events not acked yet)
 PyObject* sb_stats(SharedBrokerObject* s, PyObject*) {
   uint64_t lost = 0;
   bool finished = !s->running.load();
+  const uint64_t published = s->coff->size() - 1, acked_now = s->acked.load();  // a snapshot
   if (finished)
     for (uint8_t c : *s->ack_counts) lost += c == 0;
+  else
+    lost = published - acked_now;  // events not acked yet (acked counts each event once)
   PyObject* per = PyList_New(0);
   if (!per) return nullptr;
-  if (finished)
-    for (uint64_t v : *s->per_conn) {
-      PyObject* x = PyLong_FromUnsignedLongLong(v);
-      if (!x || PyList_Append(per, x) < 0) {
-        Py_XDECREF(x);
-        Py_DECREF(per);
-        return nullptr;
-      }
-      Py_DECREF(x);
+  const size_t nconn = size_t(s->connections.load());
+  const size_t nper = finished ? s->per_conn->size() : (nconn < kLiveSlots ? nconn : kLiveSlots);
+  for (size_t i = 0; i < nper; ++i) {
+    uint64_t v = finished ? (*s->per_conn)[i] : s->per_conn_live[i].load(std::memory_order_relaxed);
+    PyObject* x = PyLong_FromUnsignedLongLong(v);
+    if (!x || PyList_Append(per, x) < 0) {
+      Py_XDECREF(x);
+      Py_DECREF(per);
+      return nullptr;
     }
+    Py_DECREF(x);
+  }
   // t_first / t_done / cpu_s are written by the loop thread before it sets `done`
   const bool done = s->done.load();
   double span = done && s->t_first ? double(s->t_done - s->t_first) * 1e-9 : 0.0;
@@ -670,7 +688,7 @@ PyObject* sb_stats(SharedBrokerObject* s, PyObject*) {
                        (unsigned long long)s->acked.load(), "dup_acks", (unsigned long long)s->dup_acks.load(),
                        "unknown_acks", (unsigned long long)s->unknown_acks.load(), "redelivered",
                        (unsigned long long)s->redelivered.load(), "connections",
-                       (unsigned long long)s->connections.load(), "lost", (unsigned long long)(finished ? lost : 0),
+                       (unsigned long long)s->connections.load(), "lost", (unsigned long long)lost,
                        "per_conn", per, "broker_s", span, "cpu_s", cpu, "done", done ? Py_True : Py_False,
                        "finished", finished ? Py_True : Py_False);
 }
@@ -678,7 +696,7 @@ PyObject* sb_stats(SharedBrokerObject* s, PyObject*) {
 PyMethodDef sb_methods[] = {
     {"listen", reinterpret_cast<PyCFunction>(sb_listen), METH_NOARGS, "listen() -> port (127.0.0.1)"},
     {"run", reinterpret_cast<PyCFunction>(sb_run), METH_VARARGS,
-     "run(linger_s=0.2): serve until every event is acked (+ linger) or stop(); releases the GIL"},
+     "run(linger_s=0.2): serve until every event is acked (+ linger; < 0: until stop()) or stop(); releases the GIL"},
     {"stop", reinterpret_cast<PyCFunction>(sb_stop), METH_NOARGS, "stop(): make run() return"},
     {"stats", reinterpret_cast<PyCFunction>(sb_stats), METH_NOARGS, "stats() -> dict"},
     {nullptr, nullptr, 0, nullptr}};
