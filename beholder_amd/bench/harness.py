@@ -368,10 +368,12 @@ async def _wait_acked(settler, n: int, task, stall_s: float = 15.0) -> None:
     service stops, or nothing moves for ``stall_s`` (a broken run must not hang the bench).
 
     The poll runs on the measured event loop, so it sleeps about a quarter of the remaining time
-    at the rate seen so far (at most 50 ms, at least 1 ms near the end): a fixed 1 ms poll made
-    ~1,000 bench wake-ups per second of the consumer's CPU."""
+    at the rate seen so far (at least 1 ms, at most 50 ms and twice the previous sleep): a fixed
+    1 ms poll made ~1,000 bench wake-ups per second of the consumer's CPU."""
     last, t_last = -1, time.monotonic()
     rate = 0.0
+    prev = 0.001  # each sleep at most doubles the last one: a rate still ramping up (the
+    # warm-up's first connections) is not trusted for a long sleep that would overshoot n
     while not task.done():
         done = _settled(settler)
         if done >= n:
@@ -384,7 +386,8 @@ async def _wait_acked(settler, n: int, task, stall_s: float = 15.0) -> None:
         elif now - t_last > stall_s:
             return
         wait = (n - done) / rate / 4 if rate > 0 else 0.001
-        await asyncio.sleep(min(0.05, max(0.001, wait)))
+        prev = min(0.05, max(0.001, min(wait, 2 * prev)))
+        await asyncio.sleep(prev)
 
 
 def _die_with_parent():
