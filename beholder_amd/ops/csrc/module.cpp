@@ -154,7 +154,7 @@ PyMODINIT_FUNC PyInit__native(void) {
       init_dispatch_functions(m) < 0 || init_http_types(m) < 0 ||
       init_pg_types(m) < 0 || init_driver_types(m) < 0 ||
       init_ack_types(m) < 0 || init_handler_types(m) < 0 || init_netconn_types(m) < 0 || init_h1call_types(m) < 0 ||
-      init_tls_types(m) < 0 || init_netpoll_types(m) < 0) {
+      init_tls_types(m) < 0 || init_netpoll_types(m) < 0 || init_clock_functions(m) < 0) {
     Py_DECREF(m);
     return nullptr;
   }

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "py_common.hpp"
+#include "gil_clock.hpp"
 #include "ring.hpp"
 
 namespace beholder {
@@ -341,7 +342,7 @@ PyObject* demux_feed_impl(AmqpDemuxObject* self, PyObject* arg) {
     base = reinterpret_cast<const uint8_t*>(carry.data());
     len = carry.size();
   }
-  int64_t now = mono_ns();
+  int64_t now = gil_mono_ns();
   size_t i = 0;
   bool ok = true;
   while (len - i >= 7) {

@@ -145,6 +145,7 @@ int init_netconn_types(PyObject* m);
 int init_h1call_types(PyObject* m);
 int init_tls_types(PyObject* m);
 int init_netpoll_types(PyObject* m);
+int init_clock_functions(PyObject* m);  // gil_clock.cpp
 
 // ---- Window (py_driver.cpp): the in-flight set dispatch_batch hands suspended handlers to ----
 bool is_window(PyObject* o);

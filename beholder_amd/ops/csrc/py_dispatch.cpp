@@ -15,6 +15,7 @@
 //   on_unroutable(delivery)            no handler for the topic id
 // Returns the index of the first delivery not dispatched (len(batch) when done).
 #include "py_common.hpp"
+#include "gil_clock.hpp"
 #include "ring.hpp"
 
 namespace beholder {
@@ -63,7 +64,7 @@ PyObject* mod_dispatch_batch(PyObject*, PyObject* const* a, Py_ssize_t n) {
       continue;
     }
     cnt[tid]++;
-    d->start_ns = mono_ns();
+    d->start_ns = gil_mono_ns();
     PyObject* coro = PyObject_CallOneArg(handler, item);
     if (!coro) {  // the handler itself failed before producing a coroutine
       PyObject *et, *ev, *tb;

@@ -38,6 +38,7 @@
 
 #include "py_common.hpp"
 #include "native_api.hpp"
+#include "gil_clock.hpp"
 
 #include <structmember.h>
 
@@ -113,11 +114,7 @@ PyObject *s_closed_attr, *s_origins, *s_counts, *s_keepalive_s, *s_timeout_s, *s
     *s_tail_cl0, *s_requests, *s_reused, *s_drop, *s_release, *s_arm, *s_resume, *s_time, *s_pop, *s_append,
     *s_buffered, *s_throw, *s_close, *s_request_py, *s_cancel, *s_enqueue, *s_after_queue, *s_exception_name;
 
-double mono_s() {
-  timespec ts;
-  clock_gettime(CLOCK_MONOTONIC, &ts);  // time.monotonic()'s clock
-  return double(ts.tv_sec) + double(ts.tv_nsec) * 1e-9;
-}
+double mono_s() { return double(gil_mono_ns()) * 1e-9; }  // time.monotonic()'s clock (gil_clock.hpp)
 
 bool is_body_method(const char* m, Py_ssize_t n) {
   auto eq = [&](const char* s) { return Py_ssize_t(strlen(s)) == n && memcmp(m, s, size_t(n)) == 0; };

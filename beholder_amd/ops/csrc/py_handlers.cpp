@@ -30,6 +30,7 @@ namespace beholder {
 PyTypeObject* h1_response_type();       // py_h1call.cpp: sinks/http.py HttpResponse, once registered
 PyObject* h1_response_status(PyObject* resp);  // its `status` slot (borrowed; NULL when unset)
 }  // namespace beholder
+#include "gil_clock.hpp"
 #include "ring.hpp"
 
 namespace beholder {
@@ -618,7 +619,7 @@ PyObject* request_finish(CallObject* c, PyObject* value) {
   c->req_native = 0;
   PyObject* stats = c->req_stats;
   c->req_stats = nullptr;
-  double dt = double(mono_ns() - c->req_t0) * 1e-9;
+  double dt = double(gil_mono_ns() - c->req_t0) * 1e-9;
   if (!value) {
     if (stats) {  // stats.record(None, dt); raise
       PyObject *et, *ev, *tb;
@@ -746,7 +747,7 @@ int trello_request(CallObject* c, PyObject* method, PyObject* method_upper, PyOb
     Py_DECREF(query);
     return -1;
   }
-  c->req_t0 = mono_ns();
+  c->req_t0 = gil_mono_ns();
   aw = http_request(c, http, method_upper, url, query, timeout);  // http.request(M, url, params=, timeout=)
   Py_DECREF(url);
   Py_DECREF(query);
@@ -813,7 +814,7 @@ int sink_get(CallObject* c, PyObject* cd, std::string& url, PyObject* const* key
   if (!full) return -1;
   PyObject* aw = http_request(c, http, s_GET, full, nullptr, timeout);  // http.request("GET", full, timeout=)
   Py_DECREF(full);
-  c->req_t0 = mono_ns();
+  c->req_t0 = gil_mono_ns();
   c->req_native = 1;
   c->req_strict = 1;
   if (stats != Py_None) {

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "py_common.hpp"
+#include "gil_clock.hpp"
 #include "ring.hpp"
 
 namespace beholder {
@@ -291,7 +292,7 @@ PyObject* delivery_py_new(PyTypeObject*, PyObject* args, PyObject* kwds) {
   }
   int64_t recv_ns;
   if (recv == Py_None) {
-    recv_ns = mono_ns();
+    recv_ns = gil_mono_ns();
   } else {
     recv_ns = PyLong_AsLongLong(recv);
     if (recv_ns == -1 && PyErr_Occurred()) return nullptr;
@@ -340,7 +341,7 @@ PyObject* settle(DeliveryObject* self, uint8_t to, const char* kind, bool requeu
   self->state = to;
   SettlerObject* s = self->settler;
   if (s) {
-    int64_t now = mono_ns();
+    int64_t now = gil_mono_ns();
     if (self->start_ns > 0) s->handle_hist->h->record(uint64_t(now > self->start_ns ? now - self->start_ns : 0));
     if (self->recv_ns > 0) s->ingest_hist->h->record(uint64_t(now > self->recv_ns ? now - self->recv_ns : 0));
     if (self->recv_ns > 0 && self->start_ns > 0)
@@ -393,7 +394,7 @@ PyObject* delivery_reject(DeliveryObject* self, PyObject* args, PyObject* kwds) 
 }
 
 PyObject* delivery_start(DeliveryObject* self, PyObject*) {
-  self->start_ns = mono_ns();
+  self->start_ns = gil_mono_ns();
   Py_RETURN_NONE;
 }
 

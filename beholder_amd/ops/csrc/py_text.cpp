@@ -17,6 +17,7 @@
 #include <string>
 
 #include "py_common.hpp"
+#include "gil_clock.hpp"
 
 namespace beholder {
 
@@ -397,12 +398,6 @@ bool append_line(std::string& out, long lvl, long long t, const char* prefix, Py
   return true;
 }
 
-long long wall_ms() {
-  struct timespec ts;
-  clock_gettime(CLOCK_REALTIME, &ts);
-  return (long long)ts.tv_sec * 1000 + ts.tv_nsec / 1000000;
-}
-
 // format_line(level:int, time_ms:int, prefix:str, extra:str|None, args:tuple) -> str
 PyObject* mod_format_line_impl(PyObject*, PyObject* const* a, Py_ssize_t n);
 PyObject* mod_format_line(PyObject*, PyObject* const* a, Py_ssize_t n) {
@@ -526,7 +521,7 @@ void sink_dealloc(LogSinkObject* self) {
 bool sink_emit_core(LogSinkObject* self, long lvl, const char* prefix, Py_ssize_t plen, PyObject* extra,
                     PyObject* const* argv, Py_ssize_t nargs) {
   size_t before = self->buf->size();
-  if (!append_line(*self->buf, lvl, wall_ms(), prefix, plen, extra, argv, nargs, self->drop_extra)) {
+  if (!append_line(*self->buf, lvl, gil_wall_ms(), prefix, plen, extra, argv, nargs, self->drop_extra)) {
     self->buf->resize(before);
     return false;
   }

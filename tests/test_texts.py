@@ -33,7 +33,7 @@ ALLOWED_IDENTIFIERS = {
     "emby", "err_message", "execute", "field_names", "get_by_id", "get_calls", "handlers", "host", "http", "inc",
     "key", "limiter", "lists", "log", "lower", "make_request", "mediaId", "message", "metadataId", "name",
     "native_log", "no_trello", "on_progress", "on_status", "params", "post", "progress", "progress_counter", "put",
-    "py_common.hpp", "raise_for_status", "record", "refresh_library", "request", "result_type", "retry", "ring.hpp",
+    "py_common.hpp", "raise_for_status", "record", "refresh_library", "request", "result_type", "retry", "ring.hpp", "gil_clock.hpp",
     "row_to_media", "send", "send_message", "state", "stats", "status", "strict", "suspended", "telegram",
     "throw", "timeout", "token", "trello", "trello_creator", "update_calls", "update_status",
     "{s:K,s:K,s:O}", "{s:O}", "{}",
