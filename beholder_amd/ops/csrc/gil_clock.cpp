@@ -39,7 +39,7 @@ int64_t gil_clock_anchor(uint64_t) {
   GilClock& c = g_gil_clock;
   // the TSC read on both sides of the CLOCK_MONOTONIC read, their midpoint paired with it; a pair
   // taken across an interrupt or a preemption (a wide bracket) is read again, up to 4 times
-  timespec m, r;
+  timespec m = {0, 0}, r;
   uint64_t t = 0, width = ~uint64_t(0);
   for (int i = 0; i < 4; ++i) {
     timespec mi;

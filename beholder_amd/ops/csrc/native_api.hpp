@@ -18,7 +18,7 @@
 namespace beholder {
 
 constexpr const char* kNativeApiName = "beholder_amd.ops._native._C_API";
-constexpr uint32_t kNativeApiAbi = 2;
+constexpr uint32_t kNativeApiAbi = 3;
 
 struct NativeApi {
   uint32_t abi;  // kNativeApiAbi
@@ -30,8 +30,10 @@ struct NativeApi {
   // http.request(method, url, params=params) on an origin with Host `host` and Authorization
   // `auth` (str, or None): "M target?query HTTP/1.1\r\nHost: ...\r\n[Authorization: ...\r\n]" then
   // `tail` (bytes; `tail_cl0` for methods with a body). *full = the URL with its query (new
-  // reference). *key_len = length of "scheme://authority" in `url`. 1 = built, 0 = not the shape
-  // the native path sends (the Python client would take it), -1 = error.
+  // reference). *key_len = length of "scheme://authority" in `url`; a caller that has it from
+  // h1_origin_key for the same arguments passes it in (> 0) and the shape check is not repeated,
+  // as the H1 client's own path checks once. 1 = built, 0 = not the shape the native path sends
+  // (the Python client would take it), -1 = error.
   int (*h1_request_text)(PyObject* method, PyObject* url, PyObject* params, PyObject* host, PyObject* auth,
                          PyObject* tail, PyObject* tail_cl0, std::string* req, PyObject** full,
                          Py_ssize_t* key_len);

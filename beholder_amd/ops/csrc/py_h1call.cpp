@@ -1131,8 +1131,11 @@ int api_h1_request_text(PyObject* method, PyObject* url, PyObject* params, PyObj
       PyErr_SetString(PyExc_TypeError, "h1_request_text: tail and tail_cl0 must be bytes");
       return -1;
     }
-    Py_ssize_t k;
-    if (!split_shape(method, url, params, &k)) return 0;
+    Py_ssize_t k = *key_len;
+    const bool known = k > 0 && PyUnicode_CheckExact(method) && PyUnicode_IS_ASCII(method) &&
+                       PyUnicode_CheckExact(url) && PyUnicode_IS_ASCII(url) && k <= PyUnicode_GET_LENGTH(url) &&
+                       (!params || PyDict_CheckExact(params));
+    if (!known && !split_shape(method, url, params, &k)) return 0;
     std::string q;
     req->clear();
     if (!request_text(method, url, k, params, host, auth, tail, tail_cl0, *req, q)) return 0;
