@@ -10,8 +10,35 @@
 
 #include <new>
 #include <stdexcept>
+#include <string>
 
 namespace beholder {
+
+// Per-event text (a log line, a URL path, a query, a request) is built in a std::string and turned
+// into a str or handed to a socket buffer before the code that built it returns. A ScratchStr lends
+// one of a few strings kept across events (cleared, capacity kept), so that text costs no heap
+// allocation per event; a nested lender (a js_str() that runs Python code that logs) takes the next
+// one, last in first out, and past kDepth a fresh local. GIL-held code only (one global pool).
+class ScratchStr {
+ public:
+  ScratchStr() : s_(depth_ < kDepth ? &pool_[depth_++] : &own_) { s_->clear(); }
+  ~ScratchStr() {
+    if (s_ == &own_) return;
+    if (s_->capacity() > kKeepBytes) std::string().swap(*s_);  // an outsized one is not kept
+    --depth_;
+  }
+  ScratchStr(const ScratchStr&) = delete;
+  ScratchStr& operator=(const ScratchStr&) = delete;
+  std::string& operator*() { return *s_; }
+
+ private:
+  static constexpr int kDepth = 8;
+  static constexpr size_t kKeepBytes = 65536;
+  static inline std::string pool_[kDepth];
+  static inline int depth_ = 0;
+  std::string own_;
+  std::string* s_;
+};
 
 // C++ exceptions must never cross into CPython (std::terminate). Entry points
 // that allocate wrap their body: BEHOLDER_TRY { ... } BEHOLDER_CATCH(nullptr)

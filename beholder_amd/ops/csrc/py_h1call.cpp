@@ -51,7 +51,7 @@ PyObject* iofuture_yield(PyObject* f);
 bool is_netconn(PyObject* o);
 bool netconn_open(PyObject* o);
 PyObject* netconn_loop(PyObject* o);
-int netconn_h1_request(PyObject* o, const std::string& data, PyObject* waiter, bool head);
+int netconn_h1_request(PyObject* o, const char* data, size_t n, PyObject* waiter, bool head);
 bool text_query_pair_append(std::string& out, PyObject* k, PyObject* v, bool* first, bool rfc3986);
 
 namespace {
@@ -799,7 +799,8 @@ int h1_start(H1CallObject* s) {
   PyObject* auth = g.origin.get(o, O_AUTH);
   PyObject* idle = g.origin.get(o, O_IDLE);
   if (!host || !auth || !idle) return 0;
-  std::string req, q;
+  ScratchStr req_buf, q_buf;  // the request goes to the connection's buffer (or a bytes) below
+  std::string &req = *req_buf, &q = *q_buf;
   if (!request_text(method, url, k, params, host, auth, tail, tail_cl0, req, q)) return 0;
   const char* m = reinterpret_cast<const char*>(PyUnicode_1BYTE_DATA(method));
   bool head = PyUnicode_GET_LENGTH(method) == 4 && memcmp(m, "HEAD", 4) == 0;
@@ -947,7 +948,7 @@ int send_on(H1CallObject* s, PyObject* conn, const char* req, size_t reqlen, PyO
   PyObject* fut = iofuture_new(loop);
   if (!fut) return fail();
   Own own_fut{fut};
-  if (netconn_h1_request(g.conn.get(conn, C_NET), std::string(req, reqlen), fut, head) < 0) return fail();
+  if (netconn_h1_request(g.conn.get(conn, C_NET), req, reqlen, fut, head) < 0) return fail();
   if (PySet_Add(busy, conn) < 0) return fail();
   PyObject* sweeper = PyDict_GetItemWithError(d, s_sweeper);
   if (!sweeper && PyErr_Occurred()) {
@@ -1136,7 +1137,8 @@ int api_h1_request_text(PyObject* method, PyObject* url, PyObject* params, PyObj
                        PyUnicode_CheckExact(url) && PyUnicode_IS_ASCII(url) && k <= PyUnicode_GET_LENGTH(url) &&
                        (!params || PyDict_CheckExact(params));
     if (!known && !split_shape(method, url, params, &k)) return 0;
-    std::string q;
+    ScratchStr q_buf;
+    std::string& q = *q_buf;
     req->clear();
     if (!request_text(method, url, k, params, host, auth, tail, tail_cl0, *req, q)) return 0;
     *full = full_url(url, q);

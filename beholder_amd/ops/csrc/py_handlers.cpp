@@ -787,7 +787,8 @@ PyObject* plain_client_dict(PyObject* client, PyObject* cls) {
 // refresh_library. `url` is the base URL text; `cd` the client's instance dict.
 int sink_get(CallObject* c, PyObject* cd, std::string& url, PyObject* const* keys, PyObject* const* vals, int n,
              PyObject** out) {
-  std::string q;
+  ScratchStr q_buf;
+  std::string& q = *q_buf;
   bool first = true;
   for (int i = 0; i < n; ++i)
     if (!text_query_pair_append(q, keys[i], vals[i], &first, true)) return -1;
@@ -836,7 +837,8 @@ int hook_telegram(CallObject* c, PyObject** out) {
   PyObject* plan = c->plan;
   int on = PyObject_IsTrue(PyTuple_GET_ITEM(plan, 0));
   if (on <= 0) return on < 0 ? -1 : 2;
-  std::string line;
+  ScratchStr line_buf;
+  std::string& line = *line_buf;
   if (!tpl_append(line, hs, T_LOG_TELEGRAM, c->media_id)) return -1;
   PyObject* lo = unicode_from(line);
   bool ok = lo && log_line(hs, 30, &lo, 1);
@@ -845,7 +847,8 @@ int hook_telegram(CallObject* c, PyObject** out) {
   // arguments in the order Python evaluates them: chat_id, deployed_text(name, metadataId), token
   PyObject* name = PyObject_GetAttr(c->media, s_name);
   PyObject* meta = name ? PyObject_GetAttr(c->media, s_metadataId) : nullptr;
-  std::string text;
+  ScratchStr text_buf;
+  std::string& text = *text_buf;
   ok = meta && tpl_append(text, hs, T_TELEGRAM_TEXT, name, meta);
   Py_XDECREF(name);
   Py_XDECREF(meta);
@@ -877,7 +880,8 @@ int hook_telegram(CallObject* c, PyObject** out) {
     return await_start(c, aw, out);
   }
   PyObject* base = PyDict_GetItemWithError(cd, s_base_url);
-  std::string url;
+  ScratchStr url_buf;
+  std::string& url = *url_buf;
   ok = base && text_js_str_append(url, base);
   ok = ok && tpl_append(url, hs, T_PATH_TELEGRAM, tok);
   Py_DECREF(tok);
@@ -901,7 +905,8 @@ int hook_emby(CallObject* c, PyObject** out) {
   if (on <= 0) return on < 0 ? -1 : 2;
   PyObject* host = PyTuple_GET_ITEM(plan, 4);
   PyObject* key = PyTuple_GET_ITEM(plan, 5);
-  std::string line;
+  ScratchStr line_buf;
+  std::string& line = *line_buf;
   if (!tpl_append(line, hs, T_LOG_EMBY, host)) return -1;
   PyObject* lo = unicode_from(line);
   bool ok = lo && log_line(hs, 30, &lo, 1);
@@ -919,7 +924,8 @@ int hook_emby(CallObject* c, PyObject** out) {
     if (!aw) return -1;
     return await_start(c, aw, out);
   }
-  std::string url;
+  ScratchStr url_buf;
+  std::string& url = *url_buf;
   if (!tpl_append(url, hs, T_PATH_EMBY, host)) return -1;
   PyObject* keys[1] = {hs->x[X_Q_API_KEY]};
   PyObject* vals[1] = {key};
@@ -1000,7 +1006,8 @@ PySendResult step_progress(CallObject* c, PyObject* value, PyObject** result) {
       Py_DECREF(creator);
       if (is_trello < 0) goto catch_;
       if (!is_trello) goto finish;
-      std::string s;  // index.js:143-146 (Q8)
+      ScratchStr s_buf;  // index.js:143-146 (Q8)
+      std::string& s = *s_buf;
       if (!tpl_append(s, hs, T_COMMENT, c->status_text, c->progress)) goto catch_;
       int has_host;
       js_truthy(c->host, &has_host);
@@ -1015,7 +1022,8 @@ PySendResult step_progress(CallObject* c, PyObject* value, PyObject** result) {
       // comment(cardId, text), index.js:50-58
       PyObject* largs[4] = {hs->x[X_LOG_COMMENT_0], card, hs->x[X_LOG_COMMENT_1], text};
       bool ok = log_line(hs, 30, largs, 4);
-      std::string path;
+      ScratchStr path_buf;
+      std::string& path = *path_buf;
       ok = ok && tpl_append(path, hs, T_PATH_COMMENT, card);
       Py_DECREF(card);
       if (!ok) {
@@ -1080,7 +1088,8 @@ PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
       c->status = c->media_id ? field(msg, hs->res_s, hs->ix_s[1], s_status) : nullptr;
       Py_DECREF(msg);
       if (!c->status) return fail(c);
-      std::string s;  // index.js:66
+      ScratchStr s_buf;  // index.js:66
+      std::string& s = *s_buf;
       if (!tpl_append(s, hs, T_LOG_STATUS, c->media_id, c->status)) return fail(c);
       PyObject* line = unicode_from(s);
       if (!line) return fail(c);
@@ -1200,9 +1209,9 @@ PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
         Py_DECREF(lp);
         return fail(c);
       }
-      std::string s;  // index.js:82
+      ScratchStr s_buf, path_buf;  // index.js:82
+      std::string &s = *s_buf, &path = *path_buf;
       bool ok = tpl_append(s, hs, T_LOG_MOVE, c->media_id, card);
-      std::string path;
       ok = ok && tpl_append(path, hs, T_PATH_CARD, card);
       Py_DECREF(card);
       PyObject* line = ok ? unicode_from(s) : nullptr;

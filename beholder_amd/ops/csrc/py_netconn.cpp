@@ -1309,7 +1309,7 @@ bool netconn_open(PyObject* o) {
 
 // The h1 request of nc_request for a caller in C (sinks/h1.py fast path, py_h1call.cpp): parser
 // started, `waiter` set, the request bytes written. 0, or -1 with an exception set.
-int netconn_h1_request(PyObject* o, const std::string& data, PyObject* waiter, bool head) {
+int netconn_h1_request(PyObject* o, const char* data, size_t n, PyObject* waiter, bool head) {
   NetConnObject* c = reinterpret_cast<NetConnObject*>(o);
   if (c->kind != K_H1) {
     PyErr_SetString(PyExc_TypeError, "not an h1 NetConn");
@@ -1322,7 +1322,7 @@ int netconn_h1_request(PyObject* o, const std::string& data, PyObject* waiter, b
   if (start_parser(c, head) < 0) return -1;  // parser.start(head=head)
   Py_INCREF(waiter);
   Py_XSETREF(c->waiter, waiter);
-  c->out->append(data);
+  c->out->append(data, n);
   if (c->writing) return 0;
   return send_out(c);
 }
