@@ -692,7 +692,21 @@ bool split_shape(PyObject* method, PyObject* url, PyObject* params, Py_ssize_t* 
   Py_ssize_t k = i + 3;
   while (k < un && u[k] != '/' && u[k] != '?' && u[k] != '#') ++k;
   bool has_q = false;
-  for (Py_ssize_t j = k; j < un; ++j) {
+  Py_ssize_t j = k;
+  // 8 bytes at a time while none is outside 0x21..0x7E, '#' or '?' (a plain path; the bytes are
+  // ASCII, so the per-byte sums below never carry); the byte loop takes over from the first word
+  // that has one
+  constexpr uint64_t ones = 0x0101010101010101ULL, highs = 0x8080808080808080ULL;
+  for (; j + 8 <= un; j += 8) {
+    uint64_t w;
+    memcpy(&w, u + j, 8);
+    const uint64_t ctl = (w - ones * 0x21) & ~w & highs;  // a byte < 0x21
+    const uint64_t del = (w + ones) & highs;              // 0x7F
+    const uint64_t h = w ^ (ones * '#'), q = w ^ (ones * '?');
+    const uint64_t hq = ((h - ones) & ~h & highs) | ((q - ones) & ~q & highs);
+    if (ctl | del | hq) break;
+  }
+  for (; j < un; ++j) {
     unsigned char ch = static_cast<unsigned char>(u[j]);
     if (ch < 0x21 || ch > 0x7E || ch == '#') return false;  // _resolve would quote it
     if (ch == '?') has_q = true;

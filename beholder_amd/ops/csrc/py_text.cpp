@@ -361,7 +361,7 @@ bool append_line(std::string& out, long lvl, long long t, const char* prefix, Py
     long long t = -1;
     std::string s;
   };
-  static thread_local Head head;
+  static Head head;  // the GIL guards it (a thread_local costs a __tls_get_addr call in a module)
   if (head.lvl != lvl || head.t != t) {
     head.s.assign("{\"level\":");
     append_i64(head.s, lvl);
@@ -387,7 +387,7 @@ bool append_line(std::string& out, long lvl, long long t, const char* prefix, Py
     const size_t at = out.size();
     if (!quick_format_append(out, argv, nargs, drop_extra)) return false;
     if (needs_escape(out.data() + at, out.size() - at)) {
-      static thread_local std::string msg;  // scratch: no allocation per line
+      static std::string msg;  // scratch, GIL-guarded: no allocation per line
       msg.assign(out, at, std::string::npos);
       out.resize(at);
       json_escape_append(out, msg.data(), msg.size());

@@ -66,7 +66,10 @@ def _cases(port, n=150, seed=7):
     rnd = random.Random(seed)
     base = [f"http://127.0.0.1:{port}", f"http://u%40s:p%3Aw@127.0.0.1:{port}"]
     paths = ["/1/cards/abc/actions/comments", "/bot123:XYZ/sendMessage?chat_id=5&text=a%20b", "/emby/library/refresh",
-             "", "/x y", "/é", "/a#frag", "?q=1", "/p?x=1", "/1/cards/C\r\nX-Evil:1/actions/comments"]
+             "", "/x y", "/é", "/a#frag", "?q=1", "/p?x=1", "/1/cards/C\r\nX-Evil:1/actions/comments",
+             # the shape check reads 8 bytes at a time: odd bytes past the first words
+             "/1/cards/abcdefghij/x y", "/1/cards/abcdefghij#frag", "/1/cards/abcdefghij\x7fz",
+             "/1/cards/abcdefghij?q=1", "/1/cards/abcdefghijklmnopqrstu/actions"]
     params = [None, {}, {"key": "k", "token": "t", "text": "DEPLOYED: **5%** (_x_) ü"}, {"a": None, "b": 1},
               {"pos": 2, "idList": "L1"}, {"api_key": "x y&z"}, {"v": 1.5, "w": True}]
     for _ in range(n):
@@ -117,7 +120,7 @@ def test_fast_path_sends_the_same_bytes_and_returns_the_same_responses():
     assert f_counts == p_counts and f_conns == p_conns
     assert "native" in f_kinds and "native" not in p_kinds
     # the shapes the sinks produce take the native path; the others decline before any state changes
-    assert f_kinds.count("native") > len(f_kinds) // 3
+    assert f_kinds.count("native") > len(f_kinds) // 4
 
 
 def test_fast_path_declines_cold_pool_and_foreign_shapes():
