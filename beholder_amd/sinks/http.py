@@ -303,6 +303,16 @@ class RecordingHttpClient(HttpClient):
             full = self._rec.record(m, with_query(url, params), None)
         if self.delay_s:
             await asyncio.sleep(self.delay_s)
+        return self.answer(m, full)
+
+    def record(self, method: str, url: str, params=None) -> str:
+        """Log one request (method upper-cased by the caller) and return its full URL."""
+        if type(params) is dict or params is None:
+            return self._rec.record(method, url, params)
+        return self._rec.record(method, with_query(url, params), None)
+
+    def answer(self, m: str, full: str) -> HttpResponse:
+        """The reply to a recorded request: the first matching rule's, else ``200 {}``."""
         if not self._rules:
             return HttpResponse(200, b"{}", None, full)
         for rm, pref, fn in self._rules:

@@ -18,9 +18,22 @@
 //   events: [["status"|"progress", hexBody]], faults: [{method, prefix, status|null, message, body}],
 //   positionalArgs: "append"|"drop", notFound: "media {id} not found", logLevel: "info",
 //   races: {mediaId: status} (the status another writer leaves in the row after each updateStatus)}
+//   concurrent: {cap, script} (scenario mode "concurrent", below)
 // NO_TRELLO comes from the environment, as in the reference (index.js:70).
 // Events are delivered one at a time and each listener's promise is awaited before the next
 // (the Python side does the same), so traces are deterministic.
+//
+// Mode "concurrent" (quirk Q9, index.js:43,62,127: up to prefetch listeners in flight, no
+// per-media order): every store call and sink request waits on a gate that only this driver
+// opens, so several deliveries are in flight at once and their awaits resume in one scripted
+// order. Each step either delivers the next event (while fewer than `cap` are in flight) or opens
+// the gate of one in-flight event, chosen by `script[step]` among the events waiting (sorted by
+// index; an event waits on one gate at most, its awaits being sequential), then lets everything
+// runnable run (setImmediate: the microtask queue is empty). Only that event runs in a step, so
+// its log lines and requests are its own. The store applies an UPDATE and reads a row when its
+// gate opens, so a status event suspended in getByID sees the UPDATE of another event that
+// resolved first (index.js:68,76,94). `order` records each step: [action, event, gate kind,
+// log lines, requests, acks, settled]. tests/reference_oracle.py replays the same script.
 const fs = require('fs')
 const path = require('path')
 
@@ -79,17 +92,28 @@ const h = global.__beholderHarness = {
   },
   onDecodeError () {
     cur.decodeError = true
-  }
+  },
+  current: null, // the event whose code runs in this step (mode "concurrent")
+  gate: null
+}
+// the gate an event's store call / sink request waits on (mode "concurrent")
+const waiting = new Map() // event index -> {kind, open}
+if (sc.concurrent) {
+  h.gate = kind => new Promise(resolve => {
+    if (waiting.has(h.current)) throw new Error('event ' + h.current + ' waits on two gates')
+    waiting.set(h.current, { kind, open: resolve })
+  })
+  const answer = h.reply
+  h.reply = (kind, method, url) => h.gate('http').then(() => answer(kind, method, url))
 }
 for (const m of sc.media) h.media.set(m.id, Object.assign({}, m))
 
 const TOPICS = { status: 'v1.telemetry.status', progress: 'v1.telemetry.progress' }
 const immediate = () => new Promise(resolve => setImmediate(resolve))
 
-async function main () {
-  require(path.resolve(arg('index'))) // the reference service: calls init() at module load
-  while (!(h.listeners[TOPICS.status] && h.listeners[TOPICS.progress])) await immediate()
-  await immediate() // let init() finish (its last statement logs 'initialized')
+const errText = e => e instanceof Error ? e.message : String(e)
+
+async function sequential () {
   const events = []
   for (const [topic, hex] of sc.events) {
     cur = { acks: 0, threw: null, decodeError: false, requests: [], logs: [] }
@@ -97,17 +121,71 @@ async function main () {
     try {
       await h.listeners[TOPICS[topic]](rmsg)
     } catch (e) {
-      cur.threw = e instanceof Error ? e.message : String(e)
+      cur.threw = errText(e)
     }
     events.push(cur)
   }
+  return { events }
+}
+
+async function concurrent () {
+  const { cap, script } = sc.concurrent
+  const n = sc.events.length
+  const events = sc.events.map(() => ({ acks: 0, threw: null, decodeError: false, requests: [], logs: [] }))
+  const settled = new Array(n).fill(false)
+  const order = []
+  let next = 0
+  let active = 0
+  for (let step = 0; ; step++) {
+    const ready = [...waiting.keys()].sort((a, b) => a - b)
+    const r = script[step % script.length]
+    let i, action, kind
+    if (next < n && (ready.length === 0 || (active < cap && r % 2 === 0))) {
+      i = next++
+      action = 'deliver'
+      kind = null
+      active++
+    } else if (ready.length) {
+      i = ready[(r >>> 1) % ready.length]
+      action = 'resolve'
+      kind = waiting.get(i).kind
+    } else {
+      if (active) throw new Error(active + ' deliveries in flight, none at a gate')
+      break
+    }
+    h.current = i
+    cur = events[i]
+    const before = [cur.logs.length, cur.requests.length, cur.acks]
+    if (action === 'deliver') {
+      const [topic, hex] = sc.events[i]
+      const rec = cur
+      const rmsg = { message: { content: Buffer.from(hex, 'hex') }, ack () { rec.acks++ } }
+      h.listeners[TOPICS[topic]](rmsg).then(() => { settled[i] = true; active-- },
+        e => { rec.threw = errText(e); settled[i] = true; active-- })
+    } else {
+      const g = waiting.get(i)
+      waiting.delete(i)
+      g.open()
+    }
+    await immediate()
+    order.push([action, i, kind, cur.logs.length - before[0], cur.requests.length - before[1],
+      cur.acks - before[2], settled[i]])
+  }
+  return { events, order }
+}
+
+async function main () {
+  require(path.resolve(arg('index'))) // the reference service: calls init() at module load
+  while (!(h.listeners[TOPICS.status] && h.listeners[TOPICS.progress])) await immediate()
+  await immediate() // let init() finish (its last statement logs 'initialized')
+  const { events, order } = sc.concurrent ? await concurrent() : await sequential()
   const counters = {}
   for (const c of h.counters) {
     counters[c.name] = Object.keys(c.hashMap).sort().map(k => [k, c.hashMap[k].value])
   }
   const media = {}
   for (const [id, m] of h.media) media[id] = m.status
-  process.stdout.write(JSON.stringify({ events, counters, media, initLogs, node: process.version }) + '\n',
+  process.stdout.write(JSON.stringify({ events, order, counters, media, initLogs, node: process.version }) + '\n',
     () => process.exit(0))
 }
 

@@ -10,12 +10,17 @@
 class Storage {
   constructor () {
     const h = global.__beholderHarness
+    this.h = h
     this.media = h.media
     this.notFound = h.notFound || 'media {id} not found'
     this.races = h.races || {}
   }
 
+  // Mode "concurrent" (oracle.js): each call first waits on the harness's gate; the UPDATE
+  // lands, and the row is read, when the gate opens. getByID returns a copy of the row, as a
+  // query returns a fresh row object: a row read before another event's UPDATE keeps its status.
   async updateStatus (mediaId, status) {
+    if (this.h.gate) await this.h.gate('update')
     const m = this.media.get(mediaId)
     if (m) m.status = status
     // scenario mode "reread": another writer's UPDATE of the same row lands between this
@@ -25,9 +30,10 @@ class Storage {
   }
 
   async getByID (mediaId) {
+    if (this.h.gate) await this.h.gate('get')
     const m = this.media.get(mediaId)
     if (!m) throw new Error(this.notFound.split('{id}').join(mediaId))
-    return m
+    return Object.assign({}, m)
   }
 }
 module.exports = Storage

@@ -54,6 +54,41 @@ def progress_msg(media_id: str, status, progress=0, host: str = "") -> bytes:
 # which handler implementation Rig drives: "python" (handlers.py) or "native" (py_handlers.cpp);
 # tests/test_handlers.py runs every case under both
 HANDLER_IMPL = "python"
+# whether Rig's default store and HTTP client suspend at every call, as production's socket
+# clients always do (tests/test_handlers.py runs every case both ways): the compiled handlers
+# then leave C at each await and resume in their state machine (py_handlers.cpp, states 1-6)
+SUSPEND = False
+
+
+def suspending(base):
+    """``base`` (a MemoryStore class) whose every access yields to the loop once before it runs
+    (a network store's shape). Its synchronous accessors are hidden from the handlers, so
+    they await the coroutines."""
+    class Suspending(base):
+        async def update_status(self, media_id, status):
+            await asyncio.sleep(0)
+            base.update_status_nowait(self, media_id, status)
+
+        async def get_by_id(self, media_id):
+            await asyncio.sleep(0)
+            return base.get_by_id_nowait(self, media_id)
+    Suspending.__name__ = Suspending.__qualname__ = "Suspending" + base.__name__
+    return Suspending
+
+
+SuspendingStore = suspending(MemoryStore)
+
+
+class SuspendingHttpClient(RecordingHttpClient):
+    """Records a request, yields to the loop once, then answers it (rules and faults included),
+    so every answer, a failure too, reaches the handler through a resumed await (a socket
+    client's shape; the plain recorder answers within the call)."""
+
+    async def request(self, method, url, *, params=None, timeout=None):
+        m = method.upper()
+        full = self.record(m, url, params)
+        await asyncio.sleep(0)
+        return self.answer(m, full)
 
 
 async def _await(aw):
@@ -66,8 +101,8 @@ class Rig:
     def __init__(self, config: Optional[Config] = None, medias=(), no_trello: Optional[bool] = None,
                  http: Optional[RecordingHttpClient] = None, positional_args: str = "append", store=None):
         self.config = config or cfg()
-        self.http = http or RecordingHttpClient()
-        self.store = store if store is not None else MemoryStore(list(medias))
+        self.http = http or (SuspendingHttpClient() if SUSPEND else RecordingHttpClient())
+        self.store = store if store is not None else (SuspendingStore if SUSPEND else MemoryStore)(list(medias))
         self.stream = MemoryStream()
         self.log = Logger(stream=self.stream, positional_args=positional_args)
         self.registry = Registry()

@@ -57,7 +57,11 @@ ORACLE_JS = os.path.join(ROOT, "scripts", "reference_node", "oracle.js")
 STUBS = os.path.join(ROOT, "scripts", "reference_node", "stubs")
 NODE = shutil.which("node")
 NOT_FOUND = "media {id} not found"  # beholder_amd.store.base.MediaNotFound's text
-MODES = ("base", "no_trello", "faults", "drop", "reread")
+# sendMessage for a row named "Cowboy Bebop" (query order chat_id, text, parse_mode; RFC 3986)
+TELEGRAM_FAULT_PREFIX = ("https://api.telegram.org/bot123:TG/sendMessage?chat_id=-1001&text="
+                         "%2ANew%20Anime%3A%2A%20Cowboy%20Bebop")
+MODES = ("base", "no_trello", "faults", "drop", "reread", "concurrent")
+CONCURRENT_CAP = 4  # deliveries in flight at once in mode "concurrent"
 
 _S = codec_for(proto.load("api.TelemetryStatus"))
 _P = codec_for(proto.load("api.TelemetryProgress"))
@@ -156,9 +160,25 @@ def make_scenario(seed: int, n_events: int = 520, mode: str = "base") -> dict:
         config["instance"]["telegram"] = {"enabled": True, "channel": "-1001"}
         config["instance"]["emby"] = {"enabled": True, "host": rng.choice(["http://emby:8096", "https://e.example/x"])}
         pool = [("POST", "https://api.trello.com"), ("PUT", "https://api.trello.com"),
-                ("GET", "https://api.telegram.org"), ("GET", "http://emby"), ("GET", "https://e.example"),
+                ("GET", "http://emby"), ("GET", "https://e.example"),
                 ("*", "https://api.trello.com/1/cards/card1")]
-        for method, prefix in rng.sample(pool, rng.randrange(1, 4)):
+        # always: a Telegram failure for the rows named "Cowboy Bebop" (Emby still runs for the
+        # others, so a handler that runs Emby after a failed Telegram call diverges, Q4,
+        # index.js:92-122) and a failing comment POST on card "card1" (its counter must not count,
+        # index.js:53-57, and the progress handler still acks, Q7)
+        rows = {m["id"]: m for m in media}
+        for mid, over in (("m1", {"creator": 1, "creatorId": "card1"}), ("m2", {"name": "Cowboy Bebop"})):
+            if mid not in rows:
+                rows[mid] = {"id": mid, "name": "Trigun", "creator": 0, "creatorId": "", "metadataId": "1",
+                             "status": 0}
+                media.append(rows[mid])
+            rows[mid].update(over)
+        faults.append({"method": "GET", "prefix": TELEGRAM_FAULT_PREFIX, "status": rng.choice([None, 400, 500, 502]),
+                       "message": rng.choice(["ECONNREFUSED", "socket hang up"]),
+                       "body": '{"ok":false,"description":"Bad Request: chat not found é"}'})
+        faults.append({"method": "POST", "prefix": "https://api.trello.com/1/cards/card1/actions/comments",
+                       "status": None, "message": "ETIMEDOUT", "body": '"error"'})
+        for method, prefix in rng.sample(pool, rng.randrange(0, 4)):
             f = {"method": method, "prefix": prefix, "status": rng.choice([None, 404, 500, 502, 204]),
                  "message": rng.choice(["ECONNREFUSED", "socket hang up"]),
                  "body": rng.choice(['"error"', '{"ok":false,"description":"Bad Request: chat not found é"}'])}
@@ -174,7 +194,19 @@ def make_scenario(seed: int, n_events: int = 520, mode: str = "base") -> dict:
         for m in media:
             if rng.random() < 0.7:
                 races[m["id"]] = 4 if rng.random() < 0.5 else rng.choice([0, 1, 2, 3, 5])
-    msg_ids = ids + ["missing", "m1", "m1", "m2"]
+    concurrent = None
+    if mode == "concurrent":
+        # few media, both hooks on: many deliveries of one media in flight together (Q9)
+        config["keys"]["telegram"] = {"token": "123:TG"}
+        config["keys"]["emby"] = {"token": "EMBYKEY"}
+        config["instance"]["telegram"] = {"enabled": True, "channel": "-1001"}
+        config["instance"]["emby"] = {"enabled": True, "host": "http://emby:8096"}
+        for m in media:
+            if m["id"] in ("m1", "m2", "m3"):
+                m["creator"] = 1 if m["id"] != "m3" else 0
+        concurrent = {"cap": CONCURRENT_CAP, "script": [rng.randrange(2 ** 31) for _ in range(4096)]}
+    msg_ids = (["m1", "m2", "m3", "m1", "m2", "missing"] if mode == "concurrent"
+               else ids + ["missing", "m1", "m1", "m2"])
     events = []
     for _ in range(n_events):
         r = rng.random()
@@ -190,7 +222,7 @@ def make_scenario(seed: int, n_events: int = 520, mode: str = "base") -> dict:
             events.append(["progress", _P.encode((mid, st, prog, host)).hex()])
     return {"seed": seed, "mode": mode, "config": config, "media": media, "events": events, "faults": faults,
             "positionalArgs": "drop" if mode == "drop" else "append", "notFound": NOT_FOUND, "logLevel": "info",
-            "noTrello": mode == "no_trello", "races": races}
+            "noTrello": mode == "no_trello", "races": races, "concurrent": concurrent}
 
 
 def bench_scenario(n_events: int, seed: int = 0) -> dict:
@@ -261,20 +293,78 @@ class RacingStore(MemoryStore):
             self._rows[media_id] = row._replace(status=self.races[media_id])
 
 
-def run_python(sc: dict, impl: str = "python", mutate=None) -> dict:
-    """This repo's handlers (``impl`` = python | native) over the same scenario."""
+class _Gates:
+    """Mode ``concurrent``: the gate each in-flight event's store call / sink request waits on,
+    opened by :func:`_run_concurrent` in the scenario's scripted order (oracle.js ``concurrent``)."""
+
+    def __init__(self):
+        self.current: Optional[int] = None  # the event whose code runs in this step
+        self.waiting: Dict[int, tuple] = {}  # event index -> (kind, future)
+
+    def wait(self, kind: str):
+        i = self.current
+        if i in self.waiting:
+            raise RuntimeError(f"event {i} waits on two gates")
+        f = asyncio.get_running_loop().create_future()
+        self.waiting[i] = (kind, f)
+        return f
+
+
+def _gated_store(base, gates: _Gates):
+    """``base`` whose UPDATE lands, and whose row is read, when the event's gate opens."""
+    class Gated(base):
+        async def update_status(self, media_id, status):
+            await gates.wait("update")
+            base.update_status_nowait(self, media_id, status)
+
+        async def get_by_id(self, media_id):
+            await gates.wait("get")
+            return base.get_by_id_nowait(self, media_id)
+    return Gated
+
+
+class _GatedHttpClient(RecordingHttpClient):
+    """Records a request when it is issued and answers it when the event's gate opens."""
+
+    def __init__(self, gates: _Gates):
+        super().__init__()
+        self.gates = gates
+
+    async def request(self, method, url, *, params=None, timeout=None):
+        m = method.upper()
+        full = self.record(m, url, params)
+        await self.gates.wait("http")
+        return self.answer(m, full)
+
+
+def run_python(sc: dict, impl: str = "python", mutate=None, suspend: bool = False) -> dict:
+    """This repo's handlers (``impl`` = python | native) over the same scenario.
+
+    ``suspend``: the store and the sink client yield to the loop at every call before they answer
+    (production's shape: its socket clients always wait), so the compiled handlers finish each
+    event in their resume states. Mode ``concurrent`` always suspends (at its gates)."""
     import helpers
     from beholder_amd.handlers import native_handlers
     from beholder_amd.models.proto import DecodeError
 
     config = Config.from_dict(sc["config"], env={})
-    http = RecordingHttpClient()
+    conc = sc.get("concurrent")
+    gates = _Gates() if conc else None
+    if gates is not None:
+        http = _GatedHttpClient(gates)
+    else:
+        http = helpers.SuspendingHttpClient() if suspend else RecordingHttpClient()
     for f in sc["faults"]:
         http.fail(f["method"], f["prefix"], status=f["status"], message=f["message"],
                   body=f["body"].encode())
     rows = [Media(id=m["id"], name=m["name"], creator=m["creator"], creatorId=m["creatorId"],
                   metadataId=m["metadataId"], status=m["status"]) for m in sc["media"]]
-    store = RacingStore(rows, sc["races"]) if sc.get("races") else None
+    base = RacingStore if sc.get("races") else MemoryStore
+    if gates is not None:
+        cls = _gated_store(base, gates)
+    else:
+        cls = helpers.suspending(base) if suspend else base
+    store = cls(rows, sc["races"]) if base is RacingStore else cls(rows)
     rig = helpers.Rig(config=config, medias=rows, no_trello=bool(sc.get("noTrello")), http=http,
                       positional_args=sc["positionalArgs"], store=store)
     if mutate is not None:
@@ -282,16 +372,20 @@ def run_python(sc: dict, impl: str = "python", mutate=None) -> dict:
     target = rig.h if impl == "python" else native_handlers(rig.h)
     assert target is not None
     dec = {"status": rig.h.decode_status, "progress": rig.h.decode_progress}
+
+    def decode_error(topic, body) -> bool:
+        try:
+            dec[topic](body)
+            return False
+        except DecodeError:
+            return True
+
     events = []
+    order = None
 
     async def go():
         for topic, hexbody in sc["events"]:
             body = bytes.fromhex(hexbody)
-            try:
-                dec[topic](body)
-                decode_error = False
-            except DecodeError:
-                decode_error = True
             n_http = len(http.calls)
             n_log = len(rig.stream.lines)
             d = rig.delivery(1 if topic == "status" else 2, body)
@@ -302,16 +396,108 @@ def run_python(sc: dict, impl: str = "python", mutate=None) -> dict:
                 threw = str(e)
             rig.log.flush()
             logs = [[x["level"], x["msg"]] for x in map(json.loads, rig.stream.lines[n_log:])]
-            events.append({"acks": 1 if d.state == "acked" else 0, "threw": threw, "decodeError": decode_error,
+            events.append({"acks": 1 if d.state == "acked" else 0, "threw": threw,
+                           "decodeError": decode_error(topic, body),
                            "requests": [list(c) for c in list(http.calls)[n_http:]], "logs": logs})
 
-    asyncio.run(go())
+    if conc:
+        events, order = asyncio.run(_run_concurrent(sc, rig, target, gates, decode_error))
+    else:
+        asyncio.run(go())
     counters = {
         "beholder_progress_updates_total": _counter_hashes(rig.progress, ["status"]),
         "beholder_trello_comments": _counter_hashes(rig.comments, []),
     }
     snap = rig.h.store.snapshot()
-    return {"events": events, "counters": counters, "media": {k: v.status for k, v in snap.items()}}
+    out = {"events": events, "counters": counters, "media": {k: v.status for k, v in snap.items()}}
+    if order is not None:
+        out["order"] = order
+    return out
+
+
+async def _run_concurrent(sc: dict, rig, target, gates: _Gates, decode_error):
+    """oracle.js ``concurrent()``, step for step: deliver the next event or open one waiting
+    event's gate (the scenario's script decides), then run the loop until nothing is runnable.
+    Deliveries go through the service's ordering layer when ``service.ordering`` is ``per_media``
+    (parallel/ordering.py, as service.py wires it); the default, ``none``, is the reference's."""
+    from beholder_amd.parallel.ordering import KeyedSerializer
+    loop = asyncio.get_running_loop()
+    cap, script = sc["concurrent"]["cap"], sc["concurrent"]["script"]
+    n = len(sc["events"])
+    bodies = [bytes.fromhex(h) for _, h in sc["events"]]
+    topics = [t for t, _ in sc["events"]]
+    events = [{"acks": 0, "threw": None, "decodeError": decode_error(t, b), "requests": [], "logs": []}
+              for t, b in zip(topics, bodies)]
+    deliveries = [rig.delivery(1 if t == "status" else 2, b) for t, b in zip(topics, bodies)]
+    tasks: Dict[int, asyncio.Task] = {}
+    settled = [False] * n
+    http = rig.http
+
+    def start(i: int, on_finish=None) -> bool:
+        d = deliveries[i]
+        coro = target.on_status(d) if topics[i] == "status" else target.on_progress(d)
+
+        async def run():
+            try:
+                await coro
+            except Exception as e:  # noqa: BLE001 - Q1: status errors escape
+                events[i]["threw"] = str(e)
+            finally:
+                settled[i] = True
+                if on_finish is not None:
+                    on_finish()
+        tasks[i] = loop.create_task(run())
+        return False
+
+    def media_key(i: int):
+        h = rig.h
+        return (h.decode_status if topics[i] == "status" else h.decode_progress)(bodies[i]).mediaId
+
+    ordering = rig.config.data.get("service", {}).get("ordering", "none")
+    submit = KeyedSerializer(start, media_key).submit if ordering == "per_media" else start
+
+    order = []
+    nxt = 0
+    step = 0
+    while True:
+        ready = sorted(gates.waiting)
+        r = script[step % len(script)]
+        step += 1
+        active = nxt - sum(settled[:nxt])
+        if nxt < n and (not ready or (active < cap and r % 2 == 0)):
+            i, action, kind = nxt, "deliver", None
+            nxt += 1
+        elif ready:
+            i = ready[(r >> 1) % len(ready)]
+            action = "resolve"
+        else:
+            if active:
+                raise RuntimeError(f"{active} deliveries in flight, none at a gate")
+            break
+        gates.current = i
+        n_http, n_log = len(http.calls), len(rig.stream.lines)
+        acked = deliveries[i].state == "acked"
+        if action == "deliver":
+            submit(i)
+        else:
+            kind, fut = gates.waiting.pop(i)
+            fut.set_result(None)
+        for _ in range(10000):  # until nothing is runnable (oracle.js: one setImmediate)
+            await asyncio.sleep(0)
+            if not loop._ready:  # noqa: SLF001 - the loop's runnable queue
+                break
+        rig.log.flush()
+        ev = events[i]
+        logs = [[x["level"], x["msg"]] for x in map(json.loads, rig.stream.lines[n_log:])]
+        reqs = [list(c) for c in list(http.calls)[n_http:]]
+        ev["logs"] += logs
+        ev["requests"] += reqs
+        now_acked = deliveries[i].state == "acked"
+        ev["acks"] = 1 if now_acked else 0
+        order.append([action, i, kind, len(logs), len(reqs), int(now_acked and not acked), settled[i]])
+    for t in tasks.values():
+        await t
+    return events, order
 
 
 def diff(ref: dict, got: dict, limit: int = 8) -> List[str]:
@@ -325,6 +511,14 @@ def diff(ref: dict, got: dict, limit: int = 8) -> List[str]:
                 out.append(f"event {i} {k}: reference={a[k]!r} ours={b[k]!r}")
                 if len(out) >= limit:
                     return out
+    if "order" in ref or "order" in got:
+        for j, (a, b) in enumerate(zip(ref.get("order") or [], got.get("order") or [])):
+            if a != b:
+                out.append(f"step {j}: reference={a!r} ours={b!r}")
+                break
+        else:
+            if len(ref.get("order") or []) != len(got.get("order") or []):
+                out.append(f"steps {len(ref.get('order') or [])} != {len(got.get('order') or [])}")
     ref_counters = {k: [e for e in v if e[1]] for k, v in ref["counters"].items()}
     if ref_counters != got["counters"]:
         out.append(f"counters: reference={ref_counters} ours={got['counters']}")
@@ -333,10 +527,11 @@ def diff(ref: dict, got: dict, limit: int = 8) -> List[str]:
     return out
 
 
-def check(seed: int, mode: str, n_events: int = 520, impls=("python", "native")) -> Dict[str, List[str]]:
+def check(seed: int, mode: str, n_events: int = 520, impls=("python", "native"),
+          suspend: bool = False) -> Dict[str, List[str]]:
     sc = make_scenario(seed, n_events, mode)
     ref = run_node(sc)
-    return {impl: diff(ref, run_python(sc, impl)) for impl in impls}
+    return {impl: diff(ref, run_python(sc, impl, suspend=suspend)) for impl in impls}
 
 
 def coverage(ref: dict) -> dict:
@@ -381,6 +576,50 @@ def reread_coverage(sc: dict, ref: dict) -> dict:
             "hooks_skipped_on_deployed_msg": hooks_skipped_on_deployed_msg}
 
 
+def _media_ids(sc: dict) -> List[Optional[str]]:
+    out: List[Optional[str]] = []
+    for topic, hexbody in sc["events"]:
+        try:
+            out.append((_S if topic == "status" else _P).decode(bytes.fromhex(hexbody))[0])
+        except Exception:  # noqa: BLE001 - undecodable: no media
+            out.append(None)
+    return out
+
+
+def concurrent_coverage(sc: dict, ref: dict) -> dict:
+    """For a ``concurrent`` scenario, as the reference ran it: steps with two deliveries of one
+    media in flight, status events whose hooks decision (index.js:94, the re-read row) disagrees
+    with the message's status because another delivery's UPDATE landed in between, and steps
+    that resumed a delivery other than the oldest one waiting."""
+    ids = _media_ids(sc)
+    known = {m["id"] for m in sc["media"]}
+    inflight: set = set()
+    overlap = out_of_order = 0
+    waiting: set = set()
+    for action, i, kind, _logs, _reqs, _acks, settled in ref["order"]:
+        if action == "deliver":
+            inflight.add(i)
+        else:
+            if waiting and i != min(waiting):
+                out_of_order += 1
+            waiting.discard(i)
+        if settled:
+            inflight.discard(i)
+        else:
+            waiting.add(i)
+        live = [ids[j] for j in inflight if ids[j] is not None]
+        overlap += len(live) != len(set(live))
+    flipped = 0
+    for (topic, hexbody), ev, mid in zip(sc["events"], ref["events"], ids):
+        if topic != "status" or ev["decodeError"] or mid not in known or ev["threw"] is not None:
+            continue
+        st = _S.decode(bytes.fromhex(hexbody))[1]
+        hooked = any("api.telegram.org" in u for _, u in ev["requests"])
+        flipped += hooked != (st == 4)
+    return {"same_media_overlap_steps": overlap, "hooks_flipped_by_interleaving": flipped,
+            "resumed_out_of_arrival_order": out_of_order}
+
+
 def main(argv: Optional[List[str]] = None) -> int:
     import argparse
     ap = argparse.ArgumentParser(description="reference-executed parity gate")
@@ -388,6 +627,8 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--events", type=int, default=520)
     ap.add_argument("--modes", default=",".join(MODES))
     ap.add_argument("--impls", default="python,native")
+    ap.add_argument("--suspend", action="store_true",
+                    help="store and sink client yield at every call (the compiled handlers' resume states)")
     a = ap.parse_args(argv)
     bad = 0
     for seed in range(a.seeds):
@@ -395,9 +636,9 @@ def main(argv: Optional[List[str]] = None) -> int:
             sc = make_scenario(seed, a.events, mode)
             ref = run_node(sc)
             for impl in a.impls.split(","):
-                d = diff(ref, run_python(sc, impl))
+                d = diff(ref, run_python(sc, impl, suspend=a.suspend))
                 bad += bool(d)
-                print(f"seed {seed} {mode:9s} {impl:6s} {'OK' if not d else 'DIFF'} {coverage(ref) if not d else ''}")
+                print(f"seed {seed} {mode:10s} {impl:6s} {'OK' if not d else 'DIFF'} {coverage(ref) if not d else ''}")
                 for line in d:
                     print("   ", line)
     return 1 if bad else 0

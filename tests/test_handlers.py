@@ -2,6 +2,8 @@
 
 Each test names the reference lines / quirk it pins.
 """
+import asyncio
+
 import pytest
 
 import helpers
@@ -18,6 +20,16 @@ TRELLO = "https://api.trello.com"
 def impl(request, monkeypatch):
     """Every case runs against the Python handlers and the compiled ones (ops/csrc/py_handlers.cpp)."""
     monkeypatch.setattr(helpers, "HANDLER_IMPL", request.param)
+    return request.param
+
+
+@pytest.fixture(autouse=True, params=["sync", "suspend"])
+def io(request, monkeypatch):
+    """...and with a store and sink client that answer within the call, and with ones that suspend
+    at every call (production's shape: the socket clients always wait). Suspended, the compiled
+    handlers return to the loop at each await and finish the event in their resume states
+    (py_handlers.cpp: a Telegram failure resumed in state 5 must still skip Emby, Q4)."""
+    monkeypatch.setattr(helpers, "SUSPEND", request.param == "suspend")
     return request.param
 
 
@@ -96,8 +108,10 @@ def test_status_deployed_runs_telegram_then_emby():
 
 def test_status_deployed_uses_reread_db_status():
     """Q3 (index.js:76,94): the hooks key off the DB row, not the message status."""
-    class StaleStore(MemoryStore):
+    class StaleStore(helpers.SuspendingStore if helpers.SUSPEND else MemoryStore):
         async def update_status(self, media_id, status):  # write lost / lagging replica
+            if helpers.SUSPEND:
+                await asyncio.sleep(0)
             self.update_calls += 1
 
     r = Rig(medias=[api_media("m2", "DEPLOYED")])
@@ -296,3 +310,14 @@ def test_progress_zero_progress_renders_zero():
 def test_js_truthy():
     assert not js_truthy(None) and not js_truthy("") and not js_truthy(0) and not js_truthy(float("nan"))
     assert js_truthy("0") and js_truthy({}) and js_truthy([]) and js_truthy(-1) and js_truthy("false")
+
+
+def test_suspending_rig_resumes_the_native_state_machine(impl, io):
+    """The ``suspend`` cases really leave C: every await of a DEPLOYED status event suspends
+    (update, re-read, Telegram, Emby) and the call completes in its resume states."""
+    r = Rig(medias=[api_media("m2")])
+    d, exc = r.status(status_msg("m2", "DEPLOYED"))
+    assert exc is None and d.acked and len(r.calls()) == 2
+    if impl == "native":
+        st = r.impl.stats()
+        assert (st["suspended"], st["completed_sync"]) == ((1, 0) if io == "suspend" else (0, 1))

@@ -32,16 +32,7 @@ from beholder_amd.store import Media, MemoryStore
 from helpers import Rig, cfg, progress_msg, status_msg
 
 
-class SuspendingStore(MemoryStore):
-    """Every access awaits a real loop iteration (a network store's shape)."""
-
-    async def update_status(self, media_id, status):
-        await asyncio.sleep(0)
-        MemoryStore.update_status_nowait(self, media_id, status)
-
-    async def get_by_id(self, media_id):
-        await asyncio.sleep(0)
-        return MemoryStore.get_by_id_nowait(self, media_id)
+SuspendingStore = helpers.SuspendingStore  # every access awaits a real loop iteration
 
 
 class FlakyStore(MemoryStore):

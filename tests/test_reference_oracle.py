@@ -16,18 +16,51 @@ SEEDS = range(5)
 EVENTS = 520
 
 
+@pytest.mark.parametrize("io", ["sync", "suspend"])
 @pytest.mark.parametrize("mode", ro.MODES)
-def test_reference_parity(mode):
+def test_reference_parity(mode, io):
+    """``suspend``: the store and the sink client yield at every call, as production's socket
+    clients do, so the compiled handlers finish every event in their resume states. The
+    ``concurrent`` mode always suspends (at its gates) and is run once."""
+    if mode == "concurrent" and io == "suspend":
+        pytest.skip("the concurrent mode suspends at every call already")
     failures = {}
     for seed in SEEDS:
         sc = ro.make_scenario(seed, EVENTS, mode)
         ref = ro.run_node(sc)
         assert len(ref["events"]) == EVENTS
         for impl in ("python", "native"):
-            d = ro.diff(ref, ro.run_python(sc, impl))
+            d = ro.diff(ref, ro.run_python(sc, impl, suspend=io == "suspend"))
             if d:
                 failures[(seed, impl)] = d
     assert not failures, "\n".join(f"{k}: " + "\n  ".join(v) for k, v in failures.items())
+
+
+def test_concurrent_scenarios_interleave():
+    """Mode ``concurrent`` (Q9, index.js:43,62,127): the reference's own runs of the scripted
+    schedules have two deliveries of one media in flight, resume deliveries out of arrival order,
+    and flip the DEPLOYED-hooks decision of some status events against their message (another
+    delivery's UPDATE lands between an event's updateStatus and its getByID, index.js:68,76,94)."""
+    total: dict = {}
+    for seed in SEEDS:
+        sc = ro.make_scenario(seed, EVENTS, "concurrent")
+        for k, v in ro.concurrent_coverage(sc, ro.run_node(sc)).items():
+            total[k] = total.get(k, 0) + v
+    assert all(v > 0 for v in total.values()), total
+
+
+def test_faults_mode_fails_telegram_with_emby_on():
+    """Every ``faults`` scenario fails Telegram for some DEPLOYED rows while Emby is on (Q4,
+    index.js:92-122) and fails some comment POSTs (index.js:53-57), so a handler that runs
+    Emby after a failed Telegram call, or counts a failed comment, diverges on every seed."""
+    for seed in SEEDS:
+        sc = ro.make_scenario(seed, EVENTS, "faults")
+        ref = ro.run_node(sc)
+        reqs = [(e, m, u) for e in ref["events"] for m, u in e["requests"]]
+        failed_tg = [e for e, m, u in reqs if u.startswith(ro.TELEGRAM_FAULT_PREFIX)]
+        assert failed_tg and all(not any("/emby/" in u for _, u in e["requests"]) for e in failed_tg), seed
+        assert any("/emby/" in u for _, _, u in reqs), seed
+        assert any(u.startswith("https://api.trello.com/1/cards/card1/actions/comments") for _, _, u in reqs), seed
 
 
 def test_streams_reach_every_reference_branch():
