@@ -13,7 +13,9 @@ The HIP library is optional for the service: ``main`` builds it only when ``hipc
 (``--hip`` makes it required, ``--no-hip`` skips it), so the deployment image and CI, which have
 no ROCm, build the runtime alone.
 
-Usage: ``python -m beholder_amd.ops.build [--debug] [--sanitize=address,undefined] [--hip|--no-hip] [--no-bench]``
+Usage: ``python -m beholder_amd.ops.build [--debug] [--sanitize=address,undefined] [--coverage] [--hip|--no-hip]
+[--no-bench]`` (``--coverage``: gcov-instrumented, objects and their ``.gcno`` / ``.gcda`` kept under
+``build/coverage/``; ``scripts/native_coverage.py`` and ``make coverage`` use it)
 (thin CLI over this module)
 """
 from __future__ import annotations
@@ -60,12 +62,19 @@ def source_hash(flags: list, dirs=(CSRC,)) -> str:
     return h.hexdigest()
 
 
-def compile_flags(debug: bool = False, sanitize: str = "") -> list:
+# objects of a --coverage build (gcov reads the .gcno written at compile time and the .gcda the
+# instrumented extension writes next to them at exit)
+COVERAGE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "build", "coverage")
+
+
+def compile_flags(debug: bool = False, sanitize: str = "", coverage: bool = False) -> list:
     inc = sysconfig.get_paths()["include"]
     flags = ["-std=c++17", "-fPIC", "-shared", "-pthread", "-fvisibility=hidden",
              "-Wall", "-Wextra", "-Wno-missing-field-initializers", "-Wno-cast-function-type",
              f"-I{inc}", f"-I{CSRC}", f"-I{CSRC_BENCH}"]
-    if debug:
+    if coverage:  # line / branch counts per source line: unoptimised, counters updated atomically
+        flags += ["-O0", "-g", "--coverage", "-fprofile-update=atomic"]
+    elif debug:
         flags += ["-O0", "-g"]
     else:
         # x86-64-v2 keeps the .so portable across the build container and the
@@ -112,23 +121,29 @@ class _BuildLock:
         self.fd = -1
 
 
-def build(force: bool = False, debug: bool = False, sanitize: str = "", cxx: str = "", verbose: bool = False) -> str:
+def build(force: bool = False, debug: bool = False, sanitize: str = "", cxx: str = "", verbose: bool = False,
+          coverage: bool = False) -> str:
     """The service's extension ``_native`` from ``csrc/``."""
-    return _build_module(TARGET, sources(CSRC), (CSRC,), LIBS, force, debug, sanitize, cxx, verbose)
+    return _build_module(TARGET, sources(CSRC), (CSRC,), LIBS, force, debug, sanitize, cxx, verbose, coverage)
 
 
 def build_bench(force: bool = False, debug: bool = False, sanitize: str = "", cxx: str = "",
-                verbose: bool = False) -> str:
+                verbose: bool = False, coverage: bool = False) -> str:
     """The bench/test extension ``_native_bench`` from ``csrc_bench/`` (headers from ``csrc/``:
     it calls the service's code through ``_native._C_API``, never links it)."""
     return _build_module(BENCH_TARGET, sources(CSRC_BENCH), (CSRC_BENCH, CSRC), [], force, debug, sanitize, cxx,
-                         verbose)
+                         verbose, coverage)
+
+
+def coverage_objdir(target: str) -> str:
+    """Where a --coverage build of ``target`` keeps its objects (and gcov its counts)."""
+    return os.path.join(COVERAGE_DIR, os.path.basename(target).split(".")[0])
 
 
 def _build_module(target: str, srcs: list, dirs: tuple, libs: list, force: bool, debug: bool, sanitize: str,
-                  cxx: str, verbose: bool) -> str:
+                  cxx: str, verbose: bool, coverage: bool = False) -> str:
     cxx = cxx or os.environ.get("CXX") or "g++"
-    flags = compile_flags(debug, sanitize)
+    flags = compile_flags(debug, sanitize, coverage)
     stamp = target + ".srchash"
     # hash path-independent flags so a snapshot copied elsewhere (GPU box) reuses the .so
     digest = source_hash([f for f in flags if not f.startswith("-I")] + libs + [cxx, sysconfig.get_config_var("SOABI") or ""],
@@ -147,7 +162,13 @@ def _build_module(target: str, srcs: list, dirs: tuple, libs: list, force: bool,
         cflags = [f for f in flags if f != "-shared"]
         jobs = max(1, min(len(srcs), int(os.environ.get("MAX_JOBS", "0") or 0) or (os.cpu_count() or 1), 16))
         try:
-            with tempfile.TemporaryDirectory(prefix="beholder-build-") as td:
+            if coverage:
+                import shutil
+                shutil.rmtree(coverage_objdir(target), ignore_errors=True)  # stale counts with the objects
+                os.makedirs(coverage_objdir(target))
+            with tempfile.TemporaryDirectory(prefix="beholder-build-") as tmpd:
+                td = coverage_objdir(target) if coverage else tmpd
+
                 def compile_one(src: str) -> str:
                     obj = os.path.join(td, os.path.basename(src) + ".o")
                     cmd = [cxx, *cflags, "-c", src, "-o", obj]
@@ -221,6 +242,7 @@ def main(argv=None) -> int:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--sanitize", default="")
+    ap.add_argument("--coverage", action="store_true", help="gcov-instrumented build (objects kept in build/coverage)")
     ap.add_argument("--cxx", default="")
     g = ap.add_mutually_exclusive_group()
     g.add_argument("--hip", action="store_true", help="require the gfx950 HIP extension (fail without hipcc)")
@@ -228,10 +250,11 @@ def main(argv=None) -> int:
     ap.add_argument("--no-bench", action="store_true",
                     help="skip the bench/test extension _native_bench (the runtime image ships only the service)")
     a = ap.parse_args(argv)
-    print(build(force=a.force, debug=a.debug, sanitize=a.sanitize, cxx=a.cxx, verbose=True))
+    print(build(force=a.force, debug=a.debug, sanitize=a.sanitize, cxx=a.cxx, verbose=True, coverage=a.coverage))
     if not a.no_bench:
-        print(build_bench(force=a.force, debug=a.debug, sanitize=a.sanitize, cxx=a.cxx, verbose=True))
-    if a.no_hip or a.sanitize:
+        print(build_bench(force=a.force, debug=a.debug, sanitize=a.sanitize, cxx=a.cxx, verbose=True,
+                          coverage=a.coverage))
+    if a.no_hip or a.sanitize or a.coverage:
         return 0
     if not a.hip and not hipcc():
         print("hipcc not found: skipping the optional gfx950 HIP extension (ops/hip); the service does not use it",
