@@ -512,7 +512,7 @@ def _io_counts(src) -> Dict[str, int]:
 
 
 def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = False, preconnect: int = 0,
-             max_connecting: int = 8, hooks: Optional[tuple] = None) -> dict:
+             max_connecting: int = 8, hooks: Optional[tuple] = None, rate: float = 0.0) -> dict:
     """Production-shaped: every dependency over real TCP. A replay AMQP broker streams n
     events (prefetch 100, index.js:43). Each handler reads / updates the media row in a
     fake Postgres (pipelined ``pgwire``). Every sink call goes to a fake HTTP endpoint
@@ -522,7 +522,10 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = Fal
     Telegram are in production (certificate verified against the bench's own CA). ``preconnect``:
     ``service.http.preconnect`` (sink connections opened at init, before the clock).
     ``max_connecting``: ``service.http.max_connecting`` (connects + handshakes in flight per origin).
-    ``hooks``: ``(start, stop)`` callables run around the measured phase (scripts/cprof.py)."""
+    ``hooks``: ``(start, stop)`` callables run around the measured phase (scripts/cprof.py).
+    ``rate``: the broker paces its sends at that many events per second (BASELINE configs 2-4 on
+    the production path: each event's receive->ack latency with its Postgres and HTTP round trips,
+    not queueing behind a saturated prefetch window); the warm-up is then a tenth of the events."""
     from ..config import Config
     from ..service import Service
     from ..sinks import H1Client
@@ -532,10 +535,12 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = Fal
     from ..utils.log import Logger
     from .stallmon import StallMonitor
 
-    warm = min(5000, n // 10)
-    bport, bprocs = _spawn("beholder_amd.bench.replay_broker", 1, ("--events", str(n)))
+    warm = n // 10 if rate else min(5000, n // 10)
+    bargs = ("--events", str(n)) + (("--rate", str(rate)) if rate else ())
+    bport, bprocs = _spawn("beholder_amd.bench.replay_broker", 1, bargs)
     procs = list(bprocs)
-    out: dict = {"events": n, "prefetch": 100, "preconnect": preconnect, "max_connecting": max_connecting}
+    out: dict = {"events": n, "prefetch": 100, "preconnect": preconnect, "max_connecting": max_connecting,
+                 "rate": rate}
     diag = None
     try:
         hport, hp = _spawn("beholder_amd.bench.http_sink_server", http_servers, ("--tls",) if tls else ())
@@ -643,6 +648,9 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = Fal
             "cpu_us_per_event": cpu / m * 1e6 if m else None,
             "sys_cpu_us_per_event": sys_s / m * 1e6 if m else None,
             "handle_latency_us": {k: v / 1e3 for k, v in stats["handle_latency_ns"].items() if k.startswith("p")},
+            # receive -> ack (the handler's wait for the loop included) and receive -> handler start
+            "ingest_latency_us": {k: v / 1e3 for k, v in stats["ingest_latency_ns"].items() if k.startswith("p")},
+            "queue_latency_us": {k: v / 1e3 for k, v in stats["queue_latency_ns"].items() if k.startswith("p")},
             "warmup_handle_latency_us": {k: v / 1e3 for k, v in cold.items() if k.startswith("p")},
             "errors": sum(stats.get("handler_errors", {}).values()),
             "pg_connections": pg_conns, "http": http_stats, "rss_growth_mb": round(rss_growth, 2),
@@ -664,6 +672,12 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = Fal
             "run_delay_ms": diag["run_delay_ms"],
         })
     finally:
+        if diag is not None:  # the broker prints its DONE line (paced: how late its sends were) and exits
+            for p in bprocs:
+                try:
+                    p.wait(timeout=3)
+                except Exception:  # noqa: BLE001 - reaped below either way
+                    pass
         stalls: list = []
         counters = _reap(procs, stalls)
         out["server_side"] = counters
@@ -735,6 +749,9 @@ def _amqp(n: int) -> dict:
     return {"events": n, "acked": stats["source"]["acked"], "warmup_events": warm, "measured_events": measured,
             "elapsed_s": elapsed, "ingest_rate_eps": measured / elapsed if elapsed > 0 else None,
             "handle_latency_us": {k: v / 1e3 for k, v in stats["handle_latency_ns"].items() if k.startswith("p")},
+            # receive -> ack (the handler's wait for the loop included) and receive -> handler start
+            "ingest_latency_us": {k: v / 1e3 for k, v in stats["ingest_latency_ns"].items() if k.startswith("p")},
+            "queue_latency_us": {k: v / 1e3 for k, v in stats["queue_latency_ns"].items() if k.startswith("p")},
             "broker": tail, "prefetch": 100, "native_demux": True,
             "cpu_us_per_event": cpu / measured * 1e6 if measured else None,
             "ack_frames": stats["source"].get("ack_frames")}

@@ -13,7 +13,9 @@ at most ``prefetch × consumers`` un-acked deliveries in flight (RabbitMQ's
 per-consumer ``basic.qos`` summed over the channel's consumers).
 
 Run as a process: ``python -m beholder_amd.bench.replay_broker --events N --port P``
-(prints ``READY <port>`` then serves one consumer connection). ``--shared --consumers N``: any
+(prints ``READY <port>`` then serves one consumer connection). ``--rate R``: paced, event i is
+sent at ``t0 + i / R`` (not before; later only when the prefetch window is full), for the
+production path's latency at BASELINE's rates; the DONE line then has how late the sends were. ``--shared --consumers N``: any
 number of connections share the queues (:class:`SharedQueueBroker`, competing consumers).
 """
 from __future__ import annotations
@@ -33,8 +35,10 @@ _ACK = (60, 80)
 
 
 class ReplayBroker:
-    def __init__(self, events: List[Tuple[str, bytes]], port: int = 0, channel: int = 1):
+    def __init__(self, events: List[Tuple[str, bytes]], port: int = 0, channel: int = 1, rate: float = 0.0):
         self.events = events
+        self.rate = rate
+        self.late_us: List[float] = []  # paced: per send batch, how late its first event went out
         # content header + body frames pre-encoded at startup (channel 1: the consumer's first channel)
         self.content = [wire.encode_content(channel, 60, body, None, 131072) for _, body in events]
         self.port = port
@@ -60,12 +64,16 @@ class ReplayBroker:
         mhead: Dict[str, bytes] = {}
         mtail: Dict[str, bytes] = {}
         acked_upto = 0
+        acked_run = 0
+        above: set = set()
         sent = 0
         total = len(self.events)
         pending_window = asyncio.Event()
 
         async def pump():
             nonlocal sent
+            rate = self.rate
+            t0 = None
             while sent < total:
                 window = prefetch * max(1, len(consumers)) if prefetch else total
                 room = window - (sent - acked_upto)
@@ -73,7 +81,21 @@ class ReplayBroker:
                     pending_window.clear()
                     await pending_window.wait()
                     continue
-                n = min(room, total - sent, 512)
+                if rate:
+                    # paced: everything due by now (event i is due at t0 + i / rate); until the next
+                    # due time, sleep (the loop's timers are 1 ms coarse) then yield until it comes
+                    now = time.perf_counter()
+                    if t0 is None:
+                        t0 = now
+                    due = min(total, int((now - t0) * rate) + 1)
+                    if due <= sent:
+                        wait = t0 + sent / rate - now
+                        await asyncio.sleep(wait - 0.0012 if wait > 0.0015 else 0)
+                        continue
+                    self.late_us.append((now - (t0 + sent / rate)) * 1e6)
+                    n = min(room, due - sent, 512)
+                else:
+                    n = min(room, total - sent, 512)
                 if self.t_first is None:
                     self.t_first = time.perf_counter()
                 parts = []
@@ -99,11 +121,21 @@ class ReplayBroker:
                     cid, mid = struct.unpack_from(">HH", payload)
                     if (cid, mid) == _ACK:
                         tag, flags = struct.unpack_from(">QB", payload, 4)
-                        # `acked_upto` counts settled deliveries (window = sent - acked_upto)
-                        acked_upto = max(acked_upto, tag) if flags & 1 else acked_upto + 1
+                        # every tag <= acked_run is settled, and the tags in `above` (acked one by
+                        # one above a gap); a multiple ack may cover tags acked singly before
+                        if flags & 1:
+                            if tag > acked_run:
+                                acked_run = tag
+                                above = {t for t in above if t > acked_run}
+                        elif tag > acked_run:
+                            above.add(tag)
+                        while acked_run + 1 in above:
+                            acked_run += 1
+                            above.discard(acked_run)
+                        acked_upto = acked_run + len(above)  # settled deliveries (window = sent - acked_upto)
                         self.acked = acked_upto
                         pending_window.set()
-                        if acked_upto >= total and not self.done.is_set():
+                        if acked_run >= total and not self.done.is_set():
                             self.t_done = time.perf_counter()
                             self.done.set()
                         continue
@@ -493,14 +525,19 @@ async def _main(a) -> None:
             asyncio.get_running_loop().add_signal_handler(signal.SIGTERM, lambda: stop.done() or stop.set_result(None))
             await stop
         return
-    b = await ReplayBroker(events, a.port).start()
+    b = await ReplayBroker(events, a.port, rate=a.rate).start()
     del w
     from .stallmon import fake_monitor
     mon = fake_monitor()
     print(f"READY {b.port}", flush=True)
     await b.done.wait()
     mon.stop()
-    print(f"DONE sent={b.sent} acked={b.acked} broker_s={b.t_done - b.t_first:.6f}", flush=True)
+    late = ""
+    if b.late_us:
+        lu = sorted(b.late_us)
+        late = " " + " ".join(f"late_{k}_us={int(lu[min(len(lu) - 1, int(q * len(lu)))])}"
+                              for k, q in (("p50", 0.5), ("p99", 0.99), ("max", 1.0)))
+    print(f"DONE sent={b.sent} acked={b.acked} broker_s={b.t_done - b.t_first:.6f}{late}", flush=True)
     print(mon.dump_line("broker"), flush=True)
     await asyncio.sleep(0.5)
 
@@ -511,6 +548,8 @@ def main(argv=None) -> int:
     ap.add_argument("--media", type=int, default=10000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--port", type=int, default=0)
+    ap.add_argument("--rate", type=float, default=0.0,
+                    help="paced: events per second (0 = as fast as the prefetch window allows)")
     ap.add_argument("--shared", action="store_true",
                     help="competing consumers: any number of connections share the queues (SharedQueueBroker)")
     ap.add_argument("--consumers", type=int, default=1,

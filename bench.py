@@ -109,6 +109,8 @@ def parse(argv=None):
                     help="events of each tcp_e2e / tls_e2e measurement (the first 5,000 are the warm-up)")
     ap.add_argument("--e2e-repeats", type=int, default=3,
                     help="tcp_e2e / tls_e2e runs each; the line has the median run (by rate) and every run's figures")
+    ap.add_argument("--e2e-paced-scale", type=float, default=1.0,
+                    help="events of the paced tcp_e2e / tls_e2e runs (E2E_RATES) times this (0 = skip them)")
     ap.add_argument("--soak-events", type=int, default=1_000_000)
     ap.add_argument("--shared-queue-events", type=int, default=100_000,
                     help="events per worker of each shared-queue run (run --workers N on one queue; 0 = skip)")
@@ -219,6 +221,7 @@ async def run_consumer(a, seed: int, go, stop=None, *, steps: int = None, warmup
     from beholder_amd.sinks import RecordingHttpClient
     from beholder_amd.store import MemoryStore
     from beholder_amd.transport.ingest import FdSource
+    from beholder_amd.utils.hostinfo import proc_run_delay_ns, thread_run_delay_ns
     from beholder_amd.utils.log import Logger
 
     steps = a.steps if steps is None else steps
@@ -241,12 +244,21 @@ async def run_consumer(a, seed: int, go, stop=None, *, steps: int = None, warmup
     run_task = asyncio.ensure_future(svc.run())
     settler = svc.source.settler
 
-    def write_step(i: int) -> threading.Thread:
+    pump_delay = [0, True]  # run-queue wait of the timed steps' pump threads (ns), all known
+
+    def write_step(i: int, timed: bool) -> threading.Thread:
         def pump(data=step_bytes[i]):
+            r0 = thread_run_delay_ns() if timed else None
             mv = memoryview(data)
             while mv:
                 n = os.write(wfd, mv[:1 << 20])
                 mv = mv[n:]
+            if timed:
+                r1 = thread_run_delay_ns()
+                if r0 is None or r1 is None:
+                    pump_delay[1] = False
+                else:
+                    pump_delay[0] += r1 - r0
         t = threading.Thread(target=pump, daemon=True)
         t.start()
         return t
@@ -261,15 +273,21 @@ async def run_consumer(a, seed: int, go, stop=None, *, steps: int = None, warmup
 
     t0 = 0.0
     ru0 = None
+    rq0 = pq0 = rq1 = pq1 = None
     for i in range(total_steps):
         if i == warmup:
             settler.reset_latency()
             go()
             t0 = time.perf_counter()
             ru0 = resource.getrusage(resource.RUSAGE_SELF)
-        th = write_step(i)
+            # run-queue waits over exactly the timed steps: this (the event loop's) thread, and every
+            # thread of the process alive across them (the native reader thread, HIP's runtime
+            # threads started by go()'s synchronize); the pump threads report their own
+            rq0, pq0 = thread_run_delay_ns(), proc_run_delay_ns()
+        th = write_step(i, i >= warmup)
         await wait_settled((i + 1) * E)
         th.join()
+    rq1, pq1 = thread_run_delay_ns(), proc_run_delay_ns()
     if stop is not None:
         stop()
     elapsed = time.perf_counter() - t0
@@ -295,6 +313,9 @@ async def run_consumer(a, seed: int, go, stop=None, *, steps: int = None, warmup
         # page faults in the timed steps: a box still compacting memory shows here, not in calib_*
         "minflt": ru1.ru_minflt - ru0.ru_minflt if ru0 else 0,
         "majflt": ru1.ru_majflt - ru0.ru_majflt if ru0 else 0,
+        "timed_run_delay_ms": (rq1 - rq0) / 1e6 if rq0 is not None and rq1 is not None else None,
+        "timed_proc_run_delay_ms": (pq1 - pq0) / 1e6 if pq0 is not None and pq1 is not None else None,
+        "timed_pump_run_delay_ms": pump_delay[0] / 1e6 if pump_delay[1] and steps else None,
     }
 
 
@@ -373,6 +394,11 @@ def run_procs(a, dist: _Dist, procs: int, steps: int, warmup: int = 1) -> dict:
 
 def _r(x, nd=3):
     return None if x is None else round(float(x), nd)
+
+
+def _max_or_none(xs, nd=2):
+    xs = list(xs)
+    return None if not xs or any(x is None for x in xs) else round(max(xs), nd)
 
 
 def _attr_keys(prefix: str, att: dict) -> dict:
@@ -480,6 +506,42 @@ def _e2e_keys(prefix: str, run, n: int, repeats: int = 1, **kw) -> dict:
     return out
 
 
+# The production path at BASELINE's rates (configs 2-4: 1k, 10k, 100k events/s): tcp_e2e / tls_e2e
+# with the replay broker pacing its sends, so each event's receive->ack latency is its own Postgres
+# and HTTP round trips, not queueing behind a saturated prefetch window. (name, events/s, events:
+# a tenth of them is the warm-up, connection pools filling at that rate)
+E2E_RATES = (("1k", 1000, 3000), ("10k", 10000, 20000), ("100k", 100000, 100000))
+
+
+def _paced_e2e_keys(prefix: str, name: str, e: dict) -> dict:
+    """Keys of one paced production-path run: handler start->ack and receive->ack p50/p99/p999,
+    the achieved rate, CPU per event, and how late the broker's sends were against their due time
+    (p99; late sends mean the consumer held the prefetch window full)."""
+    hl = e.get("handle_latency_us") or {}
+    il = e.get("ingest_latency_us") or {}
+    ss = e.get("server_side") or {}
+    p = f"{prefix}_rate_{name}"
+    return {f"{p}_events_per_sec": _r(e.get("ingest_rate_eps"), 1),
+            f"{p}_p50_handle_latency_us": _r(hl.get("p50"), 1), f"{p}_p99_handle_latency_us": _r(hl.get("p99"), 1),
+            f"{p}_p999_handle_latency_us": _r(hl.get("p999"), 1),
+            f"{p}_p50_ingest_latency_us": _r(il.get("p50"), 1), f"{p}_p99_ingest_latency_us": _r(il.get("p99"), 1),
+            f"{p}_cpu_us_per_event": _r(e.get("cpu_us_per_event"), 2),
+            f"{p}_broker_late_p99_us": ss.get("late_p99_us"),
+            f"{p}_measured_events": e.get("measured_events"), f"{p}_errors": e.get("errors"),
+            f"{p}_run_delay_ms": _r(e.get("run_delay_ms"), 2)}
+
+
+def paced_e2e_keys(a, prefix: str, **kw) -> dict:
+    from beholder_amd.bench import harness
+    out = {}
+    if a.e2e_paced_scale <= 0:
+        return out
+    for name, rate, n in E2E_RATES:
+        n = max(200, int(n * a.e2e_paced_scale))
+        out.update(_paced_e2e_keys(prefix, name, harness._tcp_e2e(n, rate=rate, **kw)))
+    return out
+
+
 def shared_queue_workers(cpus: int, cap: int = 8) -> list:
     """N of the shared-queue sweep: 1, 2, 4, 8 while N workers + the broker + this process + one
     spare CPU fit in the share."""
@@ -530,8 +592,10 @@ def io_extras(a) -> dict:
     out.update(_e2e_keys("tcp_e2e", harness._tcp_e2e, a.e2e_events, a.e2e_repeats))
     # and of the TLS path: its first run in a process paid ~1 µs/event more system time (OpenSSL's
     # connection buffers first touched; profiles/box_r5_runs/, box_r5_pgn/)
+    out.update(paced_e2e_keys(a, "tcp_e2e"))
     harness._tcp_e2e(min(100000, a.e2e_events), http_servers=4, tls=True)
     out.update(_e2e_keys("tls_e2e", harness._tcp_e2e, a.e2e_events, a.e2e_repeats, http_servers=4, tls=True))
+    out.update(paced_e2e_keys(a, "tls_e2e", http_servers=4, tls=True))
     # the same with service.http.preconnect = prefetch: the first wave of TLS handshakes happens
     # in init (`_init_ms`), not inside the first deliveries' handle latency
     pre = harness._tcp_e2e(a.io_events, http_servers=4, tls=True, preconnect=100)
@@ -750,9 +814,14 @@ TAIL_KEYS = (
     "tls_e2e_preconnect_warmup_p999_handle_latency_us",
     "tls_e2e_warmup_p999_handle_latency_us", "tls_e2e_p999_handle_latency_us", "tls_e2e_cpu_us_per_event",
     "tls_e2e_events_per_sec",
+    "tls_e2e_rate_10k_p50_handle_latency_us", "tls_e2e_rate_10k_p99_handle_latency_us",
+    "tcp_e2e_rate_1k_p50_handle_latency_us", "tcp_e2e_rate_1k_p99_handle_latency_us",
+    "tcp_e2e_rate_100k_p50_handle_latency_us", "tcp_e2e_rate_100k_p99_handle_latency_us",
+    "tcp_e2e_rate_10k_p50_ingest_latency_us", "tcp_e2e_rate_10k_p99_ingest_latency_us",
+    "tcp_e2e_rate_10k_p50_handle_latency_us", "tcp_e2e_rate_10k_p99_handle_latency_us",
     "tcp_e2e_warmup_p999_handle_latency_us", "tcp_e2e_p999_handle_latency_us", "tcp_e2e_p99_handle_latency_us",
     "tcp_e2e_sys_cpu_us_per_event", "tcp_e2e_cpu_us_per_event", "tcp_e2e_events_per_sec",
-    "calib_ns", "value_calibrated", "handler_errors",
+    "calib_ns", "value_calibrated", "handler_errors", "headline_timed_run_delay_ms",
     "cpu_us_per_event", "p99_handle_latency_us", "p50_handle_latency_us", "value",
 )
 # diagnostics that go on the line first, while it has room (the rest follow in run order)
@@ -762,7 +831,11 @@ DIAG_FIRST = (
     "tcp_e2e_runs", "tls_e2e_runs",
     "tls_e2e_calib_ns", "tls_e2e_sys_cpu_us_per_event", "tls_e2e_minflt", "tls_e2e_nivcsw",
     "tls_e2e_fakes_cpu_us_per_event", "tls_e2e_host_cpu_busy_pct", "tls_e2e_slow_blamed",
-    "headline_minflt", "headline_run_delay_ms", "involuntary_ctx_switches", "headline_host_cpu_busy_pct",
+    "headline_minflt", "headline_run_delay_ms", "headline_timed_pump_run_delay_ms",
+    "headline_timed_proc_run_delay_ms", "involuntary_ctx_switches", "headline_host_cpu_busy_pct",
+    "tcp_e2e_rate_1k_events_per_sec", "tcp_e2e_rate_10k_events_per_sec", "tcp_e2e_rate_100k_events_per_sec",
+    "tcp_e2e_rate_10k_cpu_us_per_event", "tcp_e2e_rate_10k_broker_late_p99_us",
+    "tcp_e2e_rate_100k_broker_late_p99_us", "tls_e2e_rate_10k_events_per_sec",
     "calib_mem_ns", "calib_py_ns",
     "shared_queue_broker_cpu_us_per_event", "shared_queue_acked", "shared_queue_published",
     "plumbing_rc", "plumbing_acked", "plumbing_sink_requests", "rate_1k_acked", "rate_10k_acked",
@@ -860,7 +933,8 @@ def main(argv=None) -> int:
     calib1 = calibrate()
     elapsed = dist.max(res["elapsed"])
     parts = dist.gather({k: res[k] for k in ("handle_hist", "ingest_hist", "http_calls", "errors", "abandoned",
-                                             "events", "cpu_s", "nivcsw", "minflt", "majflt")})
+                                             "events", "cpu_s", "nivcsw", "minflt", "majflt", "timed_run_delay_ms",
+                                             "timed_proc_run_delay_ms", "timed_pump_run_delay_ms")})
     calibs = dist.gather((calib0, calib1))
     # the loop thread's time runnable without a CPU over the headline (warm-up steps included); the
     # process total would also hold the reader thread's many short wake-up waits
@@ -916,6 +990,11 @@ def main(argv=None) -> int:
             "headline_minflt": sum(p["minflt"] for p in parts),
             "headline_run_delay_ms": (round(max(run_delays), 2) if all(x is not None for x in run_delays)
                                       else None),
+            # the same over exactly the K timed steps (after go(), at stop()): the loop thread, every
+            # thread alive across them, and the pump threads feeding the pipe (the worst rank)
+            "headline_timed_run_delay_ms": _max_or_none(p["timed_run_delay_ms"] for p in parts),
+            "headline_timed_proc_run_delay_ms": _max_or_none(p["timed_proc_run_delay_ms"] for p in parts),
+            "headline_timed_pump_run_delay_ms": _max_or_none(p["timed_pump_run_delay_ms"] for p in parts),
             "headline_majflt": sum(p["majflt"] for p in parts),
             "thp": _thp_mode(),
             **cal,

@@ -28,14 +28,25 @@ EXTRAS = {"all_procs_events_per_sec", "rate_10k_p50_ingest_latency_us", "rate_10
           "tls_e2e_nr_throttled", "tcp_e2e_nivcsw", "soak_cpu_us_per_event", "tls_e2e_dial_max_us",
           "tls_e2e_queue_wait_max_us", "headline_minflt", "thp", "tls_e2e_preconnect_warmup_p999_handle_latency_us",
           "tls_e2e_preconnect_init_ms", "tls_e2e_init_ms", "rate_1k_p99_due_to_ack_us",
-          "rate_10k_p99_due_to_ack_us", "rate_100k_p99_due_to_ack_us", "rate_10k_p99_due_to_recv_us"}
+          "rate_10k_p99_due_to_ack_us", "rate_100k_p99_due_to_ack_us", "rate_10k_p99_due_to_recv_us",
+          # round 6: the production path paced at BASELINE's rates, the timed steps' run-queue waits
+          "tcp_e2e_rate_1k_p50_handle_latency_us", "tcp_e2e_rate_10k_p99_handle_latency_us",
+          "tcp_e2e_rate_100k_p99_ingest_latency_us", "tls_e2e_rate_10k_p50_handle_latency_us",
+          "tls_e2e_rate_100k_p99_handle_latency_us", "tcp_e2e_rate_10k_broker_late_p99_us",
+          "headline_timed_run_delay_ms", "headline_timed_proc_run_delay_ms", "headline_timed_pump_run_delay_ms"}
 SMALL = ["--steps", "2", "--warmup", "1", "--events-per-step", "4096", "--media", "500", "--full-out", ""]
 # the keys the driver's `tail` (the last ~2,000 characters of stdout) must show
 DECISION = ("value", "p50_handle_latency_us", "p99_handle_latency_us", "cpu_us_per_event", "calib_ns",
             "value_calibrated", "tcp_e2e_events_per_sec", "tcp_e2e_cpu_us_per_event", "tcp_e2e_sys_cpu_us_per_event",
             "tcp_e2e_p999_handle_latency_us", "tls_e2e_events_per_sec", "tls_e2e_p999_handle_latency_us",
             "rate_1k_p99_ingest_latency_us", "rate_10k_p99_ingest_latency_us", "rate_100k_p99_ingest_latency_us",
-            "soak_events_per_sec", "soak_gc_max_pause_us", "all_procs_events_per_sec")
+            "soak_events_per_sec", "soak_gc_max_pause_us", "all_procs_events_per_sec",
+            "tcp_e2e_rate_1k_p50_handle_latency_us", "tcp_e2e_rate_1k_p99_handle_latency_us",
+            "tcp_e2e_rate_10k_p50_handle_latency_us", "tcp_e2e_rate_10k_p99_handle_latency_us",
+            "tcp_e2e_rate_10k_p50_ingest_latency_us", "tcp_e2e_rate_10k_p99_ingest_latency_us",
+            "tcp_e2e_rate_100k_p50_handle_latency_us", "tcp_e2e_rate_100k_p99_handle_latency_us",
+            "tls_e2e_rate_10k_p50_handle_latency_us", "tls_e2e_rate_10k_p99_handle_latency_us",
+            "headline_timed_run_delay_ms")
 
 
 def _last_json(stdout: str) -> dict:
@@ -50,7 +61,8 @@ def test_bench_single_rank_contract(tmp_path):
     full_path = str(tmp_path / "full.json")
     r = subprocess.run([sys.executable, "bench.py", *SMALL, "--procs-per-rank", "2", "--all-procs-steps", "1",
                         "--io-events", "2000", "--e2e-events", "4000", "--soak-events", "20000",
-                        "--shared-queue-events", "3000", "--e2e-repeats", "2", "--full-out", full_path],
+                        "--shared-queue-events", "3000", "--e2e-repeats", "2", "--e2e-paced-scale", "0.1",
+                        "--full-out", full_path],
                        cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.strip()][-1]
@@ -108,6 +120,13 @@ def test_bench_single_rank_contract(tmp_path):
     assert out["tcp_e2e_run_delay_ms"] is None or out["tcp_e2e_run_delay_ms"] >= 0
     assert out["rate_10k_loop_run_delay_us"] is None or out["rate_10k_loop_run_delay_us"] >= 0
     assert out["headline_run_delay_ms"] is None or out["headline_run_delay_ms"] >= 0
+    assert out["headline_timed_run_delay_ms"] is None or out["headline_timed_run_delay_ms"] >= 0
+    # the paced production path: every event of each rate measured and acked, none failing
+    for pre in ("tcp_e2e", "tls_e2e"):
+        for name, rate, n in bench.E2E_RATES:
+            k = f"{pre}_rate_{name}"
+            assert out[f"{k}_errors"] == 0 and out[f"{k}_measured_events"] >= max(200, int(n * 0.1)) * 0.85, k
+            assert out[f"{k}_p50_handle_latency_us"] <= out[f"{k}_p99_handle_latency_us"], k
     # the consumer's socket calls per event: a send per sink request, queries
     # and acks batched, every kind of connection seen
     io = out["tcp_e2e_io_per_event"]
@@ -192,7 +211,8 @@ def test_no_hip_before_child_processes(monkeypatch, capsys):
     monkeypatch.setattr(harness, "_spawn", spy_spawn)
     monkeypatch.setattr(bench, "run_procs", spy_procs)
     assert bench.main([*SMALL, "--procs-per-rank", "2", "--all-procs-steps", "1", "--io-events", "1000",
-                       "--e2e-events", "1000", "--soak-events", "5000", "--shared-queue-events", "0"]) == 0
+                       "--e2e-events", "1000", "--soak-events", "5000", "--shared-queue-events", "0",
+                       "--e2e-paced-scale", "0"]) == 0
     out = _last_json(capsys.readouterr().out)
     assert out["value"] > 0
     assert "spawn" in order and "procs" in order and "sync" in order
