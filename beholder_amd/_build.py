@@ -78,8 +78,10 @@ def compile_flags(debug: bool = False, sanitize: str = "", coverage: bool = Fals
         flags += ["-O0", "-g"]
     else:
         # x86-64-v2 keeps the .so portable across the build container and the
-        # GPU box hosts (both are x86-64 with SSE4.2/POPCNT).
-        flags += ["-O3", "-march=x86-64-v2", "-mtune=generic", "-DNDEBUG"]
+        # GPU box hosts (both are x86-64 with SSE4.2/POPCNT); other machines get the compiler's default
+        import platform
+        flags += ["-O3", "-DNDEBUG"] + (["-march=x86-64-v2", "-mtune=generic"]
+                                         if platform.machine() in ("x86_64", "AMD64") else [])
     if sanitize:
         flags += [f"-fsanitize={sanitize}", "-fno-omit-frame-pointer", "-g"]
     return flags

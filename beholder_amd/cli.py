@@ -33,15 +33,16 @@ def _load_fixture(path: str):
     return [Media(**r) for r in rows]
 
 
+WORKER_MODULE_ENV = "BEHOLDER_WORKER_MODULE"
+
+
 def worker_command() -> List[str]:
-    """How ``run --workers N`` starts each worker: the interpreter and entry module this process
-    was started with (``python -m beholder_amd`` -> the same; a wrapper entry module such as the
-    bench's ``beholder_amd.bench.shared_worker`` -> that module again), then the run arguments."""
-    main = sys.modules.get("__main__")
-    spec = getattr(main, "__spec__", None)
-    name = getattr(spec, "name", None) or "beholder_amd"
-    if name.endswith(".__main__"):
-        name = name[: -len(".__main__")]
+    """How ``run --workers N`` starts each worker: ``python -m beholder_amd`` with the run
+    arguments. A wrapper entry module that must be in force in every worker (the bench's
+    ``beholder_amd.bench.shared_worker``) opts in by naming itself in ``BEHOLDER_WORKER_MODULE``;
+    the supervisor never guesses it from ``__main__`` (a launcher or test runner hosting ``run``
+    would otherwise be restarted in its place)."""
+    name = os.environ.get(WORKER_MODULE_ENV, "").strip() or "beholder_amd"
     return [sys.executable, "-m", name]
 
 

@@ -32,7 +32,7 @@ void gil_clock_init() {
   c = GilClock();
   const char* env = getenv("BEHOLDER_TSC_CLOCK");
   if (env && env[0] == '0') return;
-  c.mode = kernel_uses_tsc() ? 1 : 0;
+  c.mode = BEHOLDER_HAVE_TSC && kernel_uses_tsc() ? 1 : 0;
 }
 
 int64_t gil_clock_anchor(uint64_t) {
@@ -43,9 +43,9 @@ int64_t gil_clock_anchor(uint64_t) {
   uint64_t t = 0, width = ~uint64_t(0);
   for (int i = 0; i < 4; ++i) {
     timespec mi;
-    const uint64_t a = __rdtsc();
+    const uint64_t a = gil_tsc();
     clock_gettime(CLOCK_MONOTONIC, &mi);
-    const uint64_t b = __rdtsc();
+    const uint64_t b = gil_tsc();
     if (b - a < width) {
       width = b - a;
       t = a + (b - a) / 2;

@@ -14,18 +14,32 @@
 // instant than the last extrapolated value returns that value again. The TSC going backwards or
 // jumping (migration, suspend) reads as a huge tick count and re-anchors.
 //
-// Used only where the kernel itself uses the TSC (`current_clocksource` is `tsc`: invariant and
-// synchronised across CPUs); elsewhere, or with BEHOLDER_TSC_CLOCK=0, every read is a
-// clock_gettime. The state is one global guarded by the GIL: threads that run without the GIL (the
+// Used only on x86 where the kernel itself uses the TSC (`current_clocksource` is `tsc`: invariant
+// and synchronised across CPUs); elsewhere (other architectures included), or with
+// BEHOLDER_TSC_CLOCK=0, every read is a clock_gettime. The state is one global guarded by the GIL: threads that run without the GIL (the
 // ingest reader, the handshake reactor) keep calling mono_ns() (ring.hpp).
 #pragma once
 
 #include <time.h>
-#include <x86intrin.h>
 
 #include <cstdint>
 
+#if (defined(__x86_64__) || defined(__i386__)) && !defined(BEHOLDER_NO_TSC)
+#include <x86intrin.h>
+#define BEHOLDER_HAVE_TSC 1
+#else  // no TSC: mode 0 (clock_gettime on every read) is the only mode
+#define BEHOLDER_HAVE_TSC 0
+#endif
+
 namespace beholder {
+
+inline uint64_t gil_tsc() {
+#if BEHOLDER_HAVE_TSC
+  return __rdtsc();
+#else
+  return 0;
+#endif
+}
 
 struct GilClock {
   int mode = 0;            // 1 = TSC extrapolation, 0 = clock_gettime on every read
@@ -52,7 +66,7 @@ int64_t gil_clock_anchor(uint64_t tsc);  // the slow path: re-anchor, return CLO
 inline int64_t gil_mono_ns() {
   GilClock& c = g_gil_clock;
   if (c.mode == 1) {
-    const uint64_t t = __rdtsc();
+    const uint64_t t = gil_tsc();
     const uint64_t d = t - c.tsc0;
     if (d < c.span) {
       int64_t v = c.mono0 + int64_t(double(d) * c.ns_per_tick);

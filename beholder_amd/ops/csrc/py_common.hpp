@@ -4,6 +4,8 @@
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 
+#include <pthread.h>
+
 #include <cstdint>
 
 #include "histogram.hpp"
@@ -18,10 +20,23 @@ namespace beholder {
 // into a str or handed to a socket buffer before the code that built it returns. A ScratchStr lends
 // one of a few strings kept across events (cleared, capacity kept), so that text costs no heap
 // allocation per event; a nested lender (a js_str() that runs Python code that logs) takes the next
-// one, last in first out, and past kDepth a fresh local. GIL-held code only (one global pool).
+// one, last in first out, and past kDepth a fresh local.
+//
+// The pool belongs to one thread: the first that makes a ScratchStr (the event loop's, in the
+// service). Python code runs while a lent string is alive (a logger, a token callable, a __str__),
+// and it may hand the GIL to another thread; a ScratchStr made on any other thread is a fresh local,
+// so it never takes, or returns, a slot of the owner's stack.
 class ScratchStr {
  public:
-  ScratchStr() : s_(depth_ < kDepth ? &pool_[depth_++] : &own_) { s_->clear(); }
+  ScratchStr() : s_(&own_) {
+    const pthread_t me = pthread_self();
+    if (!owned_) {
+      owner_ = me;
+      owned_ = true;
+    }
+    if (depth_ < kDepth && pthread_equal(owner_, me)) s_ = &pool_[depth_++];
+    s_->clear();
+  }
   ~ScratchStr() {
     if (s_ == &own_) return;
     if (s_->capacity() > kKeepBytes) std::string().swap(*s_);  // an outsized one is not kept
@@ -36,6 +51,8 @@ class ScratchStr {
   static constexpr size_t kKeepBytes = 65536;
   static inline std::string pool_[kDepth];
   static inline int depth_ = 0;
+  static inline pthread_t owner_;
+  static inline bool owned_ = false;
   std::string own_;
   std::string* s_;
 };

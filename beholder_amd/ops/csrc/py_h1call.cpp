@@ -1138,6 +1138,23 @@ PyObject* h1_call_new(PyObject* client, PyObject* method, PyObject* url, PyObjec
 }
 
 // ---- NativeApi entries (native_api.hpp) -------------------------------------------------------
+// A caller's key_len (from h1_origin_key) fits `url` (ASCII): u[0..k) is "scheme://authority" with
+// a printable, non-empty authority and no '/', '?' or '#' in it, and u[k] (if any) starts the path,
+// query or fragment. A key_len taken for another URL fails this and the full check runs instead.
+bool origin_prefix_fits(PyObject* url, Py_ssize_t k) {
+  const Py_UCS1* u = PyUnicode_1BYTE_DATA(url);
+  const Py_ssize_t n = PyUnicode_GET_LENGTH(url);
+  if (k > n || (k < n && u[k] != '/' && u[k] != '?' && u[k] != '#')) return false;
+  Py_ssize_t i = 0;
+  while (i < k && u[i] != ':') ++i;
+  if (i == 0 || i + 3 >= k || u[i + 1] != '/' || u[i + 2] != '/') return false;
+  for (Py_ssize_t j = i + 3; j < k; ++j) {
+    const Py_UCS1 c = u[j];
+    if (c <= 0x20 || c >= 0x7f || c == '/' || c == '?' || c == '#') return false;
+  }
+  return true;
+}
+
 int api_h1_request_text(PyObject* method, PyObject* url, PyObject* params, PyObject* host, PyObject* auth,
                         PyObject* tail, PyObject* tail_cl0, std::string* req, PyObject** full, Py_ssize_t* key_len) {
   BEHOLDER_TRY {
@@ -1149,7 +1166,7 @@ int api_h1_request_text(PyObject* method, PyObject* url, PyObject* params, PyObj
     Py_ssize_t k = *key_len;
     const bool known = k > 0 && PyUnicode_CheckExact(method) && PyUnicode_IS_ASCII(method) &&
                        PyUnicode_CheckExact(url) && PyUnicode_IS_ASCII(url) && k <= PyUnicode_GET_LENGTH(url) &&
-                       (!params || PyDict_CheckExact(params));
+                       (!params || PyDict_CheckExact(params)) && origin_prefix_fits(url, k);
     if (!known && !split_shape(method, url, params, &k)) return 0;
     ScratchStr q_buf;
     std::string& q = *q_buf;

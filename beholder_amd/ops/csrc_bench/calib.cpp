@@ -1,9 +1,11 @@
 // Fixed-work calibration loops for the bench line (bench.py calib_*): how fast this core and
 // its caches are right now, independent of the service's code.
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "bench_common.hpp"
+#include "py_common.hpp"  // ScratchStr, BEHOLDER_TRY (header-only: this module keeps its own pool)
 
 namespace beholder {
 namespace bench {
@@ -89,7 +91,58 @@ PyObject* mod_calib_mem(PyObject*, PyObject* args) {
   return Py_BuildValue("(LK)", (long long)(t1 - t0), (unsigned long long)idx);
 }
 
+// scratch_probe(text, fn) -> str: a ScratchStr (py_common.hpp) holding `text`, then fn() (any
+// Python code: it may hand the GIL to other threads), then the ScratchStr's content, which nothing
+// else may have been lent meanwhile (tests/test_native_tools.py)
+PyObject* mod_scratch_probe(PyObject*, PyObject* args) {
+  const char* t;
+  Py_ssize_t n;
+  PyObject* fn;
+  if (!PyArg_ParseTuple(args, "s#O", &t, &n, &fn)) return nullptr;
+  BEHOLDER_TRY {
+    ScratchStr buf_;
+    std::string& buf = *buf_;
+    buf.assign(t, size_t(n));
+    PyObject* r = PyObject_CallNoArgs(fn);
+    if (!r) return nullptr;
+    Py_DECREF(r);
+    return PyUnicode_FromStringAndSize(buf.data(), Py_ssize_t(buf.size()));
+  }
+  BEHOLDER_CATCH(nullptr)
+}
+
+// request_text_probe(method, url, params, key_len) -> (rc, request bytes, full URL, key_len): the
+// _C_API's h1_request_text with Host "h", no Authorization and an empty tail (tests)
+PyObject* mod_request_text_probe(PyObject*, PyObject* args) {
+  PyObject *method, *url, *params;
+  Py_ssize_t k;
+  if (!PyArg_ParseTuple(args, "OOOn", &method, &url, &params, &k)) return nullptr;
+  BEHOLDER_TRY {
+    PyObject* host = PyUnicode_FromString("h");
+    PyObject* tail = PyBytes_FromString("\r\n");
+    if (!host || !tail) {
+      Py_XDECREF(host);
+      Py_XDECREF(tail);
+      return nullptr;
+    }
+    std::string req;
+    PyObject* full = nullptr;
+    const int rc = g_api->h1_request_text(method, url, params, host, Py_None, tail, tail, &req, &full, &k);
+    Py_DECREF(host);
+    Py_DECREF(tail);
+    if (rc < 0) return nullptr;
+    PyObject* out = Py_BuildValue("(iy#On)", rc, req.data(), Py_ssize_t(req.size()), full ? full : Py_None, k);
+    Py_XDECREF(full);
+    return out;
+  }
+  BEHOLDER_CATCH(nullptr)
+}
+
 PyMethodDef calib_methods[] = {
+    {"request_text_probe", mod_request_text_probe, METH_VARARGS,
+     "request_text_probe(method, url, params, key_len) -> (rc, request, full, key_len)"},
+    {"scratch_probe", mod_scratch_probe, METH_VARARGS,
+     "scratch_probe(text, fn) -> text as a scratch string holds it after fn() ran"},
     {"calib_mem", mod_calib_mem, METH_VARARGS,
      "calib_mem(bytes, steps) -> (ns, checksum): fixed-work dependent random walk over `bytes`"},
     {"calib", mod_calib, METH_VARARGS, "calib(iters) -> (ns, checksum): fixed-work CPU calibration loop"},

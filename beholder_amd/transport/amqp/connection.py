@@ -451,6 +451,8 @@ class Connection:
     def _write_now(self, data: bytes) -> None:
         """Append and send at once (with anything already queued, in order): the ack flush runs
         once per loop iteration already, so it need not wait for another one."""
+        if self._aborting:  # closing on purpose: a late write (an ack) is dropped, not a loss
+            return
         t = self._transport
         if not self._wbuf and t is not None and not t.is_closing():  # nothing queued: no copy
             try:
@@ -469,6 +471,9 @@ class Connection:
         self._flush_scheduled = False
         t = self._transport
         if not self._wbuf or t is None:
+            return
+        if self._aborting:  # the transport is being closed on purpose (_abort): not a loss
+            self._wbuf.clear()
             return
         if t.is_closing():
             self._wbuf.clear()
@@ -629,7 +634,7 @@ class Connection:
                 pass
         if self._hb_task is not None:
             self._hb_task.cancel()
-        if not self._lost_reported and (was_open or err is not None):
+        if not self._lost_reported and not self._aborting and (was_open or err is not None):
             self._lost_reported = True
             if self.on_lost is not None:
                 self.on_lost(err)

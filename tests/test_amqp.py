@@ -464,3 +464,26 @@ def test_protocol_write_backpressure_and_loss_wake_the_publisher():
         return blocked, c.lost is err, p.closed.done(), c.data
     blocked, lost, closed, data = asyncio.run(go())
     assert blocked and lost and closed and data == [b"x"]
+
+
+def test_a_write_while_closing_on_purpose_is_not_a_loss():
+    """an ack flushed in _abort's window (the transport already closing on purpose,
+    ``_aborting`` set) is dropped; it must not reach ``on_lost`` as a connection loss (AmqpSource
+    guards itself, but any other on_lost user would take a clean close for a failure)."""
+    async def go():
+        b = await AmqpBroker().start()
+        try:
+            lost = []
+            c = Connection(b.url, on_lost=lost.append)
+            await c.open()
+            await c.channel()
+            t = c._transport
+            c._aborting = True  # what _abort sets right before it closes the transport
+            t.close()
+            c._write_now(b"\x01" * 21)  # an ack frame's size: the direct path
+            c._write(b"\x01" * 21)      # and the scheduled flush
+            await asyncio.sleep(0.05)  # the scheduled flush and the transport's connection_lost ran
+            return list(lost)
+        finally:
+            await b.stop()
+    assert run(go()) == []

@@ -3,6 +3,7 @@ from the TSC between anchors where the kernel's clocksource is the TSC. Every va
 between two time.monotonic_ns() reads around it (within a tolerance for a preempted test
 process), never go backwards, stay right across idle gaps longer than an anchor interval, and
 give Date.now()-compatible milliseconds for log lines; BEHOLDER_TSC_CLOCK=0 turns it off."""
+import os
 import time
 
 import pytest
@@ -65,3 +66,23 @@ def test_env_turns_it_off(clock, monkeypatch):
     m.gil_clock_reset()
     assert m.gil_clock_info()["mode"] == "clock_gettime"
     assert _check(5_000) == 0
+
+
+def test_builds_without_a_tsc():
+    """Off x86: no <x86intrin.h>, no rdtsc, mode 0 only. BEHOLDER_NO_TSC takes the
+    path other architectures take; the clock's translation unit must compile on it."""
+    import shutil
+    import subprocess
+    import sysconfig
+
+    from beholder_amd import _build
+    cxx = shutil.which("g++") or shutil.which("c++")
+    if cxx is None:
+        pytest.skip("no C++ compiler")
+    src = os.path.join(_build.CSRC, "gil_clock.cpp")
+    r = subprocess.run([cxx, "-std=c++17", "-fsyntax-only", "-DBEHOLDER_NO_TSC", f"-I{_build.CSRC}",
+                        f"-I{sysconfig.get_paths()['include']}", src], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    with open(os.path.join(_build.CSRC, "gil_clock.hpp")) as f:
+        text = f.read()
+    assert "#include <x86intrin.h>" in text.split("#else")[0] and "BEHOLDER_HAVE_TSC 0" in text

@@ -153,3 +153,43 @@ def test_recording_client_exposes_a_sink_hook_capsule():
     assert type(c.native_record).__name__ == "PyCapsule" and "beholder_amd.sink_hook" in repr(c.native_record)
     with pytest.raises(ValueError):
         RecordingHttpClient(stub="nope")
+
+
+def test_scratch_strings_stay_with_the_owner_thread():
+    """ScratchStr (py_common.hpp) lends strings of one pool, last in first out. Python
+    code runs while a string is lent and may let another thread run: that thread's scratch string
+    must not be a pool slot, or the owner, returning its own slot and lending it again, would
+    overwrite the other thread's text while that thread still builds it."""
+    f = native.native_bench.scratch_probe
+    entered, release = threading.Event(), threading.Event()
+    out = {}
+
+    def other_thread():
+        out["b"] = f("bbbb", lambda: (entered.set(), release.wait(10)))
+
+    def start_other():  # runs while this thread's "aaaa" is lent
+        out["t"] = threading.Thread(target=other_thread)
+        out["t"].start()
+        assert entered.wait(10)
+
+    out["a"] = f("aaaa", start_other)
+    out["c"] = f("cccc", lambda: None)  # this thread again, while the other one's string is lent
+    release.set()
+    out["t"].join(10)
+    assert (out["a"], out["b"], out["c"]) == ("aaaa", "bbbb", "cccc")
+
+
+def test_request_text_does_not_trust_a_key_len_that_does_not_fit():
+    """_C_API h1_request_text: a caller's key_len is trusted (the shape scan skipped)
+    only when u[0..k) is the URL's "scheme://authority"; any other value gets the full check,
+    so it builds the same request as no key_len at all, or refuses the URL as the H1 client would."""
+    f = native.native_bench.request_text_probe
+    url = "https://api.trello.com/1/cards/c1"
+    want = f("PUT", url, {"pos": "2"}, 0)
+    assert want[0] == 1 and want[3] == len("https://api.trello.com")
+    for k in (1, 5, 8, 9, 21, 23, 30, len(url), len(url) + 4):
+        assert f("PUT", url, {"pos": "2"}, k) == want, k
+    assert f("PUT", url, {"pos": "2"}, want[3]) == want
+    for bad in ("https://api.trello.com/1/cards#frag", "https://api.trello.com/a\x01b", "https://api.trello.com/a b"):
+        assert f("GET", bad, None, 0)[0] == 0, bad
+        assert f("GET", bad, None, 3)[0] == 0, bad  # a wrong key_len: scanned, refused

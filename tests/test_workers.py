@@ -247,19 +247,21 @@ def test_shared_queue_two_workers_ack_every_event_exactly_once(broker):
     assert r["events_per_sec"] > 0 and r["broker_cpu_us_per_event"] > 0
 
 
-def test_worker_command_reruns_the_entry_module(monkeypatch):
-    """Workers re-run the module the supervisor was started with, so a wrapper entry (the bench's
-    shared_worker) stays in force in every worker."""
+def test_worker_command_is_the_service_unless_a_wrapper_opts_in(monkeypatch):
+    """Workers run ``python -m beholder_amd`` whatever module hosts the supervisor (a
+    launcher or test runner must not be restarted in its place); a wrapper entry that must be in
+    force in every worker (the bench's shared_worker) names itself in BEHOLDER_WORKER_MODULE."""
     import types
 
     from beholder_amd import cli
     fake = types.ModuleType("__main__")
-    fake.__spec__ = types.SimpleNamespace(name="beholder_amd.bench.shared_worker")
+    fake.__spec__ = types.SimpleNamespace(name="some.launcher")
     monkeypatch.setitem(sys.modules, "__main__", fake)
-    assert cli.worker_command() == [sys.executable, "-m", "beholder_amd.bench.shared_worker"]
-    fake.__spec__ = types.SimpleNamespace(name="beholder_amd.__main__")
+    monkeypatch.delenv(cli.WORKER_MODULE_ENV, raising=False)
     assert cli.worker_command() == [sys.executable, "-m", "beholder_amd"]
-    fake.__spec__ = None
+    monkeypatch.setenv(cli.WORKER_MODULE_ENV, "beholder_amd.bench.shared_worker")
+    assert cli.worker_command() == [sys.executable, "-m", "beholder_amd.bench.shared_worker"]
+    monkeypatch.setenv(cli.WORKER_MODULE_ENV, " ")
     assert cli.worker_command() == [sys.executable, "-m", "beholder_amd"]
 
 
