@@ -724,7 +724,6 @@ PyObject* iof_iternext(IOFutureObject* f) {
 }
 
 PyObject* iof_send(IOFutureObject* f, PyObject*) { return iof_iternext(f); }
-PyObject* iof_await_method(IOFutureObject* f, PyObject*) { return iof_await(f); }
 
 PyObject* iof_throw(IOFutureObject*, PyObject* args) {
   PyObject *t, *v = nullptr, *tb = nullptr;
@@ -759,7 +758,6 @@ PyMethodDef iof_methods[] = {
     {"_make_cancelled_error", reinterpret_cast<PyCFunction>(iof_make_cancelled_error), METH_NOARGS, nullptr},
     {"send", reinterpret_cast<PyCFunction>(iof_send), METH_O, nullptr},
     {"throw", reinterpret_cast<PyCFunction>(iof_throw), METH_VARARGS, nullptr},
-    {"__await__", reinterpret_cast<PyCFunction>(iof_await_method), METH_NOARGS, nullptr},
     {nullptr, nullptr, 0, nullptr}};
 
 PyGetSetDef iof_getset[] = {
@@ -1063,6 +1061,5 @@ int iofuture_reject(PyObject* f, PyObject* exc) {
   return 0;
 }
 
-bool is_iofuture(PyObject* o) { return Py_TYPE(o) == &IOFutureType; }
 
 }  // namespace beholder

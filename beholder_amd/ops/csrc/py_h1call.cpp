@@ -45,7 +45,6 @@
 namespace beholder {
 
 PyObject* iofuture_new(PyObject* loop);
-bool is_iofuture(PyObject* o);
 int iofuture_peek(PyObject* f, PyObject** result);
 PyObject* iofuture_yield(PyObject* f);
 bool is_netconn(PyObject* o);

@@ -1266,10 +1266,6 @@ PySendResult step_status(CallObject* c, PyObject* value, PyObject** result) {
       if (k == 1) Py_DECREF(v);
       goto emby;
     }
-    case 4:  // (unused since the hooks run here; kept for the numbering in the header comment)
-      if (!value) goto hooks_catch;
-      Py_DECREF(value);
-      return finish_ack(c, result);
     case 5:
       value = request_finish(c, value);
       if (!value) goto hooks_catch;

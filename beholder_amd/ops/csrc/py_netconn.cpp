@@ -250,7 +250,7 @@ void hs_fail(NetConnObject* c, PyObject* exc) {
 
 // owner.<name>(arg) for a rare path; the error (if any) is reported, never propagated into the loop
 void notify(NetConnObject* c, PyObject* name, PyObject* arg) {
-  if (!c->owner) return;
+  if (!c->owner || c->owner == Py_None) return;  // owner None: nobody to tell
   PyObject* r = PyObject_CallMethodOneArg(c->owner, name, arg ? arg : Py_None);
   if (!r) {
     PyErr_WriteUnraisable(c->owner);
@@ -659,9 +659,9 @@ void on_pg_data(NetConnObject* c, const char* data, size_t len) {
   for (Py_ssize_t i = 0; i < n; ++i) {
     PyObject* it = PyList_GET_ITEM(items, i);
     if (PyTuple_GET_SIZE(it) != 4) {  // NoticeResponse / ParameterStatus / ...
-      PyObject* r = c->owner ? PyObject_CallMethodObjArgs(c->owner, s_net_message, PyTuple_GET_ITEM(it, 0),
-                                                          PyTuple_GET_ITEM(it, 1), nullptr)
-                             : (Py_INCREF(Py_None), Py_None);
+      if (!c->owner || c->owner == Py_None) continue;  // nobody to tell
+      PyObject* r = PyObject_CallMethodObjArgs(c->owner, s_net_message, PyTuple_GET_ITEM(it, 0),
+                                               PyTuple_GET_ITEM(it, 1), nullptr);
       if (!r) PyErr_WriteUnraisable(c->owner);
       Py_XDECREF(r);
       continue;
@@ -800,7 +800,8 @@ PyObject* nc_on_writable(NetConnObject* c, PyObject*);
 PyObject* nc_flush(NetConnObject* c, PyObject*);
 
 // NetConn(fd, loop, kind, owner, parser, stmts=None, pg_error=None, closed_exc=ConnectionError):
-// takes ownership of fd (a connected TCP socket) and starts watching it.
+// takes ownership of fd (a connected TCP socket) and starts watching it. `owner` gets the
+// _net_lost / _net_error / _net_message calls (None: nobody is told; a reply future still ends).
 int nc_init(NetConnObject* c, PyObject* args, PyObject* kwds) {
   static const char* kwlist[] = {"fd",        "loop", "kind",       "owner",     "parser", "stmts", "pg_error",
                                  "closed_exc", "tls",  "server_hostname", "port", "tls_error", nullptr};

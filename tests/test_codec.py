@@ -132,6 +132,21 @@ def test_all_scalar_kinds_against_upb():
     for k, v in vals.items():
         assert getattr(dec, k) == v, k
     assert codec.encode(vals) == upb
+    # the reference's reader (protobufjs 6.8.8 dialect, ops/csrc/pbjs.hpp) reads the kinds it models
+    # alike: length-delimited bytes, fixed32 / float, fixed64 / double (64-bit integers it refuses)
+    with pytest.raises(ValueError, match="64-bit integer"):
+        MessageCodec("t.All", field_table(desc), "protobufjs")
+    keep = [f for f in field_table(desc) if f[1] in ("s", "b", "i32", "u32", "s32", "bo", "e", "f", "d", "f32", "sf32")]
+    pbjs = MessageCodec("t.All", keep, "protobufjs")
+    assert pbjs.dialect == "protobufjs" and pbjs.type_name == "t.All" and codec.type_name == "t.All"
+    small = {k: vals[k] for k in ("s", "b", "i32", "u32", "s32", "bo", "e", "f", "d", "f32", "sf32")}
+    data = cls(**small).SerializeToString()
+    dec = pbjs.decode(data)
+    for k, v in small.items():
+        assert getattr(dec, k) == v, k
+    for bad in (b"\x6d\x01\x02", b"\x61\x01\x02\x03", b"\x12\x05ab"):  # fixed32 / double / bytes cut short
+        with pytest.raises(Exception):
+            pbjs.decode(bad)
 
 
 # ------------------------------------------------------------- fuzzing ----

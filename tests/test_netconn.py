@@ -15,6 +15,7 @@ import pytest
 
 import test_h1
 import test_stores
+import test_tls
 from beholder_amd.ops import H1Parser, IOFuture
 from beholder_amd.sinks import H1Client
 from beholder_amd.store.pgwire import PgConnection
@@ -42,6 +43,67 @@ ASYNCIO_PATH = ([f for f in _no_arg_tests(test_h1, "test_")
 def test_asyncio_transport_path(fn, monkeypatch):
     monkeypatch.setenv("BEHOLDER_NATIVE_IO", "0")
     fn()
+
+
+class _NoPollerLoop(asyncio.SelectorEventLoop):
+    """A loop that cannot hold the NetPoller (as a loop type without an instance dict): each
+    NetConn then registers its own socket with loop.add_reader / add_writer and runs its TLS
+    handshake on the loop (py_netpoll.cpp netpoll_for, py_netconn.cpp tls_start)."""
+
+    def __setattr__(self, name, value):
+        if name == "_beholder_netpoller":
+            raise AttributeError(name)
+        super().__setattr__(name, value)
+
+
+class _NoPollerPolicy(asyncio.DefaultEventLoopPolicy):
+    def new_event_loop(self):
+        return _NoPollerLoop()
+
+
+# (the TLS tests of the handshake threads need a NetPoller to take the socket out of)
+PER_SOCKET_PATH = ASYNCIO_PATH + [f for f in _no_arg_tests(test_tls, "test_")
+                                  if "reactor" not in f.__name__ and "handshake_threads" not in f.__name__
+                                  and "churn" not in f.__name__]
+
+
+@pytest.mark.parametrize("fn", PER_SOCKET_PATH, ids=[f"{f.__module__}.{f.__name__}" for f in PER_SOCKET_PATH])
+def test_per_socket_reader_path(fn):
+    """The network tests of both clients and the TLS suite, on loops with no NetPoller."""
+    if not netconn.enabled():
+        pytest.skip("BEHOLDER_NATIVE_IO=0")
+    old = asyncio.get_event_loop_policy()
+    asyncio.set_event_loop_policy(_NoPollerPolicy())
+    try:
+        fn()
+    finally:
+        asyncio.set_event_loop_policy(old)
+
+
+def test_per_socket_readers_register_each_socket_with_the_loop():
+    """Without a NetPoller every NetConn's fd is in the loop's selector itself, and leaves it on close."""
+    if not netconn.enabled():
+        pytest.skip("BEHOLDER_NATIVE_IO=0")
+
+    async def go():
+        loop = asyncio.get_running_loop()
+        s = await test_h1.Scripted(lambda n, m, t, h: test_h1.OK).start()
+        try:
+            c = H1Client(timeout_s=5)
+            await asyncio.gather(*[c.request("GET", f"http://127.0.0.1:{s.port}/{i}") for i in range(3)])
+            fds = {conn.net.fd for o in c._origins.values() for conn in o.idle}
+            registered = set(loop._selector.get_map())
+            out = (hasattr(loop, "_beholder_netpoller"), bool(fds) and fds <= registered)
+            await c.close()
+            return out + (bool(fds & set(loop._selector.get_map())),)
+        finally:
+            await s.stop()
+    old = asyncio.get_event_loop_policy()
+    asyncio.set_event_loop_policy(_NoPollerPolicy())
+    try:
+        assert run(go()) == (False, True, False)
+    finally:
+        asyncio.set_event_loop_policy(old)
 
 
 def test_both_clients_adopt_plain_tcp_connections():

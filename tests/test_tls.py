@@ -737,3 +737,33 @@ def test_peer_reset_during_offloaded_handshakes_fails_them_promptly():
     res, took, left = run(go())
     assert all(isinstance(x, HttpError) for x in res), res
     assert took < 2.0 and left == 0
+
+
+def test_tls_after_fork_starts_fresh_handshake_threads(tmp_path):
+    """A process that forks after its TLS handshakes ran on the handshake threads (the supervisor's
+    workers are spawned, but a library user may fork): the child has none of those threads, so the
+    atfork handler drops the reactor (py_netconn.cpp hs_after_fork_child) and the child's first
+    handshake starts new ones. Both processes complete their HTTPS requests."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "fork_tls.py"
+    script.write_text(
+        "import asyncio, os, sys\n"
+        f"sys.path[:0] = [{root!r}, {os.path.join(root, 'tests')!r}]\n"
+        "from test_tls import TlsServer, ok, TLS_CERT\n"
+        "from beholder_amd.sinks import H1Client\n"
+        "async def once():\n"
+        "    srv = await TlsServer(lambda t: ok()).start()\n"
+        "    c = H1Client(timeout_s=5, ssl_cafile=TLS_CERT)\n"
+        "    rs = await asyncio.gather(*[c.request('GET', f'https://127.0.0.1:{srv.port}/a') for _ in range(4)])\n"
+        "    await c.close()\n"
+        "    await srv.stop()\n"
+        "    return all(r.status == 200 for r in rs)\n"
+        "assert asyncio.run(once())\n"
+        "pid = os.fork()\n"
+        "if pid == 0:\n"
+        "    sys.exit(0 if asyncio.run(once()) else 3)\n"
+        "_, st = os.waitpid(pid, 0)\n"
+        "sys.exit(os.waitstatus_to_exitcode(st) or (0 if asyncio.run(once()) else 4))\n")
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
