@@ -573,7 +573,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = Fal
             t_init = time.perf_counter()
             await svc.init()  # connects to the broker and PG; preconnect opens the sink connections
             out["init_ms"] = round((time.perf_counter() - t_init) * 1e3, 2)
-            mon = StallMonitor().start()
+            mon = StallMonitor(work=lambda: _settled(src.settler)).start()
             src.settler.trace_slow(SLOW_TRACE_NS)
             cg0 = cgroup_cpu_stat()
             task = asyncio.ensure_future(svc.run())

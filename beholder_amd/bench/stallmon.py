@@ -21,16 +21,25 @@ import asyncio
 import gc
 import json
 import time
-from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, Iterable, List, Optional, Sequence, Tuple
 
 Interval = Tuple[int, int]
 
 
 class StallMonitor:
-    def __init__(self, period_s: float = 0.001, threshold_us: float = 1000.0, max_events: int = 20000):
+    """``work``: a cheap callable returning a running count of the process's work (the consumer's
+    settled deliveries). Each loop stall then records how much work the loop did inside it
+    (``stall_work``: [stall us, work done]): a stall that settled hundreds of deliveries was one
+    long callback working through a batch, one that settled none was the loop blocked or the
+    process descheduled."""
+
+    def __init__(self, period_s: float = 0.001, threshold_us: float = 1000.0, max_events: int = 20000,
+                 work: Optional[Callable[[], int]] = None):
         self.period_ns = int(period_s * 1e9)
         self.threshold_ns = int(threshold_us * 1e3)
         self.max_events = max_events
+        self.work = work
+        self.stall_work: List[Tuple[float, int]] = []
         self.loop_stalls: List[Interval] = []
         self.gc_pauses: List[Interval] = []
         self.lags_ns: List[int] = []  # every measured lateness (bounded by the run length / period)
@@ -60,8 +69,10 @@ class StallMonitor:
     async def _run(self) -> None:
         period = self.period_ns / 1e9
         mono = time.monotonic_ns
+        work = self.work
         while True:
             due = mono() + self.period_ns
+            w0 = work() if work is not None else 0
             await asyncio.sleep(period)
             now = mono()
             lag = now - due
@@ -71,6 +82,8 @@ class StallMonitor:
                 self.lags_ns.append(lag)
             if lag >= self.threshold_ns:
                 self._add(self.loop_stalls, (due, now))
+                if work is not None and len(self.stall_work) < 1000:
+                    self.stall_work.append((round(lag / 1e3, 1), work() - w0))
 
     def start(self, loop: Optional[asyncio.AbstractEventLoop] = None) -> "StallMonitor":
         loop = loop or asyncio.get_event_loop()
@@ -84,6 +97,7 @@ class StallMonitor:
         self.gc_pauses.clear()
         self.lags_ns.clear()
         self.gc_pause_ns.clear()
+        self.stall_work.clear()
         self.dropped = 0
 
     def stop(self) -> None:
@@ -110,6 +124,8 @@ class StallMonitor:
             "gc_pauses": len(self.gc_pause_ns),
             "gc_max_pause_us": round(max(self.gc_pause_ns) / 1e3, 1) if self.gc_pause_ns else None,
             "gc_stalls": len(self.gc_pauses),
+            # the longest stalls with the work done inside each ([stall us, work], see the class)
+            "stall_work": sorted(self.stall_work, reverse=True)[:5] if self.work is not None else None,
         }
 
     def dump(self) -> Dict[str, object]:

@@ -415,6 +415,8 @@ def _attr_keys(prefix: str, att: dict) -> dict:
     out[f"{prefix}_consumer_loop_lag_max_us"] = c.get("loop_lag_max_us")
     out[f"{prefix}_consumer_loop_stalls"] = c.get("loop_stalls")
     out[f"{prefix}_consumer_gc_max_pause_us"] = c.get("gc_max_pause_us")
+    # the consumer's longest loop stalls: [stall us, deliveries settled inside it] (bench/stallmon.py)
+    out[f"{prefix}_consumer_stall_work"] = c.get("stall_work")
     fakes = {k: v for k, v in procs.items() if k != "consumer"}
     out[f"{prefix}_fakes_loop_lag_max_us"] = {k: v.get("loop_lag_max_us") for k, v in fakes.items()}
     out[f"{prefix}_fakes_gc_max_pause_us"] = max([v.get("gc_max_pause_us") or 0 for v in fakes.values()] or [0])
@@ -830,7 +832,8 @@ DIAG_FIRST = (
     "tcp_e2e_host_cpu_busy_pct", "tcp_e2e_nr_throttled", "tcp_e2e_measured_events", "tcp_e2e_slow_blamed",
     "tcp_e2e_runs", "tls_e2e_runs",
     "tls_e2e_calib_ns", "tls_e2e_sys_cpu_us_per_event", "tls_e2e_minflt", "tls_e2e_nivcsw",
-    "tls_e2e_fakes_cpu_us_per_event", "tls_e2e_host_cpu_busy_pct", "tls_e2e_slow_blamed",
+    "tls_e2e_fakes_cpu_us_per_event", "tls_e2e_host_cpu_busy_pct", "tls_e2e_slow_blamed", "tls_e2e_consumer_stall_work",
+    "tcp_e2e_consumer_stall_work",
     "headline_minflt", "headline_run_delay_ms", "headline_timed_pump_run_delay_ms",
     "headline_timed_proc_run_delay_ms", "involuntary_ctx_switches", "headline_host_cpu_busy_pct",
     "tcp_e2e_rate_1k_events_per_sec", "tcp_e2e_rate_10k_events_per_sec", "tcp_e2e_rate_100k_events_per_sec",

@@ -80,3 +80,28 @@ def test_a_long_stall_that_began_well_before_the_delivery_is_still_seen():
     out = attribute(slow, {"pg": [stall], "http": [(start + 4_000_000, start + 4_100_000)]})
     assert out["blamed"]["pg"] == 1 and out["blamed"]["none"] == 0
     assert out["time_share"]["pg"] == 1.0
+
+
+def test_a_stall_records_the_work_done_inside_it():
+    """``work``: each stall says how much work the loop did while its timer was late, so a long
+    callback working through a batch (work > 0) is told apart from a loop that was blocked or not
+    scheduled (work 0)."""
+    import time as _time
+
+    from beholder_amd.bench.stallmon import StallMonitor
+    done = [0]
+
+    async def go():
+        mon = StallMonitor(work=lambda: done[0]).start(asyncio.get_running_loop())
+        await asyncio.sleep(0.01)
+        for _ in range(300):  # one 6 ms callback that does 300 units of work
+            _time.sleep(0.00002)
+            done[0] += 1
+        await asyncio.sleep(0.01)
+        _time.sleep(0.006)  # one that does none
+        await asyncio.sleep(0.01)
+        mon.stop()
+        return mon.summary()["stall_work"]
+    work = asyncio.run(go())
+    assert any(w == 300 for _, w in work) and any(w == 0 for _, w in work), work
+    assert all(us >= 1000 for us, _ in work)
