@@ -31,11 +31,11 @@ struct NativeApi {
   // `auth` (str, or None): "M target?query HTTP/1.1\r\nHost: ...\r\n[Authorization: ...\r\n]" then
   // `tail` (bytes; `tail_cl0` for methods with a body). *full = the URL with its query (new
   // reference). *key_len = length of "scheme://authority" in `url`; a caller that has it from
-  // h1_origin_key for the same (method, url, params) passes it in (> 0) and the byte scan of the
-  // shape check is not repeated, as the H1 client's own path checks once. A key_len that does not
-  // fit `url` (u[0..k) not "scheme://authority", or u[k] not '/', '?', '#' or the end) is not
-  // trusted: the full check runs. 1 = built, 0 = not the shape the native path sends (the Python
-  // client would take it), -1 = error.
+  // h1_origin_key for the same (method, url, params) objects, as its very next API call, passes
+  // it in (> 0) and the byte scan of the shape check is not repeated, as the H1 client's own path
+  // checks once. Any other key_len (another URL's, or one passed later) is not trusted: the full
+  // check runs. 1 = built, 0 = not the shape the native path sends (the Python client would take
+  // it), -1 = error.
   int (*h1_request_text)(PyObject* method, PyObject* url, PyObject* params, PyObject* host, PyObject* auth,
                          PyObject* tail, PyObject* tail_cl0, std::string* req, PyObject** full,
                          Py_ssize_t* key_len);

@@ -1137,22 +1137,18 @@ PyObject* h1_call_new(PyObject* client, PyObject* method, PyObject* url, PyObjec
 }
 
 // ---- NativeApi entries (native_api.hpp) -------------------------------------------------------
-// A caller's key_len (from h1_origin_key) fits `url` (ASCII): u[0..k) is "scheme://authority" with
-// a printable, non-empty authority and no '/', '?' or '#' in it, and u[k] (if any) starts the path,
-// query or fragment. A key_len taken for another URL fails this and the full check runs instead.
-bool origin_prefix_fits(PyObject* url, Py_ssize_t k) {
-  const Py_UCS1* u = PyUnicode_1BYTE_DATA(url);
-  const Py_ssize_t n = PyUnicode_GET_LENGTH(url);
-  if (k > n || (k < n && u[k] != '/' && u[k] != '?' && u[k] != '#')) return false;
-  Py_ssize_t i = 0;
-  while (i < k && u[i] != ':') ++i;
-  if (i == 0 || i + 3 >= k || u[i + 1] != '/' || u[i + 2] != '/') return false;
-  for (Py_ssize_t j = i + 3; j < k; ++j) {
-    const Py_UCS1 c = u[j];
-    if (c <= 0x20 || c >= 0x7f || c == '/' || c == '?' || c == '#') return false;
-  }
-  return true;
-}
+// The arguments of the last h1_origin_key call that passed the shape check (GIL-held, like every
+// API entry). h1_request_text trusts a caller's key_len only for those very objects (the caller
+// that asked h1_origin_key and builds the request next, the stub's order); any other key_len, or
+// the same URL after another check, gets the full check (a key_len taken for another
+// URL must not build a malformed request line). One use: the next request_text clears it.
+struct LastKey {
+  PyObject* method;  // borrowed identities, compared, never dereferenced
+  PyObject* url;
+  PyObject* params;
+  Py_ssize_t len;
+  Py_ssize_t k;
+} g_last_key = {nullptr, nullptr, nullptr, 0, 0};
 
 int api_h1_request_text(PyObject* method, PyObject* url, PyObject* params, PyObject* host, PyObject* auth,
                         PyObject* tail, PyObject* tail_cl0, std::string* req, PyObject** full, Py_ssize_t* key_len) {
@@ -1163,9 +1159,10 @@ int api_h1_request_text(PyObject* method, PyObject* url, PyObject* params, PyObj
       return -1;
     }
     Py_ssize_t k = *key_len;
-    const bool known = k > 0 && PyUnicode_CheckExact(method) && PyUnicode_IS_ASCII(method) &&
-                       PyUnicode_CheckExact(url) && PyUnicode_IS_ASCII(url) && k <= PyUnicode_GET_LENGTH(url) &&
-                       (!params || PyDict_CheckExact(params)) && origin_prefix_fits(url, k);
+    const LastKey last = g_last_key;
+    g_last_key.url = nullptr;
+    const bool known = k > 0 && last.url == url && last.method == method && last.params == params &&
+                       last.k == k && PyUnicode_CheckExact(url) && PyUnicode_GET_LENGTH(url) == last.len;
     if (!known && !split_shape(method, url, params, &k)) return 0;
     ScratchStr q_buf;
     std::string& q = *q_buf;
@@ -1184,7 +1181,13 @@ PyTypeObject* h1_response_type() { return g.resp.type; }
 PyObject* h1_response_status(PyObject* resp) { return g.resp.get(resp, R_STATUS); }
 
 int api_h1_origin_key(PyObject* method, PyObject* url, PyObject* params, Py_ssize_t* key_len) {
-  return split_shape(method, url, params == Py_None ? nullptr : params, key_len) ? 1 : 0;
+  if (params == Py_None) params = nullptr;
+  if (!split_shape(method, url, params, key_len)) {
+    g_last_key.url = nullptr;
+    return 0;
+  }
+  g_last_key = {method, url, params, PyUnicode_GET_LENGTH(url), *key_len};
+  return 1;
 }
 
 PyObject* api_h1_response(PyObject* parsed, PyObject* full) {

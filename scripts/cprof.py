@@ -8,7 +8,7 @@ their symbol tables (``nm``: our extension's full table, the interpreter's expor
 Prints the top functions by self samples, and the split by object.
 
     python scripts/cprof.py [--steps 20] [--hz 2000] [--top 60] [--tid main|all]
-    python scripts/cprof.py --workload tcp_e2e|tls_e2e [--events 200000]   # the production-shaped path
+    python scripts/cprof.py --workload tcp_e2e|tls_e2e [--events 200000] [--rate 10000]   # the production-shaped path
     python scripts/cprof.py ... --depth 24 [--focus send,recv]   # + inclusive cost and callers
 """
 from __future__ import annotations
@@ -107,6 +107,8 @@ def main(argv=None) -> int:
     ap.add_argument("--tid", default="main", choices=["main", "all"])
     ap.add_argument("--workload", default="headline", choices=["headline", "tcp_e2e", "tls_e2e"])
     ap.add_argument("--events", type=int, default=200_000, help="tcp_e2e / tls_e2e events")
+    ap.add_argument("--rate", type=float, default=0.0,
+                    help="tcp_e2e / tls_e2e: the broker paces its sends at this many events/s (0 = saturation)")
     ap.add_argument("--depth", type=int, default=0,
                     help="also unwind this many frames per sample: inclusive cost per function and each "
                          "top leaf's callers")
@@ -132,7 +134,7 @@ def main(argv=None) -> int:
     else:
         from beholder_amd.bench import harness
         tls = a.workload == "tls_e2e"
-        x = harness._tcp_e2e(a.events, http_servers=4 if tls else 2, tls=tls, hooks=(go, stop))
+        x = harness._tcp_e2e(a.events, http_servers=4 if tls else 2, tls=tls, hooks=(go, stop), rate=a.rate)
         r = {"events": x["measured_events"], "elapsed": x["elapsed_s"],
              "cpu_s": x["cpu_us_per_event"] * x["measured_events"] / 1e6}
     mp = maps()
