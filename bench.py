@@ -273,10 +273,11 @@ async def run_consumer(a, seed: int, go, stop=None, *, steps: int = None, warmup
 
     t0 = 0.0
     ru0 = None
-    rq0 = pq0 = rq1 = pq1 = None
+    rq0 = pq0 = rq1 = pq1 = rqg = None
     for i in range(total_steps):
         if i == warmup:
             settler.reset_latency()
+            rqg = thread_run_delay_ns()
             go()
             t0 = time.perf_counter()
             ru0 = resource.getrusage(resource.RUSAGE_SELF)
@@ -314,6 +315,8 @@ async def run_consumer(a, seed: int, go, stop=None, *, steps: int = None, warmup
         "minflt": ru1.ru_minflt - ru0.ru_minflt if ru0 else 0,
         "majflt": ru1.ru_majflt - ru0.ru_majflt if ru0 else 0,
         "timed_run_delay_ms": (rq1 - rq0) / 1e6 if rq0 is not None and rq1 is not None else None,
+        # ... and inside go() itself (the first device synchronize: HIP's initialisation, its threads)
+        "go_run_delay_ms": (rq0 - rqg) / 1e6 if rq0 is not None and rqg is not None else None,
         "timed_proc_run_delay_ms": (pq1 - pq0) / 1e6 if pq0 is not None and pq1 is not None else None,
         "timed_pump_run_delay_ms": pump_delay[0] / 1e6 if pump_delay[1] and steps else None,
     }
@@ -834,7 +837,7 @@ DIAG_FIRST = (
     "tls_e2e_calib_ns", "tls_e2e_sys_cpu_us_per_event", "tls_e2e_minflt", "tls_e2e_nivcsw",
     "tls_e2e_fakes_cpu_us_per_event", "tls_e2e_host_cpu_busy_pct", "tls_e2e_slow_blamed", "tls_e2e_consumer_stall_work",
     "tcp_e2e_consumer_stall_work",
-    "headline_minflt", "headline_run_delay_ms", "headline_timed_pump_run_delay_ms",
+    "headline_minflt", "headline_run_delay_ms", "headline_go_run_delay_ms", "headline_timed_pump_run_delay_ms",
     "headline_timed_proc_run_delay_ms", "involuntary_ctx_switches", "headline_host_cpu_busy_pct",
     "tcp_e2e_rate_1k_events_per_sec", "tcp_e2e_rate_10k_events_per_sec", "tcp_e2e_rate_100k_events_per_sec",
     "tcp_e2e_rate_10k_cpu_us_per_event", "tcp_e2e_rate_10k_broker_late_p99_us",
@@ -937,7 +940,8 @@ def main(argv=None) -> int:
     elapsed = dist.max(res["elapsed"])
     parts = dist.gather({k: res[k] for k in ("handle_hist", "ingest_hist", "http_calls", "errors", "abandoned",
                                              "events", "cpu_s", "nivcsw", "minflt", "majflt", "timed_run_delay_ms",
-                                             "timed_proc_run_delay_ms", "timed_pump_run_delay_ms")})
+                                             "timed_proc_run_delay_ms", "timed_pump_run_delay_ms",
+                                             "go_run_delay_ms")})
     calibs = dist.gather((calib0, calib1))
     # the loop thread's time runnable without a CPU over the headline (warm-up steps included); the
     # process total would also hold the reader thread's many short wake-up waits
@@ -998,6 +1002,7 @@ def main(argv=None) -> int:
             "headline_timed_run_delay_ms": _max_or_none(p["timed_run_delay_ms"] for p in parts),
             "headline_timed_proc_run_delay_ms": _max_or_none(p["timed_proc_run_delay_ms"] for p in parts),
             "headline_timed_pump_run_delay_ms": _max_or_none(p["timed_pump_run_delay_ms"] for p in parts),
+            "headline_go_run_delay_ms": _max_or_none(p["go_run_delay_ms"] for p in parts),
             "headline_majflt": sum(p["majflt"] for p in parts),
             "thp": _thp_mode(),
             **cal,
