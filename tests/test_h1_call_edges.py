@@ -411,7 +411,11 @@ def test_a_failing_sweeper_arm_hands_the_connection_back():
 def test_a_reply_whose_pool_bookkeeping_fails_drops_the_connection():
     """After the reply, the native path hands the connection back to the idle pool itself (h1.py
     _release with no waiter). If that bookkeeping raises (here the origin's waiter queue cannot
-    be sized), the request fails with the error and the connection is dropped, not left busy."""
+    be sized), the request fails with the error and the connection is dropped, not left busy.
+    Dropping it wakes the origin's waiters, which meets the same broken queue: that second error
+    goes to sys.unraisablehook."""
+    import sys
+
     class BadLen(list):
         def __len__(self):
             raise LookupError("waiters broken")
@@ -431,5 +435,12 @@ def test_a_reply_whose_pool_bookkeeping_fails_drops_the_connection():
         finally:
             await c.close()
             await s.stop()
-    whole, status, after = run(go())
+    seen = []
+    old = sys.unraisablehook
+    sys.unraisablehook = lambda u: seen.append(type(u.exc_value).__name__)
+    try:
+        whole, status, after = run(go())
+    finally:
+        sys.unraisablehook = old
     assert whole == (0, True) and status == 200 and after == (0, True)
+    assert seen == ["LookupError"]

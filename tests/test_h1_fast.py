@@ -27,6 +27,7 @@ class Raw:
         self.respond = respond
         self.raw = []
         self.connections = 0
+        self._tasks = set()
 
     async def start(self):
         self.server = await asyncio.start_server(self._serve, "127.0.0.1", 0)
@@ -36,9 +37,16 @@ class Raw:
     async def stop(self):
         self.server.close()
         await self.server.wait_closed()
+        # Python 3.10's Server.close leaves connection handlers running ("hang" ones sleep on):
+        # end them while the loop is still open
+        for t in list(self._tasks):
+            t.cancel()
+        await asyncio.gather(*self._tasks, return_exceptions=True)
 
     async def _serve(self, r, w):
         self.connections += 1
+        me = asyncio.current_task()
+        self._tasks.add(me)
         try:
             while True:
                 try:
@@ -56,6 +64,7 @@ class Raw:
                 w.write(out)
                 await w.drain()
         finally:
+            self._tasks.discard(me)
             w.close()
 
 
