@@ -1141,14 +1141,20 @@ PyObject* h1_call_new(PyObject* client, PyObject* method, PyObject* url, PyObjec
 // API entry). h1_request_text trusts a caller's key_len only for those very objects (the caller
 // that asked h1_origin_key and builds the request next, the stub's order); any other key_len, or
 // the same URL after another check, gets the full check (a key_len taken for another
-// URL must not build a malformed request line). One use: the next request_text clears it.
+// URL must not build a malformed request line). One use: the next request_text takes it. The
+// entry holds references, so a freed URL's address cannot come back as another URL that matches.
 struct LastKey {
-  PyObject* method;  // borrowed identities, compared, never dereferenced
-  PyObject* url;
-  PyObject* params;
-  Py_ssize_t len;
-  Py_ssize_t k;
-} g_last_key = {nullptr, nullptr, nullptr, 0, 0};
+  PyObject* method = nullptr;  // strong references, compared by identity
+  PyObject* url = nullptr;
+  PyObject* params = nullptr;
+  Py_ssize_t len = 0;
+  Py_ssize_t k = 0;
+  void drop() {
+    Py_CLEAR(method);
+    Py_CLEAR(url);
+    Py_CLEAR(params);
+  }
+} g_last_key;
 
 int api_h1_request_text(PyObject* method, PyObject* url, PyObject* params, PyObject* host, PyObject* auth,
                         PyObject* tail, PyObject* tail_cl0, std::string* req, PyObject** full, Py_ssize_t* key_len) {
@@ -1159,10 +1165,10 @@ int api_h1_request_text(PyObject* method, PyObject* url, PyObject* params, PyObj
       return -1;
     }
     Py_ssize_t k = *key_len;
-    const LastKey last = g_last_key;
-    g_last_key.url = nullptr;
+    LastKey& last = g_last_key;
     const bool known = k > 0 && last.url == url && last.method == method && last.params == params &&
                        last.k == k && PyUnicode_CheckExact(url) && PyUnicode_GET_LENGTH(url) == last.len;
+    last.drop();
     if (!known && !split_shape(method, url, params, &k)) return 0;
     ScratchStr q_buf;
     std::string& q = *q_buf;
@@ -1182,11 +1188,17 @@ PyObject* h1_response_status(PyObject* resp) { return g.resp.get(resp, R_STATUS)
 
 int api_h1_origin_key(PyObject* method, PyObject* url, PyObject* params, Py_ssize_t* key_len) {
   if (params == Py_None) params = nullptr;
-  if (!split_shape(method, url, params, key_len)) {
-    g_last_key.url = nullptr;
-    return 0;
-  }
-  g_last_key = {method, url, params, PyUnicode_GET_LENGTH(url), *key_len};
+  LastKey& last = g_last_key;
+  last.drop();
+  if (!split_shape(method, url, params, key_len)) return 0;
+  Py_INCREF(method);
+  last.method = method;
+  Py_INCREF(url);
+  last.url = url;
+  Py_XINCREF(params);
+  last.params = params;
+  last.len = PyUnicode_GET_LENGTH(url);
+  last.k = *key_len;
   return 1;
 }
 

@@ -138,7 +138,18 @@ PyObject* mod_request_text_probe(PyObject*, PyObject* args) {
   BEHOLDER_CATCH(nullptr)
 }
 
+// origin_key_probe(method, url, params) -> (rc, key_len): the _C_API's h1_origin_key (tests)
+PyObject* mod_origin_key_probe(PyObject*, PyObject* args) {
+  PyObject *method, *url, *params;
+  if (!PyArg_ParseTuple(args, "OOO", &method, &url, &params)) return nullptr;
+  Py_ssize_t k = 0;
+  const int rc = g_api->h1_origin_key(method, url, params, &k);
+  if (rc < 0) return nullptr;
+  return Py_BuildValue("(in)", rc, k);
+}
+
 PyMethodDef calib_methods[] = {
+    {"origin_key_probe", mod_origin_key_probe, METH_VARARGS, "origin_key_probe(method, url, params) -> (rc, key_len)"},
     {"request_text_probe", mod_request_text_probe, METH_VARARGS,
      "request_text_probe(method, url, params, key_len) -> (rc, request, full, key_len)"},
     {"scratch_probe", mod_scratch_probe, METH_VARARGS,

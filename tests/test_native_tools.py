@@ -193,3 +193,25 @@ def test_request_text_does_not_trust_a_key_len_that_does_not_fit():
     for bad in ("https://api.trello.com/1/cards#frag", "https://api.trello.com/a\x01b", "https://api.trello.com/a b"):
         assert f("GET", bad, None, 0)[0] == 0, bad
         assert f("GET", bad, None, 3)[0] == 0, bad  # a wrong key_len: scanned, refused
+
+
+def test_request_text_trusts_a_key_len_only_for_the_url_it_was_taken_for():
+    """h1_origin_key remembers the objects it checked and h1_request_text skips the scan only for
+    those very objects. The entry holds references: once the checked URL is dropped, a URL of the
+    same length allocated after it (pymalloc hands the freed block straight back) is still
+    scanned, and a fragment in it is refused."""
+    key = native.native_bench.origin_key_probe
+    f = native.native_bench.request_text_probe
+    head = "https://api.trello.com/1/cards/"
+    rc, k = key("GET", head + str(10**8 + 1), None)
+    assert (rc, k) == (1, len("https://api.trello.com"))
+    assert f("GET", head + str(10**8 + 1), None, k)[0] == 1
+    n = len(head) + 9
+    sources = [f"{head}c{j}#frag" + "y" * 64 for j in range(10)]  # longer: another size class
+    for i in range(50):
+        url = head + str(10**8 + i)
+        assert len(url) == n and key("GET", url, None)[0] == 1
+        del url
+        bad = sources[i % 10][:n]  # the one allocation of url's size between the two calls
+        assert "#" in bad
+        assert f("GET", bad, None, len("https://api.trello.com"))[0] == 0, bad
