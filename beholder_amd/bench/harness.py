@@ -511,8 +511,49 @@ def _io_counts(src) -> Dict[str, int]:
     return c
 
 
+async def _windows(settler, mon, start: int, n: int, size: int, task, t0: float, out: dict):
+    """_tcp_e2e's measured phase in windows of ``size`` settled deliveries: per window the
+    handle / ingest latency percentiles (the settler's histograms, merged into the whole phase's
+    and then cleared), the RSS and the loop stalls seen. Returns (RSS half-way, merged histograms)."""
+    from ..ops import Histogram
+    kinds = ("handle", "ingest", "queue")
+    merged = {k: Histogram() for k in kinds}
+    windows: list = []
+    rss_mid = None
+    done, t_prev = start, t0
+    stalls_prev = 0
+    while done < n and not task.done():
+        target = min(n, done + size)
+        await _wait_acked(settler, target, task)
+        now = time.perf_counter()
+        got = _settled(settler) - done
+        w = {"t_s": round(now - t0, 2), "events": got,
+             "events_per_sec": round(got / (now - t_prev), 1) if now > t_prev else None}
+        for k in kinds:
+            h = getattr(settler, f"{k}_latency")
+            summ = h.summary()
+            if k != "queue":
+                w[f"{k}_p50_us"] = round(summ["p50"] / 1e3, 2) if summ["count"] else None
+                w[f"{k}_p99_us"] = round(summ["p99"] / 1e3, 2) if summ["count"] else None
+                w[f"{k}_p999_us"] = round(summ["p999"] / 1e3, 2) if summ["count"] else None
+                w[f"{k}_max_us"] = round(summ["max"] / 1e3, 2) if summ["count"] else None
+            merged[k].merge(h)
+        settler.reset_latency()
+        w["rss_mb"] = round(_rss_mb(), 2)
+        w["loop_stalls"] = len(mon.loop_stalls) - stalls_prev
+        stalls_prev = len(mon.loop_stalls)
+        windows.append(w)
+        print("window " + json.dumps(w), file=sys.stderr, flush=True)  # a long run shows progress
+        if rss_mid is None and target >= start + (n - start) // 2:
+            rss_mid = _rss_mb()
+        done, t_prev = _settled(settler), now
+    out["windows"] = windows
+    return (rss_mid if rss_mid is not None else _rss_mb()), merged
+
+
 def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = False, preconnect: int = 0,
-             max_connecting: int = 8, hooks: Optional[tuple] = None, rate: float = 0.0) -> dict:
+             max_connecting: int = 8, hooks: Optional[tuple] = None, rate: float = 0.0,
+             window_events: int = 0) -> dict:
     """Production-shaped: every dependency over real TCP. A replay AMQP broker streams n
     events (prefetch 100, index.js:43). Each handler reads / updates the media row in a
     fake Postgres (pipelined ``pgwire``). Every sink call goes to a fake HTTP endpoint
@@ -525,7 +566,11 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = Fal
     ``hooks``: ``(start, stop)`` callables run around the measured phase (scripts/cprof.py).
     ``rate``: the broker paces its sends at that many events per second (BASELINE configs 2-4 on
     the production path: each event's receive->ack latency with its Postgres and HTTP round trips,
-    not queueing behind a saturated prefetch window); the warm-up is then a tenth of the events."""
+    not queueing behind a saturated prefetch window); the warm-up is then a tenth of the events.
+    ``window_events``: the measured phase is cut into windows of that many settled deliveries
+    (paced: a fixed time each); each window's latency percentiles, RSS and loop stalls are
+    reported (``windows``), and the whole-phase percentiles merge the windows' histograms
+    (scripts/paced_soak.py: is the production path as fast in its tenth minute as in its first?)."""
     from ..config import Config
     from ..service import Service
     from ..sinks import H1Client
@@ -597,11 +642,15 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = Fal
             if hooks:
                 hooks[0]()
             t0 = time.perf_counter()
-            # half-way: the RSS there against the end is the leak check (the first half still
-            # grows the sink pool towards its steady size: tens of connections with their buffers)
-            await _wait_acked(src.settler, warm + (n - warm) // 2, task)
-            rss_mid = _rss_mb()
-            await _wait_acked(src.settler, n, task)
+            if window_events > 0:
+                rss_mid, merged = await _windows(src.settler, mon, settled0, n, window_events, task, t0, out)
+            else:
+                merged = None
+                # half-way: the RSS there against the end is the leak check (the first half still
+                # grows the sink pool towards its steady size: tens of connections with their buffers)
+                await _wait_acked(src.settler, warm + (n - warm) // 2, task)
+                rss_mid = _rss_mb()
+                await _wait_acked(src.settler, n, task)
             elapsed = time.perf_counter() - t0
             if hooks:
                 hooks[1]()
@@ -621,6 +670,9 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = Fal
             svc.request_stop()
             await task
             stats = svc.stats()
+            if merged is not None:  # the windows reset the settler's histograms: their merge
+                for kind, h in merged.items():
+                    stats[f"{kind}_latency_ns"] = h.summary()
             pg_conns = store._pool.connections if store._pool else 0
             http_stats = http.stats()
             await svc.close()

@@ -33,3 +33,27 @@ def test_config_runs_small(name):
     if name.endswith("_preconnect"):
         assert res["preconnect"] == 100 and res["errors"] == 0
         assert res["http"]["connections"] >= 100  # opened at init, before the first delivery
+
+
+def test_paced_run_in_windows_accounts_for_every_event(tmp_path, capsys):
+    """scripts/paced_soak.py's mode: the paced production path measured in windows of settled
+    deliveries. Every window reports its own percentiles and RSS; the whole phase's percentiles
+    are the windows' histograms merged (so they count every measured delivery, not just the last
+    window's)."""
+    import json
+    import runpy
+    out = tmp_path / "soak.json"
+    script = harness.__file__.replace("beholder_amd/bench/harness.py", "scripts/paced_soak.py")
+    mod = runpy.run_path(script, run_name="paced_soak")
+    rc = mod["main"](["--rate", "4000", "--seconds", "0.9", "--window-s", "0.3", "--out", str(out)])
+    r = json.loads(out.read_text())
+    assert rc == 0 and r["errors"] == 0 and r["acked"] == 3600 + 400
+    ws = r["windows"]
+    # windows end at the first poll past each 1,200th settled delivery: a few more or less
+    assert len(ws) == 3 and all(abs(w["events"] - 1200) <= 20 for w in ws), ws
+    assert sum(w["events"] for w in ws) == r["measured_events"] and abs(r["measured_events"] - 3600) <= 20
+    assert all(w["handle_p50_us"] > 0 and w["handle_p99_us"] >= w["handle_p50_us"] and w["rss_mb"] > 0 for w in ws)
+    p50s = [w["handle_p50_us"] for w in ws]
+    assert min(p50s) * 0.99 <= r["handle_latency_us"]["p50"] <= max(p50s) * 1.01  # all windows, merged
+    line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert line["config"] == "tcp_e2e" and len(line["window_p99_us"]) == 3
