@@ -50,6 +50,35 @@ def _rss_mb() -> float:
         return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024
 
 
+def _heap_mb() -> Optional[Dict[str, float]]:
+    """glibc's view of this process's malloc heap (mallinfo2): bytes in use, bytes free inside
+    the heap, and the heap's size (main arena plus mmapped chunks). RSS growth with ``inuse``
+    flat is fragmentation, not a leak. None off glibc."""
+    global _MALLINFO
+    if _MALLINFO is None:
+        try:
+            import ctypes
+
+            class _MI2(ctypes.Structure):
+                _fields_ = [(n, ctypes.c_size_t) for n in ("arena", "ordblks", "smblks", "hblks", "hblkhd",
+                                                           "usmblks", "fsmblks", "uordblks", "fordblks",
+                                                           "keepcost")]
+            fn = ctypes.CDLL("libc.so.6").mallinfo2
+            fn.restype = _MI2
+            _MALLINFO = fn
+        except (OSError, AttributeError):
+            _MALLINFO = False
+    if not _MALLINFO:
+        return None
+    m = _MALLINFO()
+    mb = 1 / 2**20
+    return {"inuse": round(m.uordblks * mb, 2), "free": round(m.fordblks * mb, 2),
+            "size": round((m.arena + m.hblkhd) * mb, 2)}
+
+
+_MALLINFO = None
+
+
 class GcPauses:
     """Collects GC pause durations through ``gc.callbacks``."""
 
@@ -516,12 +545,14 @@ async def _windows(settler, mon, start: int, n: int, size: int, task, t0: float,
     handle / ingest latency percentiles (the settler's histograms, merged into the whole phase's
     and then cleared), the RSS and the loop stalls seen. Returns (RSS half-way, merged histograms)."""
     from ..ops import Histogram
+    from ..utils.hostinfo import thread_run_delay_ns
     kinds = ("handle", "ingest", "queue")
     merged = {k: Histogram() for k in kinds}
     windows: list = []
     rss_mid = None
     done, t_prev = start, t0
     stalls_prev = 0
+    rq_prev, ru_prev = thread_run_delay_ns(), resource.getrusage(resource.RUSAGE_SELF)
     while done < n and not task.done():
         target = min(n, done + size)
         await _wait_acked(settler, target, task)
@@ -540,8 +571,18 @@ async def _windows(settler, mon, start: int, n: int, size: int, task, t0: float,
             merged[k].merge(h)
         settler.reset_latency()
         w["rss_mb"] = round(_rss_mb(), 2)
+        w["heap_mb"] = _heap_mb()
         w["loop_stalls"] = len(mon.loop_stalls) - stalls_prev
         stalls_prev = len(mon.loop_stalls)
+        # the loop thread's wait for a CPU and the process's involuntary switches in the window:
+        # stalls with little work settled inside them and a high run delay were the consumer
+        # descheduled, not its loop blocked
+        rq, ru = thread_run_delay_ns(), resource.getrusage(resource.RUSAGE_SELF)
+        w["run_delay_ms"] = round((rq - rq_prev) / 1e6, 2) if rq is not None and rq_prev is not None else None
+        w["nivcsw"] = ru.ru_nivcsw - ru_prev.ru_nivcsw
+        w["cpu_us_per_event"] = round(((ru.ru_utime + ru.ru_stime) - (ru_prev.ru_utime + ru_prev.ru_stime)) / got * 1e6,
+                                      2) if got else None
+        rq_prev, ru_prev = rq, ru
         windows.append(w)
         print("window " + json.dumps(w), file=sys.stderr, flush=True)  # a long run shows progress
         if rss_mid is None and target >= start + (n - start) // 2:

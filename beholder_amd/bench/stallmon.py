@@ -42,7 +42,11 @@ class StallMonitor:
         self.stall_work: List[Tuple[float, int]] = []
         self.loop_stalls: List[Interval] = []
         self.gc_pauses: List[Interval] = []
-        self.lags_ns: List[int] = []  # every measured lateness (bounded by the run length / period)
+        # every measured lateness, in a fixed-size native histogram: a list of one int per tick
+        # grew the consumer's RSS by ~2 MB a minute (1,000 ticks/s), which a paced soak billed to
+        # the service as a leak (scripts/paced_soak.py, profiles/box_r6_psoak/)
+        from ..ops import Histogram
+        self.lags_ns = Histogram()
         self.gc_pause_ns: List[int] = []
         self._task: Optional[asyncio.Task] = None
         self._gc_t0 = 0
@@ -78,8 +82,7 @@ class StallMonitor:
             lag = now - due
             if lag < 0:
                 lag = 0
-            if len(self.lags_ns) < 4_000_000:
-                self.lags_ns.append(lag)
+            self.lags_ns.record(lag)
             if lag >= self.threshold_ns:
                 self._add(self.loop_stalls, (due, now))
                 if work is not None and len(self.stall_work) < 1000:
@@ -95,7 +98,7 @@ class StallMonitor:
         """Forget what was recorded so far (the end of a warm-up)."""
         self.loop_stalls.clear()
         self.gc_pauses.clear()
-        self.lags_ns.clear()
+        self.lags_ns.reset()
         self.gc_pause_ns.clear()
         self.stall_work.clear()
         self.dropped = 0
@@ -110,15 +113,11 @@ class StallMonitor:
             pass
 
     def summary(self) -> Dict[str, object]:
-        def pct(xs: List[int], q: float) -> Optional[float]:
-            if not xs:
-                return None
-            s = sorted(xs)
-            return round(s[min(len(s) - 1, int(q / 100 * len(s)))] / 1e3, 1)
-
+        lags = self.lags_ns
         return {
-            "loop_lag_p99_us": pct(self.lags_ns, 99), "loop_lag_p999_us": pct(self.lags_ns, 99.9),
-            "loop_lag_max_us": round(max(self.lags_ns) / 1e3, 1) if self.lags_ns else None,
+            "loop_lag_p99_us": round(lags.percentile(99) / 1e3, 1) if lags.count else None,
+            "loop_lag_p999_us": round(lags.percentile(99.9) / 1e3, 1) if lags.count else None,
+            "loop_lag_max_us": round(lags.max / 1e3, 1) if lags.count else None,
             "loop_stalls": len(self.loop_stalls),
             "loop_stalled_ms": round(sum(b - a for a, b in self.loop_stalls) / 1e6, 2),
             "gc_pauses": len(self.gc_pause_ns),

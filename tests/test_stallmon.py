@@ -105,3 +105,26 @@ def test_a_stall_records_the_work_done_inside_it():
     work = asyncio.run(go())
     assert any(w == 300 for _, w in work) and any(w == 0 for _, w in work), work
     assert all(us >= 1000 for us, _ in work)
+
+
+def test_loop_lags_take_fixed_memory():
+    """Every tick's lateness goes into a fixed-size histogram: a list of one int per tick grew
+    the consumer's RSS ~2 MB a minute on a paced soak (profiles/box_r6_psoak/)."""
+    import asyncio
+    import sys
+
+    from beholder_amd.bench.stallmon import StallMonitor
+
+    async def go():
+        m = StallMonitor(period_s=0.0002).start(asyncio.get_running_loop())
+        await asyncio.sleep(0.05)
+        size0, n0 = sys.getsizeof(m.lags_ns), m.lags_ns.count
+        await asyncio.sleep(0.25)
+        m.stop()
+        return m, size0, n0
+    m, size0, n0 = asyncio.run(go())
+    assert m.lags_ns.count > n0 > 0 and sys.getsizeof(m.lags_ns) == size0
+    s = m.summary()
+    assert s["loop_lag_max_us"] >= s["loop_lag_p999_us"] >= s["loop_lag_p99_us"] >= 0
+    m.reset()
+    assert m.lags_ns.count == 0 and m.summary()["loop_lag_p99_us"] is None
