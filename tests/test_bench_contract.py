@@ -125,7 +125,8 @@ def test_bench_single_rank_contract(tmp_path):
     for pre in ("tcp_e2e", "tls_e2e"):
         for name, rate, n in bench.E2E_RATES:
             k = f"{pre}_rate_{name}"
-            assert out[f"{k}_errors"] == 0 and out[f"{k}_measured_events"] >= max(200, int(n * 0.1)) * 0.85, k
+            # a tenth is warm-up, and the warm-up's end is seen at a poll (up to 50 ms of events later)
+            assert out[f"{k}_errors"] == 0 and out[f"{k}_measured_events"] >= max(200, int(n * 0.1)) * 0.6, k
             assert out[f"{k}_p50_handle_latency_us"] <= out[f"{k}_p99_handle_latency_us"], k
     # the consumer's socket calls per event: a send per sink request, queries
     # and acks batched, every kind of connection seen
