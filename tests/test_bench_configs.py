@@ -54,6 +54,7 @@ def test_paced_run_in_windows_accounts_for_every_event(tmp_path, capsys):
     assert sum(w["events"] for w in ws) == r["measured_events"] and abs(r["measured_events"] - 3600) <= 100
     assert all(w["handle_p50_us"] > 0 and w["handle_p99_us"] >= w["handle_p50_us"] and w["rss_mb"] > 0 for w in ws)
     assert all(w["cpu_us_per_event"] > 0 and w["nivcsw"] >= 0 and "run_delay_ms" in w for w in ws)
+    assert all(w["heap_mb"] is None or 0 < w["heap_mb"]["inuse"] <= w["heap_mb"]["size"] for w in ws)
     p50s = [w["handle_p50_us"] for w in ws]
     assert min(p50s) * 0.99 <= r["handle_latency_us"]["p50"] <= max(p50s) * 1.01  # all windows, merged
     line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
