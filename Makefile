@@ -28,7 +28,7 @@ tsan:              ## ring/framer stress test under ThreadSanitizer + ASan/UBSan
 asan:             ## CPython suites against an ASan+UBSan build of the extension (host code only)
 	$(PY) -m beholder_amd.ops.build --force --sanitize=address,undefined
 	BEHOLDER_ALLOW_BUILD=0 ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=halt_on_error=1 \
-	  LD_PRELOAD="$$(gcc -print-file-name=libasan.so) $$(gcc -print-file-name=libubsan.so)" \
+	  LD_PRELOAD="$$(gcc -print-file-name=libasan.so) $$(gcc -print-file-name=libubsan.so) $${LD_PRELOAD:-}" \
 	  $(PY) -m pytest -q -p no:cacheprovider -m "not gpu" tests/test_native_fuzz.py tests/test_codec.py tests/test_ingest.py \
 	  tests/test_amqp_demux.py tests/test_text.py tests/test_delivery.py tests/test_histogram.py \
 	  tests/test_handlers.py tests/test_native_handlers.py tests/test_tracing.py tests/test_amqp.py tests/test_service.py tests/test_h1.py tests/test_h1_fast.py tests/test_tls.py tests/test_netconn.py tests/test_sinks.py tests/test_stores.py tests/test_preconnect.py tests/test_driver.py tests/test_chaos.py tests/test_workers.py tests/test_gpu_decode.py tests/test_native_tools.py tests/test_pg_fake.py tests/test_gil_clock.py \
