@@ -38,7 +38,9 @@ class FakePg:
         """Abort every open client connection (a Postgres restart / failover)."""
         n = len(self._writers)
         for w in list(self._writers):
-            w.transport.abort()
+            t = w.transport
+            if t is not None:  # None: mid-upgrade to TLS (SSLRequest answered, start_tls running)
+                t.abort()
         return n
 
     @property

@@ -16,6 +16,7 @@ Nothing may be lost. Every published message ends up acked, or, for Q1 status me
 outstanding when the run stops, un-acked and held by the broker for redelivery.
 """
 import asyncio
+import os
 import random
 
 import pytest
@@ -65,7 +66,8 @@ class _HttpSink:
 
     def drop(self):
         for w in list(self.writers):
-            w.transport.abort()
+            if w.transport is not None:
+                w.transport.abort()
 
     async def stop(self):
         self.server.close()
@@ -76,7 +78,7 @@ class _HttpSink:
 def test_chaos_every_dependency_drops_connections(tls):
     """``tls``: HTTPS sinks and Postgres sslmode=verify-full, i.e. every sink and DB connection on
     the native TLS path (ops/csrc/py_tls.cpp) while the chaos task drops them."""
-    rng = random.Random(7)
+    rng = random.Random(int(os.environ.get("BEHOLDER_CHAOS_SEED", "7")))  # other seeds: a longer hunt by hand
     n_progress, n_status = 1500, 150
     medias = [Media(id=f"m{i}", name=f"Show {i}", creator=1, creatorId=f"card{i}", metadataId=str(i),
                     status=i % 5) for i in range(50)]
@@ -104,25 +106,33 @@ def test_chaos_every_dependency_drops_connections(tls):
 
             hits = []
 
-            async def chaos():
+            async def fire(what):
+                hits.append(what)
+                if what == "amqp":
+                    await broker.drop_connections()
+                elif what == "pg":
+                    pg.drop_connections()
+                else:
+                    sink.drop()
+
+            async def chaos():  # drops at random times, in flight or not
                 while True:
                     await asyncio.sleep(rng.uniform(0.03, 0.12))
-                    what = rng.choice(("amqp", "pg", "http", "pg", "http"))
-                    hits.append(what)
-                    if what == "amqp":
-                        await broker.drop_connections()
-                    elif what == "pg":
-                        pg.drop_connections()
-                    else:
-                        sink.drop()
+                    await fire(rng.choice(("amqp", "pg", "http", "pg", "http")))
 
+            # and one drop per 50 messages while they are being published, every kind in turn: a
+            # seed whose random drops come late (a loop busy with TLS handshakes) still hits each
+            # dependency with deliveries in flight
+            turns = ["amqp", "pg", "http", "pg", "http"]
+            rng.shuffle(turns)
             monkey = asyncio.ensure_future(chaos())
             for i in range(n_progress):
                 broker.publish(PROGRESS, progress_msg(f"m{i % 50}", "CONVERTING", i % 101, f"w{i % 3}"))
                 if i % 10 == 0:
                     broker.publish(STATUS, status_msg(f"m{(i // 10) % 50}", "DEPLOYED"))
-                if i % 50 == 0:
-                    await asyncio.sleep(0.05)  # ~1.5 s of traffic: the chaos task fires ~20 times
+                if i % 50 == 49:
+                    await asyncio.sleep(rng.uniform(0.01, 0.05))  # ~1.5 s of traffic
+                    await fire(turns[(i // 50) % len(turns)])
             deadline = asyncio.get_running_loop().time() + 20
             while asyncio.get_running_loop().time() < deadline:
                 if broker.stats(PROGRESS)["acked"] >= n_progress:
