@@ -133,12 +133,16 @@ def test_chaos_every_dependency_drops_connections(tls):
                 if i % 50 == 49:
                     await asyncio.sleep(rng.uniform(0.01, 0.05))  # ~1.5 s of traffic
                     await fire(turns[(i // 50) % len(turns)])
-            deadline = asyncio.get_running_loop().time() + 20
+            # the random drops go on a little past the last publish, then stop: drops every ~75 ms
+            # until the end would redeliver the window faster than a loaded machine (the pure
+            # Python I/O path under pytest -n, test_native_io_matrix) works through it
+            await asyncio.sleep(0.3)
+            monkey.cancel()
+            deadline = asyncio.get_running_loop().time() + 30
             while asyncio.get_running_loop().time() < deadline:
                 if broker.stats(PROGRESS)["acked"] >= n_progress:
                     break
                 await asyncio.sleep(0.05)
-            monkey.cancel()
             # one clean redelivery round: Q1 status messages still un-acked come back once more
             await broker.drop_connections()
             deadline = asyncio.get_running_loop().time() + 10
