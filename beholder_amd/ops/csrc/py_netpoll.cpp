@@ -43,6 +43,7 @@ struct PollerObject {
   PyObject* flush_cb;                            // bound _flush (call_soon)
   std::unordered_map<int, PyObject*>* conns;     // fd -> NetConn (strong)
   std::vector<PyObject*>* to_flush;              // connections with queued queries (strong)
+  std::vector<PyObject*>* deferred;              // callables run once at the end of this batch (strong)
   std::shared_ptr<HsWake>* wake;                 // TLS handshake completions (created on first use)
   bool flush_scheduled;
 };
@@ -99,7 +100,37 @@ void flush_all(PollerObject* p) {
   }
 }
 
+// The callables deferred to the end of the batch (defer()): the AMQP ack flush, so the acks of the
+// handlers a batch finished share one write with no extra trip through the loop.
+void run_deferred(PollerObject* p) {
+  while (p->deferred && !p->deferred->empty()) {
+    std::vector<PyObject*> tmp;
+    tmp.swap(*p->deferred);
+    for (PyObject* cb : tmp) {
+      PyObject* r = PyObject_CallNoArgs(cb);
+      if (!r)
+        PyErr_WriteUnraisable(cb);
+      else
+        Py_DECREF(r);
+      Py_DECREF(cb);
+    }
+  }
+}
+
+// End of a batch (the outermost _run or _enter/_exit scope): queued queries go out, deferred
+// callables run, and an empty poller leaves the loop.
+void end_batch(PollerObject* p) {
+  flush_all(p);
+  run_deferred(p);
+  if (!p->running && p->conns && p->conns->empty()) poller_close(p);
+}
+
 void drop_all(PollerObject* p) {
+  if (p->deferred) {
+    std::vector<PyObject*> tmp;
+    tmp.swap(*p->deferred);
+    for (PyObject* c : tmp) Py_DECREF(c);
+  }
   if (p->to_flush) {
     std::vector<PyObject*> tmp;
     tmp.swap(*p->to_flush);
@@ -117,6 +148,8 @@ int poller_traverse(PollerObject* p, visitproc visit, void* arg) {
   Py_VISIT(p->flush_cb);
   if (p->to_flush)
     for (PyObject* c : *p->to_flush) Py_VISIT(c);
+  if (p->deferred)
+    for (PyObject* c : *p->deferred) Py_VISIT(c);
   if (p->conns)
     for (auto& kv : *p->conns) Py_VISIT(kv.second);
   return 0;
@@ -147,6 +180,7 @@ void poller_dealloc(PollerObject* p) {
   Py_CLEAR(p->loop);
   delete p->conns;
   delete p->to_flush;
+  delete p->deferred;
   delete p->wake;
   Py_TYPE(p)->tp_free(reinterpret_cast<PyObject*>(p));
 }
@@ -182,10 +216,37 @@ PyObject* poller_run(PollerObject* p, PyObject*) {
     Py_DECREF(c);
   }
   --p->running;
-  if (!p->running) flush_all(p);  // queries the resumed handlers issued go out now, batched
-  if (!p->running && p->conns && p->conns->empty()) poller_close(p);
+  if (!p->running) end_batch(p);  // queries the resumed handlers issued go out now, batched
   Py_DECREF(p);
   Py_RETURN_NONE;
+}
+
+// _enter() / _exit(): a batch scope for work that starts outside a _run, e.g. deliveries dispatched
+// from the AMQP transport's read callback. Queries issued inside go out at _exit, together, and
+// deferred callables run there, instead of one call_soon trip each.
+PyObject* poller_enter(PollerObject* p, PyObject*) {
+  ++p->running;
+  Py_RETURN_NONE;
+}
+
+PyObject* poller_exit(PollerObject* p, PyObject*) {
+  if (p->running <= 0) {
+    PyErr_SetString(PyExc_RuntimeError, "NetPoller._exit without _enter");
+    return nullptr;
+  }
+  Py_INCREF(p);
+  if (--p->running == 0) end_batch(p);
+  Py_DECREF(p);
+  Py_RETURN_NONE;
+}
+
+// defer(cb) -> bool: inside a batch, run cb() once at its end and return True; outside one,
+// return False (the caller schedules it itself).
+PyObject* poller_defer(PollerObject* p, PyObject* cb) {
+  if (!p->running || !p->deferred) Py_RETURN_FALSE;
+  Py_INCREF(cb);
+  p->deferred->push_back(cb);
+  Py_RETURN_TRUE;
 }
 
 // _flush(): call_soon callback for queries queued outside a dispatch
@@ -200,6 +261,11 @@ PyObject* poller_flush(PollerObject* p, PyObject*) {
 PyMethodDef poller_methods[] = {
     {"_run", reinterpret_cast<PyCFunction>(poller_run), METH_NOARGS, "loop reader callback: dispatch ready sockets"},
     {"_flush", reinterpret_cast<PyCFunction>(poller_flush), METH_NOARGS, "send the queued Postgres queries"},
+    {"_enter", reinterpret_cast<PyCFunction>(poller_enter), METH_NOARGS, "open a batch scope (see _exit)"},
+    {"_exit", reinterpret_cast<PyCFunction>(poller_exit), METH_NOARGS,
+     "close a batch scope: queued queries go out, deferred callables run"},
+    {"defer", reinterpret_cast<PyCFunction>(poller_defer), METH_O,
+     "defer(cb) -> bool: run cb() at the end of the batch in progress (False: no batch)"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyObject* poller_get_size(PollerObject* p, void*) { return PyLong_FromSize_t(p->conns ? p->conns->size() : 0); }
@@ -241,9 +307,10 @@ PyObject* netpoll_for(PyObject* loop) {
   p->wake = nullptr;
   p->conns = new (std::nothrow) std::unordered_map<int, PyObject*>();
   p->to_flush = new (std::nothrow) std::vector<PyObject*>();
+  p->deferred = new (std::nothrow) std::vector<PyObject*>();
   PyObject_GC_Track(p);
   PyObject* po = reinterpret_cast<PyObject*>(p);
-  if (!p->conns || !p->to_flush) {
+  if (!p->conns || !p->to_flush || !p->deferred) {
     Py_DECREF(po);
     return PyErr_NoMemory();
   }

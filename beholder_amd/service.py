@@ -470,6 +470,12 @@ class Service:
         src = self.source
         counts_waits = isinstance(getattr(src, "idle_wakeups", None), int)
         last_wakeups = -1
+        # a source that can hand deliveries over from its read callback (AmqpSource.direct) gets
+        # the native dispatch itself while this task waits: a delivery at a low rate then starts
+        # its handler with no wake-up of this task, one trip through the loop fewer
+        direct = native and tracer is None and hasattr(src, "direct")
+        if direct:
+            src.direct = self._direct_dispatcher(routes, on_error, on_suspend, on_unroutable)
         try:
             async for batch in src.batches():
                 waited = self._slot_waits
@@ -499,6 +505,8 @@ class Service:
                     continue
                 await sleep(0)  # keep timers / the metrics endpoint responsive under sustained load
         finally:
+            if direct:
+                src.direct = None
             self._running = False
             flusher.cancel()
             await self._drain()
@@ -508,6 +516,22 @@ class Service:
                 log.error(f"ingest source failed: {err}")
             log.flush()
         return self.stats()
+
+    def _direct_dispatcher(self, routes, on_error, on_suspend, on_unroutable):
+        """The source's direct hand-over (AmqpSource.direct): dispatch what the prefetch window
+        allows (ops.dispatch_batch, as _dispatch_native) and return the rest, which the source
+        queues for this task; None once all of it started. Nothing after a stop request."""
+        received, inflight, prefetch, log = self.received, self._inflight, self.prefetch, self.log
+
+        def hand_over(batch):
+            if self._stop:
+                return batch
+            n = len(batch)
+            i = dispatch_batch(batch, 0, routes, received, on_error, on_suspend, on_unroutable) \
+                if len(inflight) < prefetch else 0
+            log.flush()
+            return batch[i:] if i < n else None
+        return hand_over
 
     async def _dispatch_native(self, batch, routes, on_error, on_suspend, on_unroutable) -> None:
         """The per-delivery loop in C (ops.dispatch_batch), pausing while `prefetch` handlers

@@ -69,6 +69,13 @@ class AmqpSource(Source):
         self._pending: List = []
         self._event: Optional[Signal] = None
         self.idle_wakeups = 0  # batches that came after the consumer waited for deliveries
+        # set by the consumer while it waits with nothing queued: deliveries are handed to it from
+        # the read callback itself (no wake-up of its task, no extra trip through the loop);
+        # it returns what it could not take (prefetch window full), which then queues as usual
+        self.direct = None
+        self.direct_batches = 0
+        self._in_task = False  # a batch from batches() is in the consumer's hands
+        self._direct_error: Optional[BaseException] = None
         self._loop: Optional[asyncio.AbstractEventLoop] = None  # set at start(): one lookup, not one per flush
         self._closing = False
         self._stopping = False
@@ -144,14 +151,44 @@ class AmqpSource(Source):
         pending = self._pending
         if pending:
             pending.extend(ds)
-        else:
-            self._pending = ds
+            return
+        direct = self.direct
+        # not while the consumer's task works through a queued batch: what arrives meanwhile
+        # queues behind it, so handlers start in delivery order
+        if direct is not None and not self._in_task and not self._stopping and not self._closing:
+            ds = self._hand_over(direct, ds)
+            if not ds:
+                return
+        self._pending = ds
+        self._event.set()
+
+    def _hand_over(self, direct, ds):
+        """The deliveries to the waiting consumer, inside one NetPoller batch: the queries its
+        handlers issue go out together at the end, and so do the acks of handlers that finish
+        there. Returns what it did not take. A failure of the consumer's dispatch ends the direct
+        hand-over and is raised from :meth:`batches`, as a failure in its own loop would be."""
+        self.direct_batches += 1
+        poller = getattr(self._loop, "_beholder_netpoller", None)
+        if poller is not None:
+            poller._enter()
+        try:
+            return direct(ds)
+        except BaseException as e:  # noqa: BLE001 - re-raised in the consumer's task (batches)
+            self.direct = None
+            self._direct_error = e
             self._event.set()
+            return None
+        finally:
+            if poller is not None:
+                poller._exit()
 
     def _schedule_ack_flush(self) -> None:
         loop = self._loop
         if loop is None:
             loop = self._loop = asyncio.get_running_loop()
+        poller = getattr(loop, "_beholder_netpoller", None)
+        if poller is not None and poller.defer(self._flush_acks):
+            return  # settled inside a NetPoller batch: flushed at its end, with the batch's other acks
         loop.call_soon(self._flush_acks)
 
     def _flush_acks(self) -> None:
@@ -179,9 +216,16 @@ class AmqpSource(Source):
 
     async def batches(self):
         while True:
+            if self._direct_error is not None:
+                e, self._direct_error = self._direct_error, None
+                raise e
             if self._pending:
                 batch, self._pending = self._pending, []
-                yield batch
+                self._in_task = True
+                try:
+                    yield batch
+                finally:
+                    self._in_task = False
                 continue
             if self._closing or self._stopping:
                 return

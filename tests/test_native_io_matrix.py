@@ -9,7 +9,8 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SUITES = ["tests/test_handlers.py", "tests/test_service.py", "tests/test_chaos.py", "tests/test_h1_fast.py"]
+SUITES = ["tests/test_handlers.py", "tests/test_service.py", "tests/test_chaos.py", "tests/test_h1_fast.py",
+          "tests/test_direct_dispatch.py"]
 
 
 @pytest.mark.parametrize("native_io", ["1", "0"])
