@@ -594,7 +594,7 @@ async def _windows(settler, mon, start: int, n: int, size: int, task, t0: float,
 
 def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = False, preconnect: int = 0,
              max_connecting: int = 8, hooks: Optional[tuple] = None, rate: float = 0.0,
-             window_events: int = 0) -> dict:
+             window_events: int = 0, stall_period_s: float = 0.001) -> dict:
     """Production-shaped: every dependency over real TCP. A replay AMQP broker streams n
     events (prefetch 100, index.js:43). Each handler reads / updates the media row in a
     fake Postgres (pipelined ``pgwire``). Every sink call goes to a fake HTTP endpoint
@@ -611,7 +611,9 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = Fal
     ``window_events``: the measured phase is cut into windows of that many settled deliveries
     (paced: a fixed time each); each window's latency percentiles, RSS and loop stalls are
     reported (``windows``), and the whole-phase percentiles merge the windows' histograms
-    (scripts/paced_soak.py: is the production path as fast in its tenth minute as in its first?)."""
+    (scripts/paced_soak.py: is the production path as fast in its tenth minute as in its first?).
+    ``stall_period_s``: the stall monitor's tick on the consumer's loop (each tick is a wake-up of
+    that loop, billed to the consumer's CPU: at 1k events/s the default is one tick per event)."""
     from ..config import Config
     from ..service import Service
     from ..sinks import H1Client
@@ -659,7 +661,7 @@ def _tcp_e2e(n: int, http_servers: int = 2, pg_servers: int = 1, tls: bool = Fal
             t_init = time.perf_counter()
             await svc.init()  # connects to the broker and PG; preconnect opens the sink connections
             out["init_ms"] = round((time.perf_counter() - t_init) * 1e3, 2)
-            mon = StallMonitor(work=lambda: _settled(src.settler)).start()
+            mon = StallMonitor(period_s=stall_period_s, work=lambda: _settled(src.settler)).start()
             src.settler.trace_slow(SLOW_TRACE_NS)
             cg0 = cgroup_cpu_stat()
             task = asyncio.ensure_future(svc.run())

@@ -536,6 +536,12 @@ def _paced_e2e_keys(prefix: str, name: str, e: dict) -> dict:
             f"{p}_run_delay_ms": _r(e.get("run_delay_ms"), 2)}
 
 
+# the bench's stall monitor ticks on the consumer's loop; at 1 ms (the saturated runs' tick, for
+# stall attribution) it billed the paced runs ~4 us per event at 1k/s, one wake-up per event
+# (profiles/box_r6_tick_ab/). The paced keys use no stall data: a coarse tick keeps it off the CPU.
+PACED_STALL_TICK_S = 0.05
+
+
 def paced_e2e_keys(a, prefix: str, **kw) -> dict:
     from beholder_amd.bench import harness
     out = {}
@@ -543,7 +549,9 @@ def paced_e2e_keys(a, prefix: str, **kw) -> dict:
         return out
     for name, rate, n in E2E_RATES:
         n = max(200, int(n * a.e2e_paced_scale))
-        out.update(_paced_e2e_keys(prefix, name, harness._tcp_e2e(n, rate=rate, **kw)))
+        out.update(_paced_e2e_keys(prefix, name, harness._tcp_e2e(n, rate=rate, stall_period_s=PACED_STALL_TICK_S,
+                                                                 **kw)))
+    out[f"{prefix}_paced_stall_tick_ms"] = PACED_STALL_TICK_S * 1e3
     return out
 
 

@@ -13,9 +13,12 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--tls", action="store_true")
     ap.add_argument("--scale", type=float, default=1.0, help="events per rate times this")
+    ap.add_argument("--stall-period", type=float, default=0.001,
+                    help="the stall monitor's tick on the consumer's loop, seconds")
     a = ap.parse_args()
     from beholder_amd.bench import harness
     kw = dict(http_servers=4, tls=True) if a.tls else {}
+    kw["stall_period_s"] = a.stall_period
     harness._tcp_e2e(20000, **kw)  # unmeasured: first-touch pages, lazily opened connections
     for name, rate, n in (("1k", 1000, 3000), ("10k", 10000, 20000), ("100k", 100000, 100000)):
         e = harness._tcp_e2e(max(200, int(n * a.scale)), rate=rate, **kw)
