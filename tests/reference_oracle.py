@@ -6,7 +6,9 @@ per delivered event, acks, the listener's rejection, whether decode threw, every
 (method + full URL) and every log line; at the end it records the counters and the media
 table's statuses. :func:`run_python` replays the same scenario through this repo's handlers
 (``handlers.py`` or the compiled ``ops/csrc/py_handlers.cpp``) and records the same things;
-:func:`diff` compares them field by field.
+:func:`diff` compares them field by field. :func:`run_service` replays it through the whole consumer
+instead (an in-process AMQP broker, ``AmqpSource``, the service's dispatch and its acks), as
+production receives events.
 
 A scenario (:func:`make_scenario`) is a seeded random config, media table, sink-fault list and
 event stream. The streams are built to reach every branch of index.js:50-155, malformed bodies
@@ -415,6 +417,123 @@ def run_python(sc: dict, impl: str = "python", mutate=None, suspend: bool = Fals
     return out
 
 
+def run_service(sc: dict, impl: str = "native", suspend: bool = False) -> dict:
+    """The same scenario through the whole consumer, as production runs it: each event is
+    published to an in-process AMQP broker, delivered to :class:`AmqpSource` and
+    handed to the service's dispatch (from the read callback when the service waits: the direct
+    hand-over), handled, and acked over AMQP. One event at a time, as ``oracle.js`` delivers them;
+    the next is published once this one is settled (acked, or left un-acked under Q1) and no
+    handler is in flight.
+
+    Recorded as :func:`run_python` records: ``acks`` as the broker counted them, ``threw`` from
+    the service's ``unhandled error in <topic> handler: <message>`` line (Node's unhandled
+    rejection, index.js:62; the line itself is not one of the reference's), the sink requests and
+    the other log lines. Not for mode ``concurrent``, which scripts its interleavings at gates."""
+    import copy
+    import gc
+
+    import helpers
+    from beholder_amd import topics as T
+    from beholder_amd.bench.harness import _settled
+    from beholder_amd.models.proto import DecodeError
+    from beholder_amd.service import Service
+    from beholder_amd.transport.amqp import AmqpBroker, AmqpSource
+    from beholder_amd.utils.log import Logger, MemoryStream
+
+    assert not sc.get("concurrent"), "run_service does not script interleavings"
+    data = copy.deepcopy(sc["config"])
+    data["service"] = {"native_handlers": impl == "native", "gc_freeze": False,
+                       "metrics": {"default_metrics": False},
+                       "log": {"positional_args": sc["positionalArgs"]}}
+    config = Config.from_dict(data, env={"NO_TRELLO": "1"} if sc.get("noTrello") else {})
+    http = helpers.SuspendingHttpClient() if suspend else RecordingHttpClient()
+    for f in sc["faults"]:
+        http.fail(f["method"], f["prefix"], status=f["status"], message=f["message"], body=f["body"].encode())
+    rows = [Media(id=m["id"], name=m["name"], creator=m["creator"], creatorId=m["creatorId"],
+                  metadataId=m["metadataId"], status=m["status"]) for m in sc["media"]]
+    base = RacingStore if sc.get("races") else MemoryStore
+    cls = helpers.suspending(base) if suspend else base
+    store = cls(rows, sc["races"]) if base is RacingStore else cls(rows)
+    stream = MemoryStream()
+    unhandled = ("unhandled error in %s handler: " % T.STATUS, "unhandled error in %s handler: " % T.PROGRESS)
+
+    async def go():
+        loop = asyncio.get_running_loop()
+        broker = await AmqpBroker().start()
+        try:
+            # the broker's window holds every event: the deliveries Q1 leaves un-acked keep their
+            # slots (as on a real broker, where 100 of them stall a consumer for good), and the Node
+            # stand-in has no window to fill
+            src = AmqpSource(broker.url, prefetch=max(100, len(sc["events"]) + 1))
+            svc = Service(config, source=src, store=store, http=http, serve_metrics=False,
+                          logger=Logger(stream=stream, positional_args=sc["positionalArgs"]))
+            await svc.init()
+            task = asyncio.ensure_future(svc.run())
+            h = svc.handlers
+            dec = {"status": h.decode_status, "progress": h.decode_progress}
+            settler = src.settler
+            queues = [broker.queues[q] for q in (T.STATUS, T.PROGRESS) if q in broker.queues]
+
+            def broker_acked() -> int:
+                return sum(q.acked for q in queues)
+            acks_arrive = True  # until one event's acks failed to reach the broker in a second
+            events = []
+            for topic, hexbody in sc["events"]:
+                body = bytes.fromhex(hexbody)
+                svc.log.flush()
+                n_http, n_log = len(http.calls), len(stream.lines)
+                settled0, acked0 = _settled(settler), broker_acked()
+                broker.publish(T.STATUS if topic == "status" else T.PROGRESS, body)
+                t_end = loop.time() + 10.0
+                collected = False
+                while _settled(settler) == settled0 or len(svc._inflight):
+                    if task.done():
+                        task.result()  # the service failed: raise it here
+                    if loop.time() > t_end:
+                        raise TimeoutError(f"event {len(events)} not settled in 10 s")
+                    if not collected and loop.time() > t_end - 9.8:
+                        gc.collect()  # an un-acked delivery is counted once it is freed (Q1)
+                        collected = True
+                    await asyncio.sleep(0.0002)
+                # the acks the handler settled, as the broker counts them (flushed over AMQP)
+                t_ack = loop.time() + (1.0 if acks_arrive else 0.005)
+                while broker_acked() < settler.acked and loop.time() < t_ack:
+                    await asyncio.sleep(0.0002)
+                acks_arrive = broker_acked() >= settler.acked
+                svc.log.flush()
+                threw, logs = None, []
+                for x in map(json.loads, stream.lines[n_log:]):
+                    msg = x["msg"]
+                    if x["level"] == 50 and msg.startswith(unhandled):
+                        threw = msg[len(unhandled[0 if msg.startswith(unhandled[0]) else 1]):]
+                        continue
+                    logs.append([x["level"], msg])
+                try:
+                    dec[topic](body)
+                    bad = False
+                except DecodeError:
+                    bad = True
+                events.append({"acks": broker_acked() - acked0, "threw": threw, "decodeError": bad,
+                               "requests": [list(c) for c in list(http.calls)[n_http:]], "logs": logs})
+            svc.request_stop()
+            await task
+            counters = {
+                "beholder_progress_updates_total": _counter_hashes(svc.progress_updates_total, ["status"]),
+                "beholder_trello_comments": _counter_hashes(svc.trello_comments_total, []),
+            }
+            path = {"direct_batches": src.direct_batches, "idle_wakeups": src.idle_wakeups}
+            await svc.close()
+            return events, counters, path
+        finally:
+            await broker.stop()
+
+    events, counters, path = asyncio.run(go())
+    # ``path``: how the deliveries reached the handlers (AmqpSource.direct hand-overs, and the
+    # batches the service's task woke up for); diff() does not compare it
+    return {"events": events, "counters": counters, "media": {k: v.status for k, v in store.snapshot().items()},
+            "path": path}
+
+
 async def _run_concurrent(sc: dict, rig, target, gates: _Gates, decode_error):
     """oracle.js ``concurrent()``, step for step: deliver the next event or open one waiting
     event's gate (the scenario's script decides), then run the loop until nothing is runnable.
@@ -629,6 +748,9 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--impls", default="python,native")
     ap.add_argument("--suspend", action="store_true",
                     help="store and sink client yield at every call (the compiled handlers' resume states)")
+    ap.add_argument("--service", action="store_true",
+                    help="through the whole consumer: AMQP broker, AmqpSource, Service dispatch, acks "
+                         "(run_service; not for mode concurrent)")
     a = ap.parse_args(argv)
     bad = 0
     for seed in range(a.seeds):
@@ -636,7 +758,10 @@ def main(argv: Optional[List[str]] = None) -> int:
             sc = make_scenario(seed, a.events, mode)
             ref = run_node(sc)
             for impl in a.impls.split(","):
-                d = diff(ref, run_python(sc, impl, suspend=a.suspend))
+                if a.service and mode != "concurrent":
+                    d = diff(ref, run_service(sc, impl, suspend=a.suspend))
+                else:
+                    d = diff(ref, run_python(sc, impl, suspend=a.suspend))
                 bad += bool(d)
                 print(f"seed {seed} {mode:10s} {impl:6s} {'OK' if not d else 'DIFF'} {coverage(ref) if not d else ''}")
                 for line in d:

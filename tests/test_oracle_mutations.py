@@ -12,7 +12,9 @@ listener's ``updateStatus`` and its ``getByID`` (index.js:68,76). The ``faults``
 with ``--suspend`` (every store call and sink request waits, as production's socket clients do)
 reach the compiled handlers' resume states, where the two resume mutations live. The
 ``concurrent`` scenarios (several deliveries in flight, resumed in a scripted order on both sides)
-see a per-media serialisation that the reference does not have (Q9).
+see a per-media serialisation that the reference does not have (Q9). The ``--service`` runs put
+each event through the whole consumer (AMQP broker, ``AmqpSource``, the service's dispatch, acks
+counted at the broker), where a mutation of the transport's ack flushing shows.
 """
 import os
 import shutil
@@ -32,6 +34,7 @@ pytestmark = pytest.mark.skipif(not ro.available(), reason="needs node and /root
 # of behaviour
 REREAD = ("--modes", "reread")
 FAULTS_SUSPENDED = ("--modes", "faults", "--suspend")
+SERVICE = ("--modes", "base", "--service")  # through the whole consumer (run_service)
 MUTATIONS = {
     # Q3 (index.js:94): the DEPLOYED hooks keyed off the message's status, not the re-read row's
     "hooks_off_message_status_python": (
@@ -57,6 +60,12 @@ MUTATIONS = {
         "      value = request_finish(c, value);\n      if (!value) goto catch_;",
         "      value = request_finish(c, value);\n      if (!value) { PyErr_Clear(); goto commented; }",
         FAULTS_SUSPENDED),
+    # the consumer path, which the handler-level gate does not run: acks settled by the handlers
+    # are never scheduled for a flush over AMQP (they would leave only when the channel closes)
+    "acks_never_flushed": (
+        "beholder_amd/transport/amqp/source.py",
+        "        loop.call_soon(self._flush_acks)",
+        "        pass  # loop.call_soon(self._flush_acks)", SERVICE),
     # Q9 (index.js:43,62,127): deliveries of one media serialised by default
     "per_media_ordering_by_default": (
         "beholder_amd/config.py",
@@ -95,8 +104,8 @@ def _gate(tree, impl: str, modes=REREAD) -> subprocess.CompletedProcess:
                           text=True, timeout=600)
 
 
-@pytest.mark.parametrize("modes", [REREAD, FAULTS_SUSPENDED, ("--modes", "concurrent")],
-                         ids=["reread", "faults_suspend", "concurrent"])
+@pytest.mark.parametrize("modes", [REREAD, FAULTS_SUSPENDED, ("--modes", "concurrent"), SERVICE],
+                         ids=["reread", "faults_suspend", "concurrent", "service"])
 def test_unmutated_copy_passes_the_gate(tmp_path, modes):
     r = _gate(_tree(tmp_path), "python,native", modes)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]

@@ -36,6 +36,28 @@ def test_reference_parity(mode, io):
     assert not failures, "\n".join(f"{k}: " + "\n  ".join(v) for k, v in failures.items())
 
 
+@pytest.mark.parametrize("io", ["sync", "suspend"])
+def test_reference_parity_through_the_consumer(io):
+    """Every sequential mode through the whole consumer (``run_service``): each event published to
+    an in-process AMQP broker, delivered by ``AmqpSource``, dispatched by the service (the direct
+    hand-over from the read callback when it waits), handled and acked over AMQP. Identical to
+    ``index.js`` per event, as the handler-level gate, and most deliveries took the hand-over."""
+    failures = {}
+    for mode in ro.MODES:
+        if mode == "concurrent":
+            continue
+        for seed in range(2):
+            sc = ro.make_scenario(seed, EVENTS, mode)
+            ref = ro.run_node(sc)
+            for impl in ("python", "native"):
+                got = ro.run_service(sc, impl, suspend=io == "suspend")
+                d = ro.diff(ref, got)
+                if d:
+                    failures[(mode, seed, impl)] = d
+                assert got["path"]["direct_batches"] >= EVENTS // 2, got["path"]
+    assert not failures, "\n".join(f"{k}: " + "\n  ".join(v) for k, v in failures.items())
+
+
 def test_concurrent_scenarios_interleave():
     """Mode ``concurrent`` (Q9, index.js:43,62,127): the reference's own runs of the scripted
     schedules have two deliveries of one media in flight, resume deliveries out of arrival order,
