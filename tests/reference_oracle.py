@@ -417,7 +417,101 @@ def run_python(sc: dict, impl: str = "python", mutate=None, suspend: bool = Fals
     return out
 
 
-def run_service(sc: dict, impl: str = "native", suspend: bool = False) -> dict:
+# card ids the scenarios use that a socket cannot carry as the Node stand-in records them (a raw
+# '#', '?', space or non-ASCII byte in the request path): replaced for the socket runs, on both sides
+_WIRE_CARD_IDS = {"ü": "card-u", "a&b=c?d#e": "card-amp", "%20 +": "card-pct"}
+
+
+def for_sockets(sc: dict) -> dict:
+    """The scenario as :func:`run_service` replays it over real sockets (``sockets=True``), for
+    Node and this service alike: card ids a request line cannot hold as written are replaced, and
+    the sink faults that are transport errors (their text, e.g. ``ECONNREFUSED``, is the stand-in
+    client's, not one a real socket would give) become ``503`` answers."""
+    import copy
+    sc = copy.deepcopy(sc)
+    for m in sc["media"]:
+        m["creatorId"] = _WIRE_CARD_IDS.get(m["creatorId"], m["creatorId"])
+    for f in sc["faults"]:
+        if f["status"] is None:
+            f["status"] = 503
+    sc["sockets"] = True
+    return sc
+
+
+class _SinkServer:
+    """One sink origin (Trello, Telegram or Emby) on 127.0.0.1, HTTP/1.1 keep-alive: records each
+    request as the reference's URL (its origin + the request target) and answers from the
+    scenario's faults, first match first, as RecordingHttpClient does; else ``200 {}``."""
+
+    def __init__(self, origin: str, faults: List[dict], calls: list):
+        self.origin, self.faults, self.calls = origin, faults, calls
+        self.port = 0
+        self._server = None
+
+    async def start(self) -> "_SinkServer":
+        self._server = await asyncio.start_server(self._serve, "127.0.0.1", 0)
+        self.port = self._server.sockets[0].getsockname()[1]
+        return self
+
+    @property
+    def local(self) -> str:
+        return f"http://127.0.0.1:{self.port}"
+
+    async def stop(self) -> None:
+        self._server.close()
+        await self._server.wait_closed()
+
+    def _answer(self, method: str, url: str):
+        for f in self.faults:
+            if (f["method"] == "*" or f["method"] == method) and url.startswith(f["prefix"]):
+                return f["status"], f["body"].encode()
+        return 200, b"{}"
+
+    async def _serve(self, r, w) -> None:
+        try:
+            while True:
+                line = await r.readline()
+                if not line:
+                    return
+                method, target, _ = line.decode("latin-1").split(" ", 2)
+                n = 0
+                while True:
+                    h = await r.readline()
+                    if h in (b"\r\n", b"\n", b""):
+                        break
+                    k, _, v = h.decode("latin-1").partition(":")
+                    if k.strip().lower() == "content-length":
+                        n = int(v)
+                if n:
+                    await r.readexactly(n)
+                url = self.origin + target
+                self.calls.append([method, url])
+                status, body = self._answer(method, url)
+                if status == 204:
+                    body = b""
+                w.write(b"HTTP/1.1 %d X\r\nContent-Length: %d\r\n\r\n%s" % (status, len(body), body))
+                await w.drain()
+        except (ConnectionError, asyncio.IncompleteReadError):
+            pass
+        finally:
+            w.close()
+
+
+def _racing_pg(races: Dict[str, int]):
+    """tests/pg_fake.py's server with the ``reread`` scenarios' other writer: after each UPDATE of
+    a row in ``races``, a second UPDATE leaves ``races[id]`` in it (as RacingStore does)."""
+    from pg_fake import FakePg
+
+    class RacingPg(FakePg):
+        def _run(self, sql, params):
+            out = super()._run(sql, params)
+            if races and sql.lstrip()[:6].upper() == "UPDATE" and params and str(params[-1]) in races:
+                super()._run(sql, (races[str(params[-1])], params[-1]))
+            return out
+    return RacingPg(auth="trust")
+
+
+def run_service(sc: dict, impl: str = "native", suspend: bool = False, sockets: bool = False) -> dict:
     """The same scenario through the whole consumer, as production runs it: each event is
     published to an in-process AMQP broker, delivered to :class:`AmqpSource` and
     handed to the service's dispatch (from the read callback when the service waits: the direct
@@ -428,7 +522,13 @@ def run_service(sc: dict, impl: str = "native", suspend: bool = False) -> dict:
     Recorded as :func:`run_python` records: ``acks`` as the broker counted them, ``threw`` from
     the service's ``unhandled error in <topic> handler: <message>`` line (Node's unhandled
     rejection, index.js:62; the line itself is not one of the reference's), the sink requests and
-    the other log lines. Not for mode ``concurrent``, which scripts its interleavings at gates."""
+    the other log lines. Not for mode ``concurrent``, which scripts its interleavings at gates.
+
+    ``sockets``: the store and the sinks are production's clients over TCP too, not in-process
+    fakes: ``PostgresStore`` against tests/pg_fake.py's server holding the scenario's table, and
+    ``H1Client`` against one local HTTP server per sink origin, which records each request under
+    the reference's origin (the scenario must come from :func:`for_sockets`). Every store call and
+    sink request then waits on a socket, through the NetPoller, as in production."""
     import copy
     import gc
 
@@ -446,21 +546,56 @@ def run_service(sc: dict, impl: str = "native", suspend: bool = False) -> dict:
                        "metrics": {"default_metrics": False},
                        "log": {"positional_args": sc["positionalArgs"]}}
     config = Config.from_dict(data, env={"NO_TRELLO": "1"} if sc.get("noTrello") else {})
-    http = helpers.SuspendingHttpClient() if suspend else RecordingHttpClient()
-    for f in sc["faults"]:
-        http.fail(f["method"], f["prefix"], status=f["status"], message=f["message"], body=f["body"].encode())
     rows = [Media(id=m["id"], name=m["name"], creator=m["creator"], creatorId=m["creatorId"],
                   metadataId=m["metadataId"], status=m["status"]) for m in sc["media"]]
-    base = RacingStore if sc.get("races") else MemoryStore
-    cls = helpers.suspending(base) if suspend else base
-    store = cls(rows, sc["races"]) if base is RacingStore else cls(rows)
+    if sockets:
+        assert sc.get("sockets"), "a socket run replays a for_sockets() scenario"
+        http = store = None  # made on the run's loop
+    else:
+        http = helpers.SuspendingHttpClient() if suspend else RecordingHttpClient()
+        for f in sc["faults"]:
+            http.fail(f["method"], f["prefix"], status=f["status"], message=f["message"], body=f["body"].encode())
+        base = RacingStore if sc.get("races") else MemoryStore
+        cls = helpers.suspending(base) if suspend else base
+        store = cls(rows, sc["races"]) if base is RacingStore else cls(rows)
     stream = MemoryStream()
     unhandled = ("unhandled error in %s handler: " % T.STATUS, "unhandled error in %s handler: " % T.PROGRESS)
 
+    host_back: Dict[str, str] = {}
+
     async def go():
+        nonlocal http, store, config
         loop = asyncio.get_running_loop()
         broker = await AmqpBroker().start()
+        servers, pg = [], None
         try:
+            if sockets:
+                from beholder_amd.sinks import H1Client
+                from beholder_amd.store.postgres import PostgresStore
+                calls: list = []
+                emby = data.get("instance", {}).get("emby", {}).get("host") or "http://emby:8096"
+                ep = emby.split("/", 3)  # scheme:, '', host[:port], base path
+                origins = {"trello": "https://api.trello.com", "telegram": "https://api.telegram.org",
+                           "emby": "/".join(ep[:3])}
+                for name, origin in origins.items():
+                    servers.append(await _SinkServer(origin, sc["faults"], calls).start())
+                local = {n: srv.local for n, srv in zip(origins, servers)}
+                d2 = copy.deepcopy(data)
+                d2["service"]["endpoints"] = {"trello": local["trello"], "telegram": local["telegram"]}
+                if "emby" in d2.get("instance", {}):
+                    d2["instance"]["emby"]["host"] = local["emby"] + ("/" + ep[3] if len(ep) > 3 else "")
+                    # the Emby log line names the configured host: ours, read back as the scenario's
+                    host_back[d2["instance"]["emby"]["host"]] = emby
+                config = Config.from_dict(d2, env=config.env)
+                pg = await _racing_pg(sc.get("races") or {}).start()
+                setup = PostgresStore(pg.dsn, create_schema=True)
+                await setup.connect()
+                for m in rows:
+                    await setup.upsert(m)
+                await setup.close()
+                store = PostgresStore(pg.dsn)
+                http = H1Client(timeout_s=10)
+                http.calls = calls  # what the servers recorded, read as RecordingHttpClient's
             # the broker's window holds every event: the deliveries Q1 leaves un-acked keep their
             # slots (as on a real broker, where 100 of them stall a consumer for good), and the Node
             # stand-in has no window to fill
@@ -507,6 +642,8 @@ def run_service(sc: dict, impl: str = "native", suspend: bool = False) -> dict:
                     if x["level"] == 50 and msg.startswith(unhandled):
                         threw = msg[len(unhandled[0 if msg.startswith(unhandled[0]) else 1]):]
                         continue
+                    for ours, theirs in host_back.items():
+                        msg = msg.replace(ours, theirs)
                     logs.append([x["level"], msg])
                 try:
                     dec[topic](body)
@@ -521,17 +658,31 @@ def run_service(sc: dict, impl: str = "native", suspend: bool = False) -> dict:
                 "beholder_progress_updates_total": _counter_hashes(svc.progress_updates_total, ["status"]),
                 "beholder_trello_comments": _counter_hashes(svc.trello_comments_total, []),
             }
-            path = {"direct_batches": src.direct_batches, "idle_wakeups": src.idle_wakeups}
+            path = {"direct_batches": src.direct_batches, "idle_wakeups": src.idle_wakeups,
+                    "netpoller": getattr(loop, "_beholder_netpoller", None) is not None}
+            stats = getattr(svc.handler_impl, "stats", None)
+            if callable(stats):  # the compiled handlers: how many events left C to wait on I/O
+                path["suspended"] = stats().get("suspended")
             await svc.close()
-            return events, counters, path
+            if sockets:  # the table as the server holds it (the service closed its own store)
+                check = PostgresStore(pg.dsn)
+                await check.connect()
+                media = {m.id: (await check.get_by_id(m.id)).status for m in rows}
+                await check.close()
+            else:
+                media = {k: v.status for k, v in store.snapshot().items()}
+            return events, counters, path, media
         finally:
+            for srv in servers:
+                await srv.stop()
+            if pg is not None:
+                await pg.stop()
             await broker.stop()
 
-    events, counters, path = asyncio.run(go())
+    events, counters, path, media = asyncio.run(go())
     # ``path``: how the deliveries reached the handlers (AmqpSource.direct hand-overs, and the
     # batches the service's task woke up for); diff() does not compare it
-    return {"events": events, "counters": counters, "media": {k: v.status for k, v in store.snapshot().items()},
-            "path": path}
+    return {"events": events, "counters": counters, "media": media, "path": path}
 
 
 async def _run_concurrent(sc: dict, rig, target, gates: _Gates, decode_error):
@@ -751,15 +902,19 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--service", action="store_true",
                     help="through the whole consumer: AMQP broker, AmqpSource, Service dispatch, acks "
                          "(run_service; not for mode concurrent)")
+    ap.add_argument("--sockets", action="store_true",
+                    help="with --service: Postgres and the sinks over TCP too (for_sockets scenarios)")
     a = ap.parse_args(argv)
     bad = 0
     for seed in range(a.seeds):
         for mode in a.modes.split(","):
             sc = make_scenario(seed, a.events, mode)
+            if a.service and a.sockets and mode != "concurrent":
+                sc = for_sockets(sc)
             ref = run_node(sc)
             for impl in a.impls.split(","):
                 if a.service and mode != "concurrent":
-                    d = diff(ref, run_service(sc, impl, suspend=a.suspend))
+                    d = diff(ref, run_service(sc, impl, suspend=a.suspend, sockets=a.sockets))
                 else:
                     d = diff(ref, run_python(sc, impl, suspend=a.suspend))
                 bad += bool(d)

@@ -35,6 +35,7 @@ pytestmark = pytest.mark.skipif(not ro.available(), reason="needs node and /root
 REREAD = ("--modes", "reread")
 FAULTS_SUSPENDED = ("--modes", "faults", "--suspend")
 SERVICE = ("--modes", "base", "--service")  # through the whole consumer (run_service)
+SOCKETS = ("--modes", "faults", "--service", "--sockets")  # ... with Postgres and the sinks over TCP
 MUTATIONS = {
     # Q3 (index.js:94): the DEPLOYED hooks keyed off the message's status, not the re-read row's
     "hooks_off_message_status_python": (
@@ -66,6 +67,12 @@ MUTATIONS = {
         "beholder_amd/transport/amqp/source.py",
         "        loop.call_soon(self._flush_acks)",
         "        pass  # loop.call_soon(self._flush_acks)", SERVICE),
+    # the NetPoller's batch end: the callables deferred to it (the ack flush of handlers that
+    # finished inside the batch) never run; only the socket runs have a NetPoller
+    "deferred_acks_never_flushed": (
+        "beholder_amd/ops/csrc/py_netpoll.cpp",
+        "  flush_all(p);\n  run_deferred(p);",
+        "  flush_all(p);\n  (void)run_deferred;", SOCKETS),
     # Q9 (index.js:43,62,127): deliveries of one media serialised by default
     "per_media_ordering_by_default": (
         "beholder_amd/config.py",
@@ -82,7 +89,7 @@ def _tree(tmp_path, mutation=None):
     shutil.copytree(os.path.join(ROOT, "beholder_amd"), dst / "beholder_amd", ignore=ignore)
     shutil.copytree(os.path.join(ROOT, "scripts", "reference_node"), dst / "scripts" / "reference_node")
     os.makedirs(dst / "tests")
-    for f in ("reference_oracle.py", "helpers.py", "conftest.py", "test_handlers.py"):
+    for f in ("reference_oracle.py", "helpers.py", "conftest.py", "test_handlers.py", "pg_fake.py"):
         shutil.copy(os.path.join(HERE, f), dst / "tests" / f)
     if mutation:
         path, old, new, _ = MUTATIONS[mutation]
@@ -104,8 +111,8 @@ def _gate(tree, impl: str, modes=REREAD) -> subprocess.CompletedProcess:
                           text=True, timeout=600)
 
 
-@pytest.mark.parametrize("modes", [REREAD, FAULTS_SUSPENDED, ("--modes", "concurrent"), SERVICE],
-                         ids=["reread", "faults_suspend", "concurrent", "service"])
+@pytest.mark.parametrize("modes", [REREAD, FAULTS_SUSPENDED, ("--modes", "concurrent"), SERVICE, SOCKETS],
+                         ids=["reread", "faults_suspend", "concurrent", "service", "sockets"])
 def test_unmutated_copy_passes_the_gate(tmp_path, modes):
     r = _gate(_tree(tmp_path), "python,native", modes)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]

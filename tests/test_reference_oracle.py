@@ -58,6 +58,31 @@ def test_reference_parity_through_the_consumer(io):
     assert not failures, "\n".join(f"{k}: " + "\n  ".join(v) for k, v in failures.items())
 
 
+def test_reference_parity_over_sockets():
+    """As above, with production's clients over TCP as well (``run_service(sockets=True)``): the
+    media table in a Postgres wire-protocol server (tests/pg_fake.py) read and written by
+    ``PostgresStore``, and every sink request sent by ``H1Client`` to a local HTTP server per
+    origin, which records it under the reference's origin. Every store call and sink request waits
+    on a socket, through the NetPoller; the compiled handlers finish in their resume states. The
+    scenarios are :func:`reference_oracle.for_sockets`'s, on both sides."""
+    failures = {}
+    for mode in ro.MODES:
+        if mode == "concurrent":
+            continue
+        for seed in range(2):
+            sc = ro.for_sockets(ro.make_scenario(seed, EVENTS, mode))
+            ref = ro.run_node(sc)
+            for impl in ("python", "native"):
+                got = ro.run_service(sc, impl, sockets=True)
+                d = ro.diff(ref, got)
+                if d:
+                    failures[(mode, seed, impl)] = d
+                assert got["path"]["netpoller"] and got["path"]["direct_batches"] >= EVENTS // 2, got["path"]
+                if impl == "native":
+                    assert got["path"]["suspended"] > EVENTS // 4, got["path"]
+    assert not failures, "\n".join(f"{k}: " + "\n  ".join(v) for k, v in failures.items())
+
+
 def test_concurrent_scenarios_interleave():
     """Mode ``concurrent`` (Q9, index.js:43,62,127): the reference's own runs of the scripted
     schedules have two deliveries of one media in flight, resume deliveries out of arrival order,
