@@ -443,19 +443,23 @@ class _SinkServer:
     request as the reference's URL (its origin + the request target) and answers from the
     scenario's faults, first match first, as RecordingHttpClient does; else ``200 {}``."""
 
-    def __init__(self, origin: str, faults: List[dict], calls: list):
-        self.origin, self.faults, self.calls = origin, faults, calls
+    def __init__(self, origin: str, faults: List[dict], calls: list, tls: bool = False):
+        self.origin, self.faults, self.calls, self.tls = origin, faults, calls, tls
         self.port = 0
         self._server = None
 
     async def start(self) -> "_SinkServer":
-        self._server = await asyncio.start_server(self._serve, "127.0.0.1", 0)
+        ctx = None
+        if self.tls:  # the bench's own CA and certificate for 127.0.0.1
+            from beholder_amd.bench.http_sink_server import server_ssl_context
+            ctx = server_ssl_context()
+        self._server = await asyncio.start_server(self._serve, "127.0.0.1", 0, ssl=ctx)
         self.port = self._server.sockets[0].getsockname()[1]
         return self
 
     @property
     def local(self) -> str:
-        return f"http://127.0.0.1:{self.port}"
+        return f"{'https' if self.tls else 'http'}://127.0.0.1:{self.port}"
 
     async def stop(self) -> None:
         self._server.close()
@@ -511,7 +515,8 @@ def _racing_pg(races: Dict[str, int]):
     return RacingPg(auth="trust")
 
 
-def run_service(sc: dict, impl: str = "native", suspend: bool = False, sockets: bool = False) -> dict:
+def run_service(sc: dict, impl: str = "native", suspend: bool = False, sockets: bool = False,
+                tls: bool = False) -> dict:
     """The same scenario through the whole consumer, as production runs it: each event is
     published to an in-process AMQP broker, delivered to :class:`AmqpSource` and
     handed to the service's dispatch (from the read callback when the service waits: the direct
@@ -528,7 +533,9 @@ def run_service(sc: dict, impl: str = "native", suspend: bool = False, sockets: 
     fakes: ``PostgresStore`` against tests/pg_fake.py's server holding the scenario's table, and
     ``H1Client`` against one local HTTP server per sink origin, which records each request under
     the reference's origin (the scenario must come from :func:`for_sockets`). Every store call and
-    sink request then waits on a socket, through the NetPoller, as in production."""
+    sink request then waits on a socket, through the NetPoller, as in production. ``tls`` (with
+    ``sockets``): the sink servers speak HTTPS, as Trello's and Telegram's do, and the H1 client's
+    native TLS connections verify them against the bench's CA."""
     import copy
     import gc
 
@@ -578,7 +585,7 @@ def run_service(sc: dict, impl: str = "native", suspend: bool = False, sockets: 
                 origins = {"trello": "https://api.trello.com", "telegram": "https://api.telegram.org",
                            "emby": "/".join(ep[:3])}
                 for name, origin in origins.items():
-                    servers.append(await _SinkServer(origin, sc["faults"], calls).start())
+                    servers.append(await _SinkServer(origin, sc["faults"], calls, tls=tls).start())
                 local = {n: srv.local for n, srv in zip(origins, servers)}
                 d2 = copy.deepcopy(data)
                 d2["service"]["endpoints"] = {"trello": local["trello"], "telegram": local["telegram"]}
@@ -594,7 +601,11 @@ def run_service(sc: dict, impl: str = "native", suspend: bool = False, sockets: 
                     await setup.upsert(m)
                 await setup.close()
                 store = PostgresStore(pg.dsn)
-                http = H1Client(timeout_s=10)
+                if tls:
+                    from beholder_amd.bench.http_sink_server import TLS_CERT
+                    http = H1Client(timeout_s=10, ssl_cafile=TLS_CERT)
+                else:
+                    http = H1Client(timeout_s=10)
                 http.calls = calls  # what the servers recorded, read as RecordingHttpClient's
             # the broker's window holds every event: the deliveries Q1 leaves un-acked keep their
             # slots (as on a real broker, where 100 of them stall a consumer for good), and the Node
@@ -904,6 +915,7 @@ def main(argv: Optional[List[str]] = None) -> int:
                          "(run_service; not for mode concurrent)")
     ap.add_argument("--sockets", action="store_true",
                     help="with --service: Postgres and the sinks over TCP too (for_sockets scenarios)")
+    ap.add_argument("--tls", action="store_true", help="with --sockets: the sinks over HTTPS")
     a = ap.parse_args(argv)
     bad = 0
     for seed in range(a.seeds):
@@ -914,7 +926,7 @@ def main(argv: Optional[List[str]] = None) -> int:
             ref = run_node(sc)
             for impl in a.impls.split(","):
                 if a.service and mode != "concurrent":
-                    d = diff(ref, run_service(sc, impl, suspend=a.suspend, sockets=a.sockets))
+                    d = diff(ref, run_service(sc, impl, suspend=a.suspend, sockets=a.sockets, tls=a.tls))
                 else:
                     d = diff(ref, run_python(sc, impl, suspend=a.suspend))
                 bad += bool(d)

@@ -58,13 +58,15 @@ def test_reference_parity_through_the_consumer(io):
     assert not failures, "\n".join(f"{k}: " + "\n  ".join(v) for k, v in failures.items())
 
 
-def test_reference_parity_over_sockets():
+@pytest.mark.parametrize("transport", ["tcp", "tls"])
+def test_reference_parity_over_sockets(transport):
     """As above, with production's clients over TCP as well (``run_service(sockets=True)``): the
     media table in a Postgres wire-protocol server (tests/pg_fake.py) read and written by
     ``PostgresStore``, and every sink request sent by ``H1Client`` to a local HTTP server per
     origin, which records it under the reference's origin. Every store call and sink request waits
     on a socket, through the NetPoller; the compiled handlers finish in their resume states. The
-    scenarios are :func:`reference_oracle.for_sockets`'s, on both sides."""
+    scenarios are :func:`reference_oracle.for_sockets`'s, on both sides. ``tls``: the sink servers
+    speak HTTPS (as Trello and Telegram do), through the H1 client's native TLS connections."""
     failures = {}
     for mode in ro.MODES:
         if mode == "concurrent":
@@ -73,7 +75,7 @@ def test_reference_parity_over_sockets():
             sc = ro.for_sockets(ro.make_scenario(seed, EVENTS, mode))
             ref = ro.run_node(sc)
             for impl in ("python", "native"):
-                got = ro.run_service(sc, impl, sockets=True)
+                got = ro.run_service(sc, impl, sockets=True, tls=transport == "tls")
                 d = ro.diff(ref, got)
                 if d:
                     failures[(mode, seed, impl)] = d
