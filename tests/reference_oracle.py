@@ -527,7 +527,9 @@ def run_service(sc: dict, impl: str = "native", suspend: bool = False, sockets: 
     Recorded as :func:`run_python` records: ``acks`` as the broker counted them, ``threw`` from
     the service's ``unhandled error in <topic> handler: <message>`` line (Node's unhandled
     rejection, index.js:62; the line itself is not one of the reference's), the sink requests and
-    the other log lines. Not for mode ``concurrent``, which scripts its interleavings at gates.
+    the other log lines. Mode ``concurrent`` follows ``oracle.js``'s script step for step: a step
+    publishes the next event or opens one waiting event's gate, then waits until that event is at
+    its next gate or settled, and records what the step did (as :func:`_run_concurrent`).
 
     ``sockets``: the store and the sinks are production's clients over TCP too, not in-process
     fakes: ``PostgresStore`` against tests/pg_fake.py's server holding the scenario's table, and
@@ -547,7 +549,9 @@ def run_service(sc: dict, impl: str = "native", suspend: bool = False, sockets: 
     from beholder_amd.transport.amqp import AmqpBroker, AmqpSource
     from beholder_amd.utils.log import Logger, MemoryStream
 
-    assert not sc.get("concurrent"), "run_service does not script interleavings"
+    conc = sc.get("concurrent")
+    assert not (conc and sockets), "the concurrent mode's gates are in-process fakes"
+    gates = _Gates() if conc else None
     data = copy.deepcopy(sc["config"])
     data["service"] = {"native_handlers": impl == "native", "gc_freeze": False,
                        "metrics": {"default_metrics": False},
@@ -559,11 +563,17 @@ def run_service(sc: dict, impl: str = "native", suspend: bool = False, sockets: 
         assert sc.get("sockets"), "a socket run replays a for_sockets() scenario"
         http = store = None  # made on the run's loop
     else:
-        http = helpers.SuspendingHttpClient() if suspend else RecordingHttpClient()
+        if gates is not None:
+            http = _GatedHttpClient(gates)
+        else:
+            http = helpers.SuspendingHttpClient() if suspend else RecordingHttpClient()
         for f in sc["faults"]:
             http.fail(f["method"], f["prefix"], status=f["status"], message=f["message"], body=f["body"].encode())
         base = RacingStore if sc.get("races") else MemoryStore
-        cls = helpers.suspending(base) if suspend else base
+        if gates is not None:
+            cls = _gated_store(base, gates)
+        else:
+            cls = helpers.suspending(base) if suspend else base
         store = cls(rows, sc["races"]) if base is RacingStore else cls(rows)
     stream = MemoryStream()
     unhandled = ("unhandled error in %s handler: " % T.STATUS, "unhandled error in %s handler: " % T.PROGRESS)
@@ -623,29 +633,10 @@ def run_service(sc: dict, impl: str = "native", suspend: bool = False, sockets: 
             def broker_acked() -> int:
                 return sum(q.acked for q in queues)
             acks_arrive = True  # until one event's acks failed to reach the broker in a second
-            events = []
-            for topic, hexbody in sc["events"]:
-                body = bytes.fromhex(hexbody)
-                svc.log.flush()
-                n_http, n_log = len(http.calls), len(stream.lines)
-                settled0, acked0 = _settled(settler), broker_acked()
-                broker.publish(T.STATUS if topic == "status" else T.PROGRESS, body)
-                t_end = loop.time() + 10.0
-                collected = False
-                while _settled(settler) == settled0 or len(svc._inflight):
-                    if task.done():
-                        task.result()  # the service failed: raise it here
-                    if loop.time() > t_end:
-                        raise TimeoutError(f"event {len(events)} not settled in 10 s")
-                    if not collected and loop.time() > t_end - 9.8:
-                        gc.collect()  # an un-acked delivery is counted once it is freed (Q1)
-                        collected = True
-                    await asyncio.sleep(0.0002)
-                # the acks the handler settled, as the broker counts them (flushed over AMQP)
-                t_ack = loop.time() + (1.0 if acks_arrive else 0.005)
-                while broker_acked() < settler.acked and loop.time() < t_ack:
-                    await asyncio.sleep(0.0002)
-                acks_arrive = broker_acked() >= settler.acked
+
+            def logs_since(n_log: int):
+                """The log lines written since ``n_log``: Node's rejection (the service's line for
+                an unhandled handler error) apart from the reference's own lines."""
                 svc.log.flush()
                 threw, logs = None, []
                 for x in map(json.loads, stream.lines[n_log:]):
@@ -656,12 +647,103 @@ def run_service(sc: dict, impl: str = "native", suspend: bool = False, sockets: 
                     for ours, theirs in host_back.items():
                         msg = msg.replace(ours, theirs)
                     logs.append([x["level"], msg])
+                return threw, logs
+
+            def decode_error(topic: str, body: bytes) -> bool:
                 try:
                     dec[topic](body)
-                    bad = False
+                    return False
                 except DecodeError:
-                    bad = True
-                events.append({"acks": broker_acked() - acked0, "threw": threw, "decodeError": bad,
+                    return True
+
+            async def until(cond, what: str) -> None:
+                t_end = loop.time() + 10.0
+                collected = False
+                while not cond():
+                    if task.done():
+                        task.result()  # the service failed: raise it here
+                    if loop.time() > t_end:
+                        raise TimeoutError(f"{what}: not within 10 s")
+                    if not collected and loop.time() > t_end - 9.8:
+                        gc.collect()  # an un-acked delivery is counted once it is freed (Q1)
+                        collected = True
+                    await asyncio.sleep(0.0002)
+
+            async def acks_flushed() -> None:
+                """The acks the handlers settled, as the broker counts them (flushed over AMQP)."""
+                nonlocal acks_arrive
+                t_ack = loop.time() + (1.0 if acks_arrive else 0.005)
+                while broker_acked() < settler.acked and loop.time() < t_ack:
+                    await asyncio.sleep(0.0002)
+                acks_arrive = broker_acked() >= settler.acked
+
+            order = None
+            events = []
+            if conc:  # oracle.js concurrent(), step for step, with each delivery over AMQP
+                cap, script = conc["cap"], conc["script"]
+                topics = [t for t, _ in sc["events"]]
+                bodies = [bytes.fromhex(hx) for _, hx in sc["events"]]
+                n = len(bodies)
+                events = [{"acks": 0, "threw": None, "decodeError": decode_error(t, b), "requests": [], "logs": []}
+                          for t, b in zip(topics, bodies)]
+                settled = [False] * n
+                order = []
+                nxt = step = 0
+                while True:
+                    ready = sorted(gates.waiting)
+                    r = script[step % len(script)]
+                    step += 1
+                    active = nxt - sum(settled[:nxt])
+                    if nxt < n and (not ready or (active < cap and r % 2 == 0)):
+                        i, action, kind = nxt, "deliver", None
+                        nxt += 1
+                    elif ready:
+                        i = ready[(r >> 1) % len(ready)]
+                        action = "resolve"
+                    else:
+                        if active:
+                            raise RuntimeError(f"{active} deliveries in flight, none at a gate")
+                        break
+                    gates.current = i
+                    svc.log.flush()
+                    n_http, n_log = len(http.calls), len(stream.lines)
+                    s0, a0 = _settled(settler), broker_acked()
+                    if action == "deliver":
+                        broker.publish(T.STATUS if topics[i] == "status" else T.PROGRESS, bodies[i])
+                    else:
+                        kind, fut = gates.waiting.pop(i)
+                        fut.set_result(None)
+                    # the event reaches its next gate, or ends (settled); then whatever else that
+                    # made runnable runs (oracle.js: one setImmediate)
+                    await until(lambda: i in gates.waiting or _settled(settler) > s0, f"step {step} event {i}")
+                    for _ in range(10000):
+                        await asyncio.sleep(0)
+                        if not loop._ready:  # noqa: SLF001 - the loop's runnable queue
+                            break
+                    await acks_flushed()
+                    if _settled(settler) > s0:
+                        settled[i] = True
+                    threw, logs = logs_since(n_log)
+                    reqs = [list(c) for c in list(http.calls)[n_http:]]
+                    ev = events[i]
+                    ev["logs"] += logs
+                    ev["requests"] += reqs
+                    if threw is not None:
+                        ev["threw"] = threw
+                    got = broker_acked() - a0
+                    ev["acks"] += got
+                    order.append([action, i, kind, len(logs), len(reqs), int(got > 0), settled[i]])
+            for topic, hexbody in ([] if conc else sc["events"]):
+                body = bytes.fromhex(hexbody)
+                svc.log.flush()
+                n_http, n_log = len(http.calls), len(stream.lines)
+                settled0, acked0 = _settled(settler), broker_acked()
+                broker.publish(T.STATUS if topic == "status" else T.PROGRESS, body)
+                await until(lambda: _settled(settler) > settled0 and not len(svc._inflight),
+                            f"event {len(events)} settled")
+                await acks_flushed()
+                threw, logs = logs_since(n_log)
+                events.append({"acks": broker_acked() - acked0, "threw": threw, "decodeError": decode_error(topic, body),
                                "requests": [list(c) for c in list(http.calls)[n_http:]], "logs": logs})
             svc.request_stop()
             await task
@@ -682,7 +764,7 @@ def run_service(sc: dict, impl: str = "native", suspend: bool = False, sockets: 
                 await check.close()
             else:
                 media = {k: v.status for k, v in store.snapshot().items()}
-            return events, counters, path, media
+            return events, counters, path, media, order
         finally:
             for srv in servers:
                 await srv.stop()
@@ -690,10 +772,13 @@ def run_service(sc: dict, impl: str = "native", suspend: bool = False, sockets: 
                 await pg.stop()
             await broker.stop()
 
-    events, counters, path, media = asyncio.run(go())
+    events, counters, path, media, order = asyncio.run(go())
     # ``path``: how the deliveries reached the handlers (AmqpSource.direct hand-overs, and the
     # batches the service's task woke up for); diff() does not compare it
-    return {"events": events, "counters": counters, "media": media, "path": path}
+    out = {"events": events, "counters": counters, "media": media, "path": path}
+    if order is not None:
+        out["order"] = order
+    return out
 
 
 async def _run_concurrent(sc: dict, rig, target, gates: _Gates, decode_error):
@@ -912,7 +997,7 @@ def main(argv: Optional[List[str]] = None) -> int:
                     help="store and sink client yield at every call (the compiled handlers' resume states)")
     ap.add_argument("--service", action="store_true",
                     help="through the whole consumer: AMQP broker, AmqpSource, Service dispatch, acks "
-                         "(run_service; not for mode concurrent)")
+                         "(run_service)")
     ap.add_argument("--sockets", action="store_true",
                     help="with --service: Postgres and the sinks over TCP too (for_sockets scenarios)")
     ap.add_argument("--tls", action="store_true", help="with --sockets: the sinks over HTTPS")
@@ -921,12 +1006,13 @@ def main(argv: Optional[List[str]] = None) -> int:
     for seed in range(a.seeds):
         for mode in a.modes.split(","):
             sc = make_scenario(seed, a.events, mode)
-            if a.service and a.sockets and mode != "concurrent":
+            sockets = a.sockets and mode != "concurrent"  # the concurrent gates are in-process
+            if a.service and sockets:
                 sc = for_sockets(sc)
             ref = run_node(sc)
             for impl in a.impls.split(","):
-                if a.service and mode != "concurrent":
-                    d = diff(ref, run_service(sc, impl, suspend=a.suspend, sockets=a.sockets, tls=a.tls))
+                if a.service:
+                    d = diff(ref, run_service(sc, impl, suspend=a.suspend, sockets=sockets, tls=a.tls))
                 else:
                     d = diff(ref, run_python(sc, impl, suspend=a.suspend))
                 bad += bool(d)

@@ -41,10 +41,13 @@ def test_reference_parity_through_the_consumer(io):
     """Every sequential mode through the whole consumer (``run_service``): each event published to
     an in-process AMQP broker, delivered by ``AmqpSource``, dispatched by the service (the direct
     hand-over from the read callback when it waits), handled and acked over AMQP. Identical to
-    ``index.js`` per event, as the handler-level gate, and most deliveries took the hand-over."""
+    ``index.js`` per event, as the handler-level gate, and most deliveries took the hand-over. The
+    ``concurrent`` mode runs once (its gates suspend every call): the scripted interleavings of up
+    to 4 deliveries in flight, step for step, through the service's dispatch and the compiled
+    handlers' resumes."""
     failures = {}
     for mode in ro.MODES:
-        if mode == "concurrent":
+        if mode == "concurrent" and io == "suspend":
             continue
         for seed in range(2):
             sc = ro.make_scenario(seed, EVENTS, mode)
