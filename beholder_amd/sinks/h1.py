@@ -691,8 +691,15 @@ class H1Client(HttpClient):
     def _prepare(self, url: str, params) -> Tuple[str, _Origin, str, str]:
         """``(full URL, *_resolve(full URL))`` for ``url`` + ``params``."""
         if "?" in url or "#" in url:
-            full = with_query(url, params)
-            return (full, *self._resolve(full))
+            # the fragment stays on this side (it is never sent), so the parameters join the query
+            # before it, as Node's url.parse + request put them; appended after it, they were
+            # dropped with it
+            h = url.find("#")
+            if h < 0:
+                full = with_query(url, params)
+                return (full, *self._resolve(full))
+            sent = with_query(url[:h], params)
+            return (sent + url[h:], *self._resolve(sent))
         # the sinks' shape: a cached route + an encodeURIComponent query (ASCII, no spaces: the
         # quoting of _resolve would leave it as is)
         o, target, rest = self._route(url)

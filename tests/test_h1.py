@@ -293,6 +293,23 @@ def test_keep_alive_reuses_one_connection_and_target_is_verbatim():
     assert r.headers == {"content-length": "2"}
 
 
+def test_a_fragment_in_the_url_keeps_the_parameters():
+    """A path segment from the database can hold '#' (Trello's /1/cards/{creatorId}): the fragment
+    is never sent, and the parameters (the comment text, key and token) join the query before it,
+    as Node's url.parse + request put them, instead of being dropped with it."""
+    async def go():
+        s = await Scripted(lambda n, m, t, h: OK).start()
+        c = H1Client(timeout_s=5)
+        base = f"http://127.0.0.1:{s.port}/1/cards/"
+        await c.request("POST", base + "a&b=c?d#e/actions/comments", params={"text": "x y", "key": "K"})
+        await c.request("POST", base + "c#1/actions/comments", params={"text": "x", "key": "K"})
+        await c.request("GET", base + "c#1", params=None)
+        await c.close()
+        await s.stop()
+        return [t for _, t, _ in s.requests]
+    assert run(go()) == ["/1/cards/a&b=c?d&text=x%20y&key=K", "/1/cards/c?text=x&key=K", "/1/cards/c"]
+
+
 def test_connection_close_and_http10_open_new_connections():
     def respond(n, m, t, h):
         if t.startswith("/close"):
@@ -536,15 +553,17 @@ def test_cached_route_gives_the_uncached_request_target(origin, path, params):
     same URL, origin and request line as resolving the full URL from scratch."""
     c = H1Client()
     url = origin + path
+    h = url.find("#")  # a fragment is not sent: the parameters join the query before it
+    base, frag = (url, "") if h < 0 else (url[:h], url[h:])
     try:
-        want = c._resolve(with_query(url, params))
+        want = c._resolve(with_query(base, params))
     except HttpError:  # e.g. "https://u:p@h:8443=": both ways refuse it
         with pytest.raises(HttpError):
             c._prepare(url, params)
         return
     for _ in range(2):  # second time from the cache
         full, o, target, rest = c._prepare(url, params)
-        assert full == with_query(url, params)
+        assert full == with_query(base, params) + frag
         assert (o, target, rest) == want
 
 
