@@ -32,7 +32,7 @@ asan:             ## CPython suites against an ASan+UBSan build of the extension
 	  $(PY) -m pytest -q -p no:cacheprovider -m "not gpu" tests/test_native_fuzz.py tests/test_codec.py tests/test_ingest.py \
 	  tests/test_amqp_demux.py tests/test_text.py tests/test_delivery.py tests/test_histogram.py \
 	  tests/test_handlers.py tests/test_native_handlers.py tests/test_tracing.py tests/test_amqp.py tests/test_service.py tests/test_h1.py tests/test_h1_fast.py tests/test_tls.py tests/test_netconn.py tests/test_sinks.py tests/test_stores.py tests/test_preconnect.py tests/test_driver.py tests/test_chaos.py tests/test_workers.py tests/test_gpu_decode.py tests/test_native_tools.py tests/test_pg_fake.py tests/test_gil_clock.py \
-	  tests/test_native_handlers_edges.py tests/test_h1_call_edges.py tests/test_netconn_edges.py tests/test_native_surface.py tests/test_direct_dispatch.py; \
+	  tests/test_native_handlers_edges.py tests/test_h1_call_edges.py tests/test_netconn_edges.py tests/test_native_surface.py tests/test_direct_dispatch.py tests/test_reference_oracle.py; \
 	  rc=$$?; $(PY) -m beholder_amd.ops.build --force >/dev/null; exit $$rc
 
 coverage:         ## gcov line / branch coverage of the native runtime under the CPU suite -> profiles/native_coverage
