@@ -9,6 +9,7 @@ pino@5's ``positional_args: drop`` (Q11). Skipped without ``node`` or the refere
 import pytest
 
 import reference_oracle as ro
+from beholder_amd.utils import netconn
 
 pytestmark = pytest.mark.skipif(not ro.available(), reason="needs node and /root/reference/index.js")
 
@@ -82,7 +83,9 @@ def test_reference_parity_over_sockets(transport):
                 d = ro.diff(ref, got)
                 if d:
                     failures[(mode, seed, impl)] = d
-                assert got["path"]["netpoller"] and got["path"]["direct_batches"] >= EVENTS // 2, got["path"]
+                # BEHOLDER_NATIVE_IO=0: every socket on an asyncio transport, no NetPoller
+                assert got["path"]["netpoller"] == netconn.enabled(), got["path"]
+                assert got["path"]["direct_batches"] >= EVENTS // 2, got["path"]
                 if impl == "native":
                     assert got["path"]["suspended"] > EVENTS // 4, got["path"]
     assert not failures, "\n".join(f"{k}: " + "\n  ".join(v) for k, v in failures.items())
